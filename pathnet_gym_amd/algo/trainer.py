@@ -1,0 +1,258 @@
+"""Population-parallel PathNet A2C trainer (one process per GPU).
+
+Replaces the reference's worker/coordinator/PS process roles
+(``doom_pathnet.py:53-296``, ``a3c_training_thread.py:102-245``) with ONE
+synchronous loop per rank:
+
+    update():
+      rollout T steps of P_local paths x E envs      (env + policy on device)
+      backward through the stored rollout graph      (no recompute)
+      ONE fused all-reduce: active grads + fitness + counters   (parallel/comm.py)
+      clip-by-norm per tensor + TF RMSProp            (algo/optim.py)
+      replicated B-way tournament on the global fitness vector  (algo/ga.py)
+
+Semantic differences from the reference (all
+deliberate and documented): synchronous instead of Hogwild; fixed-length
+rollouts with done masks instead of cutting at episode end; genotypes only
+change at update boundaries; per-task lr anneal by default; frozen mask is
+the union over tasks by default.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..config import FITNESS_PENDING, TrainConfig
+from ..envs.registry import make, reward_threshold
+from ..models.acnet import ACPathNet
+from ..parallel.comm import FusedUpdateComm, GatherBroadcastComm
+from ..parallel.dist import DistContext
+from ..utils.metrics import MetricsLogger
+from .a2c_math import a2c_loss, nstep_returns, sample_actions
+from .ga import Population
+from .optim import RMSPropTF, anneal_lr
+
+
+def resolve_backend(backend: str, device: torch.device) -> str:
+    if backend == "auto":
+        return "hip" if device.type == "cuda" else "torch"
+    if backend == "hip" and device.type != "cuda":
+        raise RuntimeError("backend 'hip' needs a GPU device")
+    return backend
+
+
+@dataclass
+class UpdateStats:
+    loss_pi: float = 0.0
+    loss_v: float = 0.0
+    entropy: float = 0.0
+    episodes: int = 0
+    mean_return: float = float("nan")
+    tournaments: int = 0
+    best_winner: float = float("nan")
+
+
+class PathNetTrainer:
+    def __init__(self, cfg: TrainConfig, device=None, ctx: Optional[DistContext] = None,
+                 logger: Optional[MetricsLogger] = None):
+        self.cfg = cfg
+        self.ctx = ctx or DistContext()
+        if device is None:
+            device = self.ctx.device
+        self.device = torch.device(device)
+        self.backend = resolve_backend(cfg.backend, self.device)
+        self.logger = logger
+        net = cfg.net
+        self.P = cfg.paths
+        self.E = cfg.envs_per_path
+        self.P_total = self.P * self.ctx.world
+        self.path_offset = self.ctx.rank * self.P
+        self.pop = Population(self.P_total, net.L, net.M, net.N, cfg.ga.B, seed=cfg.ga.seed,
+                              mutation_kind=cfg.ga.mutation, concurrent=cfg.ga.concurrent_tournaments)
+        self.model = ACPathNet(net, self.P, self.device, self.backend, seed=cfg.seed,
+                               compute_dtype=cfg.compute_dtype)
+        a2c = cfg.a2c
+        self.opt = RMSPropTF(self.model.store.layout, self.model.store.flat, a2c.rmsp_alpha, a2c.rmsp_momentum,
+                             a2c.rmsp_epsilon, a2c.grad_norm_clip,
+                             backend="hip" if self.backend == "hip" else "torch")
+        # vars_backup: initial weights used for re-initialisation between tasks (doom_pathnet.py:204-205)
+        self.init_flat = self.model.store.flat.detach().clone()
+        comm_cls = GatherBroadcastComm if getattr(cfg, "ga_sync", "fused") == "gather_bcast" else FusedUpdateComm
+        self.comm = comm_cls(self.ctx, self.model.store.layout, self.P_total, self.P, self.device)
+        self.global_step = 0
+        self.task_start_step = 0
+        self.task_idx = 0
+        self.updates = 0
+        self.solved_generation: Dict[int, Optional[int]] = {}
+        self.env = None
+        self._start_task(0, fresh=True)
+
+    # ------------------------------------------------------------------
+    # task sequencing (doom_pathnet.py:178-293)
+    # ------------------------------------------------------------------
+    def _make_env(self, task_idx: int):
+        name = self.cfg.tasks[task_idx]
+        seed = self.cfg.seed * 7919 + self.ctx.rank * 104729 + task_idx * 113
+        kw = {}
+        if name.lower().startswith(("pong", "breakout", "spaceinvaders", "alien", "mspacman", "centipede")):
+            kw = dict(frameskip=self.cfg.frameskip, gray=self.cfg.gray)
+        env_backend = "hip" if self.backend == "hip" else "torch"
+        return make(name, num_envs=self.P * self.E, device=self.device, seed=seed, backend=env_backend, **kw)
+
+    def _start_task(self, task_idx: int, fresh: bool = False):
+        self.task_idx = task_idx
+        self.model.task = task_idx
+        if not fresh:
+            self.pop.init_genotypes()
+        if self.env is not None:
+            self.env.close()
+        self.env = self._make_env(task_idx)
+        self.obs = self.env.reset()
+        B = self.P * self.E
+        self.lstm_state = self.model.init_state(B)
+        self.fitness_local = torch.full((self.P,), FITNESS_PENDING, device=self.device)
+        self._push_genotypes()
+        self.task_start_step = self.global_step
+        self.solved_generation.setdefault(task_idx, None)
+        self._task_gen0 = self.pop.generation
+
+    def _push_genotypes(self):
+        expr = self.pop.expressed()
+        self.model.set_paths(expr[self.path_offset:self.path_offset + self.P])
+        self.comm.plan(expr, self.pop.frozen)
+
+    def end_task(self):
+        """Freeze the last winner and re-init every other parameter (doom_pathnet.py:274-293)."""
+        winner = self.pop.best()
+        frozen = self.pop.freeze(winner, union=self.cfg.ga.freeze_union)
+        self.model.set_frozen(frozen)
+        self.opt.set_frozen(frozen)
+        keep = np.zeros(self.model.store.layout.numel, bool)
+        for s in self.model.store.layout.segments:
+            if s.layer >= 0 and frozen[s.layer, s.module] > 0.5:
+                keep[s.offset:s.offset + s.numel] = True
+        keep_t = torch.from_numpy(keep).to(self.device)
+        with torch.no_grad():
+            f = self.model.store.flat
+            f.copy_(torch.where(keep_t, f, self.init_flat))
+        if self.backend == "hip":
+            self.model.hip.refresh_weights()
+        return winner, frozen
+
+    # ------------------------------------------------------------------
+    # one update
+    # ------------------------------------------------------------------
+    def rollout_and_backward(self):
+        """T env steps for the whole local population + loss.backward()."""
+        cfg = self.cfg
+        a2c = cfg.a2c
+        T, E, P = a2c.t_max, self.E, self.P
+        B = P * E
+        model, env = self.model, self.env
+        logits_l, values_l, actions_l, rewards_l, dones_l = [], [], [], [], []
+        state = self.lstm_state
+        obs = self.obs
+        ep_sum = torch.zeros(P, device=self.device)
+        ep_cnt = torch.zeros(P, device=self.device)
+        for t in range(T):
+            logits, value, state = model.forward(obs, E, state)
+            a = sample_actions(logits.detach())
+            obs, r, d, info = env.step(a)
+            finished = d.float()
+            er = info["episode_return"].float()
+            s = (er * finished).view(P, E).sum(1)
+            c = finished.view(P, E).sum(1)
+            # fitness = return of the most recently finished episode(s) (a3c_training_thread.py:145-147)
+            self.fitness_local = torch.where(c > 0, s / c.clamp(min=1.0), self.fitness_local)
+            ep_sum += s
+            ep_cnt += c
+            if state is not None:
+                keep = (1.0 - finished)[:, None]
+                state = (state[0] * keep, state[1] * keep)
+            logits_l.append(logits)
+            values_l.append(value)
+            actions_l.append(a)
+            rewards_l.append(r)
+            dones_l.append(d)
+        with torch.no_grad():
+            _, v_boot, _ = model.forward(obs, E, state)
+        values = torch.stack(values_l)
+        R, adv = nstep_returns(torch.stack(rewards_l), values.detach().float(), torch.stack(dones_l),
+                               v_boot.float(), a2c.gamma, a2c.gae_lambda, a2c.reward_clip)
+        weight = None
+        if a2c.env_reduction == "mean_env":
+            weight = torch.full((T * B,), 1.0 / E, device=self.device)
+        loss, lp, lv, ent = a2c_loss(torch.cat(logits_l), values.reshape(-1), torch.cat(actions_l),
+                                     R.reshape(-1), adv.reshape(-1), a2c.entropy_beta, a2c.value_coef, weight)
+        flat = model.store.flat
+        flat.grad = None
+        loss.backward()
+        self.obs = obs
+        if state is not None:
+            state = (state[0].detach(), state[1].detach())
+        self.lstm_state = state
+        counters = torch.stack([torch.tensor(float(T * B), device=self.device), ep_cnt.sum(), ep_sum.sum(),
+                                torch.zeros((), device=self.device)])
+        return flat.grad, counters, (lp, lv, ent)
+
+    def update(self) -> UpdateStats:
+        grad, counters, (lp, lv, ent) = self.rollout_and_backward()
+        fit_all, csum = self.comm.exchange(grad, self.fitness_local, counters)
+        lr = anneal_lr(self.cfg.a2c.lr, self.global_step, self.cfg.a2c.max_time_step,
+                       self.task_start_step, self.cfg.a2c.lr_anneal)
+        with torch.no_grad():
+            self.opt.step(grad, lr)
+        if self.backend == "hip":
+            self.model.hip.refresh_weights()
+        self.global_step += int(csum[0])
+        self.updates += 1
+        st = UpdateStats(float(lp), float(lv), float(ent), int(csum[1]),
+                         float(csum[2] / csum[1]) if csum[1] > 0 else float("nan"))
+        events = self.pop.step(fit_all, self.global_step)
+        if isinstance(self.comm, GatherBroadcastComm) and events:
+            g = self.comm.broadcast_genotypes(self.pop.genotypes)
+            self.pop.genotypes = g
+        if events:
+            st.tournaments = len(events)
+            st.best_winner = max(e.winner_fitness for e in events)
+            thr = reward_threshold(self.cfg.tasks[self.task_idx])
+            if self.solved_generation.get(self.task_idx) is None and st.best_winner >= thr:
+                self.solved_generation[self.task_idx] = self.pop.generation - self._task_gen0
+            self._push_genotypes()
+            lo, hi = self.path_offset, self.path_offset + self.P
+            self.fitness_local.copy_(torch.from_numpy(self.pop.fitness[lo:hi]).to(self.device))
+            if self.logger is not None and self.ctx.is_main:
+                for e in events:
+                    # "<step> Step Score: <s>" (doom_pathnet.py:256)
+                    self.logger.log("tournament", step=e.step, generation=e.generation, winner=e.winner,
+                                    score=e.winner_fitness, candidates=e.candidates, scores=e.scores)
+        return st
+
+    # ------------------------------------------------------------------
+    def train(self, steps_per_task: Optional[int] = None, max_updates: Optional[int] = None):
+        steps_per_task = steps_per_task or self.cfg.steps_per_task
+        t0 = time.time()
+        for task_idx in range(len(self.cfg.tasks)):
+            if task_idx != self.task_idx or task_idx > 0:
+                self._start_task(task_idx)
+            n = 0
+            while self.global_step - self.task_start_step < steps_per_task:
+                st = self.update()
+                n += 1
+                if self.logger is not None and self.ctx.is_main and self.updates % 10 == 0:
+                    el = time.time() - t0
+                    self.logger.log("perf", step=self.global_step, steps_per_sec=self.global_step / max(el, 1e-9),
+                                    loss_pi=st.loss_pi, loss_v=st.loss_v, entropy=st.entropy,
+                                    mean_return=st.mean_return, generation=self.pop.generation)
+                if max_updates is not None and n >= max_updates:
+                    break
+            winner, frozen = self.end_task()
+            if self.logger is not None and self.ctx.is_main:
+                self.logger.log("freeze", task=task_idx, winner=winner, frozen=frozen.astype(int).tolist(),
+                                solved_generation=self.solved_generation.get(task_idx))
+        return self.solved_generation

@@ -1,0 +1,241 @@
+"""Configuration: reference hyper-parameters + MI355X presets.
+
+Reference defaults live in ``constants.py`` (module-level constants) and the
+argparse flags of ``doom_pathnet.py:306-361``.  Here they are one dataclass
+tree so a run is fully described by one object (and one JSON blob in the
+checkpoint).  Every field cites where its default comes from.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+# ---------------------------------------------------------------------------
+# Reference constants (ref constants.py:4-32)
+# ---------------------------------------------------------------------------
+LOCAL_T_MAX = 20                 # constants.py:4
+RMSP_ALPHA = 0.99                # constants.py:5
+RMSP_EPSILON = 0.1               # constants.py:6
+CHECKPOINT_DIR = "checkpoints"   # constants.py:7 (unused by the reference)
+INITIAL_ALPHA_LOW = 1e-4         # constants.py:8
+INITIAL_ALPHA_HIGH = 1e-2        # constants.py:9
+PARALLEL_SIZE = 8                # constants.py:11 (unused by the reference)
+ROMZ = ["MsPacman-v0", "Alien-v0"]   # constants.py:14
+ACTION_SIZEZ = [9, 18]               # constants.py:15
+ACTION_SPACE_TYPE = "full"           # constants.py:16
+INITIAL_ALPHA_LOG_RATE = 0.4226      # constants.py:24
+GAMMA = 0.99                         # constants.py:25
+ENTROPY_BETA = 0.01                  # constants.py:26
+MAX_TIME_STEP = 4 * 10 ** 6          # constants.py:27
+GRAD_NORM_CLIP = 40.0                # constants.py:28
+USE_LSTM = True                      # constants.py:30
+USE_PATHNET = True                   # constants.py:32
+FITNESS_PENDING = -1000.0            # doom_pathnet.py:133,248,267 sentinel
+PERFORMANCE_LOG_INTERVAL = 1000      # a3c_training_thread.py:23
+
+
+def log_uniform(lo: float, hi: float, rate: float) -> float:
+    """Geometric interpolation used for lr0 (ref doom_pathnet.py:47-51)."""
+    log_lo = math.log(lo)
+    log_hi = math.log(hi)
+    return math.exp(log_lo * (1 - rate) + log_hi * rate)
+
+
+@dataclass
+class LayerSpec:
+    """One PathNet layer = M parallel modules of one kind.
+
+    kind: "conv" (VALID conv, NHWC, TF kernel layout [kh,kw,cin,cout]) or
+          "fc" (dense [din,dout]).
+    Reference: conv layers ``game_ac_network.py:328-335`` (8 maps each),
+    linear layer ``:340-341`` (1408->256).
+    """
+    kind: str
+    out: int                      # output channels (conv) / width (fc) per module
+    kernel: int = 1               # conv kernel size (square)
+    stride: int = 1               # conv stride
+    module_types: Optional[List[int]] = None   # supervised module2 types per module (pathnet.py:137-168)
+
+
+@dataclass
+class PathNetConfig:
+    """Super-network topology (ref flags --L --M --N --kernel_num --stride_size)."""
+    L: int = 4                                   # doom_pathnet.py:352
+    M: int = 10                                  # doom_pathnet.py:350
+    N: int = 4                                   # doom_pathnet.py:354
+    input_shape: Tuple[int, ...] = (160, 120, 4)  # H,W,C (game_ac_network.py:376)
+    layers: List[LayerSpec] = field(default_factory=list)
+    # FF net divides the summed trunk output by M (game_ac_network.py:194);
+    # LSTM net does not (:394).  "M" | "none".
+    trunk_scale: str = "M"
+    use_lstm: bool = False
+    lstm_size: int = 256                          # game_ac_network.py:397
+    num_actions: int = 18                         # max(ACTION_SIZEZ) unified head (:344)
+    per_task_heads: bool = False                  # paper semantics (commented at :150-151)
+    num_tasks: int = 2
+
+    def __post_init__(self):
+        if not self.layers:
+            self.layers = reference_pixel_layers(self.L)
+        self.L = len(self.layers)
+        self.layers = [l if isinstance(l, LayerSpec) else LayerSpec(**l) for l in self.layers]
+        self.input_shape = tuple(self.input_shape)
+
+    # ---- derived geometry ----
+    def layer_shapes(self):
+        """Per layer: (in_shape, out_shape, K (=fan_in), cin) with NHWC shapes."""
+        shapes = []
+        cur = tuple(self.input_shape)
+        for spec in self.layers:
+            if spec.kind == "conv":
+                H, W, C = cur
+                Ho = (H - spec.kernel) // spec.stride + 1
+                Wo = (W - spec.kernel) // spec.stride + 1
+                if Ho <= 0 or Wo <= 0:
+                    raise ValueError(f"conv layer produces empty output from {cur}")
+                out = (Ho, Wo, spec.out)
+                K = spec.kernel * spec.kernel * C
+                shapes.append((cur, out, K, C))
+            elif spec.kind == "fc":
+                din = int(math.prod(cur))
+                out = (spec.out,)
+                shapes.append((cur, out, din, din))
+            else:
+                raise ValueError(spec.kind)
+            cur = out
+        return shapes
+
+    @property
+    def feature_dim(self) -> int:
+        return int(math.prod(self.layer_shapes()[-1][1]))
+
+    def to_dict(self):
+        return dataclasses.asdict(self)
+
+    @staticmethod
+    def from_dict(d):
+        d = dict(d)
+        d["layers"] = [LayerSpec(**l) for l in d["layers"]]
+        return PathNetConfig(**d)
+
+
+def reference_pixel_layers(L: int = 4, kernels: Sequence[int] = (8, 4, 3),
+                           strides: Sequence[int] = (4, 2, 1), maps: int = 8,
+                           fc: Sequence[int] = (256,)) -> List[LayerSpec]:
+    """Reference trunk: L-1 conv layers (8 maps) + linear PathNet layer(s) of 256.
+
+    ``doom_pathnet.py:356,358`` kernel "8,4,3" stride "4,2,1";
+    ``game_ac_network.py:321`` feature_num=[8,8,8]; ``:341`` 256-wide linear.
+    """
+    nconv = L - len(fc)
+    if nconv > len(kernels):
+        raise ValueError("reference builder supports at most len(kernel_num) conv layers")
+    layers = [LayerSpec("conv", maps, kernels[i], strides[i]) for i in range(nconv)]
+    layers += [LayerSpec("fc", w) for w in fc]
+    return layers
+
+
+@dataclass
+class A2CConfig:
+    t_max: int = LOCAL_T_MAX
+    gamma: float = GAMMA
+    gae_lambda: float = 1.0            # 1.0 == reference n-step return (a3c_training_thread.py:170-180)
+    entropy_beta: float = ENTROPY_BETA
+    value_coef: float = 0.5            # 0.5*l2_loss == 0.25*sum(r-v)^2 (game_ac_network.py:56)
+    reward_clip: float = 1.0           # a3c_training_thread.py:136
+    # loss reduction over envs of one path: "sum" (ref: sum over everything)
+    # or "mean_env" (sum over time, mean over the E envs of a path, sum over paths)
+    env_reduction: str = "mean_env"
+    lr: float = log_uniform(INITIAL_ALPHA_LOW, INITIAL_ALPHA_HIGH, INITIAL_ALPHA_LOG_RATE)
+    lr_anneal: str = "per_task"        # "per_task" | "global" (ref quirk) | "none"
+    max_time_step: int = MAX_TIME_STEP
+    rmsp_alpha: float = RMSP_ALPHA
+    rmsp_epsilon: float = RMSP_EPSILON
+    rmsp_momentum: float = 0.0
+    grad_norm_clip: float = GRAD_NORM_CLIP
+
+
+@dataclass
+class GAConfig:
+    B: int = 3                          # doom_pathnet.py:360 (paper: 2)
+    mutation: str = "ref"               # "ref" (pathnet.py:50-63) | "down" (pathnet.py:32-48)
+    concurrent_tournaments: int = 1     # 1 == reference single tournament at a time
+    fitness: str = "last"               # "last" episode return (ref) | "mean"
+    fitness_window: int = 1
+    freeze_union: bool = True           # keep union of frozen paths across tasks (paper); False = ref quirk
+    seed: int = 1                       # doom_pathnet.py:104 tf.set_random_seed(1)
+
+
+@dataclass
+class TrainConfig:
+    env: str = "Pong"
+    tasks: List[str] = field(default_factory=lambda: ["Pong"])
+    paths: int = 64                     # paths per rank
+    envs_per_path: int = 16
+    net: PathNetConfig = field(default_factory=PathNetConfig)
+    a2c: A2CConfig = field(default_factory=A2CConfig)
+    ga: GAConfig = field(default_factory=GAConfig)
+    backend: str = "auto"               # "hip" | "torch" | "auto"
+    compute_dtype: str = "bf16"
+    use_graph: bool = True
+    seed: int = 1
+    log_dir: str = "./data/tensorboard/"
+    steps_per_task: int = MAX_TIME_STEP
+    checkpoint_every: int = 0
+    frameskip: int = 4
+    gray: str = "rgb"                   # "rgb" luma | "bgr" (reference cv2.COLOR_BGR2GRAY on RGB quirk)
+
+    def to_json(self):
+        return json.dumps(dataclasses.asdict(self))
+
+    @staticmethod
+    def from_json(s):
+        d = json.loads(s)
+        d["net"] = PathNetConfig.from_dict(d["net"])
+        d["a2c"] = A2CConfig(**d["a2c"])
+        d["ga"] = GAConfig(**d["ga"])
+        return TrainConfig(**d)
+
+
+# ---------------------------------------------------------------------------
+# Presets (BASELINE.json configs)
+# ---------------------------------------------------------------------------
+def preset(name: str) -> TrainConfig:
+    name = name.lower()
+    if name in ("cartpole-cpu", "cartpole_cpu"):
+        # BASELINE config 1: CartPole-v1, L=2 x N=4 MLP PathNet, binary tournament, CPU
+        net = PathNetConfig(L=2, M=4, N=2, input_shape=(4,),
+                            layers=[LayerSpec("fc", 32), LayerSpec("fc", 32)],
+                            trunk_scale="none", num_actions=2)
+        return TrainConfig(env="CartPole-v1", tasks=["CartPole-v1"], paths=4, envs_per_path=8,
+                           net=net, ga=GAConfig(B=2), backend="torch", compute_dtype="fp32",
+                           use_graph=False, a2c=A2CConfig(t_max=5, lr=7e-3, lr_anneal="none"))
+    if name == "cartpole":
+        # BASELINE config 2: 64 path-parallel A2C workers on one MI355X, bf16
+        net = PathNetConfig(L=2, M=4, N=2, input_shape=(4,),
+                            layers=[LayerSpec("fc", 32), LayerSpec("fc", 32)],
+                            trunk_scale="none", num_actions=2)
+        return TrainConfig(env="CartPole-v1", tasks=["CartPole-v1"], paths=64, envs_per_path=16,
+                           net=net, ga=GAConfig(B=2), a2c=A2CConfig(t_max=5, lr=7e-3, lr_anneal="none"))
+    if name == "pong":
+        # BASELINE config 3 (headline): Pong pixels, L=3 conv + 2 fc x M=10 modules
+        net = PathNetConfig(L=5, M=10, N=4, input_shape=(160, 120, 4),
+                            layers=reference_pixel_layers(5, fc=(256, 256)),
+                            trunk_scale="M", num_actions=6)
+        return TrainConfig(env="Pong", tasks=["Pong"], paths=64, envs_per_path=32, net=net,
+                           ga=GAConfig(B=3))
+    if name in ("atari4", "atari-suite"):
+        # BASELINE config 5: 4-task suite with unified 18-way head
+        net = PathNetConfig(L=5, M=10, N=4, input_shape=(160, 120, 4),
+                            layers=reference_pixel_layers(5, fc=(256, 256)),
+                            trunk_scale="M", num_actions=18, num_tasks=4)
+        return TrainConfig(env="Pong", tasks=["Pong", "Breakout", "SpaceInvaders", "Alien"],
+                           paths=64, envs_per_path=32, net=net)
+    if name in ("reference", "ref"):
+        # the reference's own default network: L=4 (3 conv + 1 linear), M=10, N=4, LSTM
+        net = PathNetConfig(L=4, M=10, N=4, use_lstm=True, trunk_scale="none", num_actions=18)
+        return TrainConfig(env="Pong", tasks=["Pong", "Breakout"], paths=9, envs_per_path=1, net=net)
+    raise KeyError(name)

@@ -1,0 +1,95 @@
+"""Process-group bootstrap: one process per GPU, torch.distributed over RCCL.
+
+Replaces the reference's TF gRPC parameter-server cluster
+(``doom_pathnet.py:60-91``: ClusterSpec/Server/replica_device_setter).  There
+is no PS: every rank holds a full replica of the 4-17 MB super-network in
+HBM; ranks exchange only the fused per-update buffer (``comm.py``).
+
+Launch: ``python -m torch.distributed.run --nproc-per-node N --master-addr
+127.0.0.1 ...`` (env:// rendezvous).  Backend ``nccl`` is RCCL on ROCm;
+``gloo`` is used for CPU runs/tests.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+    # -- collectives (no-ops at world 1) -----------------------------------
+    def all_reduce_(self, t: torch.Tensor):
+        if self.enabled:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        if not self.enabled:
+            return t.clone()
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out.reshape((self.world * t.shape[0],) + tuple(t.shape[1:]))
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        if self.enabled:
+            dist.broadcast(t, src)
+        return t
+
+    def barrier(self):
+        if self.enabled:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def max_scalar(self, x: float) -> float:
+        if not self.enabled:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def destroy(self):
+        if self.enabled and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def init_distributed(device: Optional[str] = None, backend: Optional[str] = None) -> DistContext:
+    """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available() if device is None else str(device).startswith("cuda")
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
+    if world <= 1:
+        return DistContext(0, 1, 0, "none", dev)
+    be = backend or ("nccl" if use_cuda else "gloo")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if not dist.is_initialized():
+        if be == "nccl":
+            dist.init_process_group(be, rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group(be, rank=rank, world_size=world)
+    return DistContext(rank, world, local_rank, be, dev)
