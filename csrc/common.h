@@ -1,0 +1,82 @@
+// Shared helpers for the pathnet_gym_amd CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave = 64 lanes; workgroups are 256 threads (4 waves) unless noted.
+//  * MFMA: v_mfma_f32_16x16x32_bf16.  Lane l holds A[row=l&15][k=8*(l>>4)+j],
+//    B[k=8*(l>>4)+j][col=l&15] (j=0..7) and C/D[row=4*(l>>4)+r][col=l&15].
+//  * bf16 is carried as uint16 bits; fp32 accumulation everywhere.
+//  * Batch layout of activations: [T][P*E][features] (step-major, path-major
+//    inside a step).  A kernel working on path p sees rows
+//    R = (s, pos) with s in [0, T*E), sample_global = (t0 + s/E)*P*E + p*E + s%E.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned short bf16_t;
+
+#define DEVI __device__ __forceinline__
+
+DEVI float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+DEVI bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);   // round to nearest even (no NaN payload care)
+  return (bf16_t)(u >> 16);
+}
+
+DEVI uint32_t pack2bf(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+DEVI f4v mfma16(const s8v& a, const s8v& b, const f4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// LDS transposed read: within each 16-lane group, lane 4q+p passes the address of
+// row q, columns 4p..4p+3 of a 4x16 block of 16-bit values; lane i receives
+// column i of the 4 rows (row q in element q).
+DEVI s4v lds_tr16(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(p));
+}
+
+DEVI int lane_id() { return threadIdx.x & 63; }
+
+// sample index (in the [T][P*E] batch) of path-local sample s
+DEVI long sample_global(int p, int s, int E, int PE, int t0) {
+  int t = s / E;
+  int e = s - t * E;
+  return (long)(t0 + t) * PE + (long)p * E + e;
+}
+
+// wave-wide sum
+DEVI float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+DEVI float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 32-bit Wang hash: bit-identical to envs/base.py:wang_hash
+DEVI uint32_t wang_hash(uint32_t x) {
+  x = (x ^ 61u) ^ (x >> 16);
+  x = x * 9u;
+  x = x ^ (x >> 4);
+  x = x * 0x27D4EB2Du;
+  x = x ^ (x >> 15);
+  return x;
+}
+
+DEVI uint32_t env_rand_u32(uint32_t seed, uint32_t env_id, uint32_t counter, uint32_t stream) {
+  uint32_t h = wang_hash(counter * 4u + stream);
+  h = wang_hash(h ^ env_id);
+  h = wang_hash(h ^ seed);
+  return h;
+}
+
+#define HIP_LAUNCH_CHECK() (hipGetLastError())

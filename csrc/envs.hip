@@ -1,0 +1,266 @@
+// On-device vectorised environments (bit-identical to envs/pong.py, envs/cartpole.py).
+//
+// pong_step: ONE launch per agent step for all envs.  One workgroup per env:
+//   * physics for `frameskip` sub-frames (integer 1/16-px fixed point, wave-
+//     uniform scalar code), reward/done/auto-reset with random no-op delay;
+//   * render + gray + bilinear resize fused: each thread produces output
+//     pixels of the 160x120 frame by evaluating the scene analytically at the
+//     4 bilinear source pixels of the (never materialised) 210x160 RGB frame
+//     -- game_state.py:41-50 (cvtColor + cv2.resize INTER_LINEAR, 11-bit
+//     fixed-point weights);
+//   * frame-stack push (game_state.py:78): out = (in >> 8) | f << 24 per pixel
+//     (uint32 = 4 uint8 channels, newest last), or f*0x01010101 after a reset.
+// This replaces ALE + OpenCV + the 4-deep numpy stack of the reference.
+#include "common.h"
+
+namespace pong {
+constexpr int SCREEN_W = 160;
+constexpr int OBS_H = 160, OBS_W = 120;
+constexpr int TOP = 34, BOTTOM = 194, WALL_TOP0 = 24;
+constexpr int PADDLE_H = 16, PADDLE_W = 4, BALL_W = 2, BALL_H = 4;
+constexpr int PLAYER_X = 140, CPU_X = 16, U = 16;
+constexpr int PLAYER_SPEED = 40, CPU_SPEED = 28, SERVE_VX = 32, MAX_VX = 64, MAX_VY = 40;
+constexpr int SERVE_DELAY = 16, WIN_SCORE = 21;
+constexpr int DIGIT_SCALE = 4, SCORE_ROW0 = 2;
+enum { BX, BY, VX, VY, PY, CY, PS, CS, SERVE, STEPS, EPRET, NSTATE = 12 };
+__constant__ int DIGITS[10] = {0b111101101101111, 0b010110010010111, 0b111001111100111, 0b111001111001111,
+                               0b101101111001001, 0b111100111001111, 0b111100111101111, 0b111001001001001,
+                               0b111101111101111, 0b111101111001111};
+
+DEVI int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+DEVI uint32_t rnd(uint32_t seed, uint32_t env, uint32_t counter, uint32_t stream, uint32_t n) {
+  return env_rand_u32(seed, env, counter, stream) % n;
+}
+
+struct St {
+  int s[NSTATE];
+};
+
+DEVI int subframe(St& st, int up, int down, uint32_t seed, uint32_t env, uint32_t counter) {
+  int* s = st.s;
+  s[PY] = clampi(s[PY] - up * PLAYER_SPEED + down * PLAYER_SPEED, TOP * U, (BOTTOM - PADDLE_H) * U);
+  const bool serving = s[SERVE] > 0;
+  const bool chase = !serving && s[VX] < 0;
+  const int target = chase ? s[BY] + (BALL_H * U) / 2 - (PADDLE_H * U) / 2 : ((TOP + BOTTOM) / 2 - PADDLE_H / 2) * U;
+  const int dy = clampi(target - s[CY], -CPU_SPEED, CPU_SPEED);
+  s[CY] = clampi(s[CY] + dy, TOP * U, (BOTTOM - PADDLE_H) * U);
+  if (serving) s[SERVE] -= 1;
+  if (serving && s[SERVE] == 0) {
+    s[BX] = 78 * U;
+    s[BY] = (TOP + 20 + (int)rnd(seed, env, counter, 0, BOTTOM - TOP - 40 - BALL_H)) * U;
+    s[VX] = rnd(seed, env, counter, 1, 2) == 0 ? -SERVE_VX : SERVE_VX;
+    s[VY] = (int)rnd(seed, env, counter, 2, 49) - 24;
+  }
+  const bool move = !serving;
+  const int bx = s[BX], by = s[BY];
+  int vx = s[VX], vy = s[VY];
+  int nx = bx + vx, ny = by + vy;
+  if (ny < TOP * U) { ny = 2 * TOP * U - ny; vy = -vy; }
+  if (ny + BALL_H * U > BOTTOM * U) { ny = 2 * (BOTTOM - BALL_H) * U - ny; vy = -vy; }
+  const int face = PLAYER_X * U;
+  const bool hit_p = (vx > 0) && (bx + BALL_W * U <= face) && (nx + BALL_W * U > face) &&
+                     (ny + BALL_H * U > s[PY]) && (ny < s[PY] + PADDLE_H * U);
+  if (hit_p) {
+    const int off = (ny + (BALL_H * U) / 2) - (s[PY] + (PADDLE_H * U) / 2);
+    nx = face - BALL_W * U;
+    vx = -min(abs(vx) + 1, MAX_VX);
+    vy = clampi((off * 3) / 16, -MAX_VY, MAX_VY);
+  }
+  const int cface = (CPU_X + PADDLE_W) * U;
+  const bool hit_c = (vx < 0) && (bx >= cface) && (nx < cface) && (ny + BALL_H * U > s[CY]) &&
+                     (ny < s[CY] + PADDLE_H * U);
+  if (hit_c) {
+    const int coff = (ny + (BALL_H * U) / 2) - (s[CY] + (PADDLE_H * U) / 2);
+    nx = cface;
+    vx = min(abs(vx) + 1, MAX_VX);
+    vy = clampi((coff * 3) / 16, -MAX_VY, MAX_VY);
+  }
+  const bool p_pt = move && (nx + BALL_W * U < 0);
+  const bool c_pt = move && (nx > SCREEN_W * U);
+  const int reward = p_pt ? 1 : (c_pt ? -1 : 0);
+  s[PS] += p_pt;
+  s[CS] += c_pt;
+  if (p_pt || c_pt) s[SERVE] = SERVE_DELAY;
+  if (move) { s[BX] = nx; s[BY] = ny; s[VX] = vx; s[VY] = vy; }
+  return reward;
+}
+
+DEVI void reset_state(St& st, uint32_t seed, uint32_t env, uint32_t counter, int no_op_max, int frameskip) {
+  int* s = st.s;
+  const int mid = ((TOP + BOTTOM) / 2 - PADDLE_H / 2) * U;
+  s[PS] = s[CS] = s[STEPS] = s[EPRET] = 0;
+  s[PY] = s[CY] = mid;
+  s[SERVE] = 1 + (int)rnd(seed, env, counter, 3, (uint32_t)((no_op_max + 1) * frameskip));
+  s[BX] = 78 * U;
+  s[BY] = (TOP + BOTTOM) / 2 * U;
+  s[VX] = s[VY] = 0;
+}
+
+struct Scene {
+  int cy, py, bx, by, vis, cs_t, cs_o, ps_t, ps_o;
+  int g_bg, g_wall, g_cpu, g_player, g_ball;
+};
+
+DEVI bool digit_lit(int dig, bool show, int r, int c, int x0) {
+  if (!show) return false;
+  const int dc = c - x0, dr = r - SCORE_ROW0;
+  if (dc < 0 || dr < 0) return false;
+  const int lc = dc / DIGIT_SCALE, lr = dr / DIGIT_SCALE;
+  if (lc >= 3 || lr >= 5) return false;
+  return (DIGITS[dig] >> (14 - (lr * 3 + lc))) & 1;
+}
+
+DEVI int scene_gray(const Scene& S, int r, int c) {
+  if (r < WALL_TOP0) {
+    if (digit_lit(S.cs_t, S.cs_t > 0, r, c, 24) || digit_lit(S.cs_o, true, r, c, 40)) return S.g_cpu;
+    if (digit_lit(S.ps_t, S.ps_t > 0, r, c, 104) || digit_lit(S.ps_o, true, r, c, 120)) return S.g_player;
+    return S.g_bg;
+  }
+  if (r < TOP || r >= BOTTOM) return S.g_wall;
+  if (S.vis && c >= S.bx && c < S.bx + BALL_W && r >= S.by && r < S.by + BALL_H) return S.g_ball;
+  if (c >= PLAYER_X && c < PLAYER_X + PADDLE_W && r >= S.py && r < S.py + PADDLE_H) return S.g_player;
+  if (c >= CPU_X && c < CPU_X + PADDLE_W && r >= S.cy && r < S.cy + PADDLE_H) return S.g_cpu;
+  return S.g_bg;
+}
+}  // namespace pong
+
+// state [B][12] int32, counter [B] uint32, actions [B] int32 (any int; >= n_actions remapped to 0)
+// obs_in/obs_out [B][160*120] uint32 (4 stacked uint8 frames), tables [8][160] int32
+__global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state, uint32_t* __restrict__ counter,
+                                                        const int* __restrict__ actions, int n_actions,
+                                                        const uint32_t* __restrict__ obs_in,
+                                                        uint32_t* __restrict__ obs_out, const int* __restrict__ tables,
+                                                        float* __restrict__ reward_out, uint8_t* __restrict__ done_out,
+                                                        float* __restrict__ epret_out, uint32_t seed, int frameskip,
+                                                        int max_steps, int no_op_max, int g_bg, int g_wall, int g_cpu,
+                                                        int g_player, int g_ball) {
+  using namespace pong;
+  __shared__ int tab[8 * 160];
+  const int env = blockIdx.x;
+  for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
+  // --- physics (wave-uniform; every thread computes the same values) ---
+  St st;
+#pragma unroll
+  for (int i = 0; i < NSTATE; ++i) st.s[i] = state[env * NSTATE + i];
+  uint32_t ctr = counter[env];
+  int a = actions[env];
+  if (a >= n_actions || a < 0) a = 0;                    // game_state.py:38-39
+  const int up = (a == 2 || a == 4), down = (a == 3 || a == 5);
+  int reward = 0;
+  for (int f = 0; f < frameskip; ++f) reward += subframe(st, up, down, seed, (uint32_t)env, ctr);
+  ctr += 1;
+  st.s[STEPS] += 1;
+  st.s[EPRET] += reward;
+  const bool done = st.s[PS] >= WIN_SCORE || st.s[CS] >= WIN_SCORE || st.s[STEPS] >= max_steps;
+  const int epret = st.s[EPRET];
+  if (done) {
+    reset_state(st, seed, (uint32_t)env, ctr, no_op_max, frameskip);
+    ctr += 1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NSTATE; ++i) state[env * NSTATE + i] = st.s[i];
+    counter[env] = ctr;
+    reward_out[env] = (float)reward;
+    done_out[env] = done ? 1 : 0;
+    epret_out[env] = done ? (float)epret : 0.f;
+  }
+  // --- fused render + gray + resize + stack push ---
+  Scene S;
+  S.cy = st.s[CY] >> 4;   // floor division by U=16 (values are non-negative)
+  S.py = st.s[PY] >> 4;
+  S.bx = st.s[BX] >= 0 ? st.s[BX] / U : -((-st.s[BX] + U - 1) / U);   // floor
+  S.by = st.s[BY] >= 0 ? st.s[BY] / U : -((-st.s[BY] + U - 1) / U);
+  S.vis = st.s[SERVE] == 0;
+  S.cs_t = st.s[CS] / 10; S.cs_o = st.s[CS] % 10;
+  S.ps_t = st.s[PS] / 10; S.ps_o = st.s[PS] % 10;
+  S.g_bg = g_bg; S.g_wall = g_wall; S.g_cpu = g_cpu; S.g_player = g_player; S.g_ball = g_ball;
+  const long base = (long)env * OBS_H * OBS_W;
+  for (int pix = threadIdx.x; pix < OBS_H * OBS_W; pix += 256) {
+    const int y = pix / OBS_W, x = pix - y * OBS_W;
+    const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
+    const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x], cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
+    const int ra = scene_gray(S, ys0, xs0) * cx0 + scene_gray(S, ys0, xs1) * cx1;
+    const int rb = scene_gray(S, ys1, xs0) * cx0 + scene_gray(S, ys1, xs1) * cx1;
+    int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+    const uint32_t f = (uint32_t)v;
+    obs_out[base + pix] = done ? f * 0x01010101u : ((obs_in[base + pix] >> 8) | (f << 24));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CartPole-v1: thread per env. state [B][4] f32, steps [B] i32, epret [B] f32,
+// counter [B] u32; writes obs bf16 [B][8] (zero padded) for the trunk.
+// ---------------------------------------------------------------------------
+__global__ void cartpole_step_kernel(float* __restrict__ state, int* __restrict__ steps, float* __restrict__ epret,
+                                     uint32_t* __restrict__ counter, const int* __restrict__ actions, int B,
+                                     uint32_t seed, int max_steps, float* __restrict__ obs_f32,
+                                     bf16_t* __restrict__ obs_bf16, float* __restrict__ reward_out,
+                                     uint8_t* __restrict__ done_out, float* __restrict__ epret_out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float g = 9.8f, mc = 1.0f, mp = 0.1f, tm = mc + mp, len = 0.5f, pml = mp * len, fm = 10.0f, tau = 0.02f;
+  const float th_thr = 12.f * 2.f * 3.14159265358979323846f / 360.f, x_thr = 2.4f;
+  float x = state[b * 4 + 0], xd = state[b * 4 + 1], th = state[b * 4 + 2], thd = state[b * 4 + 3];
+  const float force = actions[b] == 1 ? fm : -fm;
+  const float ct = cosf(th), st = sinf(th);
+  const float temp = (force + pml * thd * thd * st) / tm;
+  const float thacc = (g * st - ct * temp) / (len * (4.0f / 3.0f - mp * ct * ct / tm));
+  const float xacc = temp - pml * thacc * ct / tm;
+  x = x + tau * xd;
+  xd = xd + tau * xacc;
+  th = th + tau * thd;
+  thd = thd + tau * thacc;
+  const int n = steps[b] + 1;
+  const bool fell = x < -x_thr || x > x_thr || th < -th_thr || th > th_thr;
+  const bool done = fell || n >= max_steps;
+  const float er = epret[b] + 1.0f;
+  uint32_t ctr = counter[b];
+  reward_out[b] = 1.0f;
+  done_out[b] = done;
+  epret_out[b] = done ? er : 0.f;
+  if (done) {
+    float u[4];
+    for (int s = 0; s < 4; ++s) u[s] = (float)(env_rand_u32(seed, (uint32_t)b, ctr, (uint32_t)s) >> 8) * (1.0f / 16777216.0f);
+    x = u[0] * 0.1f - 0.05f; xd = u[1] * 0.1f - 0.05f; th = u[2] * 0.1f - 0.05f; thd = u[3] * 0.1f - 0.05f;
+    ctr += 1;
+  }
+  counter[b] = ctr;
+  steps[b] = done ? 0 : n;
+  epret[b] = done ? 0.f : er;
+  state[b * 4 + 0] = x; state[b * 4 + 1] = xd; state[b * 4 + 2] = th; state[b * 4 + 3] = thd;
+  if (obs_f32) { obs_f32[b * 4 + 0] = x; obs_f32[b * 4 + 1] = xd; obs_f32[b * 4 + 2] = th; obs_f32[b * 4 + 3] = thd; }
+  if (obs_bf16) {
+    uint4 o;
+    o.x = pack2bf(x, xd);
+    o.y = pack2bf(th, thd);
+    o.z = 0;
+    o.w = 0;
+    *reinterpret_cast<uint4*>(obs_bf16 + (long)b * 8) = o;
+  }
+}
+
+extern "C" {
+int launch_pong_step(void* state, void* counter, const int* actions, int n_actions, const void* obs_in, void* obs_out,
+                     const int* tables, float* reward, void* done, float* epret, int B, unsigned seed, int frameskip,
+                     int max_steps, int no_op_max, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
+                     hipStream_t stream) {
+  pong_step_kernel<<<B, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions,
+                                          (const uint32_t*)obs_in, (uint32_t*)obs_out, tables, reward,
+                                          (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max, g_bg, g_wall,
+                                          g_cpu, g_player, g_ball);
+  return (int)hipGetLastError();
+}
+
+int launch_cartpole_step(float* state, int* steps, float* epret, void* counter, const int* actions, int B,
+                         unsigned seed, int max_steps, float* obs_f32, void* obs_bf16, float* reward, void* done,
+                         float* epret_out, hipStream_t stream) {
+  cartpole_step_kernel<<<(B + 255) / 256, 256, 0, stream>>>(state, steps, epret, (uint32_t*)counter, actions, B, seed,
+                                                            max_steps, obs_f32, (bf16_t*)obs_bf16, reward,
+                                                            (uint8_t*)done, epret_out);
+  return (int)hipGetLastError();
+}
+}

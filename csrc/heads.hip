@@ -1,0 +1,273 @@
+// Actor-critic heads, sampling and the A2C loss gradient (CDNA4).
+//
+//  heads_fwd_sample : logits = feat Wp + bp, v = feat Wv + bv, action ~ softmax
+//                     by Gumbel-max on a counter-based hash RNG (replaces
+//                     np.random.choice on the host, a3c_training_thread.py:89-90).
+//                     One wave per sample.
+//  a2c_grad         : reverse scan over T (n-step return / GAE, reward clip,
+//                     a3c_training_thread.py:155-180) fused with the analytic
+//                     gradient of the reference loss (game_ac_network.py:38-59)
+//                     w.r.t. logits and value.  One thread per env.
+//  heads_bwd        : dfeat = dz Wp^T + dv Wv^T and dWp/dbp/dWv/dbv.
+#include "common.h"
+
+#define AMAX 32
+
+// key for the sampling RNG: depends on (seed, update counter, step, sample, action)
+DEVI float u01(uint32_t seed, uint32_t stepkey, uint32_t b, uint32_t j) {
+  uint32_t h = wang_hash(stepkey * 64u + j);
+  h = wang_hash(h ^ b);
+  h = wang_hash(h ^ seed);
+  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+__global__ __launch_bounds__(256) void heads_fwd_sample_kernel(
+    const bf16_t* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
+    int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
+    const long long* __restrict__ ctr, int t, int T, int greedy) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + w;
+  if (b >= B) return;
+  float part[AMAX];
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) part[j] = 0.f;
+  float pv = 0.f;
+  for (int f = l; f < F; f += 64) {
+    const float x = bf2f(feat[(long)b * F + f]);
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j)
+      if (j < A) part[j] += x * flat[pw + (long)f * A + j];
+    pv += x * flat[vw + f];
+  }
+  float lg[AMAX];
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) lg[j] = wave_sum(part[j]) + flat[pb + j];
+  pv = wave_sum(pv) + flat[vb];
+  if (l == 0) {
+    const uint32_t stepkey = (uint32_t)(ctr[0] * T + t);
+    int best = 0;
+    float bv = -3.0e38f;
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) {
+      if (j < A) {
+        logits[(long)b * A + j] = lg[j];
+        float s = lg[j];
+        if (!greedy) s += -__logf(-__logf(u01(seed, stepkey, (uint32_t)b, (uint32_t)j)));
+        if (s > bv) { bv = s; best = j; }
+      }
+    }
+    value[b] = pv;
+    actions[b] = best;
+  }
+}
+
+// logits/values/actions/rewards/dones: [T][B](...); vboot [B]
+__global__ __launch_bounds__(256) void a2c_grad_kernel(
+    const float* __restrict__ logits, const float* __restrict__ values, const int* __restrict__ actions,
+    const float* __restrict__ rewards, const uint8_t* __restrict__ dones, const float* __restrict__ vboot, int T,
+    int B, int A, float gamma, float lam, float rclip, float beta, float vcoef, float weight,
+    float* __restrict__ dlogits, float* __restrict__ dvalue, float* __restrict__ stats) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  float spol = 0.f, sval = 0.f, sent = 0.f;
+  if (b < B) {
+    float R = vboot[b];
+    float gae = 0.f;
+    float next_v = vboot[b];
+    for (int t = T - 1; t >= 0; --t) {
+      const long i = (long)t * B + b;
+      float r = rewards[i];
+      if (rclip > 0.f) r = fminf(fmaxf(r, -rclip), rclip);
+      const float nd = dones[i] ? 0.f : 1.f;
+      const float v = values[i];
+      float adv;
+      if (lam == 1.0f) {
+        R = r + gamma * R * nd;
+        adv = R - v;
+      } else {
+        const float delta = r + gamma * next_v * nd - v;
+        gae = delta + gamma * lam * nd * gae;
+        adv = gae;
+        R = gae + v;
+        next_v = v;
+      }
+      // softmax + clipped log (game_ac_network.py:38)
+      float z[AMAX];
+      float m = -3.0e38f;
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) { z[j] = logits[i * A + j]; m = fmaxf(m, z[j]); }
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) { z[j] = __expf(z[j] - m); se += z[j]; }
+      const float inv = 1.f / se;
+      float H = 0.f;
+      float lp[AMAX];
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) {
+          z[j] *= inv;                                   // pi
+          lp[j] = __logf(fmaxf(z[j], 1e-20f));
+          H -= z[j] * lp[j];
+        }
+      const int a = actions[i];
+      float lpa = 0.f;
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A && j == a) lpa = lp[j];
+      spol += -(lpa * adv + beta * H) * weight;
+      sval += vcoef * 0.5f * (R - v) * (R - v) * weight;
+      sent += H;
+      // d/dz_j [-(log pi_a * adv) - beta*H] = -adv*(1[j==a] - pi_j) + beta*pi_j*(log pi_j + H)
+      const bool live_a = true;   // clip(pi,1e-20) has zero grad below 1e-20; negligible, ignored
+      (void)live_a;
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) {
+          const float oh = (j == a) ? 1.f : 0.f;
+          dlogits[i * A + j] = weight * (-adv * (oh - z[j]) + beta * z[j] * (lp[j] + H));
+        }
+      dvalue[i] = weight * vcoef * (v - R);
+    }
+  }
+  // block reduce stats
+  __shared__ float red[3][4];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  spol = wave_sum(spol);
+  sval = wave_sum(sval);
+  sent = wave_sum(sent);
+  if (l == 0) { red[0][w] = spol; red[1][w] = sval; red[2][w] = sent; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const float s = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+    atomicAdd(&stats[threadIdx.x], s);
+  }
+}
+
+// grid = ceil(N / ROWS), block 256 (thread = feature f, looping f += 256)
+#define HB_ROWS 128
+__global__ __launch_bounds__(256) void heads_bwd_kernel(
+    const bf16_t* __restrict__ feat, int F, const float* __restrict__ dlogits, const float* __restrict__ dvalue,
+    int N, int A, const float* __restrict__ flat, long pw, long pb, long vw, long vb, float* __restrict__ grad,
+    float* __restrict__ dfeat) {
+  const long r0 = (long)blockIdx.x * HB_ROWS;
+  const long r1 = min((long)N, r0 + HB_ROWS);
+  for (int f = threadIdx.x; f < F; f += 256) {
+    float w[AMAX], gw[AMAX];
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) {
+      w[j] = j < A ? flat[pw + (long)f * A + j] : 0.f;
+      gw[j] = 0.f;
+    }
+    const float wv = flat[vw + f];
+    float gv = 0.f;
+    for (long r = r0; r < r1; ++r) {
+      const float x = bf2f(feat[r * F + f]);
+      const float dv = dvalue[r];
+      float d = dv * wv;
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) {
+          const float dz = dlogits[r * A + j];
+          d += dz * w[j];
+          gw[j] += x * dz;
+        }
+      gv += x * dv;
+      dfeat[r * F + f] = d;
+    }
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j)
+      if (j < A) atomicAdd(&grad[pw + (long)f * A + j], gw[j]);
+    atomicAdd(&grad[vw + f], gv);
+  }
+  if (threadIdx.x < 64) {
+    // bias grads: wave 0 reduces dz / dv over the chunk
+    const int l = threadIdx.x;
+    float bz[AMAX];
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) bz[j] = 0.f;
+    float bvv = 0.f;
+    for (long r = r0 + l; r < r1; r += 64) {
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) bz[j] += dlogits[r * A + j];
+      bvv += dvalue[r];
+    }
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j)
+      if (j < A) {
+        const float s = wave_sum(bz[j]);
+        if (l == 0) atomicAdd(&grad[pb + j], s);
+      }
+    bvv = wave_sum(bvv);
+    if (l == 0) atomicAdd(&grad[vb], bvv);
+  }
+}
+
+extern "C" {
+
+int launch_heads_fwd_sample(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb, int A,
+                            int B, float* logits, float* value, int* actions, unsigned seed, const long long* ctr,
+                            int t, int T, int greedy, hipStream_t stream) {
+  if (A > AMAX || A < 1) return -1;
+  heads_fwd_sample_kernel<<<(B + 3) / 4, 256, 0, stream>>>((const bf16_t*)feat, F, flat, pw, pb, vw, vb, A, B, logits,
+                                                            value, actions, seed, ctr, t, T, greedy);
+  return (int)hipGetLastError();
+}
+
+int launch_a2c_grad(const float* logits, const float* values, const int* actions, const float* rewards,
+                    const void* dones, const float* vboot, int T, int B, int A, float gamma, float lam, float rclip,
+                    float beta, float vcoef, float weight, float* dlogits, float* dvalue, float* stats,
+                    hipStream_t stream) {
+  if (A > AMAX) return -1;
+  a2c_grad_kernel<<<(B + 255) / 256, 256, 0, stream>>>(logits, values, actions, rewards, (const uint8_t*)dones,
+                                                        vboot, T, B, A, gamma, lam, rclip, beta, vcoef, weight,
+                                                        dlogits, dvalue, stats);
+  return (int)hipGetLastError();
+}
+
+int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float* dvalue, int N, int A,
+                     const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
+                     hipStream_t stream) {
+  if (A > AMAX) return -1;
+  heads_bwd_kernel<<<(N + HB_ROWS - 1) / HB_ROWS, 256, 0, stream>>>((const bf16_t*)feat, F, dlogits, dvalue, N, A,
+                                                                     flat, pw, pb, vw, vb, grad, dfeat);
+  return (int)hipGetLastError();
+}
+}
+
+// ---------------------------------------------------------------------------
+// fitness bookkeeping after a rollout: per path, the return of the most
+// recently finished episode(s) (a3c_training_thread.py:145-147; mean over
+// envs finishing at the same step), plus episode counters.  Thread per path.
+// counters: [0] agent steps, [1] episodes finished, [2] sum of their returns.
+// ---------------------------------------------------------------------------
+__global__ void fitness_update_kernel(const uint8_t* __restrict__ dones, const float* __restrict__ epret, int T, int P,
+                                      int E, float* __restrict__ fitness, float* __restrict__ counters) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p == 0) counters[0] = (float)T * P * E;
+  if (p >= P) return;
+  float fit = fitness[p];
+  float nep = 0.f, sret = 0.f;
+  for (int t = 0; t < T; ++t) {
+    float c = 0.f, s = 0.f;
+    for (int e = 0; e < E; ++e) {
+      const long i = (long)t * P * E + (long)p * E + e;
+      if (dones[i]) { c += 1.f; s += epret[i]; }
+    }
+    if (c > 0.f) fit = s / c;
+    nep += c;
+    sret += s;
+  }
+  fitness[p] = fit;
+  atomicAdd(&counters[1], nep);
+  atomicAdd(&counters[2], sret);
+}
+
+extern "C" int launch_fitness_update(const void* dones, const float* epret, int T, int P, int E, float* fitness,
+                                     float* counters, hipStream_t stream) {
+  hipMemsetAsync(counters, 0, sizeof(float) * 4, stream);
+  fitness_update_kernel<<<(P + 63) / 64, 64, 0, stream>>>((const uint8_t*)dones, epret, T, P, E, fitness, counters);
+  return (int)hipGetLastError();
+}

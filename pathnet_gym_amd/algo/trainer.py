@@ -115,8 +115,15 @@ class PathNetTrainer:
         self.obs = self.env.reset()
         B = self.P * self.E
         self.lstm_state = self.model.init_state(B)
-        self.fitness_local = torch.full((self.P,), FITNESS_PENDING, device=self.device)
         self._push_genotypes()
+        self.engine = None
+        if self.backend == "hip":
+            from ..runtime.engine import HipEngine
+            self.engine = HipEngine(self.model, self.env, self.cfg, self.opt,
+                                    seed=self.cfg.seed * 1000003 + self.ctx.rank * 7919 + task_idx)
+            self.fitness_local = self.engine.fitness
+        else:
+            self.fitness_local = torch.full((self.P,), FITNESS_PENDING, device=self.device)
         self.task_start_step = self.global_step
         self.solved_generation.setdefault(task_idx, None)
         self._task_gen0 = self.pop.generation
@@ -142,6 +149,7 @@ class PathNetTrainer:
             f.copy_(torch.where(keep_t, f, self.init_flat))
         if self.backend == "hip":
             self.model.hip.refresh_weights()
+            self.engine.refresh_trainable()
         return winner, frozen
 
     # ------------------------------------------------------------------
@@ -201,14 +209,20 @@ class PathNetTrainer:
         return flat.grad, counters, (lp, lv, ent)
 
     def update(self) -> UpdateStats:
-        grad, counters, (lp, lv, ent) = self.rollout_and_backward()
-        fit_all, csum = self.comm.exchange(grad, self.fitness_local, counters)
         lr = anneal_lr(self.cfg.a2c.lr, self.global_step, self.cfg.a2c.max_time_step,
                        self.task_start_step, self.cfg.a2c.lr_anneal)
-        with torch.no_grad():
-            self.opt.step(grad, lr)
-        if self.backend == "hip":
-            self.model.hip.refresh_weights()
+        if self.engine is not None:
+            eng = self.engine
+            eng.rollout_backward()
+            fit_all, csum = self.comm.exchange(eng.grad_flat, eng.fitness, eng.counters)
+            eng.optimizer_step(lr)
+            lp, lv, ent = [float(x) for x in eng.stats_host()[:3]]
+            ent /= max(1, self.cfg.a2c.t_max * self.P * self.E)
+        else:
+            grad, counters, (lp, lv, ent) = self.rollout_and_backward()
+            fit_all, csum = self.comm.exchange(grad, self.fitness_local, counters)
+            with torch.no_grad():
+                self.opt.step(grad, lr)
         self.global_step += int(csum[0])
         self.updates += 1
         st = UpdateStats(float(lp), float(lv), float(ent), int(csum[1]),

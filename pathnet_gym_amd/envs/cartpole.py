@@ -50,7 +50,8 @@ class CartPoleVec(VecEnv):
         self.seed(seed)
 
     def seed(self, seed: int):
-        self._seed = torch.tensor(seed & 0xFFFFFFFF, dtype=torch.int64, device=self.device)
+        self.seed_int = seed & 0xFFFFFFFF
+        self._seed = torch.tensor(self.seed_int, dtype=torch.int64, device=self.device)
         self.counter.zero_()
 
     def _rand_state(self, mask):
@@ -66,9 +67,16 @@ class CartPoleVec(VecEnv):
         return self.state.clone()
 
     def reset_where(self, mask):
+        hip_state = hasattr(self, "_steps32")
+        if hip_state:
+            self.steps = self._steps32.long()
+            self.counter = self._ctr32.long() & 0xFFFFFFFF
         self.state = self._rand_state(mask)
         self.steps = torch.where(mask, torch.zeros_like(self.steps), self.steps)
         self.ep_ret = torch.where(mask, torch.zeros_like(self.ep_ret), self.ep_ret)
+        if hip_state:
+            from ..ops import envs as henv
+            henv.cartpole_sync_to_device(self)
 
     def step(self, actions: torch.Tensor):
         if self.backend == "hip":

@@ -193,7 +193,8 @@ class PongVec(VecEnv):
         self.seed(seed)
 
     def seed(self, seed: int):
-        self._seed = torch.tensor(seed & 0xFFFFFFFF, dtype=torch.int64, device=self.device)
+        self.seed_int = seed & 0xFFFFFFFF
+        self._seed = torch.tensor(self.seed_int, dtype=torch.int64, device=self.device)
         self.counter.zero_()
 
     # -- rng -------------------------------------------------------------------
@@ -304,11 +305,17 @@ class PongVec(VecEnv):
         return self.obs.clone()
 
     def reset_where(self, mask):
+        hip_state = hasattr(self, "_st32")
+        if hip_state:
+            from ..ops import envs as henv
+            henv.pong_sync_from_device(self)
         self._reset_state(mask)
         self.counter += mask.long()
         f = self.frame()
         stack = f[..., None].expand(-1, -1, -1, 4)
         self.obs = torch.where(mask[:, None, None, None], stack, self.obs)
+        if hip_state:
+            henv.pong_sync_to_device(self)
 
     def step(self, actions: torch.Tensor):
         if self.backend == "hip":

@@ -47,6 +47,7 @@ class ACPathNet:
         if backend == "hip":
             from ..ops.pathnet_ops import HipPathNet
             self.hip = HipPathNet(self)
+            self.hip.set_paths(self.mask.cpu().numpy())
 
     # ------------------------------------------------------------------
     def set_paths(self, expressed: np.ndarray):
@@ -57,6 +58,8 @@ class ACPathNet:
         self.mask.copy_(torch.from_numpy(expressed))
         self.act_idx.copy_(torch.from_numpy(idx))
         self.act_cnt.copy_(torch.from_numpy(cnt))
+        if self.hip is not None:
+            self.hip.set_paths(expressed)
 
     def set_frozen(self, frozen: np.ndarray):
         self.frozen = np.asarray(frozen, np.float32).copy()

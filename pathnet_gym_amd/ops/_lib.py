@@ -1,0 +1,102 @@
+"""ctypes binding of ``libpathnet_hip.so`` (the hand-written gfx950 kernels).
+
+The library exports a plain C ABI: raw device pointers, scalars and a
+``hipStream_t``.  It is loaded AFTER torch so that it binds to the HIP
+runtime torch already loaded (same SONAME ``libamdhip64.so.7``): torch
+tensors' ``data_ptr()`` and torch streams are valid handles for it, and
+kernels launched on torch's current stream are captured by
+``torch.cuda.graph`` (hipGraph) like any torch op.
+
+No silent fallback: on a GPU box a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_long, c_uint, c_void_p, c_size_t
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_hip", "libpathnet_hip.so")
+
+P = c_void_p
+_SIGS = {
+    "launch_conv_fwd": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                        c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float,
+                        c_float, P],
+    "launch_fc_fwd": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                      c_int, c_int, c_int, c_long, c_float, P],
+    "launch_conv_wgrad": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                          c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_int,
+                          c_float, c_float, P],
+    "launch_conv_dgrad": [P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                          c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, P, P],
+    "launch_fc_dgrad": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float,
+                        P, P],
+    "launch_fc_wgrad": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                        c_int, c_int, c_long, c_float, P],
+    "launch_heads_fwd_sample": [P, c_int, P, c_long, c_long, c_long, c_long, c_int, c_int, P, P, P, c_uint, P, c_int,
+                                c_int, c_int, P],
+    "launch_a2c_grad": [P, P, P, P, P, P, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_float, c_float,
+                        P, P, P, P],
+    "launch_heads_bwd": [P, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P],
+    "launch_fitness_update": [P, P, c_int, c_int, c_int, P, P, P],
+    "launch_rmsprop": [P, P, P, P, P, P, P, c_int, P, c_int, P, P, c_float, c_float, c_float, c_float, P],
+    "launch_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
+    "launch_pong_step": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int, c_int, c_int,
+                         c_int, c_int, P],
+    "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_int, P, P, P, P, P, P],
+    "conv_fwd_smem": [c_int, c_int],
+    "conv_wgrad_smem": [c_int],
+}
+
+_lib = None
+
+
+def available() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"HIP kernel library missing at {LIB_PATH}; run `python -m pathnet_gym_amd._build`")
+        _lib = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(_lib, name)
+            fn.argtypes = args
+            fn.restype = c_size_t if name.endswith("_smem") else c_int
+    return _lib
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def check(t: torch.Tensor, dtype=None, shape=None, numel=None, name="tensor", cuda=True):
+    """Host-side validation before any launch (a bad shape must never reach a kernel)."""
+    if cuda and t.device.type != "cuda":
+        raise ValueError(f"{name} must be on the GPU")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name}: dtype {t.dtype} != {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)} != {tuple(shape)}")
+    if numel is not None and t.numel() < numel:
+        raise ValueError(f"{name}: numel {t.numel()} < required {numel}")
+    return t

@@ -1,0 +1,106 @@
+"""HIP env stepping (``csrc/envs.hip``) for the on-device environments.
+
+Two entry points per env:
+* ``*_step_into``: engine path -- reads obs slot t, writes slot t+1 and the
+  reward/done/episode-return rows of the rollout buffers in ONE launch;
+* ``*_step``: the generic VecEnv API (allocates outputs), used by tests to
+  compare bit-for-bit against the torch implementation.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+# ------------------------------------------------------------------ Pong
+def pong_sync_to_device(env):
+    """(Re)build the int32 kernel state from the torch (int64) state."""
+    env._st32 = env.state.to(torch.int32).contiguous()
+    env._ctr32 = env.counter.to(torch.int32).contiguous()
+    env._tab32 = env.tables.to(torch.int32).contiguous()
+
+
+def pong_sync_from_device(env):
+    env.state = env._st32.to(torch.int64)
+    env.counter = env._ctr32.to(torch.int64) & 0xFFFFFFFF
+
+
+def _gray_consts(env):
+    from ..envs import pong as pg
+    wr, wg, wb = pg.gray_weights(env.gray)
+
+    def g(c):
+        return (c[0] * wr + c[1] * wg + c[2] * wb + 8192) >> 14
+    return [g(pg.COLOR_BG), g(pg.COLOR_WALL), g(pg.COLOR_CPU), g(pg.COLOR_PLAYER), g(pg.COLOR_BALL)]
+
+
+def pong_step_into(env, actions, obs_in, obs_out, reward, done, epret):
+    B = env.num_envs
+    if not hasattr(env, "_st32"):
+        pong_sync_to_device(env)
+    _lib.check(actions, torch.int32, (B,), name="actions")
+    _lib.check(obs_in, torch.uint8, numel=B * 160 * 120 * 4, name="obs_in")
+    _lib.check(obs_out, torch.uint8, numel=B * 160 * 120 * 4, name="obs_out")
+    _lib.check(reward, torch.float32, numel=B, name="reward")
+    _lib.check(done, torch.uint8, numel=B, name="done")
+    _lib.check(epret, torch.float32, numel=B, name="epret")
+    if not hasattr(env, "_gray"):
+        env._gray = _gray_consts(env)
+    g = env._gray
+    _lib.call("launch_pong_step", env._st32.data_ptr(), env._ctr32.data_ptr(), actions.data_ptr(), env.num_actions,
+              obs_in.data_ptr(), obs_out.data_ptr(), env._tab32.data_ptr(), reward.data_ptr(), done.data_ptr(),
+              epret.data_ptr(), B, env.seed_int, env.frameskip, env.max_episode_steps,
+              env.no_op_max, g[0], g[1], g[2], g[3], g[4], _lib.stream())
+
+
+def pong_step(env, actions, obs):
+    B = env.num_envs
+    dev = obs.device
+    out = torch.empty_like(obs)
+    reward = torch.empty(B, dtype=torch.float32, device=dev)
+    done = torch.empty(B, dtype=torch.uint8, device=dev)
+    epret = torch.empty(B, dtype=torch.float32, device=dev)
+    pong_step_into(env, actions.to(torch.int32).contiguous(), obs.contiguous(), out, reward, done, epret)
+    env.obs = out
+    return out.clone(), reward, done.bool(), {"episode_return": epret}
+
+
+# ------------------------------------------------------------------ CartPole
+def cartpole_sync_to_device(env):
+    env._steps32 = env.steps.to(torch.int32).contiguous()
+    env._ctr32 = env.counter.to(torch.int32).contiguous()
+    env.state = env.state.contiguous()
+    env.ep_ret = env.ep_ret.contiguous()
+
+
+def cartpole_step_into(env, actions, obs_bf16_out, reward, done, epret, obs_f32_out=None):
+    B = env.num_envs
+    if not hasattr(env, "_steps32"):
+        cartpole_sync_to_device(env)
+    _lib.check(actions, torch.int32, (B,), name="actions")
+    if obs_bf16_out is not None:
+        _lib.check(obs_bf16_out, torch.bfloat16, numel=B * 8, name="obs_bf16")
+    _lib.call("launch_cartpole_step", env.state.data_ptr(), env._steps32.data_ptr(), env.ep_ret.data_ptr(),
+              env._ctr32.data_ptr(), actions.data_ptr(), B, env.seed_int,
+              env.max_episode_steps, _lib.ptr(obs_f32_out), _lib.ptr(obs_bf16_out), reward.data_ptr(),
+              done.data_ptr(), epret.data_ptr(), _lib.stream())
+
+
+def cartpole_step(env, actions):
+    B = env.num_envs
+    dev = env.state.device
+    obs = torch.empty(B, 4, dtype=torch.float32, device=dev)
+    reward = torch.empty(B, dtype=torch.float32, device=dev)
+    done = torch.empty(B, dtype=torch.uint8, device=dev)
+    epret = torch.empty(B, dtype=torch.float32, device=dev)
+    cartpole_step_into(env, actions.to(torch.int32).contiguous(), None, reward, done, epret, obs_f32_out=obs)
+    return obs, reward, done.bool(), {"episode_return": epret}
+
+
+def obs_to_bf16_padded(obs_f32: torch.Tensor) -> torch.Tensor:
+    """[B, d<=8] float -> [B, 8] bf16 zero padded (trunk input for vector envs)."""
+    B, d = obs_f32.shape
+    out = torch.zeros(B, 8, dtype=torch.bfloat16, device=obs_f32.device)
+    out[:, :d] = obs_f32.to(torch.bfloat16)
+    return out

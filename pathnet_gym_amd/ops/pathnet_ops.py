@@ -1,0 +1,256 @@
+"""HIP PathNet trunk: geometry, bf16 MFMA operand copies, per-layer launches.
+
+Buffers (all device, B = P*E, slots = T+1 steps so the bootstrap forward can
+reuse them):
+
+=============  =========================================  ==================
+name           layout                                     written by
+=============  =========================================  ==================
+obs            [T+1][B][H*W*C] uint8 (pixels) or           env step kernel
+               [T+1][B][8] bf16 (vector envs)
+acts[l]        [T+1][B][HWo*Cout] bf16 (module-sum out)    fwd epilogue
+bits[l] conv   [M][(T+1)*B*HWo] uint8 (8 maps/byte)        fwd epilogue
+bits[l] fc     [M][(T+1)*B][Cout/16] uint16                fwd epilogue
+grads[l]       [T*B][HWo*Cout] fp32 (dL/d acts[l])         dgrad of l+1 /
+                                                           heads_bwd (l=L-1)
+Wc[l]          [M][Cout][KP] bf16  (B operand, fwd)        refresh kernel
+WcT[l] (fc)    [M][KP][Cout] bf16  (B operand, fc dgrad)   refresh kernel
+=============  =========================================  ==================
+
+``bits`` rows are indexed by GLOBAL row (sample_global*HWo + pos) so the
+forward of step t and the whole-rollout backward agree.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class LayerGeom:
+    kind: str
+    K: int
+    KP: int
+    Cout: int
+    HWo: int
+    out_feat: int
+    w_off: int
+    chunk: int
+    Hin: int = 1
+    Win: int = 1
+    Cin: int = 1
+    KH: int = 1
+    KW: int = 1
+    S: int = 1
+    Ho: int = 1
+    Wo: int = 1
+    ldx: int = 0            # fc input row stride
+    u8in: bool = False
+    in_scale: float = 1.0
+
+    @property
+    def b_off(self):
+        return self.w_off + self.K * self.Cout
+
+
+class HipPathNet:
+    """Kernel-side view of an ``ACPathNet`` (created by it when backend='hip')."""
+
+    def __init__(self, model):
+        if not torch.cuda.is_available():
+            raise RuntimeError("HIP backend requested but no GPU is visible")
+        _lib.lib()   # fail loudly if the library is missing
+        self.model = model
+        cfg = model.cfg
+        self.cfg = cfg
+        self.L, self.M = cfg.L, cfg.M
+        if cfg.use_lstm:
+            raise NotImplementedError("HIP backend: LSTM trunk runs on the torch backend (use --backend torch)")
+        lay = model.store.layout
+        dev = model.device
+        self.geoms: List[LayerGeom] = []
+        for l, (spec, li) in enumerate(zip(cfg.layers, lay.layer_info)):
+            ins, outs = li["in_shape"], li["out_shape"]
+            K, cout = li["K"], li["cout"]
+            if spec.kind == "conv":
+                Hin, Win, Cin = ins
+                Ho, Wo, _ = outs
+                if Cin not in (4, 8) and not (l == 0):
+                    raise NotImplementedError("conv layers need Cin in {4, 8}")
+                if cout != 8:
+                    raise NotImplementedError("HIP conv modules have 8 output maps (reference feature_num)")
+                g = LayerGeom("conv", K, round_up(K, 32), cout, Ho * Wo, Ho * Wo * cout, li["offset"], li["chunk"],
+                              Hin, Win, Cin, spec.kernel, spec.kernel, spec.stride, Ho, Wo,
+                              u8in=(l == 0), in_scale=(1.0 / 255.0 if l == 0 else 1.0))
+                if l == 0 and (Cin * 2) % 8 != 0:
+                    raise NotImplementedError("first conv layer needs Cin*KW multiple of 8 bytes")
+            else:
+                if spec.module_types is not None and any(t != 1 for t in spec.module_types):
+                    raise NotImplementedError("HIP fc layers implement fc+ReLU modules")
+                if cout % 32 != 0:
+                    raise NotImplementedError("HIP fc modules need width % 32 == 0")
+                ldx = round_up(K, 8) if l > 0 else 8
+                if l == 0 and K > 8:
+                    raise NotImplementedError("vector observations up to 8 dims")
+                g = LayerGeom("fc", K, round_up(K, 32), cout, 1, cout, li["offset"], li["chunk"], ldx=ldx)
+                if l > 0 and self.geoms[-1].out_feat != K:
+                    raise ValueError("fc input size mismatch")
+                if l > 0 and K % 8 != 0:
+                    raise NotImplementedError("HIP fc layers need input width % 8 == 0")
+            self.geoms.append(g)
+        self.pixels = cfg.layers[0].kind == "conv"
+        self.out_scale_last = (1.0 / cfg.M) if cfg.trunk_scale == "M" else 1.0
+        # bf16 operand copies
+        self.Wc = []
+        self.WcT = []
+        for l, g in enumerate(self.geoms):
+            self.Wc.append(torch.zeros(self.M, g.Cout, g.KP, dtype=torch.bfloat16, device=dev))
+            need_t = g.kind == "fc" and l > 0
+            self.WcT.append(torch.zeros(self.M, g.KP, g.Cout, dtype=torch.bfloat16, device=dev) if need_t else None)
+        P = model.P
+        self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
+        self.inv_slot = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
+        self.inv_cnt = torch.zeros(self.L, self.M, dtype=torch.int32, device=dev)
+        lay_h = lay.heads
+        self.heads_off = lay_h
+        self.refresh_weights()
+
+    # ------------------------------------------------------------------
+    def set_paths(self, expressed: np.ndarray):
+        """Inverse module lists for the module-major fc wgrad (in place)."""
+        P, L, M = expressed.shape
+        ip = np.zeros((L, M, P), np.int32)
+        isl = np.zeros((L, M, P), np.int32)
+        ic = np.zeros((L, M), np.int32)
+        for p in range(P):
+            for l in range(L):
+                act = np.nonzero(expressed[p, l] > 0.5)[0]
+                for a, j in enumerate(act):
+                    ip[l, j, ic[l, j]] = p
+                    isl[l, j, ic[l, j]] = a
+                    ic[l, j] += 1
+        self.inv_path.copy_(torch.from_numpy(ip))
+        self.inv_slot.copy_(torch.from_numpy(isl))
+        self.inv_cnt.copy_(torch.from_numpy(ic))
+
+    def set_frozen(self, frozen):
+        pass   # frozen segments are skipped by the optimizer; kernels compute their grads (cheap)
+
+    def refresh_weights(self):
+        flat = self.model.store.flat
+        for l, g in enumerate(self.geoms):
+            _lib.call("launch_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
+                      self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), _lib.stream())
+
+    # ------------------------------------------------------------------
+    def layer_fwd(self, l: int, X: torch.Tensor, Y: torch.Tensor, bits: torch.Tensor, P: int, E: int, T: int,
+                  t0: int, bits_rows: int):
+        g = self.geoms[l]
+        m = self.model
+        flat = m.store.flat
+        out_scale = self.out_scale_last if l == self.L - 1 else 1.0
+        st = _lib.stream()
+        if g.kind == "conv":
+            if (E * g.HWo) % 16 != 0:
+                raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
+            _lib.call("launch_conv_fwd", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
+                      self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
+                      m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo,
+                      g.K, g.KP, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
+        else:
+            _lib.call("launch_fc_fwd", X.data_ptr(), g.ldx, Y.data_ptr(), bits.data_ptr(), self.Wc[l].data_ptr(),
+                      flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L,
+                      self.M, g.K, g.KP, g.Cout, P, E, T, t0, bits_rows, out_scale, st)
+
+    def layer_bwd(self, l: int, X: torch.Tensor, G: torch.Tensor, bits: torch.Tensor, grad_flat: torch.Tensor,
+                  dX: Optional[torch.Tensor], P: int, E: int, T: int, bits_rows: int, rows_per_chunk: int = 0):
+        g = self.geoms[l]
+        m = self.model
+        flat = m.store.flat
+        g_scale = self.out_scale_last if l == self.L - 1 else 1.0
+        st = _lib.stream()
+        if g.kind == "conv":
+            if rows_per_chunk <= 0:
+                rows = T * E * g.HWo
+                # ~8 chunks per path keeps >= 8*P workgroups while bounding atomics
+                rows_per_chunk = max(32, round_up((rows + 7) // 8, 32))
+            _lib.call("launch_conv_wgrad", X.data_ptr(), int(g.u8in), G.data_ptr(), bits.data_ptr(),
+                      grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l,
+                      self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo, g.K, g.KP, P, E, T,
+                      bits_rows, rows_per_chunk, g.in_scale, g_scale, st)
+            if dX is not None:
+                _lib.call("launch_conv_dgrad", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
+                          m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH,
+                          g.KW, g.S, g.Ho, g.Wo, P, E, T, bits_rows, g_scale, dX.data_ptr(), st)
+        else:
+            _lib.call("launch_fc_wgrad", X.data_ptr(), g.ldx, G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(),
+                      g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(), self.inv_slot.data_ptr(),
+                      self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T, bits_rows, g_scale, st)
+            if dX is not None:
+                _lib.call("launch_fc_dgrad", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
+                          m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.K, g.KP, g.Cout, P, E,
+                          T, bits_rows, g_scale, dX.data_ptr(), st)
+
+    # ------------------------------------------------------------------
+    def alloc_bits(self, l: int, steps: int, B: int):
+        g = self.geoms[l]
+        dev = self.model.device
+        if g.kind == "conv":
+            rows = steps * B * g.HWo
+            return torch.zeros(self.M, rows, dtype=torch.uint8, device=dev), rows
+        rows = steps * B
+        return torch.zeros(self.M, rows, g.Cout // 16, dtype=torch.int16, device=dev), rows
+
+    def heads_fwd(self, feat, logits, value, actions, seed, ctr, t, T, greedy=False, task=0):
+        m = self.model
+        h = m.store.layout.heads[task if m.cfg.per_task_heads else 0]
+        B = feat.shape[0]
+        F = feat.shape[1]
+        A = m.cfg.num_actions
+        _lib.call("launch_heads_fwd_sample", feat.data_ptr(), F, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"],
+                  h["vb"], A, B, logits.data_ptr(), value.data_ptr(), actions.data_ptr(), seed & 0xFFFFFFFF,
+                  ctr.data_ptr(), t, T, int(greedy), _lib.stream())
+
+    def heads_bwd(self, feat, dlogits, dvalue, grad_flat, dfeat, task=0):
+        m = self.model
+        h = m.store.layout.heads[task if m.cfg.per_task_heads else 0]
+        N, F = feat.shape
+        _lib.call("launch_heads_bwd", feat.data_ptr(), F, dlogits.data_ptr(), dvalue.data_ptr(), N,
+                  m.cfg.num_actions, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"],
+                  grad_flat.data_ptr(), dfeat.data_ptr(), _lib.stream())
+
+    # -- standalone forward (tests / acting): obs [B, ...] -> feat [B, F] --------
+    def trunk(self, obs: torch.Tensor, samples_per_path: int):
+        m = self.model
+        P, E = m.P, samples_per_path
+        B = P * E
+        x = self._prep_input(obs)
+        out = None
+        for l, g in enumerate(self.geoms):
+            Y = torch.empty(B, g.out_feat, dtype=torch.bfloat16, device=m.device)
+            bits, rows = self.alloc_bits(l, 1, B)
+            self.layer_fwd(l, x, Y, bits, P, E, 1, 0, rows)
+            x = Y
+            out = Y
+        return out.float()
+
+    def _prep_input(self, obs):
+        if self.pixels:
+            return _lib.check(obs.contiguous(), torch.uint8, name="obs")
+        if obs.dtype == torch.bfloat16 and obs.shape[-1] == 8:
+            return obs.contiguous()
+        from .envs import obs_to_bf16_padded
+        return obs_to_bf16_padded(obs.float())
+
+    def heads(self, feat, task=0):
+        from ..models.pathnet import heads_ref
+        return heads_ref(self.model.store, feat, task)

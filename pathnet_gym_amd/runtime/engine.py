@@ -1,0 +1,210 @@
+"""HIP rollout/update engine: static buffers + hipGraph-captured update.
+
+One A2C update of the local population (P paths x E envs, T steps) is a
+fixed sequence of kernel launches on one stream:
+
+  for t in 0..T-1:                                   (rollout)
+      trunk fwd layer 0..L-1   (obs[t] -> acts[l][t], ReLU bits)
+      heads fwd + Gumbel-max sample  (logits[t], values[t], actions[t])
+      env step                 (obs[t] -> obs[t+1], rewards/dones/epret[t])
+  trunk+heads fwd on obs[T] (greedy) -> bootstrap value
+  fitness update (per-path last-episode return) + counters
+  a2c_grad                     (reverse scan + analytic loss gradient)
+  memset grad; heads bwd; for l = L-1..0: wgrad_l (+ dgrad_l)
+  -------------------------------- fused RCCL all-reduce (outside the graph)
+  clip + RMSProp + refresh bf16 weight copies; obs[0] <- obs[T]; ctr += 1
+
+All shapes and addresses are static (genotype changes only rewrite the
+compacted index tensors in place), so the two halves are captured once as
+hipGraphs (``torch.cuda.graph`` over our ctypes launches) and replayed:
+~(T*(L+2)+2L+6) launches become two graph launches per update.  This is
+the MI355X replacement for the reference's per-step ``sess.run`` over gRPC
+(SURVEY.md call sites C1-C3).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..ops import _lib
+from ..ops import envs as henv
+
+
+class HipEngine:
+    def __init__(self, model, env, cfg, opt, seed: int = 1):
+        self.model = model
+        self.hip = model.hip
+        self.env = env
+        self.cfg = cfg
+        self.opt = opt
+        self.seed = seed & 0xFFFFFFFF
+        a2c = cfg.a2c
+        self.T = T = a2c.t_max
+        self.P = P = model.P
+        self.E = E = cfg.envs_per_path
+        self.B = B = P * E
+        self.A = A = model.cfg.num_actions
+        dev = model.device
+        self.device = dev
+        hp = self.hip
+        self.pixels = hp.pixels
+        if self.pixels:
+            H, W, C = model.cfg.input_shape
+            self.obs = torch.zeros(T + 1, B, H * W * C, dtype=torch.uint8, device=dev)
+        else:
+            self.obs = torch.zeros(T + 1, B, 8, dtype=torch.bfloat16, device=dev)
+        self.acts, self.bits, self.bits_rows, self.grads = [], [], [], []
+        for l, g in enumerate(hp.geoms):
+            self.acts.append(torch.zeros(T + 1, B, g.out_feat, dtype=torch.bfloat16, device=dev))
+            b, rows = hp.alloc_bits(l, T + 1, B)
+            self.bits.append(b)
+            self.bits_rows.append(rows)
+            self.grads.append(torch.zeros(T * B, g.out_feat, dtype=torch.float32, device=dev))
+        self.logits = torch.zeros(T + 1, B, A, device=dev)
+        self.values = torch.zeros(T + 1, B, device=dev)
+        self.actions = torch.zeros(T + 1, B, dtype=torch.int32, device=dev)
+        self.rewards = torch.zeros(T, B, device=dev)
+        self.dones = torch.zeros(T, B, dtype=torch.uint8, device=dev)
+        self.epret = torch.zeros(T, B, device=dev)
+        self.dlogits = torch.zeros(T, B, A, device=dev)
+        self.dvalue = torch.zeros(T, B, device=dev)
+        self.stats = torch.zeros(4, device=dev)
+        self.grad_flat = torch.zeros_like(model.store.flat, requires_grad=False)
+        self.fitness = torch.full((P,), -1000.0, device=dev)
+        self.counters = torch.zeros(4, device=dev)
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.lr = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.weight = (1.0 / E) if a2c.env_reduction == "mean_env" else 1.0
+        # optimizer block table (segments split into <= 8192-element blocks)
+        self._build_opt_tables()
+        self.g_rollout = None
+        self.g_opt = None
+        self.use_graph = bool(cfg.use_graph)
+        self.load_obs(env)
+
+    # ------------------------------------------------------------------
+    def load_obs(self, env):
+        """Copy the env's current observation into slot 0."""
+        o = env.obs if self.pixels else None
+        if self.pixels:
+            self.obs[0].copy_(o.reshape(self.B, -1))
+        else:
+            self.obs[0].copy_(henv.obs_to_bf16_padded(env.state.float()))
+
+    def _build_opt_tables(self):
+        segs = self.model.store.layout.segments
+        seg_id, beg, end = [], [], []
+        BLK = 8192
+        for i, s in enumerate(segs):
+            o = s.offset
+            while o < s.offset + s.numel:
+                e = min(o + BLK, s.offset + s.numel)
+                seg_id.append(i)
+                beg.append(o)
+                end.append(e)
+                o = e
+        dev = self.device
+        self.blk_seg = torch.tensor(seg_id, dtype=torch.int32, device=dev)
+        self.blk_beg = torch.tensor(beg, dtype=torch.int64, device=dev)
+        self.blk_end = torch.tensor(end, dtype=torch.int64, device=dev)
+        self.nblk = len(seg_id)
+        self.sq = torch.zeros(len(segs), dtype=torch.float32, device=dev)
+        self.trainable_u8 = self.opt.seg_trainable.to(torch.uint8)
+
+    def refresh_trainable(self):
+        self.trainable_u8.copy_(self.opt.seg_trainable.to(torch.uint8))
+
+    # ------------------------------------------------------------------
+    def _env_step(self, t):
+        env = self.env
+        if self.pixels:
+            henv.pong_step_into(env, self.actions[t], self.obs[t], self.obs[t + 1], self.rewards[t], self.dones[t],
+                                self.epret[t])
+        else:
+            henv.cartpole_step_into(env, self.actions[t], self.obs[t + 1], self.rewards[t], self.dones[t],
+                                    self.epret[t])
+
+    def _forward_step(self, t, greedy=False):
+        hp = self.hip
+        P, E = self.P, self.E
+        x = self.obs
+        for l in range(len(hp.geoms)):
+            hp.layer_fwd(l, x, self.acts[l], self.bits[l], P, E, 1, t, self.bits_rows[l])
+            x = self.acts[l]
+        hp.heads_fwd(self.acts[-1][t], self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t,
+                     self.T + 1, greedy=greedy, task=self.model.task)
+
+    def _rollout_backward_body(self):
+        T, P, E, B = self.T, self.P, self.E, self.B
+        a2c = self.cfg.a2c
+        hp = self.hip
+        for t in range(T):
+            self._forward_step(t)
+            self._env_step(t)
+        self._forward_step(T, greedy=True)
+        _lib.call("launch_fitness_update", self.dones.data_ptr(), self.epret.data_ptr(), T, P, E,
+                  self.fitness.data_ptr(), self.counters.data_ptr(), _lib.stream())
+        self.stats.zero_()
+        _lib.call("launch_a2c_grad", self.logits.data_ptr(), self.values.data_ptr(), self.actions.data_ptr(),
+                  self.rewards.data_ptr(), self.dones.data_ptr(), self.values[T].data_ptr(), T, B, self.A,
+                  a2c.gamma, a2c.gae_lambda, a2c.reward_clip, a2c.entropy_beta, a2c.value_coef, self.weight,
+                  self.dlogits.data_ptr(), self.dvalue.data_ptr(), self.stats.data_ptr(), _lib.stream())
+        self.grad_flat.zero_()
+        L = len(hp.geoms)
+        feat = self.acts[L - 1][:T].reshape(T * B, -1)
+        hp.heads_bwd(feat, self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1), self.grad_flat,
+                     self.grads[L - 1], task=self.model.task)
+        for l in range(L - 1, -1, -1):
+            X = self.obs if l == 0 else self.acts[l - 1]
+            dX = self.grads[l - 1] if l > 0 else None
+            hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
+
+    def _optimizer_body(self):
+        o = self.opt
+        _lib.call("launch_rmsprop", self.model.store.flat.data_ptr(), self.grad_flat.data_ptr(), o.ms.data_ptr(),
+                  o.mom.data_ptr(), self.blk_seg.data_ptr(), self.blk_beg.data_ptr(), self.blk_end.data_ptr(),
+                  self.nblk, self.sq.data_ptr(), self.sq.numel(), self.trainable_u8.data_ptr(), self.lr.data_ptr(),
+                  o.decay, o.momentum, o.epsilon, o.clip_norm, _lib.stream())
+        self.hip.refresh_weights()
+        self.obs[0].copy_(self.obs[self.T])
+        self.ctr.add_(1)
+
+    # ------------------------------------------------------------------
+    def _capture(self):
+        # warm up once on a side stream (torch requirement), then capture
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        self.g_rollout = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_rollout):
+            self._rollout_backward_body()
+        self.g_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_opt):
+            self._optimizer_body()
+        torch.cuda.synchronize()
+
+    def rollout_backward(self):
+        if self.use_graph:
+            if self.g_rollout is None:
+                # first update eagerly (validates every launch), capture for the next ones
+                self._rollout_backward_body()
+                self._pending_capture = True
+                return
+            self.g_rollout.replay()
+        else:
+            self._rollout_backward_body()
+
+    def optimizer_step(self, lr: float):
+        self.lr.fill_(lr)
+        if self.use_graph and self.g_opt is not None:
+            self.g_opt.replay()
+        else:
+            self._optimizer_body()
+            if self.use_graph and getattr(self, "_pending_capture", False):
+                self._pending_capture = False
+                self._capture()
+
+    def stats_host(self):
+        return self.stats.cpu().numpy()

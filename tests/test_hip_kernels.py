@@ -1,0 +1,307 @@
+"""HIP kernel numerics vs the fp32 PyTorch oracle (run on an MI355X).
+
+Every test compares a hand-written gfx950 kernel against a plain PyTorch
+fp32 implementation of the same op (``models/pathnet.py``,
+``algo/a2c_math.py``, ``algo/optim.py``, ``envs/*.py``).  bf16 MFMA operands
+give ~1e-2 relative error; envs are integer/bit exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from pathnet_gym_amd.algo.a2c_math import a2c_loss, nstep_returns
+from pathnet_gym_amd.algo.ga import Population, get_geopath
+from pathnet_gym_amd.config import LayerSpec, PathNetConfig, preset
+from pathnet_gym_amd.models.acnet import ACPathNet
+from pathnet_gym_amd.models.pathnet import heads_ref, trunk_forward_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.float().flatten()
+    b = b.float().flatten()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def random_masks(P, L, M, N, seed=0, with_edge=True):
+    rng = np.random.RandomState(seed)
+    m = np.stack([get_geopath(L, M, N, rng) for _ in range(P)])
+    if with_edge and P >= 3:
+        m[0, 1, :] = 0          # empty layer -> zero output
+        m[1, :, :] = 1          # all modules active
+        m[2, 0, :] = 0
+        m[2, 0, M - 1] = 1      # single (odd) module
+    return m
+
+
+def small_pixel_cfg(M=10, N=4):
+    return PathNetConfig(L=5, M=M, N=N, input_shape=(160, 120, 4),
+                         layers=[LayerSpec("conv", 8, 8, 4), LayerSpec("conv", 8, 4, 2), LayerSpec("conv", 8, 3, 1),
+                                 LayerSpec("fc", 256), LayerSpec("fc", 256)],
+                         trunk_scale="M", num_actions=6)
+
+
+def make_model(cfg, P, masks, seed=3):
+    m = ACPathNet(cfg, P, DEV, "hip", seed=seed)
+    m.set_paths(masks)
+    return m
+
+
+# ---------------------------------------------------------------------------
+def test_trunk_forward_matches_oracle(hip_lib):
+    cfg = small_pixel_cfg()
+    P, E = 4, 16
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N)
+    m = make_model(cfg, P, masks)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    obs = torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+    feat = m.hip.trunk(obs, E)
+    with torch.no_grad():
+        ref = trunk_forward_ref(m.store, obs.float() / 255.0, m.mask.repeat_interleave(E, 0))
+    assert feat.shape == ref.shape
+    # path 0 has an empty layer 1 -> every later layer sees zeros
+    for p in range(P):
+        sl = slice(p * E, (p + 1) * E)
+        assert rel(feat[sl], ref[sl]) < 3e-2, (p, rel(feat[sl], ref[sl]))
+
+
+def test_fc_trunk_forward_vector_input(hip_lib):
+    cfg = preset("cartpole").net
+    P, E = 6, 16
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, with_edge=False)
+    m = make_model(cfg, P, masks)
+    x = torch.randn(P * E, 4, device=DEV)
+    feat = m.hip.trunk(x, E)
+    with torch.no_grad():
+        ref = trunk_forward_ref(m.store, x.to(torch.bfloat16).float(), m.mask.repeat_interleave(E, 0))
+    assert rel(feat, ref) < 3e-2
+
+
+def _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E):
+    """Run T forward steps into engine-style buffers, then the trunk backward."""
+    hp = m.hip
+    T = len(obs_steps)
+    B = P * E
+    obs = torch.stack(obs_steps).reshape(T, B, -1).contiguous()
+    acts, bits, rows, grads = [], [], [], []
+    for l, g in enumerate(hp.geoms):
+        acts.append(torch.zeros(T, B, g.out_feat, dtype=torch.bfloat16, device=DEV))
+        b, r = hp.alloc_bits(l, T, B)
+        bits.append(b)
+        rows.append(r)
+        grads.append(torch.zeros(T * B, g.out_feat, dtype=torch.float32, device=DEV))
+    for t in range(T):
+        x = obs
+        for l in range(len(hp.geoms)):
+            hp.layer_fwd(l, x, acts[l], bits[l], P, E, 1, t, rows[l])
+            x = acts[l]
+    grad_flat = torch.zeros_like(m.store.flat, requires_grad=False)
+    grads[-1].copy_(dfeat)
+    L = len(hp.geoms)
+    for l in range(L - 1, -1, -1):
+        X = obs if l == 0 else acts[l - 1]
+        dX = grads[l - 1] if l > 0 else None
+        hp.layer_bwd(l, X, grads[l], bits[l], grad_flat, dX, P, E, T, rows[l])
+    torch.cuda.synchronize()
+    return acts[-1].reshape(T * B, -1).float(), grad_flat
+
+
+def test_trunk_backward_matches_autograd(hip_lib):
+    cfg = small_pixel_cfg()
+    P, E, T = 4, 16, 2
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, seed=5)
+    m = make_model(cfg, P, masks, seed=7)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    obs_steps = [torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+                 for _ in range(T)]
+    dfeat = torch.randn(T * P * E, 256, generator=g).to(DEV)
+    feat_hip, grad_hip = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+    # oracle: rows ordered [t][p][e]
+    flat = m.store.flat.detach().clone().requires_grad_(True)
+    from pathnet_gym_amd.models.pathnet import ParamStore
+    st = ParamStore(cfg, DEV, flat=flat)
+    x = torch.cat(obs_steps).float() / 255.0
+    mask = m.mask.repeat_interleave(E, 0).repeat(T, 1, 1)
+    feat_ref = trunk_forward_ref(st, x, mask)
+    (feat_ref * dfeat).sum().backward()
+    gref = flat.grad
+    assert rel(feat_hip, feat_ref.detach()) < 3e-2
+    lay = m.store.layout
+    checked = 0
+    for s in lay.segments:
+        if s.layer < 0:
+            continue
+        a = grad_hip[s.offset:s.offset + s.numel]
+        b = gref[s.offset:s.offset + s.numel]
+        if b.norm() < 1e-6:
+            assert a.norm() < 1e-4, s.name
+            continue
+        assert rel(a, b) < 5e-2, (s.name, rel(a, b))
+        checked += 1
+    assert checked > 20
+
+
+def test_fc_backward_vector(hip_lib):
+    cfg = preset("cartpole").net
+    P, E, T = 4, 16, 3
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, seed=2, with_edge=False)
+    m = make_model(cfg, P, masks)
+    from pathnet_gym_amd.ops.envs import obs_to_bf16_padded
+    xs = [torch.randn(P * E, 4, device=DEV) for _ in range(T)]
+    obs_steps = [obs_to_bf16_padded(x) for x in xs]
+    dfeat = torch.randn(T * P * E, 32, device=DEV)
+    feat_hip, grad_hip = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+    flat = m.store.flat.detach().clone().requires_grad_(True)
+    from pathnet_gym_amd.models.pathnet import ParamStore
+    st = ParamStore(cfg, DEV, flat=flat)
+    x = torch.cat(xs).to(torch.bfloat16).float()
+    feat_ref = trunk_forward_ref(st, x, m.mask.repeat_interleave(E, 0).repeat(T, 1, 1))
+    (feat_ref * dfeat).sum().backward()
+    for s in m.store.layout.segments:
+        if s.layer < 0:
+            continue
+        a, b = grad_hip[s.offset:s.offset + s.numel], flat.grad[s.offset:s.offset + s.numel]
+        if b.norm() < 1e-6:
+            continue
+        assert rel(a, b) < 5e-2, (s.name, rel(a, b))
+
+
+def test_heads_and_a2c_grad(hip_lib):
+    from pathnet_gym_amd.ops import _lib
+    cfg = small_pixel_cfg()
+    P, E, T = 2, 16, 5
+    B = P * E
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, with_edge=False)
+    m = make_model(cfg, P, masks)
+    hp = m.hip
+    A = cfg.num_actions
+    feat = (torch.randn(T + 1, B, 256, device=DEV) * 0.5).to(torch.bfloat16)
+    logits = torch.zeros(T + 1, B, A, device=DEV)
+    values = torch.zeros(T + 1, B, device=DEV)
+    actions = torch.zeros(T + 1, B, dtype=torch.int32, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    for t in range(T + 1):
+        hp.heads_fwd(feat[t], logits[t], values[t], actions[t], 123, ctr, t, T + 1, greedy=(t == T))
+    lr_, vr_ = heads_ref(m.store, feat.float().reshape(-1, 256))
+    assert rel(logits.reshape(-1, A), lr_.detach()) < 1e-4
+    assert rel(values.reshape(-1), vr_.detach()) < 1e-4
+    assert int(actions.min()) >= 0 and int(actions.max()) < A
+    # sampling frequency sanity: greedy step picks the argmax
+    assert torch.equal(actions[T].long(), logits[T].argmax(-1))
+    rewards = torch.randint(-1, 2, (T, B), device=DEV).float() * 2
+    dones = (torch.rand(T, B, device=DEV) < 0.2).to(torch.uint8)
+    dlog = torch.zeros(T, B, A, device=DEV)
+    dval = torch.zeros(T, B, device=DEV)
+    stats = torch.zeros(4, device=DEV)
+    beta, w = 0.01, 1.0 / E
+    _lib.call("launch_a2c_grad", logits.data_ptr(), values.data_ptr(), actions.data_ptr(), rewards.data_ptr(),
+              dones.data_ptr(), values[T].data_ptr(), T, B, A, 0.99, 1.0, 1.0, beta, 0.5, w, dlog.data_ptr(),
+              dval.data_ptr(), stats.data_ptr(), _lib.stream())
+    R, adv = nstep_returns(rewards, values[:T], dones.bool(), values[T], 0.99, 1.0, 1.0)
+    lg = logits[:T].reshape(-1, A).clone().requires_grad_(True)
+    vv = values[:T].reshape(-1).clone().requires_grad_(True)
+    loss, lp, lv, ent = a2c_loss(lg, vv, actions[:T].reshape(-1), R.reshape(-1), adv.reshape(-1), beta, 0.5,
+                                 torch.full((T * B,), w, device=DEV))
+    loss.backward()
+    assert rel(dlog.reshape(-1, A), lg.grad) < 1e-4
+    assert rel(dval.reshape(-1), vv.grad) < 1e-4
+    assert abs(float(stats[0]) - float(lp)) < 1e-3 * max(1.0, abs(float(lp)))
+    # heads backward
+    gflat = torch.zeros_like(m.store.flat, requires_grad=False)
+    dfeat = torch.zeros(T * B, 256, device=DEV)
+    hp.heads_bwd(feat[:T].reshape(T * B, 256), dlog.reshape(T * B, A), dval.reshape(-1), gflat, dfeat)
+    flat = m.store.flat.detach().clone().requires_grad_(True)
+    from pathnet_gym_amd.models.pathnet import ParamStore
+    st = ParamStore(cfg, DEV, flat=flat)
+    fx = feat[:T].reshape(T * B, 256).float().requires_grad_(True)
+    l2, v2 = heads_ref(st, fx)
+    ((l2 * dlog.reshape(T * B, A)).sum() + (v2 * dval.reshape(-1)).sum()).backward()
+    assert rel(dfeat, fx.grad) < 1e-4
+    for name in ("policy.weight", "policy.bias", "value.weight", "value.bias"):
+        s = m.store.layout.by_name[name]
+        assert rel(gflat[s.offset:s.offset + s.numel], flat.grad[s.offset:s.offset + s.numel]) < 1e-4, name
+
+
+def test_rmsprop_kernel_matches_torch(hip_lib):
+    from pathnet_gym_amd.algo.optim import RMSPropTF
+    from pathnet_gym_amd.runtime.engine import HipEngine
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 2, 16, 2
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng = tr.engine
+    frozen = np.zeros((cfg.net.L, cfg.net.M), np.float32)
+    frozen[0, 3] = 1
+    tr.opt.set_frozen(frozen)
+    eng.refresh_trainable()
+    flat0 = tr.model.store.flat.detach().clone()
+    g = torch.randn_like(flat0) * 3.0
+    ref = RMSPropTF(tr.model.store.layout, flat0.clone(), clip_norm=40.0)
+    ref.set_frozen(frozen)
+    ref.ms.copy_(tr.opt.ms)
+    ref.step(g, 7e-4)
+    eng.grad_flat.copy_(g)
+    eng.lr.fill_(7e-4)
+    eng._optimizer_body()
+    torch.cuda.synchronize()
+    assert rel(tr.model.store.flat.detach() - flat0, ref.flat - flat0) < 1e-4
+    s = tr.model.store.layout.by_name["layer0.module3.weight"]
+    assert torch.equal(tr.model.store.flat[s.offset:s.offset + s.numel], flat0[s.offset:s.offset + s.numel])
+
+
+def test_pong_env_hip_bit_exact_vs_torch(hip_lib):
+    from pathnet_gym_amd.envs.pong import PongVec
+    N = 24
+    et = PongVec(N, device=DEV, seed=11, backend="torch")
+    eh = PongVec(N, device=DEV, seed=11, backend="hip")
+    ot = et.reset()
+    oh = eh.reset()
+    assert torch.equal(ot, oh)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    ndone = 0
+    for i in range(700):
+        a = torch.randint(0, 6, (N,), generator=g).to(DEV)
+        ot, rt, dt, it = et.step(a)
+        oh, rh, dh, ih = eh.step(a)
+        assert torch.equal(rt, rh), i
+        assert torch.equal(dt, dh), i
+        assert torch.equal(ot, oh), i
+        assert torch.equal(it["episode_return"], ih["episode_return"]), i
+        ndone += int(dt.sum())
+    assert ndone > 0     # at least one auto-reset exercised
+
+
+def test_cartpole_env_hip_vs_torch(hip_lib):
+    from pathnet_gym_amd.envs.cartpole import CartPoleVec
+    N = 64
+    et = CartPoleVec(N, device=DEV, seed=3, backend="torch")
+    eh = CartPoleVec(N, device=DEV, seed=3, backend="hip")
+    ot, oh = et.reset(), eh.reset()
+    assert torch.allclose(ot, oh)
+    for i in range(8):
+        a = (torch.arange(N, device=DEV) + i) % 2
+        ot, rt, dt, _ = et.step(a)
+        oh, rh, dh, _ = eh.step(a)
+        assert torch.equal(dt, dh)
+        assert torch.allclose(ot, oh, atol=1e-5)
+
+
+@pytest.mark.parametrize("preset_name", ["pong", "cartpole"])
+def test_engine_update_and_graph_replay(hip_lib, preset_name):
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset(preset_name)
+    cfg.paths = 4
+    cfg.envs_per_path = 16
+    cfg.a2c.t_max = 5
+    cfg.use_graph = True
+    tr = PathNetTrainer(cfg, device=DEV)
+    w0 = tr.model.store.flat.detach().clone()
+    for _ in range(4):          # eager, then capture, then replays
+        st = tr.update()
+        assert np.isfinite(st.loss_pi) and np.isfinite(st.loss_v)
+    assert tr.engine.g_rollout is not None
+    assert torch.isfinite(tr.model.store.flat).all()
+    assert not torch.equal(w0, tr.model.store.flat.detach())
+    assert tr.global_step == 4 * 4 * 16 * 5
