@@ -186,13 +186,21 @@ def module_type(spec, j: int) -> int:
     return int(spec.module_types[j % len(spec.module_types)])
 
 
+def bf16_ste(x: torch.Tensor) -> torch.Tensor:
+    """Round to bf16 in the forward pass, identity gradient (emulates bf16 storage)."""
+    return x + (x.to(torch.bfloat16).float() - x).detach()
+
+
 def trunk_forward_ref(store: ParamStore, x: torch.Tensor, mask: torch.Tensor,
                       W_override: Optional[List[torch.Tensor]] = None,
-                      b_override: Optional[List[torch.Tensor]] = None) -> torch.Tensor:
+                      b_override: Optional[List[torch.Tensor]] = None,
+                      emulate_bf16: bool = False) -> torch.Tensor:
     """Dense masked PathNet trunk.
 
     x    : [B, *input_shape] float (NHWC for pixels, already scaled to [0,1])
     mask : [B, L, M] float (expressed genotype of each sample's path)
+    emulate_bf16: round weights and every layer output to bf16 (the HIP
+                  kernels' storage precision; fp32 accumulation either way)
     returns [B, feature_dim]
     """
     cfg = store.cfg
@@ -203,6 +211,8 @@ def trunk_forward_ref(store: ParamStore, x: torch.Tensor, mask: torch.Tensor,
         li = store.layout.layer_info[l]
         W = store.W(l) if W_override is None else W_override[l]
         b = store.b(l) if b_override is None else b_override[l]
+        if emulate_bf16:
+            W = bf16_ste(W)
         m = mask[:, l, :]
         cout = li["cout"]
         if spec.kind == "conv":
@@ -227,9 +237,13 @@ def trunk_forward_ref(store: ParamStore, x: torch.Tensor, mask: torch.Tensor,
                     o = F.relu(pre[:, j]) + hf
                 outs.append(o * m[:, j:j + 1])
             h = torch.stack(outs, 1).sum(1)
+        if emulate_bf16 and l < cfg.L - 1:
+            h = bf16_ste(h)
     h = h.reshape(B, -1)
     if cfg.trunk_scale == "M":
         h = h / M
+    if emulate_bf16:
+        h = bf16_ste(h)
     return h
 
 

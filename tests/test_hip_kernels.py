@@ -124,12 +124,12 @@ def test_trunk_backward_matches_autograd(hip_lib):
     st = ParamStore(cfg, DEV, flat=flat)
     x = torch.cat(obs_steps).float() / 255.0
     mask = m.mask.repeat_interleave(E, 0).repeat(T, 1, 1)
-    feat_ref = trunk_forward_ref(st, x, mask)
+    feat_ref = trunk_forward_ref(st, x, mask, emulate_bf16=True)
     (feat_ref * dfeat).sum().backward()
     gref = flat.grad
-    assert rel(feat_hip, feat_ref.detach()) < 3e-2
+    assert rel(feat_hip, feat_ref.detach()) < 1e-2
     lay = m.store.layout
-    checked = 0
+    errs = {}
     for s in lay.segments:
         if s.layer < 0:
             continue
@@ -138,9 +138,11 @@ def test_trunk_backward_matches_autograd(hip_lib):
         if b.norm() < 1e-6:
             assert a.norm() < 1e-4, s.name
             continue
-        assert rel(a, b) < 5e-2, (s.name, rel(a, b))
-        checked += 1
-    assert checked > 20
+        errs[s.name] = rel(a, b)
+    print({k: round(v, 4) for k, v in errs.items()})
+    assert len(errs) > 20
+    worst = max(errs, key=errs.get)
+    assert errs[worst] < 3e-2, (worst, errs[worst])
 
 
 def test_fc_backward_vector(hip_lib):
@@ -157,7 +159,7 @@ def test_fc_backward_vector(hip_lib):
     from pathnet_gym_amd.models.pathnet import ParamStore
     st = ParamStore(cfg, DEV, flat=flat)
     x = torch.cat(xs).to(torch.bfloat16).float()
-    feat_ref = trunk_forward_ref(st, x, m.mask.repeat_interleave(E, 0).repeat(T, 1, 1))
+    feat_ref = trunk_forward_ref(st, x, m.mask.repeat_interleave(E, 0).repeat(T, 1, 1), emulate_bf16=True)
     (feat_ref * dfeat).sum().backward()
     for s in m.store.layout.segments:
         if s.layer < 0:
@@ -165,7 +167,7 @@ def test_fc_backward_vector(hip_lib):
         a, b = grad_hip[s.offset:s.offset + s.numel], flat.grad[s.offset:s.offset + s.numel]
         if b.norm() < 1e-6:
             continue
-        assert rel(a, b) < 5e-2, (s.name, rel(a, b))
+        assert rel(a, b) < 3e-2, (s.name, rel(a, b))
 
 
 def test_heads_and_a2c_grad(hip_lib):
@@ -228,7 +230,7 @@ def test_rmsprop_kernel_matches_torch(hip_lib):
     from pathnet_gym_amd.algo.optim import RMSPropTF
     from pathnet_gym_amd.runtime.engine import HipEngine
     cfg = preset("pong")
-    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 2, 16, 2
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 2
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     tr = PathNetTrainer(cfg, device=DEV)
     eng = tr.engine
