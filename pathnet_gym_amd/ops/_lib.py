@@ -47,6 +47,12 @@ _SIGS = {
     "launch_pong_step": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, P],
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_int, P, P, P, P, P, P],
+    "fast_conv_fwd": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                      c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P],
+    "fast_conv_wgrad": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                        c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P],
+    "fast_conv_dgrad": [P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                        c_int, c_int, c_int, c_long, c_float, P, P],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }
@@ -85,6 +91,17 @@ def call(name: str, *args):
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def call_fast(name: str, *args) -> bool:
+    """Specialised-shape launcher: True if it handled the call, False if the shape is not specialised."""
+    rc = getattr(lib(), name)(*args)
+    if rc < 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+    return rc == 1
+
+
+USE_FAST = True
 
 
 def check(t: torch.Tensor, dtype=None, shape=None, numel=None, name="tensor", cuda=True):

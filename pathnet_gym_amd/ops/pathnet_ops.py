@@ -162,6 +162,12 @@ class HipPathNet:
         if g.kind == "conv":
             if (E * g.HWo) % 16 != 0:
                 raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
+            if _lib.USE_FAST and _lib.call_fast(
+                    "fast_conv_fwd", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
+                    self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
+                    m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T, t0,
+                    bits_rows, g.in_scale, out_scale, st):
+                return
             _lib.call("launch_conv_fwd", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
                       self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
                       m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo,
@@ -179,6 +185,17 @@ class HipPathNet:
         g_scale = self.out_scale_last if l == self.L - 1 else 1.0
         st = _lib.stream()
         if g.kind == "conv":
+            fast_w = _lib.USE_FAST and _lib.call_fast(
+                "fast_conv_wgrad", X.data_ptr(), int(g.u8in), G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(),
+                g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin,
+                g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T, bits_rows, g.in_scale, g_scale, st)
+            fast_d = dX is None or (_lib.USE_FAST and _lib.call_fast(
+                "fast_conv_dgrad", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
+                m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S,
+                P, E, T, bits_rows, g_scale, dX.data_ptr(), st))
+            if fast_w and fast_d:
+                return
+        if g.kind == "conv" and not fast_w:
             if rows_per_chunk <= 0:
                 rows = T * E * g.HWo
                 # ~8 chunks per path keeps >= 8*P workgroups while bounding atomics
@@ -187,11 +204,12 @@ class HipPathNet:
                       grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l,
                       self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo, g.K, g.KP, P, E, T,
                       bits_rows, rows_per_chunk, g.in_scale, g_scale, st)
+        if g.kind == "conv" and not fast_d:
             if dX is not None:
                 _lib.call("launch_conv_dgrad", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
                           m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH,
                           g.KW, g.S, g.Ho, g.Wo, P, E, T, bits_rows, g_scale, dX.data_ptr(), st)
-        else:
+        if g.kind == "fc":
             _lib.call("launch_fc_wgrad", X.data_ptr(), g.ldx, G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(),
                       g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(), self.inv_slot.data_ptr(),
                       self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T, bits_rows, g_scale, st)

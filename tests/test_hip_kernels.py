@@ -307,3 +307,30 @@ def test_engine_update_and_graph_replay(hip_lib, preset_name):
     assert torch.isfinite(tr.model.store.flat).all()
     assert not torch.equal(w0, tr.model.store.flat.detach())
     assert tr.global_step == 4 * 4 * 16 * 5
+
+
+def test_fast_conv_kernels_match_generic(hip_lib):
+    """Compile-time-geometry conv kernels == generic runtime-geometry kernels."""
+    from pathnet_gym_amd.ops import _lib
+    cfg = small_pixel_cfg()
+    P, E, T = 4, 16, 2
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, seed=9)
+    m = make_model(cfg, P, masks, seed=11)
+    g = torch.Generator(device="cpu").manual_seed(4)
+    obs_steps = [torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+                 for _ in range(T)]
+    dfeat = torch.randn(T * P * E, 256, generator=g).to(DEV)
+    try:
+        _lib.USE_FAST = False
+        f0, g0 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+    finally:
+        _lib.USE_FAST = True
+    f1, g1 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+    assert torch.equal(f0, f1)          # same math, same rounding in the forward
+    for s in m.store.layout.segments:
+        if s.layer < 0 or s.layer > 2:
+            continue
+        a, b = g1[s.offset:s.offset + s.numel], g0[s.offset:s.offset + s.numel]
+        if b.norm() < 1e-6:
+            continue
+        assert rel(a, b) < 1e-3, (s.name, rel(a, b))
