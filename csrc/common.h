@@ -21,10 +21,32 @@ typedef unsigned short bf16_t;
 
 DEVI float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
+// RNE conversion through the compiler's __bf16 type: lowers to v_cvt_pk_bf16_f32 on gfx950
 DEVI bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);   // round to nearest even (no NaN payload care)
-  return (bf16_t)(u >> 16);
+  const __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, h);
+}
+
+// 8 x uint8 (0..255, exact in bf16) -> 8 x bf16: v_cvt_f32_ubyteN + v_cvt_pk_bf16_f32
+DEVI s8v u8x8_to_bf16(uint2 v) {
+  __bf16 h[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] = (__bf16)(float)((v.x >> (8 * j)) & 0xFFu);
+    h[j + 4] = (__bf16)(float)((v.y >> (8 * j)) & 0xFFu);
+  }
+  s8v r;
+  __builtin_memcpy(&r, h, 16);
+  return r;
+}
+
+DEVI s8v f32x8_to_bf16(const float* f) {
+  __bf16 h[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = (__bf16)f[j];
+  s8v r;
+  __builtin_memcpy(&r, h, 16);
+  return r;
 }
 
 DEVI uint32_t pack2bf(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }

@@ -11,6 +11,7 @@
 //          tap set and every weight index are wave-uniform -> weights come
 //          through the scalar cache (s_load) and feed v_fma as SGPR operands.
 #include "common.h"
+#include <type_traits>
 
 #define NCT 5            // column-tile capacity: 10 modules x 8 maps (M <= 10)
 #define MAXM_F 16
@@ -31,16 +32,35 @@ using C1 = CG<160, 120, 4, 8, 8, 4, true>;
 using C2 = CG<39, 29, 8, 4, 4, 2, false>;
 using C3 = CG<18, 13, 8, 3, 3, 1, false>;
 
+// Path-local row r = (s, pos) with s = t*E + e.  Advancing by a stage of n rows
+// (n < HOWO) needs at most one wrap: no divisions inside the main loops.
+struct RowIt {
+  int r, t, e, pos;
+};
+DEVI void rowit_init(RowIt& it, int r, int E, int howo) {
+  it.r = r;
+  const int s = r / howo;
+  it.pos = r - s * howo;
+  it.t = s / E;
+  it.e = s - it.t * E;
+}
+DEVI void rowit_adv(RowIt& it, int n, int E, int howo) {
+  it.r += n;
+  it.pos += n;
+  while (it.pos >= howo) {
+    it.pos -= howo;
+    if (++it.e == E) { it.e = 0; ++it.t; }
+  }
+}
+DEVI long rowit_sample(const RowIt& it, int p, int E, int PE, int t0) {
+  return (long)(t0 + it.t) * PE + (long)p * E + it.e;
+}
+
 template <bool U8IN>
 DEVI s8v ld8(const void* X, long off) {
   s8v r;
   if constexpr (U8IN) {
-    const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + off);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      r[j] = (short)(__float_as_uint((float)((v.x >> (8 * j)) & 0xFFu)) >> 16);
-      r[j + 4] = (short)(__float_as_uint((float)((v.y >> (8 * j)) & 0xFFu)) >> 16);
-    }
+    r = u8x8_to_bf16(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + off));
   } else {
     r = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + off);
   }
@@ -50,7 +70,7 @@ DEVI s8v ld8(const void* X, long off) {
 // ===========================================================================
 // forward: grid = (ceil(T*E*HOWO / 256), P); each wave loops over 32-row tiles
 // ===========================================================================
-#define FF_ROWS 256
+#define FF_ROWS 512
 template <class G>
 __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X, bf16_t* __restrict__ Y,
                                                      uint8_t* __restrict__ bits, const bf16_t* __restrict__ Wc,
@@ -78,61 +98,81 @@ __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X,
   if (tid < NCT * 16) bias_s[tid] = (tid >> 3) < cnt ? flat[bias_off + (long)mods[tid >> 3] * chunk + (tid & 7)] : 0.f;
   __syncthreads();
 
-  const long Rtot = (long)T * E * G::HOWO;
+  const int Rtot = T * E * G::HOWO;
   const int PE = P * E;
   const int w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
-  for (int tile = 0; tile < FF_ROWS / 128; ++tile) {
-    const long rbase = (long)blockIdx.x * FF_ROWS + tile * 128 + w * 32;
-    if (rbase >= Rtot) break;
-    long xb[2];
-    bool va[2];
+  // lane rows: A-operand rows (rbase + 16i + c16) and epilogue rows (rbase + 16i + 4q + r)
+  const int rfirst = blockIdx.x * FF_ROWS + w * 32;
+  RowIt ait[2], eit[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rowit_init(ait[i], rfirst + i * 16 + c16, E, G::HOWO);
+    rowit_init(eit[i], rfirst + i * 16 + 4 * q, E, G::HOWO);
+  }
+  constexpr int NK = G::KP / 32;
+  using ARaw = typename std::conditional<G::U8, uint2, s8v>::type;
+  ARaw araw[2][NK];
+  // issue the global loads of one 32-row tile (2 MFMA row tiles x NK k-steps) into registers
+  auto load_tile = [&](int rbase) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const long ra = rbase + i * 16 + c16;
-      va[i] = ra < Rtot;
-      const long rr = va[i] ? ra : rbase;
-      const int s = (int)(rr / G::HOWO);
-      const int pos = (int)(rr - (long)s * G::HOWO);
-      const int oh = pos / G::WO, ow = pos - oh * G::WO;
-      xb[i] = sample_global(p, s, E, PE, t0) * (long)G::IN_ELEMS + (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN;
+      const bool va = rbase < Rtot && ait[i].r < Rtot;
+      const int oh = ait[i].pos / G::WO, ow = ait[i].pos - oh * G::WO;
+      const long xb = rowit_sample(ait[i], p, E, PE, t0) * (long)G::IN_ELEMS +
+                      (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN;
+      rowit_adv(ait[i], 128, E, G::HOWO);
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const int off = G::koff(kk * 4 + grp);
+        if constexpr (G::U8) {
+          araw[i][kk] = make_uint2(0u, 0u);
+          if (va && off >= 0) araw[i][kk] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xb + off);
+        } else {
+          araw[i][kk] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+          if (va && off >= 0) araw[i][kk] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xb + off);
+        }
+      }
     }
+  };
+  load_tile(rfirst);
+  for (int tile = 0; tile < FF_ROWS / 128; ++tile) {
+    const int rbase = rfirst + tile * 128;
+    if (rbase >= Rtot) break;
+    s8v a[2][NK];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        if constexpr (G::U8) a[i][kk] = u8x8_to_bf16(araw[i][kk]);
+        else a[i][kk] = araw[i][kk];
+      }
+    if (tile + 1 < FF_ROWS / 128) load_tile(rbase + 128);     // next tile in flight during MFMAs + epilogue
     f4v acc[2][NCT];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kk = 0; kk < G::KP / 32; ++kk) {
+    for (int kk = 0; kk < NK; ++kk) {
       const int kc = kk * 4 + grp;
-      const int off = G::koff(kc);     // grp-dependent: computed per lane from a constexpr table
-      s8v a[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        a[i] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
-        if (va[i] && off >= 0) a[i] = ld8<G::U8>(X, xb[i] + off);
-      }
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
         if (ct < nct) {
           const s8v b = *reinterpret_cast<const s8v*>(Ws + (ct * 16 + c16) * KPs + kc * 8);
-          acc[0][ct] = mfma16(a[0], b, acc[0][ct]);
-          acc[1][ct] = mfma16(a[1], b, acc[1][ct]);
+          acc[0][ct] = mfma16(a[0][kk], b, acc[0][ct]);
+          acc[1][ct] = mfma16(a[1][kk], b, acc[1][ct]);
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const long r16 = rbase + i * 16;
-      if (r16 >= Rtot) break;
+      const int r16 = rbase + i * 16;
+      const RowIt e0 = eit[i];
+      rowit_adv(eit[i], 128, E, G::HOWO);
+      if (r16 >= Rtot) continue;
       float sum[4] = {0.f, 0.f, 0.f, 0.f};
-      long grow4;
-      {
-        const long r4 = r16 + 4 * q;
-        const int s = (int)(r4 / G::HOWO);
-        const int pos = (int)(r4 - (long)s * G::HOWO);
-        grow4 = sample_global(p, s, E, PE, t0) * G::HOWO + pos;
-      }
+      const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
         if (ct < nct) {
@@ -153,42 +193,43 @@ __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X,
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
-      // pack: lanes c16 0..7 hold maps 0..7 of rows 4q+r -> gather 8 bf16 into lane c16==0 per row
       if (h == 0) {
+        // rows 4q..4q+3 of this tile are consecutive global rows (E*HOWO % 16 == 0)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const long row = r16 + 4 * q + r;
-          const int s = (int)(row / G::HOWO);
-          const int pos = (int)(row - (long)s * G::HOWO);
-          Y[(sample_global(p, s, E, PE, t0) * G::HOWO + pos) * 8 + ch] = f2bf(sum[r] * out_scale);
-        }
+        for (int r = 0; r < 4; ++r) Y[(grow4 + r) * 8 + ch] = f2bf(sum[r] * out_scale);
       }
     }
   }
 }
 
 // ===========================================================================
-// wgrad: grid = (nchunks, P); 64-row stages
+// wgrad: grid = (nchunks, P), 512 threads (8 waves), 32-row stages, register
+// prefetch + double-buffered LDS: one barrier per stage; stage i+1's global
+// loads are in flight while the MFMAs of stage i run.
+//   A = im2col(X)^T  (m = k index, reduction = rows)  -> ds_read_b64_tr_b16
+//   B = masked G      (reduction = rows, n = slot*8+map) -> ds_read_b64_tr_b16
 // ===========================================================================
-#define WG_RB 64
+#define WG_RB 32
+#define WG_NT 512
 template <class G>
-__global__ __launch_bounds__(256) void conv_wgrad_fast(const void* __restrict__ X, const float* __restrict__ Gr,
-                                                       const uint8_t* __restrict__ bits, float* __restrict__ grad,
-                                                       long w_off, long b_off, int chunk,
-                                                       const int* __restrict__ act_idx,
-                                                       const int* __restrict__ act_cnt, int layer, int L, int M,
-                                                       int P, int E, int T, long bits_rows, int rows_per_chunk,
-                                                       float in_scale, float g_scale) {
+__global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restrict__ X, const float* __restrict__ Gr,
+                                                         const uint8_t* __restrict__ bits, float* __restrict__ grad,
+                                                         long w_off, long b_off, int chunk,
+                                                         const int* __restrict__ act_idx,
+                                                         const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                         int P, int E, int T, long bits_rows, int rows_per_chunk,
+                                                         float in_scale, float g_scale) {
   constexpr int XS = G::KP + 8;
   constexpr int GS = NCT * 16 + 8;
   constexpr int NMT = G::KP / 16;
-  constexpr int MPW = (NMT + 3) / 4;   // m tiles per wave
-  __shared__ __attribute__((aligned(16))) bf16_t Xs[WG_RB * XS];
-  __shared__ __attribute__((aligned(16))) bf16_t Gs[WG_RB * GS];
-  __shared__ long rowx[WG_RB];
-  __shared__ long rowg[WG_RB];
+  constexpr int NW = WG_NT / 64;
+  constexpr int MPW = (NMT + NW - 1) / NW;
+  constexpr int XIT = (WG_RB * G::KC + WG_NT - 1) / WG_NT;
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][WG_RB * XS];
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][WG_RB * GS];
   __shared__ float dbias[NCT * 16];
   __shared__ int mods[MAXM_F];
+  __shared__ __attribute__((aligned(16))) uint32_t mtab[256 * 8];   // byte -> 8 x (0 | 0xFFFFFFFF)
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
   if (cnt == 0) return;
@@ -196,105 +237,138 @@ __global__ __launch_bounds__(256) void conv_wgrad_fast(const void* __restrict__ 
   const int tid = threadIdx.x;
   if (tid < MAXM_F) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
   if (tid < NCT * 16) dbias[tid] = 0.f;
-  for (int i = tid; i < WG_RB * GS; i += 256) Gs[i] = 0;
-  const long Rtot = (long)T * E * G::HOWO;
+  for (int i = tid; i < 256 * 8; i += WG_NT) mtab[i] = ((i >> 3) >> (i & 7)) & 1u ? 0xFFFFFFFFu : 0u;
+  for (int i = tid; i < 2 * WG_RB * GS; i += WG_NT) (&Gs[0][0])[i] = 0;
+  static_assert(G::HOWO > WG_RB, "row iterator assumes one wrap per stage");
+  const int Rtot = T * E * G::HOWO;          // host asserts < 2^31
   const int PE = P * E;
-  const long r_begin = (long)blockIdx.x * rows_per_chunk;
-  const long r_end = min(Rtot, r_begin + rows_per_chunk);
+  const int r_begin = blockIdx.x * rows_per_chunk;
+  const int r_end = min(Rtot, r_begin + rows_per_chunk);
   const int w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
-  // G staging role: fixed slot per thread
-  const int gslot = tid & 15, grow0 = tid >> 4;          // rows grow0 + 16*i
+  const int gslot = tid & 15, grow = tid >> 4;     // G staging role (fixed slot per thread)
+  const bool gact = gslot < cnt;
   float bpart[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   f4v acc[MPW][NCT];
 #pragma unroll
   for (int a = 0; a < MPW; ++a)
 #pragma unroll
     for (int b = 0; b < NCT; ++b) acc[a][b] = {0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
 
-  for (long rb = r_begin; rb < r_end; rb += WG_RB) {
-    if (tid < WG_RB) {
-      const long r = rb + tid;
-      long xo = -1, go = -1;
-      if (r < r_end) {
-        const int s = (int)(r / G::HOWO);
-        const int pos = (int)(r - (long)s * G::HOWO);
-        const int oh = pos / G::WO, ow = pos - oh * G::WO;
-        const long sg = sample_global(p, s, E, PE, 0);
-        xo = sg * (long)G::IN_ELEMS + (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN;
-        go = sg * G::HOWO + pos;
-      }
-      rowx[tid] = xo;
-      rowg[tid] = go;
-    }
-    __syncthreads();
-    // X tile
+  // ---- prefetch registers ----
+  using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
+  XRaw xr[XIT];
+  bool xv[XIT];
+  float4 g0r, g1r;
+  uint32_t gbr = 0;
+  bool gv = false;
+
+  // per-item row iterators (rows advance by WG_RB per stage)
+  RowIt xit[XIT];
+  int xkoff[XIT];
 #pragma unroll
-    for (int it0 = 0; it0 < WG_RB * G::KC; it0 += 256) {
-      const int it = it0 + tid;
+  for (int j = 0; j < XIT; ++j) {
+    const int it = tid + WG_NT * j;
+    const int row = it / G::KC, kc = it - row * G::KC;
+    xkoff[j] = (it < WG_RB * G::KC) ? G::koff(kc) : -1;
+    rowit_init(xit[j], (int)r_begin + row, E, G::HOWO);
+  }
+  RowIt git;
+  rowit_init(git, (int)r_begin + grow, E, G::HOWO);
+
+  auto load_stage = [&]() {
+#pragma unroll
+    for (int j = 0; j < XIT; ++j) {
+      xv[j] = xkoff[j] >= 0 && xit[j].r < r_end;
+      if (xv[j]) {
+        const int oh = xit[j].pos / G::WO, ow = xit[j].pos - oh * G::WO;
+        const long xo = rowit_sample(xit[j], p, E, PE, 0) * (long)G::IN_ELEMS +
+                        (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN + xkoff[j];
+        if constexpr (G::U8)
+          xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xo);
+        else
+          xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xo);
+      }
+      rowit_adv(xit[j], WG_RB, E, G::HOWO);
+    }
+    gv = gact && git.r < r_end;
+    if (gv) {
+      const long go = rowit_sample(git, p, E, PE, 0) * G::HOWO + git.pos;
+      g0r = *reinterpret_cast<const float4*>(Gr + go * 8);
+      g1r = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+      gbr = bits[(long)gslot * bits_rows + go];
+    }
+    rowit_adv(git, WG_RB, E, G::HOWO);
+  };
+  auto write_stage = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < XIT; ++j) {
+      const int it = tid + WG_NT * j;
       if (it < WG_RB * G::KC) {
         const int row = it / G::KC, kc = it - row * G::KC;
-        const long xo = rowx[row];
-        const int off = G::koff(kc);
         s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (xo >= 0 && off >= 0) v = ld8<G::U8>(X, xo + off);
-        *reinterpret_cast<s8v*>(Xs + row * XS + kc * 8) = v;
-      }
-    }
-    // masked G tile: thread = (slot gslot, rows grow0 + 16 i)
-    if (gslot < cnt) {
-#pragma unroll
-      for (int i = 0; i < WG_RB / 16; ++i) {
-        const int row = grow0 + 16 * i;
-        const long go = rowg[row];
-        s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (go >= 0) {
-          const float4 g0 = *reinterpret_cast<const float4*>(Gr + go * 8);
-          const float4 g1 = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
-          const uint32_t b = bits[(long)gslot * bits_rows + go];
-          const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            const float x = ((b >> c) & 1u) ? gv[c] * g_scale : 0.f;
-            bpart[c] += x;
-            v[c] = (short)f2bf(x);
-          }
+        if (xv[j]) {
+          if constexpr (G::U8)
+            v = u8x8_to_bf16(xr[j]);
+          else
+            v = xr[j];
         }
-        *reinterpret_cast<s8v*>(Gs + row * GS + gslot * 8) = v;
+        *reinterpret_cast<s8v*>(&Xs[buf][row * XS + kc * 8]) = v;
       }
     }
+    if (gact) {
+      s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (gv) {
+        // ReLU-bit byte -> 8 fp32 AND masks from the LDS table (one b128 x2 read, 8 v_and)
+        const uint4 m0 = *reinterpret_cast<const uint4*>(&mtab[gbr * 8]);
+        const uint4 m1 = *reinterpret_cast<const uint4*>(&mtab[gbr * 8 + 4]);
+        float gg[8] = {__uint_as_float(__float_as_uint(g0r.x) & m0.x), __uint_as_float(__float_as_uint(g0r.y) & m0.y),
+                       __uint_as_float(__float_as_uint(g0r.z) & m0.z), __uint_as_float(__float_as_uint(g0r.w) & m0.w),
+                       __uint_as_float(__float_as_uint(g1r.x) & m1.x), __uint_as_float(__float_as_uint(g1r.y) & m1.y),
+                       __uint_as_float(__float_as_uint(g1r.z) & m1.z), __uint_as_float(__float_as_uint(g1r.w) & m1.w)};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) bpart[c] += gg[c];
+        v = f32x8_to_bf16(gg);
+      }
+      *reinterpret_cast<s8v*>(&Gs[buf][grow * GS + gslot * 8]) = v;
+    }
+  };
+
+  __syncthreads();
+  if (r_begin < r_end) load_stage();
+  int buf = 0;
+  for (int rb = r_begin; rb < r_end; rb += WG_RB, buf ^= 1) {
+    write_stage(buf);
     __syncthreads();
+    if (rb + WG_RB < r_end) load_stage();
+    const bf16_t* xs = Xs[buf];
+    const bf16_t* gs = Gs[buf];
+    s8v bfr[NCT];
 #pragma unroll
-    for (int ks = 0; ks < WG_RB / 32; ++ks) {
-      s8v bfr[NCT];
-#pragma unroll
-      for (int nt = 0; nt < NCT; ++nt) {
-        if (nt < nct) {
-          const s4v v0 = lds_tr16(Gs + (32 * ks + 8 * grp + q) * GS + nt * 16 + 4 * pp);
-          const s4v v1 = lds_tr16(Gs + (32 * ks + 8 * grp + 4 + q) * GS + nt * 16 + 4 * pp);
-          bfr[nt] = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        }
-      }
-#pragma unroll
-      for (int mi = 0; mi < MPW; ++mi) {
-        const int mt = w + 4 * mi;
-        if (mt < NMT) {
-          const s4v v0 = lds_tr16(Xs + (32 * ks + 8 * grp + q) * XS + mt * 16 + 4 * pp);
-          const s4v v1 = lds_tr16(Xs + (32 * ks + 8 * grp + 4 + q) * XS + mt * 16 + 4 * pp);
-          const s8v afr = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-#pragma unroll
-          for (int nt = 0; nt < NCT; ++nt)
-            if (nt < nct) acc[mi][nt] = mfma16(afr, bfr[nt], acc[mi][nt]);
-        }
+    for (int nt = 0; nt < NCT; ++nt) {
+      if (nt < nct) {
+        const s4v v0 = lds_tr16(gs + (8 * grp + q) * GS + nt * 16 + 4 * pp);
+        const s4v v1 = lds_tr16(gs + (8 * grp + 4 + q) * GS + nt * 16 + 4 * pp);
+        bfr[nt] = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       }
     }
-    __syncthreads();
+#pragma unroll
+    for (int mi = 0; mi < MPW; ++mi) {
+      const int mt = w + NW * mi;
+      if (mt < NMT) {
+        const s4v v0 = lds_tr16(xs + (8 * grp + q) * XS + mt * 16 + 4 * pp);
+        const s4v v1 = lds_tr16(xs + (8 * grp + 4 + q) * XS + mt * 16 + 4 * pp);
+        const s8v afr = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int nt = 0; nt < NCT; ++nt)
+          if (nt < nct) acc[mi][nt] = mfma16(afr, bfr[nt], acc[mi][nt]);
+      }
+    }
   }
   const int h = i16 >> 3, ch = l & 7;
 #pragma unroll
   for (int mi = 0; mi < MPW; ++mi) {
-    const int mt = w + 4 * mi;
+    const int mt = w + NW * mi;
     if (mt < NMT) {
 #pragma unroll
       for (int nt = 0; nt < NCT; ++nt) {
@@ -305,16 +379,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_fast(const void* __restrict__ 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int k = mt * 16 + 4 * grp + r;
-              if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * in_scale);
+              if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale));
             }
           }
         }
       }
     }
   }
-  if (gslot < cnt) {
+  if (gact) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) atomicAdd(&dbias[gslot * 8 + c], bpart[c]);
+    for (int c = 0; c < 8; ++c) atomicAdd(&dbias[gslot * 8 + c], bpart[c] * g_scale);
   }
   __syncthreads();
   if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
@@ -406,12 +480,12 @@ static int wgrad_t(const void* X, const float* Gr, const void* bits, float* grad
                    const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, long br, float is,
                    float gs, hipStream_t st) {
   const long rows = (long)T * E * G::HOWO;
-  // ~64 chunks per path (>= 16 workgroups per CU at P=64) in whole 64-row stages
-  long rpc = (rows + 63) / 64;
+  // 16 chunks per path: P*16 workgroups of 512 threads, whole 32-row stages
+  long rpc = (rows + 15) / 16;
   rpc = (rpc + WG_RB - 1) / WG_RB * WG_RB;
   if (rpc < WG_RB * 4) rpc = WG_RB * 4;
   dim3 grid((unsigned)((rows + rpc - 1) / rpc), P);
-  conv_wgrad_fast<G><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L,
+  conv_wgrad_fast<G><<<grid, WG_NT, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L,
                                            M, P, E, T, br, (int)rpc, is, gs);
   return (int)hipGetLastError();
 }

@@ -168,6 +168,10 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
     epret_out[env] = done ? (float)epret : 0.f;
   }
   // --- fused render + gray + resize + stack push ---
+  // (1) the 210x160 gray image is evaluated ONCE per source pixel into LDS
+  //     (4 pixels per thread-iteration, one 32-bit LDS store);
+  // (2) every output pixel reads its 4 bilinear taps from LDS.
+  __shared__ uint32_t gray[210 * 160 / 4];
   Scene S;
   S.cy = st.s[CY] >> 4;   // floor division by U=16 (values are non-negative)
   S.py = st.s[PY] >> 4;
@@ -177,13 +181,22 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
   S.cs_t = st.s[CS] / 10; S.cs_o = st.s[CS] % 10;
   S.ps_t = st.s[PS] / 10; S.ps_o = st.s[PS] % 10;
   S.g_bg = g_bg; S.g_wall = g_wall; S.g_cpu = g_cpu; S.g_player = g_player; S.g_ball = g_ball;
+  for (int q4 = threadIdx.x; q4 < 210 * 160 / 4; q4 += 256) {
+    const int r = q4 / 40, c0 = (q4 - r * 40) * 4;
+    uint32_t wv = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wv |= (uint32_t)scene_gray(S, r, c0 + e) << (8 * e);
+    gray[q4] = wv;
+  }
+  __syncthreads();
+  const uint8_t* g8 = reinterpret_cast<const uint8_t*>(gray);
   const long base = (long)env * OBS_H * OBS_W;
   for (int pix = threadIdx.x; pix < OBS_H * OBS_W; pix += 256) {
     const int y = pix / OBS_W, x = pix - y * OBS_W;
     const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
     const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x], cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
-    const int ra = scene_gray(S, ys0, xs0) * cx0 + scene_gray(S, ys0, xs1) * cx1;
-    const int rb = scene_gray(S, ys1, xs0) * cx0 + scene_gray(S, ys1, xs1) * cx1;
+    const int ra = g8[ys0 * 160 + xs0] * cx0 + g8[ys0 * 160 + xs1] * cx1;
+    const int rb = g8[ys1 * 160 + xs0] * cx0 + g8[ys1 * 160 + xs1] * cx1;
     int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
     v = v < 0 ? 0 : (v > 255 ? 255 : v);
     const uint32_t f = (uint32_t)v;
