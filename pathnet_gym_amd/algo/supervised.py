@@ -1,0 +1,189 @@
+"""Supervised PathNet: sequential transfer with module locking (MNIST -> SVHN).
+
+BASELINE.json config 4.  The reference only keeps the leftovers of the
+upstream supervised PathNet scripts (``pathnet.py:10-18,65-76,100-196``,
+``input_data.py``): FC modules, the heterogeneous ``module2`` (skip / FC+ReLU /
+residual by module index), ``select_two_candi`` binary tournaments and
+parameter backup/restore.  This module rebuilds that workload on the shared
+engine pieces:
+
+* population of P paths trained in ONE batched forward (dense-masked PathNet
+  trunk; every path gets its own minibatch), gradients summed over paths
+  (shared modules, Hogwild-equivalent), plain SGD as in the supervised
+  scripts;
+* fitness = accuracy of the path on a held-out batch after its training
+  steps; binary tournament (B=2) with the same mutation operator;
+* task end: freeze the best path, re-initialise every other parameter, new
+  task = new classification head, evolution restarts with the frozen modules
+  always expressed.
+
+Data: no dataset download is possible here, so both tasks are synthetic and
+shape-compatible: ``mnist`` = 28x28 white-on-black bitmap digits with random
+scale/shift/stroke/noise padded to 32x32x3; ``svhn`` = 32x32x3 coloured digits
+on coloured backgrounds with neighbouring distractor digits.  Both are 10-way.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Dict, List
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..config import LayerSpec, PathNetConfig
+from ..models.pathnet import ParamStore, trunk_forward_ref
+from .ga import Population
+
+FONT5x7 = [
+    "01110 10001 10011 10101 11001 10001 01110", "00100 01100 00100 00100 00100 00100 01110",
+    "01110 10001 00001 00010 00100 01000 11111", "11111 00010 00100 00010 00001 10001 01110",
+    "00010 00110 01010 10010 11111 00010 00010", "11111 10000 11110 00001 00001 10001 01110",
+    "00110 01000 10000 11110 10001 10001 01110", "11111 00001 00010 00100 01000 01000 01000",
+    "01110 10001 10001 01110 10001 10001 01110", "01110 10001 10001 01111 00001 00010 01100",
+]
+
+
+def _glyphs(device):
+    g = torch.zeros(10, 7, 5, device=device)
+    for d, s in enumerate(FONT5x7):
+        for r, row in enumerate(s.split()):
+            for c, ch in enumerate(row):
+                g[d, r, c] = float(ch == "1")
+    return g
+
+
+def make_digits(kind: str, n: int, seed: int, device="cpu"):
+    """Synthetic digit dataset -> (X [n, 32*32*3] float in [0,1], y [n] long)."""
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    y = torch.randint(0, 10, (n,), generator=gen)
+    glyph = _glyphs("cpu")
+    img = torch.zeros(n, 3, 32, 32)
+    for i in range(n):
+        if kind == "mnist":
+            s = int(torch.randint(3, 5, (1,), generator=gen))
+            g = F.interpolate(glyph[y[i]][None, None], scale_factor=s, mode="nearest")[0, 0]
+            if torch.rand(1, generator=gen) < 0.5:      # thicker stroke
+                g = torch.clamp(g + torch.roll(g, 1, 1), 0, 1)
+            h, w = g.shape
+            oy = 2 + int(torch.randint(0, max(1, 28 - h + 1), (1,), generator=gen))
+            ox = 2 + int(torch.randint(0, max(1, 28 - w + 1), (1,), generator=gen))
+            oy, ox = min(oy, 32 - h), min(ox, 32 - w)
+            img[i, :, oy:oy + h, ox:ox + w] = g
+            img[i] += 0.1 * torch.randn(3, 32, 32, generator=gen)
+            img[i, 1:] = img[i, :1]          # gray replicated to 3 channels
+        else:   # svhn-like
+            bg = torch.rand(3, generator=gen)
+            fg = (bg + 0.35 + 0.3 * torch.rand(3, generator=gen)) % 1.0
+            img[i] = bg[:, None, None]
+            s = 3
+            for k, (dx, lab) in enumerate(((-13, int(torch.randint(0, 10, (1,), generator=gen))), (0, int(y[i])),
+                                           (13, int(torch.randint(0, 10, (1,), generator=gen))))):
+                g = F.interpolate(glyph[lab][None, None], scale_factor=s, mode="nearest")[0, 0]
+                h, w = g.shape
+                oy = 5 + int(torch.randint(-2, 3, (1,), generator=gen))
+                ox = 16 - w // 2 + dx + int(torch.randint(-1, 2, (1,), generator=gen))
+                y0, y1, x0, x1 = max(oy, 0), min(oy + h, 32), max(ox, 0), min(ox + w, 32)
+                if x1 <= x0:
+                    continue
+                gg = g[y0 - oy:y1 - oy, x0 - ox:x1 - ox]
+                region = img[i, :, y0:y1, x0:x1]
+                img[i, :, y0:y1, x0:x1] = region * (1 - gg) + fg[:, None, None] * gg
+            img[i] += 0.08 * torch.randn(3, 32, 32, generator=gen)
+    X = img.clamp(0, 1).permute(0, 2, 3, 1).reshape(n, -1)     # NHWC flatten
+    return X.to(device), y.to(device)
+
+
+def supervised_config(L=3, M=10, N=3, width=20, din=32 * 32 * 3, module2=True):
+    """FC PathNet; layers >0 use module2 types (j%3: skip / fc / residual, pathnet.py:137-168)."""
+    layers = [LayerSpec("fc", width)]
+    for _ in range(L - 1):
+        layers.append(LayerSpec("fc", width, module_types=[0, 1, 2] if module2 else None))
+    return PathNetConfig(L=L, M=M, N=N, input_shape=(din,), layers=layers, trunk_scale="none", num_actions=10)
+
+
+class SupervisedPathNet:
+    def __init__(self, cfg: PathNetConfig, population: int, num_tasks: int, device, seed=1, B=2):
+        self.cfg = cfg
+        self.P = population
+        self.device = torch.device(device)
+        self.store = ParamStore(cfg, self.device, seed)
+        self.store.flat.requires_grad_(True)
+        self.init_flat = self.store.flat.detach().clone()
+        F_ = cfg.layers[-1].out
+        g = torch.Generator().manual_seed(seed + 17)
+        self.heads = [(torch.empty(F_, 10).uniform_(-1 / math.sqrt(F_), 1 / math.sqrt(F_), generator=g).to(device)
+                       .requires_grad_(True), torch.zeros(10, device=device, requires_grad=True))
+                      for _ in range(num_tasks)]
+        self.pop = Population(population, cfg.L, cfg.M, cfg.N, B=B, seed=seed, concurrent=max(1, population // B))
+        self.frozen = np.zeros((cfg.L, cfg.M), np.float32)
+        self.frozen_elems = torch.zeros_like(self.store.flat, dtype=torch.bool)
+
+    def logits(self, X, mask, task):
+        feat = trunk_forward_ref(self.store, X, mask)
+        W, b = self.heads[task]
+        return feat @ W + b
+
+    def train_generation(self, data, task, steps, batch, lr, gen):
+        X, y = data
+        n = X.shape[0]
+        P = self.P
+        masks = torch.from_numpy(self.pop.expressed()).to(self.device)
+        mask_rows = masks.repeat_interleave(batch, 0)
+        g = torch.Generator(device="cpu").manual_seed(1000003 * gen + task)
+        for _ in range(steps):
+            idx = torch.randint(0, n, (P * batch,), generator=g).to(self.device)
+            logit = self.logits(X[idx], mask_rows, task)
+            loss = F.cross_entropy(logit, y[idx], reduction="sum") / batch
+            self.store.flat.grad = None
+            W, b = self.heads[task]
+            W.grad = None
+            b.grad = None
+            loss.backward()
+            with torch.no_grad():
+                gflat = self.store.flat.grad.masked_fill(self.frozen_elems, 0.0)
+                self.store.flat.sub_(lr * gflat / P)
+                W.sub_(lr * W.grad / P)
+                b.sub_(lr * b.grad / P)
+        # fitness: accuracy of every path on a fresh evaluation batch
+        with torch.no_grad():
+            idx = torch.randint(0, n, (P * batch * 4,), generator=g).to(self.device)
+            pred = self.logits(X[idx], masks.repeat_interleave(batch * 4, 0), task).argmax(-1)
+            acc = (pred == y[idx]).float().view(P, -1).mean(1)
+        return acc.cpu().numpy()
+
+    def end_task(self, winner: int):
+        frozen = self.pop.freeze(winner, union=True)
+        self.frozen = frozen
+        keep = torch.zeros_like(self.frozen_elems)
+        for s in self.store.layout.segments:
+            if s.layer >= 0 and frozen[s.layer, s.module] > 0.5:
+                keep[s.offset:s.offset + s.numel] = True
+        self.frozen_elems = keep
+        with torch.no_grad():
+            self.store.flat.copy_(torch.where(keep, self.store.flat, self.init_flat))
+
+
+def run_supervised_transfer(a) -> Dict:
+    device = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    tasks = [t.strip() for t in a.tasks.split(",")]
+    cfg = supervised_config(a.L, a.M, a.N, a.width)
+    sp = SupervisedPathNet(cfg, a.population, len(tasks), device, a.seed, a.B)
+    out = {"tasks": tasks, "per_task": []}
+    t0 = time.time()
+    for ti, name in enumerate(tasks):
+        data = make_digits(name, 4096, a.seed * 31 + ti, device)
+        if ti > 0:
+            sp.pop.init_genotypes()
+        best_hist = []
+        for gen in range(a.generations):
+            acc = sp.train_generation(data, ti, a.steps_per_gen, a.batch, a.lr, gen)
+            sp.pop.step(acc.astype(np.float32), gen)
+            best_hist.append(float(acc.max()))
+        winner = int(np.argmax(acc))
+        sp.end_task(winner)
+        out["per_task"].append({"task": name, "best_accuracy": best_hist[-1], "curve": best_hist,
+                                "frozen": sp.frozen.astype(int).tolist()})
+    out["seconds"] = time.time() - t0
+    return out

@@ -90,6 +90,8 @@ class PathNetTrainer:
         self.updates = 0
         self.solved_generation: Dict[int, Optional[int]] = {}
         self.env = None
+        self.visualizer = None
+        self._last_vis = 0.0
         self._start_task(0, fresh=True)
 
     # ------------------------------------------------------------------
@@ -240,6 +242,10 @@ class PathNetTrainer:
             self._push_genotypes()
             lo, hi = self.path_offset, self.path_offset + self.P
             self.fitness_local.copy_(torch.from_numpy(self.pop.fitness[lo:hi]).to(self.device))
+            if self.visualizer is not None and time.time() - self._last_vis > 10.0:
+                from .ga import decode_path
+                self.visualizer.show([decode_path(g) for g in self.pop.genotypes], "m")   # visualize.py:90
+                self._last_vis = time.time()
             if self.logger is not None and self.ctx.is_main:
                 for e in events:
                     # "<step> Step Score: <s>" (doom_pathnet.py:256)
@@ -248,16 +254,22 @@ class PathNetTrainer:
         return st
 
     # ------------------------------------------------------------------
-    def train(self, steps_per_task: Optional[int] = None, max_updates: Optional[int] = None):
+    def train(self, steps_per_task: Optional[int] = None, max_updates: Optional[int] = None,
+              checkpoint: Optional[str] = None, checkpoint_every: int = 0):
+        """Run the task sequence (doom_pathnet.py:178-293 generalised to K tasks)."""
         steps_per_task = steps_per_task or self.cfg.steps_per_task
         t0 = time.time()
-        for task_idx in range(len(self.cfg.tasks)):
-            if task_idx != self.task_idx or task_idx > 0:
+        first = self.task_idx
+        for task_idx in range(first, len(self.cfg.tasks)):
+            if task_idx != self.task_idx:
                 self._start_task(task_idx)
             n = 0
             while self.global_step - self.task_start_step < steps_per_task:
                 st = self.update()
                 n += 1
+                if checkpoint and checkpoint_every and self.updates % checkpoint_every == 0:
+                    from ..utils import checkpoint as ckpt
+                    ckpt.save(self, checkpoint)
                 if self.logger is not None and self.ctx.is_main and self.updates % 10 == 0:
                     el = time.time() - t0
                     self.logger.log("perf", step=self.global_step, steps_per_sec=self.global_step / max(el, 1e-9),
@@ -266,6 +278,12 @@ class PathNetTrainer:
                 if max_updates is not None and n >= max_updates:
                     break
             winner, frozen = self.end_task()
+            if self.visualizer is not None:
+                from .ga import decode_path
+                self.visualizer.set_fixed(decode_path(frozen), "r" if task_idx == 0 else "g")   # :276
+            if checkpoint:
+                from ..utils import checkpoint as ckpt
+                ckpt.save(self, checkpoint)
             if self.logger is not None and self.ctx.is_main:
                 self.logger.log("freeze", task=task_idx, winner=winner, frozen=frozen.astype(int).tolist(),
                                 solved_generation=self.solved_generation.get(task_idx))

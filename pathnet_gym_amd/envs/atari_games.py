@@ -1,0 +1,578 @@
+"""Synthetic Atari-style games for the multi-task suite (Pong -> Breakout -> SpaceInvaders -> Alien).
+
+BASELINE.json config 5 names a 4-task Atari suite; the reference's task
+lists are Atari ids (``constants.py:12-15``: MsPacman, Alien, Centipede).
+ALE is not available in this image, so each game is a small on-device
+vectorised re-creation with the Atari screen geometry (210x160x3 uint8 RGB)
+and the same preprocessing/stacking pipeline as Pong
+(``envs/pong.py:preprocess_frames``):
+
+* ``Breakout``      4 actions (NOOP, FIRE, RIGHT, LEFT); 6x18 bricks worth
+                    7/7/4/4/1/1 by row, 5 lives, FIRE serves.
+* ``SpaceInvaders`` 6 actions (NOOP, FIRE, RIGHT, LEFT, RIGHTFIRE, LEFTFIRE);
+                    6x6 marching formation worth 30..5 by row, one player
+                    shot and one alien bomb in flight, 3 lives.
+* ``Alien`` / ``MsPacman``  18 / 9 actions; 13x11 maze with eggs (+10) and
+                    three chasing aliens, 3 lives, clearing the maze +500.
+* ``Centipede``     18 actions; a 10-segment centipede snaking down through
+                    mushrooms, shots worth 10 (segment) / 1 (mushroom).
+
+All dynamics are integer and the randomness uses the counter-based hash
+RNG of ``envs/base.py`` (same convention as Pong).  These envs run as torch
+ops on any device (CPU or GPU); they are not hipGraph-captured
+(``graph_safe = False``): the engine steps them eagerly.
+"""
+from __future__ import annotations
+
+import torch
+
+from .base import VecEnv, env_rand_u32
+from .pong import OBS_H, OBS_W, SCREEN_H, SCREEN_W, preprocess_frames, resize_tables
+
+BG = (0, 0, 0)
+
+
+class PixelGameVec(VecEnv):
+    """Common driver: state tensors, frame stack, auto-reset, RGB render -> preprocessing."""
+    graph_safe = False
+    n_actions = 4
+    max_steps = 27000
+
+    def __init__(self, num_envs: int, device="cpu", seed: int = 0, frameskip: int = 4, gray: str = "rgb",
+                 backend: str = "torch", no_op_max: int = 7):
+        self.num_envs = num_envs
+        self.num_actions = self.n_actions
+        self.obs_shape = (OBS_H, OBS_W, 4)
+        self.obs_dtype = torch.uint8
+        self.device = torch.device(device)
+        self.frameskip = frameskip
+        self.gray = gray
+        self.backend = backend
+        self.no_op_max = no_op_max
+        self.max_episode_steps = self.max_steps
+        self.env_id = torch.arange(num_envs, dtype=torch.int64, device=self.device)
+        self.counter = torch.zeros(num_envs, dtype=torch.int64, device=self.device)
+        self.tables = torch.from_numpy(resize_tables()).to(self.device)
+        self.rows = torch.arange(SCREEN_H, device=self.device)[None, :, None]
+        self.cols = torch.arange(SCREEN_W, device=self.device)[None, None, :]
+        self.steps = torch.zeros(num_envs, dtype=torch.int64, device=self.device)
+        self.epret = torch.zeros(num_envs, dtype=torch.int64, device=self.device)
+        self.obs = torch.zeros(num_envs, OBS_H, OBS_W, 4, dtype=torch.uint8, device=self.device)
+        self._colors = {}
+        self.init_state()
+        self.seed(seed)
+
+    # -- helpers -------------------------------------------------------------
+    def seed(self, seed: int):
+        self.seed_int = seed & 0xFFFFFFFF
+        self._seed = torch.tensor(self.seed_int, dtype=torch.int64, device=self.device)
+        self.counter.zero_()
+
+    def rand(self, stream: int, n: int) -> torch.Tensor:
+        return env_rand_u32(self._seed, self.env_id, self.counter, stream) % n
+
+    def color(self, c):
+        if c not in self._colors:
+            self._colors[c] = torch.tensor(c, dtype=torch.uint8, device=self.device)
+        return self._colors[c]
+
+    def rect(self, y0, x0, h, w):
+        """bool [N,210,160] for per-env rectangles (y0/x0 [N] pixel tensors or ints)."""
+        y0 = torch.as_tensor(y0, device=self.device).reshape(-1, 1, 1)
+        x0 = torch.as_tensor(x0, device=self.device).reshape(-1, 1, 1)
+        return (self.rows >= y0) & (self.rows < y0 + h) & (self.cols >= x0) & (self.cols < x0 + w)
+
+    def where_set(self, t, mask, v):
+        return torch.where(mask, torch.as_tensor(v, dtype=t.dtype, device=t.device).expand_as(t), t)
+
+    # -- to implement ------------------------------------------------------------
+    def init_state(self):
+        raise NotImplementedError
+
+    def reset_state(self, mask):
+        raise NotImplementedError
+
+    def physics(self, a):
+        """one sub-frame; returns int64 reward [N]"""
+        raise NotImplementedError
+
+    def game_over(self):
+        raise NotImplementedError
+
+    def draw(self, img):
+        raise NotImplementedError
+
+    # -- VecEnv API ----------------------------------------------------------------
+    def render(self) -> torch.Tensor:
+        img = torch.empty(self.num_envs, SCREEN_H, SCREEN_W, 3, dtype=torch.uint8, device=self.device)
+        img[:] = self.color(BG)
+        self.draw(img)
+        return img
+
+    def frame(self):
+        return preprocess_frames(self.render(), self.tables, self.gray)
+
+    def reset(self):
+        allm = torch.ones(self.num_envs, dtype=torch.bool, device=self.device)
+        self.reset_where(allm)
+        return self.obs.clone()
+
+    def reset_where(self, mask):
+        self.reset_state(mask)
+        self.steps = torch.where(mask, torch.zeros_like(self.steps), self.steps)
+        self.epret = torch.where(mask, torch.zeros_like(self.epret), self.epret)
+        self.counter += mask.long()
+        f = self.frame()
+        self.obs = torch.where(mask[:, None, None, None], f[..., None].expand(-1, -1, -1, 4), self.obs)
+
+    def step(self, actions):
+        a = actions.long().to(self.device)
+        a = torch.where((a >= self.num_actions) | (a < 0), torch.zeros_like(a), a)   # game_state.py:38-39
+        reward = torch.zeros(self.num_envs, dtype=torch.int64, device=self.device)
+        for _ in range(self.frameskip):
+            reward += self.physics(a)
+        self.counter += 1
+        self.steps += 1
+        self.epret += reward
+        done = self.game_over() | (self.steps >= self.max_episode_steps)
+        ep_return = torch.where(done, self.epret, torch.zeros_like(self.epret)).float()
+        self.reset_state(done)
+        self.steps = torch.where(done, torch.zeros_like(self.steps), self.steps)
+        self.epret = torch.where(done, torch.zeros_like(self.epret), self.epret)
+        self.counter += done.long()
+        f = self.frame()
+        pushed = torch.cat([self.obs[..., 1:], f[..., None]], dim=3)
+        self.obs = torch.where(done[:, None, None, None], f[..., None].expand(-1, -1, -1, 4), pushed)
+        return self.obs.clone(), reward.float(), done, {"episode_return": ep_return}
+
+    def step_into(self, actions, obs_in, obs_out, reward, done, epret):
+        """Engine hook: step and write into the rollout buffers (eager torch ops)."""
+        o, r, d, info = self.step(actions)
+        obs_out.copy_(o.reshape(obs_out.shape))
+        reward.copy_(r)
+        done.copy_(d.to(done.dtype))
+        epret.copy_(info["episode_return"])
+
+
+# ===========================================================================
+class BreakoutVec(PixelGameVec):
+    id = "Breakout"
+    n_actions = 4
+    reward_threshold = 30.0
+    U = 16
+    ROWS, COLS = 6, 18
+    BRICK_Y0, BRICK_H, BRICK_W, BRICK_X0 = 57, 6, 8, 8
+    ROW_REWARD = (7, 7, 4, 4, 1, 1)
+    ROW_COLOR = ((200, 72, 72), (198, 108, 58), (180, 122, 48), (162, 162, 42), (72, 160, 72), (66, 72, 200))
+    PADDLE_Y, PADDLE_W = 189, 16
+
+    def init_state(self):
+        N = self.num_envs
+        d = self.device
+        self.bricks = torch.ones(N, self.ROWS, self.COLS, dtype=torch.bool, device=d)
+        self.px = torch.zeros(N, dtype=torch.int64, device=d)
+        self.bx = torch.zeros(N, dtype=torch.int64, device=d)
+        self.by = torch.zeros(N, dtype=torch.int64, device=d)
+        self.vx = torch.zeros(N, dtype=torch.int64, device=d)
+        self.vy = torch.zeros(N, dtype=torch.int64, device=d)
+        self.inplay = torch.zeros(N, dtype=torch.bool, device=d)
+        self.lives = torch.zeros(N, dtype=torch.int64, device=d)
+        self.rew = torch.tensor(self.ROW_REWARD, dtype=torch.int64, device=d)
+
+    def reset_state(self, m):
+        self.bricks = torch.where(m[:, None, None], torch.ones_like(self.bricks), self.bricks)
+        self.px = self.where_set(self.px, m, 72 * self.U)
+        self.inplay = torch.where(m, torch.zeros_like(self.inplay), self.inplay)
+        self.lives = self.where_set(self.lives, m, 5)
+
+    def physics(self, a):
+        U = self.U
+        right = (a == 2).long()
+        left = (a == 3).long()
+        self.px = (self.px + (right - left) * 6 * U).clamp(8 * U, (152 - self.PADDLE_W) * U)
+        serve = (~self.inplay) & (a == 1)
+        dirn = torch.where(self.rand(0, 2) == 0, -1, 1)
+        self.bx = torch.where(serve, self.px + (self.PADDLE_W // 2) * U, self.bx)
+        self.by = self.where_set(self.by, serve, 120 * U)
+        self.vx = torch.where(serve, dirn * (24 + self.rand(1, 12)), self.vx)
+        self.vy = self.where_set(self.vy, serve, 40)
+        self.inplay = self.inplay | serve
+        nx, ny = self.bx + self.vx, self.by + self.vy
+        hitx = (nx < 8 * U) | (nx > 150 * U)
+        self.vx = torch.where(hitx & self.inplay, -self.vx, self.vx)
+        nx = nx.clamp(8 * U, 150 * U)
+        hit_top = ny < 32 * U
+        self.vy = torch.where(hit_top & self.inplay, self.vy.abs(), self.vy)
+        ny = torch.where(hit_top, 32 * U, ny)
+        # bricks
+        cy = torch.div(ny // U - self.BRICK_Y0, self.BRICK_H, rounding_mode="floor")
+        cx = torch.div(nx // U - self.BRICK_X0, self.BRICK_W, rounding_mode="floor")
+        inb = (cy >= 0) & (cy < self.ROWS) & (cx >= 0) & (cx < self.COLS) & self.inplay
+        cyc, cxc = cy.clamp(0, self.ROWS - 1), cx.clamp(0, self.COLS - 1)
+        b = self.bricks[torch.arange(self.num_envs, device=self.device), cyc, cxc]
+        hitb = inb & b
+        reward = torch.where(hitb, self.rew[cyc], torch.zeros_like(cy))
+        self.bricks[torch.arange(self.num_envs, device=self.device), cyc, cxc] = b & ~hitb
+        self.vy = torch.where(hitb, -self.vy, self.vy)
+        # paddle
+        onp = (self.vy > 0) & (ny // U >= self.PADDLE_Y - 4) & (ny // U < self.PADDLE_Y + 2) & \
+              (nx >= self.px - 2 * U) & (nx <= self.px + (self.PADDLE_W + 2) * U)
+        off = (nx - (self.px + (self.PADDLE_W // 2) * U))
+        self.vx = torch.where(onp & self.inplay, (off * 3 // 16).clamp(-48, 48), self.vx)
+        self.vy = torch.where(onp & self.inplay, -self.vy.abs(), self.vy)
+        lost = self.inplay & (ny > 200 * U)
+        self.lives = self.lives - lost.long()
+        self.inplay = self.inplay & ~lost
+        self.bx = torch.where(self.inplay, nx, self.bx)
+        self.by = torch.where(self.inplay, ny, self.by)
+        return reward
+
+    def game_over(self):
+        return (self.lives <= 0) | (~self.bricks.view(self.num_envs, -1).any(1))
+
+    def draw(self, img):
+        gray = self.color((142, 142, 142))
+        img[:, 17:32, :] = gray
+        img[:, 17:196, 0:8] = gray
+        img[:, 17:196, 152:160] = gray
+        for r in range(self.ROWS):
+            y0 = self.BRICK_Y0 + r * self.BRICK_H
+            cols = self.bricks[:, r].repeat_interleave(self.BRICK_W, 1)           # [N, 144]
+            m = torch.zeros(self.num_envs, SCREEN_H, SCREEN_W, dtype=torch.bool, device=self.device)
+            m[:, y0:y0 + self.BRICK_H, self.BRICK_X0:self.BRICK_X0 + self.COLS * self.BRICK_W] = cols[:, None, :]
+            img[m] = self.color(self.ROW_COLOR[r])
+        red = self.color((200, 72, 72))
+        img[self.rect(self.PADDLE_Y, self.px // self.U, 4, self.PADDLE_W)] = red
+        img[self.rect(self.by // self.U, self.bx // self.U, 4, 2) & self.inplay[:, None, None]] = red
+
+
+# ===========================================================================
+class SpaceInvadersVec(PixelGameVec):
+    id = "SpaceInvaders"
+    n_actions = 6
+    reward_threshold = 300.0
+    AR, AC = 6, 6
+    ROW_REWARD = (30, 25, 20, 15, 10, 5)
+
+    def init_state(self):
+        N, d = self.num_envs, self.device
+        z = lambda: torch.zeros(N, dtype=torch.int64, device=d)
+        self.alive = torch.ones(N, self.AR, self.AC, dtype=torch.bool, device=d)
+        self.fx, self.fy, self.fdir, self.tick = z(), z(), z(), z()
+        self.px, self.lives = z(), z()
+        self.sx, self.sy = z(), z()
+        self.shot = torch.zeros(N, dtype=torch.bool, device=d)
+        self.bxp, self.byp = z(), z()
+        self.bomb = torch.zeros(N, dtype=torch.bool, device=d)
+        self.rew = torch.tensor(self.ROW_REWARD, dtype=torch.int64, device=d)
+
+    def reset_state(self, m):
+        self.alive = torch.where(m[:, None, None], torch.ones_like(self.alive), self.alive)
+        for name, v in (("fx", 22), ("fy", 40), ("fdir", 1), ("tick", 0), ("px", 76), ("lives", 3)):
+            setattr(self, name, self.where_set(getattr(self, name), m, v))
+        self.shot = self.shot & ~m
+        self.bomb = self.bomb & ~m
+
+    def physics(self, a):
+        N, d = self.num_envs, self.device
+        ar = torch.arange(N, device=d)
+        right = ((a == 2) | (a == 4)).long()
+        left = ((a == 3) | (a == 5)).long()
+        fire = (a == 1) | (a == 4) | (a == 5)
+        self.px = (self.px + 2 * (right - left)).clamp(20, 133)
+        new_shot = fire & ~self.shot
+        self.sx = torch.where(new_shot, self.px + 3, self.sx)
+        self.sy = torch.where(new_shot, torch.full_like(self.sy, 182), self.sy)
+        self.shot = self.shot | new_shot
+        self.sy = self.sy - 4 * self.shot.long()
+        self.shot = self.shot & (self.sy > 20)
+        # formation march every 4 sub-frames
+        self.tick += 1
+        move = (self.tick % 4) == 0
+        alive_cols = self.alive.any(1)                                        # [N, AC]
+        ci = torch.arange(self.AC, device=d)
+        leftmost = torch.where(alive_cols, ci, self.AC).min(1).values
+        rightmost = torch.where(alive_cols, ci, -1).max(1).values
+        xl = self.fx + 16 * leftmost
+        xr = self.fx + 16 * rightmost + 8
+        edge = move & (((self.fdir > 0) & (xr >= 150)) | ((self.fdir < 0) & (xl <= 10)))
+        self.fdir = torch.where(edge, -self.fdir, self.fdir)
+        self.fy = self.fy + 4 * edge.long()
+        self.fx = self.fx + torch.where(move & ~edge, self.fdir, torch.zeros_like(self.fx))
+        # shot vs aliens
+        col = torch.div(self.sx - self.fx, 16, rounding_mode="floor")
+        row = torch.div(self.sy - self.fy, 18, rounding_mode="floor")
+        inx = ((self.sx - self.fx) % 16) < 8
+        iny = ((self.sy - self.fy) % 18) < 10
+        ok = self.shot & (col >= 0) & (col < self.AC) & (row >= 0) & (row < self.AR) & inx & iny
+        colc, rowc = col.clamp(0, self.AC - 1), row.clamp(0, self.AR - 1)
+        hit = ok & self.alive[ar, rowc, colc]
+        self.alive[ar, rowc, colc] = self.alive[ar, rowc, colc] & ~hit
+        reward = torch.where(hit, self.rew[rowc], torch.zeros_like(self.px))
+        self.shot = self.shot & ~hit
+        # alien bomb
+        drop = ~self.bomb & (self.rand(4, 64) == 0) & alive_cols.any(1)
+        bc = self.rand(5, self.AC)
+        has = alive_cols[ar, bc]
+        lowest = torch.where(self.alive[ar, :, bc], torch.arange(self.AR, device=d)[None], -1).max(1).values
+        drop = drop & has
+        self.bxp = torch.where(drop, self.fx + 16 * bc + 4, self.bxp)
+        self.byp = torch.where(drop, self.fy + 18 * lowest + 10, self.byp)
+        self.bomb = self.bomb | drop
+        self.byp = self.byp + 2 * self.bomb.long()
+        hitp = self.bomb & (self.byp >= 185) & (self.byp < 193) & (self.bxp >= self.px) & (self.bxp < self.px + 7)
+        self.lives = self.lives - hitp.long()
+        self.bomb = self.bomb & ~hitp & (self.byp < 196)
+        return reward
+
+    def game_over(self):
+        lowest_row = torch.where(self.alive.any(2), torch.arange(self.AR, device=self.device)[None], -1).max(1).values
+        invaded = (self.fy + 18 * lowest_row + 10) >= 180
+        return (self.lives <= 0) | (~self.alive.view(self.num_envs, -1).any(1)) | invaded
+
+    def draw(self, img):
+        N = self.num_envs
+        img[:, 195:197, :] = self.color((80, 89, 22))
+        green = self.color((50, 132, 50))
+        for r in range(self.AR):
+            for c in range(self.AC):
+                m = self.rect(self.fy + 18 * r, self.fx + 16 * c, 10, 8) & self.alive[:, r, c][:, None, None]
+                img[m] = self.color((134, 134, 29)) if r % 2 else green
+        img[self.rect(185, self.px, 8, 7)] = self.color((50, 132, 50))
+        img[self.rect(self.sy, self.sx, 6, 1) & self.shot[:, None, None]] = self.color((142, 142, 142))
+        img[self.rect(self.byp, self.bxp, 6, 1) & self.bomb[:, None, None]] = self.color((200, 200, 200))
+
+
+# ===========================================================================
+MAZE = [
+    "#############",
+    "#.....#.....#",
+    "#.###.#.###.#",
+    "#...........#",
+    "#.#.#####.#.#",
+    "#.#...#...#.#",
+    "#.###.#.###.#",
+    "#...........#",
+    "#.###.#.###.#",
+    "#.....#.....#",
+    "#############",
+]
+
+
+class AlienVec(PixelGameVec):
+    """Maze game: eggs + 3 chasing aliens (Alien: 18 actions; MsPacman: 9 actions)."""
+    id = "Alien"
+    n_actions = 18
+    reward_threshold = 400.0
+    CW, CH, Y0, X0 = 12, 16, 20, 2
+    NA = 3
+    MOVE_EVERY = 2
+
+    def init_state(self):
+        N, d = self.num_envs, self.device
+        walls = torch.tensor([[ch == "#" for ch in row] for row in MAZE], device=d)
+        self.walls = walls
+        self.H, self.W = walls.shape
+        self.dots = torch.zeros(N, self.H, self.W, dtype=torch.bool, device=d)
+        self.py, self.px = torch.zeros(N, dtype=torch.int64, device=d), torch.zeros(N, dtype=torch.int64, device=d)
+        self.ay = torch.zeros(N, self.NA, dtype=torch.int64, device=d)
+        self.ax = torch.zeros(N, self.NA, dtype=torch.int64, device=d)
+        self.lives = torch.zeros(N, dtype=torch.int64, device=d)
+        self.tick = torch.zeros(N, dtype=torch.int64, device=d)
+        self.dy = torch.tensor([0, -1, 0, 0, 1], device=d)      # none, up, right, left, down
+        self.dx = torch.tensor([0, 0, 1, -1, 0], device=d)
+        # action -> direction index (ALE: 2 UP 3 RIGHT 4 LEFT 5 DOWN; diagonals/fire variants fold onto them)
+        amap = [0, 0, 1, 2, 3, 4, 1, 1, 4, 4, 1, 2, 3, 4, 1, 1, 4, 4]
+        self.amap = torch.tensor(amap[: self.n_actions], device=d)
+        self.start_a = torch.tensor([[1, 1], [1, 11], [9, 6]], device=d)
+
+    def reset_state(self, m):
+        self.dots = torch.where(m[:, None, None], (~self.walls)[None].expand_as(self.dots), self.dots)
+        self.py = self.where_set(self.py, m, 7)
+        self.px = self.where_set(self.px, m, 6)
+        self.dots[:, 7, 6] &= ~m
+        self.ay = torch.where(m[:, None], self.start_a[:, 0][None].expand_as(self.ay), self.ay)
+        self.ax = torch.where(m[:, None], self.start_a[:, 1][None].expand_as(self.ax), self.ax)
+        self.lives = self.where_set(self.lives, m, 3)
+        self.tick = self.where_set(self.tick, m, 0)
+
+    def _free(self, y, x):
+        return ~self.walls[y.clamp(0, self.H - 1), x.clamp(0, self.W - 1)]
+
+    def physics(self, a):
+        N, d = self.num_envs, self.device
+        ar = torch.arange(N, device=d)
+        self.tick += 1
+        step_now = (self.tick % self.MOVE_EVERY) == 0
+        di = self.amap[a]
+        ny, nx = self.py + self.dy[di], self.px + self.dx[di]
+        ok = step_now & self._free(ny, nx)
+        self.py = torch.where(ok, ny, self.py)
+        self.px = torch.where(ok, nx, self.px)
+        eat = self.dots[ar, self.py, self.px]
+        self.dots[ar, self.py, self.px] = False
+        reward = eat.long() * 10
+        # aliens: every other move, step towards the player (random tie-break / 25% random move)
+        amove = (self.tick % (2 * self.MOVE_EVERY)) == 0
+        for k in range(self.NA):
+            y, x = self.ay[:, k], self.ax[:, k]
+            best_y, best_x = y.clone(), x.clone()
+            best_d = torch.full_like(y, 1 << 20)
+            r = self.rand(6 + k, 4)
+            for j in range(1, 5):
+                cy, cx = y + self.dy[j], x + self.dx[j]
+                free = self._free(cy, cx)
+                dist = (cy - self.py).abs() + (cx - self.px).abs()
+                dist = torch.where(r == (j - 1), dist - 2, dist)          # a little randomness
+                better = free & (dist < best_d)
+                best_y = torch.where(better, cy, best_y)
+                best_x = torch.where(better, cx, best_x)
+                best_d = torch.where(better, dist, best_d)
+            self.ay[:, k] = torch.where(amove, best_y, y)
+            self.ax[:, k] = torch.where(amove, best_x, x)
+        caught = ((self.ay == self.py[:, None]) & (self.ax == self.px[:, None])).any(1)
+        self.lives = self.lives - caught.long()
+        # respawn aliens on a catch
+        self.ay = torch.where(caught[:, None], self.start_a[:, 0][None].expand_as(self.ay), self.ay)
+        self.ax = torch.where(caught[:, None], self.start_a[:, 1][None].expand_as(self.ax), self.ax)
+        cleared = ~self.dots.view(N, -1).any(1)
+        reward = reward + cleared.long() * 500
+        return reward
+
+    def game_over(self):
+        return (self.lives <= 0) | (~self.dots.view(self.num_envs, -1).any(1))
+
+    def draw(self, img):
+        wall = self.color((84, 92, 214))
+        for y in range(self.H):
+            for x in range(self.W):
+                if MAZE[y][x] == "#":
+                    img[:, self.Y0 + y * self.CH:self.Y0 + (y + 1) * self.CH, self.X0 + x * self.CW:self.X0 + (x + 1) * self.CW] = wall
+        # eggs: 2x2 pixels at cell centres
+        m = torch.zeros(self.num_envs, SCREEN_H, SCREEN_W, dtype=torch.bool, device=self.device)
+        cy = self.Y0 + torch.arange(self.H, device=self.device) * self.CH + self.CH // 2
+        cx = self.X0 + torch.arange(self.W, device=self.device) * self.CW + self.CW // 2
+        for oy in (0, 1):
+            for ox in (0, 1):
+                m[:, (cy + oy)[:, None], (cx + ox)[None, :]] = self.dots
+        img[m] = self.color((223, 183, 85))
+        img[self.rect(self.Y0 + self.py * self.CH + 3, self.X0 + self.px * self.CW + 3, 10, 6)] = self.color((132, 144, 252))
+        for k in range(self.NA):
+            img[self.rect(self.Y0 + self.ay[:, k] * self.CH + 2, self.X0 + self.ax[:, k] * self.CW + 2, 12, 8)] = \
+                self.color((252, 144, 144))
+
+
+class MsPacmanVec(AlienVec):
+    id = "MsPacman"
+    n_actions = 9
+    reward_threshold = 500.0
+
+
+# ===========================================================================
+class CentipedeVec(PixelGameVec):
+    id = "Centipede"
+    n_actions = 18
+    reward_threshold = 3000.0
+    NS = 10
+    GH, GW = 20, 16          # mushroom grid (8 px rows x 10 px cols in the field rows 20..180)
+
+    def init_state(self):
+        N, d = self.num_envs, self.device
+        self.mush = torch.zeros(N, self.GH, self.GW, dtype=torch.bool, device=d)
+        self.sy = torch.zeros(N, self.NS, dtype=torch.int64, device=d)     # segment grid row
+        self.sx = torch.zeros(N, self.NS, dtype=torch.int64, device=d)     # segment grid col
+        self.sdir = torch.zeros(N, self.NS, dtype=torch.int64, device=d)
+        self.salive = torch.zeros(N, self.NS, dtype=torch.bool, device=d)
+        self.px = torch.zeros(N, dtype=torch.int64, device=d)
+        self.shot = torch.zeros(N, dtype=torch.bool, device=d)
+        self.shx = torch.zeros(N, dtype=torch.int64, device=d)
+        self.shy = torch.zeros(N, dtype=torch.int64, device=d)
+        self.lives = torch.zeros(N, dtype=torch.int64, device=d)
+        self.tick = torch.zeros(N, dtype=torch.int64, device=d)
+        self.amap_h = torch.tensor([0, 0, 0, 1, -1, 0, 1, -1, 1, -1, 0, 0, 1, -1, 0, 1, -1, 1, -1][:18], device=d)
+        self.afire = torch.tensor([0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1], device=d).bool()
+
+    def reset_state(self, m):
+        N = self.num_envs
+        r = torch.stack([self.rand(10 + k, 100) for k in range(self.GH * self.GW // 16)], 1)     # sparse field
+        field = torch.zeros(N, self.GH * self.GW, dtype=torch.bool, device=self.device)
+        pos = (torch.arange(r.shape[1], device=self.device)[None] * 16 + r % 16).clamp(max=self.GH * self.GW - 1)
+        field.scatter_(1, pos, (r < 60))
+        field = field.view(N, self.GH, self.GW)
+        field[:, self.GH - 3:] = False
+        self.mush = torch.where(m[:, None, None], field, self.mush)
+        k = torch.arange(self.NS, device=self.device)[None]
+        self.sy = torch.where(m[:, None], torch.zeros_like(self.sy), self.sy)
+        self.sx = torch.where(m[:, None], (self.GW - 1 - k).expand_as(self.sx).clamp(min=0), self.sx)
+        self.sdir = torch.where(m[:, None], -torch.ones_like(self.sdir), self.sdir)
+        self.salive = torch.where(m[:, None], torch.ones_like(self.salive), self.salive)
+        self.px = self.where_set(self.px, m, 76)
+        self.shot = self.shot & ~m
+        self.lives = self.where_set(self.lives, m, 3)
+        self.tick = self.where_set(self.tick, m, 0)
+
+    def physics(self, a):
+        N, d = self.num_envs, self.device
+        ar = torch.arange(N, device=d)
+        self.px = (self.px + 2 * self.amap_h[a]).clamp(4, 152)
+        fire = self.afire[a] & ~self.shot
+        self.shx = torch.where(fire, self.px + 2, self.shx)
+        self.shy = torch.where(fire, torch.full_like(self.shy, 180), self.shy)
+        self.shot = self.shot | fire
+        self.shy = self.shy - 6 * self.shot.long()
+        self.shot = self.shot & (self.shy > 20)
+        gy = torch.div(self.shy - 20, 8, rounding_mode="floor").clamp(0, self.GH - 1)
+        gx = torch.div(self.shx, 10, rounding_mode="floor").clamp(0, self.GW - 1)
+        reward = torch.zeros(N, dtype=torch.int64, device=d)
+        hm = self.shot & self.mush[ar, gy, gx]
+        self.mush[ar, gy, gx] = self.mush[ar, gy, gx] & ~hm
+        reward += hm.long()
+        self.shot = self.shot & ~hm
+        hs = self.shot[:, None] & self.salive & (self.sy == gy[:, None]) & (self.sx == gx[:, None])
+        anyhs = hs.any(1)
+        reward += 10 * hs.sum(1)
+        self.salive = self.salive & ~hs
+        # a hit segment leaves a mushroom
+        self.mush[ar, gy, gx] = self.mush[ar, gy, gx] | anyhs
+        self.shot = self.shot & ~anyhs
+        # centipede moves every 3 sub-frames
+        self.tick += 1
+        mv = ((self.tick % 3) == 0)[:, None] & self.salive
+        nx = self.sx + self.sdir
+        blocked = (nx < 0) | (nx >= self.GW)
+        nxc = nx.clamp(0, self.GW - 1)
+        blocked = blocked | self.mush[ar[:, None], self.sy, nxc]
+        self.sy = torch.where(mv & blocked, (self.sy + 1).clamp(max=self.GH - 1), self.sy)
+        self.sdir = torch.where(mv & blocked, -self.sdir, self.sdir)
+        self.sx = torch.where(mv & ~blocked, nx, self.sx)
+        reach = (self.salive & (self.sy >= self.GH - 1)).any(1)
+        self.lives = self.lives - reach.long()
+        k = torch.arange(self.NS, device=d)[None]
+        self.sy = torch.where(reach[:, None], torch.zeros_like(self.sy), self.sy)
+        self.sx = torch.where(reach[:, None], (self.GW - 1 - k).expand_as(self.sx).clamp(min=0), self.sx)
+        self.sdir = torch.where(reach[:, None], -torch.ones_like(self.sdir), self.sdir)
+        # wave cleared -> new centipede
+        cleared = ~self.salive.any(1)
+        self.salive = self.salive | cleared[:, None]
+        self.sy = torch.where(cleared[:, None], torch.zeros_like(self.sy), self.sy)
+        return reward
+
+    def game_over(self):
+        return self.lives <= 0
+
+    def draw(self, img):
+        m = self.mush.repeat_interleave(8, 1).repeat_interleave(10, 2)          # [N,160,160]
+        img[:, 20:180, :][m] = self.color((181, 83, 40))
+        for k in range(self.NS):
+            mm = self.rect(20 + self.sy[:, k] * 8 + 1, self.sx[:, k] * 10 + 1, 6, 8) & self.salive[:, k][:, None, None]
+            img[mm] = self.color((184, 70, 162))
+        img[self.rect(184, self.px, 8, 4)] = self.color((181, 108, 224))
+        img[self.rect(self.shy, self.shx, 6, 1) & self.shot[:, None, None]] = self.color((181, 108, 224))
+
+
+GAMES = {"Breakout": BreakoutVec, "SpaceInvaders": SpaceInvadersVec, "Alien": AlienVec, "MsPacman": MsPacmanVec,
+         "Centipede": CentipedeVec}
+
+
+def make_game(name: str, **kw) -> PixelGameVec:
+    return GAMES[name](**kw)

@@ -44,8 +44,14 @@ class DistContext:
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if not self.enabled:
             return t.clone()
-        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous())
+        flat = t.contiguous().reshape(-1)
+        out = torch.empty(self.world * flat.numel(), dtype=t.dtype, device=t.device)
+        if self.backend == "gloo":
+            parts = list(out.chunk(self.world))
+            dist.all_gather(parts, flat)
+            out = torch.cat(parts)
+        else:
+            dist.all_gather_into_tensor(out, flat)
         return out.reshape((self.world * t.shape[0],) + tuple(t.shape[1:]))
 
     def broadcast_(self, t: torch.Tensor, src: int = 0):

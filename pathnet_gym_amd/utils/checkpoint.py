@@ -1,0 +1,199 @@
+"""Checkpoint / resume.
+
+The reference's ``tf.train.Saver()`` (``doom_pathnet.py:157``) saves every
+global variable: weights, RMSProp slots, genotype masks, flag, global_step,
+scores and the frozen path.  It does NOT save the
+coordinator's evolvable genotypes, tournament sample, RNG or env state, so a
+resume is never exact (and never happens, because ``main`` appends a fresh
+timestamp to log_dir, ``doom_pathnet.py:300``).
+
+This checkpoint stores the same logical tensors under stable names PLUS the
+state the reference loses, so resume is bit-exact on the same backend:
+
+* ``layer{i}.module{j}.weight|bias``, ``policy.weight`` ..., ``lstm.kernel``
+  (TF layouts: conv [kh,kw,cin,cout], fc [din,dout])
+* ``<name>/RMSProp`` (ms, init 1.0) and ``<name>/RMSProp_1`` (momentum):
+  TF slot naming
+* ``ga.*``: genotype table [P,L,M] uint8, frozen mask, fitness, candidate
+  sets, generation, MT19937 state
+* ``train.*``: global_step, task index (``flag`` = task+1), update count
+* per rank ``env.*`` / ``engine.*``: env state, frame stack, LSTM state,
+  sampling counter (file ``<path>.rank<r>.safetensors``)
+
+Format: safetensors (no pickle; loaders never execute file content).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+from safetensors.torch import load_file, save_file
+
+FORMAT_VERSION = 1
+
+
+def _t(x) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().contiguous()
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
+
+
+def state_tensors(trainer) -> Dict[str, torch.Tensor]:
+    st = trainer.model.store
+    out: Dict[str, torch.Tensor] = {}
+    for s in st.layout.segments:
+        out[s.name] = _t(st.flat[s.offset:s.offset + s.numel].view(s.shape))
+        out[s.name + "/RMSProp"] = _t(trainer.opt.ms[s.offset:s.offset + s.numel].view(s.shape))
+        out[s.name + "/RMSProp_1"] = _t(trainer.opt.mom[s.offset:s.offset + s.numel].view(s.shape))
+    out["optim.seg_trainable"] = _t(trainer.opt.seg_trainable.to(torch.uint8))
+    out["init_flat"] = _t(trainer.init_flat)
+    for k, v in trainer.pop.state_dict().items():
+        out["ga." + k] = _t(v)
+    out["train.global_step"] = torch.tensor([trainer.global_step], dtype=torch.int64)
+    out["train.task_idx"] = torch.tensor([trainer.task_idx], dtype=torch.int64)
+    out["train.flag"] = torch.tensor([trainer.task_idx + 1], dtype=torch.int64)
+    out["train.updates"] = torch.tensor([trainer.updates], dtype=torch.int64)
+    out["train.task_start_step"] = torch.tensor([trainer.task_start_step], dtype=torch.int64)
+    out["train.task_gen0"] = torch.tensor([trainer._task_gen0], dtype=torch.int64)
+    return out
+
+
+def rank_tensors(trainer) -> Dict[str, torch.Tensor]:
+    env = trainer.env
+    out: Dict[str, torch.Tensor] = {}
+    if hasattr(env, "_st32"):          # HIP pong: kernel-side state is authoritative
+        from ..ops import envs as henv
+        henv.pong_sync_from_device(env)
+    if hasattr(env, "_steps32"):
+        env.steps = env._steps32.long()
+        env.counter = env._ctr32.long() & 0xFFFFFFFF
+    for name in ("state", "counter", "steps", "ep_ret", "obs"):
+        if hasattr(env, name) and isinstance(getattr(env, name), torch.Tensor):
+            out["env." + name] = _t(getattr(env, name))
+    out["env.seed"] = torch.tensor([env.seed_int], dtype=torch.int64)
+    if trainer.engine is not None:
+        eng = trainer.engine
+        out["engine.ctr"] = _t(eng.ctr)
+        out["engine.obs0"] = _t(eng.obs[0])
+        out["engine.fitness"] = _t(eng.fitness)
+    else:
+        out["train.obs"] = _t(trainer.obs)
+        out["train.fitness_local"] = _t(trainer.fitness_local)
+    if trainer.lstm_state is not None:
+        out["lstm.h"] = _t(trainer.lstm_state[0])
+        out["lstm.c"] = _t(trainer.lstm_state[1])
+    return out
+
+
+def save(trainer, path: str) -> str:
+    """Write ``path`` (rank-0 global state) and ``path.rank<r>.safetensors`` (every rank)."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+    meta = {"format_version": str(FORMAT_VERSION), "config": trainer.cfg.to_json(),
+            "world": str(trainer.ctx.world), "segments": json.dumps([s.name for s in trainer.model.store.layout.segments])}
+    if trainer.ctx.is_main:
+        save_file(state_tensors(trainer), path, metadata=meta)
+    save_file(rank_tensors(trainer), f"{path}.rank{trainer.ctx.rank}.safetensors", metadata=meta)
+    return path
+
+
+def load(trainer, path: str, strict: bool = True):
+    """Restore a trainer built with the same config (resume)."""
+    d = load_file(path)
+    st = trainer.model.store
+    dev = st.flat.device
+    with torch.no_grad():
+        for s in st.layout.segments:
+            if s.name not in d:
+                if strict:
+                    raise KeyError(f"checkpoint misses {s.name}")
+                continue
+            st.flat[s.offset:s.offset + s.numel].copy_(d[s.name].reshape(-1).to(dev))
+            trainer.opt.ms[s.offset:s.offset + s.numel].copy_(d[s.name + "/RMSProp"].reshape(-1).to(dev))
+            trainer.opt.mom[s.offset:s.offset + s.numel].copy_(d[s.name + "/RMSProp_1"].reshape(-1).to(dev))
+        trainer.opt.seg_trainable.copy_(d["optim.seg_trainable"].bool().to(dev))
+        trainer.init_flat.copy_(d["init_flat"].to(dev))
+    ga = {k[3:]: v.numpy() for k, v in d.items() if k.startswith("ga.")}
+    trainer.pop.load_state_dict(ga)
+    task = int(d["train.task_idx"][0])
+    if task != trainer.task_idx:
+        trainer._start_task(task, fresh=True)
+    trainer.global_step = int(d["train.global_step"][0])
+    trainer.updates = int(d["train.updates"][0])
+    trainer.task_start_step = int(d["train.task_start_step"][0])
+    trainer._task_gen0 = int(d["train.task_gen0"][0])
+    frozen = trainer.pop.frozen
+    trainer.model.set_frozen(frozen)
+    trainer._push_genotypes()
+    rp = f"{path}.rank{trainer.ctx.rank}.safetensors"
+    if os.path.exists(rp):
+        r = load_file(rp)
+        env = trainer.env
+        for name in ("state", "counter", "steps", "ep_ret", "obs"):
+            if "env." + name in r and hasattr(env, name):
+                setattr(env, name, r["env." + name].to(getattr(env, name).device))
+        if hasattr(env, "_st32"):
+            from ..ops import envs as henv
+            henv.pong_sync_to_device(env)
+        if hasattr(env, "_steps32"):
+            from ..ops import envs as henv
+            henv.cartpole_sync_to_device(env)
+        if trainer.engine is not None:
+            eng = trainer.engine
+            eng.ctr.copy_(r["engine.ctr"].to(dev))
+            eng.obs[0].copy_(r["engine.obs0"].to(dev))
+            eng.fitness.copy_(r["engine.fitness"].to(dev))
+            eng.refresh_trainable()
+        else:
+            trainer.obs = r["train.obs"].to(dev)
+            trainer.fitness_local = r["train.fitness_local"].to(dev)
+        if "lstm.h" in r:
+            trainer.lstm_state = (r["lstm.h"].to(dev), r["lstm.c"].to(dev))
+    if trainer.backend == "hip":
+        trainer.model.hip.refresh_weights()
+    return trainer
+
+
+def read_metadata(path: str) -> dict:
+    from safetensors import safe_open
+    with safe_open(path, framework="pt") as f:
+        return dict(f.metadata() or {})
+
+
+# ---------------------------------------------------------------------------
+# TF1 creation-order importer
+# ---------------------------------------------------------------------------
+def tf_creation_order(cfg) -> List[str]:
+    """Names of the reference's trainable tensors in tf.Variable creation order.
+
+    conv W/b per (layer, module) i-major j-minor, then lin W/b per module,
+    fc2 (policy), fc3 (value), then the LSTM kernel/bias
+    (game_ac_network.py:328-347,397; LSTM variables are created last).
+    """
+    from ..models.pathnet import ParamLayout
+    lay = ParamLayout(cfg)
+    names = []
+    for l in range(cfg.L):
+        for j in range(cfg.M):
+            names += [f"layer{l}.module{j}.weight", f"layer{l}.module{j}.bias"]
+    names += ["policy.weight", "policy.bias", "value.weight", "value.bias"]
+    if cfg.use_lstm:
+        names += ["lstm.kernel", "lstm.bias"]
+    assert set(names) <= set(lay.by_name)
+    return names
+
+
+def import_tf_arrays(store, arrays: List[np.ndarray]):
+    """Load reference weights given as numpy arrays in TF creation order."""
+    names = tf_creation_order(store.cfg)
+    if len(arrays) != len(names):
+        raise ValueError(f"expected {len(names)} arrays, got {len(arrays)}")
+    with torch.no_grad():
+        for n, a in zip(names, arrays):
+            s = store.layout.by_name[n]
+            a = np.asarray(a, np.float32)
+            if a.size != s.numel:
+                raise ValueError(f"{n}: size {a.size} != {s.numel}")
+            store.flat[s.offset:s.offset + s.numel].copy_(torch.from_numpy(a.reshape(-1)))

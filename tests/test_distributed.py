@@ -1,0 +1,87 @@
+"""Multi-process (gloo, world_size 2) tests: the fused all-reduce and replicated GA.
+
+Each rank runs its own PathNetTrainer (CPU, torch backend) on its half of the
+population.  After every update all ranks must hold bit-identical weights,
+optimizer slots and GA state, and the all-reduced gradient must equal the
+sum of the per-rank gradients.  Uses 127.0.0.1 rendezvous.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    try:
+        from pathnet_gym_amd.algo.trainer import PathNetTrainer
+        from pathnet_gym_amd.config import preset
+        from pathnet_gym_amd.parallel.dist import init_distributed
+        ctx = init_distributed(device="cpu", backend="gloo")
+        cfg = preset("cartpole-cpu")
+        cfg.paths, cfg.envs_per_path = 3, 4
+        cfg.ga.B = 2
+        cfg.ga.concurrent_tournaments = 2
+        cfg.ga_sync = mode
+        tr = PathNetTrainer(cfg, ctx=ctx)
+        out = {}
+        if mode == "fused":
+            # all-reduced grad == sum of local grads
+            g, c, _ = tr.rollout_and_backward()
+            local = g.clone()
+            tot = torch.zeros_like(local)
+            dist.all_reduce(local.clone(), op=dist.ReduceOp.SUM)
+            gl = [torch.zeros_like(local) for _ in range(world)]
+            dist.all_gather(gl, local)
+            tot = sum(gl)
+            tr.comm.exchange(g, tr.fitness_local, c)
+            out["grad_ok"] = bool(torch.allclose(g, tot, atol=1e-5))
+        for _ in range(6):
+            tr.update()
+        out["flat"] = tr.model.store.flat.detach().numpy().copy()
+        out["ms"] = tr.opt.ms.numpy().copy()
+        out["geno"] = tr.pop.genotypes.copy()
+        out["gen"] = tr.pop.generation
+        out["step"] = tr.global_step
+        q.put((rank, out))
+        ctx.destroy()
+    except Exception as e:   # pragma: no cover
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("mode", ["fused", "gather_bcast"])
+def test_two_ranks_stay_in_lockstep(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r in range(2):
+        assert "error" not in res[r], res[r].get("error")
+    a, b = res[0], res[1]
+    assert np.array_equal(a["flat"], b["flat"])
+    assert np.array_equal(a["ms"], b["ms"])
+    assert np.array_equal(a["geno"], b["geno"])
+    assert a["gen"] == b["gen"] and a["step"] == b["step"]
+    assert a["step"] == 6 * 2 * 3 * 4 * 5
+    if mode == "fused":
+        assert a["grad_ok"] and b["grad_ok"]

@@ -1,0 +1,126 @@
+"""On-device env semantics (CPU torch implementations; HIP parity is in test_hip_kernels.py)."""
+import math
+
+import numpy as np
+import torch
+
+from pathnet_gym_amd.envs import pong as pg
+from pathnet_gym_amd.envs.cartpole import CartPoleVec
+from pathnet_gym_amd.envs.game_state import GameState, preprocess_numpy
+from pathnet_gym_amd.envs.registry import make, registered, reward_threshold
+
+
+def test_registry():
+    ids = registered()
+    for i in ("CartPole-v1", "Pong", "Pong-v0", "Breakout", "SpaceInvaders", "Alien"):
+        assert i in ids
+    assert reward_threshold("CartPole-v1") == 475.0
+
+
+def test_cartpole_one_step_matches_equations():
+    env = CartPoleVec(3, seed=0)
+    s0 = env.reset().clone()
+    obs, r, d, _ = env.step(torch.tensor([1, 0, 1]))
+    x, xd, th, thd = s0[0].tolist()
+    f = 10.0
+    temp = (f + 0.05 * thd * thd * math.sin(th)) / 1.1
+    thacc = (9.8 * math.sin(th) - math.cos(th) * temp) / (0.5 * (4 / 3 - 0.1 * math.cos(th) ** 2 / 1.1))
+    xacc = temp - 0.05 * thacc * math.cos(th) / 1.1
+    exp = [x + 0.02 * xd, xd + 0.02 * xacc, th + 0.02 * thd, thd + 0.02 * thacc]
+    assert np.allclose(obs[0].tolist(), exp, atol=1e-6)
+    assert r.tolist() == [1.0, 1.0, 1.0] and not d.any()
+
+
+def test_cartpole_episode_ends_and_autoresets():
+    env = CartPoleVec(1, seed=1)
+    env.reset()
+    for t in range(1, 600):
+        obs, r, d, info = env.step(torch.tensor([1]))
+        if d[0]:
+            assert info["episode_return"][0] == t
+            assert float(obs.abs().max()) <= 0.05     # fresh episode
+            break
+    else:
+        raise AssertionError("episode never ended")
+
+
+def test_pong_determinism_and_rewards():
+    a = pg.PongVec(4, seed=5)
+    b = pg.PongVec(4, seed=5)
+    oa, ob = a.reset(), b.reset()
+    assert torch.equal(oa, ob)
+    g = torch.Generator().manual_seed(0)
+    tot = 0
+    for _ in range(300):
+        act = torch.randint(0, 6, (4,), generator=g)
+        oa, ra, da, _ = a.step(act)
+        ob, rb, db, _ = b.step(act)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb)
+        assert set(ra.unique().tolist()) <= {-1.0, 0.0, 1.0}
+        tot += int(ra.abs().sum())
+    assert tot > 0
+
+
+def test_pong_frame_stack_shifts_newest_last():
+    env = pg.PongVec(2, seed=3)
+    o0 = env.reset()
+    assert torch.equal(o0[..., 0], o0[..., 3])              # reset: first frame x4 (game_state.py:66)
+    o1, _, d, _ = env.step(torch.tensor([2, 3]))
+    assert torch.equal(o1[..., :3], o0[..., 1:])            # np.append(s_t[:,:,1:], x_t1) (game_state.py:78)
+
+
+def test_pong_episode_terminates_at_21():
+    env = pg.PongVec(1, seed=9)
+    env.reset()
+    env.state[0, pg.CS] = 20
+    for _ in range(2000):
+        _, r, d, info = env.step(torch.tensor([0]))
+        if d[0]:
+            assert info["episode_return"][0] <= -1
+            break
+    else:
+        raise AssertionError("no terminal")
+
+
+def test_preprocess_torch_equals_numpy_reference():
+    env = pg.PongVec(2, seed=2)
+    env.reset()
+    for _ in range(30):
+        env.step(torch.tensor([2, 5]))
+    rgb = pg.render_rgb(env.state)
+    t = pg.preprocess_frames(rgb, env.tables).float() / 255.0
+    n = preprocess_numpy(rgb[1].numpy())
+    assert np.allclose(t[1].numpy(), n, atol=1e-7)
+
+
+def test_gray_bgr_quirk_differs():
+    img = torch.zeros(1, 210, 160, 3, dtype=torch.uint8)
+    img[..., 0] = 200                                        # pure red
+    tab = torch.from_numpy(pg.resize_tables())
+    rgb = pg.preprocess_frames(img, tab, "rgb")
+    bgr = pg.preprocess_frames(img, tab, "bgr")
+    assert int(rgb[0, 0, 0]) == (200 * 4899 + 8192) >> 14
+    assert int(bgr[0, 0, 0]) == (200 * 1868 + 8192) >> 14
+
+
+def test_game_state_reference_api():
+    gs = GameState(113, "Pong", no_op_max=6)
+    assert gs.s_t.shape == (160, 120, 4) and gs.s_t.dtype == np.float32 and gs.s_t.max() <= 1.0
+    gs.process(2)
+    assert gs.s_t1.shape == (160, 120, 4)
+    assert np.array_equal(gs.s_t1[:, :, :3], gs.s_t[:, :, 1:])
+    gs.update()
+    gs.process(99)                                           # out-of-range action remapped to NOOP
+    gs.close_env()
+
+
+def test_atari_suite_games_step():
+    for name in ("Breakout", "SpaceInvaders", "Alien"):
+        env = make(name, num_envs=3, seed=1)
+        o = env.reset()
+        assert o.shape == (3, 160, 120, 4) and o.dtype == torch.uint8
+        tot = torch.zeros(3)
+        for _ in range(60):
+            o, r, d, info = env.step(torch.randint(0, env.num_actions, (3,)))
+            tot += r
+        assert o.shape == (3, 160, 120, 4)

@@ -1,0 +1,98 @@
+"""Trainer: learning, task sequencing/freeze/re-init, checkpoint resume (CPU, torch backend)."""
+import numpy as np
+import torch
+
+from pathnet_gym_amd.algo.trainer import PathNetTrainer
+from pathnet_gym_amd.config import preset
+from pathnet_gym_amd.utils import checkpoint as ckpt
+
+
+def small_cfg(**kw):
+    cfg = preset("cartpole-cpu")
+    cfg.paths, cfg.envs_per_path = 4, 4
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def test_cartpole_learns_on_cpu():
+    torch.manual_seed(0)
+    cfg = small_cfg()
+    cfg.paths, cfg.envs_per_path = 8, 8
+    tr = PathNetTrainer(cfg)
+    rets = []
+    for i in range(250):
+        st = tr.update()
+        if not np.isnan(st.mean_return):
+            rets.append(st.mean_return)
+    assert np.mean(rets[-20:]) > np.mean(rets[:20]) + 10
+    assert tr.pop.generation > 10
+
+
+def test_end_task_freezes_and_reinitialises():
+    cfg = small_cfg(tasks=["CartPole-v1", "CartPole-v1"])
+    tr = PathNetTrainer(cfg)
+    for _ in range(5):
+        tr.update()
+    before = tr.model.store.flat.detach().clone()
+    winner, frozen = tr.end_task()
+    after = tr.model.store.flat.detach()
+    lay = tr.model.store.layout
+    for s in lay.segments:
+        sl = slice(s.offset, s.offset + s.numel)
+        if s.layer >= 0 and frozen[s.layer, s.module] > 0.5:
+            assert torch.equal(after[sl], before[sl]), s.name              # frozen path kept
+        else:
+            assert torch.equal(after[sl], tr.init_flat[sl]), s.name       # re-initialised (doom_pathnet.py:290-293)
+    # frozen modules excluded from updates in the next task
+    tr._start_task(1)
+    frozen_before = after.clone()
+    for _ in range(3):
+        tr.update()
+    for s in lay.segments:
+        if s.layer >= 0 and frozen[s.layer, s.module] > 0.5:
+            sl = slice(s.offset, s.offset + s.numel)
+            assert torch.equal(tr.model.store.flat.detach()[sl], frozen_before[sl])
+    # frozen modules always expressed in task-2 genotypes
+    expr = tr.pop.expressed()
+    assert (expr[:, frozen > 0.5] == 1).all()
+
+
+def test_train_runs_task_sequence():
+    cfg = small_cfg(tasks=["CartPole-v1", "CartPole-v1"])
+    tr = PathNetTrainer(cfg)
+    solved = tr.train(steps_per_task=400)
+    assert set(solved) == {0, 1}
+    assert tr.task_idx == 1 and tr.pop.frozen.sum() > 0
+
+
+def test_checkpoint_resume_is_exact(tmp_path):
+    cfg = small_cfg()
+    torch.manual_seed(0)
+    a = PathNetTrainer(cfg)
+    for _ in range(4):
+        a.update()
+    p = str(tmp_path / "ck.safetensors")
+    ckpt.save(a, p)
+    torch.manual_seed(123)
+    for _ in range(3):
+        a.update()
+    b = PathNetTrainer(cfg)
+    ckpt.load(b, p)
+    torch.manual_seed(123)
+    for _ in range(3):
+        b.update()
+    assert torch.equal(a.model.store.flat, b.model.store.flat)
+    assert np.array_equal(a.pop.genotypes, b.pop.genotypes)
+    assert a.global_step == b.global_step
+
+
+def test_tf_creation_order_importer():
+    from pathnet_gym_amd.models.pathnet import ParamStore
+    cfg = preset("reference").net
+    names = ckpt.tf_creation_order(cfg)
+    assert names[0] == "layer0.module0.weight" and names[-1] == "lstm.bias"
+    st = ParamStore(cfg, "cpu", seed=0)
+    arrays = [np.full(st.layout.by_name[n].shape, i, np.float32) for i, n in enumerate(names)]
+    ckpt.import_tf_arrays(st, arrays)
+    assert float(st.tensor("layer3.module9.bias")[0]) == names.index("layer3.module9.bias")
