@@ -73,8 +73,6 @@ class HipPathNet:
         cfg = model.cfg
         self.cfg = cfg
         self.L, self.M = cfg.L, cfg.M
-        if cfg.use_lstm:
-            raise NotImplementedError("HIP backend: LSTM trunk runs on the torch backend (use --backend torch)")
         lay = model.store.layout
         dev = model.device
         self.geoms: List[LayerGeom] = []

@@ -81,7 +81,12 @@ class HipEngine:
         self._build_opt_tables()
         self.g_rollout = None
         self.g_opt = None
-        self.use_graph = bool(cfg.use_graph)
+        # LSTM nets: HIP trunk + torch LSTM/heads/loss (autograd), dL/dfeat fed back to the HIP trunk backward
+        self.hybrid = bool(model.cfg.use_lstm)
+        self.lstm_state = model.init_state(B) if self.hybrid else None
+        # torch-implemented games (envs/atari_games.py) are stepped eagerly, outside hipGraphs
+        self.env_graph_safe = getattr(env, "graph_safe", True)
+        self.use_graph = bool(cfg.use_graph) and not self.hybrid and self.env_graph_safe
         self.load_obs(env)
 
     # ------------------------------------------------------------------
@@ -119,7 +124,10 @@ class HipEngine:
     # ------------------------------------------------------------------
     def _env_step(self, t):
         env = self.env
-        if self.pixels:
+        if hasattr(env, "step_into"):
+            env.step_into(self.actions[t], self.obs[t], self.obs[t + 1], self.rewards[t], self.dones[t],
+                          self.epret[t])
+        elif self.pixels:
             henv.pong_step_into(env, self.actions[t], self.obs[t], self.obs[t + 1], self.rewards[t], self.dones[t],
                                 self.epret[t])
         else:
@@ -136,7 +144,69 @@ class HipEngine:
         hp.heads_fwd(self.acts[-1][t], self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t,
                      self.T + 1, greedy=greedy, task=self.model.task)
 
+    def _trunk_step(self, t):
+        hp = self.hip
+        x = self.obs
+        for l in range(len(hp.geoms)):
+            hp.layer_fwd(l, x, self.acts[l], self.bits[l], self.P, self.E, 1, t, self.bits_rows[l])
+            x = self.acts[l]
+
+    def _rollout_backward_hybrid(self):
+        """LSTM nets: HIP trunk fwd/bwd, torch (autograd) LSTM + heads + loss in between."""
+        from ..algo.a2c_math import a2c_loss, nstep_returns, sample_actions
+        from ..models.pathnet import lstm_cell_ref
+        T, P, E, B = self.T, self.P, self.E, self.B
+        a2c = self.cfg.a2c
+        model = self.model
+        st = model.store
+        k, bb = st.lstm()
+        pw, pb, vw, vb = st.head(model.task)
+        h, c = self.lstm_state
+        feats, logits_l, values_l = [], [], []
+        for t in range(T):
+            self._trunk_step(t)
+            f = self.acts[-1][t].float().detach().requires_grad_(True)
+            feats.append(f)
+            h, c = lstm_cell_ref(f, h, c, k, bb)
+            logits = h @ pw + pb
+            v = (h @ vw + vb).squeeze(-1)
+            self.actions[t].copy_(sample_actions(logits.detach()).to(torch.int32))
+            self.logits[t].copy_(logits.detach())
+            self.values[t].copy_(v.detach())
+            self._env_step(t)
+            keep = (1.0 - self.dones[t].float())[:, None]
+            h, c = h * keep, c * keep
+            logits_l.append(logits)
+            values_l.append(v)
+        with torch.no_grad():
+            self._trunk_step(T)
+            h2, _ = lstm_cell_ref(self.acts[-1][T].float(), h, c, k, bb)
+            vboot = (h2 @ vw + vb).squeeze(-1)
+        R, adv = nstep_returns(self.rewards, self.values[:T], self.dones.bool(), vboot, a2c.gamma, a2c.gae_lambda,
+                               a2c.reward_clip)
+        wt = torch.full((T * B,), self.weight, device=self.device)
+        loss, lp, lv, ent = a2c_loss(torch.cat(logits_l), torch.cat(values_l), self.actions[:T].reshape(-1).long(),
+                                     R.reshape(-1), adv.reshape(-1), a2c.entropy_beta, a2c.value_coef, wt)
+        st.flat.grad = None
+        loss.backward()
+        self.stats[0], self.stats[1], self.stats[2] = lp, lv, ent * T * B
+        self.grads[-1].copy_(torch.cat([f.grad for f in feats]))
+        self.grad_flat.zero_()
+        hp = self.hip
+        for l in range(len(hp.geoms) - 1, -1, -1):
+            X = self.obs if l == 0 else self.acts[l - 1]
+            dX = self.grads[l - 1] if l > 0 else None
+            hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
+        tn = st.layout.trunk_numel
+        self.grad_flat[tn:] += st.flat.grad[tn:]
+        st.flat.grad = None
+        _lib.call("launch_fitness_update", self.dones.data_ptr(), self.epret.data_ptr(), T, P, E,
+                  self.fitness.data_ptr(), self.counters.data_ptr(), _lib.stream())
+        self.lstm_state = (h.detach(), c.detach())
+
     def _rollout_backward_body(self):
+        if self.hybrid:
+            return self._rollout_backward_hybrid()
         T, P, E, B = self.T, self.P, self.E, self.B
         a2c = self.cfg.a2c
         hp = self.hip

@@ -334,3 +334,37 @@ def test_fast_conv_kernels_match_generic(hip_lib):
         if b.norm() < 1e-6:
             continue
         assert rel(a, b) < 1e-3, (s.name, rel(a, b))
+
+
+def test_engine_hybrid_lstm_reference_net(hip_lib):
+    """Reference default net (L=4, M=10, N=4, LSTM 256): HIP trunk + torch LSTM/heads."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("reference")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 4
+    cfg.ga.B = 3
+    tr = PathNetTrainer(cfg, device=DEV)
+    assert tr.engine.hybrid and not tr.engine.use_graph
+    w0 = tr.model.store.flat.detach().clone()
+    for _ in range(3):
+        st = tr.update()
+        assert np.isfinite(st.loss_pi)
+    lay = tr.model.store.layout
+    s = lay.by_name["lstm.kernel"]
+    assert not torch.equal(w0[s.offset:s.offset + s.numel], tr.model.store.flat.detach()[s.offset:s.offset + s.numel])
+    assert torch.isfinite(tr.model.store.flat).all()
+
+
+def test_engine_torch_implemented_game(hip_lib):
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("atari4")
+    cfg.tasks = ["Breakout", "SpaceInvaders"]
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 3
+    tr = PathNetTrainer(cfg, device=DEV)
+    assert not tr.engine.use_graph
+    for _ in range(2):
+        st = tr.update()
+        assert np.isfinite(st.loss_v)
+    tr.end_task()
+    tr._start_task(1)
+    st = tr.update()
+    assert np.isfinite(st.loss_v)
