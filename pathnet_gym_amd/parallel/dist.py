@@ -85,17 +85,20 @@ def init_distributed(device: Optional[str] = None, backend: Optional[str] = None
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available() if device is None else str(device).startswith("cuda")
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        ndev = torch.cuda.device_count()
+        dev_idx = local_rank % max(1, ndev)          # ranks > devices only in the shared-GPU rehearsal
+        torch.cuda.set_device(dev_idx)
+        dev = torch.device("cuda", dev_idx)
     else:
         dev = torch.device("cpu")
     if world <= 1:
         return DistContext(0, 1, 0, "none", dev)
-    be = backend or ("nccl" if use_cuda else "gloo")
+    # PATHNET_DIST_BACKEND=gloo lets several ranks share one GPU (test rehearsal); default RCCL ("nccl")
+    be = backend or os.environ.get("PATHNET_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if not dist.is_initialized():
         if be == "nccl":
             dist.init_process_group(be, rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group(be, rank=rank, world_size=world)
-    return DistContext(rank, world, local_rank, be, dev)
+    return DistContext(rank, world, dev.index if dev.type == "cuda" else local_rank, be, dev)
