@@ -35,6 +35,7 @@ USE_LSTM = True                      # constants.py:30
 USE_PATHNET = True                   # constants.py:32
 FITNESS_PENDING = -1000.0            # doom_pathnet.py:133,248,267 sentinel
 PERFORMANCE_LOG_INTERVAL = 1000      # a3c_training_thread.py:23
+DEVICE_TASK_STEPS = 2 * 10 ** 9      # per-task horizon for on-device presets (~20 min/GPU at 1.6M frames/s)
 
 
 def log_uniform(lo: float, hi: float, rate: float) -> float:
@@ -225,15 +226,19 @@ def preset(name: str) -> TrainConfig:
         net = PathNetConfig(L=5, M=10, N=4, input_shape=(160, 120, 4),
                             layers=reference_pixel_layers(5, fc=(256, 256)),
                             trunk_scale="M", num_actions=6)
+        # MAX_TIME_STEP (4e6, constants.py:27) is ~17 h of the reference's 63 steps/s but only ~2.5 s
+        # at on-device throughput, so the per-task anneal horizon is sized in frames for this engine.
         return TrainConfig(env="Pong", tasks=["Pong"], paths=64, envs_per_path=32, net=net,
-                           ga=GAConfig(B=3))
+                           ga=GAConfig(B=3), steps_per_task=DEVICE_TASK_STEPS,
+                           a2c=A2CConfig(max_time_step=DEVICE_TASK_STEPS))
     if name in ("atari4", "atari-suite"):
         # BASELINE config 5: 4-task suite with unified 18-way head
         net = PathNetConfig(L=5, M=10, N=4, input_shape=(160, 120, 4),
                             layers=reference_pixel_layers(5, fc=(256, 256)),
                             trunk_scale="M", num_actions=18, num_tasks=4)
         return TrainConfig(env="Pong", tasks=["Pong", "Breakout", "SpaceInvaders", "Alien"],
-                           paths=64, envs_per_path=32, net=net)
+                           paths=64, envs_per_path=32, net=net, steps_per_task=DEVICE_TASK_STEPS,
+                           a2c=A2CConfig(max_time_step=DEVICE_TASK_STEPS))
     if name in ("reference", "ref"):
         # the reference's own default network: L=4 (3 conv + 1 linear), M=10, N=4, LSTM
         net = PathNetConfig(L=4, M=10, N=4, use_lstm=True, trunk_scale="none", num_actions=18)

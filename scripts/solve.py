@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Generations-to-solve: the second half of the BASELINE.json headline metric.
+
+"Solved" (the reference defines no criterion) = the
+first GA tournament whose winner fitness (= return of that path's most
+recently finished episode, a3c_training_thread.py:145-147) reaches the env's
+gym ``reward_threshold`` (Pong 18, CartPole-v1 475; the registry spirit of
+gym_doom/__init__.py:21-90).  Reported as tournaments ("generations"), agent
+frames and wall seconds until solve, plus a learning curve in JSONL.
+
+    python scripts/solve.py --preset pong --minutes 15 [--paths 64 --envs 32]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/solve.py ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="pong")
+    ap.add_argument("--minutes", type=float, default=10.0)
+    ap.add_argument("--paths", type=int, default=None)
+    ap.add_argument("--envs", type=int, default=None)
+    ap.add_argument("--tmax", type=int, default=None)
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--B", type=int, default=None)
+    ap.add_argument("--concurrent", type=int, default=None, help="concurrent tournaments (default paths*world/16)")
+    ap.add_argument("--backend", default="auto")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--curve", default="gpurun_out/solve_curve.jsonl")
+    ap.add_argument("--report-every", type=float, default=30.0, help="seconds between progress lines")
+    ap.add_argument("--keep-going", action="store_true", help="continue after solving until --minutes")
+    args = ap.parse_args()
+
+    import torch
+    from pathnet_gym_amd.config import preset
+    from pathnet_gym_amd.envs.registry import reward_threshold
+    from pathnet_gym_amd.parallel.dist import init_distributed
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+
+    ctx = init_distributed()
+    cfg = preset(args.preset)
+    for k, v in (("paths", args.paths), ("envs_per_path", args.envs)):
+        if v is not None:
+            setattr(cfg, k, v)
+    if args.tmax is not None:
+        cfg.a2c.t_max = args.tmax
+    if args.lr is not None:
+        cfg.a2c.lr = args.lr
+    if args.B is not None:
+        cfg.ga.B = args.B
+    cfg.backend = args.backend
+    cfg.use_graph = not args.no_graph
+    cfg.ga.concurrent_tournaments = args.concurrent or max(1, (cfg.paths * ctx.world) // 16)
+    if cfg.backend in ("hip", "auto") and ctx.device.type == "cuda":
+        from pathnet_gym_amd import _build
+        _build.build()
+    tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
+    thr = reward_threshold(cfg.tasks[0])
+    curve = None
+    if ctx.is_main and args.curve:
+        os.makedirs(os.path.dirname(args.curve) or ".", exist_ok=True)
+        curve = open(args.curve, "w")
+
+    t0 = time.time()
+    last = t0
+    best = -math.inf
+    solved = None
+    ret_ema = None
+    while True:
+        st = tr.update()
+        if not math.isnan(st.mean_return):
+            ret_ema = st.mean_return if ret_ema is None else 0.9 * ret_ema + 0.1 * st.mean_return
+        if st.tournaments:
+            best = max(best, st.best_winner)
+            if solved is None and st.best_winner >= thr:
+                solved = dict(generations=tr.pop.generation, frames=tr.global_step,
+                              seconds=round(time.time() - t0, 2), winner_fitness=st.best_winner)
+        now = time.time()
+        if now - last >= args.report_every or (solved and not args.keep_going):
+            last = now
+            rec = dict(t=round(now - t0, 1), frames=tr.global_step, updates=tr.updates,
+                       generation=tr.pop.generation, mean_return=ret_ema, best_winner=best,
+                       entropy=st.entropy, frames_per_sec=round(tr.global_step / (now - t0), 1))
+            if ctx.is_main:
+                print(json.dumps(rec), flush=True)
+                if curve:
+                    curve.write(json.dumps(rec) + "\n")
+                    curve.flush()
+        if solved and not args.keep_going:
+            break
+        if now - t0 > args.minutes * 60:
+            break
+    el = time.time() - t0
+    if ctx.is_main:
+        out = {"metric": "generations_to_solve", "env": cfg.tasks[0], "threshold": thr,
+               "solved": solved is not None, "generations_to_solve": solved and solved["generations"],
+               "frames_to_solve": solved and solved["frames"], "seconds_to_solve": solved and solved["seconds"],
+               "best_winner_fitness": best, "final_mean_return": ret_ema, "generations": tr.pop.generation,
+               "frames": tr.global_step, "seconds": round(el, 1), "n_gpus": ctx.world,
+               "config": {"preset": args.preset, "paths_per_gpu": cfg.paths, "envs_per_path": cfg.envs_per_path,
+                          "t_max": cfg.a2c.t_max, "lr": cfg.a2c.lr, "B": cfg.ga.B,
+                          "concurrent_tournaments": cfg.ga.concurrent_tournaments, "backend": tr.backend}}
+        print(json.dumps(out), flush=True)
+    ctx.destroy()
+
+
+if __name__ == "__main__":
+    main()
