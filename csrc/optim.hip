@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void rmsprop_apply_kernel(float* __restrict__ 
                                                             float momentum, float eps, float clip) {
   const int blk = blockIdx.x;
   const int seg = blk_seg[blk];
-  if (!trainable[seg]) return;
+  if (!trainable[seg] || lr_ptr[1] != 0.f) return;      // lr_ptr = {lr, skip}: skip = non-finite update
   const long b0 = blk_beg[blk], b1 = blk_end[blk];
   const float norm = sqrtf(sq[seg]);
   const float scale = clip / fmaxf(norm, clip);          // tf.clip_by_norm

@@ -27,12 +27,15 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from ..config import FITNESS_PENDING, TrainConfig
+from ..config import FITNESS_PENDING, PERFORMANCE_LOG_INTERVAL, TrainConfig
 from ..envs.registry import make, reward_threshold
 from ..models.acnet import ACPathNet
 from ..parallel.comm import FusedUpdateComm, GatherBroadcastComm
 from ..parallel.dist import DistContext
+from ..runtime.consistency import check_replicas
+from ..runtime.guard import NonFiniteGuard, Watchdog
 from ..utils.metrics import MetricsLogger
+from ..utils.tracing import PhaseTracer, performance_line
 from .a2c_math import a2c_loss, nstep_returns, sample_actions
 from .ga import Population
 from .optim import RMSPropTF, anneal_lr
@@ -55,6 +58,8 @@ class UpdateStats:
     mean_return: float = float("nan")
     tournaments: int = 0
     best_winner: float = float("nan")
+    steps: int = 0
+    skipped: bool = False
 
 
 class PathNetTrainer:
@@ -92,6 +97,9 @@ class PathNetTrainer:
         self.env = None
         self.visualizer = None
         self._last_vis = 0.0
+        self.tracer = PhaseTracer(enabled=True, path=cfg.trace_path, rank=self.ctx.rank)
+        self.guard = NonFiniteGuard(cfg.max_nonfinite)
+        self.watchdog = Watchdog(cfg.watchdog_s, phase=lambda: self.tracer.current) if cfg.watchdog_s > 0 else None
         self._start_task(0, fresh=True)
 
     # ------------------------------------------------------------------
@@ -206,30 +214,42 @@ class PathNetTrainer:
         if state is not None:
             state = (state[0].detach(), state[1].detach())
         self.lstm_state = state
+        nonfinite = (~torch.isfinite(flat.grad)).sum(dtype=torch.float32)
         counters = torch.stack([torch.tensor(float(T * B), device=self.device), ep_cnt.sum(), ep_sum.sum(),
-                                torch.zeros((), device=self.device)])
+                                nonfinite])
         return flat.grad, counters, (lp, lv, ent)
 
     def update(self) -> UpdateStats:
         lr = anneal_lr(self.cfg.a2c.lr, self.global_step, self.cfg.a2c.max_time_step,
                        self.task_start_step, self.cfg.a2c.lr_anneal)
+        tr = self.tracer
         if self.engine is not None:
             eng = self.engine
-            eng.rollout_backward()
-            fit_all, csum = self.comm.exchange(eng.grad_flat, eng.fitness, eng.counters)
-            eng.optimizer_step(lr)
+            with tr.phase("rollout_backward"):
+                eng.rollout_backward()
+            with tr.phase("allreduce"):
+                fit_all, csum = self.comm.exchange(eng.grad_flat, eng.fitness, eng.counters)
+            skip = self.guard.check(float(csum[3]), self.updates)      # same decision on every rank
+            with tr.phase("optimizer"):
+                eng.optimizer_step(lr, skip=skip)
             lp, lv, ent = [float(x) for x in eng.stats_host()[:3]]
             ent /= max(1, self.cfg.a2c.t_max * self.P * self.E)
         else:
-            grad, counters, (lp, lv, ent) = self.rollout_and_backward()
-            fit_all, csum = self.comm.exchange(grad, self.fitness_local, counters)
-            with torch.no_grad():
-                self.opt.step(grad, lr)
+            with tr.phase("rollout_backward"):
+                grad, counters, (lp, lv, ent) = self.rollout_and_backward()
+            with tr.phase("allreduce"):
+                fit_all, csum = self.comm.exchange(grad, self.fitness_local, counters)
+            skip = self.guard.check(float(csum[3]), self.updates)
+            if not skip:
+                with tr.phase("optimizer"), torch.no_grad():
+                    self.opt.step(grad, lr)
         self.global_step += int(csum[0])
         self.updates += 1
         st = UpdateStats(float(lp), float(lv), float(ent), int(csum[1]),
-                         float(csum[2] / csum[1]) if csum[1] > 0 else float("nan"))
-        events = self.pop.step(fit_all, self.global_step)
+                         float(csum[2] / csum[1]) if csum[1] > 0 else float("nan"), steps=int(csum[0]),
+                         skipped=skip)
+        with tr.phase("ga"):
+            events = self.pop.step(fit_all, self.global_step)
         if isinstance(self.comm, GatherBroadcastComm) and events:
             g = self.comm.broadcast_genotypes(self.pop.genotypes)
             self.pop.genotypes = g
@@ -251,6 +271,11 @@ class PathNetTrainer:
                     # "<step> Step Score: <s>" (doom_pathnet.py:256)
                     self.logger.log("tournament", step=e.step, generation=e.generation, winner=e.winner,
                                     score=e.winner_fitness, candidates=e.candidates, scores=e.scores)
+        if self.watchdog is not None:
+            self.watchdog.beat()
+        if self.cfg.check_every and self.updates % self.cfg.check_every == 0:
+            with tr.phase("consistency"):
+                check_replicas(self)
         return st
 
     # ------------------------------------------------------------------
@@ -259,6 +284,7 @@ class PathNetTrainer:
         """Run the task sequence (doom_pathnet.py:178-293 generalised to K tasks)."""
         steps_per_task = steps_per_task or self.cfg.steps_per_task
         t0 = time.time()
+        perf_step, perf_t = self.global_step, t0
         first = self.task_idx
         for task_idx in range(first, len(self.cfg.tasks)):
             if task_idx != self.task_idx:
@@ -270,6 +296,11 @@ class PathNetTrainer:
                 if checkpoint and checkpoint_every and self.updates % checkpoint_every == 0:
                     from ..utils import checkpoint as ckpt
                     ckpt.save(self, checkpoint)
+                # reference throughput line: every PERFORMANCE_LOG_INTERVAL steps (rate-limited to 10 s)
+                if self.ctx.is_main and self.logger is not None and self.logger.echo and \
+                        self.global_step - perf_step >= PERFORMANCE_LOG_INTERVAL and time.time() - perf_t >= 10.0:
+                    perf_step, perf_t = self.global_step, time.time()
+                    print(performance_line(self.global_step, perf_t - t0), flush=True)
                 if self.logger is not None and self.ctx.is_main and self.updates % 10 == 0:
                     el = time.time() - t0
                     self.logger.log("perf", step=self.global_step, steps_per_sec=self.global_step / max(el, 1e-9),
@@ -287,4 +318,6 @@ class PathNetTrainer:
             if self.logger is not None and self.ctx.is_main:
                 self.logger.log("freeze", task=task_idx, winner=winner, frozen=frozen.astype(int).tolist(),
                                 solved_generation=self.solved_generation.get(task_idx))
+        if self.cfg.trace_path:
+            self.tracer.dump()
         return self.solved_generation

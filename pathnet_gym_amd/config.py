@@ -188,6 +188,11 @@ class TrainConfig:
     checkpoint_every: int = 0
     frameskip: int = 4
     gray: str = "rgb"                   # "rgb" luma | "bgr" (reference cv2.COLOR_BGR2GRAY on RGB quirk)
+    # failure / race detection and tracing (runtime/guard.py, runtime/consistency.py, utils/tracing.py)
+    check_every: int = 0                # replica-consistency check interval in updates (0 = off)
+    max_nonfinite: int = 3              # consecutive non-finite updates tolerated (skipped) before raising
+    watchdog_s: float = 0.0             # abort if no update completes for this long (0 = off)
+    trace_path: Optional[str] = None    # Chrome-trace JSON of update phases
 
     def to_json(self):
         return json.dumps(dataclasses.asdict(self))

@@ -53,6 +53,12 @@ _SIGS = {
                         c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P],
     "fast_conv_dgrad": [P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_long, c_float, P, P],
+    "launch_lstm_fwd": [P, c_int, P, P, P, P, P, c_long, P, P, P, P, c_int, c_int, c_int, P],
+    "launch_lstm_bwd_point": [P, P, P, P, P, P, P, P, P, P, c_int, c_int, P],
+    "launch_lstm_bwd_gemm": [P, P, P, c_int, P, c_int, c_int, c_int, P],
+    "launch_lstm_wgrad": [P, P, P, c_long, c_long, c_int, c_int, c_long, c_int, P],
+    "launch_lstm_refresh": [P, c_long, c_int, c_int, P, P, P],
+    "launch_lstm_carry": [P, P, P, P, P, c_int, c_int, P],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }

@@ -120,6 +120,15 @@ class HipPathNet:
         self.inv_cnt = torch.zeros(self.L, self.M, dtype=torch.int32, device=dev)
         lay_h = lay.heads
         self.heads_off = lay_h
+        # fused LSTM cell (csrc/lstm.hip): bf16 copies of the fp32 master kernel
+        self.lstm = None
+        if cfg.use_lstm:
+            ls = lay.lstm
+            F, H = ls["din"], ls["H"]
+            if F % 64 == 0 and H % 64 == 0:
+                self.lstm = dict(F=F, H=H, k_off=ls["kernel"], b_off=ls["bias"],
+                                 KpT=torch.zeros(4 * H, F + H, dtype=torch.bfloat16, device=dev),
+                                 Kb=torch.zeros(F + H, 4 * H, dtype=torch.bfloat16, device=dev))
         self.refresh_weights()
 
     # ------------------------------------------------------------------
@@ -148,6 +157,41 @@ class HipPathNet:
         for l, g in enumerate(self.geoms):
             _lib.call("launch_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
                       self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), _lib.stream())
+        if self.lstm is not None:
+            ls = self.lstm
+            _lib.call("launch_lstm_refresh", flat.data_ptr(), ls["k_off"], ls["F"], ls["H"], ls["KpT"].data_ptr(),
+                      ls["Kb"].data_ptr(), _lib.stream())
+
+    # -- fused LSTM cell (csrc/lstm.hip) ------------------------------------------
+    def lstm_fwd(self, x, hprev, cprev, prev_done, hout, cout, gates=None, xh=None):
+        """x [B,F] bf16, hprev [B,H] bf16, cprev [B,H] f32, prev_done [B] u8 or None -> hout/cout(/gates/xh)."""
+        ls = self.lstm
+        B = x.shape[0]
+        _lib.call("launch_lstm_fwd", x.data_ptr(), x.shape[1], hprev.data_ptr(), cprev.data_ptr(),
+                  _lib.ptr(prev_done), ls["KpT"].data_ptr(), self.model.store.flat.data_ptr(), ls["b_off"],
+                  hout.data_ptr(), cout.data_ptr(), _lib.ptr(gates), _lib.ptr(xh), ls["F"], ls["H"], B,
+                  _lib.stream())
+
+    def lstm_bwd_step(self, dh_heads, dh_rec, dc_rec, done_t, gates, c_t, c_prev, prev_done, dz, dc_out, dx,
+                      dh_prev):
+        ls = self.lstm
+        B = dh_heads.shape[0]
+        st = _lib.stream()
+        _lib.call("launch_lstm_bwd_point", dh_heads.data_ptr(), _lib.ptr(dh_rec), _lib.ptr(dc_rec),
+                  _lib.ptr(done_t), gates.data_ptr(), c_t.data_ptr(), c_prev.data_ptr(), _lib.ptr(prev_done),
+                  dz.data_ptr(), dc_out.data_ptr(), ls["H"], B, st)
+        _lib.call("launch_lstm_bwd_gemm", dz.data_ptr(), ls["Kb"].data_ptr(), dx.data_ptr(), dx.shape[-1],
+                  dh_prev.data_ptr(), ls["F"], ls["H"], B, st)
+
+    def lstm_wgrad(self, xh, dz, grad_flat, rows_per_chunk: int = 2048):
+        ls = self.lstm
+        R = xh.numel() // (ls["F"] + ls["H"])
+        _lib.call("launch_lstm_wgrad", xh.data_ptr(), dz.data_ptr(), grad_flat.data_ptr(), ls["k_off"], ls["b_off"],
+                  ls["F"], ls["H"], R, rows_per_chunk, _lib.stream())
+
+    def lstm_carry(self, hT, cT, done_last, h0, c0):
+        _lib.call("launch_lstm_carry", hT.data_ptr(), cT.data_ptr(), done_last.data_ptr(), h0.data_ptr(),
+                  c0.data_ptr(), self.lstm["H"], h0.shape[0], _lib.stream())
 
     # ------------------------------------------------------------------
     def layer_fwd(self, l: int, X: torch.Tensor, Y: torch.Tensor, bits: torch.Tensor, P: int, E: int, T: int,

@@ -75,15 +75,27 @@ class HipEngine:
         self.fitness = torch.full((P,), -1000.0, device=dev)
         self.counters = torch.zeros(4, device=dev)
         self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.lr = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.lr = torch.zeros(2, dtype=torch.float32, device=dev)      # {lr, skip}
         self.weight = (1.0 / E) if a2c.env_reduction == "mean_env" else 1.0
         # optimizer block table (segments split into <= 8192-element blocks)
         self._build_opt_tables()
         self.g_rollout = None
         self.g_opt = None
-        # LSTM nets: HIP trunk + torch LSTM/heads/loss (autograd), dL/dfeat fed back to the HIP trunk backward
-        self.hybrid = bool(model.cfg.use_lstm)
+        # LSTM nets: fused HIP LSTM cell (csrc/lstm.hip) when the widths are multiples of 64; otherwise
+        # the hybrid path (HIP trunk + autograd LSTM/heads/loss, dL/dfeat fed back to the HIP trunk backward)
+        self.lstm_hip = hp.lstm is not None
+        self.hybrid = bool(model.cfg.use_lstm) and not self.lstm_hip
         self.lstm_state = model.init_state(B) if self.hybrid else None
+        if self.lstm_hip:
+            F, H = hp.lstm["F"], hp.lstm["H"]
+            self.hst = torch.zeros(T + 2, B, H, dtype=torch.bfloat16, device=dev)   # slot t = state entering step t
+            self.cst = torch.zeros(T + 2, B, H, device=dev)
+            self.gates = torch.zeros(T, B, 4 * H, device=dev)
+            self.xh = torch.zeros(T, B, F + H, dtype=torch.bfloat16, device=dev)
+            self.dz = torch.zeros(T, B, 4 * H, device=dev)
+            self.dh_heads = torch.zeros(T, B, H, device=dev)
+            self.dh_rec = torch.zeros(2, B, H, device=dev)
+            self.dc_rec = torch.zeros(2, B, H, device=dev)
         # torch-implemented games (envs/atari_games.py) are stepped eagerly, outside hipGraphs
         self.env_graph_safe = getattr(env, "graph_safe", True)
         self.use_graph = bool(cfg.use_graph) and not self.hybrid and self.env_graph_safe
@@ -141,7 +153,15 @@ class HipEngine:
         for l in range(len(hp.geoms)):
             hp.layer_fwd(l, x, self.acts[l], self.bits[l], P, E, 1, t, self.bits_rows[l])
             x = self.acts[l]
-        hp.heads_fwd(self.acts[-1][t], self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t,
+        feat = self.acts[-1][t]
+        if self.lstm_hip:
+            # state entering step t: slot t, reset where the previous step ended an episode
+            # (slot 0 is pre-masked by the carry at the end of the previous update)
+            last = t >= self.T
+            hp.lstm_fwd(feat, self.hst[t], self.cst[t], self.dones[t - 1] if t > 0 else None, self.hst[t + 1],
+                        self.cst[t + 1], None if last else self.gates[t], None if last else self.xh[t])
+            feat = self.hst[t + 1]
+        hp.heads_fwd(feat, self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t,
                      self.T + 1, greedy=greedy, task=self.model.task)
 
     def _trunk_step(self, t):
@@ -202,6 +222,7 @@ class HipEngine:
         st.flat.grad = None
         _lib.call("launch_fitness_update", self.dones.data_ptr(), self.epret.data_ptr(), T, P, E,
                   self.fitness.data_ptr(), self.counters.data_ptr(), _lib.stream())
+        self._count_nonfinite()
         self.lstm_state = (h.detach(), c.detach())
 
     def _rollout_backward_body(self):
@@ -223,15 +244,56 @@ class HipEngine:
                   self.dlogits.data_ptr(), self.dvalue.data_ptr(), self.stats.data_ptr(), _lib.stream())
         self.grad_flat.zero_()
         L = len(hp.geoms)
-        feat = self.acts[L - 1][:T].reshape(T * B, -1)
-        hp.heads_bwd(feat, self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1), self.grad_flat,
-                     self.grads[L - 1], task=self.model.task)
+        if self.lstm_hip:
+            self._lstm_backward()
+        else:
+            feat = self.acts[L - 1][:T].reshape(T * B, -1)
+            hp.heads_bwd(feat, self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1), self.grad_flat,
+                         self.grads[L - 1], task=self.model.task)
         for l in range(L - 1, -1, -1):
             X = self.obs if l == 0 else self.acts[l - 1]
             dX = self.grads[l - 1] if l > 0 else None
             hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
+        self._count_nonfinite()
+
+    def _count_nonfinite(self):
+        # spare counter slot: non-finite gradient entries, all-reduced with the update (runtime/guard.py)
+        self.counters[3:4].copy_((~torch.isfinite(self.grad_flat)).sum(dtype=torch.float32).reshape(1))
+
+    def _lstm_backward(self):
+        """Heads backward into dL/dh, reverse scan through the fused LSTM cell, then its weight gradient."""
+        T, B = self.T, self.B
+        hp = self.hip
+        H = hp.lstm["H"]
+        hp.heads_bwd(self.hst[1:T + 1].reshape(T * B, H), self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1),
+                     self.grad_flat, self.dh_heads.reshape(T * B, H), task=self.model.task)
+        dfeat = self.grads[-1].view(T, B, -1)
+        for t in range(T - 1, -1, -1):
+            cur, nxt = t % 2, (t + 1) % 2
+            first = t == T - 1
+            hp.lstm_bwd_step(self.dh_heads[t], None if first else self.dh_rec[nxt], None if first else self.dc_rec[nxt],
+                             self.dones[t], self.gates[t], self.cst[t + 1], self.cst[t],
+                             self.dones[t - 1] if t > 0 else None, self.dz[t], self.dc_rec[cur], dfeat[t],
+                             self.dh_rec[cur])
+        hp.lstm_wgrad(self.xh, self.dz, self.grad_flat)
+
+    def lstm_state_tensors(self):
+        """Recurrent state carried into the next update (checkpointing)."""
+        if self.lstm_hip:
+            return self.hst[0].float(), self.cst[0]
+        return self.lstm_state
+
+    def load_lstm_state(self, h, c):
+        if self.lstm_hip:
+            self.hst[0].copy_(h.to(self.hst.dtype))
+            self.cst[0].copy_(c)
+        elif self.hybrid:
+            self.lstm_state = (h.clone(), c.clone())
 
     def _optimizer_body(self):
+        if self.lstm_hip:
+            T = self.T
+            self.hip.lstm_carry(self.hst[T], self.cst[T], self.dones[T - 1], self.hst[0], self.cst[0])
         o = self.opt
         _lib.call("launch_rmsprop", self.model.store.flat.data_ptr(), self.grad_flat.data_ptr(), o.ms.data_ptr(),
                   o.mom.data_ptr(), self.blk_seg.data_ptr(), self.blk_beg.data_ptr(), self.blk_end.data_ptr(),
@@ -266,8 +328,9 @@ class HipEngine:
         else:
             self._rollout_backward_body()
 
-    def optimizer_step(self, lr: float):
-        self.lr.fill_(lr)
+    def optimizer_step(self, lr: float, skip: bool = False):
+        self.lr[0:1].fill_(lr)
+        self.lr[1:2].fill_(1.0 if skip else 0.0)
         if self.use_graph and self.g_opt is not None:
             self.g_opt.replay()
         else:

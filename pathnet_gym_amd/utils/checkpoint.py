@@ -82,9 +82,10 @@ def rank_tensors(trainer) -> Dict[str, torch.Tensor]:
     else:
         out["train.obs"] = _t(trainer.obs)
         out["train.fitness_local"] = _t(trainer.fitness_local)
-    if trainer.lstm_state is not None:
-        out["lstm.h"] = _t(trainer.lstm_state[0])
-        out["lstm.c"] = _t(trainer.lstm_state[1])
+    lstm = trainer.engine.lstm_state_tensors() if trainer.engine is not None else trainer.lstm_state
+    if lstm is not None:
+        out["lstm.h"] = _t(lstm[0])
+        out["lstm.c"] = _t(lstm[1])
     return out
 
 
@@ -150,7 +151,10 @@ def load(trainer, path: str, strict: bool = True):
             trainer.obs = r["train.obs"].to(dev)
             trainer.fitness_local = r["train.fitness_local"].to(dev)
         if "lstm.h" in r:
-            trainer.lstm_state = (r["lstm.h"].to(dev), r["lstm.c"].to(dev))
+            if trainer.engine is not None:
+                trainer.engine.load_lstm_state(r["lstm.h"].to(dev), r["lstm.c"].to(dev))
+            else:
+                trainer.lstm_state = (r["lstm.h"].to(dev), r["lstm.c"].to(dev))
     if trainer.backend == "hip":
         trainer.model.hip.refresh_weights()
     return trainer

@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--tmax", type=int, default=None)
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--B", type=int, default=None)
+    ap.add_argument("--env-reduction", default=None, choices=["sum", "mean_env"])
+    ap.add_argument("--entropy-beta", type=float, default=None)
+    ap.add_argument("--trunk-scale", default=None, choices=["M", "none"])
+    ap.add_argument("--gae-lambda", type=float, default=None)
     ap.add_argument("--concurrent", type=int, default=None, help="concurrent tournaments (default paths*world/16)")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--no-graph", action="store_true")
@@ -57,6 +61,14 @@ def main():
         cfg.a2c.lr = args.lr
     if args.B is not None:
         cfg.ga.B = args.B
+    if args.env_reduction is not None:
+        cfg.a2c.env_reduction = args.env_reduction
+    if args.entropy_beta is not None:
+        cfg.a2c.entropy_beta = args.entropy_beta
+    if args.trunk_scale is not None:
+        cfg.net.trunk_scale = args.trunk_scale
+    if args.gae_lambda is not None:
+        cfg.a2c.gae_lambda = args.gae_lambda
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
     cfg.ga.concurrent_tournaments = args.concurrent or max(1, (cfg.paths * ctx.world) // 16)
@@ -77,7 +89,10 @@ def main():
     ret_ema = None
     while True:
         st = tr.update()
-        if not math.isnan(st.mean_return):
+        if not math.isnan(st.mean_return) and abs(st.mean_return) > 1000 and ctx.is_main:
+            print(json.dumps({"anomaly": "mean_return", "value": st.mean_return, "episodes": st.episodes,
+                              "update": tr.updates}), flush=True)
+        elif not math.isnan(st.mean_return):
             ret_ema = st.mean_return if ret_ema is None else 0.9 * ret_ema + 0.1 * st.mean_return
         if st.tournaments:
             best = max(best, st.best_winner)
@@ -108,7 +123,9 @@ def main():
                "frames": tr.global_step, "seconds": round(el, 1), "n_gpus": ctx.world,
                "config": {"preset": args.preset, "paths_per_gpu": cfg.paths, "envs_per_path": cfg.envs_per_path,
                           "t_max": cfg.a2c.t_max, "lr": cfg.a2c.lr, "B": cfg.ga.B,
-                          "concurrent_tournaments": cfg.ga.concurrent_tournaments, "backend": tr.backend}}
+                          "concurrent_tournaments": cfg.ga.concurrent_tournaments, "backend": tr.backend,
+                          "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
+                          "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda}}
         print(json.dumps(out), flush=True)
     ctx.destroy()
 

@@ -36,9 +36,24 @@ def _worker(rank, world, port, mode, q):
         cfg.paths, cfg.envs_per_path = 3, 4
         cfg.ga.B = 2
         cfg.ga.concurrent_tournaments = 2
-        cfg.ga_sync = mode
+        cfg.ga_sync = "fused" if mode == "diverge" else mode
+        cfg.check_every = 2
         tr = PathNetTrainer(cfg, ctx=ctx)
         out = {}
+        if mode == "diverge":
+            from pathnet_gym_amd.runtime.consistency import DivergenceError
+            tr.update()
+            if rank == 1:
+                with torch.no_grad():
+                    tr.model.store.flat[7] += 1e-3       # a replica silently drifts
+            try:
+                tr.update()
+                out["raised"] = False
+            except DivergenceError as e:
+                out["raised"] = "[1]" in str(e)
+            q.put((rank, out))
+            ctx.destroy()
+            return
         if mode == "fused":
             # all-reduced grad == sum of local grads
             g, c, _ = tr.rollout_and_backward()
@@ -85,3 +100,18 @@ def test_two_ranks_stay_in_lockstep(mode):
     assert a["step"] == 6 * 2 * 3 * 4 * 5
     if mode == "fused":
         assert a["grad_ok"] and b["grad_ok"]
+
+
+def test_replica_divergence_is_detected_on_every_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, "diverge", q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r in range(2):
+        assert "error" not in res[r], res[r].get("error")
+        assert res[r]["raised"] is True

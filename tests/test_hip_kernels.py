@@ -245,7 +245,13 @@ def test_rmsprop_kernel_matches_torch(hip_lib):
     ref.ms.copy_(tr.opt.ms)
     ref.step(g, 7e-4)
     eng.grad_flat.copy_(g)
-    eng.lr.fill_(7e-4)
+    eng.lr[0:1].fill_(7e-4)
+    eng.lr[1:2].fill_(1.0)                 # skip flag (non-finite update): nothing may change
+    ms0 = tr.opt.ms.clone()
+    eng._optimizer_body()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.model.store.flat.detach(), flat0) and torch.equal(tr.opt.ms, ms0)
+    eng.lr[1:2].zero_()
     eng._optimizer_body()
     torch.cuda.synchronize()
     assert rel(tr.model.store.flat.detach() - flat0, ref.flat - flat0) < 1e-4
@@ -337,13 +343,13 @@ def test_fast_conv_kernels_match_generic(hip_lib):
 
 
 def test_engine_hybrid_lstm_reference_net(hip_lib):
-    """Reference default net (L=4, M=10, N=4, LSTM 256): HIP trunk + torch LSTM/heads."""
+    """Reference default net (L=4, M=10, N=4, LSTM 256): HIP trunk + fused HIP LSTM, graph-captured."""
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     cfg = preset("reference")
     cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 4
     cfg.ga.B = 3
     tr = PathNetTrainer(cfg, device=DEV)
-    assert tr.engine.hybrid and not tr.engine.use_graph
+    assert tr.engine.lstm_hip and not tr.engine.hybrid and tr.engine.use_graph
     w0 = tr.model.store.flat.detach().clone()
     for _ in range(3):
         st = tr.update()
@@ -368,3 +374,156 @@ def test_engine_torch_implemented_game(hip_lib):
     tr._start_task(1)
     st = tr.update()
     assert np.isfinite(st.loss_v)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_engine_gradient_matches_oracle(hip_lib, graph):
+    """Whole engine update == autograd of the A2C loss over the SAME stored rollout.
+
+    Recomputes logits/values with the fp32 oracle from the engine's stored
+    observations, rebuilds the n-step targets from the stored rewards/dones,
+    and compares the full flat gradient (trunk modules + heads) with the
+    engine's.  Catches wiring errors (step/slot/sample indexing) that the
+    per-kernel tests cannot see.
+    """
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.models.pathnet import ParamStore
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 4
+    cfg.use_graph = graph
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng = tr.engine
+    for _ in range(3 if graph else 1):     # with graphs: eager, capture, then a replayed update
+        tr.update()
+    T, P, E, B, A = eng.T, eng.P, eng.E, eng.B, eng.A
+    obs0 = eng.obs[0].clone()
+    if graph:
+        eng.rollout_backward()
+    else:
+        eng._rollout_backward_body()
+    torch.cuda.synchronize()
+    assert torch.equal(eng.obs[0], obs0)
+    a2c = cfg.a2c
+    flat = tr.model.store.flat.detach().clone().requires_grad_(True)
+    st = ParamStore(cfg.net, DEV, flat=flat)
+    x = eng.obs[:T + 1].reshape((T + 1) * B, 160, 120, 4).float() / 255.0
+    mask = tr.model.mask.repeat_interleave(E, 0).repeat(T + 1, 1, 1)
+    feat = trunk_forward_ref(st, x, mask, emulate_bf16=True)
+    logits, values = heads_ref(st, feat)
+    assert rel(logits[:T * B], eng.logits[:T].reshape(-1, A)) < 3e-2
+    assert rel(values, eng.values[:T + 1].reshape(-1)) < 3e-2
+    R, adv = nstep_returns(eng.rewards, eng.values[:T], eng.dones.bool(), eng.values[T], a2c.gamma,
+                           a2c.gae_lambda, a2c.reward_clip)
+    loss, lp, lv, ent = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(), R.reshape(-1),
+                                 adv.reshape(-1), a2c.entropy_beta, a2c.value_coef,
+                                 torch.full((T * B,), 1.0 / E, device=DEV))
+    loss.backward()
+    g_ref, g_hip = flat.grad, eng.grad_flat
+    errs = {}
+    for s in tr.model.store.layout.segments:
+        a, b = g_hip[s.offset:s.offset + s.numel], g_ref[s.offset:s.offset + s.numel]
+        if b.norm() < 1e-7:
+            assert a.norm() < 1e-4 * max(1.0, float(g_ref.norm())), s.name
+            continue
+        errs[s.name] = rel(a, b)
+    worst = max(errs, key=errs.get)
+    print({k: round(v, 4) for k, v in sorted(errs.items(), key=lambda kv: -kv[1])[:8]})
+    assert errs[worst] < 6e-2, (worst, errs[worst])
+
+
+def test_lstm_cell_kernels_match_autograd(hip_lib):
+    """Fused LSTM fwd / bwd-step / wgrad kernels vs TF BasicLSTMCell semantics in fp32 autograd."""
+    from pathnet_gym_amd.models.pathnet import ParamStore, bf16_ste, lstm_cell_ref
+    cfg = preset("reference").net
+    P, B = 3, 96                                   # B not a multiple of the 64-row tile
+    m = make_model(cfg, P, random_masks(P, cfg.L, cfg.M, cfg.N, with_edge=False))
+    hp = m.hip
+    F, H = hp.lstm["F"], hp.lstm["H"]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = (torch.randn(B, F, generator=g) * 0.5).to(DEV).to(torch.bfloat16)
+    h = (torch.randn(B, H, generator=g) * 0.5).to(DEV).to(torch.bfloat16)
+    c = torch.randn(B, H, generator=g).to(DEV)
+    done = (torch.rand(B, generator=g) < 0.3).to(torch.uint8).to(DEV)
+    hout = torch.zeros(B, H, dtype=torch.bfloat16, device=DEV)
+    cout = torch.zeros(B, H, device=DEV)
+    gates = torch.zeros(B, 4 * H, device=DEV)
+    xh = torch.zeros(B, F + H, dtype=torch.bfloat16, device=DEV)
+    hp.lstm_fwd(x, h, c, done, hout, cout, gates, xh)
+    torch.cuda.synchronize()
+    flat = m.store.flat.detach().clone().requires_grad_(True)
+    st = ParamStore(cfg, DEV, flat=flat)
+    k, b = st.lstm()
+    keep = (1.0 - done.float())[:, None]
+    xr = x.float().requires_grad_(True)
+    hin = (h.float() * keep).requires_grad_(True)
+    h2, c2 = lstm_cell_ref(xr, hin, c * keep, bf16_ste(k), b)
+    assert rel(hout.float(), h2.detach()) < 1e-2
+    assert rel(cout, c2.detach()) < 1e-2
+    assert torch.equal(xh[:, :F], x) and torch.equal(xh[:, F:].float(), hin.detach().to(torch.bfloat16).float())
+    dh = torch.randn(B, H, generator=g).to(DEV)
+    (h2 * dh).sum().backward()
+    dz = torch.zeros(B, 4 * H, device=DEV)
+    dc_out = torch.zeros(B, H, device=DEV)
+    dx = torch.zeros(B, F, device=DEV)
+    dh_prev = torch.zeros(B, H, device=DEV)
+    gflat = torch.zeros_like(m.store.flat, requires_grad=False)
+    hp.lstm_bwd_step(dh, None, None, None, gates, cout, c, done, dz, dc_out, dx, dh_prev)
+    hp.lstm_wgrad(xh, dz, gflat, rows_per_chunk=32)
+    torch.cuda.synchronize()
+    assert rel(dx, xr.grad) < 2e-2
+    assert rel(dh_prev, hin.grad) < 2e-2
+    lay = m.store.layout
+    for name in ("lstm.kernel", "lstm.bias"):
+        s_ = lay.by_name[name]
+        assert rel(gflat[s_.offset:s_.offset + s_.numel], flat.grad[s_.offset:s_.offset + s_.numel]) < 2e-2, name
+
+
+def test_engine_lstm_gradient_matches_oracle(hip_lib):
+    """LSTM engine update (carried state, episode resets) == autograd over the stored rollout."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.models.pathnet import ParamStore, bf16_ste, lstm_cell_ref
+    cfg = preset("reference")
+    cfg.tasks = ["Pong"]
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 2, 16, 5
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng = tr.engine
+    assert eng.lstm_hip
+    for _ in range(3):
+        tr.update()
+    T, P, E, B, A = eng.T, eng.P, eng.E, eng.B, eng.A
+    h0, c0 = eng.hst[0].float().clone(), eng.cst[0].clone()
+    eng.rollout_backward()
+    torch.cuda.synchronize()
+    a2c = cfg.a2c
+    flat = tr.model.store.flat.detach().clone().requires_grad_(True)
+    st = ParamStore(cfg.net, DEV, flat=flat)
+    k, bb = st.lstm()
+    kq = bf16_ste(k)
+    x = eng.obs[:T + 1].reshape((T + 1) * B, 160, 120, 4).float() / 255.0
+    mask = tr.model.mask.repeat_interleave(E, 0).repeat(T + 1, 1, 1)
+    feat = trunk_forward_ref(st, x, mask, emulate_bf16=True).view(T + 1, B, -1)
+    h, c = h0, c0
+    hs = []
+    for t in range(T + 1):
+        if t > 0:
+            keep = (1.0 - eng.dones[t - 1].float())[:, None]
+            h, c = h * keep, c * keep
+        h, c = lstm_cell_ref(bf16_ste(feat[t]), bf16_ste(h), c, kq, bb)
+        hs.append(h)
+    logits, values = heads_ref(st, bf16_ste(torch.stack(hs)).reshape((T + 1) * B, -1))
+    assert rel(logits[:T * B], eng.logits[:T].reshape(-1, A)) < 3e-2
+    R, adv = nstep_returns(eng.rewards, eng.values[:T], eng.dones.bool(), eng.values[T], a2c.gamma,
+                           a2c.gae_lambda, a2c.reward_clip)
+    loss, _, _, _ = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(), R.reshape(-1),
+                             adv.reshape(-1), a2c.entropy_beta, a2c.value_coef,
+                             torch.full((T * B,), 1.0 / E, device=DEV))
+    loss.backward()
+    errs = {}
+    for s_ in tr.model.store.layout.segments:
+        a, b = eng.grad_flat[s_.offset:s_.offset + s_.numel], flat.grad[s_.offset:s_.offset + s_.numel]
+        if b.norm() < 1e-7:
+            continue
+        errs[s_.name] = rel(a, b)
+    worst = max(errs, key=errs.get)
+    print({k_: round(v, 4) for k_, v in sorted(errs.items(), key=lambda kv: -kv[1])[:8]})
+    assert errs[worst] < 8e-2, (worst, errs[worst])
