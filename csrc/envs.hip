@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
     reset_state(st, seed, (uint32_t)env, ctr, no_op_max, frameskip);
     ctr += 1;
   }
-  __syncthreads();
+  __syncthreads();    // every wave has read state[] (and tab[] is staged) before thread 0 overwrites it
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int i = 0; i < NSTATE; ++i) state[env * NSTATE + i] = st.s[i];
@@ -168,10 +168,12 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
     epret_out[env] = done ? (float)epret : 0.f;
   }
   // --- fused render + gray + resize + stack push ---
-  // (1) the 210x160 gray image is evaluated ONCE per source pixel into LDS
-  //     (4 pixels per thread-iteration, one 32-bit LDS store);
-  // (2) every output pixel reads its 4 bilinear taps from LDS.
-  __shared__ uint32_t gray[210 * 160 / 4];
+  // Only the score band (source rows < TOP), the bottom wall edge and the columns/rects
+  // the paddles and the ball can occupy differ from the flat background, so each output
+  // pixel evaluates its 4 bilinear source taps analytically ONLY when one of them can
+  // touch such a region; everywhere else the bilinear of a constant is that constant.
+  // Four horizontally adjacent pixels per thread: one 16-byte load of the old stack,
+  // one 16-byte store of the new (frame-stack push: (in >> 8) | f << 24 per pixel).
   Scene S;
   S.cy = st.s[CY] >> 4;   // floor division by U=16 (values are non-negative)
   S.py = st.s[PY] >> 4;
@@ -181,26 +183,42 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
   S.cs_t = st.s[CS] / 10; S.cs_o = st.s[CS] % 10;
   S.ps_t = st.s[PS] / 10; S.ps_o = st.s[PS] % 10;
   S.g_bg = g_bg; S.g_wall = g_wall; S.g_cpu = g_cpu; S.g_player = g_player; S.g_ball = g_ball;
-  for (int q4 = threadIdx.x; q4 < 210 * 160 / 4; q4 += 256) {
-    const int r = q4 / 40, c0 = (q4 - r * 40) * 4;
-    uint32_t wv = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) wv |= (uint32_t)scene_gray(S, r, c0 + e) << (8 * e);
-    gray[q4] = wv;
-  }
-  __syncthreads();
-  const uint8_t* g8 = reinterpret_cast<const uint8_t*>(gray);
-  const long base = (long)env * OBS_H * OBS_W;
-  for (int pix = threadIdx.x; pix < OBS_H * OBS_W; pix += 256) {
-    const int y = pix / OBS_W, x = pix - y * OBS_W;
+  const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OBS_H * OBS_W / 4);
+  uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OBS_H * OBS_W / 4);
+  for (int q = threadIdx.x; q < OBS_H * OBS_W / 4; q += 256) {
+    const int y = q / (OBS_W / 4), x0 = (q - y * (OBS_W / 4)) * 4;
     const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
-    const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x], cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
-    const int ra = g8[ys0 * 160 + xs0] * cx0 + g8[ys0 * 160 + xs1] * cx1;
-    const int rb = g8[ys1 * 160 + xs0] * cx0 + g8[ys1 * 160 + xs1] * cx1;
-    int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
-    v = v < 0 ? 0 : (v > 255 ? 255 : v);
-    const uint32_t f = (uint32_t)v;
-    obs_out[base + pix] = done ? f * 0x01010101u : ((obs_in[base + pix] >> 8) | (f << 24));
+    const bool row_dyn = ys0 < TOP || ys1 >= BOTTOM;
+    const bool ball_rows = S.vis && ys1 >= S.by && ys0 < S.by + BALL_H;
+    const bool pl_rows = ys1 >= S.py && ys0 < S.py + PADDLE_H;
+    const bool cpu_rows = ys1 >= S.cy && ys0 < S.cy + PADDLE_H;
+    uint32_t f4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int x = x0 + e;
+      const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x];
+      const bool dyn = row_dyn || (ball_rows && xs1 >= S.bx && xs0 < S.bx + BALL_W) ||
+                       (pl_rows && xs1 >= PLAYER_X && xs0 < PLAYER_X + PADDLE_W) ||
+                       (cpu_rows && xs1 >= CPU_X && xs0 < CPU_X + PADDLE_W);
+      int v = g_bg;
+      if (dyn) {
+        const int cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
+        const int ra = scene_gray(S, ys0, xs0) * cx0 + scene_gray(S, ys0, xs1) * cx1;
+        const int rb = scene_gray(S, ys1, xs0) * cx0 + scene_gray(S, ys1, xs1) * cx1;
+        v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+        v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      }
+      f4[e] = (uint32_t)v;
+    }
+    uint4 o;
+    if (done) {
+      o = make_uint4(f4[0] * 0x01010101u, f4[1] * 0x01010101u, f4[2] * 0x01010101u, f4[3] * 0x01010101u);
+    } else {
+      const uint4 i = in4[q];
+      o = make_uint4((i.x >> 8) | (f4[0] << 24), (i.y >> 8) | (f4[1] << 24), (i.z >> 8) | (f4[2] << 24),
+                     (i.w >> 8) | (f4[3] << 24));
+    }
+    out4[q] = o;
   }
 }
 

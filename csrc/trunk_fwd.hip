@@ -275,6 +275,120 @@ __global__ __launch_bounds__(256) void fc_fwd_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// fc forward for the rollout (<= 32 rows per path): MODULE-PER-WAVE.
+// grid = (ceil(T*E/32), Cout/64, P); wave w computes the full 32x64 tile for
+// module slots w, w+4, ... (per-module bias+ReLU+bits in registers), the 4
+// waves' module sums meet in LDS.  Each wave runs a register double-buffered
+// K loop (next k-step's A/B fragments in flight during this step's 8 MFMAs),
+// so a path's active modules stream their weights in parallel instead of one
+// after another -- the per-step fc layers are latency-bound, not FLOP-bound.
+// ---------------------------------------------------------------------------
+template <int RT>
+__global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
+    const bf16_t* __restrict__ X, int ldx, bf16_t* __restrict__ Y, uint16_t* __restrict__ bits,
+    const bf16_t* __restrict__ Wc, const float* __restrict__ flat, long bias_off, int chunk,
+    const int* __restrict__ act_idx, const int* __restrict__ act_cnt, int layer, int L, int M,
+    int K, int KP, int Cout, int P, int E, int T, int t0, long bits_rows, float out_scale) {
+  __shared__ float part[4][32][64 + 1];
+  const int p = blockIdx.z;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const long Rtot = (long)T * E;
+  const int PE = P * E;
+  const long row0 = (long)blockIdx.x * 32;
+  const int col0 = blockIdx.y * 64;
+  long xrow[RT];
+  bool xv[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) {
+    const long r = row0 + i * 16 + c16;
+    xv[i] = r < Rtot;
+    xrow[i] = sample_global(p, (int)(xv[i] ? r : row0), E, PE, t0) * ldx;
+  }
+  float sum[RT][4][4];
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sum[i][j][r] = 0.f;
+  const int nwords = Cout / 16;
+  for (int a = w; a < cnt; a += 4) {
+    const int mod = act_idx[(p * L + layer) * M + a];
+    const bf16_t* Wm = Wc + (long)mod * Cout * KP + (long)(col0 + c16) * KP + 8 * grp;
+    f4v acc[RT][4];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+    s8v an[RT], bn[4];
+    auto load = [&](int kk) {
+      const int k0 = kk + 8 * grp;
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+        an[i] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+        if (xv[i] && k0 < K) an[i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bn[j] = *reinterpret_cast<const s8v*>(Wm + (long)j * 16 * KP + kk);
+    };
+    load(0);
+    for (int kk = 0; kk < KP; kk += 32) {
+      s8v ac[RT], bc[4];
+#pragma unroll
+      for (int i = 0; i < RT; ++i) ac[i] = an[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bc[j] = bn[j];
+      if (kk + 32 < KP) load(kk + 32);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < RT; ++i) acc[i][j] = mfma16(ac[i], bc[j], acc[i][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float bb = flat[bias_off + (long)mod * chunk + col0 + j * 16 + c16];
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r] + bb;
+          const bool pos = v > 0.f;
+          sum[i][j][r] += pos ? v : 0.f;
+          const uint64_t bal = __ballot(pos);
+          const long row = row0 + i * 16 + 4 * grp + r;
+          if (c16 == 0 && row < Rtot) {
+            const long sg = sample_global(p, (int)row, E, PE, t0);
+            bits[((long)a * bits_rows + sg) * nwords + (col0 + j * 16) / 16] =
+                (uint16_t)((bal >> (16 * grp)) & 0xFFFFull);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[w][i * 16 + 4 * grp + r][j * 16 + c16] = sum[i][j][r];
+  __syncthreads();
+  // 256 threads: 32 rows x 64 cols -> 8 outputs each (one row, 8 consecutive cols)
+  const int orow = tid >> 3, oc = (tid & 7) * 8;
+  const long row = row0 + orow;
+  if (orow < RT * 16 && row < Rtot) {
+    const long sg = sample_global(p, (int)row, E, PE, t0);
+    float o[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      o[c] = (part[0][orow][oc + c] + part[1][orow][oc + c] + part[2][orow][oc + c] + part[3][orow][oc + c]) *
+             out_scale;
+    *reinterpret_cast<s8v*>(Y + sg * Cout + col0 + oc) = f32x8_to_bf16(o);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 extern "C" {
@@ -309,7 +423,17 @@ int launch_fc_fwd(const void* X, int ldx, void* Y, void* bits, const void* Wc, c
                   int P, int E, int T, int t0, long bits_rows, float out_scale, hipStream_t stream) {
   if (M > MAXM || KP % 32 != 0 || Cout % 32 != 0 || ldx % 8 != 0) return -1;
   const long rows = (long)T * E;
-  if (rows <= 32) {
+  if (rows <= 32 && Cout % 64 == 0) {
+    dim3 grid(1, Cout / 64, P);
+    if (rows <= 16)
+      fc_fwd_mw_kernel<1><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
+                                                    (const bf16_t*)Wc, flat, bias_off, chunk, act_idx, act_cnt, layer,
+                                                    L, M, K, KP, Cout, P, E, T, t0, bits_rows, out_scale);
+    else
+      fc_fwd_mw_kernel<2><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
+                                                    (const bf16_t*)Wc, flat, bias_off, chunk, act_idx, act_cnt, layer,
+                                                    L, M, K, KP, Cout, P, E, T, t0, bits_rows, out_scale);
+  } else if (rows <= 32) {
     dim3 grid((unsigned)((rows + 31) / 32), (Cout + 63) / 64, P);
     fc_fwd_kernel<32><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
                                                 (const bf16_t*)Wc, flat, bias_off, chunk, act_idx, act_cnt, layer, L,

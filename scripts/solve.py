@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--curve", default="gpurun_out/solve_curve.jsonl")
     ap.add_argument("--report-every", type=float, default=30.0, help="seconds between progress lines")
     ap.add_argument("--keep-going", action="store_true", help="continue after solving until --minutes")
+    ap.add_argument("--debug", action="store_true", help="inspect engine buffers on counter anomalies")
+    ap.add_argument("--no-ga", action="store_true", help="disable tournaments (pure A2C on fixed paths)")
+    ap.add_argument("--N", type=int, default=None, help="active modules per layer in the initial genotypes")
     args = ap.parse_args()
 
     import torch
@@ -69,6 +72,8 @@ def main():
         cfg.net.trunk_scale = args.trunk_scale
     if args.gae_lambda is not None:
         cfg.a2c.gae_lambda = args.gae_lambda
+    if args.N is not None:
+        cfg.net.N = args.N
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
     cfg.ga.concurrent_tournaments = args.concurrent or max(1, (cfg.paths * ctx.world) // 16)
@@ -76,6 +81,8 @@ def main():
         from pathnet_gym_amd import _build
         _build.build()
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
+    if args.no_ga:
+        tr.pop.step = lambda *a, **k: []
     thr = reward_threshold(cfg.tasks[0])
     curve = None
     if ctx.is_main and args.curve:
@@ -90,8 +97,16 @@ def main():
     while True:
         st = tr.update()
         if not math.isnan(st.mean_return) and abs(st.mean_return) > 1000 and ctx.is_main:
-            print(json.dumps({"anomaly": "mean_return", "value": st.mean_return, "episodes": st.episodes,
-                              "update": tr.updates}), flush=True)
+            rec = {"anomaly": "mean_return", "value": st.mean_return, "episodes": st.episodes, "update": tr.updates}
+            eng = tr.engine
+            if eng is not None and args.debug:
+                d = eng.dones.bool()
+                er = eng.epret[d]
+                rec.update(ref_count=int(d.sum()), ref_sum=float(er.sum()), counters=eng.counters.tolist(),
+                           big=torch.nonzero(d & (eng.epret.abs() > 21))[:4].tolist(),
+                           big_vals=eng.epret[d & (eng.epret.abs() > 21)][:4].tolist(),
+                           nonzero_epret_not_done=int(((eng.epret != 0) & ~d).sum()))
+            print(json.dumps(rec), flush=True)
         elif not math.isnan(st.mean_return):
             ret_ema = st.mean_return if ret_ema is None else 0.9 * ret_ema + 0.1 * st.mean_return
         if st.tournaments:

@@ -484,7 +484,7 @@ def test_engine_lstm_gradient_matches_oracle(hip_lib):
     from pathnet_gym_amd.models.pathnet import ParamStore, bf16_ste, lstm_cell_ref
     cfg = preset("reference")
     cfg.tasks = ["Pong"]
-    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 2, 16, 5
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 5
     tr = PathNetTrainer(cfg, device=DEV)
     eng = tr.engine
     assert eng.lstm_hip
