@@ -202,6 +202,177 @@ __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X,
   }
 }
 
+template <class G, int OB>
+struct Slab {
+  static constexpr int RL = G::WIN * G::CIN;               // input row length (elements)
+  static constexpr int PS = G::S * G::CIN;                 // position stride within a row
+  static constexpr int SEG = G::KW * G::CIN;               // one kernel row of k
+  static constexpr int NB = (G::HO + OB - 1) / OB;         // bands per sample
+  static constexpr int NPOS = OB * G::WO;                  // positions per (full) band
+  static constexpr int KS = (NPOS + 31) / 32;              // MFMA k-steps per stage
+  static constexpr int SR = (OB - 1) * G::S + G::KH;       // slab rows
+  static constexpr int SLAB = SR * RL;                     // slab elements
+  static constexpr int SLABP = SLAB + 64;                  // + zeroed slack for padded positions
+  static constexpr int NG8 = SLAB / 8;                     // 8-element groups per slab
+  static constexpr int XIT = (NG8 + 255) / 256;
+  static_assert(SEG == 32 && PS == 16, "slab wgrad needs KW*CIN == 32 and S*CIN == 16");
+  static_assert(SLAB % 8 == 0, "slab must be a whole number of 8-element groups");
+};
+
+// ===========================================================================
+// forward, LDS-slab implicit im2col (KW*CIN == 32, S*CIN == 16 geometries).
+// grid = (chunks, P); 256 threads.  The path's active module weights are staged
+// once in LDS (B fragments), so the unit loop only streams the input: per unit (one sample's band of OB output rows) the touched input rows
+// are one contiguous range, copied + converted once into LDS (double-buffered,
+// register prefetch); each A fragment (8 consecutive k of one position = one
+// 16-byte run of a kernel row) is a single ds_read_b128 from the slab.
+// Epilogue: bias + ReLU + ReLU bits (ballot) + module sum, as conv_fwd_fast.
+// ===========================================================================
+template <class G, int OB>
+__global__ __launch_bounds__(256, 2) void conv_fwd_slab(const void* __restrict__ X, bf16_t* __restrict__ Y,
+                                                        uint8_t* __restrict__ bits, const bf16_t* __restrict__ Wc,
+                                                        const float* __restrict__ flat, long bias_off, int chunk,
+                                                        const int* __restrict__ act_idx,
+                                                        const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                        int P, int E, int T, int t0, long bits_rows, int units_per_wg,
+                                                        float in_scale, float out_scale) {
+  using SB = Slab<G, OB>;
+  constexpr int NK = G::KP / 32;                           // = KH (one kernel row per k-step)
+  constexpr int NRT = (SB::NPOS + 15) / 16;                // 16-row tiles per unit
+  constexpr int RTW = (NRT + 3) / 4;                       // row tiles per wave
+  static_assert(NK == G::KH, "one kernel row per 32-wide k-step");
+  constexpr int KPs = G::KP + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t Ws[NCT * 16 * KPs];
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][SB::SLABP];
+  __shared__ float bias_s[NCT * 16];
+  __shared__ int mods[MAXM_F];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
+  if (tid < MAXM_F) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  for (int i = tid; i < 2 * 64; i += 256) Xs[i >> 6][SB::SLAB + (i & 63)] = 0;
+  __syncthreads();
+  if (tid < NCT * 16) bias_s[tid] = (tid >> 3) < cnt ? flat[bias_off + (long)mods[tid >> 3] * chunk + (tid & 7)] : 0.f;
+  // active module weights staged once: Ws[col = slot*8 + map][k] (B operand rows)
+  for (int i = tid; i < nct * 16 * G::KC; i += 256) {
+    const int col = i / G::KC, kc = i - col * G::KC;
+    const int slot = col >> 3;
+    s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (slot < cnt) v = *reinterpret_cast<const s8v*>(Wc + ((long)(mods[slot] * 8 + (col & 7))) * G::KP + kc * 8);
+    *reinterpret_cast<s8v*>(Ws + col * KPs + kc * 8) = v;
+  }
+  const int PE = P * E;
+  const int nunits = T * E * SB::NB;
+  const int u_beg = blockIdx.x * units_per_wg;
+  const int u_end = min(nunits, u_beg + units_per_wg);
+  // per-lane A offsets (row = position rho = tile*16 + c16) and epilogue rows (tile*16 + 4q + r)
+  int aoff[RTW];
+#pragma unroll
+  for (int i = 0; i < RTW; ++i) {
+    int rho = (w + 4 * i) * 16 + c16;
+    if (rho >= SB::NPOS) rho = 0;
+    const int ob = rho / G::WO, ow = rho - ob * G::WO;
+    aoff[i] = ob * G::S * SB::RL + ow * SB::PS + 8 * grp;
+  }
+  using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
+  XRaw xr[SB::XIT];
+  auto load_stage = [&](int u) {
+    const int s = u / SB::NB, band = u - s * SB::NB;
+    const long sg = sample_global(p, s, E, PE, t0);
+    const int ih0 = band * OB * G::S;
+    const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;
+    const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
+#pragma unroll
+    for (int j = 0; j < SB::XIT; ++j) {
+      const int gi = tid + 256 * j;
+      const int e0 = gi * 8;
+      if constexpr (G::U8) {
+        xr[j] = make_uint2(0u, 0u);
+        if (gi < SB::NG8 && e0 < navail)
+          xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xbase + e0);
+      } else {
+        xr[j] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+        if (gi < SB::NG8 && e0 < navail)
+          xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xbase + e0);
+      }
+    }
+  };
+  if (u_beg < u_end) load_stage(u_beg);
+  int buf = 0;
+  for (int u = u_beg; u < u_end; ++u, buf ^= 1) {
+#pragma unroll
+    for (int j = 0; j < SB::XIT; ++j) {
+      const int gi = tid + 256 * j;
+      if (gi < SB::NG8) {
+        s8v v;
+        if constexpr (G::U8) v = u8x8_to_bf16(xr[j]);
+        else v = xr[j];
+        *reinterpret_cast<s8v*>(&Xs[buf][gi * 8]) = v;
+      }
+    }
+    __syncthreads();
+    const int s = u / SB::NB, band = u - s * SB::NB;
+    const long sg = sample_global(p, s, E, PE, t0);
+    const long grow0 = sg * G::HOWO + (long)band * OB * G::WO;     // global row of position 0 of the band
+    const int npos = min(OB, G::HO - band * OB) * G::WO;
+    if (u + 1 < u_end) load_stage(u + 1);
+    const bf16_t* xs = Xs[buf];
+#pragma unroll
+    for (int i = 0; i < RTW; ++i) {
+      const int rt = w + 4 * i;
+      if (rt >= NRT) break;
+      f4v acc[NCT];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) acc[ct] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const s8v a = *reinterpret_cast<const s8v*>(xs + kk * SB::RL + aoff[i]);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+          if (ct < nct) {
+            const s8v b = *reinterpret_cast<const s8v*>(Ws + (ct * 16 + c16) * KPs + kk * 32 + 8 * grp);
+            acc[ct] = mfma16(a, b, acc[ct]);
+          }
+      }
+      float sum[4] = {0.f, 0.f, 0.f, 0.f};
+      const int rho0 = rt * 16 + 4 * q;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        if (ct < nct) {
+          const int slot = ct * 2 + h;
+          const bool sv = slot < cnt;
+          const float bb = bias_s[ct * 16 + c16];
+          uint32_t word = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = acc[ct][r] * in_scale + bb;
+            const bool pos = sv && v > 0.f;
+            sum[r] += pos ? v : 0.f;
+            const uint64_t bal = __ballot(pos);
+            word |= (uint32_t)((bal >> (16 * q + 8 * h)) & 0xFFull) << (8 * r);
+          }
+          if (ch == 0 && sv) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (rho0 + r < npos) bits[(long)slot * bits_rows + grow0 + rho0 + r] = (uint8_t)(word >> (8 * r));
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
+      if (h == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (rho0 + r < npos) Y[(grow0 + rho0 + r) * 8 + ch] = f2bf(sum[r] * out_scale);
+      }
+    }
+    // no trailing barrier: the next unit writes the other buffer, and this one is only rewritten
+    // after every wave has passed the next unit's post-write barrier (i.e. finished this unit)
+  }
+}
+
 // ===========================================================================
 // wgrad: grid = (nchunks, P), 512 threads (8 waves), 32-row stages, register
 // prefetch + double-buffered LDS: one barrier per stage; stage i+1's global
@@ -395,6 +566,216 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
 }
 
 // ===========================================================================
+// wgrad, LDS-slab implicit im2col (geometries with KW*CIN == 32 and S*CIN == 16:
+// the 160x120x4/8x8/s4 and 39x29x8/4x4/s2 layers).  A stage is a band of OB output
+// rows of one sample: the input rows it touches are ONE contiguous range of the
+// image, copied (and u8->bf16 converted) once into LDS; the MFMA A operand
+// (im2col^T: m = k, reduction = position) is read straight out of that slab with
+// ds_read_b64_tr_b16 -- position rows are 16 elements apart and the 32 k of one
+// kernel row are contiguous, so no im2col copy is ever materialised (each input
+// byte is converted once per stage instead of KH*KW/S^2 times).  Positions of the
+// band are packed densely into 32-row MFMA k-steps.  Masked G (ReLU bits) goes to
+// LDS as bf16 as before.  Register prefetch of the next stage + double-buffered LDS.
+// grid = (chunks, P); 256 threads; each workgroup reduces a contiguous range of
+// (sample, band) units and atomically adds its partial dW/db.
+// ===========================================================================
+
+template <class G, int OB>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict__ X, const float* __restrict__ Gr,
+                                                          const uint8_t* __restrict__ bits, float* __restrict__ grad,
+                                                          long w_off, long b_off, int chunk,
+                                                          const int* __restrict__ act_idx,
+                                                          const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                          int P, int E, int T, long bits_rows, int units_per_wg,
+                                                          float in_scale, float g_scale) {
+  using SB = Slab<G, OB>;
+  constexpr int GS = NCT * 16 + 8;
+  constexpr int NMT = G::KP / 16;
+  constexpr int MPW = NMT / 4;
+  constexpr int GROWS = SB::KS * 32;
+  constexpr int GIT = (GROWS * 4 + 255) / 256;             // (row, slot-group) items per thread
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][SB::SLABP];
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][GROWS * GS];
+  __shared__ float dbias[NCT * 16];
+  __shared__ int mods[MAXM_F];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  if (cnt == 0) return;
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
+  if (tid < MAXM_F) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  if (tid < NCT * 16) dbias[tid] = 0.f;
+  for (int i = tid; i < 2 * GROWS * GS; i += 256) (&Gs[0][0])[i] = 0;
+  for (int i = tid; i < 2 * 64; i += 256) Xs[i >> 6][SB::SLAB + (i & 63)] = 0;
+  const int PE = P * E;
+  const int nunits = T * E * SB::NB;
+  const int u_beg = blockIdx.x * units_per_wg;
+  const int u_end = min(nunits, u_beg + units_per_wg);
+  // per-lane A-operand position offsets inside the slab for each k-step (two 4-row halves)
+  int aoff[SB::KS][2];
+#pragma unroll
+  for (int ks = 0; ks < SB::KS; ++ks)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      int rho = ks * 32 + 8 * grp + 4 * hf + q;
+      if (rho >= SB::NPOS) rho = 0;                     // padded position: G row is zero
+      const int ob = rho / G::WO, ow = rho - ob * G::WO;
+      aoff[ks][hf] = ob * G::S * SB::RL + ow * SB::PS + 4 * pp;
+    }
+  float acc_b[3][8];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc_b[k][c] = 0.f;
+  f4v acc[MPW][NCT];
+#pragma unroll
+  for (int a = 0; a < MPW; ++a)
+#pragma unroll
+    for (int b = 0; b < NCT; ++b) acc[a][b] = {0.f, 0.f, 0.f, 0.f};
+
+  using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
+  XRaw xr[SB::XIT];
+  float4 g0r[GIT], g1r[GIT];
+  uint32_t gbr[GIT][3];
+  bool gvr[GIT];
+
+  auto load_stage = [&](int u) {
+    const int s = u / SB::NB, band = u - s * SB::NB;
+    const long sg = sample_global(p, s, E, PE, 0);
+    const int ih0 = band * OB * G::S;
+    const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;   // elements inside the image
+    const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
+#pragma unroll
+    for (int j = 0; j < SB::XIT; ++j) {
+      const int gi = tid + 256 * j;
+      const int e0 = gi * 8;
+      if constexpr (G::U8) {
+        xr[j] = make_uint2(0u, 0u);
+        if (gi < SB::NG8 && e0 < navail)
+          xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xbase + e0);
+      } else {
+        xr[j] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+        if (gi < SB::NG8 && e0 < navail)
+          xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xbase + e0);
+      }
+    }
+    const int oh0 = band * OB;
+#pragma unroll
+    for (int j = 0; j < GIT; ++j) {
+      const int it = tid + 256 * j;
+      const int rho = it >> 2, sub = it & 3;
+      const int ob = rho / G::WO, ow = rho - ob * G::WO;
+      gvr[j] = it < GROWS * 4 && rho < SB::NPOS && oh0 + ob < G::HO;
+      if (gvr[j]) {
+        const long go = sg * G::HOWO + (oh0 + ob) * G::WO + ow;
+        g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+        g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int slot = sub + 4 * k;
+          gbr[j][k] = slot < cnt ? bits[(long)slot * bits_rows + go] : 0u;
+        }
+      }
+    }
+  };
+  auto write_stage = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < SB::XIT; ++j) {
+      const int gi = tid + 256 * j;
+      if (gi < SB::NG8) {
+        s8v v;
+        if constexpr (G::U8) v = u8x8_to_bf16(xr[j]);
+        else v = xr[j];
+        *reinterpret_cast<s8v*>(&Xs[buf][gi * 8]) = v;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < GIT; ++j) {
+      const int it = tid + 256 * j;
+      if (it >= GROWS * 4) continue;
+      const int rho = it >> 2, sub = it & 3;
+      const float gg[8] = {g0r[j].x, g0r[j].y, g0r[j].z, g0r[j].w, g1r[j].x, g1r[j].y, g1r[j].z, g1r[j].w};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int slot = sub + 4 * k;
+        if (slot < 2 * nct) {
+          float m[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) m[c] = (gvr[j] && ((gbr[j][k] >> c) & 1u)) ? gg[c] : 0.f;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) acc_b[k][c] += m[c];
+          *reinterpret_cast<s8v*>(&Gs[buf][rho * GS + slot * 8]) = f32x8_to_bf16(m);
+        }
+      }
+    }
+  };
+  __syncthreads();
+  if (u_beg < u_end) load_stage(u_beg);
+  int buf = 0;
+  for (int u = u_beg; u < u_end; ++u, buf ^= 1) {
+    write_stage(buf);
+    __syncthreads();
+    if (u + 1 < u_end) load_stage(u + 1);
+    const bf16_t* xs = Xs[buf];
+    const bf16_t* gs = Gs[buf];
+#pragma unroll
+    for (int ks = 0; ks < SB::KS; ++ks) {
+      s8v bfr[NCT];
+#pragma unroll
+      for (int nt = 0; nt < NCT; ++nt) {
+        if (nt < nct) {
+          const s4v v0 = lds_tr16(gs + (ks * 32 + 8 * grp + q) * GS + nt * 16 + 4 * pp);
+          const s4v v1 = lds_tr16(gs + (ks * 32 + 8 * grp + 4 + q) * GS + nt * 16 + 4 * pp);
+          bfr[nt] = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        }
+      }
+#pragma unroll
+      for (int mi = 0; mi < MPW; ++mi) {
+        const int mt = w * MPW + mi;
+        const int kb = (mt * 16 / SB::SEG) * SB::RL + (mt * 16) % SB::SEG;     // kernel row kh, k offset
+        const s4v v0 = lds_tr16(xs + kb + aoff[ks][0]);
+        const s4v v1 = lds_tr16(xs + kb + aoff[ks][1]);
+        const s8v afr = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int nt = 0; nt < NCT; ++nt)
+          if (nt < nct) acc[mi][nt] = mfma16(afr, bfr[nt], acc[mi][nt]);
+      }
+    }
+  }
+  const int h = i16 >> 3, ch = l & 7;
+#pragma unroll
+  for (int mi = 0; mi < MPW; ++mi) {
+    const int mt = w * MPW + mi;
+#pragma unroll
+    for (int nt = 0; nt < NCT; ++nt) {
+      if (nt < nct) {
+        const int slot = nt * 2 + h;
+        if (slot < cnt) {
+          const long base = w_off + (long)mods[slot] * chunk;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = mt * 16 + 4 * grp + r;
+            if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale));
+          }
+        }
+      }
+    }
+  }
+  // bias: this thread's partials for slots (tid & 3) + 4k
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int slot = (tid & 3) + 4 * k;
+    if (slot < cnt) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) atomicAdd(&dbias[slot * 8 + c], acc_b[k][c] * g_scale);
+    }
+  }
+  __syncthreads();
+  if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
+}
+
+// ===========================================================================
 // dgrad (Cin = Cout = 8): grid = (ceil(T*E*NI*NJ/256), S*S, P), class (ph,pw) = blockIdx.y
 // ===========================================================================
 template <class G>
@@ -490,6 +871,35 @@ static int wgrad_t(const void* X, const float* Gr, const void* bits, float* grad
   return (int)hipGetLastError();
 }
 
+template <class G, int OB>
+static int fwd_slab_t(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off, int chunk,
+                      const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0, long br,
+                      float is, float os, hipStream_t st) {
+  using SB = Slab<G, OB>;
+  const long units = (long)T * E * SB::NB;
+  long upw = (units + 15) / 16;                 // ~16 workgroups per path
+  if (upw < 4) upw = 4;
+  dim3 grid((unsigned)((units + upw - 1) / upw), P);
+  conv_fwd_slab<G, OB><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat, bias_off, chunk,
+                                             ai, ac, layer, L, M, P, E, T, t0, br, (int)upw, is, os);
+  return (int)hipGetLastError();
+}
+
+template <class G, int OB>
+static int wgrad_slab_t(const void* X, const float* Gr, const void* bits, float* grad, long w_off, long b_off,
+                        int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, long br,
+                        float is, float gs, hipStream_t st) {
+  using SB = Slab<G, OB>;
+  const long units = (long)T * E * SB::NB;
+  // ~24 workgroups per path (>= 1.5K workgroups at P=64), at least 8 units each
+  long upw = (units + 23) / 24;
+  if (upw < 8) upw = 8;
+  dim3 grid((unsigned)((units + upw - 1) / upw), P);
+  conv_wgrad_slab<G, OB><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer,
+                                               L, M, P, E, T, br, (int)upw, is, gs);
+  return (int)hipGetLastError();
+}
+
 template <class G>
 static int dgrad_t(const float* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,
                    const int* ac, int layer, int L, int M, int P, int E, int T, long br, float gs, float* dX,
@@ -509,7 +919,12 @@ static bool is_shape(int Hin, int Win, int Cin, int KH, int KW, int S, int u8) {
          (u8 != 0) == G::U8;
 }
 
+static int SLAB_WGRAD = 1;
+static int SLAB_FWD = 1;
+
 extern "C" {
+void fast_conv_set_slab(int on) { SLAB_WGRAD = on; SLAB_FWD = on; }
+
 // return 1 if handled by a fast kernel, 0 if the shape is not specialised, <0 on error
 int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
                   int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH,
@@ -520,6 +935,11 @@ int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, 
     if ((E * Gx::HOWO) % 16) return -2;                                                                      \
     const int rc = fwd_t<Gx>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st); \
     return rc ? -rc : 1;                                                                                     \
+  }
+  if (SLAB_FWD && is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) {
+    const int rc = fwd_slab_t<C1, 2>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is,
+                                     os, st);
+    return rc ? -rc : 1;
   }
   FWD(C1) FWD(C2) FWD(C3)
 #undef FWD
@@ -534,6 +954,16 @@ int fast_conv_wgrad(const void* X, int u8in, const float* Gr, const void* bits, 
   if (is_shape<Gx>(Hin, Win, Cin, KH, KW, S, u8in)) {                                                          \
     const int rc = wgrad_t<Gx>(X, Gr, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, is, gs, st); \
     return rc ? -rc : 1;                                                                                       \
+  }
+  if (SLAB_WGRAD && is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) {
+    const int rc = wgrad_slab_t<C1, 2>(X, Gr, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, is, gs,
+                                       st);
+    return rc ? -rc : 1;
+  }
+  if (SLAB_WGRAD && is_shape<C2>(Hin, Win, Cin, KH, KW, S, u8in)) {
+    const int rc = wgrad_slab_t<C2, 7>(X, Gr, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, is, gs,
+                                       st);
+    return rc ? -rc : 1;
   }
   WG(C1) WG(C2) WG(C3)
 #undef WG

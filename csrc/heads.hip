@@ -244,7 +244,11 @@ int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float*
 // counters: [0] agent steps, [1] episodes finished, [2] sum of their returns.
 // ---------------------------------------------------------------------------
 __global__ void fitness_update_kernel(const uint8_t* __restrict__ dones, const float* __restrict__ epret, int T, int P,
-                                      int E, float* __restrict__ fitness, float* __restrict__ counters) {
+                                      int E, float* __restrict__ fitness, float* __restrict__ counters,
+                                      float* __restrict__ fit_cnt, float* __restrict__ fit_sum, int window) {
+  // window == 0: fitness = return of the most recently finished episode(s) (a3c_training_thread.py:145-147);
+  // window >= 1: fitness = mean return of the episodes finished since the path's last tournament,
+  //              pending (-1000) until at least `window` of them have finished.
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p == 0) counters[0] = (float)T * P * E;
   if (p >= P) return;
@@ -260,14 +264,22 @@ __global__ void fitness_update_kernel(const uint8_t* __restrict__ dones, const f
     nep += c;
     sret += s;
   }
+  if (window > 0) {
+    const float cnt = fit_cnt[p] + nep, sum = fit_sum[p] + sret;
+    fit_cnt[p] = cnt;
+    fit_sum[p] = sum;
+    fit = cnt >= (float)window ? sum / cnt : -1000.f;
+  }
   fitness[p] = fit;
   atomicAdd(&counters[1], nep);
   atomicAdd(&counters[2], sret);
 }
 
 extern "C" int launch_fitness_update(const void* dones, const float* epret, int T, int P, int E, float* fitness,
-                                     float* counters, hipStream_t stream) {
+                                     float* counters, float* fit_cnt, float* fit_sum, int window,
+                                     hipStream_t stream) {
   hipMemsetAsync(counters, 0, sizeof(float) * 4, stream);
-  fitness_update_kernel<<<(P + 63) / 64, 64, 0, stream>>>((const uint8_t*)dones, epret, T, P, E, fitness, counters);
+  fitness_update_kernel<<<(P + 63) / 64, 64, 0, stream>>>((const uint8_t*)dones, epret, T, P, E, fitness, counters,
+                                                          fit_cnt, fit_sum, window);
   return (int)hipGetLastError();
 }

@@ -313,6 +313,110 @@ __global__ __launch_bounds__(256) void fc_dgrad_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// fc dgrad, LDS-staged: grid = (ceil(T*E/64), P, KSPLIT), 512 threads (8 waves).
+// The masked bf16 gradient of up to 4 active modules for the workgroup's 64 rows
+// is built ONCE in LDS (G read once per row, ReLU bits applied per module), then
+// every 128-column chunk of dX is swept: wave w owns 16 columns x 64 rows, so each
+// weight fragment (global, WcT [M][KP][Cout]) feeds 4 MFMAs and each LDS A
+// fragment is a plain ds_read_b128.  >4 active modules: further groups of 4
+// accumulate into dX (the workgroup owns those outputs: no atomics).
+// ---------------------------------------------------------------------------
+template <int COUT>
+__global__ __launch_bounds__(512) void fc_dgrad_lds_kernel(
+    const float* __restrict__ G, const uint16_t* __restrict__ bits, const bf16_t* __restrict__ WcT,
+    const int* __restrict__ act_idx, const int* __restrict__ act_cnt, int layer, int L, int M, int K, int KP, int P,
+    int E, int T, long bits_rows, float g_scale, float* __restrict__ dX, int chunks_per_split) {
+  constexpr int CS = COUT + 8;
+  constexpr int NW = COUT / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[4 * 64 * CS];   // 132 KiB at COUT=256 (1 WG/CU)
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const long R = (long)T * E;
+  const int PE = P * E;
+  const long row0 = (long)blockIdx.x * 64;
+  const int nchunks = (K + 127) / 128;
+  const int ch_beg = blockIdx.z * chunks_per_split;
+  const int ch_end = min(nchunks, ch_beg + chunks_per_split);
+  if (ch_beg >= ch_end) return;
+  // epilogue rows of this lane
+  long sg_out[4][4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long row = row0 + rb * 16 + 4 * grp + r;
+      sg_out[rb][r] = row < R ? sample_global(p, (int)row, E, PE, 0) : -1;
+    }
+  const int ngroups = cnt > 0 ? (cnt + 3) / 4 : 1;
+  for (int gi = 0; gi < ngroups; ++gi) {
+    const int g0 = gi * 4;
+    const int ng = min(4, cnt - g0);
+    __syncthreads();
+    {   // stage: thread -> (row sr, column segment); G read once, masked per module
+      constexpr int SEG = COUT / 8;                 // 8 threads per row
+      const int sr = tid >> 3, c0 = (tid & 7) * SEG;
+      const long r = row0 + sr;
+      const bool v = r < R;
+      const long sg = v ? sample_global(p, (int)r, E, PE, 0) : 0;
+#pragma unroll
+      for (int cc = 0; cc < SEG; cc += 8) {
+        const int c = c0 + cc;
+        float gv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (v) {
+          const float4 a0 = *reinterpret_cast<const float4*>(G + sg * COUT + c);
+          const float4 a1 = *reinterpret_cast<const float4*>(G + sg * COUT + c + 4);
+          gv[0] = a0.x * g_scale; gv[1] = a0.y * g_scale; gv[2] = a0.z * g_scale; gv[3] = a0.w * g_scale;
+          gv[4] = a1.x * g_scale; gv[5] = a1.y * g_scale; gv[6] = a1.z * g_scale; gv[7] = a1.w * g_scale;
+        }
+        for (int a = 0; a < ng; ++a) {
+          const uint32_t bw = v ? ((uint32_t)bits[((long)(g0 + a) * bits_rows + sg) * NW + (c >> 4)] >> (c & 15)) : 0u;
+          float m[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = ((bw >> j) & 1u) ? gv[j] : 0.f;
+          *reinterpret_cast<s8v*>(Gs + (a * 64 + sr) * CS + c) = f32x8_to_bf16(m);
+        }
+      }
+    }
+    __syncthreads();
+    for (int ch = ch_beg; ch < ch_end; ++ch) {
+      const int kcol = ch * 128 + w * 16 + c16;
+      f4v acc[4];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) acc[rb] = {0.f, 0.f, 0.f, 0.f};
+      for (int a = 0; a < ng; ++a) {
+        const int mod = act_idx[(p * L + layer) * M + g0 + a];
+        const bf16_t* Wm = WcT + (long)mod * KP * COUT + (long)kcol * COUT + 8 * grp;
+        const bf16_t* As = Gs + (a * 64 + c16) * CS + 8 * grp;
+#pragma unroll
+        for (int cs = 0; cs < COUT; cs += 32) {
+          s8v b = {0, 0, 0, 0, 0, 0, 0, 0};
+          if (kcol < KP) b = *reinterpret_cast<const s8v*>(Wm + cs);
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            const s8v af = *reinterpret_cast<const s8v*>(As + rb * 16 * CS + cs);
+            acc[rb] = mfma16(af, b, acc[rb]);
+          }
+        }
+      }
+      if (kcol < K) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const long sg = sg_out[rb][r];
+            if (sg >= 0) {
+              float* o = dX + sg * K + kcol;
+              *o = gi == 0 ? acc[rb][r] : *o + acc[rb][r];
+            }
+          }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // fc wgrad, module-major.  grid = (ceil(K/64), ceil(Cout/64), M).
 // inv_path/inv_slot: [L][M][Pmax] the (path, slot) pairs using module j; inv_cnt [L][M]
 // ---------------------------------------------------------------------------
@@ -320,13 +424,17 @@ __global__ __launch_bounds__(256) void fc_wgrad_kernel(
     const bf16_t* __restrict__ X, int ldx, const float* __restrict__ G, const uint16_t* __restrict__ bits,
     float* __restrict__ grad, long w_off, long b_off, int chunk, const int* __restrict__ inv_path,
     const int* __restrict__ inv_slot, const int* __restrict__ inv_cnt, int layer, int M, int Pmax, int K, int Cout,
-    int P, int E, int T, long bits_rows, float g_scale) {
+    int P, int E, int T, long bits_rows, float g_scale, int nsplit) {
   constexpr int S = 64 + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[32 * S];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[32 * S];
   __shared__ float dbias[64];
-  const int j = blockIdx.z;
-  const int n_use = inv_cnt[layer * M + j];
+  // blockIdx.z = module * nsplit + split: the (path, slot) users of a module are split across
+  // nsplit workgroups that accumulate with fp32 atomics (grad is zeroed before the backward)
+  const int j = blockIdx.z / nsplit, split = blockIdx.z - j * nsplit;
+  const int n_all = inv_cnt[layer * M + j];
+  const int u_beg = (int)((long)n_all * split / nsplit), u_end = (int)((long)n_all * (split + 1) / nsplit);
+  if (u_beg >= u_end) return;
   const int k0b = blockIdx.x * 64, n0b = blockIdx.y * 64;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
@@ -341,7 +449,7 @@ __global__ __launch_bounds__(256) void fc_wgrad_kernel(
   float bpart[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int srow = tid >> 3, sc = (tid & 7) * 8;
   const int mt0 = 2 * (w >> 1), nt0 = 2 * (w & 1);
-  for (int u = 0; u < n_use; ++u) {
+  for (int u = u_beg; u < u_end; ++u) {
     const int p = inv_path[(layer * M + j) * Pmax + u];
     const int a = inv_slot[(layer * M + j) * Pmax + u];
     for (long rb = 0; rb < Rtot; rb += 32) {
@@ -394,13 +502,19 @@ __global__ __launch_bounds__(256) void fc_wgrad_kernel(
       for (int r = 0; r < 4; ++r) {
         const int k = k0b + (mt0 + i) * 16 + 4 * grp + r;
         const int n = n0b + (nt0 + jj) * 16 + i16;
-        if (k < K && n < Cout) grad[base + (long)k * Cout + n] = acc[i][jj][r];
+        if (k < K && n < Cout) {
+          if (nsplit == 1) grad[base + (long)k * Cout + n] = acc[i][jj][r];
+          else atomicAdd(&grad[base + (long)k * Cout + n], acc[i][jj][r]);
+        }
       }
   if (do_bias) {
 #pragma unroll
     for (int c = 0; c < 8; ++c) atomicAdd(&dbias[sc + c], bpart[c]);
     __syncthreads();
-    if (tid < 64 && n0b + tid < Cout) grad[b_off + (long)j * chunk + n0b + tid] = dbias[tid];
+    if (tid < 64 && n0b + tid < Cout) {
+      if (nsplit == 1) grad[b_off + (long)j * chunk + n0b + tid] = dbias[tid];
+      else atomicAdd(&grad[b_off + (long)j * chunk + n0b + tid], dbias[tid]);
+    }
   }
 }
 
@@ -448,6 +562,16 @@ int launch_fc_dgrad(const float* G, const void* bits, const void* WcT, const int
                     int layer, int L, int M, int K, int KP, int Cout, int P, int E, int T, long bits_rows,
                     float g_scale, float* dX, hipStream_t stream) {
   if (M > MAXM || Cout % 32 != 0) return -1;
+  if (Cout == 256) {
+    const int nchunks = (K + 127) / 128;
+    const int split = nchunks >= 8 ? 2 : 1;
+    const int per = (nchunks + split - 1) / split;
+    dim3 grid((unsigned)(((long)T * E + 63) / 64), P, split);
+    fc_dgrad_lds_kernel<256><<<grid, 512, 0, stream>>>(G, (const uint16_t*)bits, (const bf16_t*)WcT, act_idx,
+                                                        act_cnt, layer, L, M, K, KP, P, E, T, bits_rows, g_scale, dX,
+                                                        per);
+    return (int)hipGetLastError();
+  }
   dim3 grid((unsigned)(((long)T * E + 63) / 64), (K + 63) / 64, P);
   fc_dgrad_kernel<<<grid, 256, 0, stream>>>(G, (const uint16_t*)bits, (const bf16_t*)WcT, act_idx, act_cnt, layer, L,
                                             M, K, KP, Cout, P, E, T, bits_rows, g_scale, dX);
@@ -459,10 +583,14 @@ int launch_fc_wgrad(const void* X, int ldx, const float* G, const void* bits, fl
                     int Pmax, int K, int Cout, int P, int E, int T, long bits_rows, float g_scale,
                     hipStream_t stream) {
   if (Cout % 16 != 0 || ldx % 8 != 0) return -1;
-  dim3 grid((K + 63) / 64, (Cout + 63) / 64, M);
+  // split the users of each module so the grid covers >= ~2K workgroups
+  const int tiles = ((K + 63) / 64) * ((Cout + 63) / 64) * M;
+  int nsplit = (2048 + tiles - 1) / tiles;
+  nsplit = nsplit < 1 ? 1 : (nsplit > Pmax ? Pmax : nsplit);
+  dim3 grid((K + 63) / 64, (Cout + 63) / 64, M * nsplit);
   fc_wgrad_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, G, (const uint16_t*)bits, grad, w_off, b_off,
                                             chunk, inv_path, inv_slot, inv_cnt, layer, M, Pmax, K, Cout, P, E, T,
-                                            bits_rows, g_scale);
+                                            bits_rows, g_scale, nsplit);
   return (int)hipGetLastError();
 }
 }

@@ -134,6 +134,8 @@ class PathNetTrainer:
             self.fitness_local = self.engine.fitness
         else:
             self.fitness_local = torch.full((self.P,), FITNESS_PENDING, device=self.device)
+            self.fit_cnt = torch.zeros(self.P, device=self.device)
+            self.fit_sum = torch.zeros(self.P, device=self.device)
         self.task_start_step = self.global_step
         self.solved_generation.setdefault(task_idx, None)
         self._task_gen0 = self.pop.generation
@@ -197,6 +199,12 @@ class PathNetTrainer:
             actions_l.append(a)
             rewards_l.append(r)
             dones_l.append(d)
+        window = cfg.ga.window_for(E)
+        if window > 0:   # mean return over the episodes finished since the path's last tournament
+            self.fit_cnt += ep_cnt
+            self.fit_sum += ep_sum
+            self.fitness_local = torch.where(self.fit_cnt >= window, self.fit_sum / self.fit_cnt.clamp(min=1.0),
+                                             torch.full_like(self.fit_sum, FITNESS_PENDING))
         with torch.no_grad():
             _, v_boot, _ = model.forward(obs, E, state)
         values = torch.stack(values_l)
@@ -261,7 +269,14 @@ class PathNetTrainer:
                 self.solved_generation[self.task_idx] = self.pop.generation - self._task_gen0
             self._push_genotypes()
             lo, hi = self.path_offset, self.path_offset + self.P
-            self.fitness_local.copy_(torch.from_numpy(self.pop.fitness[lo:hi]).to(self.device))
+            fl = torch.from_numpy(self.pop.fitness[lo:hi]).to(self.device)
+            if self.engine is not None:
+                self.engine.reset_fitness(fl)
+            else:
+                self.fitness_local.copy_(fl)
+                pend = fl <= FITNESS_PENDING
+                self.fit_cnt.masked_fill_(pend, 0.0)
+                self.fit_sum.masked_fill_(pend, 0.0)
             if self.visualizer is not None and time.time() - self._last_vis > 10.0:
                 from .ga import decode_path
                 self.visualizer.show([decode_path(g) for g in self.pop.genotypes], "m")   # visualize.py:90

@@ -164,10 +164,16 @@ class GAConfig:
     B: int = 3                          # doom_pathnet.py:360 (paper: 2)
     mutation: str = "ref"               # "ref" (pathnet.py:50-63) | "down" (pathnet.py:32-48)
     concurrent_tournaments: int = 1     # 1 == reference single tournament at a time
-    fitness: str = "last"               # "last" episode return (ref) | "mean"
-    fitness_window: int = 1
+    fitness: str = "last"               # "last" episode return (ref) | "mean" over a window of episodes
+    fitness_window: int = 0             # "mean": episodes per tournament entry (0 = envs_per_path)
     freeze_union: bool = True           # keep union of frozen paths across tasks (paper); False = ref quirk
     seed: int = 1                       # doom_pathnet.py:104 tf.set_random_seed(1)
+
+    def window_for(self, envs_per_path: int) -> int:
+        """Episodes a path must finish before it can enter a tournament (0 = reference 'last episode')."""
+        if self.fitness != "mean":
+            return 0
+        return self.fitness_window if self.fitness_window > 0 else max(1, envs_per_path)
 
 
 @dataclass

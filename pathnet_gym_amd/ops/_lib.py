@@ -41,7 +41,7 @@ _SIGS = {
     "launch_a2c_grad": [P, P, P, P, P, P, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_float, c_float,
                         P, P, P, P],
     "launch_heads_bwd": [P, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P],
-    "launch_fitness_update": [P, P, c_int, c_int, c_int, P, P, P],
+    "launch_fitness_update": [P, P, c_int, c_int, c_int, P, P, P, P, c_int, P],
     "launch_rmsprop": [P, P, P, P, P, P, P, c_int, P, c_int, P, P, c_float, c_float, c_float, c_float, P],
     "launch_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
     "launch_pong_step": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -59,6 +59,7 @@ _SIGS = {
     "launch_lstm_wgrad": [P, P, P, c_long, c_long, c_int, c_int, c_long, c_int, P],
     "launch_lstm_refresh": [P, c_long, c_int, c_int, P, P, P],
     "launch_lstm_carry": [P, P, P, P, P, c_int, c_int, P],
+    "fast_conv_set_slab": [c_int],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }
@@ -79,7 +80,7 @@ def lib():
         for name, args in _SIGS.items():
             fn = getattr(_lib, name)
             fn.argtypes = args
-            fn.restype = c_size_t if name.endswith("_smem") else c_int
+            fn.restype = c_size_t if name.endswith("_smem") else (None if name == "fast_conv_set_slab" else c_int)
     return _lib
 
 

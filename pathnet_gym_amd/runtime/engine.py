@@ -73,6 +73,10 @@ class HipEngine:
         self.stats = torch.zeros(4, device=dev)
         self.grad_flat = torch.zeros_like(model.store.flat, requires_grad=False)
         self.fitness = torch.full((P,), -1000.0, device=dev)
+        # windowed fitness (GAConfig.fitness == "mean"): episodes / return sum since the path's last tournament
+        self.fit_window = cfg.ga.window_for(E)
+        self.fit_cnt = torch.zeros(P, device=dev)
+        self.fit_sum = torch.zeros(P, device=dev)
         self.counters = torch.zeros(4, device=dev)
         self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.zeros(2, dtype=torch.float32, device=dev)      # {lr, skip}
@@ -220,8 +224,7 @@ class HipEngine:
         tn = st.layout.trunk_numel
         self.grad_flat[tn:] += st.flat.grad[tn:]
         st.flat.grad = None
-        _lib.call("launch_fitness_update", self.dones.data_ptr(), self.epret.data_ptr(), T, P, E,
-                  self.fitness.data_ptr(), self.counters.data_ptr(), _lib.stream())
+        self._fitness_update()
         self._count_nonfinite()
         self.lstm_state = (h.detach(), c.detach())
 
@@ -235,8 +238,7 @@ class HipEngine:
             self._forward_step(t)
             self._env_step(t)
         self._forward_step(T, greedy=True)
-        _lib.call("launch_fitness_update", self.dones.data_ptr(), self.epret.data_ptr(), T, P, E,
-                  self.fitness.data_ptr(), self.counters.data_ptr(), _lib.stream())
+        self._fitness_update()
         self.stats.zero_()
         _lib.call("launch_a2c_grad", self.logits.data_ptr(), self.values.data_ptr(), self.actions.data_ptr(),
                   self.rewards.data_ptr(), self.dones.data_ptr(), self.values[T].data_ptr(), T, B, self.A,
@@ -255,6 +257,18 @@ class HipEngine:
             dX = self.grads[l - 1] if l > 0 else None
             hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
         self._count_nonfinite()
+
+    def _fitness_update(self):
+        _lib.call("launch_fitness_update", self.dones.data_ptr(), self.epret.data_ptr(), self.T, self.P, self.E,
+                  self.fitness.data_ptr(), self.counters.data_ptr(), self.fit_cnt.data_ptr(), self.fit_sum.data_ptr(),
+                  self.fit_window, _lib.stream())
+
+    def reset_fitness(self, fitness_local: torch.Tensor):
+        """Install the GA's view of the local fitness; paths reset to pending restart their episode window."""
+        self.fitness.copy_(fitness_local)
+        pend = fitness_local <= -1000.0
+        self.fit_cnt.masked_fill_(pend, 0.0)
+        self.fit_sum.masked_fill_(pend, 0.0)
 
     def _count_nonfinite(self):
         # spare counter slot: non-finite gradient entries, all-reduced with the update (runtime/guard.py)

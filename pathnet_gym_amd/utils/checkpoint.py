@@ -79,9 +79,13 @@ def rank_tensors(trainer) -> Dict[str, torch.Tensor]:
         out["engine.ctr"] = _t(eng.ctr)
         out["engine.obs0"] = _t(eng.obs[0])
         out["engine.fitness"] = _t(eng.fitness)
+        out["engine.fit_cnt"] = _t(eng.fit_cnt)
+        out["engine.fit_sum"] = _t(eng.fit_sum)
     else:
         out["train.obs"] = _t(trainer.obs)
         out["train.fitness_local"] = _t(trainer.fitness_local)
+        out["train.fit_cnt"] = _t(trainer.fit_cnt)
+        out["train.fit_sum"] = _t(trainer.fit_sum)
     lstm = trainer.engine.lstm_state_tensors() if trainer.engine is not None else trainer.lstm_state
     if lstm is not None:
         out["lstm.h"] = _t(lstm[0])
@@ -146,10 +150,16 @@ def load(trainer, path: str, strict: bool = True):
             eng.ctr.copy_(r["engine.ctr"].to(dev))
             eng.obs[0].copy_(r["engine.obs0"].to(dev))
             eng.fitness.copy_(r["engine.fitness"].to(dev))
+            if "engine.fit_cnt" in r:
+                eng.fit_cnt.copy_(r["engine.fit_cnt"].to(dev))
+                eng.fit_sum.copy_(r["engine.fit_sum"].to(dev))
             eng.refresh_trainable()
         else:
             trainer.obs = r["train.obs"].to(dev)
             trainer.fitness_local = r["train.fitness_local"].to(dev)
+            if "train.fit_cnt" in r:
+                trainer.fit_cnt = r["train.fit_cnt"].to(dev)
+                trainer.fit_sum = r["train.fit_sum"].to(dev)
         if "lstm.h" in r:
             if trainer.engine is not None:
                 trainer.engine.load_lstm_state(r["lstm.h"].to(dev), r["lstm.c"].to(dev))

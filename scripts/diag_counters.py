@@ -55,7 +55,7 @@ def main():
         if events:
             tr._push_genotypes()
             lo, hi = tr.path_offset, tr.path_offset + tr.P
-            tr.fitness_local.copy_(torch.from_numpy(tr.pop.fitness[lo:hi]).to(tr.device))
+            eng.reset_fitness(torch.from_numpy(tr.pop.fitness[lo:hi]).to(tr.device))
         n += 1
         if n % 500 == 0:
             print(json.dumps({"update": n, "bad": bad, "t": round(time.time() - t0, 1)}), flush=True)

@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--debug", action="store_true", help="inspect engine buffers on counter anomalies")
     ap.add_argument("--no-ga", action="store_true", help="disable tournaments (pure A2C on fixed paths)")
     ap.add_argument("--N", type=int, default=None, help="active modules per layer in the initial genotypes")
+    ap.add_argument("--fitness", default=None, choices=["last", "mean"])
+    ap.add_argument("--fitness-window", type=int, default=None)
     args = ap.parse_args()
 
     import torch
@@ -74,6 +76,10 @@ def main():
         cfg.a2c.gae_lambda = args.gae_lambda
     if args.N is not None:
         cfg.net.N = args.N
+    if args.fitness is not None:
+        cfg.ga.fitness = args.fitness
+    if args.fitness_window is not None:
+        cfg.ga.fitness_window = args.fitness_window
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
     cfg.ga.concurrent_tournaments = args.concurrent or max(1, (cfg.paths * ctx.world) // 16)
@@ -140,7 +146,9 @@ def main():
                           "t_max": cfg.a2c.t_max, "lr": cfg.a2c.lr, "B": cfg.ga.B,
                           "concurrent_tournaments": cfg.ga.concurrent_tournaments, "backend": tr.backend,
                           "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
-                          "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda}}
+                          "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
+                          "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
+                          "ga": not args.no_ga}}
         print(json.dumps(out), flush=True)
     ctx.destroy()
 

@@ -527,3 +527,33 @@ def test_engine_lstm_gradient_matches_oracle(hip_lib):
     worst = max(errs, key=errs.get)
     print({k_: round(v, 4) for k_, v in sorted(errs.items(), key=lambda kv: -kv[1])[:8]})
     assert errs[worst] < 8e-2, (worst, errs[worst])
+
+
+@pytest.mark.parametrize("E", [16, 32])
+def test_slab_conv_kernels_match_fast(hip_lib, E):
+    """LDS-slab implicit-im2col conv fwd/wgrad == the register-im2col fast kernels (all-active path included)."""
+    from pathnet_gym_amd.ops import _lib
+    cfg = small_pixel_cfg()
+    P, T = 3, 2
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, seed=21)          # path 1: all 10 modules active
+    m = make_model(cfg, P, masks, seed=5)
+    g = torch.Generator(device="cpu").manual_seed(8)
+    obs_steps = [torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+                 for _ in range(T)]
+    dfeat = torch.randn(T * P * E, 256, generator=g).to(DEV)
+    lib = _lib.lib()
+    try:
+        lib.fast_conv_set_slab(0)
+        f0, g0 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+    finally:
+        lib.fast_conv_set_slab(1)
+    f1, g1 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+    assert rel(f1, f0) < 1e-3
+    for s in m.store.layout.segments:
+        if s.layer < 0 or s.layer > 2:
+            continue
+        a, b = g1[s.offset:s.offset + s.numel], g0[s.offset:s.offset + s.numel]
+        if b.norm() < 1e-6:
+            assert a.norm() < 1e-6, s.name
+            continue
+        assert rel(a, b) < 2e-3, (s.name, rel(a, b))

@@ -96,3 +96,20 @@ def test_tf_creation_order_importer():
     arrays = [np.full(st.layout.by_name[n].shape, i, np.float32) for i, n in enumerate(names)]
     ckpt.import_tf_arrays(st, arrays)
     assert float(st.tensor("layer3.module9.bias")[0]) == names.index("layer3.module9.bias")
+
+
+def test_windowed_mean_fitness_slows_and_averages_tournaments():
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.config import preset
+    gens = {}
+    for mode in ("last", "mean"):
+        cfg = preset("cartpole-cpu")
+        cfg.ga.fitness = mode
+        cfg.ga.fitness_window = 4
+        tr = PathNetTrainer(cfg)
+        for _ in range(40):
+            tr.update()
+        gens[mode] = tr.pop.generation
+        if mode == "mean":
+            assert all(s > 0 for e in tr.pop.history for s in e.scores)      # real episode means, never pending
+    assert gens["mean"] < gens["last"]
