@@ -77,8 +77,13 @@ class PathNetTrainer:
         self.E = cfg.envs_per_path
         self.P_total = self.P * self.ctx.world
         self.path_offset = self.ctx.rank * self.P
-        self.pop = Population(self.P_total, net.L, net.M, net.N, cfg.ga.B, seed=cfg.ga.seed,
-                              mutation_kind=cfg.ga.mutation, concurrent=cfg.ga.concurrent_tournaments)
+        self.device_ga = cfg.ga.backend == "device"
+        pop_cls = Population
+        if self.device_ga:
+            from .ga_device import CounterPopulation
+            pop_cls = CounterPopulation      # host mirror of the device GA (identical decisions)
+        self.pop = pop_cls(self.P_total, net.L, net.M, net.N, cfg.ga.B, seed=cfg.ga.seed,
+                           mutation_kind=cfg.ga.mutation, concurrent=cfg.ga.concurrent_tournaments)
         self.model = ACPathNet(net, self.P, self.device, self.backend, seed=cfg.seed,
                                compute_dtype=cfg.compute_dtype)
         a2c = cfg.a2c
@@ -132,6 +137,8 @@ class PathNetTrainer:
             self.engine = HipEngine(self.model, self.env, self.cfg, self.opt,
                                     seed=self.cfg.seed * 1000003 + self.ctx.rank * 7919 + task_idx)
             self.fitness_local = self.engine.fitness
+            if self.device_ga:
+                self.engine.enable_device_ga(self.pop, self.comm, self.path_offset)
         else:
             self.fitness_local = torch.full((self.P,), FITNESS_PENDING, device=self.device)
             self.fit_cnt = torch.zeros(self.P, device=self.device)
@@ -162,6 +169,8 @@ class PathNetTrainer:
         if self.backend == "hip":
             self.model.hip.refresh_weights()
             self.engine.refresh_trainable()
+            if self.engine.ga_dev is not None:
+                self.engine.ga_upload(self.pop)
         return winner, frozen
 
     # ------------------------------------------------------------------
@@ -267,11 +276,17 @@ class PathNetTrainer:
             thr = reward_threshold(self.cfg.tasks[self.task_idx])
             if self.solved_generation.get(self.task_idx) is None and st.best_winner >= thr:
                 self.solved_generation[self.task_idx] = self.pop.generation - self._task_gen0
-            self._push_genotypes()
             lo, hi = self.path_offset, self.path_offset + self.P
+            if self.engine is not None and self.engine.ga_dev is not None:
+                # the device GA already mutated, compacted and reset inside the optimizer graph;
+                # the host mirror only refreshes the (multi-rank) gradient packing plan
+                self.comm.plan(self.pop.expressed(), self.pop.frozen)
+            else:
+                self._push_genotypes()
             fl = torch.from_numpy(self.pop.fitness[lo:hi]).to(self.device)
             if self.engine is not None:
-                self.engine.reset_fitness(fl)
+                if self.engine.ga_dev is None:
+                    self.engine.reset_fitness(fl)
             else:
                 self.fitness_local.copy_(fl)
                 pend = fl <= FITNESS_PENDING

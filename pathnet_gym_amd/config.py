@@ -167,6 +167,7 @@ class GAConfig:
     fitness: str = "last"               # "last" episode return (ref) | "mean" over a window of episodes
     fitness_window: int = 0             # "mean": episodes per tournament entry (0 = envs_per_path)
     freeze_union: bool = True           # keep union of frozen paths across tasks (paper); False = ref quirk
+    backend: str = "host"               # "host": reference MT19937 GA | "device": counter-hash GA kernel in the graph
     seed: int = 1                       # doom_pathnet.py:104 tf.set_random_seed(1)
 
     def window_for(self, envs_per_path: int) -> int:

@@ -60,6 +60,8 @@ _SIGS = {
     "launch_lstm_refresh": [P, c_long, c_int, c_int, P, P, P],
     "launch_lstm_carry": [P, P, P, P, P, c_int, c_int, P],
     "fast_conv_set_slab": [c_int],
+    "launch_ga_step": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_uint, P],
+    "launch_ga_compact": [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }

@@ -74,6 +74,7 @@ class FusedUpdateComm:
         self.index = None
         self.ngrad = layout.numel
         self.buf = torch.zeros(layout.numel + P_total + self.NCOUNTERS, dtype=torch.float32, device=device)
+        self.fit_reduced = torch.zeros(P_total, dtype=torch.float32, device=device)   # static: read by the device GA
         self.bytes_last = 0
 
     def plan(self, expressed_all: np.ndarray, frozen: np.ndarray):
@@ -91,6 +92,16 @@ class FusedUpdateComm:
 
     def exchange(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor):
         """All-reduce in place. Returns (fitness_all [P_total] cpu numpy, counters_sum cpu numpy)."""
+        if not self.ctx.enabled:
+            # single rank: nothing to reduce -- read back fitness + counters in ONE small D2H copy
+            P = self.P_total
+            small = self.buf[:P + self.NCOUNTERS]
+            small[:P].copy_(fitness_local)
+            small[P:].copy_(counters)
+            self.fit_reduced.copy_(small[:P])
+            self.bytes_last = 0
+            host = small.cpu().numpy()
+            return host[:P].copy(), host[P:].copy()
         n = self.ngrad
         P = self.P_total
         buf = self.buf
@@ -109,6 +120,7 @@ class FusedUpdateComm:
             grad.copy_(buf[:n])
         else:
             grad.index_copy_(0, self.index, buf[:n])
+        self.fit_reduced.copy_(buf[n:n + P])
         host = view[n:].cpu().numpy()
         return host[:P].copy(), host[P:].copy()
 
@@ -125,6 +137,7 @@ class GatherBroadcastComm(FusedUpdateComm):
             self.ctx.all_reduce_(g)
             grad.index_copy_(0, self.index, g)
         fit = self.ctx.all_gather(fitness_local.float())
+        self.fit_reduced.copy_(fit.reshape(-1))
         c = counters.clone()
         self.ctx.all_reduce_(c)
         self.bytes_last = (n + self.P_total + self.NCOUNTERS) * 4

@@ -85,6 +85,7 @@ class HipEngine:
         self._build_opt_tables()
         self.g_rollout = None
         self.g_opt = None
+        self.ga_dev = None
         # LSTM nets: fused HIP LSTM cell (csrc/lstm.hip) when the widths are multiples of 64; otherwise
         # the hybrid path (HIP trunk + autograd LSTM/heads/loss, dL/dfeat fed back to the HIP trunk backward)
         self.lstm_hip = hp.lstm is not None
@@ -270,6 +271,45 @@ class HipEngine:
         self.fit_cnt.masked_fill_(pend, 0.0)
         self.fit_sum.masked_fill_(pend, 0.0)
 
+    # -- device GA (GAConfig.backend == "device"; algo/ga_device.py mirrors it on the host) --------
+    def enable_device_ga(self, pop, comm, p_off: int):
+        dev = self.device
+        self.ga_dev = dict(
+            geno=torch.zeros(pop.P, pop.L, pop.M, dtype=torch.uint8, device=dev),
+            frozen=torch.zeros(pop.L, pop.M, dtype=torch.uint8, device=dev),
+            slots=torch.full((pop.concurrent, pop.B), -1, dtype=torch.int32, device=dev),
+            gen=torch.zeros(1, dtype=torch.int64, device=dev),
+            events=torch.zeros(pop.concurrent, 3, dtype=torch.int32, device=dev),
+            fit=comm.fit_reduced, p_off=p_off, pop=pop)
+        self.ga_upload(pop)
+
+    def ga_upload(self, pop):
+        """Host GA state -> device (task start, freeze, checkpoint load); static addresses kept."""
+        g = self.ga_dev
+        g["geno"].copy_(torch.from_numpy(pop.genotypes.astype(np.uint8)))
+        g["frozen"].copy_(torch.from_numpy(pop.frozen.astype(np.uint8)))
+        g["slots"].copy_(torch.from_numpy(pop.slots.astype(np.int32)))
+        g["gen"].fill_(int(pop.generation))
+        g["fit"].copy_(torch.from_numpy(pop.fitness.astype(np.float32)))
+
+    def _ga_body(self):
+        g = self.ga_dev
+        pop = g["pop"]
+        hp = self.hip
+        m = self.model
+        st = _lib.stream()
+        _lib.call("launch_ga_step", g["geno"].data_ptr(), g["fit"].data_ptr(), g["slots"].data_ptr(),
+                  g["gen"].data_ptr(), g["events"].data_ptr(), pop.P, pop.L, pop.M, pop.N, pop.B, pop.concurrent,
+                  pop.seed32, st)
+        _lib.call("launch_ga_compact", g["geno"].data_ptr(), g["frozen"].data_ptr(), g["p_off"], self.P, pop.L,
+                  pop.M, m.mask.data_ptr(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), hp.inv_path.data_ptr(),
+                  hp.inv_slot.data_ptr(), hp.inv_cnt.data_ptr(), st)
+        # local fitness <- the GA's view; paths reset to pending restart their episode window
+        self.fitness.copy_(g["fit"][g["p_off"]:g["p_off"] + self.P])
+        pend = self.fitness <= -1000.0
+        self.fit_cnt.masked_fill_(pend, 0.0)
+        self.fit_sum.masked_fill_(pend, 0.0)
+
     def _count_nonfinite(self):
         # spare counter slot: non-finite gradient entries, all-reduced with the update (runtime/guard.py)
         self.counters[3:4].copy_((~torch.isfinite(self.grad_flat)).sum(dtype=torch.float32).reshape(1))
@@ -314,6 +354,8 @@ class HipEngine:
                   self.nblk, self.sq.data_ptr(), self.sq.numel(), self.trainable_u8.data_ptr(), self.lr.data_ptr(),
                   o.decay, o.momentum, o.epsilon, o.clip_norm, _lib.stream())
         self.hip.refresh_weights()
+        if self.ga_dev is not None:
+            self._ga_body()
         self.obs[0].copy_(self.obs[self.T])
         self.ctr.add_(1)
 

@@ -167,6 +167,8 @@ def load(trainer, path: str, strict: bool = True):
                 trainer.lstm_state = (r["lstm.h"].to(dev), r["lstm.c"].to(dev))
     if trainer.backend == "hip":
         trainer.model.hip.refresh_weights()
+        if trainer.engine is not None and trainer.engine.ga_dev is not None:
+            trainer.engine.ga_upload(trainer.pop)
     return trainer
 
 

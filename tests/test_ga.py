@@ -162,3 +162,48 @@ def test_state_dict_roundtrip_keeps_rng_stream():
     b.step(fit.copy())
     assert np.array_equal(a.genotypes, b.genotypes)
     assert a.candidates == b.candidates
+
+
+# ---------------------------------------------------------------------------
+# counter-based (device) GA mirror
+# ---------------------------------------------------------------------------
+def _drive(pop, steps, seed):
+    rng = np.random.RandomState(seed)
+    evs = []
+    for t in range(steps):
+        f = pop.fitness.copy()
+        fresh = rng.rand(pop.P) < 0.4
+        f[fresh] = rng.randint(-21, 22, int(fresh.sum())).astype(np.float32)
+        evs += pop.step(f, t)
+    return evs
+
+
+def test_counter_ga_deterministic_and_disjoint():
+    from pathnet_gym_amd.algo.ga_device import CounterPopulation
+    a = CounterPopulation(24, 5, 10, 4, 3, seed=7, concurrent=4)
+    b = CounterPopulation(24, 5, 10, 4, 3, seed=7, concurrent=4)
+    ea, eb = _drive(a, 60, 1), _drive(b, 60, 1)
+    assert len(ea) > 20 and [e.winner for e in ea] == [e.winner for e in eb]
+    assert np.array_equal(a.genotypes, b.genotypes) and np.array_equal(a.slots, b.slots)
+    used = a.slots[a.slots >= 0]
+    assert len(set(used.tolist())) == len(used)                     # disjoint tournaments
+    for e in ea:
+        assert e.winner == e.candidates[int(np.argmax(e.scores))]
+    c = CounterPopulation(24, 5, 10, 4, 3, seed=8, concurrent=4)
+    _drive(c, 60, 1)
+    assert not np.array_equal(a.genotypes, c.genotypes)
+
+
+def test_counter_mutation_rates_match_reference_operator():
+    from pathnet_gym_amd.algo.ga_device import counter_mutation
+    L, M, N = 4, 10, 4
+    moved = trials_a = 0
+    for gen in range(3000):
+        g = np.zeros((L, M), np.float32)
+        g[:, :N] = 1
+        before = g.copy()
+        counter_mutation(g, L, M, N, seed=123, gen=gen, path=5)
+        trials_a += 1
+        moved += before[0, 0] == 1 and g[0, 0] == 0
+    # P[int(U*L*N) <= 1] = 2/(L*N), times P[the random target is not module 0 itself] = (M-1)/M
+    assert abs(moved / trials_a - 2 / (L * N) * (M - 1) / M) < 0.02

@@ -557,3 +557,72 @@ def test_slab_conv_kernels_match_fast(hip_lib, E):
             assert a.norm() < 1e-6, s.name
             continue
         assert rel(a, b) < 2e-3, (s.name, rel(a, b))
+
+
+def test_device_ga_matches_host_mirror(hip_lib):
+    """csrc/ga.hip tournament + mutation + redraw == algo/ga_device.CounterPopulation, step by step;
+    compaction == compact_active + the host inverse lists."""
+    from pathnet_gym_amd.algo.ga import compact_active
+    from pathnet_gym_amd.algo.ga_device import CounterPopulation
+    from pathnet_gym_amd.ops import _lib
+    P, L, M, N, B, C = 40, 5, 10, 4, 3, 6
+    pop = CounterPopulation(P, L, M, N, B, seed=3, concurrent=C)
+    pop.frozen[2, 7] = 1
+    geno = torch.from_numpy(pop.genotypes.astype(np.uint8)).to(DEV)
+    frozen = torch.from_numpy(pop.frozen.astype(np.uint8)).to(DEV)
+    slots = torch.from_numpy(pop.slots.astype(np.int32)).to(DEV)
+    gen = torch.zeros(1, dtype=torch.int64, device=DEV)
+    events = torch.zeros(C, 3, dtype=torch.int32, device=DEV)
+    rng = np.random.RandomState(0)
+    fired = 0
+    for t in range(80):
+        f = pop.fitness.copy()
+        fresh = rng.rand(P) < 0.35
+        f[fresh] = rng.randint(-21, 22, int(fresh.sum())).astype(np.float32)
+        fit = torch.from_numpy(f).to(DEV)
+        evs = pop.step(f, t)
+        fired += len(evs)
+        _lib.call("launch_ga_step", geno.data_ptr(), fit.data_ptr(), slots.data_ptr(), gen.data_ptr(),
+                  events.data_ptr(), P, L, M, N, B, C, pop.seed32, _lib.stream())
+        torch.cuda.synchronize()
+        assert np.array_equal(geno.cpu().numpy(), pop.genotypes.astype(np.uint8)), t
+        assert np.array_equal(slots.cpu().numpy(), pop.slots.astype(np.int32)), t
+        assert np.array_equal(fit.cpu().numpy(), pop.fitness), t
+        assert int(gen) == pop.generation
+    assert fired > 30
+    Pl, off = 16, 8
+    mask = torch.zeros(Pl, L, M, device=DEV)
+    ai = torch.zeros(Pl, L, M, dtype=torch.int32, device=DEV)
+    ac = torch.zeros(Pl, L, dtype=torch.int32, device=DEV)
+    ip = torch.zeros(L, M, Pl, dtype=torch.int32, device=DEV)
+    isl = torch.zeros_like(ip)
+    ic = torch.zeros(L, M, dtype=torch.int32, device=DEV)
+    _lib.call("launch_ga_compact", geno.data_ptr(), frozen.data_ptr(), off, Pl, L, M, mask.data_ptr(), ai.data_ptr(),
+              ac.data_ptr(), ip.data_ptr(), isl.data_ptr(), ic.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    expr = pop.expressed()[off:off + Pl]
+    idx, cnt = compact_active(expr)
+    assert np.array_equal(mask.cpu().numpy(), expr)
+    assert np.array_equal(ai.cpu().numpy(), idx) and np.array_equal(ac.cpu().numpy(), cnt)
+    for l in range(L):
+        for j in range(M):
+            users = [p for p in range(Pl) if expr[p, l, j] > 0.5]
+            assert int(ic[l, j]) == len(users)
+            assert ip[l, j, :len(users)].tolist() == users
+            assert isl[l, j, :len(users)].tolist() == [int(expr[p, l, :j].sum()) for p in users]
+
+
+def test_trainer_device_ga_stays_in_sync(hip_lib):
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 8, 16, 4
+    cfg.ga.backend = "device"
+    cfg.ga.concurrent_tournaments = 2
+    tr = PathNetTrainer(cfg, device=DEV)
+    for _ in range(40):
+        tr.update()
+    torch.cuda.synchronize()
+    g = tr.engine.ga_dev
+    assert tr.pop.generation > 0
+    assert np.array_equal(g["geno"].cpu().numpy(), tr.pop.genotypes.astype(np.uint8))
+    assert np.array_equal(tr.model.mask.cpu().numpy(), tr.pop.expressed())
