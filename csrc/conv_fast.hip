@@ -920,10 +920,13 @@ static bool is_shape(int Hin, int Win, int Cin, int KH, int KW, int S, int u8) {
 }
 
 static int SLAB_WGRAD = 1;
-static int SLAB_FWD = 1;
+// The slab forward streams one band per barrier and is latency-bound at rollout batch sizes
+// (rocprof: 451 us vs 128 us/step for conv_fwd_fast): kept for shapes/batches where it wins, off by default.
+static int SLAB_FWD = 0;
 
 extern "C" {
-void fast_conv_set_slab(int on) { SLAB_WGRAD = on; SLAB_FWD = on; }
+void fast_conv_set_slab(int on) { SLAB_WGRAD = on; }
+void fast_conv_set_slab_fwd(int on) { SLAB_FWD = on; }
 
 // return 1 if handled by a fast kernel, 0 if the shape is not specialised, <0 on error
 int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,

@@ -72,6 +72,15 @@ def build_parser():
         p.add_argument("--gray", default=None, choices=["rgb", "bgr"])
         p.add_argument("--frameskip", type=int, default=None)
         p.add_argument("--ga_sync", default=None, choices=["fused", "gather_bcast"])
+        p.add_argument("--ga_backend", default=None, choices=["host", "device"],
+                       help="host: reference MT19937 GA; device: counter-hash GA kernel inside the update graph")
+        p.add_argument("--fitness", default=None, choices=["last", "mean"],
+                       help="last: latest episode return (reference); mean: mean over a window of episodes")
+        p.add_argument("--fitness_window", type=int, default=None, help="episodes per tournament entry (0 = envs)")
+        p.add_argument("--check_every", type=int, default=None, help="replica-consistency check interval (updates)")
+        p.add_argument("--max_nonfinite", type=int, default=None, help="consecutive skipped non-finite updates")
+        p.add_argument("--watchdog_s", type=float, default=None, help="abort if an update hangs this long")
+        p.add_argument("--trace", default=None, help="write a Chrome trace of update phases to this path")
 
     t = sub.add_parser("train")
     common(t)
@@ -171,6 +180,17 @@ def config_from_args(a):
         cfg.ga_sync = a.ga_sync
     if getattr(a, "steps_per_task", None):
         cfg.steps_per_task = a.steps_per_task
+    if getattr(a, "ga_backend", None):
+        cfg.ga.backend = a.ga_backend
+    if getattr(a, "fitness", None):
+        cfg.ga.fitness = a.fitness
+    if getattr(a, "fitness_window", None) is not None:
+        cfg.ga.fitness_window = a.fitness_window
+    for k in ("check_every", "max_nonfinite", "watchdog_s"):
+        if getattr(a, k, None) is not None:
+            setattr(cfg, k, getattr(a, k))
+    if getattr(a, "trace", None):
+        cfg.trace_path = a.trace
     cfg.net.__post_init__()
     return cfg
 

@@ -544,10 +544,14 @@ def test_slab_conv_kernels_match_fast(hip_lib, E):
     lib = _lib.lib()
     try:
         lib.fast_conv_set_slab(0)
+        lib.fast_conv_set_slab_fwd(0)
         f0, g0 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+        lib.fast_conv_set_slab(1)
+        lib.fast_conv_set_slab_fwd(1)
+        f1, g1 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
     finally:
         lib.fast_conv_set_slab(1)
-    f1, g1 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+        lib.fast_conv_set_slab_fwd(0)
     assert rel(f1, f0) < 1e-3
     for s in m.store.layout.segments:
         if s.layer < 0 or s.layer > 2:
