@@ -844,6 +844,165 @@ __global__ __launch_bounds__(256) void conv_dgrad_fast(const float* __restrict__
   }
 }
 
+// ===========================================================================
+// dgrad on MFMA (Cin = Cout = 8): "superpixel" implicit GEMM.
+// For stride S the S x S input pixels (S*i+ph, S*j+pw) of superpixel (i, j) read the SAME
+// output-gradient positions (i-ta, j-tb) through different taps (kh = ph + S*ta,
+// kw = pw + S*tb), so one GEMM row = one superpixel, N = (ph, pw, ci) = 8*S*S
+// (32 for the 4x4/s2 layer: two full 16-wide MFMA tiles), K = (tap, slot, c).
+// Per sample the masked gradient of the active modules (G & ReLU bits, bf16) is
+// staged in LDS once (every element feeds up to KH*KW/S^2 rows through the A
+// fragments); the per-path weight matrix B[k][n] is staged once per workgroup.
+// grid = (chunks, P), 256 threads; waves take 16-superpixel row tiles.
+// ===========================================================================
+#define DG_NSMAX 12          // active slots rounded up to a multiple of 4 (M <= 10)
+template <class G>
+struct DGM {
+  static constexpr int S = G::S;
+  static constexpr int NA = (G::KH + S - 1) / S;            // taps per axis and class
+  static constexpr int NTAP = NA * NA;
+  static constexpr int NI = (G::HIN + S - 1) / S, NJ = (G::WIN + S - 1) / S;
+  static constexpr int NSP = NI * NJ;                       // superpixels per sample
+  static constexpr int NRT = (NSP + 15) / 16;               // row tiles
+  static constexpr int NN = 8 * S * S;                      // real N
+  static constexpr int NT = (NN + 15) / 16;                 // n tiles
+  static constexpr int KSMAX = NTAP * DG_NSMAX / 4;         // 32-wide k-steps at 12 slots
+};
+
+template <class G>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
+                                                          const float* __restrict__ flat, long w_off, int chunk,
+                                                          const int* __restrict__ act_idx,
+                                                          const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                          int P, int E, int T, long bits_rows, float g_scale,
+                                                          float* __restrict__ dX, int samples_per_wg) {
+  using D = DGM<G>;
+  constexpr int S = D::S;
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[G::HOWO * DG_NSMAX * 8];      // [pos][slot][c]
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[D::KSMAX * D::NT * 16 * 40];   // [ks][n][k (32) + 8 pad]
+  __shared__ int mods[MAXM_F];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int PE = P * E;
+  const int nsamp = T * E;
+  const int s_beg = blockIdx.x * samples_per_wg;
+  const int s_end = min(nsamp, s_beg + samples_per_wg);
+  if (s_beg >= s_end) return;
+  if (tid < MAXM_F) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  __syncthreads();
+  const int ns4 = (cnt + 3) >> 2;                  // 32-wide k-steps per tap
+  const int KS = D::NTAP * ns4;
+  // B[k][n]: k = (tap*ns4*4 + a)*8 + c, n = (ph*S + pw)*8 + ci  ->  W_a[kh][kw][ci][c]
+  for (int it = tid; it < KS * D::NT * 16 * 4; it += 256) {
+    const int kk8 = it & 3, rest = it >> 2;        // 8-wide k chunk within the step
+    const int n = rest % (D::NT * 16), ks = rest / (D::NT * 16);
+    const int tap = ks / ns4, a = (ks - tap * ns4) * 4 + kk8;
+    const int ta = tap / D::NA, tb = tap - ta * D::NA;
+    const int cls = n >> 3, ci = n & 7, ph = cls / S, pw = cls - ph * S;
+    const int kh = ph + S * ta, kw = pw + S * tb;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (n < D::NN && a < cnt && kh < G::KH && kw < G::KW) {
+      const float* wp = flat + w_off + (long)mods[a] * chunk + ((kh * G::KW + kw) * 8 + ci) * 8;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = wp[c];
+    }
+    *reinterpret_cast<s8v*>(Bs + (ks * D::NT * 16 + n) * 40 + kk8 * 8) = f32x8_to_bf16(v);
+  }
+  // staging role: one thread per output position (the G row is shared by all slots), all slots' bits
+  const int nslot = ns4 * 4;
+  constexpr int GIT = (G::HOWO + 255) / 256;
+  float4 g0r[GIT], g1r[GIT];
+  uint8_t gbr[GIT][DG_NSMAX];
+  auto load_sample = [&](int s) {
+    const long sg = sample_global(p, s, E, PE, 0);
+#pragma unroll
+    for (int j = 0; j < GIT; ++j) {
+      const int pos = tid + 256 * j;
+      if (pos < G::HOWO) {
+        const long go = sg * G::HOWO + pos;
+        g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+        g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+#pragma unroll
+        for (int a = 0; a < DG_NSMAX; ++a) gbr[j][a] = a < cnt ? bits[(long)a * bits_rows + go] : (uint8_t)0;
+      }
+    }
+  };
+  load_sample(s_beg);
+  for (int s = s_beg; s < s_end; ++s) {
+    __syncthreads();                               // previous sample's LDS reads done
+#pragma unroll
+    for (int j = 0; j < GIT; ++j) {
+      const int pos = tid + 256 * j;
+      if (pos < G::HOWO) {
+        const float gg[8] = {g0r[j].x * g_scale, g0r[j].y * g_scale, g0r[j].z * g_scale, g0r[j].w * g_scale,
+                             g1r[j].x * g_scale, g1r[j].y * g_scale, g1r[j].z * g_scale, g1r[j].w * g_scale};
+#pragma unroll
+        for (int a = 0; a < DG_NSMAX; ++a) {
+          if (a < nslot) {
+            float m[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) m[c] = ((gbr[j][a] >> c) & 1u) ? gg[c] : 0.f;
+            *reinterpret_cast<s8v*>(Gs + (pos * DG_NSMAX + a) * 8) = f32x8_to_bf16(m);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (s + 1 < s_end) load_sample(s + 1);
+    const long sg = sample_global(p, s, E, PE, 0);
+    for (int rt = w; rt < D::NRT; rt += 4) {
+      const int sp = rt * 16 + c16;
+      const int ii = sp / D::NJ, jj = sp - ii * D::NJ;
+      f4v acc[D::NT];
+#pragma unroll
+      for (int nt = 0; nt < D::NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < KS; ++ks) {
+        const int tap = ks / ns4, a = (ks - tap * ns4) * 4 + grp;
+        const int ta = tap / D::NA, tb = tap - ta * D::NA;
+        const int oh = ii - ta, ow = jj - tb;
+        s8v af = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (sp < D::NSP && oh >= 0 && oh < G::HO && ow >= 0 && ow < G::WO)
+          af = *reinterpret_cast<const s8v*>(Gs + ((oh * G::WO + ow) * DG_NSMAX + a) * 8);
+#pragma unroll
+        for (int nt = 0; nt < D::NT; ++nt) {
+          const s8v bf = *reinterpret_cast<const s8v*>(Bs + (ks * D::NT * 16 + nt * 16 + c16) * 40 + grp * 8);
+          acc[nt] = mfma16(af, bf, acc[nt]);
+        }
+      }
+      // epilogue: row (superpixel) = rt*16 + 4*grp + r, n = nt*16 + c16
+#pragma unroll
+      for (int nt = 0; nt < D::NT; ++nt) {
+        const int n = nt * 16 + c16;
+        if (n >= D::NN) continue;
+        const int cls = n >> 3, ci = n & 7, ph = cls / S, pw = cls - ph * S;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int spo = rt * 16 + 4 * grp + r;
+          if (spo >= D::NSP) continue;
+          const int io = spo / D::NJ, jo = spo - io * D::NJ;
+          const int ih = S * io + ph, iw = S * jo + pw;
+          if (ih < G::HIN && iw < G::WIN) dX[(sg * (G::HIN * G::WIN) + ih * G::WIN + iw) * 8 + ci] = acc[nt][r];
+        }
+      }
+    }
+  }
+}
+
+template <class G>
+static int dgrad_mfma_t(const float* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,
+                        const int* ac, int layer, int L, int M, int P, int E, int T, long br, float gs, float* dX,
+                        hipStream_t st) {
+  const int nsamp = T * E;
+  int spw = (nsamp + 31) / 32;                     // ~32 workgroups per path
+  if (spw < 2) spw = 2;
+  dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
+  conv_dgrad_mfma<G><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T,
+                                           br, gs, dX, spw);
+  return (int)hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 template <class G>
 static int fwd_t(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off, int chunk,
@@ -920,6 +1079,7 @@ static bool is_shape(int Hin, int Win, int Cin, int KH, int KW, int S, int u8) {
 }
 
 static int SLAB_WGRAD = 1;
+static int DGRAD_MFMA = 1;
 // The slab forward streams one band per barrier and is latency-bound at rollout batch sizes
 // (rocprof: 451 us vs 128 us/step for conv_fwd_fast): kept for shapes/batches where it wins, off by default.
 static int SLAB_FWD = 0;
@@ -927,6 +1087,7 @@ static int SLAB_FWD = 0;
 extern "C" {
 void fast_conv_set_slab(int on) { SLAB_WGRAD = on; }
 void fast_conv_set_slab_fwd(int on) { SLAB_FWD = on; }
+void fast_conv_set_dgrad_mfma(int on) { DGRAD_MFMA = on; }
 
 // return 1 if handled by a fast kernel, 0 if the shape is not specialised, <0 on error
 int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
@@ -980,6 +1141,16 @@ int fast_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w
   if (is_shape<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                      \
     const int rc = dgrad_t<Gx>(Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs, dX, st); \
     return rc ? -rc : 1;                                                                                \
+  }
+  if (M <= 10 && DGRAD_MFMA) {
+    if (is_shape<C2>(Hin, Win, Cin, KH, KW, S, 0)) {
+      const int rc = dgrad_mfma_t<C2>(Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs, dX, st);
+      return rc ? -rc : 1;
+    }
+    if (is_shape<C3>(Hin, Win, Cin, KH, KW, S, 0)) {
+      const int rc = dgrad_mfma_t<C3>(Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs, dX, st);
+      return rc ? -rc : 1;
+    }
   }
   DG(C2) DG(C3)
 #undef DG

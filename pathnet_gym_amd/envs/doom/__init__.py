@@ -19,3 +19,4 @@ from .spaces import Box, BoxToMultiDiscrete, Discrete, DiscreteToMultiDiscrete, 
 from .wrappers import CustomGame, SetPlayingMode, SetResolution, ToBox, ToDiscrete, Wrapper
 from .scoring import MetaDoomScorer
 from .env import DependencyNotInstalled, DoomEnv, DoomLock, MetaDoomEnv, DOOM_REGISTRY, make_doom
+from . import scoreboard

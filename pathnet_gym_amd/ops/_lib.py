@@ -61,6 +61,7 @@ _SIGS = {
     "launch_lstm_carry": [P, P, P, P, P, c_int, c_int, P],
     "fast_conv_set_slab": [c_int],
     "fast_conv_set_slab_fwd": [c_int],
+    "fast_conv_set_dgrad_mfma": [c_int],
     "launch_ga_step": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_uint, P],
     "launch_ga_compact": [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P],
     "conv_fwd_smem": [c_int, c_int],
@@ -83,7 +84,7 @@ def lib():
         for name, args in _SIGS.items():
             fn = getattr(_lib, name)
             fn.argtypes = args
-            fn.restype = c_size_t if name.endswith("_smem") else (None if name.startswith("fast_conv_set_slab") else c_int)
+            fn.restype = c_size_t if name.endswith("_smem") else (None if name.startswith("fast_conv_set_") else c_int)
     return _lib
 
 

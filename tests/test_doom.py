@@ -91,3 +91,9 @@ def test_meta_doom_scoring():
 def test_engine_gating():
     with pytest.raises(doom.DependencyNotInstalled):
         doom.make_doom("gym_doom/DoomBasic-v0")
+
+
+def test_scoreboard_metadata_covers_every_id():
+    from pathnet_gym_amd.envs.doom import DOOM_REGISTRY, scoreboard
+    assert set(scoreboard.TASKS) == set(DOOM_REGISTRY)
+    assert all(t["group"] == "doom" and t["summary"] for t in scoreboard.TASKS.values())

@@ -618,15 +618,45 @@ def test_device_ga_matches_host_mirror(hip_lib):
 
 def test_trainer_device_ga_stays_in_sync(hip_lib):
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
-    cfg = preset("pong")
-    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 8, 16, 4
+    cfg = preset("cartpole")                       # short episodes -> many tournaments
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 8, 16, 5
     cfg.ga.backend = "device"
     cfg.ga.concurrent_tournaments = 2
     tr = PathNetTrainer(cfg, device=DEV)
-    for _ in range(40):
+    for _ in range(60):
         tr.update()
     torch.cuda.synchronize()
     g = tr.engine.ga_dev
     assert tr.pop.generation > 0
     assert np.array_equal(g["geno"].cpu().numpy(), tr.pop.genotypes.astype(np.uint8))
     assert np.array_equal(tr.model.mask.cpu().numpy(), tr.pop.expressed())
+
+
+@pytest.mark.parametrize("layer", [1, 2])
+def test_dgrad_mfma_matches_valu(hip_lib, layer):
+    """Superpixel MFMA conv dgrad == the fp32 VALU dgrad (bf16 operand rounding only)."""
+    from pathnet_gym_amd.ops import _lib
+    cfg = small_pixel_cfg()
+    P, E, T = 3, 16, 2
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, seed=4)          # includes an all-active and an empty layer
+    m = make_model(cfg, P, masks, seed=6)
+    hp = m.hip
+    g = hp.geoms[layer]
+    B = P * E
+    G = torch.randn(T * B, g.out_feat, generator=torch.Generator().manual_seed(2)).to(DEV)
+    bits, rows = hp.alloc_bits(layer, T, B)
+    bits.copy_(torch.randint(0, 256, bits.shape, generator=torch.Generator().manual_seed(3)).to(torch.uint8).to(DEV))
+    lib = _lib.lib()
+    outs = []
+    for on in (0, 1):
+        dX = torch.zeros(T * B, g.Hin * g.Win * g.Cin, device=DEV)
+        lib.fast_conv_set_dgrad_mfma(on)
+        try:
+            assert _lib.call_fast("fast_conv_dgrad", G.data_ptr(), bits.data_ptr(), m.store.flat.data_ptr(), g.w_off,
+                                  g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), layer, hp.L, hp.M, g.Hin,
+                                  g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T, rows, 1.0, dX.data_ptr(), _lib.stream())
+        finally:
+            lib.fast_conv_set_dgrad_mfma(1)
+        torch.cuda.synchronize()
+        outs.append(dX)
+    assert rel(outs[1], outs[0]) < 1e-2
