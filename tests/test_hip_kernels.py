@@ -339,7 +339,8 @@ def test_fast_conv_kernels_match_generic(hip_lib):
         a, b = g1[s.offset:s.offset + s.numel], g0[s.offset:s.offset + s.numel]
         if b.norm() < 1e-6:
             continue
-        assert rel(a, b) < 1e-3, (s.name, rel(a, b))
+        # layers 0-1 see dX from the MFMA (bf16-operand) dgrad instead of the fp32 VALU one
+        assert rel(a, b) < (1e-3 if s.layer == 2 else 1e-2), (s.name, rel(a, b))
 
 
 def test_engine_hybrid_lstm_reference_net(hip_lib):
