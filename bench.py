@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--preset", default="pong")
+    ap.add_argument("--ga-backend", default="device", choices=["device", "host"],
+                    help="device: GA kernels inside the update graph + pipelined host bookkeeping")
     args = ap.parse_args()
 
     import numpy as np
@@ -77,6 +79,7 @@ def main():
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
     cfg.ga.concurrent_tournaments = max(1, (cfg.paths * ctx.world) // 16)
+    cfg.ga.backend = args.ga_backend
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
 
     def sync():
@@ -86,12 +89,14 @@ def main():
 
     for _ in range(args.warmup):
         tr.update()
+    tr.flush()
     sync()
     gen0 = tr.pop.generation
     step0 = tr.global_step
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.update()
+    tr.flush()                               # drain the pipelined host bookkeeping of the last update
     sync()
     dt = time.perf_counter() - t0
     dt = ctx.max_scalar(dt)
@@ -121,6 +126,8 @@ def main():
                 "parallelism": f"dp{ctx.world} (population split: {cfg.paths} paths x {cfg.envs_per_path} envs per GPU)",
                 "backend": args.backend,
                 "hipgraph": cfg.use_graph,
+                "ga": f"{cfg.ga.backend} (B={cfg.ga.B}, {cfg.ga.concurrent_tournaments} concurrent tournaments)",
+                "pipelined": bool(tr.pipelined),
             },
             "generations_in_timed_window": int(tr.pop.generation - gen0),
             # the metric's second half is measured by scripts/solve.py (minutes of training, not a bench window)

@@ -139,6 +139,9 @@ class PathNetTrainer:
             self.fitness_local = self.engine.fitness
             if self.device_ga:
                 self.engine.enable_device_ga(self.pop, self.comm, self.path_offset)
+                if self.cfg.pipeline:
+                    self.engine.set_device_skip(self.comm.cnt_reduced)
+                    self.comm.force_dense = True     # the packing plan would lag the device GA by one update
         else:
             self.fitness_local = torch.full((self.P,), FITNESS_PENDING, device=self.device)
             self.fit_cnt = torch.zeros(self.P, device=self.device)
@@ -154,6 +157,7 @@ class PathNetTrainer:
 
     def end_task(self):
         """Freeze the last winner and re-init every other parameter (doom_pathnet.py:274-293)."""
+        self.flush()
         winner = self.pop.best()
         frozen = self.pop.freeze(winner, union=self.cfg.ga.freeze_union)
         self.model.set_frozen(frozen)
@@ -236,10 +240,17 @@ class PathNetTrainer:
                                 nonfinite])
         return flat.grad, counters, (lp, lv, ent)
 
+    @property
+    def pipelined(self) -> bool:
+        """HIP engine + device GA: host bookkeeping of update u-1 overlaps the GPU work of update u."""
+        return bool(self.cfg.pipeline and self.engine is not None and self.engine.ga_dev is not None)
+
     def update(self) -> UpdateStats:
         lr = anneal_lr(self.cfg.a2c.lr, self.global_step, self.cfg.a2c.max_time_step,
                        self.task_start_step, self.cfg.a2c.lr_anneal)
         tr = self.tracer
+        if self.pipelined:
+            return self._update_pipelined(lr)
         if self.engine is not None:
             eng = self.engine
             with tr.phase("rollout_backward"):
@@ -262,11 +273,49 @@ class PathNetTrainer:
                     self.opt.step(grad, lr)
         self.global_step += int(csum[0])
         self.updates += 1
+        return self._finish_update(fit_all, csum, (lp, lv, ent), skip, self.global_step)
+
+    def _update_pipelined(self, lr) -> UpdateStats:
+        """Enqueue update u (rollout graph, fused reduce, optimizer+GA graph, async D2H), then finish u-1."""
+        tr = self.tracer
+        eng = self.engine
+        with tr.phase("rollout_backward"):
+            eng.rollout_backward()
+        with tr.phase("allreduce"):
+            handle = self.comm.exchange_async(eng.grad_flat, eng.fitness, eng.counters, extra=eng.stats)
+        with tr.phase("optimizer"):
+            eng.optimizer_step(lr)              # non-finite skip decided on device from the reduced counters
+        self.global_step += self.cfg.a2c.t_max * self.P * self.E * self.ctx.world
+        self.updates += 1
+        prev, self._pending = getattr(self, "_pending", None), (handle, self.global_step)
+        if prev is None:
+            return UpdateStats(float("nan"), float("nan"), float("nan"), 0, float("nan"),
+                               steps=self.cfg.a2c.t_max * self.P * self.E * self.ctx.world)
+        return self._collect(prev)
+
+    def _collect(self, pending) -> UpdateStats:
+        handle, step_at = pending
+        fit_all, csum, stats = self.comm.collect(handle)
+        skip = self.guard.check(float(csum[3]), self.updates)
+        ent = float(stats[2]) / max(1, self.cfg.a2c.t_max * self.P * self.E)
+        return self._finish_update(fit_all, csum, (float(stats[0]), float(stats[1]), ent), skip, step_at)
+
+    def flush(self) -> Optional[UpdateStats]:
+        """Drain the pipelined update still in flight (task end, checkpoint, end of run)."""
+        pending = getattr(self, "_pending", None)
+        self._pending = None
+        if pending is None:
+            return None
+        return self._collect(pending)
+
+    def _finish_update(self, fit_all, csum, losses, skip, step_at) -> UpdateStats:
+        tr = self.tracer
+        lp, lv, ent = losses
         st = UpdateStats(float(lp), float(lv), float(ent), int(csum[1]),
                          float(csum[2] / csum[1]) if csum[1] > 0 else float("nan"), steps=int(csum[0]),
                          skipped=skip)
         with tr.phase("ga"):
-            events = self.pop.step(fit_all, self.global_step)
+            events = self.pop.step(fit_all, step_at)
         if isinstance(self.comm, GatherBroadcastComm) and events:
             g = self.comm.broadcast_genotypes(self.pop.genotypes)
             self.pop.genotypes = g
@@ -325,6 +374,7 @@ class PathNetTrainer:
                 n += 1
                 if checkpoint and checkpoint_every and self.updates % checkpoint_every == 0:
                     from ..utils import checkpoint as ckpt
+                    self.flush()
                     ckpt.save(self, checkpoint)
                 # reference throughput line: every PERFORMANCE_LOG_INTERVAL steps (rate-limited to 10 s)
                 if self.ctx.is_main and self.logger is not None and self.logger.echo and \

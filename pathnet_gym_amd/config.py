@@ -200,6 +200,9 @@ class TrainConfig:
     max_nonfinite: int = 3              # consecutive non-finite updates tolerated (skipped) before raising
     watchdog_s: float = 0.0             # abort if no update completes for this long (0 = off)
     trace_path: Optional[str] = None    # Chrome-trace JSON of update phases
+    # HIP engine + device GA: overlap the host bookkeeping of update u-1 with the GPU work of update u
+    # (stats / tournament events are reported one update late; flush() drains the last one)
+    pipeline: bool = True
 
     def to_json(self):
         return json.dumps(dataclasses.asdict(self))

@@ -74,13 +74,20 @@ class FusedUpdateComm:
         self.index = None
         self.ngrad = layout.numel
         self.buf = torch.zeros(layout.numel + P_total + self.NCOUNTERS, dtype=torch.float32, device=device)
-        self.fit_reduced = torch.zeros(P_total, dtype=torch.float32, device=device)   # static: read by the device GA
+        # static device copy of the reduced [fitness | counters] (read by the device GA / non-finite skip)
+        self.small_dev = torch.zeros(P_total + self.NCOUNTERS, dtype=torch.float32, device=device)
+        self.fit_reduced = self.small_dev[:P_total]
+        self.cnt_reduced = self.small_dev[P_total:]
+        pin = torch.device(device).type == "cuda"
+        self.host_small = [torch.zeros(P_total + self.NCOUNTERS, dtype=torch.float32, pin_memory=pin) for _ in range(2)]
+        self._flip = 0
+        self.force_dense = False
         self.bytes_last = 0
 
     def plan(self, expressed_all: np.ndarray, frozen: np.ndarray):
         rng = active_ranges(self.layout, expressed_all, frozen)
         n = sum(e - s for s, e in rng)
-        if n >= self.dense_threshold * self.layout.numel:
+        if self.force_dense or n >= self.dense_threshold * self.layout.numel:
             self.ranges = [(0, self.layout.numel)]
             self.index = None
             self.ngrad = self.layout.numel
@@ -90,6 +97,56 @@ class FusedUpdateComm:
             self.index = torch.from_numpy(idx).to(self.device)
             self.ngrad = int(n)
 
+    def exchange_async(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor, extra=None):
+        """Pipelined variant: reduce on the stream, start a non-blocking D2H of [fitness | counters] (+ ``extra``)
+        into a pinned double buffer and return a handle for ``collect``; the host does not wait."""
+        P = self.P_total
+        if not self.ctx.enabled:
+            self.small_dev[:P].copy_(fitness_local)
+            self.small_dev[P:].copy_(counters)
+            self.bytes_last = 0
+        else:
+            n = self.ngrad
+            buf = self.buf
+            if self.index is None:
+                buf[:n].copy_(grad)
+            else:
+                buf[:n].copy_(grad.index_select(0, self.index))
+            fit = buf[n:n + P]
+            fit.zero_()
+            fit[self.offset:self.offset + self.P_local].copy_(fitness_local)
+            buf[n + P:n + P + self.NCOUNTERS].copy_(counters)
+            view = buf[:n + P + self.NCOUNTERS]
+            self.ctx.all_reduce_(view)
+            self.bytes_last = view.numel() * 4
+            if self.index is None:
+                grad.copy_(buf[:n])
+            else:
+                grad.index_copy_(0, self.index, buf[:n])
+            self.small_dev.copy_(buf[n:n + P + self.NCOUNTERS])
+        hb = self.host_small[self._flip]
+        ex = None
+        if extra is not None:
+            if getattr(self, "_extra_host", None) is None or self._extra_host[0].shape != extra.shape:
+                self._extra_host = [torch.zeros(extra.shape, dtype=extra.dtype, pin_memory=hb.is_pinned())
+                                    for _ in range(2)]
+            ex = self._extra_host[self._flip]
+            ex.copy_(extra, non_blocking=True)
+        self._flip ^= 1
+        hb.copy_(self.small_dev, non_blocking=True)
+        ev = torch.cuda.Event() if hb.is_pinned() else None
+        if ev is not None:
+            ev.record()
+        return (ev, hb, ex)
+
+    def collect(self, handle):
+        ev, hb, ex = handle
+        if ev is not None:
+            ev.synchronize()
+        h = hb.numpy()
+        P = self.P_total
+        return h[:P].copy(), h[P:].copy(), (ex.numpy().copy() if ex is not None else None)
+
     def exchange(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor):
         """All-reduce in place. Returns (fitness_all [P_total] cpu numpy, counters_sum cpu numpy)."""
         if not self.ctx.enabled:
@@ -98,7 +155,7 @@ class FusedUpdateComm:
             small = self.buf[:P + self.NCOUNTERS]
             small[:P].copy_(fitness_local)
             small[P:].copy_(counters)
-            self.fit_reduced.copy_(small[:P])
+            self.small_dev.copy_(small)
             self.bytes_last = 0
             host = small.cpu().numpy()
             return host[:P].copy(), host[P:].copy()
@@ -120,7 +177,7 @@ class FusedUpdateComm:
             grad.copy_(buf[:n])
         else:
             grad.index_copy_(0, self.index, buf[:n])
-        self.fit_reduced.copy_(buf[n:n + P])
+        self.small_dev.copy_(buf[n:n + P + self.NCOUNTERS])
         host = view[n:].cpu().numpy()
         return host[:P].copy(), host[P:].copy()
 
@@ -140,6 +197,7 @@ class GatherBroadcastComm(FusedUpdateComm):
         self.fit_reduced.copy_(fit.reshape(-1))
         c = counters.clone()
         self.ctx.all_reduce_(c)
+        self.cnt_reduced.copy_(c)
         self.bytes_last = (n + self.P_total + self.NCOUNTERS) * 4
         return fit.cpu().numpy(), c.cpu().numpy()
 

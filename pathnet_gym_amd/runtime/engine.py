@@ -86,6 +86,7 @@ class HipEngine:
         self.g_rollout = None
         self.g_opt = None
         self.ga_dev = None
+        self.skip_src = None      # device tensor: counters with the all-reduced non-finite count at [3]
         # LSTM nets: fused HIP LSTM cell (csrc/lstm.hip) when the widths are multiples of 64; otherwise
         # the hybrid path (HIP trunk + autograd LSTM/heads/loss, dL/dfeat fed back to the HIP trunk backward)
         self.lstm_hip = hp.lstm is not None
@@ -344,7 +345,13 @@ class HipEngine:
         elif self.hybrid:
             self.lstm_state = (h.clone(), c.clone())
 
+    def set_device_skip(self, counters_reduced: torch.Tensor):
+        """Pipelined mode: the optimizer skips a non-finite update by itself (no host round trip)."""
+        self.skip_src = counters_reduced
+
     def _optimizer_body(self):
+        if self.skip_src is not None:
+            self.lr[1:2].copy_((self.skip_src[3:4] > 0).to(torch.float32))
         if self.lstm_hip:
             T = self.T
             self.hip.lstm_carry(self.hst[T], self.cst[T], self.dones[T - 1], self.hst[0], self.cst[0])
@@ -386,7 +393,8 @@ class HipEngine:
 
     def optimizer_step(self, lr: float, skip: bool = False):
         self.lr[0:1].fill_(lr)
-        self.lr[1:2].fill_(1.0 if skip else 0.0)
+        if self.skip_src is None:
+            self.lr[1:2].fill_(1.0 if skip else 0.0)
         if self.use_graph and self.g_opt is not None:
             self.g_opt.replay()
         else:

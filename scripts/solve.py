@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--no-ga", action="store_true", help="disable tournaments (pure A2C on fixed paths)")
     ap.add_argument("--N", type=int, default=None, help="active modules per layer in the initial genotypes")
     ap.add_argument("--fitness", default=None, choices=["last", "mean"])
+    ap.add_argument("--ga-backend", default=None, choices=["host", "device"])
     ap.add_argument("--fitness-window", type=int, default=None)
     args = ap.parse_args()
 
@@ -78,6 +79,8 @@ def main():
         cfg.net.N = args.N
     if args.fitness is not None:
         cfg.ga.fitness = args.fitness
+    if args.ga_backend is not None:
+        cfg.ga.backend = args.ga_backend
     if args.fitness_window is not None:
         cfg.ga.fitness_window = args.fitness_window
     cfg.backend = args.backend

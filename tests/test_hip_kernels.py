@@ -661,3 +661,24 @@ def test_dgrad_mfma_matches_valu(hip_lib, layer):
         torch.cuda.synchronize()
         outs.append(dX)
     assert rel(outs[1], outs[0]) < 1e-2
+
+
+def test_pipelined_update_matches_synchronous(hip_lib):
+    """Pipelined host bookkeeping (device GA) changes nothing numerically: same weights, genotypes, steps."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    res = []
+    for pipe in (False, True):
+        cfg = preset("cartpole")
+        cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 8, 16, 5
+        cfg.ga.backend = "device"
+        cfg.ga.concurrent_tournaments = 2
+        cfg.pipeline = pipe
+        tr = PathNetTrainer(cfg, device=DEV)
+        assert tr.pipelined == pipe
+        for _ in range(30):
+            tr.update()
+        tr.flush()
+        torch.cuda.synchronize()
+        res.append((tr.model.store.flat.detach().clone(), tr.pop.genotypes.copy(), tr.pop.generation, tr.global_step))
+    assert torch.equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1]) and res[0][2] == res[1][2] > 0 and res[0][3] == res[1][3]
