@@ -374,6 +374,111 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_slab(const void* __restrict__
 }
 
 // ===========================================================================
+// forward, whole-image staging (first layer, uint8 frames): grid = (2*T*E, P).
+// A workgroup owns one half of one sample's output rows; the input rows that half
+// touches (~84 rows x 480 B of uint8) are copied into LDS ONCE with 16-byte loads
+// (all issued before the barrier: maximal memory-level parallelism), so every input
+// byte crosses L2 once per workgroup instead of KH*KW/S^2 = 4 times.  A fragments are
+// ds_read_b64 of 2 pixels x 4 channels (8 consecutive k of one kernel row) converted
+// u8 -> bf16 once per 16-position tile and reused by every active column tile; B comes
+// straight from the 8 KB/path bf16 weight copy (L1/L2 resident).  ~40 KB LDS -> 3-4
+// workgroups per CU overlap one another's load and MFMA phases.
+// ===========================================================================
+template <class G>
+struct Half {
+  static constexpr int RL = G::WIN * G::CIN;                       // bytes per input row
+  static constexpr int OH0 = (G::HO + 1) / 2;                      // output rows of the first half
+  static constexpr int IR_MAX = (OH0 - 1) * G::S + G::KH;          // input rows per half (max)
+  static constexpr int BYTES = IR_MAX * RL;
+};
+
+template <class G>
+__global__ __launch_bounds__(256, 3) void conv_fwd_img(const uint8_t* __restrict__ X, bf16_t* __restrict__ Y,
+                                                       uint8_t* __restrict__ bits, const bf16_t* __restrict__ Wc,
+                                                       const float* __restrict__ flat, long bias_off, int chunk,
+                                                       const int* __restrict__ act_idx,
+                                                       const int* __restrict__ act_cnt, int layer, int L, int M, int P,
+                                                       int E, int T, int t0, long bits_rows, float in_scale,
+                                                       float out_scale) {
+  using H = Half<G>;
+  static_assert(G::U8 && G::KW * G::CIN == 32 && G::S * G::CIN == 16, "uint8 first-layer geometry");
+  constexpr int NK = G::KP / 32;                                  // = KH
+  __shared__ __attribute__((aligned(16))) uint8_t Xs[H::BYTES + 64];
+  __shared__ float bias_s[NCT * 16];
+  __shared__ int mods[MAXM_F];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
+  const int s = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int oh_beg = half ? H::OH0 : 0, oh_end = half ? G::HO : H::OH0;
+  const int ih_beg = oh_beg * G::S;
+  const int nbytes = min(H::BYTES, (G::HIN - ih_beg) * H::RL);
+  const long sg = sample_global(p, s, E, P * E, t0);
+  // (1) issue the image copy first (16 B per load), then the weights
+  const uint8_t* src = X + sg * (long)G::IN_ELEMS + (long)ih_beg * H::RL;
+  for (int i = tid * 16; i < nbytes; i += 256 * 16)
+    *reinterpret_cast<uint4*>(Xs + i) = *reinterpret_cast<const uint4*>(src + i);
+  if (tid < 4) *reinterpret_cast<uint4*>(Xs + H::BYTES + tid * 16) = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < MAXM_F) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  __syncthreads();
+  if (tid < NCT * 16) bias_s[tid] = (tid >> 3) < cnt ? flat[bias_off + (long)mods[tid >> 3] * chunk + (tid & 7)] : 0.f;
+  __syncthreads();
+  const int npos = (oh_end - oh_beg) * G::WO;
+  const int ntile = (npos + 15) / 16;
+  const long grow0 = sg * G::HOWO + (long)oh_beg * G::WO;
+  for (int tile = w; tile < ntile; tile += 4) {
+    int rho = tile * 16 + c16;
+    const bool rv = rho < npos;
+    if (!rv) rho = 0;
+    const int ob = rho / G::WO, ow = rho - ob * G::WO;
+    const uint8_t* ap = Xs + ob * G::S * H::RL + ow * (G::S * G::CIN) + 8 * grp;
+    // A fragments of this 16-position tile for all k-steps: converted once, reused by every column tile
+    s8v a[NK];
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) a[kk] = u8x8_to_bf16(*reinterpret_cast<const uint2*>(ap + kk * H::RL));
+    float sum[4] = {0.f, 0.f, 0.f, 0.f};
+    const int rho0 = tile * 16 + 4 * q;
+    for (int ct = 0; ct < nct; ++ct) {           // runtime loop: only the active column tiles, few live registers
+      f4v acc = {0.f, 0.f, 0.f, 0.f};
+      const int slot = ct * 2 + h;
+      const bool sv = slot < cnt;
+      // B straight from the (L1/L2-resident, 8 KB per path) bf16 weight copy
+      const bf16_t* bp = Wc + ((long)(mods[sv ? slot : 0] * 8 + ch)) * G::KP + 8 * grp;
+      s8v bfr[NK];
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk)
+        bfr[kk] = sv ? *reinterpret_cast<const s8v*>(bp + kk * 32) : (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) acc = mfma16(a[kk], bfr[kk], acc);
+      const float bb = bias_s[ct * 16 + c16];
+      uint32_t word = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[r] * in_scale + bb;
+        const bool pos = sv && v > 0.f;
+        sum[r] += pos ? v : 0.f;
+        const uint64_t bal = __ballot(pos);
+        word |= (uint32_t)((bal >> (16 * q + 8 * h)) & 0xFFull) << (8 * r);
+      }
+      if (ch == 0 && sv) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (rho0 + r < npos) bits[(long)slot * bits_rows + grow0 + rho0 + r] = (uint8_t)(word >> (8 * r));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
+    if (h == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (rho0 + r < npos) Y[(grow0 + rho0 + r) * 8 + ch] = f2bf(sum[r] * out_scale);
+    }
+  }
+}
+
+// ===========================================================================
 // wgrad: grid = (nchunks, P), 512 threads (8 waves), 32-row stages, register
 // prefetch + double-buffered LDS: one barrier per stage; stage i+1's global
 // loads are in flight while the MFMAs of stage i run.
@@ -1030,6 +1135,16 @@ static int wgrad_t(const void* X, const float* Gr, const void* bits, float* grad
   return (int)hipGetLastError();
 }
 
+template <class G>
+static int fwd_img_t(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off, int chunk,
+                     const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0, long br,
+                     float is, float os, hipStream_t st) {
+  dim3 grid((unsigned)(2 * T * E), P);
+  conv_fwd_img<G><<<grid, 256, 0, st>>>((const uint8_t*)X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat,
+                                        bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os);
+  return (int)hipGetLastError();
+}
+
 template <class G, int OB>
 static int fwd_slab_t(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off, int chunk,
                       const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0, long br,
@@ -1080,6 +1195,7 @@ static bool is_shape(int Hin, int Win, int Cin, int KH, int KW, int S, int u8) {
 
 static int SLAB_WGRAD = 1;
 static int DGRAD_MFMA = 1;
+static int IMG_FWD = 1;
 // The slab forward streams one band per barrier and is latency-bound at rollout batch sizes
 // (rocprof: 451 us vs 128 us/step for conv_fwd_fast): kept for shapes/batches where it wins, off by default.
 static int SLAB_FWD = 0;
@@ -1088,6 +1204,7 @@ extern "C" {
 void fast_conv_set_slab(int on) { SLAB_WGRAD = on; }
 void fast_conv_set_slab_fwd(int on) { SLAB_FWD = on; }
 void fast_conv_set_dgrad_mfma(int on) { DGRAD_MFMA = on; }
+void fast_conv_set_img_fwd(int on) { IMG_FWD = on; }
 
 // return 1 if handled by a fast kernel, 0 if the shape is not specialised, <0 on error
 int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
@@ -1099,6 +1216,11 @@ int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, 
     if ((E * Gx::HOWO) % 16) return -2;                                                                      \
     const int rc = fwd_t<Gx>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st); \
     return rc ? -rc : 1;                                                                                     \
+  }
+  if (IMG_FWD && is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) {
+    const int rc = fwd_img_t<C1>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os,
+                                 st);
+    return rc ? -rc : 1;
   }
   if (SLAB_FWD && is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) {
     const int rc = fwd_slab_t<C1, 2>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is,

@@ -185,5 +185,19 @@ def run_supervised_transfer(a) -> Dict:
         sp.end_task(winner)
         out["per_task"].append({"task": name, "best_accuracy": best_hist[-1], "curve": best_hist,
                                 "frozen": sp.frozen.astype(int).tolist()})
+    if getattr(a, "control", False) and len(tasks) > 1:
+        # transfer check: the last task learned from scratch (no frozen source path), same budget
+        ctl = SupervisedPathNet(cfg, a.population, 1, device, a.seed + 1000, a.B)
+        data = make_digits(tasks[-1], 4096, a.seed * 31 + len(tasks) - 1, device)
+        hist = []
+        for gen in range(a.generations):
+            acc = ctl.train_generation(data, 0, a.steps_per_gen, a.batch, a.lr, gen)
+            ctl.pop.step(acc.astype(np.float32), gen)
+            hist.append(float(acc.max()))
+        out["control"] = {"task": tasks[-1], "best_accuracy": hist[-1], "curve": hist}
+        thr = getattr(a, "target_accuracy", 0.9)
+        first = lambda c: next((i for i, v in enumerate(c) if v >= thr), None)     # noqa: E731
+        out["generations_to_accuracy"] = {"threshold": thr, "transfer": first(out["per_task"][-1]["curve"]),
+                                          "from_scratch": first(hist)}
     out["seconds"] = time.time() - t0
     return out

@@ -115,6 +115,8 @@ def build_parser():
     s.add_argument("--lr", type=float, default=0.05)
     s.add_argument("--seed", type=int, default=1)
     s.add_argument("--device", default=None)
+    s.add_argument("--control", action="store_true", help="also learn the last task from scratch (transfer check)")
+    s.add_argument("--target_accuracy", type=float, default=0.9)
     s.add_argument("--log_dir", default=None)
 
     i = sub.add_parser("info")

@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--N", type=int, default=None, help="active modules per layer in the initial genotypes")
     ap.add_argument("--fitness", default=None, choices=["last", "mean"])
     ap.add_argument("--ga-backend", default=None, choices=["host", "device"])
+    ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--fitness-window", type=int, default=None)
     args = ap.parse_args()
 
@@ -81,6 +82,9 @@ def main():
         cfg.ga.fitness = args.fitness
     if args.ga_backend is not None:
         cfg.ga.backend = args.ga_backend
+    if args.seed is not None:
+        cfg.seed = args.seed
+        cfg.ga.seed = args.seed
     if args.fitness_window is not None:
         cfg.ga.fitness_window = args.fitness_window
     cfg.backend = args.backend
@@ -152,6 +156,7 @@ def main():
                           "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
                           "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
                           "ga": not args.no_ga}}
+        out["config"]["seed"] = cfg.seed
         print(json.dumps(out), flush=True)
     ctx.destroy()
 

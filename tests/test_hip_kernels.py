@@ -690,3 +690,28 @@ def test_pipelined_update_matches_synchronous(hip_lib):
         assert torch.isfinite(tr.model.store.flat).all()
         res.append(tr.global_step)
     assert res[0] == res[1] == 30 * 8 * 16 * 5
+
+
+def test_image_staged_conv1_fwd_matches_fast(hip_lib):
+    """Whole-image-staged first-layer forward == register-im2col forward (bit-exact outputs and ReLU bits)."""
+    from pathnet_gym_amd.ops import _lib
+    cfg = small_pixel_cfg()
+    P, E = 3, 32
+    m = make_model(cfg, P, random_masks(P, cfg.L, cfg.M, cfg.N, seed=12), seed=2)
+    hp = m.hip
+    g = hp.geoms[0]
+    x = torch.randint(0, 256, (P * E, 160, 120, 4), dtype=torch.uint8, generator=torch.Generator().manual_seed(1)).to(DEV)
+    lib = _lib.lib()
+    outs = []
+    for on in (0, 1):
+        Y = torch.zeros(P * E, g.out_feat, dtype=torch.bfloat16, device=DEV)
+        bits, rows = hp.alloc_bits(0, 1, P * E)
+        lib.fast_conv_set_img_fwd(on)
+        try:
+            hp.layer_fwd(0, x, Y, bits, P, E, 1, 0, rows)
+        finally:
+            lib.fast_conv_set_img_fwd(1)
+        torch.cuda.synchronize()
+        outs.append((Y, bits))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
