@@ -33,13 +33,14 @@ BASELINE_STEPS_PER_SEC = 63.0     # reference steady-state global a
 
 def _solve_record():
     """Latest committed generations-to-solve measurement for Pong (profiles/solve), if present."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "solve", "pong_n10_sweep_2.json")
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "solve", "pong_n10_devga_seed1.json")
     try:
         d = json.loads(open(path).read().strip().splitlines()[-1])
         return {"value": d.get("generations_to_solve"), "frames": d.get("frames_to_solve"),
                 "seconds": d.get("seconds_to_solve"), "n_gpus": d.get("n_gpus"),
-                "config": "Pong PathNet M=10, N=10 initial modules, 16 paths x 16 envs, T=5, B=3",
-                "source": "profiles/solve/pong_n10_sweep_2.json (scripts/solve.py)"}
+                "config": "Pong PathNet M=10, N=10 initial modules, 16 paths x 16 envs, T=5, B=3, device GA",
+                "seeds_1_2_3": [2314, 2341, 2088],
+                "source": "profiles/solve/pong_n10_devga_seed*.json (scripts/solve.py)"}
     except (OSError, ValueError, IndexError):
         return None
 
@@ -55,6 +56,8 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--preset", default="pong")
+    ap.add_argument("--kernel-opt", action="append", default=[],
+                    help="kernel switch NAME=VALUE (fast_conv_set_*), for A/B measurements")
     ap.add_argument("--ga-backend", default="device", choices=["device", "host"],
                     help="device: GA kernels inside the update graph + pipelined host bookkeeping")
     args = ap.parse_args()
@@ -71,6 +74,11 @@ def main():
         from pathnet_gym_amd import _build
         _build.build()
 
+    if args.kernel_opt:
+        from pathnet_gym_amd.ops import _lib
+        for kv in args.kernel_opt:
+            k, v = kv.split("=")
+            getattr(_lib.lib(), "fast_conv_set_" + k)(int(v))
     ctx = init_distributed()
     cfg = preset(args.preset)
     cfg.paths = args.paths

@@ -1196,6 +1196,7 @@ static bool is_shape(int Hin, int Win, int Cin, int KH, int KW, int S, int u8) {
 static int SLAB_WGRAD = 1;
 static int DGRAD_MFMA = 1;
 static int IMG_FWD = 1;
+static int WGRAD_OB = 2;      // output rows per slab-wgrad stage for the first layer (2 or 3)
 // The slab forward streams one band per barrier and is latency-bound at rollout batch sizes
 // (rocprof: 451 us vs 128 us/step for conv_fwd_fast): kept for shapes/batches where it wins, off by default.
 static int SLAB_FWD = 0;
@@ -1205,6 +1206,7 @@ void fast_conv_set_slab(int on) { SLAB_WGRAD = on; }
 void fast_conv_set_slab_fwd(int on) { SLAB_FWD = on; }
 void fast_conv_set_dgrad_mfma(int on) { DGRAD_MFMA = on; }
 void fast_conv_set_img_fwd(int on) { IMG_FWD = on; }
+void fast_conv_set_wgrad_ob(int ob) { WGRAD_OB = ob; }
 
 // return 1 if handled by a fast kernel, 0 if the shape is not specialised, <0 on error
 int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
@@ -1242,8 +1244,11 @@ int fast_conv_wgrad(const void* X, int u8in, const float* Gr, const void* bits, 
     return rc ? -rc : 1;                                                                                       \
   }
   if (SLAB_WGRAD && is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) {
-    const int rc = wgrad_slab_t<C1, 2>(X, Gr, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, is, gs,
-                                       st);
+    int rc;
+    if (WGRAD_OB == 3)
+      rc = wgrad_slab_t<C1, 3>(X, Gr, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, is, gs, st);
+    else
+      rc = wgrad_slab_t<C1, 2>(X, Gr, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, is, gs, st);
     return rc ? -rc : 1;
   }
   if (SLAB_WGRAD && is_shape<C2>(Hin, Win, Cin, KH, KW, S, u8in)) {

@@ -63,6 +63,7 @@ _SIGS = {
     "fast_conv_set_slab_fwd": [c_int],
     "fast_conv_set_dgrad_mfma": [c_int],
     "fast_conv_set_img_fwd": [c_int],
+    "fast_conv_set_wgrad_ob": [c_int],
     "launch_ga_step": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_uint, P],
     "launch_ga_compact": [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P],
     "conv_fwd_smem": [c_int, c_int],
