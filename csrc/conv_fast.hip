@@ -1195,7 +1195,8 @@ static bool is_shape(int Hin, int Win, int Cin, int KH, int KW, int S, int u8) {
 
 static int SLAB_WGRAD = 1;
 static int DGRAD_MFMA = 1;
-static int IMG_FWD = 1;
+// measured slower than conv_fwd_fast at the rollout shape (2.28M vs 2.81M frames/s end to end): off by default
+static int IMG_FWD = 0;
 static int WGRAD_OB = 2;      // output rows per slab-wgrad stage for the first layer (2 or 3)
 // The slab forward streams one band per barrier and is latency-bound at rollout batch sizes
 // (rocprof: 451 us vs 128 us/step for conv_fwd_fast): kept for shapes/batches where it wins, off by default.

@@ -710,7 +710,7 @@ def test_image_staged_conv1_fwd_matches_fast(hip_lib):
         try:
             hp.layer_fwd(0, x, Y, bits, P, E, 1, 0, rows)
         finally:
-            lib.fast_conv_set_img_fwd(1)
+            lib.fast_conv_set_img_fwd(0)
         torch.cuda.synchronize()
         outs.append((Y, bits))
     assert torch.equal(outs[0][0], outs[1][0])
