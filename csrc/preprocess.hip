@@ -1,0 +1,77 @@
+// Standalone frame preprocessing for externally rendered RGB frames (SURVEY.md K15 + K16):
+// reference game_state.py:41-50,66,78 -- cv2.cvtColor (fixed-point luma) + cv2.resize
+// INTER_LINEAR 210x160 -> 160x120 (11-bit weights) + 4-deep frame stack, newest last.
+// Bit-exact with envs/pong.py:preprocess_frames (the torch oracle).
+//
+// One workgroup per env: the 210x160 gray image is built ONCE in LDS from 12-byte RGB
+// quads (4 pixels per thread-iteration), then every output pixel reads its 4 taps from LDS;
+// the new frame is pushed into the uint32-per-pixel stack with 16-byte loads/stores
+// ((in >> 8) | f << 24, or f * 0x01010101 where the episode just reset).
+#include "common.h"
+
+namespace pre {
+constexpr int SH = 210, SW = 160, OH = 160, OW = 120;
+}
+
+__global__ __launch_bounds__(256) void rgb_stack_push_kernel(const uint8_t* __restrict__ rgb,
+                                                             const uint32_t* __restrict__ obs_in,
+                                                             uint32_t* __restrict__ obs_out,
+                                                             const uint8_t* __restrict__ reset,
+                                                             const int* __restrict__ tables, int wr, int wg, int wb) {
+  using namespace pre;
+  __shared__ int tab[8 * 160];
+  __shared__ uint32_t gray[SH * SW / 4];
+  const int env = blockIdx.x;
+  for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
+  const uint8_t* src = rgb + (long)env * SH * SW * 3;
+  for (int q4 = threadIdx.x; q4 < SH * SW / 4; q4 += 256) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src + q4 * 12);   // 4 RGB pixels = 12 bytes
+    const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];
+    const uint8_t b[12] = {(uint8_t)w0, (uint8_t)(w0 >> 8), (uint8_t)(w0 >> 16), (uint8_t)(w0 >> 24),
+                           (uint8_t)w1, (uint8_t)(w1 >> 8), (uint8_t)(w1 >> 16), (uint8_t)(w1 >> 24),
+                           (uint8_t)w2, (uint8_t)(w2 >> 8), (uint8_t)(w2 >> 16), (uint8_t)(w2 >> 24)};
+    uint32_t wv = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int g = ((int)b[3 * e] * wr + (int)b[3 * e + 1] * wg + (int)b[3 * e + 2] * wb + 8192) >> 14;
+      wv |= (uint32_t)g << (8 * e);
+    }
+    gray[q4] = wv;
+  }
+  __syncthreads();
+  const uint8_t* g8 = reinterpret_cast<const uint8_t*>(gray);
+  const bool rs = reset != nullptr && reset[env];
+  const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OH * OW / 4);
+  uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OH * OW / 4);
+  for (int q = threadIdx.x; q < OH * OW / 4; q += 256) {
+    const int y = q / (OW / 4), x0 = (q - y * (OW / 4)) * 4;
+    const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
+    uint32_t f4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int x = x0 + e;
+      const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x], cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
+      const int ra = g8[ys0 * SW + xs0] * cx0 + g8[ys0 * SW + xs1] * cx1;
+      const int rb = g8[ys1 * SW + xs0] * cx0 + g8[ys1 * SW + xs1] * cx1;
+      int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+      v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      f4[e] = (uint32_t)v;
+    }
+    uint4 o;
+    if (rs) {
+      o = make_uint4(f4[0] * 0x01010101u, f4[1] * 0x01010101u, f4[2] * 0x01010101u, f4[3] * 0x01010101u);
+    } else {
+      const uint4 i = in4[q];
+      o = make_uint4((i.x >> 8) | (f4[0] << 24), (i.y >> 8) | (f4[1] << 24), (i.z >> 8) | (f4[2] << 24),
+                     (i.w >> 8) | (f4[3] << 24));
+    }
+    out4[q] = o;
+  }
+}
+
+extern "C" int launch_rgb_stack_push(const void* rgb, const void* obs_in, void* obs_out, const void* reset,
+                                     const int* tables, int N, int wr, int wg, int wb, hipStream_t stream) {
+  rgb_stack_push_kernel<<<N, 256, 0, stream>>>((const uint8_t*)rgb, (const uint32_t*)obs_in, (uint32_t*)obs_out,
+                                               (const uint8_t*)reset, tables, wr, wg, wb);
+  return (int)hipGetLastError();
+}

@@ -122,10 +122,25 @@ class PixelGameVec(VecEnv):
         self.steps = torch.where(mask, torch.zeros_like(self.steps), self.steps)
         self.epret = torch.where(mask, torch.zeros_like(self.epret), self.epret)
         self.counter += mask.long()
-        f = self.frame()
-        self.obs = torch.where(mask[:, None, None, None], f[..., None].expand(-1, -1, -1, 4), self.obs)
+        self.obs = self._push(self.obs, mask)
 
-    def step(self, actions):
+    def _push(self, obs_in, reset, obs_out=None):
+        """Render, preprocess and push the new frame: fused HIP kernel (backend 'hip') or the torch oracle."""
+        if self.backend == "hip":
+            from ..ops import envs as henv
+            out = obs_out if obs_out is not None else torch.empty_like(obs_in)
+            henv.rgb_stack_push(self.render(), obs_in, out, reset, self.tables, self.gray)
+            return out
+        f = self.frame()
+        pushed = torch.cat([obs_in.reshape(self.obs.shape)[..., 1:], f[..., None]], dim=3)
+        new = torch.where(reset[:, None, None, None], f[..., None].expand(-1, -1, -1, 4), pushed)
+        if obs_out is not None:
+            obs_out.copy_(new.reshape(obs_out.shape))
+            return obs_out
+        return new
+
+    def _advance(self, actions):
+        """Physics for one agent step (frameskip sub-frames) + auto-reset; returns (reward, done, ep_return)."""
         a = actions.long().to(self.device)
         a = torch.where((a >= self.num_actions) | (a < 0), torch.zeros_like(a), a)   # game_state.py:38-39
         reward = torch.zeros(self.num_envs, dtype=torch.int64, device=self.device)
@@ -140,18 +155,22 @@ class PixelGameVec(VecEnv):
         self.steps = torch.where(done, torch.zeros_like(self.steps), self.steps)
         self.epret = torch.where(done, torch.zeros_like(self.epret), self.epret)
         self.counter += done.long()
-        f = self.frame()
-        pushed = torch.cat([self.obs[..., 1:], f[..., None]], dim=3)
-        self.obs = torch.where(done[:, None, None, None], f[..., None].expand(-1, -1, -1, 4), pushed)
+        return reward, done, ep_return
+
+    def step(self, actions):
+        reward, done, ep_return = self._advance(actions)
+        self.obs = self._push(self.obs, done)
         return self.obs.clone(), reward.float(), done, {"episode_return": ep_return}
 
     def step_into(self, actions, obs_in, obs_out, reward, done, epret):
-        """Engine hook: step and write into the rollout buffers (eager torch ops)."""
-        o, r, d, info = self.step(actions)
-        obs_out.copy_(o.reshape(obs_out.shape))
-        reward.copy_(r)
+        """Engine hook: torch physics + render, then (backend 'hip') ONE fused kernel that preprocesses the
+        frame and pushes it from the engine's obs slot t straight into slot t+1."""
+        r, d, ep = self._advance(actions)
+        self._push(obs_in.view(self.obs.shape), d, obs_out.view(self.obs.shape))
+        self.obs = obs_out.view(self.obs.shape)
+        reward.copy_(r.float())
         done.copy_(d.to(done.dtype))
-        epret.copy_(info["episode_return"])
+        epret.copy_(ep)
 
 
 # ===========================================================================

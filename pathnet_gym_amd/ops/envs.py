@@ -104,3 +104,25 @@ def obs_to_bf16_padded(obs_f32: torch.Tensor) -> torch.Tensor:
     out = torch.zeros(B, 8, dtype=torch.bfloat16, device=obs_f32.device)
     out[:, :d] = obs_f32.to(torch.bfloat16)
     return out
+
+
+# ------------------------------------------------------------------ RGB frame preprocessing (K15/K16)
+def rgb_stack_push(rgb: torch.Tensor, obs_in: torch.Tensor, obs_out: torch.Tensor, reset, tables: torch.Tensor,
+                   gray: str = "rgb"):
+    """[N,210,160,3] uint8 frames -> gray + bilinear 160x120 + push into the uint8 [N,160,120,4] stack.
+
+    ``reset`` (bool/uint8 [N] or None): rows whose stack is re-filled with the new frame (episode start).
+    Bit-exact with ``envs/pong.py:preprocess_frames`` + the torch stack push.
+    """
+    from ..envs.pong import gray_weights
+    N = rgb.shape[0]
+    _lib.check(rgb, torch.uint8, shape=(N, 210, 160, 3), name="rgb")
+    _lib.check(obs_out, torch.uint8, numel=N * 160 * 120 * 4, name="obs_out")
+    _lib.check(obs_in, torch.uint8, numel=N * 160 * 120 * 4, name="obs_in")
+    tab = tables.to(device=rgb.device, dtype=torch.int32).contiguous()
+    r8 = None
+    if reset is not None:
+        r8 = _lib.check(reset.to(torch.uint8).contiguous(), torch.uint8, numel=N, name="reset")
+    wr, wg, wb = gray_weights(gray)
+    _lib.call("launch_rgb_stack_push", rgb.data_ptr(), obs_in.data_ptr(), obs_out.data_ptr(), _lib.ptr(r8),
+              tab.data_ptr(), N, int(wr), int(wg), int(wb), _lib.stream())

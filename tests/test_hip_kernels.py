@@ -715,3 +715,18 @@ def test_image_staged_conv1_fwd_matches_fast(hip_lib):
         outs.append((Y, bits))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("game", ["Breakout", "SpaceInvaders", "Alien"])
+def test_rgb_preprocess_kernel_bit_exact(hip_lib, game):
+    """Fused HIP gray + bilinear resize + stack push == the torch oracle, through resets."""
+    from pathnet_gym_amd.envs.registry import make
+    envs = [make(game, num_envs=24, device=DEV, seed=5, backend=b) for b in ("torch", "hip")]
+    o0, o1 = envs[0].reset(), envs[1].reset()
+    assert torch.equal(o0, o1)
+    g = torch.Generator().manual_seed(0)
+    for t in range(40):
+        a = torch.randint(0, envs[0].num_actions, (24,), generator=g).to(DEV)
+        r = [e.step(a) for e in envs]
+        assert torch.equal(r[0][0], r[1][0]), t
+        assert torch.equal(r[0][2], r[1][2]) and torch.equal(r[0][1], r[1][1])
