@@ -75,3 +75,78 @@ extern "C" int launch_rgb_stack_push(const void* rgb, const void* obs_in, void* 
                                                (const uint8_t*)reset, tables, wr, wg, wb);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Rectangle-list renderer + preprocessing + stack push for the pixel games whose logic runs in
+// torch (envs/atari_games.py): each game emits its scene as [N][R][4] int16 rectangles
+// (y0, x0, h, w; h*w == 0 = hidden) painted in order with one gray level per rectangle slot.
+// One workgroup per env rasterises the scene into an LDS gray image (cooperative fill, one
+// barrier per visible rectangle keeps the painter's order), then resizes + pushes as above.
+// Replaces N x R full-frame boolean mask ops of the torch renderer.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rects_stack_push_kernel(const int16_t* __restrict__ rects,
+                                                               const uint8_t* __restrict__ rect_gray, int R, int bg,
+                                                               const uint32_t* __restrict__ obs_in,
+                                                               uint32_t* __restrict__ obs_out,
+                                                               const uint8_t* __restrict__ reset,
+                                                               const int* __restrict__ tables) {
+  using namespace pre;
+  __shared__ int tab[8 * 160];
+  __shared__ uint32_t gray[SH * SW / 4];
+  const int env = blockIdx.x;
+  for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
+  const uint32_t bg4 = (uint32_t)bg * 0x01010101u;
+  for (int i = threadIdx.x; i < SH * SW / 4; i += 256) gray[i] = bg4;
+  __syncthreads();
+  uint8_t* g8 = reinterpret_cast<uint8_t*>(gray);
+  const int16_t* rr = rects + (long)env * R * 4;
+  for (int r = 0; r < R; ++r) {
+    int y0 = rr[r * 4 + 0], x0 = rr[r * 4 + 1];
+    int y1 = y0 + rr[r * 4 + 2], x1 = x0 + rr[r * 4 + 3];
+    y0 = max(y0, 0); x0 = max(x0, 0); y1 = min(y1, SH); x1 = min(x1, SW);
+    if (y1 <= y0 || x1 <= x0) continue;            // uniform across the workgroup
+    const int w = x1 - x0, area = (y1 - y0) * w;
+    const uint8_t g = rect_gray[r];
+    for (int i = threadIdx.x; i < area; i += 256) {
+      const int y = y0 + i / w, x = x0 + (i - (i / w) * w);
+      g8[y * SW + x] = g;
+    }
+    __syncthreads();
+  }
+  const bool rs = reset != nullptr && reset[env];
+  const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OH * OW / 4);
+  uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OH * OW / 4);
+  for (int q = threadIdx.x; q < OH * OW / 4; q += 256) {
+    const int y = q / (OW / 4), x0 = (q - y * (OW / 4)) * 4;
+    const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
+    uint32_t f4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int x = x0 + e;
+      const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x], cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
+      const int ra = g8[ys0 * SW + xs0] * cx0 + g8[ys0 * SW + xs1] * cx1;
+      const int rb = g8[ys1 * SW + xs0] * cx0 + g8[ys1 * SW + xs1] * cx1;
+      int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+      v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      f4[e] = (uint32_t)v;
+    }
+    uint4 o;
+    if (rs) {
+      o = make_uint4(f4[0] * 0x01010101u, f4[1] * 0x01010101u, f4[2] * 0x01010101u, f4[3] * 0x01010101u);
+    } else {
+      const uint4 i = in4[q];
+      o = make_uint4((i.x >> 8) | (f4[0] << 24), (i.y >> 8) | (f4[1] << 24), (i.z >> 8) | (f4[2] << 24),
+                     (i.w >> 8) | (f4[3] << 24));
+    }
+    out4[q] = o;
+  }
+}
+
+extern "C" int launch_rects_stack_push(const void* rects, const void* rect_gray, int R, int bg, const void* obs_in,
+                                       void* obs_out, const void* reset, const int* tables, int N,
+                                       hipStream_t stream) {
+  rects_stack_push_kernel<<<N, 256, 0, stream>>>((const int16_t*)rects, (const uint8_t*)rect_gray, R, bg,
+                                                 (const uint32_t*)obs_in, (uint32_t*)obs_out, (const uint8_t*)reset,
+                                                 tables);
+  return (int)hipGetLastError();
+}

@@ -32,6 +32,47 @@ from .pong import OBS_H, OBS_W, SCREEN_H, SCREEN_W, preprocess_frames, resize_ta
 BG = (0, 0, 0)
 
 
+class Scene:
+    """Ordered list of per-env rectangles (painter's order) with one RGB colour per rectangle slot.
+
+    Games describe a frame with ``add`` (one rectangle per env) and ``add_many`` (a batch of R
+    rectangles, e.g. a brick grid); hidden rectangles have h == 0.  The same scene feeds the torch
+    renderer (``PixelGameVec.draw``, the oracle) and the fused HIP rasteriser
+    (``csrc/preprocess.hip:rects_stack_push``).
+    """
+
+    def __init__(self, n: int, device):
+        self.n, self.device = n, device
+        self.parts, self.colors = [], []
+
+    def _t(self, v):
+        t = torch.as_tensor(v, device=self.device, dtype=torch.int64)
+        return t
+
+    def add(self, y0, x0, h, w, color, visible=None):
+        y0, x0, h, w = [self._t(v).reshape(-1).expand(self.n) for v in (y0, x0, h, w)]
+        if visible is not None:
+            h = torch.where(visible, h, torch.zeros_like(h))
+        self.parts.append(torch.stack([y0, x0, h, w], -1)[:, None])
+        self.colors.append(tuple(color))
+
+    def add_many(self, y0, x0, h, w, colors, visible=None):
+        """y0/x0/h/w: [R] or [N, R]; colors: R RGB tuples; visible: [N, R] bool."""
+        R = len(colors)
+
+        def full(v):
+            t = self._t(v)
+            return t.expand(self.n, R) if t.dim() == 0 else (t[None].expand(self.n, R) if t.dim() == 1 else t)
+        y0, x0, h, w = [full(v) for v in (y0, x0, h, w)]
+        if visible is not None:
+            h = torch.where(visible, h, torch.zeros_like(h))
+        self.parts.append(torch.stack([y0, x0, h, w], -1))
+        self.colors.extend(tuple(c) for c in colors)
+
+    def geometry(self) -> torch.Tensor:
+        return torch.cat(self.parts, 1)                    # [N, R, 4] int64
+
+
 class PixelGameVec(VecEnv):
     """Common driver: state tensors, frame stack, auto-reset, RGB render -> preprocessing."""
     graph_safe = False
@@ -99,8 +140,18 @@ class PixelGameVec(VecEnv):
     def game_over(self):
         raise NotImplementedError
 
-    def draw(self, img):
+    def scene(self) -> Scene:
         raise NotImplementedError
+
+    def draw(self, img):
+        """Torch renderer (oracle): paint the scene's rectangles in order."""
+        sc = self.scene()
+        geo = sc.geometry()
+        for r, c in enumerate(sc.colors):
+            y0, x0, h, w = geo[:, r].unbind(-1)
+            y0, x0, h, w = y0[:, None, None], x0[:, None, None], h[:, None, None], w[:, None, None]
+            m = (self.rows >= y0) & (self.rows < y0 + h) & (self.cols >= x0) & (self.cols < x0 + w)
+            img[m] = self.color(c)
 
     # -- VecEnv API ----------------------------------------------------------------
     def render(self) -> torch.Tensor:
@@ -129,7 +180,8 @@ class PixelGameVec(VecEnv):
         if self.backend == "hip":
             from ..ops import envs as henv
             out = obs_out if obs_out is not None else torch.empty_like(obs_in)
-            henv.rgb_stack_push(self.render(), obs_in, out, reset, self.tables, self.gray)
+            sc = self.scene()
+            henv.rects_stack_push(sc.geometry(), sc.colors, BG, obs_in, out, reset, self.tables, self.gray)
             return out
         f = self.frame()
         pushed = torch.cat([obs_in.reshape(self.obs.shape)[..., 1:], f[..., None]], dim=3)
@@ -249,20 +301,20 @@ class BreakoutVec(PixelGameVec):
     def game_over(self):
         return (self.lives <= 0) | (~self.bricks.view(self.num_envs, -1).any(1))
 
-    def draw(self, img):
-        gray = self.color((142, 142, 142))
-        img[:, 17:32, :] = gray
-        img[:, 17:196, 0:8] = gray
-        img[:, 17:196, 152:160] = gray
-        for r in range(self.ROWS):
-            y0 = self.BRICK_Y0 + r * self.BRICK_H
-            cols = self.bricks[:, r].repeat_interleave(self.BRICK_W, 1)           # [N, 144]
-            m = torch.zeros(self.num_envs, SCREEN_H, SCREEN_W, dtype=torch.bool, device=self.device)
-            m[:, y0:y0 + self.BRICK_H, self.BRICK_X0:self.BRICK_X0 + self.COLS * self.BRICK_W] = cols[:, None, :]
-            img[m] = self.color(self.ROW_COLOR[r])
-        red = self.color((200, 72, 72))
-        img[self.rect(self.PADDLE_Y, self.px // self.U, 4, self.PADDLE_W)] = red
-        img[self.rect(self.by // self.U, self.bx // self.U, 4, 2) & self.inplay[:, None, None]] = red
+    def scene(self) -> Scene:
+        sc = Scene(self.num_envs, self.device)
+        wall = (142, 142, 142)
+        sc.add(17, 0, 15, 160, wall)
+        sc.add(17, 0, 179, 8, wall)
+        sc.add(17, 152, 179, 8, wall)
+        r = torch.arange(self.ROWS, device=self.device).repeat_interleave(self.COLS)
+        c = torch.arange(self.COLS, device=self.device).repeat(self.ROWS)
+        sc.add_many(self.BRICK_Y0 + r * self.BRICK_H, self.BRICK_X0 + c * self.BRICK_W, self.BRICK_H, self.BRICK_W,
+                    [self.ROW_COLOR[int(i)] for i in r.tolist()], visible=self.bricks.reshape(self.num_envs, -1))
+        red = (200, 72, 72)
+        sc.add(self.PADDLE_Y, self.px // self.U, 4, self.PADDLE_W, red)
+        sc.add(self.by // self.U, self.bx // self.U, 4, 2, red, visible=self.inplay)
+        return sc
 
 
 # ===========================================================================
@@ -349,17 +401,18 @@ class SpaceInvadersVec(PixelGameVec):
         invaded = (self.fy + 18 * lowest_row + 10) >= 180
         return (self.lives <= 0) | (~self.alive.view(self.num_envs, -1).any(1)) | invaded
 
-    def draw(self, img):
-        N = self.num_envs
-        img[:, 195:197, :] = self.color((80, 89, 22))
-        green = self.color((50, 132, 50))
-        for r in range(self.AR):
-            for c in range(self.AC):
-                m = self.rect(self.fy + 18 * r, self.fx + 16 * c, 10, 8) & self.alive[:, r, c][:, None, None]
-                img[m] = self.color((134, 134, 29)) if r % 2 else green
-        img[self.rect(185, self.px, 8, 7)] = self.color((50, 132, 50))
-        img[self.rect(self.sy, self.sx, 6, 1) & self.shot[:, None, None]] = self.color((142, 142, 142))
-        img[self.rect(self.byp, self.bxp, 6, 1) & self.bomb[:, None, None]] = self.color((200, 200, 200))
+    def scene(self) -> Scene:
+        sc = Scene(self.num_envs, self.device)
+        sc.add(195, 0, 2, 160, (80, 89, 22))
+        green, olive = (50, 132, 50), (134, 134, 29)
+        r = torch.arange(self.AR, device=self.device).repeat_interleave(self.AC)
+        c = torch.arange(self.AC, device=self.device).repeat(self.AR)
+        sc.add_many(self.fy[:, None] + 18 * r[None], self.fx[:, None] + 16 * c[None], 10, 8,
+                    [olive if int(i) % 2 else green for i in r.tolist()], visible=self.alive.reshape(self.num_envs, -1))
+        sc.add(185, self.px, 8, 7, (50, 132, 50))
+        sc.add(self.sy, self.sx, 6, 1, (142, 142, 142), visible=self.shot)
+        sc.add(self.byp, self.bxp, 6, 1, (200, 200, 200), visible=self.bomb)
+        return sc
 
 
 # ===========================================================================
@@ -461,24 +514,21 @@ class AlienVec(PixelGameVec):
     def game_over(self):
         return (self.lives <= 0) | (~self.dots.view(self.num_envs, -1).any(1))
 
-    def draw(self, img):
-        wall = self.color((84, 92, 214))
-        for y in range(self.H):
-            for x in range(self.W):
-                if MAZE[y][x] == "#":
-                    img[:, self.Y0 + y * self.CH:self.Y0 + (y + 1) * self.CH, self.X0 + x * self.CW:self.X0 + (x + 1) * self.CW] = wall
+    def scene(self) -> Scene:
+        sc = Scene(self.num_envs, self.device)
+        cells = [(y, x) for y in range(self.H) for x in range(self.W) if MAZE[y][x] == "#"]
+        wy = torch.tensor([self.Y0 + y * self.CH for y, _ in cells], device=self.device)
+        wx = torch.tensor([self.X0 + x * self.CW for _, x in cells], device=self.device)
+        sc.add_many(wy, wx, self.CH, self.CW, [(84, 92, 214)] * len(cells))
         # eggs: 2x2 pixels at cell centres
-        m = torch.zeros(self.num_envs, SCREEN_H, SCREEN_W, dtype=torch.bool, device=self.device)
-        cy = self.Y0 + torch.arange(self.H, device=self.device) * self.CH + self.CH // 2
-        cx = self.X0 + torch.arange(self.W, device=self.device) * self.CW + self.CW // 2
-        for oy in (0, 1):
-            for ox in (0, 1):
-                m[:, (cy + oy)[:, None], (cx + ox)[None, :]] = self.dots
-        img[m] = self.color((223, 183, 85))
-        img[self.rect(self.Y0 + self.py * self.CH + 3, self.X0 + self.px * self.CW + 3, 10, 6)] = self.color((132, 144, 252))
-        for k in range(self.NA):
-            img[self.rect(self.Y0 + self.ay[:, k] * self.CH + 2, self.X0 + self.ax[:, k] * self.CW + 2, 12, 8)] = \
-                self.color((252, 144, 144))
+        yy = torch.arange(self.H, device=self.device).repeat_interleave(self.W)
+        xx = torch.arange(self.W, device=self.device).repeat(self.H)
+        sc.add_many(self.Y0 + yy * self.CH + self.CH // 2, self.X0 + xx * self.CW + self.CW // 2, 2, 2,
+                    [(223, 183, 85)] * (self.H * self.W), visible=self.dots.reshape(self.num_envs, -1))
+        sc.add(self.Y0 + self.py * self.CH + 3, self.X0 + self.px * self.CW + 3, 10, 6, (132, 144, 252))
+        sc.add_many(self.Y0 + self.ay * self.CH + 2, self.X0 + self.ax * self.CW + 2, 12, 8,
+                    [(252, 144, 144)] * self.NA)
+        return sc
 
 
 class MsPacmanVec(AlienVec):
@@ -579,14 +629,16 @@ class CentipedeVec(PixelGameVec):
     def game_over(self):
         return self.lives <= 0
 
-    def draw(self, img):
-        m = self.mush.repeat_interleave(8, 1).repeat_interleave(10, 2)          # [N,160,160]
-        img[:, 20:180, :][m] = self.color((181, 83, 40))
-        for k in range(self.NS):
-            mm = self.rect(20 + self.sy[:, k] * 8 + 1, self.sx[:, k] * 10 + 1, 6, 8) & self.salive[:, k][:, None, None]
-            img[mm] = self.color((184, 70, 162))
-        img[self.rect(184, self.px, 8, 4)] = self.color((181, 108, 224))
-        img[self.rect(self.shy, self.shx, 6, 1) & self.shot[:, None, None]] = self.color((181, 108, 224))
+    def scene(self) -> Scene:
+        sc = Scene(self.num_envs, self.device)
+        gy = torch.arange(self.GH, device=self.device).repeat_interleave(self.GW)
+        gx = torch.arange(self.GW, device=self.device).repeat(self.GH)
+        sc.add_many(20 + gy * 8, gx * 10, 8, 10, [(181, 83, 40)] * (self.GH * self.GW),
+                    visible=self.mush.reshape(self.num_envs, -1))
+        sc.add_many(20 + self.sy * 8 + 1, self.sx * 10 + 1, 6, 8, [(184, 70, 162)] * self.NS, visible=self.salive)
+        sc.add(184, self.px, 8, 4, (181, 108, 224))
+        sc.add(self.shy, self.shx, 6, 1, (181, 108, 224), visible=self.shot)
+        return sc
 
 
 GAMES = {"Breakout": BreakoutVec, "SpaceInvaders": SpaceInvadersVec, "Alien": AlienVec, "MsPacman": MsPacmanVec,

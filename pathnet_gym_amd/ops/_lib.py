@@ -48,6 +48,7 @@ _SIGS = {
                          c_int, c_int, P],
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_int, P, P, P, P, P, P],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
+    "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],
     "fast_conv_fwd": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P],
     "fast_conv_wgrad": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -126,3 +126,23 @@ def rgb_stack_push(rgb: torch.Tensor, obs_in: torch.Tensor, obs_out: torch.Tenso
     wr, wg, wb = gray_weights(gray)
     _lib.call("launch_rgb_stack_push", rgb.data_ptr(), obs_in.data_ptr(), obs_out.data_ptr(), _lib.ptr(r8),
               tab.data_ptr(), N, int(wr), int(wg), int(wb), _lib.stream())
+
+
+def rects_stack_push(geom: torch.Tensor, colors, bg, obs_in: torch.Tensor, obs_out: torch.Tensor, reset,
+                     tables: torch.Tensor, gray: str = "rgb"):
+    """Rasterise a rectangle scene ([N, R, 4] y0/x0/h/w, painter's order) + preprocess + stack push on device."""
+    from ..envs.pong import gray_weights
+    N, R = geom.shape[0], geom.shape[1]
+    _lib.check(obs_out, torch.uint8, numel=N * 160 * 120 * 4, name="obs_out")
+    _lib.check(obs_in, torch.uint8, numel=N * 160 * 120 * 4, name="obs_in")
+    g16 = geom.clamp(-32768, 32767).to(torch.int16).contiguous()
+    wr, wg, wb = gray_weights(gray)
+    lum = lambda c: (c[0] * wr + c[1] * wg + c[2] * wb + 8192) >> 14      # noqa: E731  cv2 fixed-point luma
+    key = (tuple(colors), gray, str(geom.device))
+    cache = rects_stack_push.__dict__.setdefault("_gray", {})
+    if key not in cache:
+        cache[key] = torch.tensor([lum(c) for c in colors], dtype=torch.uint8, device=geom.device)
+    tab = tables.to(device=geom.device, dtype=torch.int32).contiguous()
+    r8 = None if reset is None else _lib.check(reset.to(torch.uint8).contiguous(), torch.uint8, numel=N, name="reset")
+    _lib.call("launch_rects_stack_push", g16.data_ptr(), cache[key].data_ptr(), R, int(lum(bg)), obs_in.data_ptr(),
+              obs_out.data_ptr(), _lib.ptr(r8), tab.data_ptr(), N, _lib.stream())

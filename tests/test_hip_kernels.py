@@ -717,9 +717,9 @@ def test_image_staged_conv1_fwd_matches_fast(hip_lib):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("game", ["Breakout", "SpaceInvaders", "Alien"])
-def test_rgb_preprocess_kernel_bit_exact(hip_lib, game):
-    """Fused HIP gray + bilinear resize + stack push == the torch oracle, through resets."""
+@pytest.mark.parametrize("game", ["Breakout", "SpaceInvaders", "Alien", "MsPacman", "Centipede"])
+def test_rect_scene_render_kernel_bit_exact(hip_lib, game):
+    """HIP rectangle rasteriser + gray + bilinear resize + stack push == the torch renderer/preprocess oracle."""
     from pathnet_gym_amd.envs.registry import make
     envs = [make(game, num_envs=24, device=DEV, seed=5, backend=b) for b in ("torch", "hip")]
     o0, o1 = envs[0].reset(), envs[1].reset()
@@ -730,3 +730,22 @@ def test_rgb_preprocess_kernel_bit_exact(hip_lib, game):
         r = [e.step(a) for e in envs]
         assert torch.equal(r[0][0], r[1][0]), t
         assert torch.equal(r[0][2], r[1][2]) and torch.equal(r[0][1], r[1][1])
+
+
+def test_rgb_stack_push_matches_oracle(hip_lib):
+    """Standalone RGB -> gray -> resize -> stack push kernel (external frames) == preprocess_frames + push."""
+    from pathnet_gym_amd.envs.pong import preprocess_frames, resize_tables
+    from pathnet_gym_amd.ops.envs import rgb_stack_push
+    N = 10
+    g = torch.Generator().manual_seed(0)
+    rgb = torch.randint(0, 256, (N, 210, 160, 3), dtype=torch.uint8, generator=g).to(DEV)
+    obs_in = torch.randint(0, 256, (N, 160, 120, 4), dtype=torch.uint8, generator=g).to(DEV)
+    reset = torch.tensor([i % 3 == 0 for i in range(N)], device=DEV)
+    out = torch.empty_like(obs_in)
+    tabs = torch.from_numpy(resize_tables()).to(DEV)
+    for gray in ("rgb", "bgr"):
+        rgb_stack_push(rgb, obs_in, out, reset, tabs, gray)
+        f = preprocess_frames(rgb, tabs, gray)
+        ref = torch.where(reset[:, None, None, None], f[..., None].expand(-1, -1, -1, 4),
+                          torch.cat([obs_in[..., 1:], f[..., None]], 3))
+        assert torch.equal(out, ref), gray
