@@ -18,9 +18,12 @@ and the same preprocessing/stacking pipeline as Pong
                     mushrooms, shots worth 10 (segment) / 1 (mushroom).
 
 All dynamics are integer and the randomness uses the counter-based hash
-RNG of ``envs/base.py`` (same convention as Pong).  These envs run as torch
-ops on any device (CPU or GPU); they are not hipGraph-captured
-(``graph_safe = False``): the engine steps them eagerly.
+RNG of ``envs/base.py`` (same convention as Pong).  The game logic runs as
+torch ops on any device; a step has no host synchronisation and commits its
+state in place, so the engine captures it in the rollout hipGraph like the
+HIP envs.  On the GPU the frame is not rendered by torch at all: each game
+describes its scene as a rectangle list (``Scene``) that one fused kernel
+rasterises, preprocesses and pushes into the frame stack.
 """
 from __future__ import annotations
 
@@ -46,8 +49,10 @@ class Scene:
         self.parts, self.colors = [], []
 
     def _t(self, v):
-        t = torch.as_tensor(v, device=self.device, dtype=torch.int64)
-        return t
+        if isinstance(v, torch.Tensor):
+            return v.to(torch.int64)
+        # python scalar -> device fill kernel (no host->device copy: capturable in a hipGraph)
+        return torch.full((), int(v), dtype=torch.int64, device=self.device)
 
     def add(self, y0, x0, h, w, color, visible=None):
         y0, x0, h, w = [self._t(v).reshape(-1).expand(self.n) for v in (y0, x0, h, w)]
@@ -75,7 +80,7 @@ class Scene:
 
 class PixelGameVec(VecEnv):
     """Common driver: state tensors, frame stack, auto-reset, RGB render -> preprocessing."""
-    graph_safe = False
+    graph_safe = True          # no host syncs / host->device copies inside a step; state updated in place
     n_actions = 4
     max_steps = 27000
 
@@ -101,6 +106,11 @@ class PixelGameVec(VecEnv):
         self.obs = torch.zeros(num_envs, OBS_H, OBS_W, 4, dtype=torch.uint8, device=self.device)
         self._colors = {}
         self.init_state()
+        # per-env state tensors are updated IN PLACE at the end of every step (_commit), so a
+        # captured step (hipGraph) keeps reading and writing the same storage on replay
+        self._persist = {k: v for k, v in vars(self).items()
+                         if isinstance(v, torch.Tensor) and v.dim() >= 1 and v.shape[0] == num_envs
+                         and k not in ("obs", "env_id")}
         self.seed(seed)
 
     # -- helpers -------------------------------------------------------------
@@ -108,6 +118,13 @@ class PixelGameVec(VecEnv):
         self.seed_int = seed & 0xFFFFFFFF
         self._seed = torch.tensor(self.seed_int, dtype=torch.int64, device=self.device)
         self.counter.zero_()
+
+    def _commit(self):
+        for k, p in self._persist.items():
+            t = getattr(self, k)
+            if t is not p:
+                p.copy_(t)
+                setattr(self, k, p)
 
     def rand(self, stream: int, n: int) -> torch.Tensor:
         return env_rand_u32(self._seed, self.env_id, self.counter, stream) % n
@@ -124,7 +141,7 @@ class PixelGameVec(VecEnv):
         return (self.rows >= y0) & (self.rows < y0 + h) & (self.cols >= x0) & (self.cols < x0 + w)
 
     def where_set(self, t, mask, v):
-        return torch.where(mask, torch.as_tensor(v, dtype=t.dtype, device=t.device).expand_as(t), t)
+        return torch.where(mask, torch.full_like(t, v), t)
 
     # -- to implement ------------------------------------------------------------
     def init_state(self):
@@ -173,6 +190,7 @@ class PixelGameVec(VecEnv):
         self.steps = torch.where(mask, torch.zeros_like(self.steps), self.steps)
         self.epret = torch.where(mask, torch.zeros_like(self.epret), self.epret)
         self.counter += mask.long()
+        self._commit()
         self.obs = self._push(self.obs, mask)
 
     def _push(self, obs_in, reset, obs_out=None):
@@ -207,6 +225,7 @@ class PixelGameVec(VecEnv):
         self.steps = torch.where(done, torch.zeros_like(self.steps), self.steps)
         self.epret = torch.where(done, torch.zeros_like(self.epret), self.epret)
         self.counter += done.long()
+        self._commit()
         return reward, done, ep_return
 
     def step(self, actions):
@@ -310,7 +329,8 @@ class BreakoutVec(PixelGameVec):
         r = torch.arange(self.ROWS, device=self.device).repeat_interleave(self.COLS)
         c = torch.arange(self.COLS, device=self.device).repeat(self.ROWS)
         sc.add_many(self.BRICK_Y0 + r * self.BRICK_H, self.BRICK_X0 + c * self.BRICK_W, self.BRICK_H, self.BRICK_W,
-                    [self.ROW_COLOR[int(i)] for i in r.tolist()], visible=self.bricks.reshape(self.num_envs, -1))
+                    [self.ROW_COLOR[i // self.COLS] for i in range(self.ROWS * self.COLS)],
+                    visible=self.bricks.reshape(self.num_envs, -1))
         red = (200, 72, 72)
         sc.add(self.PADDLE_Y, self.px // self.U, 4, self.PADDLE_W, red)
         sc.add(self.by // self.U, self.bx // self.U, 4, 2, red, visible=self.inplay)
@@ -408,7 +428,8 @@ class SpaceInvadersVec(PixelGameVec):
         r = torch.arange(self.AR, device=self.device).repeat_interleave(self.AC)
         c = torch.arange(self.AC, device=self.device).repeat(self.AR)
         sc.add_many(self.fy[:, None] + 18 * r[None], self.fx[:, None] + 16 * c[None], 10, 8,
-                    [olive if int(i) % 2 else green for i in r.tolist()], visible=self.alive.reshape(self.num_envs, -1))
+                    [olive if (i // self.AC) % 2 else green for i in range(self.AR * self.AC)],
+                    visible=self.alive.reshape(self.num_envs, -1))
         sc.add(185, self.px, 8, 7, (50, 132, 50))
         sc.add(self.sy, self.sx, 6, 1, (142, 142, 142), visible=self.shot)
         sc.add(self.byp, self.bxp, 6, 1, (200, 200, 200), visible=self.bomb)
@@ -516,10 +537,12 @@ class AlienVec(PixelGameVec):
 
     def scene(self) -> Scene:
         sc = Scene(self.num_envs, self.device)
-        cells = [(y, x) for y in range(self.H) for x in range(self.W) if MAZE[y][x] == "#"]
-        wy = torch.tensor([self.Y0 + y * self.CH for y, _ in cells], device=self.device)
-        wx = torch.tensor([self.X0 + x * self.CW for _, x in cells], device=self.device)
-        sc.add_many(wy, wx, self.CH, self.CW, [(84, 92, 214)] * len(cells))
+        if not hasattr(self, "_walls_yx"):          # static maze walls, built once (outside any capture)
+            cells = [(y, x) for y in range(self.H) for x in range(self.W) if MAZE[y][x] == "#"]
+            self._walls_yx = (torch.tensor([self.Y0 + y * self.CH for y, _ in cells], device=self.device),
+                              torch.tensor([self.X0 + x * self.CW for _, x in cells], device=self.device))
+        wy, wx = self._walls_yx
+        sc.add_many(wy, wx, self.CH, self.CW, [(84, 92, 214)] * wy.shape[0])
         # eggs: 2x2 pixels at cell centres
         yy = torch.arange(self.H, device=self.device).repeat_interleave(self.W)
         xx = torch.arange(self.W, device=self.device).repeat(self.H)

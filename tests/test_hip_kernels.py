@@ -367,8 +367,8 @@ def test_engine_torch_implemented_game(hip_lib):
     cfg.tasks = ["Breakout", "SpaceInvaders"]
     cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 3
     tr = PathNetTrainer(cfg, device=DEV)
-    assert not tr.engine.use_graph
-    for _ in range(2):
+    assert tr.engine.use_graph                     # torch-logic games are capturable (in-place state, no syncs)
+    for _ in range(3):
         st = tr.update()
         assert np.isfinite(st.loss_v)
     tr.end_task()
@@ -749,3 +749,43 @@ def test_rgb_stack_push_matches_oracle(hip_lib):
         ref = torch.where(reset[:, None, None, None], f[..., None].expand(-1, -1, -1, 4),
                           torch.cat([obs_in[..., 1:], f[..., None]], 3))
         assert torch.equal(out, ref), gray
+
+
+@pytest.mark.parametrize("game", ["Breakout", "Centipede"])
+def test_torch_game_step_replays_in_hipgraph(hip_lib, game):
+    """A torch-logic game step captured once and replayed == the same game stepped eagerly."""
+    from pathnet_gym_amd.envs.registry import make
+    N = 32
+    ea = make(game, num_envs=N, device=DEV, seed=9, backend="hip")
+    eb = make(game, num_envs=N, device=DEV, seed=9, backend="hip")
+    oa = ea.reset()
+    eb.reset()
+    A = eb.num_actions
+    act = torch.zeros(N, dtype=torch.int32, device=DEV)
+    obs_in = eb.obs.clone().reshape(N, -1)
+    obs_out = torch.empty_like(obs_in)
+    rew = torch.zeros(N, device=DEV)
+    done = torch.zeros(N, dtype=torch.uint8, device=DEV)
+    epr = torch.zeros(N, device=DEV)
+    g = torch.Generator().manual_seed(3)
+    seq = [torch.randint(0, A, (N,), generator=g).to(torch.int32).to(DEV) for _ in range(25)]
+    # first step eager on both (warm-up, lazily built caches), then capture eb's step
+    oa, ra, da, _ = ea.step(seq[0])
+    act.copy_(seq[0])
+    eb.step_into(act, obs_in, obs_out, rew, done, epr)
+    assert torch.equal(obs_out.view_as(oa), oa)
+    obs_in.copy_(obs_out)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        eb.step_into(act, obs_in, obs_out, rew, done, epr)
+    torch.cuda.synchronize()
+    for t in range(1, 25):
+        oa, ra, da, _ = ea.step(seq[t])
+        act.copy_(seq[t])
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(obs_out.view_as(oa), oa), t
+        assert torch.equal(rew, ra) and torch.equal(done.bool(), da), t
+        obs_in.copy_(obs_out)
