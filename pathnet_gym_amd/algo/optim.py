@@ -42,11 +42,13 @@ class RMSPropTF:
         self.seg_trainable = torch.ones(self.nseg, dtype=torch.bool, device=dev)
         self.last_norms: Optional[torch.Tensor] = None
 
-    def set_frozen(self, frozen_mask: np.ndarray):
-        """frozen_mask [L, M]: exclude every segment of frozen modules."""
+    def set_frozen(self, frozen_mask: np.ndarray, frozen_tasks=()):
+        """frozen_mask [L, M]: exclude every segment of frozen modules (and per-task heads of finished tasks)."""
         tr = np.ones(self.nseg, bool)
         for i, s in enumerate(self.layout.segments):
             if s.layer >= 0 and frozen_mask[s.layer, s.module] > 0.5:
+                tr[i] = False
+            if s.task >= 0 and s.task in frozen_tasks:
                 tr[i] = False
         self.seg_trainable.copy_(torch.from_numpy(tr))
 

@@ -99,6 +99,8 @@ class PathNetTrainer:
         self.task_idx = 0
         self.updates = 0
         self.solved_generation: Dict[int, Optional[int]] = {}
+        self.task_paths: Dict[int, np.ndarray] = {}
+        self.frozen_tasks = set()
         self.env = None
         self.visualizer = None
         self._last_vis = 0.0
@@ -159,12 +161,16 @@ class PathNetTrainer:
         """Freeze the last winner and re-init every other parameter (doom_pathnet.py:274-293)."""
         self.flush()
         winner = self.pop.best()
+        # the path that solved this task, as expressed (its genotype OR the earlier frozen modules)
+        self.task_paths[self.task_idx] = self.pop.expressed()[winner].copy()
         frozen = self.pop.freeze(winner, union=self.cfg.ga.freeze_union)
+        if self.cfg.net.per_task_heads:
+            self.frozen_tasks.add(self.task_idx)          # keep this task's own head with its path
         self.model.set_frozen(frozen)
-        self.opt.set_frozen(frozen)
+        self.opt.set_frozen(frozen, self.frozen_tasks)
         keep = np.zeros(self.model.store.layout.numel, bool)
         for s in self.model.store.layout.segments:
-            if s.layer >= 0 and frozen[s.layer, s.module] > 0.5:
+            if (s.layer >= 0 and frozen[s.layer, s.module] > 0.5) or (s.task >= 0 and s.task in self.frozen_tasks):
                 keep[s.offset:s.offset + s.numel] = True
         keep_t = torch.from_numpy(keep).to(self.device)
         with torch.no_grad():
