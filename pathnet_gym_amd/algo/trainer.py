@@ -103,6 +103,7 @@ class PathNetTrainer:
         self.frozen_tasks = set()
         self.env = None
         self.visualizer = None
+        self.monitor = None          # envs.monitor.UpdateMonitor (--monitor_dir)
         self._last_vis = 0.0
         self.tracer = PhaseTracer(enabled=True, path=cfg.trace_path, rank=self.ctx.rank)
         self.guard = NonFiniteGuard(cfg.max_nonfinite)
@@ -392,6 +393,9 @@ class PathNetTrainer:
                     self.logger.log("perf", step=self.global_step, steps_per_sec=self.global_step / max(el, 1e-9),
                                     loss_pi=st.loss_pi, loss_v=st.loss_v, entropy=st.entropy,
                                     mean_return=st.mean_return, generation=self.pop.generation)
+                if self.monitor is not None:
+                    self.monitor.record(task_idx, self.updates, self.global_step, st.episodes, st.mean_return,
+                                        self.pop.generation)
                 if max_updates is not None and n >= max_updates:
                     break
             winner, frozen = self.end_task()

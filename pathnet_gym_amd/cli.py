@@ -38,7 +38,8 @@ def build_parser():
         p.add_argument("--job_name", default=None, help="accepted, ignored (every rank is a worker)")
         p.add_argument("--task_index", type=int, default=None, help="accepted, ignored (RANK env var)")
         p.add_argument("--log_dir", default=None)
-        p.add_argument("--monitor_dir", default=None, help="accepted (gym Monitor not used)")
+        p.add_argument("--monitor_dir", default=None,
+                       help="write gym-Monitor-style per-update episode records (envs/monitor.py)")
         p.add_argument("--M", type=int, default=None)
         p.add_argument("--L", type=int, default=None)
         p.add_argument("--N", type=int, default=None)
@@ -217,6 +218,9 @@ def cmd_train(a):
     if a.graphs and ctx.is_main:
         from .utils.visualize import GraphVisualize
         tr.visualizer = GraphVisualize([cfg.net.M] * cfg.net.L, out_dir=os.path.join(log_dir, "graphs"))
+    if getattr(a, "monitor_dir", None):
+        from .envs.monitor import UpdateMonitor
+        tr.monitor = UpdateMonitor(a.monitor_dir, rank=ctx.rank)
     logger.log("config", config=json.loads(cfg.to_json()), world=ctx.world, backend=tr.backend)
     solved = tr.train(max_updates=a.max_updates, checkpoint=a.checkpoint, checkpoint_every=a.checkpoint_every)
     if a.checkpoint:

@@ -13,6 +13,9 @@ Backends:
   random no-op start; the reference's ``time.sleep(3)`` on reset and
   ``env.render()`` every step are not reproduced;
 * ``gym_doom/...`` ids: ``envs/doom`` (needs the ViZDoom engine).
+
+``display=True`` (or ``monitor_dir=``) wraps on-device envs in ``envs.monitor.VecMonitor``
+writing to ``GYM_MONITOR_DIR-ROM``, as the reference's ``wrappers.Monitor`` (``:29-30``).
 """
 from __future__ import annotations
 
@@ -38,7 +41,7 @@ def preprocess_numpy(frame_rgb: np.ndarray, gray: str = "rgb") -> np.ndarray:
 
 class GameState:
     def __init__(self, rand_seed: int, ROM: str, display: bool = False, no_op_max: int = 7, task_index: int = -1,
-                 device="cpu", gray: str = "rgb"):
+                 device="cpu", gray: str = "rgb", monitor_dir=None):
         self.task_index = task_index
         self.ROM = ROM
         self.display = display
@@ -51,6 +54,12 @@ class GameState:
         if ROM in registered():
             kw = {} if ROM.startswith("CartPole") else dict(no_op_max=no_op_max)
             self._vec = make(ROM, num_envs=1, device=device, seed=rand_seed, **kw)
+            if display or monitor_dir:      # game_state.py:29-30: Monitor to GYM_MONITOR_DIR-ROM when displaying
+                from .monitor import VecMonitor
+                if monitor_dir is None:
+                    from ..compat.constants import GYM_MONITOR_DIR
+                    monitor_dir = GYM_MONITOR_DIR + "-" + ROM
+                self._vec = VecMonitor(self._vec, monitor_dir, force=True)
             self.n_actions = self._vec.num_actions
         elif ROM.startswith("gym_doom/"):
             from .doom import make_doom
