@@ -104,10 +104,12 @@ def supervised_config(L=3, M=10, N=3, width=20, din=32 * 32 * 3, module2=True):
 
 
 class SupervisedPathNet:
-    def __init__(self, cfg: PathNetConfig, population: int, num_tasks: int, device, seed=1, B=2):
+    def __init__(self, cfg: PathNetConfig, population: int, num_tasks: int, device, seed=1, B=2, backend="auto"):
         self.cfg = cfg
         self.P = population
         self.device = torch.device(device)
+        # "hip": the typed-module FC kernels (csrc/typed_fc.hip, K19); "torch": the dense masked oracle
+        self.backend = ("hip" if self.device.type == "cuda" else "torch") if backend == "auto" else backend
         self.store = ParamStore(cfg, self.device, seed)
         self.store.flat.requires_grad_(True)
         self.init_flat = self.store.flat.detach().clone()
@@ -120,8 +122,13 @@ class SupervisedPathNet:
         self.frozen = np.zeros((cfg.L, cfg.M), np.float32)
         self.frozen_elems = torch.zeros_like(self.store.flat, dtype=torch.bool)
 
-    def logits(self, X, mask, task):
-        feat = trunk_forward_ref(self.store, X, mask)
+    def logits(self, X, masks, rows_per_path, task):
+        """X rows grouped by path: masks [P, L, M], row r -> path r // rows_per_path."""
+        if self.backend == "hip":
+            from ..ops.typed_fc import typed_trunk_forward
+            feat = typed_trunk_forward(self.store, X, masks, rows_per_path)
+        else:
+            feat = trunk_forward_ref(self.store, X, masks.repeat_interleave(rows_per_path, 0))
         W, b = self.heads[task]
         return feat @ W + b
 
@@ -130,11 +137,10 @@ class SupervisedPathNet:
         n = X.shape[0]
         P = self.P
         masks = torch.from_numpy(self.pop.expressed()).to(self.device)
-        mask_rows = masks.repeat_interleave(batch, 0)
         g = torch.Generator(device="cpu").manual_seed(1000003 * gen + task)
         for _ in range(steps):
             idx = torch.randint(0, n, (P * batch,), generator=g).to(self.device)
-            logit = self.logits(X[idx], mask_rows, task)
+            logit = self.logits(X[idx], masks, batch, task)
             loss = F.cross_entropy(logit, y[idx], reduction="sum") / batch
             self.store.flat.grad = None
             W, b = self.heads[task]
@@ -149,7 +155,7 @@ class SupervisedPathNet:
         # fitness: accuracy of every path on a fresh evaluation batch
         with torch.no_grad():
             idx = torch.randint(0, n, (P * batch * 4,), generator=g).to(self.device)
-            pred = self.logits(X[idx], masks.repeat_interleave(batch * 4, 0), task).argmax(-1)
+            pred = self.logits(X[idx], masks, batch * 4, task).argmax(-1)
             acc = (pred == y[idx]).float().view(P, -1).mean(1)
         return acc.cpu().numpy()
 
