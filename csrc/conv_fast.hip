@@ -70,8 +70,9 @@ DEVI s8v ld8(const void* X, long off) {
 // ===========================================================================
 // forward: grid = (ceil(T*E*HOWO / 256), P); each wave loops over 32-row tiles
 // ===========================================================================
-#define FF_ROWS 512
-template <class G>
+// NT = 32-row tiles per wave: a workgroup covers NT*128 rows and stages the path's
+// active weights in LDS once for all of them.
+template <class G, int NT>
 __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X, bf16_t* __restrict__ Y,
                                                      uint8_t* __restrict__ bits, const bf16_t* __restrict__ Wc,
                                                      const float* __restrict__ flat, long bias_off, int chunk,
@@ -98,107 +99,118 @@ __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X,
   if (tid < NCT * 16) bias_s[tid] = (tid >> 3) < cnt ? flat[bias_off + (long)mods[tid >> 3] * chunk + (tid & 7)] : 0.f;
   __syncthreads();
 
-  const int Rtot = T * E * G::HOWO;
-  const int PE = P * E;
-  const int w = tid >> 6, l = tid & 63;
-  const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
-  // lane rows: A-operand rows (rbase + 16i + c16) and epilogue rows (rbase + 16i + 4q + r)
-  const int rfirst = blockIdx.x * FF_ROWS + w * 32;
-  RowIt ait[2], eit[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    rowit_init(ait[i], rfirst + i * 16 + c16, E, G::HOWO);
-    rowit_init(eit[i], rfirst + i * 16 + 4 * q, E, G::HOWO);
-  }
-  constexpr int NK = G::KP / 32;
-  using ARaw = typename std::conditional<G::U8, uint2, s8v>::type;
-  ARaw araw[2][NK];
-  // issue the global loads of one 32-row tile (2 MFMA row tiles x NK k-steps) into registers
-  auto load_tile = [&](int rbase) {
+  // compile-time column-tile count per instantiation (see conv_wgrad_slab)
+  auto run = [&](auto ncc) {
+    constexpr int NC = decltype(ncc)::value;
+    const int Rtot = T * E * G::HOWO;
+    const int PE = P * E;
+    const int w = tid >> 6, l = tid & 63;
+    const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
+    // lane rows: A-operand rows (rbase + 16i + c16) and epilogue rows (rbase + 16i + 4q + r)
+    constexpr int FF_ROWS = NT * 128;
+    const int rfirst = blockIdx.x * FF_ROWS + w * 32;
+    RowIt ait[2], eit[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const bool va = rbase < Rtot && ait[i].r < Rtot;
-      const int oh = ait[i].pos / G::WO, ow = ait[i].pos - oh * G::WO;
-      const long xb = rowit_sample(ait[i], p, E, PE, t0) * (long)G::IN_ELEMS +
-                      (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN;
-      rowit_adv(ait[i], 128, E, G::HOWO);
+      rowit_init(ait[i], rfirst + i * 16 + c16, E, G::HOWO);
+      rowit_init(eit[i], rfirst + i * 16 + 4 * q, E, G::HOWO);
+    }
+    constexpr int NK = G::KP / 32;
+    using ARaw = typename std::conditional<G::U8, uint2, s8v>::type;
+    ARaw araw[2][NK];
+    // issue the global loads of one 32-row tile (2 MFMA row tiles x NK k-steps) into registers
+    auto load_tile = [&](int rbase) {
 #pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        const int off = G::koff(kk * 4 + grp);
-        if constexpr (G::U8) {
-          araw[i][kk] = make_uint2(0u, 0u);
-          if (va && off >= 0) araw[i][kk] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xb + off);
-        } else {
-          araw[i][kk] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
-          if (va && off >= 0) araw[i][kk] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xb + off);
+      for (int i = 0; i < 2; ++i) {
+        const bool va = rbase < Rtot && ait[i].r < Rtot;
+        const int oh = ait[i].pos / G::WO, ow = ait[i].pos - oh * G::WO;
+        const long xb = rowit_sample(ait[i], p, E, PE, t0) * (long)G::IN_ELEMS +
+                        (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN;
+        rowit_adv(ait[i], 128, E, G::HOWO);
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const int off = G::koff(kk * 4 + grp);
+          if constexpr (G::U8) {
+            araw[i][kk] = make_uint2(0u, 0u);
+            if (va && off >= 0) araw[i][kk] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xb + off);
+          } else {
+            araw[i][kk] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+            if (va && off >= 0) araw[i][kk] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xb + off);
+          }
         }
       }
-    }
-  };
-  load_tile(rfirst);
-  for (int tile = 0; tile < FF_ROWS / 128; ++tile) {
-    const int rbase = rfirst + tile * 128;
-    if (rbase >= Rtot) break;
-    s8v a[2][NK];
+    };
+    load_tile(rfirst);
+    for (int tile = 0; tile < FF_ROWS / 128; ++tile) {
+      const int rbase = rfirst + tile * 128;
+      if (rbase >= Rtot) break;
+      s8v a[2][NK];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          if constexpr (G::U8) a[i][kk] = u8x8_to_bf16(araw[i][kk]);
+          else a[i][kk] = araw[i][kk];
+        }
+      if (tile + 1 < FF_ROWS / 128) load_tile(rbase + 128);     // next tile in flight during MFMAs + epilogue
+      f4v acc[2][NC];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ct = 0; ct < NC; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
-        if constexpr (G::U8) a[i][kk] = u8x8_to_bf16(araw[i][kk]);
-        else a[i][kk] = araw[i][kk];
-      }
-    if (tile + 1 < FF_ROWS / 128) load_tile(rbase + 128);     // next tile in flight during MFMAs + epilogue
-    f4v acc[2][NCT];
+        const int kc = kk * 4 + grp;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < NK; ++kk) {
-      const int kc = kk * 4 + grp;
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) {
-        if (ct < nct) {
+        for (int ct = 0; ct < NC; ++ct) {
           const s8v b = *reinterpret_cast<const s8v*>(Ws + (ct * 16 + c16) * KPs + kc * 8);
           acc[0][ct] = mfma16(a[0][kk], b, acc[0][ct]);
           acc[1][ct] = mfma16(a[1][kk], b, acc[1][ct]);
         }
       }
-    }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r16 = rbase + i * 16;
-      const RowIt e0 = eit[i];
-      rowit_adv(eit[i], 128, E, G::HOWO);
-      if (r16 >= Rtot) continue;
-      float sum[4] = {0.f, 0.f, 0.f, 0.f};
-      const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
+      for (int i = 0; i < 2; ++i) {
+        const int r16 = rbase + i * 16;
+        const RowIt e0 = eit[i];
+        rowit_adv(eit[i], 128, E, G::HOWO);
+        if (r16 >= Rtot) continue;
+        float sum[4] = {0.f, 0.f, 0.f, 0.f};
+        const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) {
-        if (ct < nct) {
-          const int slot = ct * 2 + h;
-          const bool sv = slot < cnt;
-          const float bb = bias_s[ct * 16 + c16];
-          uint32_t word = 0;
+        for (int ct = 0; ct < NC; ++ct) {
+          {
+            const int slot = ct * 2 + h;
+            const bool sv = slot < cnt;
+            const float bb = bias_s[ct * 16 + c16];
+            uint32_t word = 0;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = acc[i][ct][r] * in_scale + bb;
-            const bool pos = sv && v > 0.f;
-            sum[r] += pos ? v : 0.f;
-            const uint64_t bal = __ballot(pos);
-            word |= (uint32_t)((bal >> (16 * q + 8 * h)) & 0xFFull) << (8 * r);
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[i][ct][r] * in_scale + bb;
+              const bool pos = sv && v > 0.f;
+              sum[r] += pos ? v : 0.f;
+              const uint64_t bal = __ballot(pos);
+              word |= (uint32_t)((bal >> (16 * q + 8 * h)) & 0xFFull) << (8 * r);
+            }
+            if (ch == 0 && sv) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
           }
-          if (ch == 0 && sv) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
+        if (h == 0) {
+          // rows 4q..4q+3 of this tile are consecutive global rows (E*HOWO % 16 == 0)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Y[(grow4 + r) * 8 + ch] = f2bf(sum[r] * out_scale);
         }
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
-      if (h == 0) {
-        // rows 4q..4q+3 of this tile are consecutive global rows (E*HOWO % 16 == 0)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Y[(grow4 + r) * 8 + ch] = f2bf(sum[r] * out_scale);
-      }
     }
+  };
+  switch (nct) {
+    case 0:   // empty layer: zero weights -> zero output, cheapest instantiation
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    case 3: run(std::integral_constant<int, 3>{}); break;
+    case 4: run(std::integral_constant<int, 4>{}); break;
+    default: run(std::integral_constant<int, NCT>{}); break;
   }
 }
 
@@ -685,7 +697,12 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
 // (sample, band) units and atomically adds its partial dW/db.
 // ===========================================================================
 
-template <class G, int OB>
+// PF = stages of global loads in flight (register sets).  PF=2 keeps stage u+2's
+// loads in flight while stage u computes: one stage of MFMA work (~256 cycles
+// per wave) is far shorter than an HBM round trip, so with PF=1 every stage
+// waited on its own prefetch.  X loads are branch-free (clamped address, zeroed
+// at write time) so hipcc can count vmcnt across the two sets.
+template <class G, int OB, int PF>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict__ X, const float* __restrict__ Gr,
                                                           const uint8_t* __restrict__ bits, float* __restrict__ grad,
                                                           long w_off, long b_off, int chunk,
@@ -728,133 +745,158 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
       const int ob = rho / G::WO, ow = rho - ob * G::WO;
       aoff[ks][hf] = ob * G::S * SB::RL + ow * SB::PS + 4 * pp;
     }
-  float acc_b[3][8];
+  // The column-tile count is a compile-time constant in each instantiation: the
+  // MFMA / LDS-read loops are branch-free and fully unrolled (a runtime `nt < nct`
+  // guard around every MFMA made hipcc emit a scalar branch per MFMA and
+  // serialise the operand reads behind them).
+  auto run = [&](auto ncc) {
+    constexpr int NC = decltype(ncc)::value;
+    float acc_b[3][8];
 #pragma unroll
-  for (int k = 0; k < 3; ++k)
+    for (int k = 0; k < 3; ++k)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc_b[k][c] = 0.f;
-  f4v acc[MPW][NCT];
+      for (int c = 0; c < 8; ++c) acc_b[k][c] = 0.f;
+    f4v acc[MPW][NC];
 #pragma unroll
-  for (int a = 0; a < MPW; ++a)
+    for (int a = 0; a < MPW; ++a)
 #pragma unroll
-    for (int b = 0; b < NCT; ++b) acc[a][b] = {0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < NC; ++b) acc[a][b] = {0.f, 0.f, 0.f, 0.f};
 
-  using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
-  XRaw xr[SB::XIT];
-  float4 g0r[GIT], g1r[GIT];
-  uint32_t gbr[GIT][3];
-  bool gvr[GIT];
+    using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
+    struct Regs {
+      XRaw xr[SB::XIT];
+      float4 g0r[GIT], g1r[GIT];
+      uint32_t gbr[GIT][3];
+      bool gvr[GIT];
+      int navail;
+    };
+    Regs R[PF];
 
-  auto load_stage = [&](int u) {
-    const int s = u / SB::NB, band = u - s * SB::NB;
-    const long sg = sample_global(p, s, E, PE, 0);
-    const int ih0 = band * OB * G::S;
-    const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;   // elements inside the image
-    const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
+    auto load_stage = [&](Regs& Rg, int u) {
+      const int s = u / SB::NB, band = u - s * SB::NB;
+      const long sg = sample_global(p, s, E, PE, 0);
+      const int ih0 = band * OB * G::S;
+      const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;   // elements inside the image
+      Rg.navail = navail;
+      const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
 #pragma unroll
-    for (int j = 0; j < SB::XIT; ++j) {
-      const int gi = tid + 256 * j;
-      const int e0 = gi * 8;
-      if constexpr (G::U8) {
-        xr[j] = make_uint2(0u, 0u);
-        if (gi < SB::NG8 && e0 < navail)
-          xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xbase + e0);
-      } else {
-        xr[j] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
-        if (gi < SB::NG8 && e0 < navail)
-          xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xbase + e0);
+      for (int j = 0; j < SB::XIT; ++j) {
+        const int gi = tid + 256 * j;
+        const int e0 = (gi < SB::NG8 && gi * 8 < navail) ? gi * 8 : 0;   // clamped, zeroed at write time
+        if constexpr (G::U8)
+          Rg.xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xbase + e0);
+        else
+          Rg.xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xbase + e0);
       }
-    }
-    const int oh0 = band * OB;
+      const int oh0 = band * OB;
 #pragma unroll
-    for (int j = 0; j < GIT; ++j) {
-      const int it = tid + 256 * j;
-      const int rho = it >> 2, sub = it & 3;
-      const int ob = rho / G::WO, ow = rho - ob * G::WO;
-      gvr[j] = it < GROWS * 4 && rho < SB::NPOS && oh0 + ob < G::HO;
-      if (gvr[j]) {
-        const long go = sg * G::HOWO + (oh0 + ob) * G::WO + ow;
-        g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
-        g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+      for (int j = 0; j < GIT; ++j) {
+        const int it = tid + 256 * j;
+        const int rho = it >> 2, sub = it & 3;
+        const int ob = rho / G::WO, ow = rho - ob * G::WO;
+        Rg.gvr[j] = it < GROWS * 4 && rho < SB::NPOS && oh0 + ob < G::HO;
+        if (Rg.gvr[j]) {
+          const long go = sg * G::HOWO + (oh0 + ob) * G::WO + ow;
+          Rg.g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+          Rg.g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const int slot = sub + 4 * k;
+            Rg.gbr[j][k] = slot < cnt ? bits[(long)slot * bits_rows + go] : 0u;
+          }
+        }
+      }
+    };
+    auto write_stage = [&](const Regs& Rg, int buf) {
+#pragma unroll
+      for (int j = 0; j < SB::XIT; ++j) {
+        const int gi = tid + 256 * j;
+        if (gi < SB::NG8) {
+          s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
+          if (gi * 8 < Rg.navail) {
+            if constexpr (G::U8) v = u8x8_to_bf16(Rg.xr[j]);
+            else v = Rg.xr[j];
+          }
+          *reinterpret_cast<s8v*>(&Xs[buf][gi * 8]) = v;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < GIT; ++j) {
+        const int it = tid + 256 * j;
+        if (it >= GROWS * 4) continue;
+        const int rho = it >> 2, sub = it & 3;
+        const float gg[8] = {Rg.g0r[j].x, Rg.g0r[j].y, Rg.g0r[j].z, Rg.g0r[j].w,
+                             Rg.g1r[j].x, Rg.g1r[j].y, Rg.g1r[j].z, Rg.g1r[j].w};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           const int slot = sub + 4 * k;
-          gbr[j][k] = slot < cnt ? bits[(long)slot * bits_rows + go] : 0u;
+          if (slot < 2 * NC) {
+            float m[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) m[c] = (Rg.gvr[j] && ((Rg.gbr[j][k] >> c) & 1u)) ? gg[c] : 0.f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc_b[k][c] += m[c];
+            *reinterpret_cast<s8v*>(&Gs[buf][rho * GS + slot * 8]) = f32x8_to_bf16(m);
+          }
         }
       }
-    }
-  };
-  auto write_stage = [&](int buf) {
+    };
+    auto compute_stage = [&](int buf) {
+      const bf16_t* xs = Xs[buf];
+      const bf16_t* gs = Gs[buf];
 #pragma unroll
-    for (int j = 0; j < SB::XIT; ++j) {
-      const int gi = tid + 256 * j;
-      if (gi < SB::NG8) {
-        s8v v;
-        if constexpr (G::U8) v = u8x8_to_bf16(xr[j]);
-        else v = xr[j];
-        *reinterpret_cast<s8v*>(&Xs[buf][gi * 8]) = v;
-      }
-    }
+      for (int ks = 0; ks < SB::KS; ++ks) {
+        s8v bfr[NC];
 #pragma unroll
-    for (int j = 0; j < GIT; ++j) {
-      const int it = tid + 256 * j;
-      if (it >= GROWS * 4) continue;
-      const int rho = it >> 2, sub = it & 3;
-      const float gg[8] = {g0r[j].x, g0r[j].y, g0r[j].z, g0r[j].w, g1r[j].x, g1r[j].y, g1r[j].z, g1r[j].w};
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int slot = sub + 4 * k;
-        if (slot < 2 * nct) {
-          float m[8];
-#pragma unroll
-          for (int c = 0; c < 8; ++c) m[c] = (gvr[j] && ((gbr[j][k] >> c) & 1u)) ? gg[c] : 0.f;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) acc_b[k][c] += m[c];
-          *reinterpret_cast<s8v*>(&Gs[buf][rho * GS + slot * 8]) = f32x8_to_bf16(m);
-        }
-      }
-    }
-  };
-  __syncthreads();
-  if (u_beg < u_end) load_stage(u_beg);
-  int buf = 0;
-  for (int u = u_beg; u < u_end; ++u, buf ^= 1) {
-    write_stage(buf);
-    __syncthreads();
-    if (u + 1 < u_end) load_stage(u + 1);
-    const bf16_t* xs = Xs[buf];
-    const bf16_t* gs = Gs[buf];
-#pragma unroll
-    for (int ks = 0; ks < SB::KS; ++ks) {
-      s8v bfr[NCT];
-#pragma unroll
-      for (int nt = 0; nt < NCT; ++nt) {
-        if (nt < nct) {
+        for (int nt = 0; nt < NC; ++nt) {
           const s4v v0 = lds_tr16(gs + (ks * 32 + 8 * grp + q) * GS + nt * 16 + 4 * pp);
           const s4v v1 = lds_tr16(gs + (ks * 32 + 8 * grp + 4 + q) * GS + nt * 16 + 4 * pp);
           bfr[nt] = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
         }
+#pragma unroll
+        for (int mi = 0; mi < MPW; ++mi) {
+          const int mt = w * MPW + mi;
+          const int kb = (mt * 16 / SB::SEG) * SB::RL + (mt * 16) % SB::SEG;     // kernel row kh, k offset
+          const s4v v0 = lds_tr16(xs + kb + aoff[ks][0]);
+          const s4v v1 = lds_tr16(xs + kb + aoff[ks][1]);
+          const s8v afr = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+          for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mfma16(afr, bfr[nt], acc[mi][nt]);
+        }
       }
-#pragma unroll
-      for (int mi = 0; mi < MPW; ++mi) {
-        const int mt = w * MPW + mi;
-        const int kb = (mt * 16 / SB::SEG) * SB::RL + (mt * 16) % SB::SEG;     // kernel row kh, k offset
-        const s4v v0 = lds_tr16(xs + kb + aoff[ks][0]);
-        const s4v v1 = lds_tr16(xs + kb + aoff[ks][1]);
-        const s8v afr = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-#pragma unroll
-        for (int nt = 0; nt < NCT; ++nt)
-          if (nt < nct) acc[mi][nt] = mfma16(afr, bfr[nt], acc[mi][nt]);
+    };
+    __syncthreads();
+    if constexpr (PF == 1) {
+      if (u_beg < u_end) load_stage(R[0], u_beg);
+      int buf = 0;
+      for (int u = u_beg; u < u_end; ++u, buf ^= 1) {
+        write_stage(R[0], buf);
+        __syncthreads();
+        if (u + 1 < u_end) load_stage(R[0], u + 1);
+        compute_stage(buf);
+      }
+    } else {
+      // stage u lives in register set (u - u_beg) & 1 and LDS buffer (u - u_beg) & 1
+      if (u_beg < u_end) load_stage(R[0], u_beg);
+      if (u_beg + 1 < u_end) load_stage(R[1], u_beg + 1);
+      for (int u = u_beg; u < u_end; u += 2) {
+        write_stage(R[0], 0);
+        __syncthreads();
+        if (u + 2 < u_end) load_stage(R[0], u + 2);
+        compute_stage(0);
+        if (u + 1 >= u_end) break;
+        write_stage(R[1], 1);
+        __syncthreads();
+        if (u + 3 < u_end) load_stage(R[1], u + 3);
+        compute_stage(1);
       }
     }
-  }
-  const int h = i16 >> 3, ch = l & 7;
+    const int h = i16 >> 3, ch = l & 7;
 #pragma unroll
-  for (int mi = 0; mi < MPW; ++mi) {
-    const int mt = w * MPW + mi;
+    for (int mi = 0; mi < MPW; ++mi) {
+      const int mt = w * MPW + mi;
 #pragma unroll
-    for (int nt = 0; nt < NCT; ++nt) {
-      if (nt < nct) {
+      for (int nt = 0; nt < NC; ++nt) {
         const int slot = nt * 2 + h;
         if (slot < cnt) {
           const long base = w_off + (long)mods[slot] * chunk;
@@ -866,17 +908,24 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
         }
       }
     }
-  }
-  // bias: this thread's partials for slots (tid & 3) + 4k
+    // bias: this thread's partials for slots (tid & 3) + 4k
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int slot = (tid & 3) + 4 * k;
-    if (slot < cnt) {
+    for (int k = 0; k < 3; ++k) {
+      const int slot = (tid & 3) + 4 * k;
+      if (slot < cnt) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) atomicAdd(&dbias[slot * 8 + c], acc_b[k][c] * g_scale);
+        for (int c = 0; c < 8; ++c) atomicAdd(&dbias[slot * 8 + c], acc_b[k][c] * g_scale);
+      }
     }
+    __syncthreads();
+  };
+  switch (nct) {
+    case 1: run(std::integral_constant<int, 1>{}); break;
+    case 2: run(std::integral_constant<int, 2>{}); break;
+    case 3: run(std::integral_constant<int, 3>{}); break;
+    case 4: run(std::integral_constant<int, 4>{}); break;
+    default: run(std::integral_constant<int, NCT>{}); break;
   }
-  __syncthreads();
   if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
 }
 
@@ -1109,14 +1158,31 @@ static int dgrad_mfma_t(const float* Gr, const void* bits, const float* flat, lo
 }
 
 // ---------------------------------------------------------------------------
+static int FWD_NT = 4;         // 32-row tiles per wave in conv_fwd_fast (4 -> 512 rows per workgroup)
+static int WGRAD_PF = 1;       // register sets of slab-wgrad loads in flight (1 or 2)
+
+template <class G, int NT>
+static void fwd_launch(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
+                       int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0,
+                       long br, float is, float os, hipStream_t st) {
+  const long rows = (long)T * E * G::HOWO;
+  dim3 grid((unsigned)((rows + NT * 128 - 1) / (NT * 128)), P);
+  conv_fwd_fast<G, NT><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat, bias_off, chunk,
+                                             ai, ac, layer, L, M, P, E, T, t0, br, is, os);
+}
+
 template <class G>
 static int fwd_t(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off, int chunk,
                  const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0, long br,
                  float is, float os, hipStream_t st) {
-  const long rows = (long)T * E * G::HOWO;
-  dim3 grid((unsigned)((rows + FF_ROWS - 1) / FF_ROWS), P);
-  conv_fwd_fast<G><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat, bias_off, chunk, ai,
-                                         ac, layer, L, M, P, E, T, t0, br, is, os);
+  if (FWD_NT >= 16)
+    fwd_launch<G, 16>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st);
+  else if (FWD_NT >= 8)
+    fwd_launch<G, 8>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st);
+  else if (FWD_NT >= 4)
+    fwd_launch<G, 4>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st);
+  else
+    fwd_launch<G, 2>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st);
   return (int)hipGetLastError();
 }
 
@@ -1169,8 +1235,12 @@ static int wgrad_slab_t(const void* X, const float* Gr, const void* bits, float*
   long upw = (units + 23) / 24;
   if (upw < 8) upw = 8;
   dim3 grid((unsigned)((units + upw - 1) / upw), P);
-  conv_wgrad_slab<G, OB><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer,
-                                               L, M, P, E, T, br, (int)upw, is, gs);
+  if (WGRAD_PF >= 2)
+    conv_wgrad_slab<G, OB, 2><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac,
+                                                    layer, L, M, P, E, T, br, (int)upw, is, gs);
+  else
+    conv_wgrad_slab<G, OB, 1><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac,
+                                                    layer, L, M, P, E, T, br, (int)upw, is, gs);
   return (int)hipGetLastError();
 }
 
@@ -1208,6 +1278,8 @@ void fast_conv_set_slab_fwd(int on) { SLAB_FWD = on; }
 void fast_conv_set_dgrad_mfma(int on) { DGRAD_MFMA = on; }
 void fast_conv_set_img_fwd(int on) { IMG_FWD = on; }
 void fast_conv_set_wgrad_ob(int ob) { WGRAD_OB = ob; }
+void fast_conv_set_fwd_nt(int nt) { FWD_NT = nt; }
+void fast_conv_set_wgrad_pf(int pf) { WGRAD_PF = pf; }
 
 // return 1 if handled by a fast kernel, 0 if the shape is not specialised, <0 on error
 int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,

@@ -185,7 +185,16 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
   S.g_bg = g_bg; S.g_wall = g_wall; S.g_cpu = g_cpu; S.g_player = g_player; S.g_ball = g_ball;
   const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OBS_H * OBS_W / 4);
   uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OBS_H * OBS_W / 4);
-  for (int q = threadIdx.x; q < OBS_H * OBS_W / 4; q += 256) {
+  // The old-stack load of the NEXT item is issued before this item's render work
+  // (one load in flight ahead; a fully unrolled 19-deep prefetch bloated the code
+  // past the instruction cache and measured slower).  Each item is owned by one
+  // thread, so obs_in == obs_out stays correct.
+  constexpr int NQ = OBS_H * OBS_W / 4;
+  uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
+  if (!done) nxt = in4[min((int)threadIdx.x, NQ - 1)];
+  for (int q = threadIdx.x; q < NQ; q += 256) {
+    const uint4 cur = nxt;
+    if (!done && q + 256 < NQ) nxt = in4[q + 256];
     const int y = q / (OBS_W / 4), x0 = (q - y * (OBS_W / 4)) * 4;
     const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
     const bool row_dyn = ys0 < TOP || ys1 >= BOTTOM;
@@ -214,7 +223,7 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
     if (done) {
       o = make_uint4(f4[0] * 0x01010101u, f4[1] * 0x01010101u, f4[2] * 0x01010101u, f4[3] * 0x01010101u);
     } else {
-      const uint4 i = in4[q];
+      const uint4 i = cur;
       o = make_uint4((i.x >> 8) | (f4[0] << 24), (i.y >> 8) | (f4[1] << 24), (i.z >> 8) | (f4[2] << 24),
                      (i.w >> 8) | (f4[3] << 24));
     }

@@ -66,6 +66,8 @@ _SIGS = {
     "fast_conv_set_dgrad_mfma": [c_int],
     "fast_conv_set_img_fwd": [c_int],
     "fast_conv_set_wgrad_ob": [c_int],
+    "fast_conv_set_fwd_nt": [c_int],
+    "fast_conv_set_wgrad_pf": [c_int],
     "launch_ga_step": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_uint, P],
     "launch_ga_compact": [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P],
     "launch_typed_fc_fwd": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],

@@ -564,6 +564,38 @@ def test_slab_conv_kernels_match_fast(hip_lib, E):
         assert rel(a, b) < 2e-3, (s.name, rel(a, b))
 
 
+@pytest.mark.parametrize("nt,pf", [(2, 2), (8, 1), (16, 2)])
+def test_conv_pipeline_variants_match_default(hip_lib, nt, pf):
+    """conv_fwd_fast with 2/8/16 row tiles per wave and the 2-deep-prefetch slab wgrad == the default kernels."""
+    from pathnet_gym_amd.ops import _lib
+    cfg = small_pixel_cfg()
+    P, T, E = 3, 3, 16
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, seed=21)          # path 1: all 10 modules active
+    m = make_model(cfg, P, masks, seed=5)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    obs_steps = [torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+                 for _ in range(T)]
+    dfeat = torch.randn(T * P * E, 256, generator=g).to(DEV)
+    lib = _lib.lib()
+    f0, g0 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+    try:
+        lib.fast_conv_set_fwd_nt(nt)
+        lib.fast_conv_set_wgrad_pf(pf)
+        f1, g1 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
+    finally:
+        lib.fast_conv_set_fwd_nt(4)
+        lib.fast_conv_set_wgrad_pf(1)
+    assert rel(f1, f0) < 1e-5
+    for s in m.store.layout.segments:
+        if s.layer < 0 or s.layer > 2:
+            continue
+        a, b = g1[s.offset:s.offset + s.numel], g0[s.offset:s.offset + s.numel]
+        if b.norm() < 1e-6:
+            assert a.norm() < 1e-6, s.name
+            continue
+        assert rel(a, b) < 1e-4, (s.name, rel(a, b))
+
+
 def test_device_ga_matches_host_mirror(hip_lib):
     """csrc/ga.hip tournament + mutation + redraw == algo/ga_device.CounterPopulation, step by step;
     compaction == compact_active + the host inverse lists."""
