@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--tmax", type=int, default=20)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--ring", action="store_true", help="frame ring (single-frame writes) instead of packed stacks")
     ap.add_argument("--preset", default="pong")
     ap.add_argument("--kernel-opt", action="append", default=[],
                     help="kernel switch NAME=VALUE (fast_conv_set_*), for A/B measurements")
@@ -86,6 +87,7 @@ def main():
     cfg.a2c.t_max = args.tmax
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
+    cfg.frame_ring = args.ring
     cfg.ga.concurrent_tournaments = max(1, (cfg.paths * ctx.world) // 16)
     cfg.ga.backend = args.ga_backend
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
@@ -134,6 +136,7 @@ def main():
                 "parallelism": f"dp{ctx.world} (population split: {cfg.paths} paths x {cfg.envs_per_path} envs per GPU)",
                 "backend": args.backend,
                 "hipgraph": cfg.use_graph,
+                "frame_ring": bool(getattr(tr.engine, "ring", False)),
                 "ga": f"{cfg.ga.backend} (B={cfg.ga.B}, {cfg.ga.concurrent_tournaments} concurrent tournaments)",
                 "pipelined": bool(tr.pipelined),
             },

@@ -72,13 +72,22 @@ DEVI s8v ld8(const void* X, long off) {
 // ===========================================================================
 // NT = 32-row tiles per wave: a workgroup covers NT*128 rows and stages the path's
 // active weights in LDS once for all of them.
-template <class G, int NT>
+//
+// RING (first layer only): X is the frame ring [P*E][nslots][HIN*WIN] uint8 instead of packed
+// 4-channel stacks; channel c of sample (t, b) reads frame slot t + max(c, fc[t][b]) of env b
+// (fc = first valid channel after an episode reset, written by the env step).  A sample's four
+// planes are one contiguous 77 KB run, as a packed stack was.  k is channel-major
+// (k = (c*KH + kh)*KW + kw) so each A fragment is 8 consecutive pixels of one kernel row of one
+// frame plane: still one 8-byte load.  Wc holds the weights in that k order.
+template <class G, int NT, bool RING = false>
 __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X, bf16_t* __restrict__ Y,
                                                      uint8_t* __restrict__ bits, const bf16_t* __restrict__ Wc,
                                                      const float* __restrict__ flat, long bias_off, int chunk,
                                                      const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
                                                      int layer, int L, int M, int P, int E, int T, int t0,
-                                                     long bits_rows, float in_scale, float out_scale) {
+                                                     long bits_rows, float in_scale, float out_scale,
+                                                     const uint8_t* __restrict__ fcv = nullptr, int nslots = 0) {
+  static_assert(!RING || (G::U8 && G::CIN == 4 && G::KW == 8 && G::K == 256), "ring input: 8x8x4 uint8 layer");
   constexpr int KPs = G::KP + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Ws[NCT * 16 * KPs];
   __shared__ float bias_s[NCT * 16];
@@ -119,11 +128,44 @@ __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X,
     using ARaw = typename std::conditional<G::U8, uint2, s8v>::type;
     ARaw araw[2][NK];
     // issue the global loads of one 32-row tile (2 MFMA row tiles x NK k-steps) into registers
+    // RING: the first-valid-channel bytes of every tile this wave will touch, loaded once up
+    // front (a per-tile byte load would sit on the dependency path of that tile's X loads and
+    // expose its latency on every tile)
+    uint64_t fcw[2] = {0ull, 0ull};
+    if constexpr (RING) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        RowIt it = ait[i];
+#pragma unroll
+        for (int tl = 0; tl < NT; ++tl) {
+          if (it.r < Rtot) fcw[i] |= (uint64_t)fcv[rowit_sample(it, p, E, PE, t0)] << (8 * tl);
+          rowit_adv(it, 128, E, G::HOWO);
+        }
+      }
+    }
     auto load_tile = [&](int rbase) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const bool va = rbase < Rtot && ait[i].r < Rtot;
         const int oh = ait[i].pos / G::WO, ow = ait[i].pos - oh * G::WO;
+        if constexpr (RING) {
+          const int fc = (int)((fcw[i] >> (8 * ((rbase - rfirst) >> 7))) & 0xFFull);
+          const long slot0 = (long)(p * E + ait[i].e) * nslots + t0 + ait[i].t;
+          const long pix = (long)(oh * G::S * G::WIN + ow * G::S);
+          long cb[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) cb[c] = (slot0 + max(c, fc)) * (long)(G::HIN * G::WIN) + pix;
+          rowit_adv(ait[i], 128, E, G::HOWO);
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            const int kc = kk * 4 + grp;                 // channel kk/2, kernel row kc & 7
+            araw[i][kk] = make_uint2(0u, 0u);
+            if (va)
+              araw[i][kk] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + cb[kk >> 1] +
+                                                            (kc & 7) * G::WIN);
+          }
+          continue;
+        }
         const long xb = rowit_sample(ait[i], p, E, PE, t0) * (long)G::IN_ELEMS +
                         (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN;
         rowit_adv(ait[i], 128, E, G::HOWO);
@@ -702,15 +744,24 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
 // per wave) is far shorter than an HBM round trip, so with PF=1 every stage
 // waited on its own prefetch.  X loads are branch-free (clamped address, zeroed
 // at write time) so hipcc can count vmcnt across the two sets.
-template <class G, int OB, int PF>
+//
+// RING: X is the frame ring (see conv_fwd_fast); a stage loads 8 pixels of each of the 4
+// channel planes per thread and interleaves them into the packed (pixel, channel) slab at
+// LDS-write time, so the slab layout and every MFMA operand read are unchanged.
+template <class G, int OB, int PF, bool RING = false>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict__ X, const float* __restrict__ Gr,
                                                           const uint8_t* __restrict__ bits, float* __restrict__ grad,
                                                           long w_off, long b_off, int chunk,
                                                           const int* __restrict__ act_idx,
                                                           const int* __restrict__ act_cnt, int layer, int L, int M,
                                                           int P, int E, int T, long bits_rows, int units_per_wg,
-                                                          float in_scale, float g_scale) {
+                                                          float in_scale, float g_scale,
+                                                          const uint8_t* __restrict__ fcv = nullptr,
+                                                          int nslots = 0) {
   using SB = Slab<G, OB>;
+  static_assert(!RING || (G::U8 && G::CIN == 4 && G::WIN % 8 == 0), "ring input: uint8 4-channel first layer");
+  constexpr int NGP = SB::SR * G::WIN / 8;                 // ring: 8-pixel groups per slab
+  constexpr int XIT4 = (NGP + 255) / 256;
   constexpr int GS = NCT * 16 + 8;
   constexpr int NMT = G::KP / 16;
   constexpr int MPW = NMT / 4;
@@ -720,6 +771,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][GROWS * GS];
   __shared__ float dbias[NCT * 16];
   __shared__ int mods[MAXM_F];
+  constexpr int FCS = RING ? 1024 : 1;
+  __shared__ uint8_t fcs[FCS];     // RING: first-valid channel of this workgroup's samples
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
   if (cnt == 0) return;
@@ -727,6 +780,14 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
   if (tid < MAXM_F) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  const int s_first = (blockIdx.x * units_per_wg) / SB::NB;
+  if constexpr (RING) {
+    // staged once: a per-stage global byte load would expose its latency ahead of the X loads
+    const int s_last = min(T * E, (blockIdx.x * units_per_wg + units_per_wg + SB::NB - 1) / SB::NB);
+    for (int i = tid; i < s_last - s_first && i < FCS; i += 256) {
+      fcs[i] = fcv[sample_global(p, s_first + i, E, P * E, 0)];
+    }
+  }
   if (tid < NCT * 16) dbias[tid] = 0.f;
   for (int i = tid; i < 2 * GROWS * GS; i += 256) (&Gs[0][0])[i] = 0;
   for (int i = tid; i < 2 * 64; i += 256) Xs[i >> 6][SB::SLAB + (i & 63)] = 0;
@@ -764,7 +825,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
 
     using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
     struct Regs {
-      XRaw xr[SB::XIT];
+      XRaw xr[RING ? 1 : SB::XIT];
+      uint2 xq[RING ? XIT4 : 1][4];
       float4 g0r[GIT], g1r[GIT];
       uint32_t gbr[GIT][3];
       bool gvr[GIT];
@@ -778,9 +840,26 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
       const int ih0 = band * OB * G::S;
       const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;   // elements inside the image
       Rg.navail = navail;
+      if constexpr (RING) {
+        const int fc = (int)fcs[s - s_first];
+        const int ts = s / E;
+        const long slot0 = (long)(p * E + (s - ts * E)) * nslots + ts;
+        const int npx = min(SB::SR, G::HIN - ih0) * G::WIN;        // pixels inside the image
+        Rg.navail = npx;
+#pragma unroll
+        for (int j = 0; j < XIT4; ++j) {
+          const int gi = tid + 256 * j;
+          const int e0 = (gi < NGP && gi * 8 < npx) ? gi * 8 : 0;   // clamped, zeroed at write time
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            Rg.xq[j][c] = *reinterpret_cast<const uint2*>(
+                reinterpret_cast<const uint8_t*>(X) + (slot0 + max(c, fc)) * (long)(G::HIN * G::WIN) +
+                (long)ih0 * G::WIN + e0);
+        }
+      }
       const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
 #pragma unroll
-      for (int j = 0; j < SB::XIT; ++j) {
+      for (int j = 0; j < (RING ? 0 : SB::XIT); ++j) {
         const int gi = tid + 256 * j;
         const int e0 = (gi < SB::NG8 && gi * 8 < navail) ? gi * 8 : 0;   // clamped, zeroed at write time
         if constexpr (G::U8)
@@ -808,8 +887,32 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
       }
     };
     auto write_stage = [&](const Regs& Rg, int buf) {
+      if constexpr (RING) {
 #pragma unroll
-      for (int j = 0; j < SB::XIT; ++j) {
+        for (int j = 0; j < XIT4; ++j) {
+          const int gi = tid + 256 * j;
+          if (gi < NGP) {
+            const bool valid = gi * 8 < Rg.navail;
+#pragma unroll
+            for (int pr = 0; pr < 4; ++pr) {       // pixels 2pr, 2pr+1: (pixel, channel) bytes
+              uint32_t w2[2];
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const int px = 2 * pr + h, sh = 8 * (px & 3);
+                uint32_t w = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) w |= (((px < 4 ? Rg.xq[j][c].x : Rg.xq[j][c].y) >> sh) & 0xFFu) << (8 * c);
+                w2[h] = w;
+              }
+              s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
+              if (valid) v = u8x8_to_bf16(make_uint2(w2[0], w2[1]));
+              *reinterpret_cast<s8v*>(&Xs[buf][gi * 32 + pr * 8]) = v;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < (RING ? 0 : SB::XIT); ++j) {
         const int gi = tid + 256 * j;
         if (gi < SB::NG8) {
           s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1161,14 +1264,15 @@ static int dgrad_mfma_t(const float* Gr, const void* bits, const float* flat, lo
 static int FWD_NT = 4;         // 32-row tiles per wave in conv_fwd_fast (4 -> 512 rows per workgroup)
 static int WGRAD_PF = 1;       // register sets of slab-wgrad loads in flight (1 or 2)
 
-template <class G, int NT>
+template <class G, int NT, bool RING = false>
 static void fwd_launch(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
                        int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0,
-                       long br, float is, float os, hipStream_t st) {
+                       long br, float is, float os, hipStream_t st, const uint8_t* fcv = nullptr,
+                       int nslots = 0) {
   const long rows = (long)T * E * G::HOWO;
   dim3 grid((unsigned)((rows + NT * 128 - 1) / (NT * 128)), P);
-  conv_fwd_fast<G, NT><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat, bias_off, chunk,
-                                             ai, ac, layer, L, M, P, E, T, t0, br, is, os);
+  conv_fwd_fast<G, NT, RING><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat, bias_off,
+                                                   chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, fcv, nslots);
 }
 
 template <class G>
@@ -1225,10 +1329,10 @@ static int fwd_slab_t(const void* X, void* Y, void* bits, const void* Wc, const 
   return (int)hipGetLastError();
 }
 
-template <class G, int OB>
+template <class G, int OB, bool RING = false>
 static int wgrad_slab_t(const void* X, const float* Gr, const void* bits, float* grad, long w_off, long b_off,
                         int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, long br,
-                        float is, float gs, hipStream_t st) {
+                        float is, float gs, hipStream_t st, const uint8_t* fcv = nullptr, int nslots = 0) {
   using SB = Slab<G, OB>;
   const long units = (long)T * E * SB::NB;
   // ~24 workgroups per path (>= 1.5K workgroups at P=64), at least 8 units each
@@ -1236,11 +1340,11 @@ static int wgrad_slab_t(const void* X, const float* Gr, const void* bits, float*
   if (upw < 8) upw = 8;
   dim3 grid((unsigned)((units + upw - 1) / upw), P);
   if (WGRAD_PF >= 2)
-    conv_wgrad_slab<G, OB, 2><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac,
-                                                    layer, L, M, P, E, T, br, (int)upw, is, gs);
+    conv_wgrad_slab<G, OB, 2, RING><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai,
+                                                          ac, layer, L, M, P, E, T, br, (int)upw, is, gs, fcv, nslots);
   else
-    conv_wgrad_slab<G, OB, 1><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac,
-                                                    layer, L, M, P, E, T, br, (int)upw, is, gs);
+    conv_wgrad_slab<G, OB, 1, RING><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai,
+                                                          ac, layer, L, M, P, E, T, br, (int)upw, is, gs, fcv, nslots);
   return (int)hipGetLastError();
 }
 
@@ -1332,6 +1436,39 @@ int fast_conv_wgrad(const void* X, int u8in, const float* Gr, const void* bits, 
   WG(C1) WG(C2) WG(C3)
 #undef WG
   return 0;
+}
+
+// First layer on the frame ring (160x120 uint8 planes, 4 channels, 8x8/s4): fc = first valid
+// channel per (step, sample) [T+1][P*E] uint8.  Wc must be channel-major (launch_refresh_weights_cmajor).
+// frames [P*E][nslots][160*120] uint8 with nslots >= t0 + T + 3 (rollout: T_roll + 4 slots)
+int fast_conv1_ring_fwd(const void* frames, const void* fc, void* Y, void* bits, const void* Wc, const float* flat,
+                        long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E,
+                        int T, int t0, int nslots, long br, float is, float os, hipStream_t st) {
+  if (M > 2 * NCT) return -22;
+  if ((E * C1::HOWO) % 16) return -2;
+  if (nslots < t0 + T + 3) return -33;
+  const uint8_t* f = (const uint8_t*)fc;
+  if (FWD_NT >= 8)
+    fwd_launch<C1, 8, true>(frames, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os,
+                            st, f, nslots);
+  else
+    fwd_launch<C1, 4, true>(frames, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os,
+                            st, f, nslots);
+  return (int)hipGetLastError();
+}
+
+int fast_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, const void* bits, float* grad,
+                          long w_off, long b_off, int chunk, const int* ai, const int* ac, int layer, int L, int M,
+                          int P, int E, int T, int nslots, long br, float is, float gs, hipStream_t st) {
+  if (M > 2 * NCT) return -22;
+  if (nslots < T + 3) return -33;
+  if ((long)T * E / 24 + 3 > 1024) return -34;   // samples per workgroup vs the LDS first-channel table
+  const uint8_t* f = (const uint8_t*)fc;
+  if (WGRAD_OB == 3)
+    return wgrad_slab_t<C1, 3, true>(frames, Gr, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, is,
+                                     gs, st, f, nslots);
+  return wgrad_slab_t<C1, 2, true>(frames, Gr, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, is,
+                                   gs, st, f, nslots);
 }
 
 int fast_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,

@@ -111,6 +111,12 @@ DEVI bool digit_lit(int dig, bool show, int r, int c, int x0) {
   return (DIGITS[dig] >> (14 - (lr * 3 + lc))) & 1;
 }
 
+// scene colour of source row r ignoring the digits, paddles and ball
+DEVI int static_gray(const Scene& S, int r) {
+  if (r < WALL_TOP0) return S.g_bg;
+  return (r < TOP || r >= BOTTOM) ? S.g_wall : S.g_bg;
+}
+
 DEVI int scene_gray(const Scene& S, int r, int c) {
   if (r < WALL_TOP0) {
     if (digit_lit(S.cs_t, S.cs_t > 0, r, c, 24) || digit_lit(S.cs_o, true, r, c, 40)) return S.g_cpu;
@@ -127,24 +133,34 @@ DEVI int scene_gray(const Scene& S, int r, int c) {
 
 // state [B][12] int32, counter [B] uint32, actions [B] int32 (any int; >= n_actions remapped to 0)
 // obs_in/obs_out [B][160*120] uint32 (4 stacked uint8 frames), tables [8][160] int32
-__global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state, uint32_t* __restrict__ counter,
+//
+// RING: instead of pushing into a packed stack, write ONLY the new 160x120 frame plane
+// (frame_out [B][160*120] uint8, 19.2 KB per env instead of a 77 KB stack read + 77 KB
+// stack write) and the next stack's first valid channel: fc_out = done ? 3 : max(fc_in-1, 0)
+// (a reset stack repeats the fresh frame in all 4 channels; see conv_fwd_fast RING).
+template <bool RING>
+__global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ state, uint32_t* __restrict__ counter,
                                                         const int* __restrict__ actions, int n_actions,
                                                         const uint32_t* __restrict__ obs_in,
                                                         uint32_t* __restrict__ obs_out, const int* __restrict__ tables,
                                                         float* __restrict__ reward_out, uint8_t* __restrict__ done_out,
                                                         float* __restrict__ epret_out, uint32_t seed, int frameskip,
                                                         int max_steps, int no_op_max, int g_bg, int g_wall, int g_cpu,
-                                                        int g_player, int g_ball) {
+                                                        int g_player, int g_ball,
+                                                        const uint8_t* __restrict__ fc_in = nullptr,
+                                                        uint8_t* __restrict__ fc_out = nullptr,
+                                                        long out_stride = 0) {
   using namespace pong;
   __shared__ int tab[8 * 160];
   const int env = blockIdx.x;
   for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
   // --- physics (wave-uniform; every thread computes the same values) ---
   St st;
+  // wave-uniform state: readfirstlane keeps the physics on the scalar unit (SGPRs / SALU)
 #pragma unroll
-  for (int i = 0; i < NSTATE; ++i) st.s[i] = state[env * NSTATE + i];
-  uint32_t ctr = counter[env];
-  int a = actions[env];
+  for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
+  uint32_t ctr = (uint32_t)__builtin_amdgcn_readfirstlane((int)counter[env]);
+  int a = __builtin_amdgcn_readfirstlane(actions[env]);
   if (a >= n_actions || a < 0) a = 0;                    // game_state.py:38-39
   const int up = (a == 2 || a == 4), down = (a == 3 || a == 5);
   int reward = 0;
@@ -166,14 +182,20 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
     reward_out[env] = (float)reward;
     done_out[env] = done ? 1 : 0;
     epret_out[env] = done ? (float)epret : 0.f;
+    if constexpr (RING) fc_out[env] = done ? 3 : (uint8_t)max((int)fc_in[env] - 1, 0);
   }
   // --- fused render + gray + resize + stack push ---
-  // Only the score band (source rows < TOP), the bottom wall edge and the columns/rects
-  // the paddles and the ball can occupy differ from the flat background, so each output
-  // pixel evaluates its 4 bilinear source taps analytically ONLY when one of them can
-  // touch such a region; everywhere else the bilinear of a constant is that constant.
-  // Four horizontally adjacent pixels per thread: one 16-byte load of the old stack,
-  // one 16-byte store of the new (frame-stack push: (in >> 8) | f << 24 per pixel).
+  // Every source pixel outside five rectangles (the two score-digit blocks, the ball and the two
+  // paddles) has its row's static colour (background or wall band), so an output pixel none of
+  // whose 4 bilinear taps falls in a rectangle is the per-row constant vrow[y] -- the same
+  // fixed-point blend, since the horizontal weights sum to 2048.  Per workgroup, one pass over
+  // the 160 rows and 120 columns tabulates vrow and the rectangles each output row / column can
+  // touch; a quad then costs one LDS read unless its row touches a rectangle, and only pixels
+  // whose row AND column touch the same rectangle evaluate their 4 taps analytically.
+  // Packed mode: one 16-byte load of the old stack + one 16-byte store of the new per quad
+  // (frame-stack push (in >> 8) | f << 24); ring mode: one 4-byte store of the new frame.
+  __shared__ int rowinfo[OBS_H];     // vrow | (rect mask << 8)
+  __shared__ int colmask[OBS_W];
   Scene S;
   S.cy = st.s[CY] >> 4;   // floor division by U=16 (values are non-negative)
   S.py = st.s[PY] >> 4;
@@ -183,51 +205,81 @@ __global__ __launch_bounds__(256) void pong_step_kernel(int* __restrict__ state,
   S.cs_t = st.s[CS] / 10; S.cs_o = st.s[CS] % 10;
   S.ps_t = st.s[PS] / 10; S.ps_o = st.s[PS] % 10;
   S.g_bg = g_bg; S.g_wall = g_wall; S.g_cpu = g_cpu; S.g_player = g_player; S.g_ball = g_ball;
+  // source rectangles [r0, r1) x [c0, c1): cpu digits, player digits, ball, player, cpu
+  const int by0 = S.vis ? S.by : -1000, by1 = S.vis ? S.by + BALL_H : -1000;   // matches no row when hidden
+  const int R0[5] = {SCORE_ROW0, SCORE_ROW0, by0, S.py, S.cy};
+  const int R1[5] = {SCORE_ROW0 + 5 * DIGIT_SCALE, SCORE_ROW0 + 5 * DIGIT_SCALE, by1, S.py + PADDLE_H,
+                     S.cy + PADDLE_H};
+  const int C0[5] = {24, 104, S.bx, PLAYER_X, CPU_X};
+  const int C1[5] = {40 + 3 * DIGIT_SCALE, 120 + 3 * DIGIT_SCALE, S.bx + BALL_W, PLAYER_X + PADDLE_W,
+                     CPU_X + PADDLE_W};
+  for (int i = threadIdx.x; i < OBS_H + OBS_W; i += 256) {
+    if (i < OBS_H) {
+      const int ys0 = tab[0 * 160 + i], ys1 = tab[1 * 160 + i], cy0 = tab[2 * 160 + i], cy1 = tab[3 * 160 + i];
+      int m = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) m |= (ys1 >= R0[k] && ys0 < R1[k]) ? (1 << k) : 0;
+      int v = (static_gray(S, ys0) * cy0 + static_gray(S, ys1) * cy1 + 1024) >> 11;
+      v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      rowinfo[i] = v | (m << 8);
+    } else {
+      const int x = i - OBS_H;
+      const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x];
+      int m = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) m |= (xs1 >= C0[k] && xs0 < C1[k]) ? (1 << k) : 0;
+      colmask[x] = m;
+    }
+  }
+  __syncthreads();
   const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OBS_H * OBS_W / 4);
   uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OBS_H * OBS_W / 4);
-  // The old-stack load of the NEXT item is issued before this item's render work
-  // (one load in flight ahead; a fully unrolled 19-deep prefetch bloated the code
-  // past the instruction cache and measured slower).  Each item is owned by one
-  // thread, so obs_in == obs_out stays correct.
-  constexpr int NQ = OBS_H * OBS_W / 4;
+  uint32_t* outw = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(obs_out) + (long)env * out_stride);
+  // The old-stack load of the NEXT item is issued before this item's render work (one load in
+  // flight ahead).  Each item is owned by one thread, so obs_in == obs_out stays correct.
+  constexpr int NQ = OBS_H * OBS_W / 4, QR = OBS_W / 4;      // quads per frame / per row
+  static_assert(256 % QR == 16 && 256 / QR == 8, "quad walk below assumes 30 quads per row");
   uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
-  if (!done) nxt = in4[min((int)threadIdx.x, NQ - 1)];
+  if (!RING && !done) nxt = in4[min((int)threadIdx.x, NQ - 1)];
+  int y = (int)threadIdx.x / QR, xq = (int)threadIdx.x - y * QR;
   for (int q = threadIdx.x; q < NQ; q += 256) {
     const uint4 cur = nxt;
-    if (!done && q + 256 < NQ) nxt = in4[q + 256];
-    const int y = q / (OBS_W / 4), x0 = (q - y * (OBS_W / 4)) * 4;
-    const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
-    const bool row_dyn = ys0 < TOP || ys1 >= BOTTOM;
-    const bool ball_rows = S.vis && ys1 >= S.by && ys0 < S.by + BALL_H;
-    const bool pl_rows = ys1 >= S.py && ys0 < S.py + PADDLE_H;
-    const bool cpu_rows = ys1 >= S.cy && ys0 < S.cy + PADDLE_H;
-    uint32_t f4[4];
+    if (!RING && !done && q + 256 < NQ) nxt = in4[q + 256];
+    const int ri = rowinfo[y];
+    const uint32_t vr = (uint32_t)(ri & 0xFF);
+    uint32_t f4[4] = {vr, vr, vr, vr};
+    const int rm = ri >> 8;
+    if (rm) {
+      const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int x = x0 + e;
-      const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x];
-      const bool dyn = row_dyn || (ball_rows && xs1 >= S.bx && xs0 < S.bx + BALL_W) ||
-                       (pl_rows && xs1 >= PLAYER_X && xs0 < PLAYER_X + PADDLE_W) ||
-                       (cpu_rows && xs1 >= CPU_X && xs0 < CPU_X + PADDLE_W);
-      int v = g_bg;
-      if (dyn) {
-        const int cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
-        const int ra = scene_gray(S, ys0, xs0) * cx0 + scene_gray(S, ys0, xs1) * cx1;
-        const int rb = scene_gray(S, ys1, xs0) * cx0 + scene_gray(S, ys1, xs1) * cx1;
-        v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
-        v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      for (int e = 0; e < 4; ++e) {
+        const int x = xq * 4 + e;
+        if (rm & colmask[x]) {
+          const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x];
+          const int cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
+          const int ra = scene_gray(S, ys0, xs0) * cx0 + scene_gray(S, ys0, xs1) * cx1;
+          const int rb = scene_gray(S, ys1, xs0) * cx0 + scene_gray(S, ys1, xs1) * cx1;
+          const int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+          f4[e] = (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+        }
       }
-      f4[e] = (uint32_t)v;
     }
-    uint4 o;
-    if (done) {
-      o = make_uint4(f4[0] * 0x01010101u, f4[1] * 0x01010101u, f4[2] * 0x01010101u, f4[3] * 0x01010101u);
+    if constexpr (RING) {
+      outw[q] = f4[0] | (f4[1] << 8) | (f4[2] << 16) | (f4[3] << 24);
     } else {
-      const uint4 i = cur;
-      o = make_uint4((i.x >> 8) | (f4[0] << 24), (i.y >> 8) | (f4[1] << 24), (i.z >> 8) | (f4[2] << 24),
-                     (i.w >> 8) | (f4[3] << 24));
+      uint4 o;
+      if (done) {
+        o = make_uint4(f4[0] * 0x01010101u, f4[1] * 0x01010101u, f4[2] * 0x01010101u, f4[3] * 0x01010101u);
+      } else {
+        const uint4 i = cur;
+        o = make_uint4((i.x >> 8) | (f4[0] << 24), (i.y >> 8) | (f4[1] << 24), (i.z >> 8) | (f4[2] << 24),
+                       (i.w >> 8) | (f4[3] << 24));
+      }
+      out4[q] = o;
     }
-    out4[q] = o;
+    xq += 16;
+    y += 8;
+    if (xq >= QR) { xq -= QR; ++y; }
   }
 }
 
@@ -288,10 +340,24 @@ int launch_pong_step(void* state, void* counter, const int* actions, int n_actio
                      const int* tables, float* reward, void* done, float* epret, int B, unsigned seed, int frameskip,
                      int max_steps, int no_op_max, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
                      hipStream_t stream) {
-  pong_step_kernel<<<B, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions,
-                                          (const uint32_t*)obs_in, (uint32_t*)obs_out, tables, reward,
-                                          (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max, g_bg, g_wall,
-                                          g_cpu, g_player, g_ball);
+  pong_step_kernel<false><<<B, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions,
+                                                 (const uint32_t*)obs_in, (uint32_t*)obs_out, tables, reward,
+                                                 (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max, g_bg,
+                                                 g_wall, g_cpu, g_player, g_ball);
+  return (int)hipGetLastError();
+}
+
+// frame-ring variant: frame_out = env 0's new frame (160*120 uint8), env b's at + b*out_stride bytes;
+// fc_in/fc_out [B] uint8
+int launch_pong_step_ring(void* state, void* counter, const int* actions, int n_actions, void* frame_out,
+                          long out_stride, const void* fc_in, void* fc_out, const int* tables, float* reward,
+                          void* done, float* epret, int B, unsigned seed, int frameskip, int max_steps, int no_op_max,
+                          int g_bg, int g_wall, int g_cpu, int g_player, int g_ball, hipStream_t stream) {
+  if (out_stride < 160 * 120 || out_stride % 16) return -22;
+  pong_step_kernel<true><<<B, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions, nullptr,
+                                                (uint32_t*)frame_out, tables, reward, (uint8_t*)done, epret, seed,
+                                                frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu, g_player,
+                                                g_ball, (const uint8_t*)fc_in, (uint8_t*)fc_out, out_stride);
   return (int)hipGetLastError();
 }
 

@@ -317,6 +317,11 @@ class PongVec(VecEnv):
         if hip_state:
             henv.pong_sync_to_device(self)
 
+    def step_ring_into(self, actions, frames, slot, fc_in, fc_out, reward, done, epret):
+        """Engine frame-ring step (HIP only): write frames[:, slot] + the next first valid channel."""
+        from ..ops import envs as henv
+        henv.pong_step_ring_into(self, actions, frames, slot, fc_in, fc_out, reward, done, epret)
+
     def step(self, actions: torch.Tensor):
         if self.backend == "hip":
             from ..ops import envs as henv

@@ -46,6 +46,13 @@ _SIGS = {
     "launch_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
     "launch_pong_step": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, P],
+    "launch_refresh_weights_cmajor": [P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P, P],
+    "fast_conv1_ring_fwd": [P, P, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                            c_int, c_long, c_float, c_float, P],
+    "fast_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_long, c_float, c_float, P],
+    "launch_pong_step_ring": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int,
+                              c_int, c_int, c_int, c_int, P],
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_int, P, P, P, P, P, P],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],

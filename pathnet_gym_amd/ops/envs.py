@@ -54,6 +54,32 @@ def pong_step_into(env, actions, obs_in, obs_out, reward, done, epret):
               env.no_op_max, g[0], g[1], g[2], g[3], g[4], _lib.stream())
 
 
+def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done, epret):
+    """Frame-ring engine path: write only the new newest frame plane frames[:, slot] of the ring
+    [B][slots][160*120] and the next stack's first valid channel (csrc/envs.hip RING;
+    runtime/engine.py frame ring)."""
+    B = env.num_envs
+    if not hasattr(env, "_st32"):
+        pong_sync_to_device(env)
+    _lib.check(actions, torch.int32, (B,), name="actions")
+    _lib.check(frames, torch.uint8, name="frames")
+    if frames.dim() != 3 or frames.shape[0] != B or frames.shape[2] != 160 * 120 or not 0 <= slot < frames.shape[1]:
+        raise ValueError(f"frames {tuple(frames.shape)} / slot {slot} do not match [{B}, slots, 19200]")
+    _lib.check(fc_in, torch.uint8, numel=B, name="fc_in")
+    _lib.check(fc_out, torch.uint8, numel=B, name="fc_out")
+    _lib.check(reward, torch.float32, numel=B, name="reward")
+    _lib.check(done, torch.uint8, numel=B, name="done")
+    _lib.check(epret, torch.float32, numel=B, name="epret")
+    if not hasattr(env, "_gray"):
+        env._gray = _gray_consts(env)
+    g = env._gray
+    _lib.call("launch_pong_step_ring", env._st32.data_ptr(), env._ctr32.data_ptr(), actions.data_ptr(),
+              env.num_actions, frames[0, slot].data_ptr(), frames.stride(0), fc_in.data_ptr(), fc_out.data_ptr(),
+              env._tab32.data_ptr(),
+              reward.data_ptr(), done.data_ptr(), epret.data_ptr(), B, env.seed_int, env.frameskip,
+              env.max_episode_steps, env.no_op_max, g[0], g[1], g[2], g[3], g[4], _lib.stream())
+
+
 def pong_step(env, actions, obs):
     B = env.num_envs
     dev = obs.device

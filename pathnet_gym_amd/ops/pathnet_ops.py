@@ -8,6 +8,8 @@ name           layout                                     written by
 =============  =========================================  ==================
 obs            [T+1][B][H*W*C] uint8 (pixels) or           env step kernel
                [T+1][B][8] bf16 (vector envs)
+frames, fc     frame ring [B][T+4][H*W] uint8 + first valid    ring env step
+               channel [T+1][B] (replaces obs for Pong)
 acts[l]        [T+1][B][HWo*Cout] bf16 (module-sum out)    fwd epilogue
 bits[l] conv   [M][(T+1)*B*HWo] uint8 (8 maps/byte)        fwd epilogue
 bits[l] fc     [M][(T+1)*B][Cout/16] uint16                fwd epilogue
@@ -129,7 +131,21 @@ class HipPathNet:
                 self.lstm = dict(F=F, H=H, k_off=ls["kernel"], b_off=ls["bias"],
                                  KpT=torch.zeros(4 * H, F + H, dtype=torch.bfloat16, device=dev),
                                  Kb=torch.zeros(F + H, 4 * H, dtype=torch.bfloat16, device=dev))
+        # frame-ring input for the first layer (runtime/engine.py): channel-major bf16 weights
+        g0 = self.geoms[0]
+        self.ring_ok = (g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
+                        and self.M <= 10 and g0.Cout == 8)
+        self.Wc_ring = None
         self.refresh_weights()
+
+    def enable_ring(self):
+        """Allocate the channel-major first-layer weight copy used with the frame ring."""
+        if not self.ring_ok:
+            raise NotImplementedError("frame ring needs the 160x120x4 / 8x8 s4 first conv layer and M <= 10")
+        if self.Wc_ring is None:
+            g = self.geoms[0]
+            self.Wc_ring = torch.zeros(self.M, g.Cout, g.KP, dtype=torch.bfloat16, device=self.model.device)
+            self.refresh_weights()
 
     # ------------------------------------------------------------------
     def set_paths(self, expressed: np.ndarray):
@@ -157,6 +173,10 @@ class HipPathNet:
         for l, g in enumerate(self.geoms):
             _lib.call("launch_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
                       self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), _lib.stream())
+        if self.Wc_ring is not None:
+            g = self.geoms[0]
+            _lib.call("launch_refresh_weights_cmajor", flat.data_ptr(), g.w_off, g.chunk, g.KH, g.KW, g.Cin, g.Cout,
+                      self.M, self.Wc_ring.data_ptr(), _lib.stream())
         if self.lstm is not None:
             ls = self.lstm
             _lib.call("launch_lstm_refresh", flat.data_ptr(), ls["k_off"], ls["F"], ls["H"], ls["KpT"].data_ptr(),
@@ -259,6 +279,35 @@ class HipPathNet:
                 _lib.call("launch_fc_dgrad", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
                           m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.K, g.KP, g.Cout, P, E,
                           T, bits_rows, g_scale, dX.data_ptr(), st)
+
+    # -- first layer on the frame ring (frames [B][T+4][H*W] u8, fc [T+1][B] u8) --------
+    def _check_ring(self, frames, fc, P, E, steps):
+        g = self.geoms[0]
+        _lib.check(frames, torch.uint8, name="frames")
+        _lib.check(fc, torch.uint8, name="fc")
+        if frames.dim() != 3 or frames.shape[0] != P * E or frames.shape[2] != g.Hin * g.Win:
+            raise ValueError(f"frames shape {tuple(frames.shape)} != [P*E, slots, {g.Hin * g.Win}]")
+        if frames.shape[1] < steps + 3 or fc.numel() < steps * P * E:
+            raise ValueError("frame ring too short for the requested steps")
+
+    def ring_fwd(self, frames, fc, Y, bits, P: int, E: int, T: int, t0: int, bits_rows: int):
+        self._check_ring(frames, fc, P, E, t0 + T)
+        g = self.geoms[0]
+        m = self.model
+        out_scale = self.out_scale_last if self.L == 1 else 1.0
+        _lib.call("fast_conv1_ring_fwd", frames.data_ptr(), fc.data_ptr(), Y.data_ptr(), bits.data_ptr(),
+                  self.Wc_ring.data_ptr(), m.store.flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
+                  m.act_cnt.data_ptr(), 0, self.L, self.M, P, E, T, t0, frames.shape[1], bits_rows, g.in_scale,
+                  out_scale, _lib.stream())
+
+    def ring_wgrad(self, frames, fc, G, bits, grad_flat, P: int, E: int, T: int, bits_rows: int):
+        self._check_ring(frames, fc, P, E, T)
+        g = self.geoms[0]
+        m = self.model
+        g_scale = self.out_scale_last if self.L == 1 else 1.0
+        _lib.call("fast_conv1_ring_wgrad", frames.data_ptr(), fc.data_ptr(), G.data_ptr(), bits.data_ptr(),
+                  grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), 0,
+                  self.L, self.M, P, E, T, frames.shape[1], bits_rows, g.in_scale, g_scale, _lib.stream())
 
     # ------------------------------------------------------------------
     def alloc_bits(self, l: int, steps: int, B: int):

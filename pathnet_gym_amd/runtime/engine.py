@@ -50,7 +50,20 @@ class HipEngine:
         self.device = dev
         hp = self.hip
         self.pixels = hp.pixels
-        if self.pixels:
+        # Frame ring (Pong, standard 160x120x4 trunk): the rollout keeps T+4 single frame planes
+        # instead of T+1 packed 4-frame stacks; stack t = frames t..t+3 (newest last) with the
+        # channels before fc[t] replaced by the first valid frame after an episode reset.  The env
+        # step writes 19.2 KB per env instead of reading + writing a 77 KB stack.
+        self.ring = bool(self.pixels and getattr(cfg, "frame_ring", True) and hp.ring_ok and _lib.USE_FAST
+                         and hasattr(env, "step_ring_into"))
+        self.obs = None
+        if self.ring:
+            H, W, C = model.cfg.input_shape
+            hp.enable_ring()
+            self.HW = H * W
+            self.frames = torch.zeros(B, T + 4, H * W, dtype=torch.uint8, device=dev)   # env-major: a stack is contiguous
+            self.fc = torch.zeros(T + 1, B, dtype=torch.uint8, device=dev)
+        elif self.pixels:
             H, W, C = model.cfg.input_shape
             self.obs = torch.zeros(T + 1, B, H * W * C, dtype=torch.uint8, device=dev)
         else:
@@ -112,9 +125,38 @@ class HipEngine:
         """Copy the env's current observation into slot 0."""
         o = env.obs if self.pixels else None
         if self.pixels:
-            self.obs[0].copy_(o.reshape(self.B, -1))
+            self.set_obs_stack0(o.reshape(self.B, -1))
         else:
             self.obs[0].copy_(henv.obs_to_bf16_padded(env.state.float()))
+
+    # -- packed-stack views of the observation buffers (tests, checkpoints) -------
+    def obs_stack(self, t: int) -> torch.Tensor:
+        """Stack of step t as [B, H*W*4] uint8 (pixel-major, channel-minor, newest frame last)."""
+        if not self.ring:
+            return self.obs[t]
+        B = self.B
+        dev = self.device
+        c = torch.arange(4, device=dev)
+        idx = t + torch.maximum(c[None, :], self.fc[t].long()[:, None])           # [B, 4] frame slots
+        planes = self.frames[torch.arange(B, device=dev)[:, None], idx]           # [B, 4, H*W]
+        return planes.permute(0, 2, 1).reshape(B, -1).contiguous()
+
+    def obs_stacks(self, n: Optional[int] = None) -> torch.Tensor:
+        """Stacks of steps 0..n-1 (default T+1) as [n, B, H*W*4] uint8 (or the vector obs)."""
+        n = self.T + 1 if n is None else n
+        if not self.ring:
+            return self.obs[:n]
+        return torch.stack([self.obs_stack(t) for t in range(n)])
+
+    def set_obs_stack0(self, stack: torch.Tensor):
+        """Install a packed [B, H*W*4] stack as the observation entering step 0."""
+        if not self.ring:
+            self.obs[0].copy_(stack.reshape(self.B, -1))
+            return
+        st = stack.reshape(self.B, self.HW, 4)
+        for c in range(4):
+            self.frames[:, c].copy_(st[:, :, c])
+        self.fc[0].zero_()
 
     def _build_opt_tables(self):
         segs = self.model.store.layout.segments
@@ -142,7 +184,10 @@ class HipEngine:
     # ------------------------------------------------------------------
     def _env_step(self, t):
         env = self.env
-        if hasattr(env, "step_into"):
+        if self.ring:
+            env.step_ring_into(self.actions[t], self.frames, t + 4, self.fc[t], self.fc[t + 1], self.rewards[t],
+                               self.dones[t], self.epret[t])
+        elif hasattr(env, "step_into"):
             env.step_into(self.actions[t], self.obs[t], self.obs[t + 1], self.rewards[t], self.dones[t],
                           self.epret[t])
         elif self.pixels:
@@ -152,13 +197,31 @@ class HipEngine:
             henv.cartpole_step_into(env, self.actions[t], self.obs[t + 1], self.rewards[t], self.dones[t],
                                     self.epret[t])
 
-    def _forward_step(self, t, greedy=False):
+    def _trunk_step(self, t):
         hp = self.hip
-        P, E = self.P, self.E
         x = self.obs
         for l in range(len(hp.geoms)):
-            hp.layer_fwd(l, x, self.acts[l], self.bits[l], P, E, 1, t, self.bits_rows[l])
+            if l == 0 and self.ring:
+                hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0])
+            else:
+                hp.layer_fwd(l, x, self.acts[l], self.bits[l], self.P, self.E, 1, t, self.bits_rows[l])
             x = self.acts[l]
+
+    def _layer_bwd_all(self, T):
+        hp = self.hip
+        P, E = self.P, self.E
+        for l in range(len(hp.geoms) - 1, -1, -1):
+            if l == 0 and self.ring:
+                hp.ring_wgrad(self.frames, self.fc, self.grads[0], self.bits[0], self.grad_flat, P, E, T,
+                              self.bits_rows[0])
+                continue
+            X = self.obs if l == 0 else self.acts[l - 1]
+            dX = self.grads[l - 1] if l > 0 else None
+            hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
+
+    def _forward_step(self, t, greedy=False):
+        hp = self.hip
+        self._trunk_step(t)
         feat = self.acts[-1][t]
         if self.lstm_hip:
             # state entering step t: slot t, reset where the previous step ended an episode
@@ -169,13 +232,6 @@ class HipEngine:
             feat = self.hst[t + 1]
         hp.heads_fwd(feat, self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t,
                      self.T + 1, greedy=greedy, task=self.model.task)
-
-    def _trunk_step(self, t):
-        hp = self.hip
-        x = self.obs
-        for l in range(len(hp.geoms)):
-            hp.layer_fwd(l, x, self.acts[l], self.bits[l], self.P, self.E, 1, t, self.bits_rows[l])
-            x = self.acts[l]
 
     def _rollout_backward_hybrid(self):
         """LSTM nets: HIP trunk fwd/bwd, torch (autograd) LSTM + heads + loss in between."""
@@ -218,11 +274,7 @@ class HipEngine:
         self.stats[0], self.stats[1], self.stats[2] = lp, lv, ent * T * B
         self.grads[-1].copy_(torch.cat([f.grad for f in feats]))
         self.grad_flat.zero_()
-        hp = self.hip
-        for l in range(len(hp.geoms) - 1, -1, -1):
-            X = self.obs if l == 0 else self.acts[l - 1]
-            dX = self.grads[l - 1] if l > 0 else None
-            hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
+        self._layer_bwd_all(T)
         tn = st.layout.trunk_numel
         self.grad_flat[tn:] += st.flat.grad[tn:]
         st.flat.grad = None
@@ -254,10 +306,7 @@ class HipEngine:
             feat = self.acts[L - 1][:T].reshape(T * B, -1)
             hp.heads_bwd(feat, self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1), self.grad_flat,
                          self.grads[L - 1], task=self.model.task)
-        for l in range(L - 1, -1, -1):
-            X = self.obs if l == 0 else self.acts[l - 1]
-            dX = self.grads[l - 1] if l > 0 else None
-            hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
+        self._layer_bwd_all(T)
         self._count_nonfinite()
 
     def _fitness_update(self):
@@ -363,7 +412,12 @@ class HipEngine:
         self.hip.refresh_weights()
         if self.ga_dev is not None:
             self._ga_body()
-        self.obs[0].copy_(self.obs[self.T])
+        if self.ring:
+            src = self.frames[:, self.T:self.T + 4]
+            self.frames[:, 0:4].copy_(src if self.T >= 4 else src.clone())   # T < 4: the slot ranges overlap
+            self.fc[0].copy_(self.fc[self.T])
+        else:
+            self.obs[0].copy_(self.obs[self.T])
         self.ctr.add_(1)
 
     # ------------------------------------------------------------------

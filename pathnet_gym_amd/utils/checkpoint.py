@@ -77,7 +77,7 @@ def rank_tensors(trainer) -> Dict[str, torch.Tensor]:
     if trainer.engine is not None:
         eng = trainer.engine
         out["engine.ctr"] = _t(eng.ctr)
-        out["engine.obs0"] = _t(eng.obs[0])
+        out["engine.obs0"] = _t(eng.obs_stack(0))
         out["engine.fitness"] = _t(eng.fitness)
         out["engine.fit_cnt"] = _t(eng.fit_cnt)
         out["engine.fit_sum"] = _t(eng.fit_sum)
@@ -148,7 +148,7 @@ def load(trainer, path: str, strict: bool = True):
         if trainer.engine is not None:
             eng = trainer.engine
             eng.ctr.copy_(r["engine.ctr"].to(dev))
-            eng.obs[0].copy_(r["engine.obs0"].to(dev))
+            eng.set_obs_stack0(r["engine.obs0"].to(dev))
             eng.fitness.copy_(r["engine.fitness"].to(dev))
             if "engine.fit_cnt" in r:
                 eng.fit_cnt.copy_(r["engine.fit_cnt"].to(dev))

@@ -377,8 +377,8 @@ def test_engine_torch_implemented_game(hip_lib):
     assert np.isfinite(st.loss_v)
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_engine_gradient_matches_oracle(hip_lib, graph):
+@pytest.mark.parametrize("graph,ring", [(False, True), (True, True), (False, False)])
+def test_engine_gradient_matches_oracle(hip_lib, graph, ring):
     """Whole engine update == autograd of the A2C loss over the SAME stored rollout.
 
     Recomputes logits/values with the fp32 oracle from the engine's stored
@@ -392,22 +392,26 @@ def test_engine_gradient_matches_oracle(hip_lib, graph):
     cfg = preset("pong")
     cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 4
     cfg.use_graph = graph
+    cfg.frame_ring = ring
     tr = PathNetTrainer(cfg, device=DEV)
     eng = tr.engine
+    assert eng.ring == ring
+    tr.env.max_episode_steps = 5           # episode resets inside the rollouts (frame-ring first-channel path)
     for _ in range(3 if graph else 1):     # with graphs: eager, capture, then a replayed update
         tr.update()
     T, P, E, B, A = eng.T, eng.P, eng.E, eng.B, eng.A
-    obs0 = eng.obs[0].clone()
+    obs0 = eng.obs_stack(0).clone()
     if graph:
         eng.rollout_backward()
     else:
         eng._rollout_backward_body()
     torch.cuda.synchronize()
-    assert torch.equal(eng.obs[0], obs0)
+    assert torch.equal(eng.obs_stack(0), obs0)
+    assert eng.dones.any()
     a2c = cfg.a2c
     flat = tr.model.store.flat.detach().clone().requires_grad_(True)
     st = ParamStore(cfg.net, DEV, flat=flat)
-    x = eng.obs[:T + 1].reshape((T + 1) * B, 160, 120, 4).float() / 255.0
+    x = eng.obs_stacks().reshape((T + 1) * B, 160, 120, 4).float() / 255.0
     mask = tr.model.mask.repeat_interleave(E, 0).repeat(T + 1, 1, 1)
     feat = trunk_forward_ref(st, x, mask, emulate_bf16=True)
     logits, values = heads_ref(st, feat)
@@ -430,6 +434,46 @@ def test_engine_gradient_matches_oracle(hip_lib, graph):
     worst = max(errs, key=errs.get)
     print({k: round(v, 4) for k, v in sorted(errs.items(), key=lambda kv: -kv[1])[:8]})
     assert errs[worst] < 6e-2, (worst, errs[worst])
+
+
+def test_frame_ring_stacks_match_packed_env(hip_lib):
+    """Frame-ring rollout (single-frame writes + first-valid-channel bytes) reproduces, bit for bit,
+    the packed 4-frame stacks the packed Pong kernel produces for the same actions, resets included."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.ops import envs as henv
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 7
+    cfg.use_graph = False
+    cfg.frame_ring = True
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng, env = tr.engine, tr.env
+    assert eng.ring
+    env.max_episode_steps = 3
+    tr.update()
+    torch.cuda.synchronize()
+    st0, ctr0 = env._st32.clone(), env._ctr32.clone()
+    cur = eng.obs_stack(0).clone()
+    eng._rollout_backward_body()
+    torch.cuda.synchronize()
+    st_eng, ctr_eng = env._st32, env._ctr32
+    env._st32, env._ctr32 = st0, ctr0
+    B = eng.B
+    try:
+        for t in range(eng.T):
+            nxt = torch.empty_like(cur)
+            r = torch.empty(B, device=DEV)
+            d = torch.empty(B, dtype=torch.uint8, device=DEV)
+            e = torch.empty(B, device=DEV)
+            henv.pong_step_into(env, eng.actions[t].contiguous(), cur, nxt, r, d, e)
+            torch.cuda.synchronize()
+            assert torch.equal(d, eng.dones[t]), t
+            assert torch.equal(r, eng.rewards[t]), t
+            assert torch.equal(nxt, eng.obs_stack(t + 1)), t
+            cur = nxt
+        assert eng.dones.any()
+        assert torch.equal(env._st32, st_eng)
+    finally:
+        env._st32, env._ctr32 = st_eng, ctr_eng
 
 
 def test_lstm_cell_kernels_match_autograd(hip_lib):
@@ -500,7 +544,7 @@ def test_engine_lstm_gradient_matches_oracle(hip_lib):
     st = ParamStore(cfg.net, DEV, flat=flat)
     k, bb = st.lstm()
     kq = bf16_ste(k)
-    x = eng.obs[:T + 1].reshape((T + 1) * B, 160, 120, 4).float() / 255.0
+    x = eng.obs_stacks().reshape((T + 1) * B, 160, 120, 4).float() / 255.0
     mask = tr.model.mask.repeat_interleave(E, 0).repeat(T + 1, 1, 1)
     feat = trunk_forward_ref(st, x, mask, emulate_bf16=True).view(T + 1, B, -1)
     h, c = h0, c0
