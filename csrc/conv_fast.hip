@@ -80,7 +80,7 @@ DEVI s8v ld8(const void* X, long off) {
 // (k = (c*KH + kh)*KW + kw) so each A fragment is 8 consecutive pixels of one kernel row of one
 // frame plane: still one 8-byte load.  Wc holds the weights in that k order.
 template <class G, int NT, bool RING = false>
-__global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X, bf16_t* __restrict__ Y,
+__global__ __launch_bounds__(256, 3) void conv_fwd_fast(const void* __restrict__ X, bf16_t* __restrict__ Y,
                                                      uint8_t* __restrict__ bits, const bf16_t* __restrict__ Wc,
                                                      const float* __restrict__ flat, long bias_off, int chunk,
                                                      const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
@@ -186,14 +186,13 @@ __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X,
     for (int tile = 0; tile < FF_ROWS / 128; ++tile) {
       const int rbase = rfirst + tile * 128;
       if (rbase >= Rtot) break;
-      s8v a[2][NK];
+      // raw fragments of this tile; the uint8 -> bf16 conversion happens per k-step next to its
+      // MFMAs (holding all converted fragments cost 64 VGPRs and capped occupancy at 2 waves)
+      ARaw cur[2][NK];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int kk = 0; kk < NK; ++kk) {
-          if constexpr (G::U8) a[i][kk] = u8x8_to_bf16(araw[i][kk]);
-          else a[i][kk] = araw[i][kk];
-        }
+        for (int kk = 0; kk < NK; ++kk) cur[i][kk] = araw[i][kk];
       if (tile + 1 < FF_ROWS / 128) load_tile(rbase + 128);     // next tile in flight during MFMAs + epilogue
       f4v acc[2][NC];
 #pragma unroll
@@ -203,11 +202,19 @@ __global__ __launch_bounds__(256) void conv_fwd_fast(const void* __restrict__ X,
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
         const int kc = kk * 4 + grp;
+        s8v a0, a1;
+        if constexpr (G::U8) {
+          a0 = u8x8_to_bf16(cur[0][kk]);
+          a1 = u8x8_to_bf16(cur[1][kk]);
+        } else {
+          a0 = cur[0][kk];
+          a1 = cur[1][kk];
+        }
 #pragma unroll
         for (int ct = 0; ct < NC; ++ct) {
           const s8v b = *reinterpret_cast<const s8v*>(Ws + (ct * 16 + c16) * KPs + kc * 8);
-          acc[0][ct] = mfma16(a[0][kk], b, acc[0][ct]);
-          acc[1][ct] = mfma16(a[1][kk], b, acc[1][ct]);
+          acc[0][ct] = mfma16(a0, b, acc[0][ct]);
+          acc[1][ct] = mfma16(a1, b, acc[1][ct]);
         }
       }
 #pragma unroll

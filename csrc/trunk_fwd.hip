@@ -283,7 +283,11 @@ __global__ __launch_bounds__(256) void fc_fwd_kernel(
 // so a path's active modules stream their weights in parallel instead of one
 // after another -- the per-step fc layers are latency-bound, not FLOP-bound.
 // ---------------------------------------------------------------------------
-template <int RT>
+//
+// D = k-steps of A/B fragments in flight per wave.  The grid is one workgroup per (path, 64
+// columns) -- one wave per SIMD -- so registers are free and a deep prefetch ring cuts the
+// latency chain of the 44-step K loop (fc1: K = 1408) by D.
+template <int RT, int D>
 __global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
     const bf16_t* __restrict__ X, int ldx, bf16_t* __restrict__ Y, uint16_t* __restrict__ bits,
     const bf16_t* __restrict__ Wc, const float* __restrict__ flat, long bias_off, int chunk,
@@ -322,29 +326,37 @@ __global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
     for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
-    s8v an[RT], bn[4];
-    auto load = [&](int kk) {
+    s8v an[D][RT], bn[D][4];
+    auto load = [&](s8v (&ad)[RT], s8v (&bd)[4], int kk) {
       const int k0 = kk + 8 * grp;
 #pragma unroll
       for (int i = 0; i < RT; ++i) {
-        an[i] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
-        if (xv[i] && k0 < K) an[i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+        ad[i] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+        if (xv[i] && k0 < K) ad[i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bn[j] = *reinterpret_cast<const s8v*>(Wm + (long)j * 16 * KP + kk);
+      for (int j = 0; j < 4; ++j) bd[j] = *reinterpret_cast<const s8v*>(Wm + (long)j * 16 * KP + kk);
     };
-    load(0);
-    for (int kk = 0; kk < KP; kk += 32) {
-      s8v ac[RT], bc[4];
 #pragma unroll
-      for (int i = 0; i < RT; ++i) ac[i] = an[i];
+    for (int d = 0; d < D; ++d)
+      if (d * 32 < KP) load(an[d], bn[d], d * 32);
+    for (int kk0 = 0; kk0 < KP; kk0 += 32 * D) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bc[j] = bn[j];
-      if (kk + 32 < KP) load(kk + 32);
+      for (int d = 0; d < D; ++d) {
+        const int kk = kk0 + d * 32;
+        if (kk < KP) {
+          s8v ac[RT], bc[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+          for (int i = 0; i < RT; ++i) ac[i] = an[d][i];
 #pragma unroll
-        for (int i = 0; i < RT; ++i) acc[i][j] = mfma16(ac[i], bc[j], acc[i][j]);
+          for (int j = 0; j < 4; ++j) bc[j] = bn[d][j];
+          if (kk + 32 * D < KP) load(an[d], bn[d], kk + 32 * D);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < RT; ++i) acc[i][j] = mfma16(ac[i], bc[j], acc[i][j]);
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -391,6 +403,8 @@ __global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+#define FC_MW_D 4
+
 extern "C" {
 
 size_t conv_fwd_smem(int KP, int M) {
@@ -426,11 +440,11 @@ int launch_fc_fwd(const void* X, int ldx, void* Y, void* bits, const void* Wc, c
   if (rows <= 32 && Cout % 64 == 0) {
     dim3 grid(1, Cout / 64, P);
     if (rows <= 16)
-      fc_fwd_mw_kernel<1><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
+      fc_fwd_mw_kernel<1, FC_MW_D><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
                                                     (const bf16_t*)Wc, flat, bias_off, chunk, act_idx, act_cnt, layer,
                                                     L, M, K, KP, Cout, P, E, T, t0, bits_rows, out_scale);
     else
-      fc_fwd_mw_kernel<2><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
+      fc_fwd_mw_kernel<2, FC_MW_D><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
                                                     (const bf16_t*)Wc, flat, bias_off, chunk, act_idx, act_cnt, layer,
                                                     L, M, K, KP, Cout, P, E, T, t0, bits_rows, out_scale);
   } else if (rows <= 32) {
