@@ -169,6 +169,21 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_fast(const void* __restrict__
         const long xb = rowit_sample(ait[i], p, E, PE, t0) * (long)G::IN_ELEMS +
                         (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN;
         rowit_adv(ait[i], 128, E, G::HOWO);
+        if constexpr (G::KW * G::CIN == 32 && G::K == G::KP) {
+          // one kernel row per 32-k block: the lane offset is koff(grp) and block kk adds the
+          // compile-time row stride -> one 64-bit address per row half, immediate load offsets
+          using El = typename std::conditional<G::U8, uint8_t, bf16_t>::type;
+          const El* src = reinterpret_cast<const El*>(X) + xb + G::koff(grp);
+          if (va) {
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk)
+              araw[i][kk] = *reinterpret_cast<const ARaw*>(src + kk * G::WIN * G::CIN);
+          } else {
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk) araw[i][kk] = ARaw{};
+          }
+          continue;
+        }
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) {
           const int off = G::koff(kk * 4 + grp);

@@ -12,6 +12,8 @@ rm -rf /tmp/kprof
     || { echo "PROF FAIL"; tail -20 gpurun_out/kprof_$TAG.log; exit 4; }
 f=$(find /tmp/kprof -name "*kernel_stats.csv" | head -1)
 cp "$f" gpurun_out/kstats_$TAG.csv
+t=$(find /tmp/kprof -name "*kernel_trace.csv" | head -1)
+gzip -c "$t" > gpurun_out/ktrace_$TAG.csv.gz
 python3 scripts/prof_summary.py gpurun_out/kstats_$TAG.csv $(( ${STEPS:-5} + 2 )) "$TAG [${ARGS:-}]" > gpurun_out/kstats_$TAG.md
 head -20 gpurun_out/kstats_$TAG.md
 tail -1 gpurun_out/kprof_$TAG.log
