@@ -13,6 +13,14 @@
 // This replaces ALE + OpenCV + the 4-deep numpy stack of the reference.
 #include "common.h"
 
+// phase stamps for the diagnostic probe (scripts/probe_env.hip defines PONG_STAMP); no-op here
+#ifndef PONG_STAMP
+#define PONG_STAMP(i)
+#endif
+#ifndef PONG_LOOP_STAMP
+#define PONG_LOOP_STAMP(it, slow)
+#endif
+
 namespace pong {
 constexpr int SCREEN_W = 160;
 constexpr int OBS_H = 160, OBS_W = 120;
@@ -98,17 +106,19 @@ DEVI void reset_state(St& st, uint32_t seed, uint32_t env, uint32_t counter, int
 }
 
 struct Scene {
-  int cy, py, bx, by, vis, cs_t, cs_o, ps_t, ps_o;
+  int cy, py, bx, by, vis;
+  int dmask[4];           // 3x5 glyph bits of cpu tens / ones, player tens / ones (0 = not shown)
   int g_bg, g_wall, g_cpu, g_player, g_ball;
 };
 
-DEVI bool digit_lit(int dig, bool show, int r, int c, int x0) {
-  if (!show) return false;
+// glyph bits are resolved once per workgroup (Scene::dmask): a per-tap DIGITS[] load put a
+// scalar-memory round trip on every evaluated score pixel
+DEVI bool digit_lit(int mask, int r, int c, int x0) {
   const int dc = c - x0, dr = r - SCORE_ROW0;
   if (dc < 0 || dr < 0) return false;
   const int lc = dc / DIGIT_SCALE, lr = dr / DIGIT_SCALE;
   if (lc >= 3 || lr >= 5) return false;
-  return (DIGITS[dig] >> (14 - (lr * 3 + lc))) & 1;
+  return (mask >> (14 - (lr * 3 + lc))) & 1;
 }
 
 // scene colour of source row r ignoring the digits, paddles and ball
@@ -117,11 +127,28 @@ DEVI int static_gray(const Scene& S, int r) {
   return (r < TOP || r >= BOTTOM) ? S.g_wall : S.g_bg;
 }
 
-DEVI int scene_gray(const Scene& S, int r, int c) {
+// score band (source rows SCORE_ROW0 .. +5*DIGIT_SCALE, digit columns 24..51 and 104..131) as
+// per-source-pixel gray levels, built once per workgroup in LDS
+constexpr int BAND_R = 5 * DIGIT_SCALE, BAND_C = 56;
+constexpr int DL_R = 18;    // output rows of the per-workgroup score-digit box (rows 0..16 reach a digit)
+
+DEVI int band_col(int c) { return (c >= 24 && c < 52) ? c - 24 : ((c >= 104 && c < 132) ? c - 104 + 28 : -1); }
+
+// playfield-side scene colour, branch-free (walls / background + ball > player > cpu): the quad
+// loop's per-pixel path only ever sees paddle / ball rows (digit pixels come from dlut)
+DEVI int scene_gray_pf(const Scene& S, int r, int c) {
+  int g = (r < TOP || r >= BOTTOM) ? (r < WALL_TOP0 ? S.g_bg : S.g_wall) : S.g_bg;
+  const bool play = r >= TOP && r < BOTTOM;
+  g = (play && c >= CPU_X && c < CPU_X + PADDLE_W && r >= S.cy && r < S.cy + PADDLE_H) ? S.g_cpu : g;
+  g = (play && c >= PLAYER_X && c < PLAYER_X + PADDLE_W && r >= S.py && r < S.py + PADDLE_H) ? S.g_player : g;
+  g = (play && S.vis && c >= S.bx && c < S.bx + BALL_W && r >= S.by && r < S.by + BALL_H) ? S.g_ball : g;
+  return g;
+}
+
+DEVI int scene_gray(const Scene& S, const uint8_t* band, int r, int c) {
   if (r < WALL_TOP0) {
-    if (digit_lit(S.cs_t, S.cs_t > 0, r, c, 24) || digit_lit(S.cs_o, true, r, c, 40)) return S.g_cpu;
-    if (digit_lit(S.ps_t, S.ps_t > 0, r, c, 104) || digit_lit(S.ps_o, true, r, c, 120)) return S.g_player;
-    return S.g_bg;
+    const int bc = band_col(c);
+    return (r >= SCORE_ROW0 && r < SCORE_ROW0 + BAND_R && bc >= 0) ? (int)band[(r - SCORE_ROW0) * BAND_C + bc] : S.g_bg;
   }
   if (r < TOP || r >= BOTTOM) return S.g_wall;
   if (S.vis && c >= S.bx && c < S.bx + BALL_W && r >= S.by && r < S.by + BALL_H) return S.g_ball;
@@ -151,39 +178,54 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
                                                         uint8_t* __restrict__ fc_out = nullptr,
                                                         long out_stride = 0) {
   using namespace pong;
-  __shared__ int tab[8 * 160];
+  __shared__ __attribute__((aligned(16))) int tab[8 * 160];
   const int env = blockIdx.x;
+  PONG_STAMP(0);
   for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
-  // --- physics (wave-uniform; every thread computes the same values) ---
-  St st;
-  // wave-uniform state: readfirstlane keeps the physics on the scalar unit (SGPRs / SALU)
+  // --- physics: wave 0 only (scalar code; the 4 waves of a workgroup share ONE scalar unit per
+  // CU with the other workgroups there, so running it redundantly in every wave made the SALU the
+  // kernel's bottleneck), published through LDS ---
+  __shared__ int phys[NSTATE + 4];
+  if (threadIdx.x < 64) {
+    St st;
 #pragma unroll
-  for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
-  uint32_t ctr = (uint32_t)__builtin_amdgcn_readfirstlane((int)counter[env]);
-  int a = __builtin_amdgcn_readfirstlane(actions[env]);
-  if (a >= n_actions || a < 0) a = 0;                    // game_state.py:38-39
-  const int up = (a == 2 || a == 4), down = (a == 3 || a == 5);
-  int reward = 0;
-  for (int f = 0; f < frameskip; ++f) reward += subframe(st, up, down, seed, (uint32_t)env, ctr);
-  ctr += 1;
-  st.s[STEPS] += 1;
-  st.s[EPRET] += reward;
-  const bool done = st.s[PS] >= WIN_SCORE || st.s[CS] >= WIN_SCORE || st.s[STEPS] >= max_steps;
-  const int epret = st.s[EPRET];
-  if (done) {
-    reset_state(st, seed, (uint32_t)env, ctr, no_op_max, frameskip);
+    for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
+    uint32_t ctr = (uint32_t)__builtin_amdgcn_readfirstlane((int)counter[env]);
+    int a = __builtin_amdgcn_readfirstlane(actions[env]);
+    if (a >= n_actions || a < 0) a = 0;                    // game_state.py:38-39
+    const int up = (a == 2 || a == 4), down = (a == 3 || a == 5);
+    int reward = 0;
+    for (int f = 0; f < frameskip; ++f) reward += subframe(st, up, down, seed, (uint32_t)env, ctr);
     ctr += 1;
-  }
-  __syncthreads();    // every wave has read state[] (and tab[] is staged) before thread 0 overwrites it
-  if (threadIdx.x == 0) {
+    st.s[STEPS] += 1;
+    st.s[EPRET] += reward;
+    const bool done = st.s[PS] >= WIN_SCORE || st.s[CS] >= WIN_SCORE || st.s[STEPS] >= max_steps;
+    const int epret = st.s[EPRET];
+    if (done) {
+      reset_state(st, seed, (uint32_t)env, ctr, no_op_max, frameskip);
+      ctr += 1;
+    }
+    if (threadIdx.x == 0) {
 #pragma unroll
-    for (int i = 0; i < NSTATE; ++i) state[env * NSTATE + i] = st.s[i];
-    counter[env] = ctr;
-    reward_out[env] = (float)reward;
-    done_out[env] = done ? 1 : 0;
-    epret_out[env] = done ? (float)epret : 0.f;
-    if constexpr (RING) fc_out[env] = done ? 3 : (uint8_t)max((int)fc_in[env] - 1, 0);
+      for (int i = 0; i < NSTATE; ++i) {
+        state[env * NSTATE + i] = st.s[i];
+        phys[i] = st.s[i];
+      }
+      phys[NSTATE] = done ? 1 : 0;
+      counter[env] = ctr;
+      reward_out[env] = (float)reward;
+      done_out[env] = done ? 1 : 0;
+      epret_out[env] = done ? (float)epret : 0.f;
+      if constexpr (RING) fc_out[env] = done ? 3 : (uint8_t)max((int)fc_in[env] - 1, 0);
+    }
   }
+  PONG_STAMP(1);
+  __syncthreads();    // tab[] staged and the new state published
+  PONG_STAMP(2);
+  St st;
+#pragma unroll
+  for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(phys[i]);
+  const bool done = __builtin_amdgcn_readfirstlane(phys[NSTATE]) != 0;
   // --- fused render + gray + resize + stack push ---
   // Every source pixel outside five rectangles (the two score-digit blocks, the ball and the two
   // paddles) has its row's static colour (background or wall band), so an output pixel none of
@@ -195,15 +237,21 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   // Packed mode: one 16-byte load of the old stack + one 16-byte store of the new per quad
   // (frame-stack push (in >> 8) | f << 24); ring mode: one 4-byte store of the new frame.
   __shared__ int rowinfo[OBS_H];     // vrow | (rect mask << 8)
-  __shared__ int colmask[OBS_W];
+  __shared__ __attribute__((aligned(16))) int colmask[OBS_W];
+  __shared__ int quadmask[OBS_W / 4];    // OR of the 4 columns' masks per quad
   Scene S;
   S.cy = st.s[CY] >> 4;   // floor division by U=16 (values are non-negative)
   S.py = st.s[PY] >> 4;
   S.bx = st.s[BX] >= 0 ? st.s[BX] / U : -((-st.s[BX] + U - 1) / U);   // floor
   S.by = st.s[BY] >= 0 ? st.s[BY] / U : -((-st.s[BY] + U - 1) / U);
   S.vis = st.s[SERVE] == 0;
-  S.cs_t = st.s[CS] / 10; S.cs_o = st.s[CS] % 10;
-  S.ps_t = st.s[PS] / 10; S.ps_o = st.s[PS] % 10;
+  {
+    const int cs_t = st.s[CS] / 10, cs_o = st.s[CS] % 10, ps_t = st.s[PS] / 10, ps_o = st.s[PS] % 10;
+    S.dmask[0] = cs_t > 0 ? DIGITS[cs_t] : 0;        // tens digit only when non-zero
+    S.dmask[1] = DIGITS[cs_o];
+    S.dmask[2] = ps_t > 0 ? DIGITS[ps_t] : 0;
+    S.dmask[3] = DIGITS[ps_o];
+  }
   S.g_bg = g_bg; S.g_wall = g_wall; S.g_cpu = g_cpu; S.g_player = g_player; S.g_ball = g_ball;
   // source rectangles [r0, r1) x [c0, c1): cpu digits, player digits, ball, player, cpu
   const int by0 = S.vis ? S.by : -1000, by1 = S.vis ? S.by + BALL_H : -1000;   // matches no row when hidden
@@ -213,6 +261,15 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   const int C0[5] = {24, 104, S.bx, PLAYER_X, CPU_X};
   const int C1[5] = {40 + 3 * DIGIT_SCALE, 120 + 3 * DIGIT_SCALE, S.bx + BALL_W, PLAYER_X + PADDLE_W,
                      CPU_X + PADDLE_W};
+  __shared__ uint8_t band[BAND_R * BAND_C];
+  for (int i = threadIdx.x; i < BAND_R * BAND_C; i += 256) {
+    const int r = SCORE_ROW0 + i / BAND_C, bc = i - (i / BAND_C) * BAND_C;
+    const int c = bc < 28 ? 24 + bc : 104 + (bc - 28);
+    int g = S.g_bg;
+    if (digit_lit(S.dmask[0], r, c, 24) || digit_lit(S.dmask[1], r, c, 40)) g = S.g_cpu;
+    else if (digit_lit(S.dmask[2], r, c, 104) || digit_lit(S.dmask[3], r, c, 120)) g = S.g_player;
+    band[i] = (uint8_t)g;
+  }
   for (int i = threadIdx.x; i < OBS_H + OBS_W; i += 256) {
     if (i < OBS_H) {
       const int ys0 = tab[0 * 160 + i], ys1 = tab[1 * 160 + i], cy0 = tab[2 * 160 + i], cy1 = tab[3 * 160 + i];
@@ -232,6 +289,25 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
     }
   }
   __syncthreads();
+  if (threadIdx.x < OBS_W / 4)
+    quadmask[threadIdx.x] = colmask[4 * threadIdx.x] | colmask[4 * threadIdx.x + 1] | colmask[4 * threadIdx.x + 2] |
+                            colmask[4 * threadIdx.x + 3];
+  // score-digit output box (rows < DL_R, quads 4..9 and 19..24 = x 16..39 and 76..99: every output
+  // pixel whose taps can reach a digit), each pixel evaluated once per workgroup from the LDS band
+  // map instead of inside the (divergent) quad loop
+  __shared__ __attribute__((aligned(4))) uint8_t dlut[DL_R * 48];
+  for (int i = threadIdx.x; i < DL_R * 48; i += 256) {
+    const int yy = i / 48, lx = i - yy * 48;
+    const int x = lx < 24 ? 16 + lx : 76 + (lx - 24);
+    const int ys0 = tab[0 * 160 + yy], ys1 = tab[1 * 160 + yy], cy0 = tab[2 * 160 + yy], cy1 = tab[3 * 160 + yy];
+    const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x], cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
+    const int ra = scene_gray(S, band, ys0, xs0) * cx0 + scene_gray(S, band, ys0, xs1) * cx1;
+    const int rb = scene_gray(S, band, ys1, xs0) * cx0 + scene_gray(S, band, ys1, xs1) * cx1;
+    const int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+    dlut[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+  }
+  __syncthreads();
+  PONG_STAMP(3);
   const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OBS_H * OBS_W / 4);
   uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OBS_H * OBS_W / 4);
   uint32_t* outw = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(obs_out) + (long)env * out_stride);
@@ -242,26 +318,42 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
   if (!RING && !done) nxt = in4[min((int)threadIdx.x, NQ - 1)];
   int y = (int)threadIdx.x / QR, xq = (int)threadIdx.x - y * QR;
+  int ri_next = rowinfo[y];            // row word of the next quad, read one iteration ahead
   for (int q = threadIdx.x; q < NQ; q += 256) {
+    PONG_LOOP_STAMP((q >> 8), rowinfo[y] >> 8);
     const uint4 cur = nxt;
     if (!RING && !done && q + 256 < NQ) nxt = in4[q + 256];
-    const int ri = rowinfo[y];
+    const int ri = ri_next;
+    {
+      int yn = y + 8 + (xq + 16 >= QR ? 1 : 0);
+      ri_next = rowinfo[yn < OBS_H ? yn : OBS_H - 1];
+    }
     const uint32_t vr = (uint32_t)(ri & 0xFF);
     uint32_t f4[4] = {vr, vr, vr, vr};
     const int rm = ri >> 8;
-    if (rm) {
+    const int dq = xq >= 4 && xq < 10 ? (xq - 4) * 4 : (xq >= 19 && xq < 25 ? 24 + (xq - 19) * 4 : -1);
+    if (y < DL_R && dq >= 0) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(&dlut[y * 48 + dq]);
+      f4[0] = w & 0xFFu; f4[1] = (w >> 8) & 0xFFu; f4[2] = (w >> 16) & 0xFFu; f4[3] = w >> 24;
+    } else if (rm && (rm & quadmask[xq])) {
+      // paddle / ball rows: all 4 pixels' taps and weights in 4 vector LDS reads, branch-free
+      // scene evaluation, result kept only where the row AND column touch the same rectangle
       const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
+      const int4 xs0v = *reinterpret_cast<const int4*>(&tab[4 * 160 + xq * 4]);
+      const int4 xs1v = *reinterpret_cast<const int4*>(&tab[5 * 160 + xq * 4]);
+      const int4 cx0v = *reinterpret_cast<const int4*>(&tab[6 * 160 + xq * 4]);
+      const int4 cx1v = *reinterpret_cast<const int4*>(&tab[7 * 160 + xq * 4]);
+      const int4 cmv = *reinterpret_cast<const int4*>(&colmask[xq * 4]);
+      const int xs0a[4] = {xs0v.x, xs0v.y, xs0v.z, xs0v.w}, xs1a[4] = {xs1v.x, xs1v.y, xs1v.z, xs1v.w};
+      const int cx0a[4] = {cx0v.x, cx0v.y, cx0v.z, cx0v.w}, cx1a[4] = {cx1v.x, cx1v.y, cx1v.z, cx1v.w};
+      const int cma[4] = {cmv.x, cmv.y, cmv.z, cmv.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int x = xq * 4 + e;
-        if (rm & colmask[x]) {
-          const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x];
-          const int cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
-          const int ra = scene_gray(S, ys0, xs0) * cx0 + scene_gray(S, ys0, xs1) * cx1;
-          const int rb = scene_gray(S, ys1, xs0) * cx0 + scene_gray(S, ys1, xs1) * cx1;
-          const int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
-          f4[e] = (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
-        }
+        const int ra = scene_gray_pf(S, ys0, xs0a[e]) * cx0a[e] + scene_gray_pf(S, ys0, xs1a[e]) * cx1a[e];
+        const int rb = scene_gray_pf(S, ys1, xs0a[e]) * cx0a[e] + scene_gray_pf(S, ys1, xs1a[e]) * cx1a[e];
+        int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+        v = v < 0 ? 0 : (v > 255 ? 255 : v);
+        f4[e] = (rm & cma[e]) ? (uint32_t)v : f4[e];
       }
     }
     if constexpr (RING) {
@@ -281,6 +373,7 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
     y += 8;
     if (xq >= QR) { xq -= QR; ++y; }
   }
+  PONG_STAMP(4);
 }
 
 // ---------------------------------------------------------------------------
