@@ -152,17 +152,21 @@ __global__ __launch_bounds__(256, 3) void conv_fwd_fast(const void* __restrict__
           const int fc = (int)((fcw[i] >> (8 * ((rbase - rfirst) >> 7))) & 0xFFull);
           const long slot0 = (long)(p * E + ait[i].e) * nslots + t0 + ait[i].t;
           const long pix = (long)(oh * G::S * G::WIN + ow * G::S);
-          long cb[4];
+          // channel c's plane base with this lane's kernel row (grp) folded in; k-step kk then
+          // reads plane kk/2 at the compile-time row offset (kk&1)*4 rows -> immediate offsets
+          const uint8_t* pc[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) cb[c] = (slot0 + max(c, fc)) * (long)(G::HIN * G::WIN) + pix;
+          for (int c = 0; c < 4; ++c)
+            pc[c] = reinterpret_cast<const uint8_t*>(X) + (slot0 + max(c, fc)) * (long)(G::HIN * G::WIN) + pix +
+                    grp * G::WIN;
           rowit_adv(ait[i], 128, E, G::HOWO);
+          if (va) {
 #pragma unroll
-          for (int kk = 0; kk < NK; ++kk) {
-            const int kc = kk * 4 + grp;                 // channel kk/2, kernel row kc & 7
-            araw[i][kk] = make_uint2(0u, 0u);
-            if (va)
-              araw[i][kk] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + cb[kk >> 1] +
-                                                            (kc & 7) * G::WIN);
+            for (int kk = 0; kk < NK; ++kk)
+              araw[i][kk] = *reinterpret_cast<const uint2*>(pc[kk >> 1] + (kk & 1) * 4 * G::WIN);
+          } else {
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk) araw[i][kk] = make_uint2(0u, 0u);
           }
           continue;
         }
@@ -915,19 +919,25 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
           const int gi = tid + 256 * j;
           if (gi < NGP) {
             const bool valid = gi * 8 < Rg.navail;
+            // 4x4 byte transposes (channel-planar -> pixel-interleaved), 8 v_perm_b32 per 4 pixels
+            uint32_t px[8];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const uint32_t A = hh ? Rg.xq[j][0].y : Rg.xq[j][0].x, B = hh ? Rg.xq[j][1].y : Rg.xq[j][1].x;
+              const uint32_t C = hh ? Rg.xq[j][2].y : Rg.xq[j][2].x, D = hh ? Rg.xq[j][3].y : Rg.xq[j][3].x;
+              const uint32_t t0 = __builtin_amdgcn_perm(B, A, 0x05010400u);    // A0 B0 A1 B1
+              const uint32_t t1 = __builtin_amdgcn_perm(B, A, 0x07030602u);    // A2 B2 A3 B3
+              const uint32_t t2 = __builtin_amdgcn_perm(D, C, 0x05010400u);    // C0 D0 C1 D1
+              const uint32_t t3 = __builtin_amdgcn_perm(D, C, 0x07030602u);    // C2 D2 C3 D3
+              px[4 * hh + 0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);     // A0 B0 C0 D0
+              px[4 * hh + 1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);     // A1 B1 C1 D1
+              px[4 * hh + 2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+              px[4 * hh + 3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+            }
 #pragma unroll
             for (int pr = 0; pr < 4; ++pr) {       // pixels 2pr, 2pr+1: (pixel, channel) bytes
-              uint32_t w2[2];
-#pragma unroll
-              for (int h = 0; h < 2; ++h) {
-                const int px = 2 * pr + h, sh = 8 * (px & 3);
-                uint32_t w = 0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) w |= (((px < 4 ? Rg.xq[j][c].x : Rg.xq[j][c].y) >> sh) & 0xFFu) << (8 * c);
-                w2[h] = w;
-              }
               s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
-              if (valid) v = u8x8_to_bf16(make_uint2(w2[0], w2[1]));
+              if (valid) v = u8x8_to_bf16(make_uint2(px[2 * pr], px[2 * pr + 1]));
               *reinterpret_cast<s8v*>(&Xs[buf][gi * 32 + pr * 8]) = v;
             }
           }
