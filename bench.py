@@ -79,7 +79,8 @@ def main():
         from pathnet_gym_amd.ops import _lib
         for kv in args.kernel_opt:
             k, v = kv.split("=")
-            getattr(_lib.lib(), "fast_conv_set_" + k)(int(v))
+            lib = _lib.lib()
+            (getattr(lib, k) if hasattr(lib, k) and "_set_" in k else getattr(lib, "fast_conv_set_" + k))(int(v))
     ctx = init_distributed()
     cfg = preset(args.preset)
     cfg.paths = args.paths
