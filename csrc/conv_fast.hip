@@ -1247,17 +1247,24 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
       f4v acc[D::NT];
 #pragma unroll
       for (int nt = 0; nt < D::NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
-      for (int ks = 0; ks < KS; ++ks) {
-        const int tap = ks / ns4, a = (ks - tap * ns4) * 4 + grp;
+      // k = (tap, slot group): the tap loop is compile-time (no per-step divisions by the
+      // runtime slot count -- they made this kernel SALU-bound), the A address is formed once
+      // per tap and out-of-image taps read position 0 and are zeroed by a select
+#pragma unroll
+      for (int tap = 0; tap < D::NTAP; ++tap) {
         const int ta = tap / D::NA, tb = tap - ta * D::NA;
         const int oh = ii - ta, ow = jj - tb;
-        s8v af = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (sp < D::NSP && oh >= 0 && oh < G::HO && ow >= 0 && ow < G::WO)
-          af = *reinterpret_cast<const s8v*>(Gs + ((oh * G::WO + ow) * DG_NSMAX + a) * 8);
+        const bool ok = sp < D::NSP && oh >= 0 && oh < G::HO && ow >= 0 && ow < G::WO;
+        const bf16_t* ap = Gs + ((ok ? oh * G::WO + ow : 0) * DG_NSMAX + grp) * 8;
+        const bf16_t* bp = Bs + (tap * ns4 * D::NT * 16 + c16) * 40 + grp * 8;
+        for (int a4 = 0; a4 < ns4; ++a4) {
+          s8v af = *reinterpret_cast<const s8v*>(ap + a4 * 32);
+          if (!ok) af = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-        for (int nt = 0; nt < D::NT; ++nt) {
-          const s8v bf = *reinterpret_cast<const s8v*>(Bs + (ks * D::NT * 16 + nt * 16 + c16) * 40 + grp * 8);
-          acc[nt] = mfma16(af, bf, acc[nt]);
+          for (int nt = 0; nt < D::NT; ++nt) {
+            const s8v bf = *reinterpret_cast<const s8v*>(bp + (a4 * D::NT * 16 + nt * 16) * 40);
+            acc[nt] = mfma16(af, bf, acc[nt]);
+          }
         }
       }
       // epilogue: row (superpixel) = rt*16 + 4*grp + r, n = nt*16 + c16
