@@ -860,16 +860,30 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict
     };
     Regs R[PF];
 
+    // stages are loaded strictly in unit order (both PF modes): the (t, e, band) of the next
+    // unit is advanced incrementally instead of dividing by the runtime E at every stage
+    int it_band, it_e, it_t;
+    {
+      const int s0 = u_beg / SB::NB;
+      it_band = u_beg - s0 * SB::NB;
+      it_t = s0 / E;
+      it_e = s0 - it_t * E;
+    }
     auto load_stage = [&](Regs& Rg, int u) {
-      const int s = u / SB::NB, band = u - s * SB::NB;
-      const long sg = sample_global(p, s, E, PE, 0);
+      (void)u;
+      const int band = it_band, ut = it_t, ue = it_e;
+      const int s = ut * E + ue;
+      const long sg = (long)ut * PE + (long)p * E + ue;
+      if (++it_band == SB::NB) {
+        it_band = 0;
+        if (++it_e == E) { it_e = 0; ++it_t; }
+      }
       const int ih0 = band * OB * G::S;
       const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;   // elements inside the image
       Rg.navail = navail;
       if constexpr (RING) {
         const int fc = (int)fcs[s - s_first];
-        const int ts = s / E;
-        const long slot0 = (long)(p * E + (s - ts * E)) * nslots + ts;
+        const long slot0 = (long)(p * E + ue) * nslots + ut;
         const int npx = min(SB::SR, G::HIN - ih0) * G::WIN;        // pixels inside the image
         Rg.navail = npx;
 #pragma unroll

@@ -318,6 +318,15 @@ __global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) sum[i][j][r] = 0.f;
   const int nwords = Cout / 16;
+  // global sample rows of this lane's epilogue rows, once (not a runtime division by E per bit store)
+  long sgb[RT][4];
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long row = row0 + i * 16 + 4 * grp + r;
+      sgb[i][r] = sample_global(p, (int)(row < Rtot ? row : row0), E, PE, t0);
+    }
   for (int a = w; a < cnt; a += 4) {
     const int mod = act_idx[(p * L + layer) * M + a];
     const bf16_t* Wm = Wc + (long)mod * Cout * KP + (long)(col0 + c16) * KP + 8 * grp;
@@ -369,12 +378,9 @@ __global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
           const bool pos = v > 0.f;
           sum[i][j][r] += pos ? v : 0.f;
           const uint64_t bal = __ballot(pos);
-          const long row = row0 + i * 16 + 4 * grp + r;
-          if (c16 == 0 && row < Rtot) {
-            const long sg = sample_global(p, (int)row, E, PE, t0);
-            bits[((long)a * bits_rows + sg) * nwords + (col0 + j * 16) / 16] =
+          if (c16 == 0 && row0 + i * 16 + 4 * grp + r < Rtot)
+            bits[((long)a * bits_rows + sgb[i][r]) * nwords + (col0 + j * 16) / 16] =
                 (uint16_t)((bal >> (16 * grp)) & 0xFFFFull);
-          }
         }
       }
     }
