@@ -15,5 +15,11 @@ pass() {
 }
 pass a SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY || exit 1
 pass b SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES TCC_HIT_sum TCC_MISS_sum || exit 1
+if [ -n "$MEM" ]; then
+  pass c SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAVES FETCH_SIZE || exit 1
+  pass d WRITE_SIZE SQ_WAVES || exit 1
+  python3 scripts/pmc_summary.py --mem gpurun_out/bpmc_c.csv gpurun_out/bpmc_d.csv > gpurun_out/bpmc_mem.md
+  cat gpurun_out/bpmc_mem.md
+fi
 python3 scripts/pmc_summary.py gpurun_out/bpmc_a.csv gpurun_out/bpmc_b.csv > gpurun_out/bpmc_summary.md
 cat gpurun_out/bpmc_summary.md

@@ -8,6 +8,33 @@ import csv
 import sys
 
 
+def main_mem(paths):
+    """LDS bank conflicts, MFMA busy and HBM bytes per kernel (per dispatch averages)."""
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
+    nd = collections.defaultdict(set)
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            k = r["Kernel_Name"].split("(")[0][:60]
+            tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            nd[(k, p)].add(r.get("Dispatch_Id"))
+    order = sorted(tot, key=lambda k: -tot[k].get("SQ_WAVE_CYCLES", 0))[:14]
+    print("| kernel | dispatches | LDS bank conflicts / LDS inst | MFMA busy / wave-cycle | "
+          "HBM read MB / dispatch | HBM write MB / dispatch |")
+    print("|---|---:|---:|---:|---:|---:|")
+    for k in order:
+        d = tot[k]
+        n_c = max(len(nd[(k, paths[0])]), 1)
+        n_d = max(len(nd[(k, paths[-1])]), 1)
+        lds = d.get("SQ_INSTS_LDS", 0)
+        conf = d.get("SQ_LDS_BANK_CONFLICT", 0) / max(lds, 1)
+        mfma = d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(4 * d.get("SQ_WAVE_CYCLES", 1), 1)
+        fetch = d.get("FETCH_SIZE", 0) / n_c / 1024.0      # FETCH_SIZE / WRITE_SIZE are in KB
+        write = d.get("WRITE_SIZE", 0) / n_d / 1024.0
+        print(f"| `{k}` | {n_c} | {conf:.2f} | {mfma:.3f} | {fetch:.1f} | {write:.1f} |")
+    print("\nMFMA busy / wave-cycle = SQ_VALU_MFMA_BUSY_CYCLES / (4 x SQ_WAVE_CYCLES) (wave cycles count quad-cycles); "
+          "FETCH_SIZE / WRITE_SIZE are rocprofv3 derived TCC-EA counters (KB).")
+
+
 def main(paths):
     tot = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
@@ -39,4 +66,7 @@ def main(paths):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    if sys.argv[1] == "--mem":
+        main_mem(sys.argv[2:])
+    else:
+        main(sys.argv[1:])
