@@ -1159,6 +1159,10 @@ __global__ __launch_bounds__(256) void conv_dgrad_fast(const float* __restrict__
 // grid = (chunks, P), 256 threads; waves take 16-superpixel row tiles.
 // ===========================================================================
 #define DG_NSMAX 12          // active slots rounded up to a multiple of 4 (M <= 10)
+// LDS stride of one position's [slot][c] block: 96 elements + 8 pad = 52 dwords, so the 16 lanes of
+// an A-fragment read (consecutive positions, 16 bytes each) hit 16 distinct 4-bank groups (the
+// unpadded 48-dword stride measured 5.5 bank conflicts per LDS instruction)
+#define DG_PSTR (DG_NSMAX * 8 + 8)
 template <class G>
 struct DGM {
   static constexpr int S = G::S;
@@ -1181,7 +1185,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
                                                           float* __restrict__ dX, int samples_per_wg) {
   using D = DGM<G>;
   constexpr int S = D::S;
-  __shared__ __attribute__((aligned(16))) bf16_t Gs[G::HOWO * DG_NSMAX * 8];      // [pos][slot][c]
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[G::HOWO * DG_PSTR];           // [pos][slot][c] + pad
   __shared__ __attribute__((aligned(16))) bf16_t Bs[D::KSMAX * D::NT * 16 * 40];   // [ks][n][k (32) + 8 pad]
   __shared__ int mods[MAXM_F];
   const int p = blockIdx.y;
@@ -1247,7 +1251,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
             float m[8];
 #pragma unroll
             for (int c = 0; c < 8; ++c) m[c] = ((gbr[j][a] >> c) & 1u) ? gg[c] : 0.f;
-            *reinterpret_cast<s8v*>(Gs + (pos * DG_NSMAX + a) * 8) = f32x8_to_bf16(m);
+            *reinterpret_cast<s8v*>(Gs + pos * DG_PSTR + a * 8) = f32x8_to_bf16(m);
           }
         }
       }
@@ -1269,7 +1273,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
         const int ta = tap / D::NA, tb = tap - ta * D::NA;
         const int oh = ii - ta, ow = jj - tb;
         const bool ok = sp < D::NSP && oh >= 0 && oh < G::HO && ow >= 0 && ow < G::WO;
-        const bf16_t* ap = Gs + ((ok ? oh * G::WO + ow : 0) * DG_NSMAX + grp) * 8;
+        const bf16_t* ap = Gs + (ok ? oh * G::WO + ow : 0) * DG_PSTR + grp * 8;
         const bf16_t* bp = Bs + (tap * ns4 * D::NT * 16 + c16) * 40 + grp * 8;
         for (int a4 = 0; a4 < ns4; ++a4) {
           s8v af = *reinterpret_cast<const s8v*>(ap + a4 * 32);
