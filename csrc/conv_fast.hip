@@ -80,7 +80,7 @@ DEVI s8v ld8(const void* X, long off) {
 // (k = (c*KH + kh)*KW + kw) so each A fragment is 8 consecutive pixels of one kernel row of one
 // frame plane: still one 8-byte load.  Wc holds the weights in that k order.
 template <class G, int NT, bool RING = false>
-__global__ __launch_bounds__(256, 3) void conv_fwd_fast(const void* __restrict__ X, bf16_t* __restrict__ Y,
+__global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* __restrict__ X, bf16_t* __restrict__ Y,
                                                      uint8_t* __restrict__ bits, const bf16_t* __restrict__ Wc,
                                                      const float* __restrict__ flat, long bias_off, int chunk,
                                                      const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
