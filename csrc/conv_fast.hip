@@ -775,7 +775,7 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
 // channel planes per thread and interleaves them into the packed (pixel, channel) slab at
 // LDS-write time, so the slab layout and every MFMA operand read are unchanged.
 template <class G, int OB, int PF, bool RING = false>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_slab(const void* __restrict__ X, const float* __restrict__ Gr,
+__global__ __launch_bounds__(256, 3) void conv_wgrad_slab(const void* __restrict__ X, const float* __restrict__ Gr,
                                                           const uint8_t* __restrict__ bits, float* __restrict__ grad,
                                                           long w_off, long b_off, int chunk,
                                                           const int* __restrict__ act_idx,
