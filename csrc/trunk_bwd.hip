@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256) void fc_dgrad_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// fc dgrad, LDS-staged: grid = (ceil(T*E/64), P, KSPLIT), 512 threads (8 waves).
+// fc dgrad, LDS-staged: 1-D grid over (KSPLIT, P, ceil(T*E/64)), 512 threads (8 waves).
 // The masked bf16 gradient of up to 4 active modules for the workgroup's 64 rows
 // is built ONCE in LDS (G read once per row, ReLU bits applied per module), then
 // every 128-column chunk of dX is swept: wave w owns 16 columns x 64 rows, so each
@@ -325,19 +325,25 @@ template <int COUT>
 __global__ __launch_bounds__(512) void fc_dgrad_lds_kernel(
     const float* __restrict__ G, const uint16_t* __restrict__ bits, const bf16_t* __restrict__ WcT,
     const int* __restrict__ act_idx, const int* __restrict__ act_cnt, int layer, int L, int M, int K, int KP, int P,
-    int E, int T, long bits_rows, float g_scale, float* __restrict__ dX, int chunks_per_split) {
+    int E, int T, long bits_rows, float g_scale, float* __restrict__ dX, int chunks_per_split, int nrowb,
+    int nsplit, bf16_t* __restrict__ Gm) {
   constexpr int CS = COUT + 8;
   constexpr int NW = COUT / 16;
   __shared__ __attribute__((aligned(16))) bf16_t Gs[4 * 64 * CS];   // 132 KiB at COUT=256 (1 WG/CU)
-  const int p = blockIdx.y;
+  // XCD-aware order (workgroup b runs on XCD b % 8): split-major, so each XCD's L2 holds the
+  // weight columns of one chunk range instead of every XCD cycling through all of them
+  const int seq = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (seq >= nrowb * P * nsplit) return;
+  const int bz = seq / (nrowb * P), sr_ = seq - bz * (nrowb * P);
+  const int p = sr_ / nrowb, bx = sr_ - p * nrowb;
   const int cnt = act_cnt[p * L + layer];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
   const long R = (long)T * E;
   const int PE = P * E;
-  const long row0 = (long)blockIdx.x * 64;
+  const long row0 = (long)bx * 64;
   const int nchunks = (K + 127) / 128;
-  const int ch_beg = blockIdx.z * chunks_per_split;
+  const int ch_beg = bz * chunks_per_split;
   const int ch_end = min(nchunks, ch_beg + chunks_per_split);
   if (ch_beg >= ch_end) return;
   // epilogue rows of this lane
@@ -375,32 +381,60 @@ __global__ __launch_bounds__(512) void fc_dgrad_lds_kernel(
           float m[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) m[j] = ((bw >> j) & 1u) ? gv[j] : 0.f;
-          *reinterpret_cast<s8v*>(Gs + (a * 64 + sr) * CS + c) = f32x8_to_bf16(m);
+          const s8v mb = f32x8_to_bf16(m);
+          *reinterpret_cast<s8v*>(Gs + (a * 64 + sr) * CS + c) = mb;
+          // side output for fc_wgrad_gm_kernel: the masked bf16 gradient of slot g0+a, row sg
+          // (every K split stages the same rows: each writes its share of the column segments)
+          if (Gm != nullptr && v && (tid & 7) % nsplit == bz)
+            *reinterpret_cast<s8v*>(Gm + ((long)(g0 + a) * bits_rows + sg) * COUT + c) = mb;
         }
       }
     }
     __syncthreads();
-    for (int ch = ch_beg; ch < ch_end; ++ch) {
-      const int kcol = ch * 128 + w * 16 + c16;
-      f4v acc[4];
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) acc[rb] = {0.f, 0.f, 0.f, 0.f};
-      for (int a = 0; a < ng; ++a) {
-        const int mod = act_idx[(p * L + layer) * M + g0 + a];
-        const bf16_t* Wm = WcT + (long)mod * KP * COUT + (long)kcol * COUT + 8 * grp;
-        const bf16_t* As = Gs + (a * 64 + c16) * CS + 8 * grp;
-#pragma unroll
-        for (int cs = 0; cs < COUT; cs += 32) {
-          s8v b = {0, 0, 0, 0, 0, 0, 0, 0};
-          if (kcol < KP) b = *reinterpret_cast<const s8v*>(Wm + cs);
-#pragma unroll
-          for (int rb = 0; rb < 4; ++rb) {
-            const s8v af = *reinterpret_cast<const s8v*>(As + rb * 16 * CS + cs);
-            acc[rb] = mfma16(af, b, acc[rb]);
-          }
-        }
+    // (chunk, module) iterations flattened and software-pipelined: the 8 weight fragments of
+    // iteration it+1 are loaded into registers before the 32 MFMAs of iteration it
+    if (ng <= 0) {   // no active module in this layer: dX = 0
+      for (int ch = ch_beg; ch < ch_end; ++ch) {
+        const int kcol = ch * 128 + w * 16 + c16;
+        if (kcol < K)
+          for (int rb = 0; rb < 4; ++rb)
+            for (int r = 0; r < 4; ++r)
+              if (sg_out[rb][r] >= 0) dX[sg_out[rb][r] * K + kcol] = 0.f;
       }
-      if (kcol < K) {
+      continue;
+    }
+    const int n_it = (ch_end - ch_beg) * ng;
+    const int* aidx = act_idx + (p * L + layer) * M + g0;
+    s8v bcur[COUT / 32], bnxt[COUT / 32];
+    auto wload = [&](s8v* b, int it) {
+      const int ch = ch_beg + it / ng, a = it - (it / ng) * ng;
+      const int kc = ch * 128 + w * 16 + c16;
+      const bf16_t* Wm = WcT + (long)aidx[a] * KP * COUT + (long)kc * COUT + 8 * grp;
+#pragma unroll
+      for (int c = 0; c < COUT / 32; ++c)
+        b[c] = kc < KP ? *reinterpret_cast<const s8v*>(Wm + 32 * c) : (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+    };
+    wload(bcur, 0);
+    f4v acc[4];
+    for (int it = 0; it < n_it; ++it) {
+      const int ch = ch_beg + it / ng, a = it - (it / ng) * ng;
+      if (it + 1 < n_it) wload(bnxt, it + 1);
+      if (a == 0) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) acc[rb] = {0.f, 0.f, 0.f, 0.f};
+      }
+      const bf16_t* As = Gs + (a * 64 + c16) * CS + 8 * grp;
+#pragma unroll
+      for (int c = 0; c < COUT / 32; ++c)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const s8v af = *reinterpret_cast<const s8v*>(As + rb * 16 * CS + 32 * c);
+          acc[rb] = mfma16(af, bcur[c], acc[rb]);
+        }
+#pragma unroll
+      for (int c = 0; c < COUT / 32; ++c) bcur[c] = bnxt[c];
+      const int kcol = ch * 128 + w * 16 + c16;
+      if (a == ng - 1 && kcol < K) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
@@ -518,6 +552,131 @@ __global__ __launch_bounds__(256) void fc_wgrad_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// fc wgrad from the masked bf16 gradient Gm [slot][bits_rows][COUT] that fc_dgrad_lds_kernel
+// writes while staging (wide layers, K >= 1024).  The old kernel re-read fp32 G + ReLU bits for
+// each of its K/64 x COUT/64 tiles (3.7 GB of G traffic for fc1 per update); a 128 x COUT tile
+// reads each X row once per module user and each Gm row K/128 times at half the bytes.
+// 1-D grid: (module, split) major, then k-tile.  512 threads: wave w owns k rows
+// 32*(w>>1).. and n columns (COUT/2)*(w&1).., i.e. 2 x COUT/32 MFMA tiles; the row stages are
+// double-buffered in LDS with the next stage's global loads issued before the MFMAs.
+// The k-tile-0 workgroups also reduce the bias gradient from the same B fragments.
+// ---------------------------------------------------------------------------
+template <int COUT>
+__global__ __launch_bounds__(512) void fc_wgrad_gm_kernel(
+    const bf16_t* __restrict__ X, int ldx, const bf16_t* __restrict__ Gm, float* __restrict__ grad, long w_off,
+    long b_off, int chunk, const int* __restrict__ inv_path, const int* __restrict__ inv_slot,
+    const int* __restrict__ inv_cnt, int layer, int M, int Pmax, int K, int P, int E, int T, long bits_rows,
+    int nsplit) {
+  constexpr int XS = 128 + 8;
+  constexpr int GS = COUT + 8;
+  constexpr int NT = COUT / 32;                               // n tiles per wave
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][32 * XS];
+  __shared__ __attribute__((aligned(16))) bf16_t Gsh[2][32 * GS];
+  const int kt = (K + 127) / 128;
+  const int zt = blockIdx.x / kt, tile_k = blockIdx.x - zt * kt;
+  const int j = zt / nsplit, split = zt - j * nsplit;
+  const int n_all = inv_cnt[layer * M + j];
+  const int u_beg = (int)((long)n_all * split / nsplit), u_end = (int)((long)n_all * (split + 1) / nsplit);
+  if (u_beg >= u_end) return;
+  const int k0 = tile_k * 128;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
+  const int wk = w >> 1, wn = w & 1;
+  const int Rtot = T * E, PE = P * E;
+  const int nrb = (Rtot + 31) / 32;
+  const int n_it = (u_end - u_beg) * nrb;
+  const int* ip = inv_path + (layer * M + j) * Pmax;
+  const int* is = inv_slot + (layer * M + j) * Pmax;
+  // loader: thread -> row lr of the 32-row stage, 8 k values of X and COUT/16 n values of Gm
+  constexpr int GSEG = COUT / 16;
+  const int lr = tid >> 4, lxs = (tid & 15) * 8, lgs = (tid & 15) * GSEG;
+  const bool xin = k0 + lxs < K;
+  s8v xr, gr[GSEG / 8];
+  auto gload = [&](int it) {
+    const int ui = it / nrb;
+    const int r = (it - ui * nrb) * 32 + lr;
+    const int p = ip[u_beg + ui], a = is[u_beg + ui];
+    xr = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int h = 0; h < GSEG / 8; ++h) gr[h] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < Rtot) {
+      const long sg = sample_global(p, r, E, PE, 0);
+      if (xin) xr = *reinterpret_cast<const s8v*>(X + sg * ldx + k0 + lxs);
+      const bf16_t* gp = Gm + ((long)a * bits_rows + sg) * COUT + lgs;
+#pragma unroll
+      for (int h = 0; h < GSEG / 8; ++h) gr[h] = *reinterpret_cast<const s8v*>(gp + 8 * h);
+    }
+  };
+  f4v acc[2][NT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
+  float bsum[NT];
+#pragma unroll
+  for (int jj = 0; jj < NT; ++jj) bsum[jj] = 0.f;
+  const bool do_bias = tile_k == 0 && wk == 0;
+  gload(0);
+  for (int it = 0; it < n_it; ++it) {
+    const int buf = it & 1;
+    bf16_t* xs = Xs[buf];
+    bf16_t* gs = Gsh[buf];
+    *reinterpret_cast<s8v*>(xs + lr * XS + lxs) = xr;
+#pragma unroll
+    for (int h = 0; h < GSEG / 8; ++h) *reinterpret_cast<s8v*>(gs + lr * GS + lgs + 8 * h) = gr[h];
+    __syncthreads();
+    if (it + 1 < n_it) gload(it + 1);
+    s8v af[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const s4v v0 = lds_tr16(xs + (8 * grp + q) * XS + 32 * wk + 16 * i + 4 * pp);
+      const s4v v1 = lds_tr16(xs + (8 * grp + 4 + q) * XS + 32 * wk + 16 * i + 4 * pp);
+      af[i] = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj) {
+      const int nb = (COUT / 2) * wn + 16 * jj;
+      const s4v u0 = lds_tr16(gs + (8 * grp + q) * GS + nb + 4 * pp);
+      const s4v u1 = lds_tr16(gs + (8 * grp + 4 + q) * GS + nb + 4 * pp);
+      const s8v bf = (s8v){u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      acc[0][jj] = mfma16(af[0], bf, acc[0][jj]);
+      acc[1][jj] = mfma16(af[1], bf, acc[1][jj]);
+      if (do_bias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum[jj] += bf2f((uint16_t)bf[e]);
+      }
+    }
+  }
+  const long base = w_off + (long)j * chunk;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + 32 * wk + 16 * i + 4 * grp + r;
+        const int n = (COUT / 2) * wn + 16 * jj + i16;
+        if (k < K) {
+          if (nsplit == 1) grad[base + (long)k * COUT + n] = acc[i][jj][r];
+          else atomicAdd(&grad[base + (long)k * COUT + n], acc[i][jj][r]);
+        }
+      }
+  if (do_bias) {
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj) {
+      float v = bsum[jj];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (grp == 0) {
+        const long o = b_off + (long)j * chunk + (COUT / 2) * wn + 16 * jj + i16;
+        if (nsplit == 1) grad[o] = v;
+        else atomicAdd(&grad[o], v);
+      }
+    }
+  }
+}
+
 extern "C" {
 
 size_t conv_wgrad_smem(int KP) {
@@ -560,21 +719,33 @@ int launch_conv_dgrad(const float* G, const void* bits, const float* flat, long 
 
 int launch_fc_dgrad(const float* G, const void* bits, const void* WcT, const int* act_idx, const int* act_cnt,
                     int layer, int L, int M, int K, int KP, int Cout, int P, int E, int T, long bits_rows,
-                    float g_scale, float* dX, hipStream_t stream) {
+                    float g_scale, float* dX, void* Gm, hipStream_t stream) {
   if (M > MAXM || Cout % 32 != 0) return -1;
   if (Cout == 256) {
     const int nchunks = (K + 127) / 128;
     const int split = nchunks >= 8 ? 2 : 1;
     const int per = (nchunks + split - 1) / split;
-    dim3 grid((unsigned)(((long)T * E + 63) / 64), P, split);
-    fc_dgrad_lds_kernel<256><<<grid, 512, 0, stream>>>(G, (const uint16_t*)bits, (const bf16_t*)WcT, act_idx,
-                                                        act_cnt, layer, L, M, K, KP, P, E, T, bits_rows, g_scale, dX,
-                                                        per);
+    const int nrowb = (int)(((long)T * E + 63) / 64);
+    const int nwg = (nrowb * P * split + 7) / 8 * 8;
+    fc_dgrad_lds_kernel<256><<<nwg, 512, 0, stream>>>(G, (const uint16_t*)bits, (const bf16_t*)WcT, act_idx,
+                                                       act_cnt, layer, L, M, K, KP, P, E, T, bits_rows, g_scale, dX,
+                                                       per, nrowb, split, (bf16_t*)Gm);
     return (int)hipGetLastError();
   }
   dim3 grid((unsigned)(((long)T * E + 63) / 64), (K + 63) / 64, P);
   fc_dgrad_kernel<<<grid, 256, 0, stream>>>(G, (const uint16_t*)bits, (const bf16_t*)WcT, act_idx, act_cnt, layer, L,
                                             M, K, KP, Cout, P, E, T, bits_rows, g_scale, dX);
+  return (int)hipGetLastError();
+}
+
+int launch_fc_wgrad_gm(const void* X, int ldx, const void* Gm, float* grad, long w_off, long b_off, int chunk,
+                       const int* inv_path, const int* inv_slot, const int* inv_cnt, int layer, int M, int Pmax,
+                       int K, int Cout, int P, int E, int T, long bits_rows, int nsplit, hipStream_t stream) {
+  if (Cout != 256 || ldx % 8 != 0 || K % 8 != 0 || nsplit < 1) return -1;
+  const int kt = (K + 127) / 128;
+  fc_wgrad_gm_kernel<256><<<kt * M * nsplit, 512, 0, stream>>>((const bf16_t*)X, ldx, (const bf16_t*)Gm, grad, w_off,
+                                                               b_off, chunk, inv_path, inv_slot, inv_cnt, layer, M,
+                                                               Pmax, K, P, E, T, bits_rows, nsplit);
   return (int)hipGetLastError();
 }
 

@@ -33,7 +33,9 @@ _SIGS = {
     "launch_conv_dgrad": [P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                           c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, P, P],
     "launch_fc_dgrad": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float,
-                        P, P],
+                        P, P, P],
+    "launch_fc_wgrad_gm": [P, c_int, P, P, c_long, c_long, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_int, c_int, c_long, c_int, P],
     "launch_fc_wgrad": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_long, c_float, P],
     "launch_heads_fwd_sample": [P, c_int, P, c_long, c_long, c_long, c_long, c_int, c_int, P, P, P, c_uint, P, c_int,

@@ -24,6 +24,7 @@ forward of step t and the whole-rollout backward agree.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -66,6 +67,11 @@ class LayerGeom:
 
 class HipPathNet:
     """Kernel-side view of an ``ACPathNet`` (created by it when backend='hip')."""
+
+    # wide fc layers take their weight gradient from the masked bf16 gradient the dgrad kernel
+    # writes (fc_wgrad_gm_kernel); PATHNET_FC_WGRAD_GM=0 selects the fp32-G tile kernel (A/B)
+    fc_wgrad_gm = os.environ.get("PATHNET_FC_WGRAD_GM", "1") != "0"
+    fc_wgrad_gm_min_k = int(os.environ.get("PATHNET_FC_WGRAD_GM_MIN_K", "1024"))
 
     def __init__(self, model):
         if not torch.cuda.is_available():
@@ -272,13 +278,33 @@ class HipPathNet:
                           m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH,
                           g.KW, g.S, g.Ho, g.Wo, P, E, T, bits_rows, g_scale, dX.data_ptr(), st)
         if g.kind == "fc":
-            _lib.call("launch_fc_wgrad", X.data_ptr(), g.ldx, G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(),
-                      g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(), self.inv_slot.data_ptr(),
-                      self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T, bits_rows, g_scale, st)
+            # wide fc layers: the dgrad kernel also writes the masked bf16 gradient per active slot,
+            # and the weight gradient is a 128 x 256-tile GEMM over it (csrc/trunk_bwd.hip)
+            gm = self._gm_buffer(bits_rows) if (dX is not None and g.Cout == 256 and g.K >= self.fc_wgrad_gm_min_k
+                                                and self.fc_wgrad_gm) else None
             if dX is not None:
                 _lib.call("launch_fc_dgrad", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
                           m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.K, g.KP, g.Cout, P, E,
-                          T, bits_rows, g_scale, dX.data_ptr(), st)
+                          T, bits_rows, g_scale, dX.data_ptr(), 0 if gm is None else gm.data_ptr(), st)
+            if gm is not None:
+                tiles = ((g.K + 127) // 128) * self.M
+                nsplit = max(1, min(m.P, -(-512 // tiles)))
+                _lib.call("launch_fc_wgrad_gm", X.data_ptr(), g.ldx, gm.data_ptr(), grad_flat.data_ptr(), g.w_off,
+                          g.b_off, g.chunk, self.inv_path.data_ptr(), self.inv_slot.data_ptr(),
+                          self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T, bits_rows, nsplit, st)
+            else:
+                _lib.call("launch_fc_wgrad", X.data_ptr(), g.ldx, G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(),
+                          g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(), self.inv_slot.data_ptr(),
+                          self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T, bits_rows, g_scale, st)
+
+    def _gm_buffer(self, bits_rows: int) -> torch.Tensor:
+        """[M][bits_rows][256] bf16 scratch for the masked fc gradient (allocated before graph capture)."""
+        n = self.M * bits_rows * 256
+        buf = getattr(self, "_gm", None)
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(n, dtype=torch.bfloat16, device=self.model.store.flat.device)
+            self._gm = buf
+        return buf
 
     # -- first layer on the frame ring (frames [B][T+4][H*W] u8, fc [T+1][B] u8) --------
     def _check_ring(self, frames, fc, P, E, steps):

@@ -108,11 +108,13 @@ def _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E):
     return acts[-1].reshape(T * B, -1).float(), grad_flat
 
 
-def test_trunk_backward_matches_autograd(hip_lib):
+@pytest.mark.parametrize("wgrad_gm", [True, False], ids=["fc_wgrad_gm", "fc_wgrad_tiles"])
+def test_trunk_backward_matches_autograd(hip_lib, wgrad_gm):
     cfg = small_pixel_cfg()
     P, E, T = 4, 16, 2
     masks = random_masks(P, cfg.L, cfg.M, cfg.N, seed=5)
     m = make_model(cfg, P, masks, seed=7)
+    m.hip.fc_wgrad_gm = wgrad_gm     # fc1 (K=1408): wgrad from the dgrad's masked-bf16 side output, or not
     g = torch.Generator(device="cpu").manual_seed(1)
     obs_steps = [torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
                  for _ in range(T)]
