@@ -68,19 +68,23 @@ __global__ __launch_bounds__(256) void a2c_grad_kernel(
     const float* __restrict__ rewards, const uint8_t* __restrict__ dones, const float* __restrict__ vboot, int T,
     int B, int A, float gamma, float lam, float rclip, float beta, float vcoef, float weight,
     float* __restrict__ dlogits, float* __restrict__ dvalue, float* __restrict__ stats) {
-  const int b = blockIdx.x * 256 + threadIdx.x;
+  // one thread per (t, b): the n-step / GAE recurrence from T-1 down to t is recomputed per
+  // thread (O(T) independent loads, same arithmetic order as a serial scan, so bit-identical),
+  // which spreads the T*B softmax gradients over the whole GPU instead of B threads.
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   float spol = 0.f, sval = 0.f, sent = 0.f;
-  if (b < B) {
+  if (idx < (long)T * B) {
+    const int t = (int)(idx / B), b = (int)(idx - (long)t * B);
     float R = vboot[b];
     float gae = 0.f;
     float next_v = vboot[b];
-    for (int t = T - 1; t >= 0; --t) {
-      const long i = (long)t * B + b;
+    float adv = 0.f, v = 0.f;
+    for (int tt = T - 1; tt >= t; --tt) {
+      const long i = (long)tt * B + b;
       float r = rewards[i];
       if (rclip > 0.f) r = fminf(fmaxf(r, -rclip), rclip);
       const float nd = dones[i] ? 0.f : 1.f;
-      const float v = values[i];
-      float adv;
+      v = values[i];
       if (lam == 1.0f) {
         R = r + gamma * R * nd;
         adv = R - v;
@@ -91,6 +95,9 @@ __global__ __launch_bounds__(256) void a2c_grad_kernel(
         R = gae + v;
         next_v = v;
       }
+    }
+    const long i = idx;
+    {
       // softmax + clipped log (game_ac_network.py:38)
       float z[AMAX];
       float m = -3.0e38f;
@@ -120,8 +127,7 @@ __global__ __launch_bounds__(256) void a2c_grad_kernel(
       sval += vcoef * 0.5f * (R - v) * (R - v) * weight;
       sent += H;
       // d/dz_j [-(log pi_a * adv) - beta*H] = -adv*(1[j==a] - pi_j) + beta*pi_j*(log pi_j + H)
-      const bool live_a = true;   // clip(pi,1e-20) has zero grad below 1e-20; negligible, ignored
-      (void)live_a;
+      // (clip(pi, 1e-20) has zero gradient below 1e-20; negligible, ignored)
 #pragma unroll
       for (int j = 0; j < AMAX; ++j)
         if (j < A) {
@@ -221,7 +227,7 @@ int launch_a2c_grad(const float* logits, const float* values, const int* actions
                     float beta, float vcoef, float weight, float* dlogits, float* dvalue, float* stats,
                     hipStream_t stream) {
   if (A > AMAX) return -1;
-  a2c_grad_kernel<<<(B + 255) / 256, 256, 0, stream>>>(logits, values, actions, rewards, (const uint8_t*)dones,
+  a2c_grad_kernel<<<(unsigned)(((long)T * B + 255) / 256), 256, 0, stream>>>(logits, values, actions, rewards, (const uint8_t*)dones,
                                                         vboot, T, B, A, gamma, lam, rclip, beta, vcoef, weight,
                                                         dlogits, dvalue, stats);
   return (int)hipGetLastError();
@@ -243,23 +249,36 @@ int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float*
 // envs finishing at the same step), plus episode counters.  Thread per path.
 // counters: [0] agent steps, [1] episodes finished, [2] sum of their returns.
 // ---------------------------------------------------------------------------
-__global__ void fitness_update_kernel(const uint8_t* __restrict__ dones, const float* __restrict__ epret, int T, int P,
-                                      int E, float* __restrict__ fitness, float* __restrict__ counters,
-                                      float* __restrict__ fit_cnt, float* __restrict__ fit_sum, int window) {
+__global__ __launch_bounds__(256) void fitness_update_kernel(const uint8_t* __restrict__ dones,
+                                                             const float* __restrict__ epret, int T, int P, int E,
+                                                             float* __restrict__ fitness, float* __restrict__ counters,
+                                                             float* __restrict__ fit_cnt, float* __restrict__ fit_sum,
+                                                             int window) {
   // window == 0: fitness = return of the most recently finished episode(s) (a3c_training_thread.py:145-147);
   // window >= 1: fitness = mean return of the episodes finished since the path's last tournament,
   //              pending (-1000) until at least `window` of them have finished.
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p == 0) counters[0] = (float)T * P * E;
-  if (p >= P) return;
+  // One workgroup per path: the T x E (done, return) pairs are read in parallel into per-step
+  // LDS sums, then one thread scans the T steps (was: one thread per path, T*E serial loads).
+  extern __shared__ float ts[];                  // [T][2]: finished episodes, sum of their returns
+  const int p = blockIdx.x, tid = threadIdx.x;
+  if (p == 0 && tid == 0) counters[0] = (float)T * P * E;
+  for (int i = tid; i < 2 * T; i += blockDim.x) ts[i] = 0.f;
+  __syncthreads();
+  const long PE = (long)P * E;
+  for (int i = tid; i < T * E; i += blockDim.x) {
+    const int t = i / E, e = i - t * E;
+    const long g = t * PE + (long)p * E + e;
+    if (dones[g]) {
+      atomicAdd(&ts[2 * t], 1.f);
+      atomicAdd(&ts[2 * t + 1], epret[g]);
+    }
+  }
+  __syncthreads();
+  if (tid != 0) return;
   float fit = fitness[p];
   float nep = 0.f, sret = 0.f;
   for (int t = 0; t < T; ++t) {
-    float c = 0.f, s = 0.f;
-    for (int e = 0; e < E; ++e) {
-      const long i = (long)t * P * E + (long)p * E + e;
-      if (dones[i]) { c += 1.f; s += epret[i]; }
-    }
+    const float c = ts[2 * t], s = ts[2 * t + 1];
     if (c > 0.f) fit = s / c;
     nep += c;
     sret += s;
@@ -279,7 +298,7 @@ extern "C" int launch_fitness_update(const void* dones, const float* epret, int 
                                      float* counters, float* fit_cnt, float* fit_sum, int window,
                                      hipStream_t stream) {
   hipMemsetAsync(counters, 0, sizeof(float) * 4, stream);
-  fitness_update_kernel<<<(P + 63) / 64, 64, 0, stream>>>((const uint8_t*)dones, epret, T, P, E, fitness, counters,
-                                                          fit_cnt, fit_sum, window);
+  fitness_update_kernel<<<P, 256, sizeof(float) * 2 * T, stream>>>((const uint8_t*)dones, epret, T, P, E, fitness,
+                                                                    counters, fit_cnt, fit_sum, window);
   return (int)hipGetLastError();
 }

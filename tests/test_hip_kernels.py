@@ -911,3 +911,47 @@ def test_supervised_hip_backend_trains(hip_lib):
         sp.pop.step(acc.astype(np.float32), gen)
         accs.append(float(acc.max()))
     assert accs[-1] > 0.5
+
+
+@pytest.mark.parametrize("window", [0, 3])
+def test_fitness_update_kernel_matches_reference(hip_lib, window):
+    """Per-path fitness from the rollout's (done, episode return) pairs (a3c_training_thread.py:145-147)."""
+    from pathnet_gym_amd.ops import _lib
+    T, P, E = 7, 5, 48
+    rng = np.random.RandomState(4)
+    dones = (rng.rand(T, P, E) < 0.05).astype(np.uint8)
+    dones[:, 3, :] = 0                                   # a path with no finished episode keeps its fitness
+    epret = rng.randint(-21, 22, size=(T, P, E)).astype(np.float32)
+    fit0 = rng.randn(P).astype(np.float32)
+    cnt0 = rng.randint(0, 3, size=P).astype(np.float32)
+    sum0 = (cnt0 * 2.0).astype(np.float32)
+    # numpy reference of the per-path scan
+    fit_ref, cnt_ref, sum_ref = fit0.copy(), cnt0.copy(), sum0.copy()
+    for p in range(P):
+        nep = sret = 0.0
+        for t in range(T):
+            c = float(dones[t, p].sum())
+            s = float((epret[t, p] * dones[t, p]).sum())
+            if c > 0:
+                fit_ref[p] = s / c
+            nep += c
+            sret += s
+        if window > 0:
+            cnt_ref[p] += nep
+            sum_ref[p] += sret
+            fit_ref[p] = sum_ref[p] / cnt_ref[p] if cnt_ref[p] >= window else -1000.0
+    d = torch.from_numpy(dones).to(DEV)
+    r = torch.from_numpy(epret).to(DEV)
+    fit = torch.from_numpy(fit0).to(DEV)
+    cnt = torch.from_numpy(cnt0).to(DEV)
+    sm = torch.from_numpy(sum0).to(DEV)
+    counters = torch.full((4,), 7.0, device=DEV)
+    _lib.call("launch_fitness_update", d.data_ptr(), r.data_ptr(), T, P, E, fit.data_ptr(), counters.data_ptr(),
+              cnt.data_ptr(), sm.data_ptr(), window, _lib.stream())
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(fit.cpu().numpy(), fit_ref, rtol=1e-6)
+    c = counters.cpu().numpy()
+    assert c[0] == T * P * E and c[1] == dones.sum() and c[2] == (epret * dones).sum() and c[3] == 0
+    if window > 0:
+        np.testing.assert_allclose(cnt.cpu().numpy(), cnt_ref)
+        np.testing.assert_allclose(sm.cpu().numpy(), sum_ref)
