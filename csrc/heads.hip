@@ -153,6 +153,7 @@ __global__ __launch_bounds__(256) void a2c_grad_kernel(
 
 // grid = ceil(N / ROWS), block 256 (thread = feature f, looping f += 256)
 #define HB_ROWS 128
+template <int AM>
 __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const bf16_t* __restrict__ feat, int F, const float* __restrict__ dlogits, const float* __restrict__ dvalue,
     int N, int A, const float* __restrict__ flat, long pw, long pb, long vw, long vb, float* __restrict__ grad,
@@ -160,9 +161,9 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
   const long r0 = (long)blockIdx.x * HB_ROWS;
   const long r1 = min((long)N, r0 + HB_ROWS);
   for (int f = threadIdx.x; f < F; f += 256) {
-    float w[AMAX], gw[AMAX];
+    float w[AM], gw[AM];
 #pragma unroll
-    for (int j = 0; j < AMAX; ++j) {
+    for (int j = 0; j < AM; ++j) {
       w[j] = j < A ? flat[pw + (long)f * A + j] : 0.f;
       gw[j] = 0.f;
     }
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
       const float dv = dvalue[r];
       float d = dv * wv;
 #pragma unroll
-      for (int j = 0; j < AMAX; ++j)
+      for (int j = 0; j < AM; ++j)
         if (j < A) {
           const float dz = dlogits[r * A + j];
           d += dz * w[j];
@@ -183,25 +184,25 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
       dfeat[r * F + f] = d;
     }
 #pragma unroll
-    for (int j = 0; j < AMAX; ++j)
+    for (int j = 0; j < AM; ++j)
       if (j < A) atomicAdd(&grad[pw + (long)f * A + j], gw[j]);
     atomicAdd(&grad[vw + f], gv);
   }
   if (threadIdx.x < 64) {
     // bias grads: wave 0 reduces dz / dv over the chunk
     const int l = threadIdx.x;
-    float bz[AMAX];
+    float bz[AM];
 #pragma unroll
-    for (int j = 0; j < AMAX; ++j) bz[j] = 0.f;
+    for (int j = 0; j < AM; ++j) bz[j] = 0.f;
     float bvv = 0.f;
     for (long r = r0 + l; r < r1; r += 64) {
 #pragma unroll
-      for (int j = 0; j < AMAX; ++j)
+      for (int j = 0; j < AM; ++j)
         if (j < A) bz[j] += dlogits[r * A + j];
       bvv += dvalue[r];
     }
 #pragma unroll
-    for (int j = 0; j < AMAX; ++j)
+    for (int j = 0; j < AM; ++j)
       if (j < A) {
         const float s = wave_sum(bz[j]);
         if (l == 0) atomicAdd(&grad[pb + j], s);
@@ -237,8 +238,12 @@ int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float*
                      const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
                      hipStream_t stream) {
   if (A > AMAX) return -1;
-  heads_bwd_kernel<<<(N + HB_ROWS - 1) / HB_ROWS, 256, 0, stream>>>((const bf16_t*)feat, F, dlogits, dvalue, N, A,
-                                                                     flat, pw, pb, vw, vb, grad, dfeat);
+  if (A <= 8)
+    heads_bwd_kernel<8><<<(N + HB_ROWS - 1) / HB_ROWS, 256, 0, stream>>>((const bf16_t*)feat, F, dlogits, dvalue, N,
+                                                                        A, flat, pw, pb, vw, vb, grad, dfeat);
+  else
+    heads_bwd_kernel<AMAX><<<(N + HB_ROWS - 1) / HB_ROWS, 256, 0, stream>>>((const bf16_t*)feat, F, dlogits, dvalue,
+                                                                           N, A, flat, pw, pb, vw, vb, grad, dfeat);
   return (int)hipGetLastError();
 }
 }
@@ -246,7 +251,7 @@ int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float*
 // ---------------------------------------------------------------------------
 // fitness bookkeeping after a rollout: per path, the return of the most
 // recently finished episode(s) (a3c_training_thread.py:145-147; mean over
-// envs finishing at the same step), plus episode counters.  Thread per path.
+// envs finishing at the same step), plus episode counters.  Workgroup per path.
 // counters: [0] agent steps, [1] episodes finished, [2] sum of their returns.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void fitness_update_kernel(const uint8_t* __restrict__ dones,
