@@ -611,13 +611,13 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
 #pragma unroll
     for (int b = 0; b < NCT; ++b) acc[a][b] = {0.f, 0.f, 0.f, 0.f};
 
-  // ---- prefetch registers ----
+  // ---- prefetch registers: two sets, stages s+1 and s+2 in flight while stage s computes ----
   using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
-  XRaw xr[XIT];
-  bool xv[XIT];
-  float4 g0r, g1r;
-  uint32_t gbr = 0;
-  bool gv = false;
+  XRaw xr[2][XIT];
+  bool xv[2][XIT];
+  float4 g0r[2], g1r[2];
+  uint32_t gbr[2] = {0u, 0u};
+  bool gv[2] = {false, false};
 
   // per-item row iterators (rows advance by WG_RB per stage)
   RowIt xit[XIT];
@@ -632,56 +632,56 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
   RowIt git;
   rowit_init(git, (int)r_begin + grow, E, G::HOWO);
 
-  auto load_stage = [&]() {
+  auto load_stage = [&](const int k) {
 #pragma unroll
     for (int j = 0; j < XIT; ++j) {
-      xv[j] = xkoff[j] >= 0 && xit[j].r < r_end;
-      if (xv[j]) {
+      xv[k][j] = xkoff[j] >= 0 && xit[j].r < r_end;
+      if (xv[k][j]) {
         const int oh = xit[j].pos / G::WO, ow = xit[j].pos - oh * G::WO;
         const long xo = rowit_sample(xit[j], p, E, PE, 0) * (long)G::IN_ELEMS +
                         (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN + xkoff[j];
         if constexpr (G::U8)
-          xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xo);
+          xr[k][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xo);
         else
-          xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xo);
+          xr[k][j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xo);
       }
       rowit_adv(xit[j], WG_RB, E, G::HOWO);
     }
-    gv = gact && git.r < r_end;
-    if (gv) {
+    gv[k] = gact && git.r < r_end;
+    if (gv[k]) {
       const long go = rowit_sample(git, p, E, PE, 0) * G::HOWO + git.pos;
-      g0r = *reinterpret_cast<const float4*>(Gr + go * 8);
-      g1r = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
-      gbr = bits[(long)gslot * bits_rows + go];
+      g0r[k] = *reinterpret_cast<const float4*>(Gr + go * 8);
+      g1r[k] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+      gbr[k] = bits[(long)gslot * bits_rows + go];
     }
     rowit_adv(git, WG_RB, E, G::HOWO);
   };
-  auto write_stage = [&](int buf) {
+  auto write_stage = [&](const int buf) {   // register set k == LDS buffer buf
 #pragma unroll
     for (int j = 0; j < XIT; ++j) {
       const int it = tid + WG_NT * j;
       if (it < WG_RB * G::KC) {
         const int row = it / G::KC, kc = it - row * G::KC;
         s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (xv[j]) {
+        if (xv[buf][j]) {
           if constexpr (G::U8)
-            v = u8x8_to_bf16(xr[j]);
+            v = u8x8_to_bf16(xr[buf][j]);
           else
-            v = xr[j];
+            v = xr[buf][j];
         }
         *reinterpret_cast<s8v*>(&Xs[buf][row * XS + kc * 8]) = v;
       }
     }
     if (gact) {
       s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (gv) {
+      if (gv[buf]) {
         // ReLU-bit byte -> 8 fp32 AND masks from the LDS table (one b128 x2 read, 8 v_and)
-        const uint4 m0 = *reinterpret_cast<const uint4*>(&mtab[gbr * 8]);
-        const uint4 m1 = *reinterpret_cast<const uint4*>(&mtab[gbr * 8 + 4]);
-        float gg[8] = {__uint_as_float(__float_as_uint(g0r.x) & m0.x), __uint_as_float(__float_as_uint(g0r.y) & m0.y),
-                       __uint_as_float(__float_as_uint(g0r.z) & m0.z), __uint_as_float(__float_as_uint(g0r.w) & m0.w),
-                       __uint_as_float(__float_as_uint(g1r.x) & m1.x), __uint_as_float(__float_as_uint(g1r.y) & m1.y),
-                       __uint_as_float(__float_as_uint(g1r.z) & m1.z), __uint_as_float(__float_as_uint(g1r.w) & m1.w)};
+        const uint4 m0 = *reinterpret_cast<const uint4*>(&mtab[gbr[buf] * 8]);
+        const uint4 m1 = *reinterpret_cast<const uint4*>(&mtab[gbr[buf] * 8 + 4]);
+        float gg[8] = {__uint_as_float(__float_as_uint(g0r[buf].x) & m0.x), __uint_as_float(__float_as_uint(g0r[buf].y) & m0.y),
+                       __uint_as_float(__float_as_uint(g0r[buf].z) & m0.z), __uint_as_float(__float_as_uint(g0r[buf].w) & m0.w),
+                       __uint_as_float(__float_as_uint(g1r[buf].x) & m1.x), __uint_as_float(__float_as_uint(g1r[buf].y) & m1.y),
+                       __uint_as_float(__float_as_uint(g1r[buf].z) & m1.z), __uint_as_float(__float_as_uint(g1r[buf].w) & m1.w)};
 #pragma unroll
         for (int c = 0; c < 8; ++c) bpart[c] += gg[c];
         v = f32x8_to_bf16(gg);
@@ -690,13 +690,9 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
     }
   };
 
-  __syncthreads();
-  if (r_begin < r_end) load_stage();
-  int buf = 0;
-  for (int rb = r_begin; rb < r_end; rb += WG_RB, buf ^= 1) {
-    write_stage(buf);
-    __syncthreads();
-    if (rb + WG_RB < r_end) load_stage();
+  // Stage s uses register set and LDS buffer s & 1.  Writing buffer b at stage s is safe: every
+  // wave finished its stage s-2 MFMAs (same buffer) before the barrier of stage s-1.
+  auto compute = [&](const int buf) {
     const bf16_t* xs = Xs[buf];
     const bf16_t* gs = Gs[buf];
     s8v bfr[NCT];
@@ -720,6 +716,19 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
           if (nt < nct) acc[mi][nt] = mfma16(afr, bfr[nt], acc[mi][nt]);
       }
     }
+  };
+  auto stage = [&](const int k, const int rb) {
+    write_stage(k);
+    __syncthreads();
+    if (rb + 2 * WG_RB < r_end) load_stage(k);
+    compute(k);
+  };
+  __syncthreads();
+  if (r_begin < r_end) load_stage(0);
+  if (r_begin + WG_RB < r_end) load_stage(1);
+  for (int rb = r_begin; rb < r_end; rb += 2 * WG_RB) {
+    stage(0, rb);
+    if (rb + WG_RB < r_end) stage(1, rb + WG_RB);
   }
   const int h = i16 >> 3, ch = l & 7;
 #pragma unroll
