@@ -4,13 +4,17 @@
 (``--offload-arch=gfx950``) into ``pathnet_gym_amd/_hip/libpathnet_hip.so``.
 The library has a plain C ABI (raw device pointers + hipStream_t) and is
 loaded with ctypes after torch, so it shares torch's HIP runtime
-(libamdhip64.so.7).  Objects are rebuilt only when a source or header is
-newer than the object.
+(libamdhip64.so.7).  An object is rebuilt when the SHA-256 of its source,
+the shared headers and the compile flags differs from the stamp written next
+to it (``<obj>.sha``); the library is relinked when the combined stamp of
+its objects changes.  File mtimes are never trusted: a snapshot pushed to a
+GPU box with skewed mtimes still rebuilds exactly what changed.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -24,44 +28,69 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
-def _needs(obj, deps):
-    if not os.path.exists(obj):
-        return True
-    t = os.path.getmtime(obj)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _digest(paths, extra=()) -> str:
+    h = hashlib.sha256()
+    for x in extra:
+        h.update(str(x).encode())
+        h.update(b"\0")
+    for p in paths:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _stamp(path) -> str:
+    try:
+        with open(path + ".sha") as f:
+            return f.read().strip()
+    except OSError:
+        return ""
+
+
+def _needs(obj, digest) -> bool:
+    return not os.path.exists(obj) or _stamp(obj) != digest
 
 
 def build(verbose: bool = False, jobs: int = 0) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    headers = sorted(glob.glob(os.path.join(CSRC, "*.h")))
     objs = []
     todo = []
+    digests = []
     for s in srcs:
         o = os.path.join(OUT_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if _needs(o, [s] + headers):
-            todo.append((s, o))
+        d = _digest([s] + headers, [HIPCC] + FLAGS)
+        digests.append(d)
+        if _needs(o, d):
+            todo.append((s, o, d))
 
-    def comp(so):
-        s, o = so
+    def comp(sod):
+        s, o, d = sod
         cmd = [HIPCC] + FLAGS + ["-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {s}:\n{r.stderr}")
+        with open(o + ".sha", "w") as f:
+            f.write(d)
         return o
 
     n = jobs or min(8, max(1, (os.cpu_count() or 2)))
     n = min(n, 16)
     with cf.ThreadPoolExecutor(n) as ex:
         list(ex.map(comp, todo))
-    if todo or not os.path.exists(LIB):
+    lib_digest = hashlib.sha256("".join(digests).encode()).hexdigest()
+    if todo or _needs(LIB, lib_digest):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+        with open(LIB + ".sha", "w") as f:
+            f.write(lib_digest)
     return LIB
 
 

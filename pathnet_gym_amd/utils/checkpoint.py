@@ -58,6 +58,21 @@ def state_tensors(trainer) -> Dict[str, torch.Tensor]:
     out["train.updates"] = torch.tensor([trainer.updates], dtype=torch.int64)
     out["train.task_start_step"] = torch.tensor([trainer.task_start_step], dtype=torch.int64)
     out["train.task_gen0"] = torch.tensor([trainer._task_gen0], dtype=torch.int64)
+    # continual-learning bookkeeping: finished tasks whose per-task heads are frozen, the expressed path
+    # each finished task was solved with, and generations-to-solve per task (-1 = not solved / not run)
+    out["train.frozen_tasks"] = torch.tensor(sorted(trainer.frozen_tasks) or [-1], dtype=torch.int64)
+    K = len(trainer.cfg.tasks)
+    L, M = trainer.cfg.net.L, trainer.cfg.net.M
+    paths = np.zeros((K, L, M), np.uint8)
+    have = np.zeros(K, np.uint8)
+    for t, p in trainer.task_paths.items():
+        if 0 <= t < K:
+            paths[t] = (np.asarray(p) > 0.5).astype(np.uint8)
+            have[t] = 1
+    out["train.task_paths"] = torch.from_numpy(paths)
+    out["train.task_paths_valid"] = torch.from_numpy(have)
+    solved = [-1 if trainer.solved_generation.get(t) is None else int(trainer.solved_generation[t]) for t in range(K)]
+    out["train.solved_generation"] = torch.tensor(solved, dtype=torch.int64)
     return out
 
 
@@ -129,8 +144,17 @@ def load(trainer, path: str, strict: bool = True):
     trainer.updates = int(d["train.updates"][0])
     trainer.task_start_step = int(d["train.task_start_step"][0])
     trainer._task_gen0 = int(d["train.task_gen0"][0])
+    if "train.frozen_tasks" in d:
+        trainer.frozen_tasks = set(int(x) for x in d["train.frozen_tasks"].tolist() if int(x) >= 0)
+        valid = d["train.task_paths_valid"].numpy()
+        paths = d["train.task_paths"].numpy().astype(np.float32)
+        trainer.task_paths = {t: paths[t].copy() for t in range(len(valid)) if valid[t]}
+        trainer.solved_generation = {t: (None if int(g) < 0 else int(g))
+                                     for t, g in enumerate(d["train.solved_generation"].tolist())
+                                     if t <= task or int(g) >= 0}
     frozen = trainer.pop.frozen
     trainer.model.set_frozen(frozen)
+    trainer.opt.set_frozen(frozen, trainer.frozen_tasks)
     trainer._push_genotypes()
     rp = f"{path}.rank{trainer.ctx.rank}.safetensors"
     if os.path.exists(rp):

@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--ga-backend", default=None, choices=["host", "device"])
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--fitness-window", type=int, default=None)
+    ap.add_argument("--same-path", action="store_true",
+                    help="every path starts from the same random N-module genotype (ablation)")
+    ap.add_argument("--out", default=None, help="also write the final JSON record to this file")
     args = ap.parse_args()
 
     import torch
@@ -96,6 +99,11 @@ def main():
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
     if args.no_ga:
         tr.pop.step = lambda *a, **k: []
+    if args.same_path:
+        tr.pop.genotypes[:] = tr.pop.genotypes[0]
+        tr._push_genotypes()
+        if tr.engine is not None and tr.engine.ga_dev is not None:
+            tr.engine.ga_upload(tr.pop)
     thr = reward_threshold(cfg.tasks[0])
     curve = None
     if ctx.is_main and args.curve:
@@ -155,9 +163,13 @@ def main():
                           "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
                           "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
                           "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
-                          "ga": not args.no_ga}}
+                          "ga": not args.no_ga, "same_path": args.same_path}}
         out["config"]["seed"] = cfg.seed
         print(json.dumps(out), flush=True)
+        if args.out:
+            os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+            with open(args.out, "w") as f:
+                f.write(json.dumps(out) + "\n")
     ctx.destroy()
 
 

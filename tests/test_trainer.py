@@ -113,3 +113,35 @@ def test_windowed_mean_fitness_slows_and_averages_tournaments():
         if mode == "mean":
             assert all(s > 0 for e in tr.pop.history for s in e.scores)      # real episode means, never pending
     assert gens["mean"] < gens["last"]
+
+
+def test_checkpoint_keeps_continual_state_across_resume(tmp_path):
+    """Resume inside task 1 with per-task heads: the next end_task must keep task 0's head."""
+    cfg = small_cfg(tasks=["CartPole-v1", "CartPole-v1", "CartPole-v1"])
+    cfg.net.per_task_heads = True
+    cfg.net.num_tasks = 3
+    a = PathNetTrainer(cfg)
+    for _ in range(3):
+        a.update()
+    a.end_task()
+    a._start_task(1)
+    for _ in range(2):
+        a.update()
+    p = str(tmp_path / "ck.safetensors")
+    ckpt.save(a, p)
+    b = PathNetTrainer(cfg)
+    ckpt.load(b, p)
+    assert b.task_idx == 1 and b.frozen_tasks == {0}
+    assert set(b.task_paths) == {0} and np.array_equal(b.task_paths[0], a.task_paths[0])
+    assert b.solved_generation.get(0) == a.solved_generation.get(0)
+    lay = b.model.store.layout
+    head0 = [s for s in lay.segments if s.task == 0]
+    assert head0 and not any(bool(b.opt.seg_trainable[lay.segments.index(s)]) for s in head0)
+    before = b.model.store.flat.detach().clone()
+    b.update()
+    b.end_task()
+    after = b.model.store.flat.detach()
+    for s in head0:
+        sl = slice(s.offset, s.offset + s.numel)
+        assert torch.equal(after[sl], before[sl]), s.name          # task-0 head neither trained nor re-initialised
+    assert b.frozen_tasks == {0, 1} and set(b.task_paths) == {0, 1}
