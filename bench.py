@@ -31,18 +31,48 @@ import time
 BASELINE_STEPS_PER_SEC = 63.0     # reference steady-state global agent steps/s
 
 
-def _solve_record():
-    """Latest committed generations-to-solve measurement for Pong (profiles/solve), if present."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "solve", "pong_n10_devga_seed1.json")
-    try:
-        d = json.loads(open(path).read().strip().splitlines()[-1])
-        return {"value": d.get("generations_to_solve"), "frames": d.get("frames_to_solve"),
-                "seconds": d.get("seconds_to_solve"), "n_gpus": d.get("n_gpus"),
-                "config": "Pong PathNet M=10, N=10 initial modules, 16 paths x 16 envs, T=5, B=3, device GA",
-                "seeds_1_2_3": [2314, 2341, 2088],
-                "source": "profiles/solve/pong_n10_devga_seed*.json (scripts/solve.py)"}
-    except (OSError, ValueError, IndexError):
-        return None
+SOLVE_KEYS = ("preset", "paths_per_gpu", "envs_per_path", "t_max", "N", "B", "trunk_scale", "env_reduction", "lr",
+              "entropy_beta", "gae_lambda", "fitness", "concurrent_tournaments", "dtype")
+
+
+def solve_key(cfg, preset_name: str) -> dict:
+    """The fields of a scripts/solve.py record that must equal the bench config for its
+    generations-to-solve to be reported next to the bench's frames/s."""
+    return {"preset": preset_name, "paths_per_gpu": cfg.paths, "envs_per_path": cfg.envs_per_path,
+            "t_max": cfg.a2c.t_max, "N": cfg.net.N, "B": cfg.ga.B, "trunk_scale": cfg.net.trunk_scale,
+            "env_reduction": cfg.a2c.env_reduction, "lr": round(float(cfg.a2c.lr), 8),
+            "entropy_beta": cfg.a2c.entropy_beta, "gae_lambda": cfg.a2c.gae_lambda, "fitness": cfg.ga.fitness,
+            "concurrent_tournaments": cfg.ga.concurrent_tournaments, "dtype": cfg.compute_dtype}
+
+
+def solve_records(key: dict, n_gpus: int):
+    """Every committed solve run (profiles/solve/*.json, written by scripts/solve.py --out) whose config equals
+    ``key`` on ``n_gpus`` GPUs -- solved or not, every seed -- or None when no run of this exact config exists."""
+    import glob
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "solve")
+    runs = []
+    for f in sorted(glob.glob(os.path.join(root, "*.json"))):
+        try:
+            d = json.loads(open(f).read().strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError):
+            continue
+        c = d.get("config") or {}
+        if d.get("metric") != "generations_to_solve" or d.get("n_gpus") != n_gpus or not c.get("ga", True) \
+                or c.get("same_path"):
+            continue
+        c = dict(c, dtype=c.get("dtype", "bf16"), lr=round(float(c.get("lr", 0.0)), 8))
+        if any(c.get(k) != key[k] for k in SOLVE_KEYS):
+            continue
+        runs.append({"seed": c.get("seed"), "solved": bool(d.get("solved")),
+                     "generations": d.get("generations_to_solve"), "frames": d.get("frames_to_solve"),
+                     "seconds": d.get("seconds_to_solve"), "best_winner": d.get("best_winner_fitness"),
+                     "budget_s": d.get("seconds"), "file": os.path.relpath(f, os.path.dirname(root))})
+    if not runs:
+        return {"value": None, "note": "no scripts/solve.py run of exactly this config is committed", "config": key}
+    gens = sorted(r["generations"] for r in runs if r["solved"])
+    med = gens[len(gens) // 2] if gens and len(gens) * 2 > len(runs) else None
+    return {"value": med, "statistic": "median over seeds (null unless most seeds solved)",
+            "solved_seeds": len(gens), "seeds": len(runs), "runs": runs, "config": key}
 
 
 def main():
@@ -61,6 +91,9 @@ def main():
                     help="kernel switch NAME=VALUE (fast_conv_set_*), for A/B measurements")
     ap.add_argument("--ga-backend", default="device", choices=["device", "host"],
                     help="device: GA kernels inside the update graph + pipelined host bookkeeping")
+    ap.add_argument("--concurrent", type=int, default=None,
+                    help="concurrent tournaments (default paths/16 -- per rank count, NOT scaled by the world size, so "
+                         "the GA takes the same number of tournaments per update on 1, 2, 4 and 8 GPUs)")
     args = ap.parse_args()
 
     import numpy as np
@@ -89,7 +122,7 @@ def main():
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
     cfg.frame_ring = args.ring
-    cfg.ga.concurrent_tournaments = max(1, (cfg.paths * ctx.world) // 16)
+    cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
     cfg.ga.backend = args.ga_backend
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
 
@@ -143,7 +176,7 @@ def main():
             },
             "generations_in_timed_window": int(tr.pop.generation - gen0),
             # the metric's second half is measured by scripts/solve.py (minutes of training, not a bench window)
-            "generations_to_solve": _solve_record(),
+            "generations_to_solve": solve_records(solve_key(cfg, args.preset), ctx.world),
         }
         print(json.dumps(rec), flush=True)
     ctx.destroy()

@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from ..config import FITNESS_PENDING, PERFORMANCE_LOG_INTERVAL, TrainConfig
-from ..envs.registry import make, reward_threshold
+from ..envs.registry import is_synthetic, make, reward_threshold
 from ..models.acnet import ACPathNet
 from ..parallel.comm import FusedUpdateComm, GatherBroadcastComm
 from ..parallel.dist import DistContext
@@ -116,9 +116,9 @@ class PathNetTrainer:
     def _make_env(self, task_idx: int):
         name = self.cfg.tasks[task_idx]
         seed = self.cfg.seed * 7919 + self.ctx.rank * 104729 + task_idx * 113
-        kw = {}
-        if name.lower().startswith(("pong", "breakout", "spaceinvaders", "alien", "mspacman", "centipede")):
-            kw = dict(frameskip=self.cfg.frameskip, gray=self.cfg.gray)
+        kw = dict(gray=self.cfg.gray)
+        if is_synthetic(name):
+            kw["frameskip"] = self.cfg.frameskip
         env_backend = "hip" if self.backend == "hip" else "torch"
         return make(name, num_envs=self.P * self.E, device=self.device, seed=seed, backend=env_backend, **kw)
 

@@ -1,10 +1,21 @@
 """Environment registry (``make``), mirroring gym ids where they exist.
 
 Reference tasks are gym Atari ids (``constants.py:14``) and the gym_doom
-ids (``gym_doom/__init__.py:18-91``).  On-device implementations exist for
-CartPole and the synthetic Atari-style games; Doom ids resolve to the
-``envs/doom`` package, which needs the ViZDoom engine (not installed) for
-stepping but whose action/scoring logic is pure Python.
+ids (``gym_doom/__init__.py:18-91``).  Three kinds of env live here:
+
+* on-device envs: ``CartPole-v1`` (the classic-control dynamics, exact) and
+  the SYNTHETIC Atari-style games ``SynthPong-v0``, ``SynthBreakout-v0``,
+  ``SynthSpaceInvaders-v0``, ``SynthAlien-v0``, ``SynthMsPacman-v0``,
+  ``SynthCentipede-v0`` (short aliases ``Pong``, ``Breakout``, ... are kept for
+  the presets).  They are not ALE games and never answer to ALE ids;
+* real Gym ids (``Pong-v0``, ``PongNoFrameskip-v4``, ``Alien-v0`` ... or any
+  other id): resolved through the batched host bridge ``envs/gym_bridge.py``
+  with ``gym.make`` when gym/gymnasium is importable, and a clear error
+  otherwise (neither is installed in this image);
+* user envs: ``register_gym_env(id, entry_point)`` puts any class with the
+  classic gym API behind the same bridge.
+
+Doom ids resolve to the ``envs/doom`` package (needs the ViZDoom engine).
 """
 from __future__ import annotations
 
@@ -14,6 +25,11 @@ from .base import VecEnv
 
 _REGISTRY: Dict[str, Callable[..., VecEnv]] = {}
 _THRESHOLDS: Dict[str, float] = {}
+_SYNTH_ALIASES: Dict[str, str] = {}
+
+# real ALE ids the reference and BASELINE.json name; reward thresholds are the solve criteria used here
+REAL_ATARI_THRESHOLDS = {"Pong": 18.0, "Breakout": 30.0, "SpaceInvaders": 300.0, "Alien": 400.0,
+                         "MsPacman": 500.0, "Centipede": 3000.0}
 
 
 def register(env_id: str, factory: Callable[..., VecEnv], reward_threshold: float = float("inf")):
@@ -21,20 +37,40 @@ def register(env_id: str, factory: Callable[..., VecEnv], reward_threshold: floa
     _THRESHOLDS[env_id] = reward_threshold
 
 
+def register_gym_env(env_id: str, entry_point: Callable[[], object], reward_threshold: float = float("inf")):
+    """Register a class/callable that builds ONE env with the classic gym API (``reset``, ``step``,
+    ``action_space.n``); ``make(env_id, num_envs=N)`` then returns N of them behind ``GymVecEnv``."""
+    from .gym_bridge import gym_factory
+    register(env_id, gym_factory(entry_point, env_id), reward_threshold)
+
+
 def registered():
     return sorted(_REGISTRY)
 
 
+def is_synthetic(env_id: str) -> bool:
+    return env_id in _SYNTH_ALIASES
+
+
 def make(env_id: str, num_envs: int = 1, device="cpu", seed: int = 0, backend: str = "torch", **kw) -> VecEnv:
-    if env_id not in _REGISTRY:
-        raise KeyError(f"unknown env id {env_id!r}; registered: {registered()}")
-    env = _REGISTRY[env_id](num_envs=num_envs, device=device, seed=seed, backend=backend, **kw)
+    factory = _REGISTRY.get(env_id)
+    if factory is None:
+        if "/" in env_id:
+            raise KeyError(f"unknown env id {env_id!r}; registered: {registered()}")
+        from .gym_bridge import gym_make_factory
+        factory = gym_make_factory(env_id)          # raises a clear KeyError when gym is not importable
+    if not is_synthetic(env_id):
+        kw.pop("frameskip", None)                   # gym envs apply their own frame skip
+    env = factory(num_envs=num_envs, device=device, seed=seed, backend=backend, **kw)
     env.id = env_id
     return env
 
 
 def reward_threshold(env_id: str) -> float:
-    return _THRESHOLDS.get(env_id, float("inf"))
+    if env_id in _THRESHOLDS:
+        return _THRESHOLDS[env_id]
+    base = env_id.split("-")[0].replace("NoFrameskip", "").replace("Deterministic", "")
+    return REAL_ATARI_THRESHOLDS.get(base, float("inf"))
 
 
 def _pong(**kw):
@@ -46,6 +82,7 @@ def _cartpole(**kw):
     from .cartpole import CartPoleVec
     kw.pop("frameskip", None)
     kw.pop("gray", None)
+    kw.pop("no_op_max", None)
     return CartPoleVec(**kw)
 
 
@@ -57,9 +94,17 @@ def _atari_game(name):
 
 
 register("CartPole-v1", _cartpole, 475.0)
-for _id in ("Pong", "Pong-v0", "PongNoFrameskip-v4", "PongSynth-v0"):
-    register(_id, _pong, 18.0)
-for _g, _thr in (("Breakout", 30.0), ("SpaceInvaders", 300.0), ("Alien", 400.0), ("MsPacman", 500.0),
-                 ("Centipede", 3000.0)):
-    register(_g, _atari_game(_g), _thr)
-    register(_g + "-v0", _atari_game(_g), _thr)
+for _g, _thr in REAL_ATARI_THRESHOLDS.items():
+    _f = _pong if _g == "Pong" else _atari_game(_g)
+    for _id in ("Synth" + _g + "-v0", _g):
+        register(_id, _f, _thr)
+        _SYNTH_ALIASES[_id] = _g
+
+
+def _register_bridge_examples():
+    from .gym_bridge import PyCartPole, PyCatch
+    register_gym_env("PyCartPole-v1", PyCartPole, 475.0)
+    register_gym_env("PyCatch-v0", PyCatch, 4.0)
+
+
+_register_bridge_examples()

@@ -434,6 +434,19 @@ class HipEngine:
             self._optimizer_body()
         torch.cuda.synchronize()
 
+    @staticmethod
+    def _graph_fence():
+        """Stream-order everything after a graph replay behind the whole graph.
+
+        Measured on MI355X / ROCm 7 (scripts/diag_pipeline2.py, profiles/r2_graph_fence.md): with the host
+        running ahead (pipelined device-GA mode), back-to-back hipGraph replays and the async copies between
+        them on one stream are NOT fully ordered -- the episode counters / returns written by one update were
+        intermittently garbage (~1 update in 12 after ~1-5 k updates), while eager launches, a host sync, or
+        this event record + stream wait after each replay gave zero bad updates in 5000."""
+        ev = torch.cuda.Event()
+        ev.record()
+        torch.cuda.current_stream().wait_event(ev)
+
     def rollout_backward(self):
         if self.use_graph:
             if self.g_rollout is None:
@@ -442,6 +455,7 @@ class HipEngine:
                 self._pending_capture = True
                 return
             self.g_rollout.replay()
+            self._graph_fence()
         else:
             self._rollout_backward_body()
 
@@ -451,6 +465,7 @@ class HipEngine:
             self.lr[1:2].fill_(1.0 if skip else 0.0)
         if self.use_graph and self.g_opt is not None:
             self.g_opt.replay()
+            self._graph_fence()
         else:
             self._optimizer_body()
             if self.use_graph and getattr(self, "_pending_capture", False):

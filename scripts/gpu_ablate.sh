@@ -7,8 +7,8 @@ cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out/abl
 export TMPDIR=/tmp
 SECS=${SECS:-150}
-SHAPE=${SHAPE:---paths 16 --envs 16 --tmax 5}
-COMMON="--preset pong --N 4 --ga-backend device --seed ${SEED:-1} --report-every 30 --keep-going"
+SHAPE=${SHAPE:---paths 16 --envs 16 --tmax 5 --N 4}
+COMMON="--preset pong --ga-backend device --seed ${SEED:-1} --report-every 30 --keep-going"
 if [ $# -eq 0 ]; then
   set -- "base=" "trunk_none=--trunk-scale none" "sum=--env-reduction sum" "same_path=--same-path" "lr2e-3=--lr 2e-3"
 fi

@@ -36,7 +36,8 @@ def main():
     ap.add_argument("--entropy-beta", type=float, default=None)
     ap.add_argument("--trunk-scale", default=None, choices=["M", "none"])
     ap.add_argument("--gae-lambda", type=float, default=None)
-    ap.add_argument("--concurrent", type=int, default=None, help="concurrent tournaments (default paths*world/16)")
+    ap.add_argument("--concurrent", type=int, default=None,
+                    help="concurrent tournaments (default paths/16 per rank count, independent of the world size)")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--curve", default="gpurun_out/solve_curve.jsonl")
@@ -92,7 +93,7 @@ def main():
         cfg.ga.fitness_window = args.fitness_window
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
-    cfg.ga.concurrent_tournaments = args.concurrent or max(1, (cfg.paths * ctx.world) // 16)
+    cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
     if cfg.backend in ("hip", "auto") and ctx.device.type == "cuda":
         from pathnet_gym_amd import _build
         _build.build()
@@ -163,7 +164,7 @@ def main():
                           "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
                           "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
                           "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
-                          "ga": not args.no_ga, "same_path": args.same_path}}
+                          "ga": not args.no_ga, "same_path": args.same_path, "dtype": cfg.compute_dtype}}
         out["config"]["seed"] = cfg.seed
         print(json.dumps(out), flush=True)
         if args.out:

@@ -12,9 +12,13 @@ from pathnet_gym_amd.envs.registry import make, registered, reward_threshold
 
 def test_registry():
     ids = registered()
-    for i in ("CartPole-v1", "Pong", "Pong-v0", "Breakout", "SpaceInvaders", "Alien"):
+    for i in ("CartPole-v1", "Pong", "SynthPong-v0", "Breakout", "SynthBreakout-v0", "SpaceInvaders", "Alien",
+              "PyCartPole-v1"):
         assert i in ids
+    for real in ("Pong-v0", "PongNoFrameskip-v4", "Alien-v0", "MsPacman-v0", "Centipede-v0"):
+        assert real not in ids                     # real ALE ids are never shadowed by the synthetic games
     assert reward_threshold("CartPole-v1") == 475.0
+    assert reward_threshold("PongNoFrameskip-v4") == 18.0
 
 
 def test_cartpole_one_step_matches_equations():
