@@ -251,32 +251,33 @@ int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float*
 // ---------------------------------------------------------------------------
 // fitness bookkeeping after a rollout: per path, the return of the most
 // recently finished episode(s) (a3c_training_thread.py:145-147; mean over
-// envs finishing at the same step), plus episode counters.  Workgroup per path.
-// counters: [0] agent steps, [1] episodes finished, [2] sum of their returns.
+// envs finishing at the same step), plus episode counters.
+// counters: [0] agent steps, [1] episodes finished, [2] sum of their returns, [3] 0.
+// Deterministic and memset-free: every sum runs in a fixed order (thread t sums step t over the envs in
+// order; path partials are combined by one thread in path order), so non-integer returns (Doom) give
+// bit-identical fitness run to run, and nothing in the captured graph depends on a hipMemsetAsync node.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void fitness_update_kernel(const uint8_t* __restrict__ dones,
                                                              const float* __restrict__ epret, int T, int P, int E,
-                                                             float* __restrict__ fitness, float* __restrict__ counters,
+                                                             float* __restrict__ fitness,
                                                              float* __restrict__ fit_cnt, float* __restrict__ fit_sum,
-                                                             int window) {
+                                                             float* __restrict__ path_part, int window) {
   // window == 0: fitness = return of the most recently finished episode(s) (a3c_training_thread.py:145-147);
   // window >= 1: fitness = mean return of the episodes finished since the path's last tournament,
   //              pending (-1000) until at least `window` of them have finished.
-  // One workgroup per path: the T x E (done, return) pairs are read in parallel into per-step
-  // LDS sums, then one thread scans the T steps (was: one thread per path, T*E serial loads).
   extern __shared__ float ts[];                  // [T][2]: finished episodes, sum of their returns
   const int p = blockIdx.x, tid = threadIdx.x;
-  if (p == 0 && tid == 0) counters[0] = (float)T * P * E;
-  for (int i = tid; i < 2 * T; i += blockDim.x) ts[i] = 0.f;
-  __syncthreads();
   const long PE = (long)P * E;
-  for (int i = tid; i < T * E; i += blockDim.x) {
-    const int t = i / E, e = i - t * E;
-    const long g = t * PE + (long)p * E + e;
-    if (dones[g]) {
-      atomicAdd(&ts[2 * t], 1.f);
-      atomicAdd(&ts[2 * t + 1], epret[g]);
-    }
+  for (int t = tid; t < T; t += blockDim.x) {
+    float c = 0.f, s = 0.f;
+    const long base = t * PE + (long)p * E;
+    for (int e = 0; e < E; ++e)
+      if (dones[base + e]) {
+        c += 1.f;
+        s += epret[base + e];
+      }
+    ts[2 * t] = c;
+    ts[2 * t + 1] = s;
   }
   __syncthreads();
   if (tid != 0) return;
@@ -295,15 +296,30 @@ __global__ __launch_bounds__(256) void fitness_update_kernel(const uint8_t* __re
     fit = cnt >= (float)window ? sum / cnt : -1000.f;
   }
   fitness[p] = fit;
-  atomicAdd(&counters[1], nep);
-  atomicAdd(&counters[2], sret);
+  path_part[2 * p] = nep;
+  path_part[2 * p + 1] = sret;
+}
+
+__global__ void fitness_counters_kernel(const float* __restrict__ path_part, int T, int P, int E,
+                                        float* __restrict__ counters) {
+  if (threadIdx.x != 0) return;
+  float n = 0.f, s = 0.f;
+  for (int p = 0; p < P; ++p) {
+    n += path_part[2 * p];
+    s += path_part[2 * p + 1];
+  }
+  counters[0] = (float)T * P * E;
+  counters[1] = n;
+  counters[2] = s;
+  counters[3] = 0.f;
 }
 
 extern "C" int launch_fitness_update(const void* dones, const float* epret, int T, int P, int E, float* fitness,
-                                     float* counters, float* fit_cnt, float* fit_sum, int window,
+                                     float* counters, float* fit_cnt, float* fit_sum, int window, float* path_part,
                                      hipStream_t stream) {
-  hipMemsetAsync(counters, 0, sizeof(float) * 4, stream);
-  fitness_update_kernel<<<P, 256, sizeof(float) * 2 * T, stream>>>((const uint8_t*)dones, epret, T, P, E, fitness,
-                                                                    counters, fit_cnt, fit_sum, window);
+  if (T <= 0 || P <= 0 || E <= 0) return -1;
+  fitness_update_kernel<<<P, 64, sizeof(float) * 2 * T, stream>>>((const uint8_t*)dones, epret, T, P, E, fitness,
+                                                                   fit_cnt, fit_sum, path_part, window);
+  fitness_counters_kernel<<<1, 64, 0, stream>>>(path_part, T, P, E, counters);
   return (int)hipGetLastError();
 }

@@ -5,15 +5,21 @@
 // var -= mom.  A "variable" is a segment of the flat buffer; frozen segments
 // are skipped (no apply op in the reference, a3c_training_thread.py:190-216).
 //
-// Two launches: (1) per-segment squared norms (block partials + one atomic per
-// block), (2) fused clip + apply.  A third kernel refreshes the bf16 MFMA
-// operand copies of the trunk weights (Wc [M][Cout][KP], WcT [M][KP][Cout]).
+// Two launches, no atomics and no memset (both deterministic and safe inside a hipGraph replayed
+// back-to-back -- see profiles/r2_graph_fence.md for what a captured hipMemsetAsync did):
+//  (1) seg_sqnorm: every <= 8192-element block of a segment writes its partial sum of squares;
+//  (2) rmsprop_apply: every block first checks the partials of all TRAINABLE blocks for a non-finite
+//      value (the update is then skipped on every rank alike: the partials come from the all-reduced
+//      gradient) and records that in status[0]; then sums its segment's partials in a fixed order
+//      (identical in every block of the segment, bit-reproducible) for clip_by_norm, and applies.
+// A third kernel refreshes the bf16 MFMA operand copies of the trunk weights (Wc [M][Cout][KP],
+// WcT [M][KP][Cout]).
 #include "common.h"
 
-__global__ __launch_bounds__(256) void seg_sqnorm_kernel(const float* __restrict__ g, const int* __restrict__ blk_seg,
+__global__ __launch_bounds__(256) void seg_sqnorm_kernel(const float* __restrict__ g,
                                                          const long long* __restrict__ blk_beg,
                                                          const long long* __restrict__ blk_end,
-                                                         float* __restrict__ sq) {
+                                                         float* __restrict__ partial) {
   const int blk = blockIdx.x;
   const long b0 = blk_beg[blk], b1 = blk_end[blk];
   float s = 0.f;
@@ -25,7 +31,7 @@ __global__ __launch_bounds__(256) void seg_sqnorm_kernel(const float* __restrict
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(&sq[blk_seg[blk]], red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) partial[blk] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __global__ __launch_bounds__(256) void rmsprop_apply_kernel(float* __restrict__ w, const float* __restrict__ g,
@@ -33,18 +39,31 @@ __global__ __launch_bounds__(256) void rmsprop_apply_kernel(float* __restrict__ 
                                                             const int* __restrict__ blk_seg,
                                                             const long long* __restrict__ blk_beg,
                                                             const long long* __restrict__ blk_end,
-                                                            const float* __restrict__ sq,
+                                                            const float* __restrict__ partial,
+                                                            const int* __restrict__ seg_blk0, int nblk,
                                                             const uint8_t* __restrict__ trainable,
-                                                            const float* __restrict__ lr_ptr, float decay,
-                                                            float momentum, float eps, float clip) {
-  const int blk = blockIdx.x;
+                                                            const float* __restrict__ lr_ptr, float* __restrict__ status,
+                                                            float decay, float momentum, float eps, float clip) {
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  int bad = 0;
+  for (int i = tid; i < nblk; i += 256)
+    if (trainable[blk_seg[i]] && !isfinite(partial[i])) bad = 1;
+  bad = __syncthreads_or(bad);
+  if (blk == 0 && tid == 0 && status) status[0] = bad ? 1.f : 0.f;
   const int seg = blk_seg[blk];
-  if (!trainable[seg] || lr_ptr[1] != 0.f) return;      // lr_ptr = {lr, skip}: skip = non-finite update
+  if (bad || !trainable[seg] || lr_ptr[1] != 0.f) return;      // lr_ptr = {lr, skip}: skip = host-decided skip
+  __shared__ float segsq;
+  if (tid == 0) {
+    float s = 0.f;
+    for (int i = seg_blk0[seg]; i < seg_blk0[seg + 1]; ++i) s += partial[i];
+    segsq = s;
+  }
+  __syncthreads();
   const long b0 = blk_beg[blk], b1 = blk_end[blk];
-  const float norm = sqrtf(sq[seg]);
+  const float norm = sqrtf(segsq);
   const float scale = clip / fmaxf(norm, clip);          // tf.clip_by_norm
   const float lr = lr_ptr[0];
-  for (long i = b0 + threadIdx.x; i < b1; i += 256) {
+  for (long i = b0 + tid; i < b1; i += 256) {
     const float gi = g[i] * scale;
     const float m = decay * ms[i] + (1.f - decay) * gi * gi;
     const float mo = momentum * mom[i] + lr * gi / sqrtf(m + eps);
@@ -99,13 +118,17 @@ int launch_refresh_weights_cmajor(const float* flat, long w_off, int chunk, int 
   return (int)hipGetLastError();
 }
 
+// partial: float [nblk] scratch; seg_blk0: int [nseg + 1] first block of every segment (blocks are
+// segment-ordered); status: float [1] <- 1 if the (reduced) gradient held a non-finite value (update skipped)
 int launch_rmsprop(float* w, const float* g, float* ms, float* mom, const int* blk_seg, const long long* blk_beg,
-                   const long long* blk_end, int nblk, float* sq, int nseg, const void* trainable, const float* lr_ptr,
-                   float decay, float momentum, float eps, float clip, hipStream_t stream) {
-  hipMemsetAsync(sq, 0, sizeof(float) * nseg, stream);
-  seg_sqnorm_kernel<<<nblk, 256, 0, stream>>>(g, blk_seg, blk_beg, blk_end, sq);
-  rmsprop_apply_kernel<<<nblk, 256, 0, stream>>>(w, g, ms, mom, blk_seg, blk_beg, blk_end, sq,
-                                                 (const uint8_t*)trainable, lr_ptr, decay, momentum, eps, clip);
+                   const long long* blk_end, int nblk, float* partial, const int* seg_blk0, const void* trainable,
+                   const float* lr_ptr, float* status, float decay, float momentum, float eps, float clip,
+                   hipStream_t stream) {
+  if (nblk <= 0) return -1;
+  seg_sqnorm_kernel<<<nblk, 256, 0, stream>>>(g, blk_beg, blk_end, partial);
+  rmsprop_apply_kernel<<<nblk, 256, 0, stream>>>(w, g, ms, mom, blk_seg, blk_beg, blk_end, partial, seg_blk0, nblk,
+                                                 (const uint8_t*)trainable, lr_ptr, status, decay, momentum, eps,
+                                                 clip);
   return (int)hipGetLastError();
 }
 

@@ -142,9 +142,6 @@ class PathNetTrainer:
             self.fitness_local = self.engine.fitness
             if self.device_ga:
                 self.engine.enable_device_ga(self.pop, self.comm, self.path_offset)
-                if self.cfg.pipeline:
-                    self.engine.set_device_skip(self.comm.cnt_reduced)
-                    self.comm.force_dense = True     # the packing plan would lag the device GA by one update
         else:
             self.fitness_local = torch.full((self.P,), FITNESS_PENDING, device=self.device)
             self.fit_cnt = torch.zeros(self.P, device=self.device)
@@ -264,9 +261,9 @@ class PathNetTrainer:
                 eng.rollout_backward()
             with tr.phase("allreduce"):
                 fit_all, csum = self.comm.exchange(eng.grad_flat, eng.fitness, eng.counters)
-            skip = self.guard.check(float(csum[3]), self.updates)      # same decision on every rank
             with tr.phase("optimizer"):
-                eng.optimizer_step(lr, skip=skip)
+                eng.optimizer_step(lr)       # skips itself on a non-finite reduced gradient (same on every rank)
+            skip = self.guard.check(float(eng.opt_status.item()), self.updates)
             lp, lv, ent = [float(x) for x in eng.stats_host()[:3]]
             ent /= max(1, self.cfg.a2c.t_max * self.P * self.E)
         else:
@@ -289,9 +286,15 @@ class PathNetTrainer:
         with tr.phase("rollout_backward"):
             eng.rollout_backward()
         with tr.phase("allreduce"):
-            handle = self.comm.exchange_async(eng.grad_flat, eng.fitness, eng.counters, extra=eng.stats)
+            if self.ctx.enabled:
+                # modules the running rollout uses, from the device GA of the previous optimizer step (the GPU is
+                # busy with this rollout while the host waits for that small read-back and builds the plan)
+                union = eng.active_union()
+                if union is not None:
+                    self.comm.plan_union(union)
+            handle = self.comm.exchange_async(eng.grad_flat, eng.fitness, eng.counters, extra=eng.report_tensor())
         with tr.phase("optimizer"):
-            eng.optimizer_step(lr)              # non-finite skip decided on device from the reduced counters
+            eng.optimizer_step(lr)              # non-finite reduced gradient: skipped on device, on every rank
         self.global_step += self.cfg.a2c.t_max * self.P * self.E * self.ctx.world
         self.updates += 1
         prev, self._pending = getattr(self, "_pending", None), (handle, self.global_step)
@@ -303,7 +306,8 @@ class PathNetTrainer:
     def _collect(self, pending) -> UpdateStats:
         handle, step_at = pending
         fit_all, csum, stats = self.comm.collect(handle)
-        skip = self.guard.check(float(csum[3]), self.updates)
+        # stats[4]: whether the optimizer step BEFORE this update skipped a non-finite gradient (one-update lag)
+        skip = self.guard.check(float(stats[4]), self.updates)
         ent = float(stats[2]) / max(1, self.cfg.a2c.t_max * self.P * self.E)
         return self._finish_update(fit_all, csum, (float(stats[0]), float(stats[1]), ent), skip, step_at)
 
@@ -318,8 +322,9 @@ class PathNetTrainer:
     def _finish_update(self, fit_all, csum, losses, skip, step_at) -> UpdateStats:
         tr = self.tracer
         lp, lv, ent = losses
-        st = UpdateStats(float(lp), float(lv), float(ent), int(csum[1]),
-                         float(csum[2] / csum[1]) if csum[1] > 0 else float("nan"), steps=int(csum[0]),
+        eps = float(csum[1]) if np.isfinite(csum[1]) else 0.0
+        st = UpdateStats(float(lp), float(lv), float(ent), int(round(eps)),
+                         float(csum[2] / csum[1]) if eps >= 0.5 else float("nan"), steps=int(csum[0]),
                          skipped=skip)
         with tr.phase("ga"):
             events = self.pop.step(fit_all, step_at)
@@ -334,9 +339,11 @@ class PathNetTrainer:
                 self.solved_generation[self.task_idx] = self.pop.generation - self._task_gen0
             lo, hi = self.path_offset, self.path_offset + self.P
             if self.engine is not None and self.engine.ga_dev is not None:
-                # the device GA already mutated, compacted and reset inside the optimizer graph;
-                # the host mirror only refreshes the (multi-rank) gradient packing plan
-                self.comm.plan(self.pop.expressed(), self.pop.frozen)
+                # the device GA already mutated, compacted and reset inside the optimizer graph; without the
+                # pipeline the host mirror is current and refreshes the (multi-rank) packing plan, with it the
+                # plan comes from the device union instead (this mirror lags one update)
+                if not self.pipelined:
+                    self.comm.plan(self.pop.expressed(), self.pop.frozen)
             else:
                 self._push_genotypes()
             fl = torch.from_numpy(self.pop.fitness[lo:hi]).to(self.device)

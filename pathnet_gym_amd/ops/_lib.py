@@ -43,8 +43,8 @@ _SIGS = {
     "launch_a2c_grad": [P, P, P, P, P, P, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_float, c_float,
                         P, P, P, P],
     "launch_heads_bwd": [P, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P],
-    "launch_fitness_update": [P, P, c_int, c_int, c_int, P, P, P, P, c_int, P],
-    "launch_rmsprop": [P, P, P, P, P, P, P, c_int, P, c_int, P, P, c_float, c_float, c_float, c_float, P],
+    "launch_fitness_update": [P, P, c_int, c_int, c_int, P, P, P, P, c_int, P, P],
+    "launch_rmsprop": [P, P, P, P, P, P, P, c_int, P, P, P, P, P, c_float, c_float, c_float, c_float, P],
     "launch_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
     "launch_pong_step": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, P],
@@ -82,6 +82,8 @@ _SIGS = {
     "launch_typed_fc_fwd": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],
     "launch_typed_fc_dgrad": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],
     "launch_typed_fc_wgrad": [P, P, c_int, c_long, c_long, c_int, c_int, c_int, P, P, c_int, P, P, P],
+    "launch_active_union": [P, P, c_int, c_int, c_int, P, P],
+    "launch_pack_ranges": [P, P, P, c_int, c_long, c_int, P],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }

@@ -18,8 +18,9 @@ def _tables(opt):
     t = getattr(opt, "_hip_tables", None)
     if t is not None:
         return t
-    seg_id, beg, end = [], [], []
+    seg_id, beg, end, blk0 = [], [], [], []
     for i, s in enumerate(opt.layout.segments):
+        blk0.append(len(seg_id))
         o = s.offset
         while o < s.offset + s.numel:
             e = min(o + _BLK, s.offset + s.numel)
@@ -27,11 +28,14 @@ def _tables(opt):
             beg.append(o)
             end.append(e)
             o = e
+    blk0.append(len(seg_id))
     dev = opt.flat.device
     t = dict(seg=torch.tensor(seg_id, dtype=torch.int32, device=dev),
              beg=torch.tensor(beg, dtype=torch.int64, device=dev),
              end=torch.tensor(end, dtype=torch.int64, device=dev),
-             sq=torch.zeros(len(opt.layout.segments), dtype=torch.float32, device=dev),
+             blk0=torch.tensor(blk0, dtype=torch.int32, device=dev),
+             partial=torch.zeros(len(seg_id), dtype=torch.float32, device=dev),
+             status=torch.zeros(1, dtype=torch.float32, device=dev),
              lr=torch.zeros(2, dtype=torch.float32, device=dev))
     opt._hip_tables = t
     return t
@@ -44,5 +48,5 @@ def rmsprop_step(opt, grad: torch.Tensor, lr: float) -> None:
     trainable = opt.seg_trainable.to(torch.uint8)
     _lib.call("launch_rmsprop", opt.flat.data_ptr(), grad.data_ptr(), opt.ms.data_ptr(), opt.mom.data_ptr(),
               t["seg"].data_ptr(), t["beg"].data_ptr(), t["end"].data_ptr(), int(t["seg"].numel()),
-              t["sq"].data_ptr(), int(t["sq"].numel()), trainable.data_ptr(), t["lr"].data_ptr(), opt.decay,
-              opt.momentum, opt.epsilon, opt.clip_norm, _lib.stream())
+              t["partial"].data_ptr(), t["blk0"].data_ptr(), trainable.data_ptr(), t["lr"].data_ptr(),
+              t["status"].data_ptr(), opt.decay, opt.momentum, opt.epsilon, opt.clip_norm, _lib.stream())

@@ -10,8 +10,10 @@ update exchanges exactly one flat fp32 buffer::
   frozen, plus the always-trainable heads/LSTM (BASELINE north star:
   "A2C rollout gradients are all-reduced only over active-path
   parameters").  Modules are contiguous chunks of the flat buffer, so the
-  pack is a list of ranges; when the union covers most of the network one
-  dense range is used instead (cheaper than gather/scatter).
+  pack is a list of ranges (gathered/scattered by ``csrc/comm.hip`` on the
+  GPU); only when the union covers >= 95 % of the network is the dense
+  buffer reduced instead.  With the device GA the union comes from the GPU
+  (``HipEngine.active_union``) so the plan always matches the running rollout.
 * fitness: each rank writes its own paths' slots, the rest are 0, so the
   SUM is an all-gather (replaces PS polling C5/C6).
 * counters: agent steps / episodes (replaces the racy global_step RMW, C4).
@@ -37,18 +39,15 @@ from ..models.pathnet import ParamLayout
 from .dist import DistContext
 
 
-def active_ranges(layout: ParamLayout, expressed: np.ndarray, frozen: np.ndarray) -> List[Tuple[int, int]]:
-    """Contiguous flat-buffer ranges holding trainable gradients.
+def active_union(expressed: np.ndarray, frozen: np.ndarray) -> np.ndarray:
+    """[L, M] bool: modules some path of the WHOLE population expresses and that are not frozen."""
+    return (np.asarray(expressed) > 0.5).any(0) & ~(np.asarray(frozen) > 0.5)
 
-    expressed: [P_total, L, M] masks of the WHOLE population.
-    """
-    union = (np.asarray(expressed) > 0.5).any(0) & ~(np.asarray(frozen) > 0.5)
-    ranges = []
-    for l in range(layout.cfg.L):
-        for j in range(layout.cfg.M):
-            if union[l, j]:
-                ranges.append(layout.module_range(l, j))
-    # heads / lstm: everything after the trunk
+
+def union_ranges(layout: ParamLayout, union: np.ndarray) -> List[Tuple[int, int]]:
+    """Contiguous flat-buffer ranges holding trainable gradients for a module union (+ the heads/LSTM tail)."""
+    union = np.asarray(union).reshape(layout.cfg.L, layout.cfg.M)
+    ranges = [layout.module_range(l, j) for l in range(layout.cfg.L) for j in range(layout.cfg.M) if union[l, j]]
     ranges.append((layout.trunk_numel, layout.numel))
     merged = []
     for s, e in sorted(ranges):
@@ -59,16 +58,21 @@ def active_ranges(layout: ParamLayout, expressed: np.ndarray, frozen: np.ndarray
     return merged
 
 
+def active_ranges(layout: ParamLayout, expressed: np.ndarray, frozen: np.ndarray) -> List[Tuple[int, int]]:
+    """Contiguous flat-buffer ranges holding trainable gradients. expressed: [P_total, L, M] of the population."""
+    return union_ranges(layout, active_union(expressed, frozen))
+
+
 class FusedUpdateComm:
     NCOUNTERS = 4   # agent steps, episodes finished, sum of finished returns, spare
 
     def __init__(self, ctx: DistContext, layout: ParamLayout, P_total: int, P_local: int, device,
-                 dense_threshold: float = 0.75):
+                 dense_threshold: float = 0.95):
         self.ctx = ctx
         self.layout = layout
         self.P_total, self.P_local = P_total, P_local
         self.offset = ctx.rank * P_local
-        self.device = device
+        self.device = torch.device(device)
         self.dense_threshold = dense_threshold
         self.ranges = [(0, layout.numel)]
         self.index = None
@@ -78,25 +82,112 @@ class FusedUpdateComm:
         self.small_dev = torch.zeros(P_total + self.NCOUNTERS, dtype=torch.float32, device=device)
         self.fit_reduced = self.small_dev[:P_total]
         self.cnt_reduced = self.small_dev[P_total:]
-        pin = torch.device(device).type == "cuda"
+        pin = self.device.type == "cuda"
         self.host_small = [torch.zeros(P_total + self.NCOUNTERS, dtype=torch.float32, pin_memory=pin) for _ in range(2)]
         self._flip = 0
         self.force_dense = False
         self.bytes_last = 0
+        # GPU packing: a (src_off, len, dst_off) int64 range table per plan, staged through a pinned double
+        # buffer (a plan changes only when the population's module union does)
+        cap = layout.cfg.L * layout.cfg.M + 1
+        self._gpu_pack = pin
+        if pin:
+            self._rtab_host = [torch.zeros(cap, 3, dtype=torch.int64, pin_memory=True) for _ in range(2)]
+            self._rtab_dev = [torch.zeros(cap, 3, dtype=torch.int64, device=device) for _ in range(2)]
+            self._rtab_ev = [None, None]
+            self._rtab_flip = 0
+        self.rtab = None            # device range table of the current sparse plan (None: dense)
+        self.nranges = 0
+        self._union_key = None
+        self.plans = 0              # number of distinct plans built (diagnostics)
 
+    # -- planning ---------------------------------------------------------------
     def plan(self, expressed_all: np.ndarray, frozen: np.ndarray):
-        rng = active_ranges(self.layout, expressed_all, frozen)
+        """Host view: plan from the population's expressed masks [P_total, L, M] and the frozen mask."""
+        self.plan_union(active_union(expressed_all, frozen))
+
+    def plan_union(self, union: np.ndarray):
+        """Plan from an [L, M] module union (e.g. read back from the device GA, runtime/engine.py)."""
+        union = np.asarray(union).astype(bool).reshape(self.layout.cfg.L, self.layout.cfg.M)
+        key = (union.tobytes(), self.force_dense)
+        if key == self._union_key:
+            return
+        self._union_key = key
+        self.plans += 1
+        rng = union_ranges(self.layout, union)
         n = sum(e - s for s, e in rng)
         if self.force_dense or n >= self.dense_threshold * self.layout.numel:
             self.ranges = [(0, self.layout.numel)]
             self.index = None
+            self.rtab = None
             self.ngrad = self.layout.numel
+            return
+        self.ranges = rng
+        self.ngrad = int(n)
+        if self._gpu_pack:
+            f = self._rtab_flip
+            self._rtab_flip ^= 1
+            if self._rtab_ev[f] is not None:
+                self._rtab_ev[f].synchronize()          # the previous upload from this pinned buffer finished
+            tab = np.zeros((len(rng), 3), np.int64)
+            d = 0
+            for i, (s, e) in enumerate(rng):
+                tab[i] = (s, e - s, d)
+                d += e - s
+            self._rtab_host[f][:len(rng)].copy_(torch.from_numpy(tab))
+            self._rtab_dev[f].copy_(self._rtab_host[f], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._rtab_ev[f] = ev
+            self.rtab = self._rtab_dev[f]
+            self.nranges = len(rng)
+            self.index = None
         else:
-            self.ranges = rng
             idx = np.concatenate([np.arange(s, e, dtype=np.int64) for s, e in rng])
             self.index = torch.from_numpy(idx).to(self.device)
-            self.ngrad = int(n)
 
+    @property
+    def dense(self) -> bool:
+        return self.index is None and self.rtab is None
+
+    def _pack(self, grad: torch.Tensor, n: int):
+        if self.dense:
+            self.buf[:n].copy_(grad)
+        elif self.rtab is not None:
+            from ..ops import _lib
+            _lib.call("launch_pack_ranges", grad.data_ptr(), self.buf.data_ptr(), self.rtab.data_ptr(), self.nranges,
+                      n, 0, _lib.stream())
+        else:
+            self.buf[:n].copy_(grad.index_select(0, self.index))
+
+    def _unpack(self, grad: torch.Tensor, n: int):
+        if self.dense:
+            grad.copy_(self.buf[:n])
+        elif self.rtab is not None:
+            from ..ops import _lib
+            _lib.call("launch_pack_ranges", grad.data_ptr(), self.buf.data_ptr(), self.rtab.data_ptr(), self.nranges,
+                      n, 1, _lib.stream())
+        else:
+            grad.index_copy_(0, self.index, self.buf[:n])
+
+    def _reduce(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor) -> int:
+        """Pack [active grads | fitness (own slots) | counters], ONE all-reduce, unpack. Returns n."""
+        n = self.ngrad
+        P = self.P_total
+        buf = self.buf
+        self._pack(grad, n)
+        fit = buf[n:n + P]
+        fit.zero_()
+        fit[self.offset:self.offset + self.P_local].copy_(fitness_local)
+        buf[n + P:n + P + self.NCOUNTERS].copy_(counters)
+        view = buf[:n + P + self.NCOUNTERS]
+        self.ctx.all_reduce_(view)
+        self.bytes_last = view.numel() * 4
+        self._unpack(grad, n)
+        self.small_dev.copy_(buf[n:n + P + self.NCOUNTERS])
+        return n
+
+    # -- exchange ---------------------------------------------------------------
     def exchange_async(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor, extra=None):
         """Pipelined variant: reduce on the stream, start a non-blocking D2H of [fitness | counters] (+ ``extra``)
         into a pinned double buffer and return a handle for ``collect``; the host does not wait."""
@@ -106,24 +197,7 @@ class FusedUpdateComm:
             self.small_dev[P:].copy_(counters)
             self.bytes_last = 0
         else:
-            n = self.ngrad
-            buf = self.buf
-            if self.index is None:
-                buf[:n].copy_(grad)
-            else:
-                buf[:n].copy_(grad.index_select(0, self.index))
-            fit = buf[n:n + P]
-            fit.zero_()
-            fit[self.offset:self.offset + self.P_local].copy_(fitness_local)
-            buf[n + P:n + P + self.NCOUNTERS].copy_(counters)
-            view = buf[:n + P + self.NCOUNTERS]
-            self.ctx.all_reduce_(view)
-            self.bytes_last = view.numel() * 4
-            if self.index is None:
-                grad.copy_(buf[:n])
-            else:
-                grad.index_copy_(0, self.index, buf[:n])
-            self.small_dev.copy_(buf[n:n + P + self.NCOUNTERS])
+            self._reduce(grad, fitness_local, counters)
         hb = self.host_small[self._flip]
         ex = None
         if extra is not None:
@@ -149,9 +223,9 @@ class FusedUpdateComm:
 
     def exchange(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor):
         """All-reduce in place. Returns (fitness_all [P_total] cpu numpy, counters_sum cpu numpy)."""
+        P = self.P_total
         if not self.ctx.enabled:
             # single rank: nothing to reduce -- read back fitness + counters in ONE small D2H copy
-            P = self.P_total
             small = self.buf[:P + self.NCOUNTERS]
             small[:P].copy_(fitness_local)
             small[P:].copy_(counters)
@@ -159,26 +233,8 @@ class FusedUpdateComm:
             self.bytes_last = 0
             host = small.cpu().numpy()
             return host[:P].copy(), host[P:].copy()
-        n = self.ngrad
-        P = self.P_total
-        buf = self.buf
-        if self.index is None:
-            buf[:n].copy_(grad)
-        else:
-            buf[:n].copy_(grad.index_select(0, self.index))
-        fit = buf[n:n + P]
-        fit.zero_()
-        fit[self.offset:self.offset + self.P_local].copy_(fitness_local)
-        buf[n + P:n + P + self.NCOUNTERS].copy_(counters)
-        view = buf[:n + P + self.NCOUNTERS]
-        self.ctx.all_reduce_(view)
-        self.bytes_last = view.numel() * 4
-        if self.index is None:
-            grad.copy_(buf[:n])
-        else:
-            grad.index_copy_(0, self.index, buf[:n])
-        self.small_dev.copy_(buf[n:n + P + self.NCOUNTERS])
-        host = view[n:].cpu().numpy()
+        n = self._reduce(grad, fitness_local, counters)
+        host = self.buf[n:n + P + self.NCOUNTERS].cpu().numpy()
         return host[:P].copy(), host[P:].copy()
 
 
@@ -187,12 +243,12 @@ class GatherBroadcastComm(FusedUpdateComm):
 
     def exchange(self, grad, fitness_local, counters):
         n = self.ngrad
-        if self.index is None:
+        if self.dense:
             self.ctx.all_reduce_(grad)
         else:
-            g = grad.index_select(0, self.index)
-            self.ctx.all_reduce_(g)
-            grad.index_copy_(0, self.index, g)
+            self._pack(grad, n)
+            self.ctx.all_reduce_(self.buf[:n])
+            self._unpack(grad, n)
         fit = self.ctx.all_gather(fitness_local.float())
         self.fit_reduced.copy_(fit.reshape(-1))
         c = counters.clone()

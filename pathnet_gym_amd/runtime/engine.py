@@ -83,7 +83,7 @@ class HipEngine:
         self.epret = torch.zeros(T, B, device=dev)
         self.dlogits = torch.zeros(T, B, A, device=dev)
         self.dvalue = torch.zeros(T, B, device=dev)
-        self.stats = torch.zeros(4, device=dev)
+        self.stats = torch.zeros(4, device=dev)          # a2c_grad: loss_pi, loss_v, entropy sum
         self.grad_flat = torch.zeros_like(model.store.flat, requires_grad=False)
         self.fitness = torch.full((P,), -1000.0, device=dev)
         # windowed fitness (GAConfig.fitness == "mean"): episodes / return sum since the path's last tournament
@@ -91,6 +91,7 @@ class HipEngine:
         self.fit_cnt = torch.zeros(P, device=dev)
         self.fit_sum = torch.zeros(P, device=dev)
         self.counters = torch.zeros(4, device=dev)
+        self.path_part = torch.zeros(P, 2, device=dev)     # per-path (episodes, return sum) of the last rollout
         self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.zeros(2, dtype=torch.float32, device=dev)      # {lr, skip}
         self.weight = (1.0 / E) if a2c.env_reduction == "mean_env" else 1.0
@@ -99,7 +100,6 @@ class HipEngine:
         self.g_rollout = None
         self.g_opt = None
         self.ga_dev = None
-        self.skip_src = None      # device tensor: counters with the all-reduced non-finite count at [3]
         # LSTM nets: fused HIP LSTM cell (csrc/lstm.hip) when the widths are multiples of 64; otherwise
         # the hybrid path (HIP trunk + autograd LSTM/heads/loss, dL/dfeat fed back to the HIP trunk backward)
         self.lstm_hip = hp.lstm is not None
@@ -160,9 +160,10 @@ class HipEngine:
 
     def _build_opt_tables(self):
         segs = self.model.store.layout.segments
-        seg_id, beg, end = [], [], []
+        seg_id, beg, end, blk0 = [], [], [], []
         BLK = 8192
         for i, s in enumerate(segs):
+            blk0.append(len(seg_id))
             o = s.offset
             while o < s.offset + s.numel:
                 e = min(o + BLK, s.offset + s.numel)
@@ -170,12 +171,18 @@ class HipEngine:
                 beg.append(o)
                 end.append(e)
                 o = e
+        blk0.append(len(seg_id))
         dev = self.device
         self.blk_seg = torch.tensor(seg_id, dtype=torch.int32, device=dev)
         self.blk_beg = torch.tensor(beg, dtype=torch.int64, device=dev)
         self.blk_end = torch.tensor(end, dtype=torch.int64, device=dev)
+        self.seg_blk0 = torch.tensor(blk0, dtype=torch.int32, device=dev)
         self.nblk = len(seg_id)
-        self.sq = torch.zeros(len(segs), dtype=torch.float32, device=dev)
+        self.partial = torch.zeros(self.nblk, dtype=torch.float32, device=dev)
+        # 1.0 when the last optimizer step found a non-finite (all-reduced) gradient and skipped itself
+        self.opt_status = torch.zeros(1, dtype=torch.float32, device=dev)
+        # [loss_pi, loss_v, entropy, spare, previous optimizer step skipped] read back per update (pipelined mode)
+        self.report = torch.zeros(5, dtype=torch.float32, device=dev)
         self.trainable_u8 = self.opt.seg_trainable.to(torch.uint8)
 
     def refresh_trainable(self):
@@ -279,7 +286,6 @@ class HipEngine:
         self.grad_flat[tn:] += st.flat.grad[tn:]
         st.flat.grad = None
         self._fitness_update()
-        self._count_nonfinite()
         self.lstm_state = (h.detach(), c.detach())
 
     def _rollout_backward_body(self):
@@ -307,12 +313,11 @@ class HipEngine:
             hp.heads_bwd(feat, self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1), self.grad_flat,
                          self.grads[L - 1], task=self.model.task)
         self._layer_bwd_all(T)
-        self._count_nonfinite()
 
     def _fitness_update(self):
         _lib.call("launch_fitness_update", self.dones.data_ptr(), self.epret.data_ptr(), self.T, self.P, self.E,
                   self.fitness.data_ptr(), self.counters.data_ptr(), self.fit_cnt.data_ptr(), self.fit_sum.data_ptr(),
-                  self.fit_window, _lib.stream())
+                  self.fit_window, self.path_part.data_ptr(), _lib.stream())
 
     def reset_fitness(self, fitness_local: torch.Tensor):
         """Install the GA's view of the local fitness; paths reset to pending restart their episode window."""
@@ -330,7 +335,12 @@ class HipEngine:
             slots=torch.full((pop.concurrent, pop.B), -1, dtype=torch.int32, device=dev),
             gen=torch.zeros(1, dtype=torch.int64, device=dev),
             events=torch.zeros(pop.concurrent, 3, dtype=torch.int32, device=dev),
-            fit=comm.fit_reduced, p_off=p_off, pop=pop)
+            fit=comm.fit_reduced, p_off=p_off, pop=pop,
+            # union of the modules the whole population expresses next, minus frozen ones (csrc/comm.hip):
+            # read back after every optimizer step to plan the active-path gradient all-reduce
+            union=torch.zeros(pop.L * pop.M, dtype=torch.uint8, device=dev),
+            union_host=torch.zeros(pop.L * pop.M, dtype=torch.uint8, pin_memory=True))
+        self._union_ev = None
         self.ga_upload(pop)
 
     def ga_upload(self, pop):
@@ -341,6 +351,7 @@ class HipEngine:
         g["slots"].copy_(torch.from_numpy(pop.slots.astype(np.int32)))
         g["gen"].fill_(int(pop.generation))
         g["fit"].copy_(torch.from_numpy(pop.fitness.astype(np.float32)))
+        self._union_ev = None          # the last read-back union described the old genotypes
 
     def _ga_body(self):
         g = self.ga_dev
@@ -354,15 +365,37 @@ class HipEngine:
         _lib.call("launch_ga_compact", g["geno"].data_ptr(), g["frozen"].data_ptr(), g["p_off"], self.P, pop.L,
                   pop.M, m.mask.data_ptr(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), hp.inv_path.data_ptr(),
                   hp.inv_slot.data_ptr(), hp.inv_cnt.data_ptr(), st)
+        _lib.call("launch_active_union", g["geno"].data_ptr(), g["frozen"].data_ptr(), pop.P, pop.L, pop.M,
+                  g["union"].data_ptr(), st)
         # local fitness <- the GA's view; paths reset to pending restart their episode window
         self.fitness.copy_(g["fit"][g["p_off"]:g["p_off"] + self.P])
         pend = self.fitness <= -1000.0
         self.fit_cnt.masked_fill_(pend, 0.0)
         self.fit_sum.masked_fill_(pend, 0.0)
 
-    def _count_nonfinite(self):
-        # spare counter slot: non-finite gradient entries, all-reduced with the update (runtime/guard.py)
-        self.counters[3:4].copy_((~torch.isfinite(self.grad_flat)).sum(dtype=torch.float32).reshape(1))
+    def _read_union(self):
+        """After an optimizer step: start the D2H of the device GA's next module union (outside any graph)."""
+        if self.ga_dev is None:
+            return
+        self.ga_dev["union_host"].copy_(self.ga_dev["union"], non_blocking=True)
+        self._union_ev = torch.cuda.Event()
+        self._union_ev.record()
+
+    def active_union(self):
+        """[L, M] bool union of the modules the population expresses in the rollout now running (minus frozen),
+        as computed on device by the last optimizer step; None before the first one."""
+        if self.ga_dev is None or self._union_ev is None:
+            return None
+        self._union_ev.synchronize()
+        pop = self.ga_dev["pop"]
+        return self.ga_dev["union_host"].numpy().reshape(pop.L, pop.M).astype(bool)
+
+    def report_tensor(self) -> torch.Tensor:
+        """Assemble [loss_pi, loss_v, entropy, 0, last optimizer step skipped] for the async read-back
+        (enqueued after the rollout: the skip flag is the PREVIOUS optimizer step's)."""
+        self.report[:4].copy_(self.stats)
+        self.report[4:5].copy_(self.opt_status)
+        return self.report
 
     def _lstm_backward(self):
         """Heads backward into dL/dh, reverse scan through the fused LSTM cell, then its weight gradient."""
@@ -394,21 +427,18 @@ class HipEngine:
         elif self.hybrid:
             self.lstm_state = (h.clone(), c.clone())
 
-    def set_device_skip(self, counters_reduced: torch.Tensor):
-        """Pipelined mode: the optimizer skips a non-finite update by itself (no host round trip)."""
-        self.skip_src = counters_reduced
-
     def _optimizer_body(self):
-        if self.skip_src is not None:
-            self.lr[1:2].copy_((self.skip_src[3:4] > 0).to(torch.float32))
         if self.lstm_hip:
             T = self.T
             self.hip.lstm_carry(self.hst[T], self.cst[T], self.dones[T - 1], self.hst[0], self.cst[0])
         o = self.opt
+        # non-finite (all-reduced) gradients: the kernel skips the step by itself, identically on every rank,
+        # and records it in opt_status (runtime/guard.py counts consecutive skips on the host)
         _lib.call("launch_rmsprop", self.model.store.flat.data_ptr(), self.grad_flat.data_ptr(), o.ms.data_ptr(),
                   o.mom.data_ptr(), self.blk_seg.data_ptr(), self.blk_beg.data_ptr(), self.blk_end.data_ptr(),
-                  self.nblk, self.sq.data_ptr(), self.sq.numel(), self.trainable_u8.data_ptr(), self.lr.data_ptr(),
-                  o.decay, o.momentum, o.epsilon, o.clip_norm, _lib.stream())
+                  self.nblk, self.partial.data_ptr(), self.seg_blk0.data_ptr(), self.trainable_u8.data_ptr(),
+                  self.lr.data_ptr(), self.opt_status.data_ptr(), o.decay, o.momentum, o.epsilon, o.clip_norm,
+                  _lib.stream())
         self.hip.refresh_weights()
         if self.ga_dev is not None:
             self._ga_body()
@@ -434,19 +464,6 @@ class HipEngine:
             self._optimizer_body()
         torch.cuda.synchronize()
 
-    @staticmethod
-    def _graph_fence():
-        """Stream-order everything after a graph replay behind the whole graph.
-
-        Measured on MI355X / ROCm 7 (scripts/diag_pipeline2.py, profiles/r2_graph_fence.md): with the host
-        running ahead (pipelined device-GA mode), back-to-back hipGraph replays and the async copies between
-        them on one stream are NOT fully ordered -- the episode counters / returns written by one update were
-        intermittently garbage (~1 update in 12 after ~1-5 k updates), while eager launches, a host sync, or
-        this event record + stream wait after each replay gave zero bad updates in 5000."""
-        ev = torch.cuda.Event()
-        ev.record()
-        torch.cuda.current_stream().wait_event(ev)
-
     def rollout_backward(self):
         if self.use_graph:
             if self.g_rollout is None:
@@ -455,22 +472,21 @@ class HipEngine:
                 self._pending_capture = True
                 return
             self.g_rollout.replay()
-            self._graph_fence()
         else:
             self._rollout_backward_body()
 
     def optimizer_step(self, lr: float, skip: bool = False):
+        """``skip``: host-decided skip (tests); non-finite gradients are skipped by the kernel itself."""
         self.lr[0:1].fill_(lr)
-        if self.skip_src is None:
-            self.lr[1:2].fill_(1.0 if skip else 0.0)
+        self.lr[1:2].fill_(1.0 if skip else 0.0)
         if self.use_graph and self.g_opt is not None:
             self.g_opt.replay()
-            self._graph_fence()
         else:
             self._optimizer_body()
             if self.use_graph and getattr(self, "_pending_capture", False):
                 self._pending_capture = False
                 self._capture()
+        self._read_union()
 
     def stats_host(self):
         return self.stats.cpu().numpy()

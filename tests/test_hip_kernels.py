@@ -254,11 +254,29 @@ def test_rmsprop_kernel_matches_torch(hip_lib):
     torch.cuda.synchronize()
     assert torch.equal(tr.model.store.flat.detach(), flat0) and torch.equal(tr.opt.ms, ms0)
     eng.lr[1:2].zero_()
+    # a non-finite entry in a trainable segment: the kernel skips the whole step by itself and flags it
+    gbad = g.clone()
+    gbad[5] = float("nan")
+    eng.grad_flat.copy_(gbad)
     eng._optimizer_body()
     torch.cuda.synchronize()
+    assert torch.equal(tr.model.store.flat.detach(), flat0) and float(eng.opt_status) == 1.0
+    eng.grad_flat.copy_(g)
+    ms_before = tr.opt.ms.clone()
+    eng._optimizer_body()
+    torch.cuda.synchronize()
+    assert float(eng.opt_status) == 0.0
     assert rel(tr.model.store.flat.detach() - flat0, ref.flat - flat0) < 1e-4
     s = tr.model.store.layout.by_name["layer0.module3.weight"]
     assert torch.equal(tr.model.store.flat[s.offset:s.offset + s.numel], flat0[s.offset:s.offset + s.numel])
+    # deterministic: the same step from the same state is bit-identical (no atomics in the norm reduction)
+    w1, m1 = tr.model.store.flat.detach().clone(), tr.opt.ms.clone()
+    with torch.no_grad():
+        tr.model.store.flat.copy_(flat0)
+    tr.opt.ms.copy_(ms_before)
+    eng._optimizer_body()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.model.store.flat.detach(), w1) and torch.equal(tr.opt.ms, m1)
 
 
 def test_pong_env_hip_bit_exact_vs_torch(hip_lib):
@@ -946,12 +964,26 @@ def test_fitness_update_kernel_matches_reference(hip_lib, window):
     cnt = torch.from_numpy(cnt0).to(DEV)
     sm = torch.from_numpy(sum0).to(DEV)
     counters = torch.full((4,), 7.0, device=DEV)
+    part = torch.full((P, 2), 5.0, device=DEV)
     _lib.call("launch_fitness_update", d.data_ptr(), r.data_ptr(), T, P, E, fit.data_ptr(), counters.data_ptr(),
-              cnt.data_ptr(), sm.data_ptr(), window, _lib.stream())
+              cnt.data_ptr(), sm.data_ptr(), window, part.data_ptr(), _lib.stream())
     torch.cuda.synchronize()
     np.testing.assert_allclose(fit.cpu().numpy(), fit_ref, rtol=1e-6)
     c = counters.cpu().numpy()
     assert c[0] == T * P * E and c[1] == dones.sum() and c[2] == (epret * dones).sum() and c[3] == 0
+    # non-integer returns (Doom): the fixed-order sums make fitness bit-identical run to run
+    rf = torch.from_numpy(epret * 0.37 + 0.011).to(DEV)
+    outs = []
+    for _ in range(3):
+        f2 = torch.from_numpy(fit0).to(DEV)
+        c2 = torch.zeros(4, device=DEV)
+        _lib.call("launch_fitness_update", d.data_ptr(), rf.data_ptr(), T, P, E, f2.data_ptr(), c2.data_ptr(),
+                  torch.from_numpy(cnt0).to(DEV).data_ptr(), torch.from_numpy(sum0).to(DEV).data_ptr(), 0,
+                  part.data_ptr(), _lib.stream())
+        torch.cuda.synchronize()
+        outs.append((f2.cpu().numpy().copy(), c2.cpu().numpy().copy()))
+    for f2, c2 in outs[1:]:
+        assert np.array_equal(f2, outs[0][0]) and np.array_equal(c2, outs[0][1])
     if window > 0:
         np.testing.assert_allclose(cnt.cpu().numpy(), cnt_ref)
         np.testing.assert_allclose(sm.cpu().numpy(), sum_ref)

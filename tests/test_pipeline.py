@@ -1,6 +1,6 @@
 """Pipelined device-GA mode on the GPU: host runs ahead of two hipGraph replays per update.
 
-Regression for the replay-ordering race recorded in profiles/r2_graph_fence.md: the episode counters
+Regression for the captured-memset race recorded in profiles/r2_graph_memset_race.md: the episode counters
 written by the rollout graph must stay plausible for thousands of un-synchronised updates.
 """
 import numpy as np
