@@ -59,7 +59,10 @@ class DoomEnv:
         self.vzd = _engine()
         self.level = level
         self.previous_level = -1
-        self.assets_dir = assets_dir or os.environ.get("PATHNET_DOOM_ASSETS", "")
+        if not assets_dir:
+            from .scenarios import assets_dir as _default_assets
+            assets_dir = _default_assets()      # PATHNET_DOOM_ASSETS, or the nine generated scenario configs
+        self.assets_dir = assets_dir
         self.lock = DoomLock().get_lock()
         self.action_space = MultiDiscrete(BUTTON_RANGES)
         self.allowed_actions = list(range(NUM_ACTIONS))

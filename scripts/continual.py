@@ -1,22 +1,97 @@
 #!/usr/bin/env python3
-"""Continual learning across a task sequence (BASELINE config 5: Pong -> Breakout -> SpaceInvaders -> Alien).
+"""Continual learning across a task sequence: the reference's only experiment, generalised to K tasks.
 
-Each task trains the population for a frame budget. At task end the winner path is frozen together with its
-task-specific head. Every other parameter is then re-initialised (doom_pathnet.py:274-293). After the last
-task, every task is re-evaluated greedily with its own frozen path and head. Frozen parameters are never
-updated, so the earlier tasks' scores must survive the later tasks (no catastrophic forgetting).
+Reference: task 1 -> freeze the last winner -> re-initialise every other parameter -> task 2
+(``doom_pathnet.py:274-293``), logged as Alien -> Centipede (``aliencentipede.txt:55-93``).  BASELINE
+config 5 names the 4-task suite Pong -> Breakout -> SpaceInvaders -> Alien.
 
-    python scripts/continual.py --frames 25000000 [--tasks Pong,Breakout,SpaceInvaders,Alien]
+Per task this records the tournament-winner curve and generations-to-solve, the frozen path, and a greedy
+evaluation of the task's own frozen path + head right after the task AND again after the whole sequence.
+Frozen parameters are never updated, so the two evaluations must agree (no forgetting).  ``--control``
+also trains every task >= 2 from scratch with the same budget, so transfer = sequence vs scratch.
+
+    python scripts/continual.py --tasks Pong,Breakout --frames 30000000 --control --out profiles/continual/x.json
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def build_cfg(args, tasks):
+    from pathnet_gym_amd.config import preset
+    cfg = preset("atari4")
+    cfg.tasks = list(tasks)
+    cfg.net.num_tasks = len(cfg.tasks)
+    cfg.net.per_task_heads = True
+    cfg.net.N = args.N
+    if args.trunk_scale:
+        cfg.net.trunk_scale = args.trunk_scale
+    if args.lr:
+        cfg.a2c.lr = args.lr
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = args.paths, args.envs, args.tmax
+    cfg.ga.backend = "device"
+    cfg.ga.concurrent_tournaments = max(1, args.paths // 16)
+    cfg.steps_per_task = args.frames
+    cfg.a2c.max_time_step = args.frames
+    cfg.a2c.lr_anneal = "none"
+    cfg.seed = cfg.ga.seed = args.seed
+    return cfg
+
+
+def greedy_eval(tr, ti, name, args, dev):
+    from pathnet_gym_amd.algo.evaluate import evaluate_model
+    from pathnet_gym_amd.models.acnet import ACPathNet
+    import torch
+    m = ACPathNet(tr.cfg.net, 1, dev, "torch")
+    with torch.no_grad():
+        m.store.flat.copy_(tr.model.store.flat.detach())
+    m.set_paths(tr.task_paths[ti][None])
+    m.task = ti
+    r = evaluate_model(m, name, episodes=args.eval_episodes, max_steps=args.eval_steps, device=dev,
+                       frameskip=tr.cfg.frameskip, gray=tr.cfg.gray)
+    return r[0] if math.isfinite(r[0]) else None
+
+
+def train_task(tr, ti, args, label):
+    """Train task ti of the trainer for args.frames frames; returns the per-task record (curve included)."""
+    if ti != tr.task_idx:
+        tr._start_task(ti)
+    name = tr.cfg.tasks[ti]
+    from pathnet_gym_amd.envs.registry import reward_threshold
+    thr = reward_threshold(name)
+    best, n, ema = -math.inf, 0, None
+    curve = []
+    ts = time.time()
+    last = ts
+    solved = None
+    while tr.global_step - tr.task_start_step < args.frames:
+        st = tr.update()
+        n += 1
+        if not math.isnan(st.mean_return):
+            ema = st.mean_return if ema is None else 0.95 * ema + 0.05 * st.mean_return
+        if st.tournaments:
+            best = max(best, st.best_winner)
+            if solved is None and st.best_winner >= thr:
+                solved = dict(generation=tr.pop.generation - tr._task_gen0, frames=tr.global_step - tr.task_start_step,
+                              seconds=round(time.time() - ts, 1))
+        if time.time() - last >= args.report_every:
+            last = time.time()
+            rec = dict(run=label, task=name, t=round(last - ts, 1), frames=tr.global_step - tr.task_start_step,
+                       generation=tr.pop.generation - tr._task_gen0, best_winner=best, mean_return=ema)
+            curve.append(rec)
+            print(json.dumps(rec), flush=True)
+    tr.flush()
+    return {"task": name, "updates": n, "seconds": round(time.time() - ts, 1), "frames": args.frames,
+            "threshold": thr, "best_winner": best if math.isfinite(best) else None, "final_mean_return": ema, "solved": solved is not None,
+            "generations_to_solve": solved and solved["generation"], "frames_to_solve": solved and solved["frames"],
+            "generations": tr.pop.generation - tr._task_gen0, "curve": curve}
 
 
 def main():
@@ -26,67 +101,76 @@ def main():
     ap.add_argument("--paths", type=int, default=16)
     ap.add_argument("--envs", type=int, default=16)
     ap.add_argument("--tmax", type=int, default=5)
-    ap.add_argument("--N", type=int, default=10)
+    ap.add_argument("--N", type=int, default=4)
+    ap.add_argument("--trunk-scale", default=None, choices=["M", "none"])
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--eval-episodes", type=int, default=4)
     ap.add_argument("--eval-steps", type=int, default=6000)
+    ap.add_argument("--report-every", type=float, default=20.0)
+    ap.add_argument("--control", action="store_true", help="also train tasks >= 2 from scratch (transfer control)")
     ap.add_argument("--out", default="gpurun_out/continual.json")
     args = ap.parse_args()
     import numpy as np
     import torch
     from pathnet_gym_amd import _build
-    from pathnet_gym_amd.algo.evaluate import evaluate_model
+    from pathnet_gym_amd.algo.ga import decode_path
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
-    from pathnet_gym_amd.config import preset
-    from pathnet_gym_amd.models.acnet import ACPathNet
     if torch.cuda.is_available():
         _build.build()
-    cfg = preset("atari4")
-    cfg.tasks = [t.strip() for t in args.tasks.split(",")]
-    cfg.net.num_tasks = len(cfg.tasks)
-    cfg.net.per_task_heads = True
-    cfg.net.N = args.N
-    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = args.paths, args.envs, args.tmax
-    cfg.ga.backend = "device"
-    cfg.ga.concurrent_tournaments = max(1, args.paths // 16)
-    cfg.steps_per_task = args.frames
-    cfg.a2c.max_time_step = args.frames
     dev = "cuda" if torch.cuda.is_available() else "cpu"
+    tasks = [t.strip() for t in args.tasks.split(",")]
+    cfg = build_cfg(args, tasks)
     tr = PathNetTrainer(cfg, device=dev)
     t0 = time.time()
     per_task = []
-    for ti, name in enumerate(cfg.tasks):
-        if ti != tr.task_idx:
-            tr._start_task(ti)
-        best, n = -1e9, 0
-        ts = time.time()
-        while tr.global_step - tr.task_start_step < args.frames:
-            st = tr.update()
-            n += 1
-            if st.tournaments:
-                best = max(best, st.best_winner)
-        tr.flush()
+    frozen_snap = []
+    for ti, name in enumerate(tasks):
+        rec = train_task(tr, ti, args, "sequence")
         winner, frozen = tr.end_task()
-        per_task.append({"task": name, "updates": n, "seconds": round(time.time() - ts, 1), "best_winner": best,
-                         "solved_generation": tr.solved_generation.get(ti),
-                         "frozen_modules": int(frozen.sum())})
-        print(json.dumps(per_task[-1]), flush=True)
-    # re-evaluate every task with its own frozen path + head after the whole sequence
-    evals = []
-    for ti, name in enumerate(cfg.tasks):
-        m = ACPathNet(cfg.net, 1, dev, "torch")
-        with torch.no_grad():
-            m.store.flat.copy_(tr.model.store.flat.detach())
-        m.set_paths(tr.task_paths[ti][None])
-        m.task = ti
-        r = evaluate_model(m, name, episodes=args.eval_episodes, max_steps=args.eval_steps, device=dev,
-                           frameskip=cfg.frameskip, gray=cfg.gray)
-        evals.append({"task": name, "greedy_return": r[0]})
-        print(json.dumps(evals[-1]), flush=True)
-    out = {"tasks": cfg.tasks, "frames_per_task": args.frames, "per_task": per_task, "final_eval": evals,
-           "seconds": round(time.time() - t0, 1)}
+        rec["frozen_path"] = [p.tolist() for p in decode_path(tr.task_paths[ti])]
+        rec["frozen_modules_total"] = int(frozen.sum())
+        rec["greedy_after_task"] = greedy_eval(tr, ti, name, args, dev)
+        # snapshot of this task's frozen parameters (its modules + its head) to prove they never change again
+        lay = tr.model.store.layout
+        keep = np.zeros(lay.numel, bool)
+        for s in lay.segments:
+            if (s.layer >= 0 and tr.task_paths[ti][s.layer, s.module] > 0.5) or s.task == ti:
+                keep[s.offset:s.offset + s.numel] = True
+        frozen_snap.append((keep, tr.model.store.flat.detach().cpu().numpy()[keep].copy()))
+        per_task.append(rec)
+        print(json.dumps({k: v for k, v in rec.items() if k != "curve"}), flush=True)
+    flat_end = tr.model.store.flat.detach().cpu().numpy()
+    for ti, name in enumerate(tasks):
+        keep, vals = frozen_snap[ti]
+        per_task[ti]["frozen_params_bit_identical_at_end"] = bool(np.array_equal(flat_end[keep], vals))
+        per_task[ti]["greedy_after_sequence"] = greedy_eval(tr, ti, name, args, dev)
+        a, b = per_task[ti]["greedy_after_task"], per_task[ti]["greedy_after_sequence"]
+        per_task[ti]["forgetting"] = None if a is None or b is None else a - b
+        print(json.dumps({"task": name, "greedy_after_task": per_task[ti]["greedy_after_task"],
+                          "greedy_after_sequence": per_task[ti]["greedy_after_sequence"],
+                          "frozen_params_bit_identical_at_end": per_task[ti]["frozen_params_bit_identical_at_end"]}),
+              flush=True)
+    controls = []
+    if args.control:
+        for name in tasks[1:]:
+            ctr = PathNetTrainer(build_cfg(args, [name]), device=dev)
+            rec = train_task(ctr, 0, args, "scratch")
+            controls.append({k: v for k, v in rec.items()})
+            print(json.dumps({k: v for k, v in rec.items() if k != "curve"}), flush=True)
+            del ctr
+            torch.cuda.empty_cache() if dev == "cuda" else None
+    out = {"experiment": "continual", "reference": "doom_pathnet.py:274-293, aliencentipede.txt:55-93",
+           "tasks": tasks, "frames_per_task": args.frames, "n_gpus": 1,
+           "config": {"paths": args.paths, "envs_per_path": args.envs, "t_max": args.tmax, "N": args.N,
+                      "M": cfg.net.M, "B": cfg.ga.B, "trunk_scale": cfg.net.trunk_scale, "lr": cfg.a2c.lr,
+                      "per_task_heads": True, "freeze_union": cfg.ga.freeze_union, "seed": args.seed,
+                      "env_reduction": cfg.a2c.env_reduction, "dtype": cfg.compute_dtype},
+           "per_task": per_task, "scratch_control": controls, "seconds": round(time.time() - t0, 1)}
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
-    json.dump(out, open(args.out, "w"), indent=1)
-    print(json.dumps({"done": True, "seconds": out["seconds"]}))
+    with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({"done": True, "seconds": out["seconds"], "out": args.out}), flush=True)
 
 
 if __name__ == "__main__":

@@ -97,3 +97,22 @@ def test_scoreboard_metadata_covers_every_id():
     from pathnet_gym_amd.envs.doom import DOOM_REGISTRY, scoreboard
     assert set(scoreboard.TASKS) == set(DOOM_REGISTRY)
     assert all(t["group"] == "doom" and t["summary"] for t in scoreboard.TASKS.values())
+
+
+def test_generated_scenario_configs_match_reference_settings(tmp_path):
+    """The nine scenario .cfg files (gym_doom/assets/*.cfg) generated from one table."""
+    from pathnet_gym_amd.envs.doom import scenarios as sc
+    from pathnet_gym_amd.envs.doom.constants import ALLOWED_ACTIONS, BUTTONS, DOOM_SETTINGS
+    d = sc.write_assets(str(tmp_path))
+    for li, row in enumerate(DOOM_SETTINGS):
+        cfg = sc.parse_cfg(open(f"{d}/{row[0]}").read())
+        assert cfg["screen_format"] == "BGR24" and cfg["sound_enabled"] == "false"
+        assert len(cfg["available_game_variables"]) == 22
+        # the level's allowed buttons (doom_env.py:33-44) are exactly the config's buttons
+        names = [BUTTONS[i].replace("ALT_ATTACK", "ALTATTACK") for i in ALLOWED_ACTIONS[li]]
+        assert sorted(cfg["available_buttons"]) == sorted(names), row[0]
+    basic = sc.parse_cfg(sc.render_cfg("basic.cfg"))
+    assert basic["living_reward"] == "-10" and basic["episode_start_time"] == "14" and basic["episode_timeout"] == "350"
+    assert basic["available_buttons"] == ["ATTACK", "MOVE_RIGHT", "MOVE_LEFT"]
+    assert sc.parse_cfg(sc.render_cfg("deathmatch.cfg"))["episode_timeout"] == "6300"
+    assert sc.parse_cfg(sc.render_cfg("health_gathering.cfg"))["death_penalty"] == "100"
