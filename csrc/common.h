@@ -40,6 +40,26 @@ DEVI s8v u8x8_to_bf16(uint2 v) {
   return r;
 }
 
+// 8 x uint8 -> 8 x fp16 holding (1024 + v): fp16(1024 + v) has the bit pattern 0x6400 | v for v < 1024,
+// so one v_perm_b32 per 2 pixels builds it (vs 12 VALU for u8 -> f32 -> bf16).  The +1024 offset is
+// removed in the epilogue through a per-column bias correction (1024 * sum_k w_k, csrc/optim.hip).
+DEVI s8v u8x8_to_f16off(uint2 v) {
+  const uint32_t o = 0x64646464u;
+  uint32_t d[4];
+  d[0] = __builtin_amdgcn_perm(o, v.x, 0x04010400u);
+  d[1] = __builtin_amdgcn_perm(o, v.x, 0x04030402u);
+  d[2] = __builtin_amdgcn_perm(o, v.y, 0x04010400u);
+  d[3] = __builtin_amdgcn_perm(o, v.y, 0x04030402u);
+  s8v r;
+  __builtin_memcpy(&r, d, 16);
+  return r;
+}
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+DEVI f4v mfma16_f16(const s8v& a, const s8v& b, const f4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+}
+
 DEVI s8v f32x8_to_bf16(const float* f) {
   __bf16 h[8];
 #pragma unroll

@@ -86,8 +86,12 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
                                                      const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
                                                      int layer, int L, int M, int P, int E, int T, int t0,
                                                      long bits_rows, float in_scale, float out_scale,
-                                                     const uint8_t* __restrict__ fcv = nullptr, int nslots = 0) {
+                                                     const uint8_t* __restrict__ fcv = nullptr, int nslots = 0,
+                                                     const float* __restrict__ hcorr = nullptr) {
   static_assert(!RING || (G::U8 && G::CIN == 4 && G::KW == 8 && G::K == 256), "ring input: 8x8x4 uint8 layer");
+  // uint8 input (packed stacks): fp16 MFMA on (1024 + pixel) operands built with one v_perm per 2 pixels;
+  // Wc then holds fp16 weights and hcorr[module*8 + map] = sum_k w_k (the offset's contribution)
+  constexpr bool F16 = G::U8 && !RING;
   constexpr int KPs = G::KP + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Ws[NCT * 16 * KPs];
   __shared__ float bias_s[NCT * 16];
@@ -105,7 +109,14 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
     if (slot < cnt) v = *reinterpret_cast<const s8v*>(Wc + ((long)(mods[slot] * 8 + (col & 7))) * G::KP + kc * 8);
     *reinterpret_cast<s8v*>(Ws + col * KPs + kc * 8) = v;
   }
-  if (tid < NCT * 16) bias_s[tid] = (tid >> 3) < cnt ? flat[bias_off + (long)mods[tid >> 3] * chunk + (tid & 7)] : 0.f;
+  if (tid < NCT * 16) {
+    float bv = 0.f;
+    if ((tid >> 3) < cnt) {
+      bv = flat[bias_off + (long)mods[tid >> 3] * chunk + (tid & 7)];
+      if constexpr (F16) bv -= 1024.f * in_scale * hcorr[mods[tid >> 3] * 8 + (tid & 7)];
+    }
+    bias_s[tid] = bv;
+  }
   __syncthreads();
 
   // compile-time column-tile count per instantiation (see conv_wgrad_slab)
@@ -222,7 +233,10 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
       for (int kk = 0; kk < NK; ++kk) {
         const int kc = kk * 4 + grp;
         s8v a0, a1;
-        if constexpr (G::U8) {
+        if constexpr (F16) {
+          a0 = u8x8_to_f16off(cur[0][kk]);
+          a1 = u8x8_to_f16off(cur[1][kk]);
+        } else if constexpr (G::U8) {
           a0 = u8x8_to_bf16(cur[0][kk]);
           a1 = u8x8_to_bf16(cur[1][kk]);
         } else {
@@ -232,8 +246,13 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
 #pragma unroll
         for (int ct = 0; ct < NC; ++ct) {
           const s8v b = *reinterpret_cast<const s8v*>(Ws + (ct * 16 + c16) * KPs + kc * 8);
-          acc[0][ct] = mfma16(a0, b, acc[0][ct]);
-          acc[1][ct] = mfma16(a1, b, acc[1][ct]);
+          if constexpr (F16) {
+            acc[0][ct] = mfma16_f16(a0, b, acc[0][ct]);
+            acc[1][ct] = mfma16_f16(a1, b, acc[1][ct]);
+          } else {
+            acc[0][ct] = mfma16(a0, b, acc[0][ct]);
+            acc[1][ct] = mfma16(a1, b, acc[1][ct]);
+          }
         }
       }
 #pragma unroll
@@ -1334,25 +1353,31 @@ template <class G, int NT, bool RING = false>
 static void fwd_launch(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
                        int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0,
                        long br, float is, float os, hipStream_t st, const uint8_t* fcv = nullptr,
-                       int nslots = 0) {
+                       int nslots = 0, const float* hcorr = nullptr) {
   const long rows = (long)T * E * G::HOWO;
   dim3 grid((unsigned)((rows + NT * 128 - 1) / (NT * 128)), P);
   conv_fwd_fast<G, NT, RING><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat, bias_off,
-                                                   chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, fcv, nslots);
+                                                   chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, fcv, nslots,
+                                                   hcorr);
 }
 
 template <class G>
 static int fwd_t(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off, int chunk,
                  const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0, long br,
-                 float is, float os, hipStream_t st) {
+                 float is, float os, hipStream_t st, const float* hcorr = nullptr) {
+  if (G::U8 && !hcorr) return 22;       // uint8 layers run the fp16-offset path: fp16 weights + correction table
   if (FWD_NT >= 16)
-    fwd_launch<G, 16>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st);
+    fwd_launch<G, 16>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st,
+                      nullptr, 0, hcorr);
   else if (FWD_NT >= 8)
-    fwd_launch<G, 8>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st);
+    fwd_launch<G, 8>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st,
+                     nullptr, 0, hcorr);
   else if (FWD_NT >= 4)
-    fwd_launch<G, 4>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st);
+    fwd_launch<G, 4>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st,
+                     nullptr, 0, hcorr);
   else
-    fwd_launch<G, 2>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st);
+    fwd_launch<G, 2>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st,
+                     nullptr, 0, hcorr);
   return (int)hipGetLastError();
 }
 
@@ -1452,24 +1477,28 @@ void fast_conv_set_fwd_nt(int nt) { FWD_NT = nt; }
 void fast_conv_set_wgrad_pf(int pf) { WGRAD_PF = pf; }
 
 // return 1 if handled by a fast kernel, 0 if the shape is not specialised, <0 on error
+// uint8 layers: Wc must be the fp16 weight copy and hcorr[M*8] its per-column sums (launch_refresh_weights_f16);
+// the img / slab experiments still take the bf16 copy in Wc_bf16
 int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
                   int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH,
-                  int KW, int S, int P, int E, int T, int t0, long br, float is, float os, hipStream_t st) {
+                  int KW, int S, int P, int E, int T, int t0, long br, float is, float os, const float* hcorr,
+                  const void* Wc_bf16, hipStream_t st) {
   if (M > 2 * NCT) return 0;
 #define FWD(Gx)                                                                                              \
   if (is_shape<Gx>(Hin, Win, Cin, KH, KW, S, u8in)) {                                                        \
     if ((E * Gx::HOWO) % 16) return -2;                                                                      \
-    const int rc = fwd_t<Gx>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st); \
+    const int rc = fwd_t<Gx>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st, \
+                             hcorr);                                                                         \
     return rc ? -rc : 1;                                                                                     \
   }
   if (IMG_FWD && is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) {
-    const int rc = fwd_img_t<C1>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os,
-                                 st);
+    const int rc = fwd_img_t<C1>(X, Y, bits, Wc_bf16, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is,
+                                 os, st);
     return rc ? -rc : 1;
   }
   if (SLAB_FWD && is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) {
-    const int rc = fwd_slab_t<C1, 2>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is,
-                                     os, st);
+    const int rc = fwd_slab_t<C1, 2>(X, Y, bits, Wc_bf16, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br,
+                                     is, os, st);
     return rc ? -rc : 1;
   }
   FWD(C1) FWD(C2) FWD(C3)

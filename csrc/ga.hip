@@ -25,10 +25,13 @@ DEVI uint32_t ga_rand(uint32_t seed, uint32_t gen, uint32_t x, uint32_t y, uint3
 __global__ __launch_bounds__(256) void ga_step_kernel(uint8_t* __restrict__ geno, float* __restrict__ fitness,
                                                       int* __restrict__ slots, long long* __restrict__ gen_ctr,
                                                       int* __restrict__ events, int P, int L, int M, int N, int B,
-                                                      int C, uint32_t seed) {
+                                                      int C, uint32_t seed, uint8_t* __restrict__ reset) {
   __shared__ int ready[GA_MAXC], winner[GA_MAXC], gen_of[GA_MAXC];
   __shared__ int nfired;
   const int tid = threadIdx.x;
+  // reset[i] = 1 for the candidates of tournaments that fire now (their episode windows restart)
+  if (reset)
+    for (int i = tid; i < P; i += 256) reset[i] = 0;
   if (tid < C) {
     int r = slots[tid * B] >= 0;
     int w = -1;
@@ -89,7 +92,10 @@ __global__ __launch_bounds__(256) void ga_step_kernel(uint8_t* __restrict__ geno
   // every fired slot's candidates -> pending (read by nothing else in this kernel from here on)
   for (int item = tid; item < C * B; item += 256) {
     const int c = item / B;
-    if (ready[c]) fitness[slots[item]] = GA_PENDING;
+    if (ready[c]) {
+      fitness[slots[item]] = GA_PENDING;
+      if (reset) reset[slots[item]] = 1;
+    }
   }
   __syncthreads();
   // redraw the freed slots (serial, as the mirror): busy = candidates of slots still pending
@@ -165,10 +171,10 @@ __global__ void ga_compact_inverse_kernel(const float* __restrict__ mask, int P_
 
 extern "C" {
 int launch_ga_step(void* geno, float* fitness, int* slots, long long* gen_ctr, int* events, int P, int L, int M,
-                   int N, int B, int C, unsigned seed, hipStream_t stream) {
+                   int N, int B, int C, unsigned seed, void* reset, hipStream_t stream) {
   if (C > GA_MAXC || B > GA_MAXB || L > GA_MAXL || M > GA_MAXM || C < 1) return -1;
   ga_step_kernel<<<1, 256, (size_t)P, stream>>>((uint8_t*)geno, fitness, slots, gen_ctr, events, P, L, M, N, B, C,
-                                                seed);
+                                                seed, (uint8_t*)reset);
   return (int)hipGetLastError();
 }
 

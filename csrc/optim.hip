@@ -89,6 +89,27 @@ __global__ __launch_bounds__(256) void refresh_weights_kernel(const float* __res
   }
 }
 
+// fp16 operand copy of a uint8-input conv layer (conv_fwd_fast F16 path): Wh[j][c][k] = fp16(w) for k < K
+// (zero to KP), and hcorr[j*Cout + c] = sum_k float(fp16(w_k)) -- the (1024 + pixel) offset's share of the
+// accumulator, removed through the bias.  One workgroup per (module, map); fixed-order reduction.
+__global__ __launch_bounds__(256) void refresh_f16_kernel(const float* __restrict__ flat, long w_off, int chunk, int K,
+                                                          int KP, int Cout, uint16_t* __restrict__ Wh,
+                                                          float* __restrict__ hcorr) {
+  const int jc = blockIdx.x, j = jc / Cout, c = jc - j * Cout, tid = threadIdx.x;
+  float s = 0.f;
+  for (int k = tid; k < KP; k += 256) {
+    const float v = k < K ? flat[w_off + (long)j * chunk + (long)k * Cout + c] : 0.f;
+    const _Float16 h = (_Float16)v;
+    Wh[(long)jc * KP + k] = __builtin_bit_cast(uint16_t, h);
+    s += (float)h;
+  }
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) hcorr[jc] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // first conv layer on the frame ring: Wc[j][c][k'] with channel-major k' = (ci*KH + kh)*KW + kw,
 // read from the flat (kh, kw, ci)-ordered module weights.  K == KP (K % 32 == 0).
 __global__ __launch_bounds__(256) void refresh_cmajor_kernel(const float* __restrict__ flat, long w_off, int chunk,
@@ -129,6 +150,13 @@ int launch_rmsprop(float* w, const float* g, float* ms, float* mom, const int* b
   rmsprop_apply_kernel<<<nblk, 256, 0, stream>>>(w, g, ms, mom, blk_seg, blk_beg, blk_end, partial, seg_blk0, nblk,
                                                  (const uint8_t*)trainable, lr_ptr, status, decay, momentum, eps,
                                                  clip);
+  return (int)hipGetLastError();
+}
+
+int launch_refresh_weights_f16(const float* flat, long w_off, int chunk, int K, int KP, int Cout, int M, void* Wh,
+                               float* hcorr, hipStream_t stream) {
+  if (M <= 0 || Cout <= 0 || KP < K) return -1;
+  refresh_f16_kernel<<<M * Cout, 256, 0, stream>>>(flat, w_off, chunk, K, KP, Cout, (uint16_t*)Wh, hcorr);
   return (int)hipGetLastError();
 }
 

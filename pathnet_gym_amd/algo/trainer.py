@@ -346,15 +346,21 @@ class PathNetTrainer:
                     self.comm.plan(self.pop.expressed(), self.pop.frozen)
             else:
                 self._push_genotypes()
-            fl = torch.from_numpy(self.pop.fitness[lo:hi]).to(self.device)
-            if self.engine is not None:
-                if self.engine.ga_dev is None:
-                    self.engine.reset_fitness(fl)
-            else:
-                self.fitness_local.copy_(fl)
-                pend = fl <= FITNESS_PENDING
-                self.fit_cnt.masked_fill_(pend, 0.0)
-                self.fit_sum.masked_fill_(pend, 0.0)
+            if self.engine is None or self.engine.ga_dev is None:
+                fl = torch.from_numpy(self.pop.fitness[lo:hi]).to(self.device)
+                # only the candidates of the tournaments that fired restart their episode window
+                fired_np = np.zeros(self.P, bool)
+                for e in events:
+                    for i in e.candidates:
+                        if lo <= i < hi:
+                            fired_np[i - lo] = True
+                fired = torch.from_numpy(fired_np).to(self.device)
+                if self.engine is not None:
+                    self.engine.reset_fitness(fl, fired)
+                else:
+                    self.fitness_local.copy_(fl)
+                    self.fit_cnt.masked_fill_(fired, 0.0)
+                    self.fit_sum.masked_fill_(fired, 0.0)
             if self.visualizer is not None and time.time() - self._last_vis > 10.0:
                 from .ga import decode_path
                 self.visualizer.show([decode_path(g) for g in self.pop.genotypes], "m")   # visualize.py:90

@@ -59,7 +59,8 @@ _SIGS = {
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],
     "fast_conv_fwd": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                      c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P],
+                      c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P, P, P],
+    "launch_refresh_weights_f16": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
     "fast_conv_wgrad": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P],
     "fast_conv_dgrad": [P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -77,7 +78,7 @@ _SIGS = {
     "fast_conv_set_wgrad_ob": [c_int],
     "fast_conv_set_fwd_nt": [c_int],
     "fast_conv_set_wgrad_pf": [c_int],
-    "launch_ga_step": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_uint, P],
+    "launch_ga_step": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_uint, P, P],
     "launch_ga_compact": [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P],
     "launch_typed_fc_fwd": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],
     "launch_typed_fc_dgrad": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],

@@ -142,6 +142,12 @@ class HipPathNet:
         self.ring_ok = (g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
                         and self.M <= 10 and g0.Cout == 8)
         self.Wc_ring = None
+        # uint8 first conv layer: fp16 operand copy + per-column weight sums for the fp16-offset MFMA path
+        # (conv_fwd_fast: pixels enter as fp16(1024 + v), built with one v_perm per two pixels)
+        self.Wh0 = self.hcorr0 = None
+        if g0.kind == "conv" and g0.u8in:
+            self.Wh0 = torch.zeros(self.M, g0.Cout, g0.KP, dtype=torch.float16, device=dev)
+            self.hcorr0 = torch.zeros(self.M * g0.Cout, dtype=torch.float32, device=dev)
         self.refresh_weights()
 
     def enable_ring(self):
@@ -179,6 +185,10 @@ class HipPathNet:
         for l, g in enumerate(self.geoms):
             _lib.call("launch_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
                       self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), _lib.stream())
+        if self.Wh0 is not None:
+            g = self.geoms[0]
+            _lib.call("launch_refresh_weights_f16", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
+                      self.Wh0.data_ptr(), self.hcorr0.data_ptr(), _lib.stream())
         if self.Wc_ring is not None:
             g = self.geoms[0]
             _lib.call("launch_refresh_weights_cmajor", flat.data_ptr(), g.w_off, g.chunk, g.KH, g.KW, g.Cin, g.Cout,
@@ -230,11 +240,13 @@ class HipPathNet:
         if g.kind == "conv":
             if (E * g.HWo) % 16 != 0:
                 raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
+            f16 = g.u8in and self.Wh0 is not None
             if _lib.USE_FAST and _lib.call_fast(
                     "fast_conv_fwd", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
-                    self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
-                    m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T, t0,
-                    bits_rows, g.in_scale, out_scale, st):
+                    (self.Wh0 if f16 else self.Wc[l]).data_ptr(), flat.data_ptr(), g.b_off, g.chunk,
+                    m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW,
+                    g.S, P, E, T, t0, bits_rows, g.in_scale, out_scale, _lib.ptr(self.hcorr0 if f16 else None),
+                    self.Wc[l].data_ptr(), st):
                 return
             _lib.call("launch_conv_fwd", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
                       self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),

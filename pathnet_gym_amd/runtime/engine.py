@@ -319,12 +319,13 @@ class HipEngine:
                   self.fitness.data_ptr(), self.counters.data_ptr(), self.fit_cnt.data_ptr(), self.fit_sum.data_ptr(),
                   self.fit_window, self.path_part.data_ptr(), _lib.stream())
 
-    def reset_fitness(self, fitness_local: torch.Tensor):
-        """Install the GA's view of the local fitness; paths reset to pending restart their episode window."""
+    def reset_fitness(self, fitness_local: torch.Tensor, fired: Optional[torch.Tensor] = None):
+        """Install the GA's view of the local fitness; the candidates of tournaments that fired (``fired``,
+        bool [P]) restart their episode window."""
         self.fitness.copy_(fitness_local)
-        pend = fitness_local <= -1000.0
-        self.fit_cnt.masked_fill_(pend, 0.0)
-        self.fit_sum.masked_fill_(pend, 0.0)
+        if fired is not None:
+            self.fit_cnt.masked_fill_(fired, 0.0)
+            self.fit_sum.masked_fill_(fired, 0.0)
 
     # -- device GA (GAConfig.backend == "device"; algo/ga_device.py mirrors it on the host) --------
     def enable_device_ga(self, pop, comm, p_off: int):
@@ -335,6 +336,7 @@ class HipEngine:
             slots=torch.full((pop.concurrent, pop.B), -1, dtype=torch.int32, device=dev),
             gen=torch.zeros(1, dtype=torch.int64, device=dev),
             events=torch.zeros(pop.concurrent, 3, dtype=torch.int32, device=dev),
+            reset=torch.zeros(pop.P, dtype=torch.uint8, device=dev),      # candidates of the tournaments just fired
             fit=comm.fit_reduced, p_off=p_off, pop=pop,
             # union of the modules the whole population expresses next, minus frozen ones (csrc/comm.hip):
             # read back after every optimizer step to plan the active-path gradient all-reduce
@@ -361,17 +363,19 @@ class HipEngine:
         st = _lib.stream()
         _lib.call("launch_ga_step", g["geno"].data_ptr(), g["fit"].data_ptr(), g["slots"].data_ptr(),
                   g["gen"].data_ptr(), g["events"].data_ptr(), pop.P, pop.L, pop.M, pop.N, pop.B, pop.concurrent,
-                  pop.seed32, st)
+                  pop.seed32, g["reset"].data_ptr(), st)
         _lib.call("launch_ga_compact", g["geno"].data_ptr(), g["frozen"].data_ptr(), g["p_off"], self.P, pop.L,
                   pop.M, m.mask.data_ptr(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), hp.inv_path.data_ptr(),
                   hp.inv_slot.data_ptr(), hp.inv_cnt.data_ptr(), st)
         _lib.call("launch_active_union", g["geno"].data_ptr(), g["frozen"].data_ptr(), pop.P, pop.L, pop.M,
                   g["union"].data_ptr(), st)
-        # local fitness <- the GA's view; paths reset to pending restart their episode window
+        # local fitness <- the GA's view; ONLY the candidates of tournaments that just fired restart their
+        # episode window (paths still filling theirs keep accumulating)
         self.fitness.copy_(g["fit"][g["p_off"]:g["p_off"] + self.P])
-        pend = self.fitness <= -1000.0
-        self.fit_cnt.masked_fill_(pend, 0.0)
-        self.fit_sum.masked_fill_(pend, 0.0)
+        if self.fit_window > 0:
+            fired = g["reset"][g["p_off"]:g["p_off"] + self.P].bool()
+            self.fit_cnt.masked_fill_(fired, 0.0)
+            self.fit_sum.masked_fill_(fired, 0.0)
 
     def _read_union(self):
         """After an optimizer step: start the D2H of the device GA's next module union (outside any graph)."""

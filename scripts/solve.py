@@ -103,6 +103,9 @@ def main():
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
     if args.no_ga:
         tr.pop.step = lambda *a, **k: []
+        if tr.engine is not None and tr.engine.ga_dev is not None:
+            tr.pop.slots[:] = -1                 # no tournament slots: the device GA never fires
+            tr.engine.ga_upload(tr.pop)
     if args.same_path:
         tr.pop.genotypes[:] = tr.pop.genotypes[0]
         tr._push_genotypes()

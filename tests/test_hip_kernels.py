@@ -683,9 +683,14 @@ def test_device_ga_matches_host_mirror(hip_lib):
         fit = torch.from_numpy(f).to(DEV)
         evs = pop.step(f, t)
         fired += len(evs)
+        reset = torch.full((P,), 7, dtype=torch.uint8, device=DEV)
         _lib.call("launch_ga_step", geno.data_ptr(), fit.data_ptr(), slots.data_ptr(), gen.data_ptr(),
-                  events.data_ptr(), P, L, M, N, B, C, pop.seed32, _lib.stream())
+                  events.data_ptr(), P, L, M, N, B, C, pop.seed32, reset.data_ptr(), _lib.stream())
         torch.cuda.synchronize()
+        want = np.zeros(P, np.uint8)
+        for e in evs:
+            want[e.candidates] = 1
+        assert np.array_equal(reset.cpu().numpy(), want), t          # exactly the fired candidates restart
         assert np.array_equal(geno.cpu().numpy(), pop.genotypes.astype(np.uint8)), t
         assert np.array_equal(slots.cpu().numpy(), pop.slots.astype(np.int32)), t
         assert np.array_equal(fit.cpu().numpy(), pop.fitness), t

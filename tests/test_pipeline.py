@@ -45,3 +45,41 @@ def test_pipelined_device_ga_counters_stay_sane(hip_lib):
     assert (np.abs(ret) <= 21.0 * np.maximum(cnt, 1.0)).all(), np.nonzero(np.abs(ret) > 21.0 * np.maximum(cnt, 1.0))[0][:5]
     fit = H[:, :P]
     assert ((fit == -1000.0) | (np.abs(fit) <= 21.0)).all()
+
+
+def test_frozen_modules_bit_identical_across_task2_updates_hip(hip_lib):
+    """Continual learning on the HIP engine: after task 1 freezes its winner path (and per-task head),
+    task-2 updates (device GA, pipelined, hipGraphs) leave every frozen parameter bit-identical and
+    keep the frozen modules expressed in every task-2 path (doom_pathnet.py:274-293)."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.config import preset
+    cfg = preset("atari4")
+    cfg.tasks = ["Pong", "Pong"]
+    cfg.net.num_tasks = 2
+    cfg.net.per_task_heads = True
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 8, 16, 4
+    cfg.ga.backend = "device"
+    cfg.ga.concurrent_tournaments = 2
+    tr = PathNetTrainer(cfg, device="cuda")
+    for _ in range(30):
+        tr.update()
+    winner, frozen = tr.end_task()
+    tr._start_task(1)
+    lay = tr.model.store.layout
+    keep = torch.zeros(lay.numel, dtype=torch.bool)
+    for s in lay.segments:
+        if (s.layer >= 0 and frozen[s.layer, s.module] > 0.5) or s.task == 0:
+            keep[s.offset:s.offset + s.numel] = True
+    keep = keep.cuda()
+    before = tr.model.store.flat.detach()[keep].clone()
+    other0 = tr.model.store.flat.detach()[~keep].clone()
+    for _ in range(40):
+        tr.update()
+    tr.flush()
+    torch.cuda.synchronize()
+    after = tr.model.store.flat.detach()
+    assert torch.equal(after[keep], before)
+    assert not torch.equal(after[~keep], other0)                 # task 2 does train the rest
+    geno = tr.engine.ga_dev["geno"].cpu().numpy() | tr.engine.ga_dev["frozen"].cpu().numpy()[None]
+    assert (geno[:, frozen > 0.5] == 1).all()
+    assert (tr.model.mask.cpu().numpy()[:, frozen > 0.5] == 1).all()

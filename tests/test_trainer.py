@@ -145,3 +145,25 @@ def test_checkpoint_keeps_continual_state_across_resume(tmp_path):
         sl = slice(s.offset, s.offset + s.numel)
         assert torch.equal(after[sl], before[sl]), s.name          # task-0 head neither trained nor re-initialised
     assert b.frozen_tasks == {0, 1} and set(b.task_paths) == {0, 1}
+
+
+def test_windowed_fitness_windows_restart_only_for_tournament_candidates():
+    """A tournament firing must not wipe the episode windows of paths that are still filling theirs."""
+    cfg = preset("cartpole-cpu")
+    cfg.paths, cfg.envs_per_path = 8, 4
+    cfg.ga.fitness = "mean"
+    cfg.ga.fitness_window = 6
+    tr = PathNetTrainer(cfg)
+    fired_any = False
+    for _ in range(120):
+        before = tr.fit_cnt.clone()
+        st = tr.update()
+        if st.tournaments:
+            fired_any = True
+            cands = set(i for e in tr.pop.history[-st.tournaments:] for i in e.candidates)
+            for p in range(tr.P):
+                if p not in cands:
+                    assert float(tr.fit_cnt[p]) >= float(before[p])      # still accumulating
+                else:
+                    assert float(tr.fit_cnt[p]) == 0.0
+    assert fired_any
