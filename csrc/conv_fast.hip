@@ -79,7 +79,7 @@ DEVI s8v ld8(const void* X, long off) {
 // planes are one contiguous 77 KB run, as a packed stack was.  k is channel-major
 // (k = (c*KH + kh)*KW + kw) so each A fragment is 8 consecutive pixels of one kernel row of one
 // frame plane: still one 8-byte load.  Wc holds the weights in that k order.
-template <class G, int NT, bool RING = false>
+template <class G, int NT, bool RING = false, bool F16 = false>
 __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* __restrict__ X, bf16_t* __restrict__ Y,
                                                      uint8_t* __restrict__ bits, const bf16_t* __restrict__ Wc,
                                                      const float* __restrict__ flat, long bias_off, int chunk,
@@ -89,9 +89,9 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
                                                      const uint8_t* __restrict__ fcv = nullptr, int nslots = 0,
                                                      const float* __restrict__ hcorr = nullptr) {
   static_assert(!RING || (G::U8 && G::CIN == 4 && G::KW == 8 && G::K == 256), "ring input: 8x8x4 uint8 layer");
-  // uint8 input (packed stacks): fp16 MFMA on (1024 + pixel) operands built with one v_perm per 2 pixels;
+  // F16 (uint8 input only): fp16 MFMA on (1024 + pixel) operands built with one v_perm per 2 pixels;
   // Wc then holds fp16 weights and hcorr[module*8 + map] = sum_k w_k (the offset's contribution)
-  constexpr bool F16 = G::U8 && !RING;
+  static_assert(!F16 || G::U8, "fp16-offset operands are for uint8 inputs");
   constexpr int KPs = G::KP + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Ws[NCT * 16 * KPs];
   __shared__ float bias_s[NCT * 16];
@@ -1347,6 +1347,9 @@ static int dgrad_mfma_t(const float* Gr, const void* bits, const float* flat, lo
 
 // ---------------------------------------------------------------------------
 static int FWD_NT = 4;         // 32-row tiles per wave in conv_fwd_fast (4 -> 512 rows per workgroup)
+// uint8 first layer: fp16-offset MFMA operands (1 v_perm per 2 pixels) instead of u8 -> f32 -> bf16 converts.
+// Off only for A/B runs and for the exact-equality tests against the bf16 alternative kernels.
+static int F16_FWD = 1;
 static int WGRAD_PF = 1;       // register sets of slab-wgrad loads in flight (1 or 2)
 
 template <class G, int NT, bool RING = false>
@@ -1356,16 +1359,23 @@ static void fwd_launch(const void* X, void* Y, void* bits, const void* Wc, const
                        int nslots = 0, const float* hcorr = nullptr) {
   const long rows = (long)T * E * G::HOWO;
   dim3 grid((unsigned)((rows + NT * 128 - 1) / (NT * 128)), P);
-  conv_fwd_fast<G, NT, RING><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat, bias_off,
-                                                   chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, fcv, nslots,
-                                                   hcorr);
+  if constexpr (G::U8) {
+    if (hcorr) {
+      conv_fwd_fast<G, NT, RING, true><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat,
+                                                             bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br,
+                                                             is, os, fcv, nslots, hcorr);
+      return;
+    }
+  }
+  conv_fwd_fast<G, NT, RING, false><<<grid, 256, 0, st>>>(X, (bf16_t*)Y, (uint8_t*)bits, (const bf16_t*)Wc, flat,
+                                                          bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is,
+                                                          os, fcv, nslots, nullptr);
 }
 
 template <class G>
 static int fwd_t(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off, int chunk,
                  const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0, long br,
                  float is, float os, hipStream_t st, const float* hcorr = nullptr) {
-  if (G::U8 && !hcorr) return 22;       // uint8 layers run the fp16-offset path: fp16 weights + correction table
   if (FWD_NT >= 16)
     fwd_launch<G, 16>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st,
                       nullptr, 0, hcorr);
@@ -1475,6 +1485,7 @@ void fast_conv_set_img_fwd(int on) { IMG_FWD = on; }
 void fast_conv_set_wgrad_ob(int ob) { WGRAD_OB = ob; }
 void fast_conv_set_fwd_nt(int nt) { FWD_NT = nt; }
 void fast_conv_set_wgrad_pf(int pf) { WGRAD_PF = pf; }
+void fast_conv_set_f16_fwd(int on) { F16_FWD = on; }
 
 // return 1 if handled by a fast kernel, 0 if the shape is not specialised, <0 on error
 // uint8 layers: Wc must be the fp16 weight copy and hcorr[M*8] its per-column sums (launch_refresh_weights_f16);
@@ -1484,6 +1495,10 @@ int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, 
                   int KW, int S, int P, int E, int T, int t0, long br, float is, float os, const float* hcorr,
                   const void* Wc_bf16, hipStream_t st) {
   if (M > 2 * NCT) return 0;
+  if (u8in && (!F16_FWD || !hcorr)) {      // bf16 operands: the bf16 weight copy, no offset correction
+    Wc = Wc_bf16;
+    hcorr = nullptr;
+  }
 #define FWD(Gx)                                                                                              \
   if (is_shape<Gx>(Hin, Win, Cin, KH, KW, S, u8in)) {                                                        \
     if ((E * Gx::HOWO) % 16) return -2;                                                                      \
@@ -1536,19 +1551,25 @@ int fast_conv_wgrad(const void* X, int u8in, const float* Gr, const void* bits, 
 // First layer on the frame ring (160x120 uint8 planes, 4 channels, 8x8/s4): fc = first valid
 // channel per (step, sample) [T+1][P*E] uint8.  Wc must be channel-major (launch_refresh_weights_cmajor).
 // frames [P*E][nslots][160*120] uint8 with nslots >= t0 + T + 3 (rollout: T_roll + 4 slots)
+// Wc: channel-major fp16 weights with hcorr (fp16-offset path) or channel-major bf16 with hcorr = null
 int fast_conv1_ring_fwd(const void* frames, const void* fc, void* Y, void* bits, const void* Wc, const float* flat,
                         long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E,
-                        int T, int t0, int nslots, long br, float is, float os, hipStream_t st) {
+                        int T, int t0, int nslots, long br, float is, float os, const float* hcorr,
+                        const void* Wc_bf16, hipStream_t st) {
   if (M > 2 * NCT) return -22;
   if ((E * C1::HOWO) % 16) return -2;
   if (nslots < t0 + T + 3) return -33;
+  if (!F16_FWD || !hcorr) {
+    Wc = Wc_bf16;
+    hcorr = nullptr;
+  }
   const uint8_t* f = (const uint8_t*)fc;
   if (FWD_NT >= 8)
     fwd_launch<C1, 8, true>(frames, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os,
-                            st, f, nslots);
+                            st, f, nslots, hcorr);
   else
     fwd_launch<C1, 4, true>(frames, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os,
-                            st, f, nslots);
+                            st, f, nslots, hcorr);
   return (int)hipGetLastError();
 }
 

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void refresh_f16_kernel(const float* __restric
 // read from the flat (kh, kw, ci)-ordered module weights.  K == KP (K % 32 == 0).
 __global__ __launch_bounds__(256) void refresh_cmajor_kernel(const float* __restrict__ flat, long w_off, int chunk,
                                                              int KH, int KW, int CIN, int Cout, int M,
-                                                             bf16_t* __restrict__ Wc) {
+                                                             bf16_t* __restrict__ Wc, int f16) {
   const int K = KH * KW * CIN;
   const long n = (long)M * K * Cout;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
@@ -123,19 +123,20 @@ __global__ __launch_bounds__(256) void refresh_cmajor_kernel(const float* __rest
     const int c = rem / K, kd = rem - c * K;
     const int ci = kd / (KH * KW), kh = (kd / KW) % KH, kw = kd % KW;
     const int ks = (kh * KW + kw) * CIN + ci;
-    Wc[i] = f2bf(flat[w_off + (long)j * chunk + (long)ks * Cout + c]);
+    const float v = flat[w_off + (long)j * chunk + (long)ks * Cout + c];
+    Wc[i] = f16 ? __builtin_bit_cast(uint16_t, (_Float16)v) : f2bf(v);
   }
 }
 
 extern "C" {
 
 int launch_refresh_weights_cmajor(const float* flat, long w_off, int chunk, int KH, int KW, int CIN, int Cout, int M,
-                                  void* Wc, hipStream_t stream) {
+                                  void* Wc, int f16, hipStream_t stream) {
   if ((KH * KW * CIN) % 32) return -22;
   const long n = (long)M * KH * KW * CIN * Cout;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;
-  refresh_cmajor_kernel<<<blocks, 256, 0, stream>>>(flat, w_off, chunk, KH, KW, CIN, Cout, M, (bf16_t*)Wc);
+  refresh_cmajor_kernel<<<blocks, 256, 0, stream>>>(flat, w_off, chunk, KH, KW, CIN, Cout, M, (bf16_t*)Wc, f16);
   return (int)hipGetLastError();
 }
 

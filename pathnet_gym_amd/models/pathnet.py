@@ -191,6 +191,11 @@ def bf16_ste(x: torch.Tensor) -> torch.Tensor:
     return x + (x.to(torch.bfloat16).float() - x).detach()
 
 
+def f16_ste(x: torch.Tensor) -> torch.Tensor:
+    """Round to fp16 in the forward pass, identity gradient (the HIP uint8-input conv layer's weight copy)."""
+    return x + (x.to(torch.float16).float() - x).detach()
+
+
 def trunk_forward_ref(store: ParamStore, x: torch.Tensor, mask: torch.Tensor,
                       W_override: Optional[List[torch.Tensor]] = None,
                       b_override: Optional[List[torch.Tensor]] = None,
@@ -200,7 +205,10 @@ def trunk_forward_ref(store: ParamStore, x: torch.Tensor, mask: torch.Tensor,
     x    : [B, *input_shape] float (NHWC for pixels, already scaled to [0,1])
     mask : [B, L, M] float (expressed genotype of each sample's path)
     emulate_bf16: round weights and every layer output to bf16 (the HIP
-                  kernels' storage precision; fp32 accumulation either way)
+                  kernels' storage precision; fp32 accumulation either way).  A
+                  first conv layer (uint8 pixels in the HIP engine) keeps fp16
+                  weights there (csrc/conv_fast.hip fp16-offset path), so it is
+                  rounded to fp16 instead.
     returns [B, feature_dim]
     """
     cfg = store.cfg
@@ -212,7 +220,7 @@ def trunk_forward_ref(store: ParamStore, x: torch.Tensor, mask: torch.Tensor,
         W = store.W(l) if W_override is None else W_override[l]
         b = store.b(l) if b_override is None else b_override[l]
         if emulate_bf16:
-            W = bf16_ste(W)
+            W = f16_ste(W) if (l == 0 and spec.kind == "conv") else bf16_ste(W)
         m = mask[:, l, :]
         cout = li["cout"]
         if spec.kind == "conv":

@@ -48,9 +48,9 @@ _SIGS = {
     "launch_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
     "launch_pong_step": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, P],
-    "launch_refresh_weights_cmajor": [P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P, P],
+    "launch_refresh_weights_cmajor": [P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P],
     "fast_conv1_ring_fwd": [P, P, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                            c_int, c_long, c_float, c_float, P],
+                            c_int, c_long, c_float, c_float, P, P, P],
     "fast_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_long, c_float, c_float, P],
     "launch_pong_step_ring": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int,
@@ -78,6 +78,7 @@ _SIGS = {
     "fast_conv_set_wgrad_ob": [c_int],
     "fast_conv_set_fwd_nt": [c_int],
     "fast_conv_set_wgrad_pf": [c_int],
+    "fast_conv_set_f16_fwd": [c_int],
     "launch_ga_step": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_uint, P, P],
     "launch_ga_compact": [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, P, P],
     "launch_typed_fc_fwd": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],

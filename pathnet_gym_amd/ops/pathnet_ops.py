@@ -156,7 +156,9 @@ class HipPathNet:
             raise NotImplementedError("frame ring needs the 160x120x4 / 8x8 s4 first conv layer and M <= 10")
         if self.Wc_ring is None:
             g = self.geoms[0]
-            self.Wc_ring = torch.zeros(self.M, g.Cout, g.KP, dtype=torch.bfloat16, device=self.model.device)
+            dev = self.model.device
+            self.Wc_ring = torch.zeros(self.M, g.Cout, g.KP, dtype=torch.bfloat16, device=dev)
+            self.Wh_ring = torch.zeros(self.M, g.Cout, g.KP, dtype=torch.float16, device=dev)     # fp16-offset path
             self.refresh_weights()
 
     # ------------------------------------------------------------------
@@ -191,8 +193,9 @@ class HipPathNet:
                       self.Wh0.data_ptr(), self.hcorr0.data_ptr(), _lib.stream())
         if self.Wc_ring is not None:
             g = self.geoms[0]
-            _lib.call("launch_refresh_weights_cmajor", flat.data_ptr(), g.w_off, g.chunk, g.KH, g.KW, g.Cin, g.Cout,
-                      self.M, self.Wc_ring.data_ptr(), _lib.stream())
+            for buf, f16 in ((self.Wc_ring, 0), (self.Wh_ring, 1)):
+                _lib.call("launch_refresh_weights_cmajor", flat.data_ptr(), g.w_off, g.chunk, g.KH, g.KW, g.Cin,
+                          g.Cout, self.M, buf.data_ptr(), f16, _lib.stream())
         if self.lstm is not None:
             ls = self.lstm
             _lib.call("launch_lstm_refresh", flat.data_ptr(), ls["k_off"], ls["F"], ls["H"], ls["KpT"].data_ptr(),
@@ -334,9 +337,9 @@ class HipPathNet:
         m = self.model
         out_scale = self.out_scale_last if self.L == 1 else 1.0
         _lib.call("fast_conv1_ring_fwd", frames.data_ptr(), fc.data_ptr(), Y.data_ptr(), bits.data_ptr(),
-                  self.Wc_ring.data_ptr(), m.store.flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
+                  self.Wh_ring.data_ptr(), m.store.flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
                   m.act_cnt.data_ptr(), 0, self.L, self.M, P, E, T, t0, frames.shape[1], bits_rows, g.in_scale,
-                  out_scale, _lib.stream())
+                  out_scale, self.hcorr0.data_ptr(), self.Wc_ring.data_ptr(), _lib.stream())
 
     def ring_wgrad(self, frames, fc, G, bits, grad_flat, P: int, E: int, T: int, bits_rows: int):
         self._check_ring(frames, fc, P, E, T)

@@ -4,9 +4,12 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out/learn1
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
-    > gpurun_out/pytest_gpu.log 2>&1 || { echo "PYTEST FAIL"; grep -E "PASS|FAIL|Error|^E " gpurun_out/pytest_gpu.log | tail -40; exit 1; }
-tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread \
+    > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+# assertion failures (rc 1) are reported and the learning runs still go; anything else (crash, timeout) stops here
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "PYTEST rc=$rc"; tail -30 gpurun_out/pytest_gpu.log; exit 1; fi
+grep -E "FAILED|^E " gpurun_out/pytest_gpu.log | head -20; tail -1 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_f16.log 2>&1 || { echo "BENCH FAIL"; tail -20 gpurun_out/bench_f16.log; exit 1; }
 tail -1 gpurun_out/bench_f16.log | cut -c1-300
 C="--preset pong --ga-backend device --seed 1 --report-every 30 --keep-going --N 4 --fitness mean"
