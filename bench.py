@@ -32,7 +32,7 @@ BASELINE_STEPS_PER_SEC = 63.0     # reference steady-state global a
 
 
 SOLVE_KEYS = ("preset", "paths_per_gpu", "envs_per_path", "t_max", "N", "B", "trunk_scale", "env_reduction", "lr",
-              "entropy_beta", "gae_lambda", "fitness", "concurrent_tournaments", "dtype")
+              "entropy_beta", "gae_lambda", "fitness", "concurrent_tournaments", "dtype", "rmsp_epsilon")
 
 
 def solve_key(cfg, preset_name: str) -> dict:
@@ -42,7 +42,8 @@ def solve_key(cfg, preset_name: str) -> dict:
             "t_max": cfg.a2c.t_max, "N": cfg.net.N, "B": cfg.ga.B, "trunk_scale": cfg.net.trunk_scale,
             "env_reduction": cfg.a2c.env_reduction, "lr": round(float(cfg.a2c.lr), 8),
             "entropy_beta": cfg.a2c.entropy_beta, "gae_lambda": cfg.a2c.gae_lambda, "fitness": cfg.ga.fitness,
-            "concurrent_tournaments": cfg.ga.concurrent_tournaments, "dtype": cfg.compute_dtype}
+            "concurrent_tournaments": cfg.ga.concurrent_tournaments, "dtype": cfg.compute_dtype,
+            "rmsp_epsilon": cfg.a2c.rmsp_epsilon}
 
 
 def solve_records(key: dict, n_gpus: int):
@@ -60,7 +61,8 @@ def solve_records(key: dict, n_gpus: int):
         if d.get("metric") != "generations_to_solve" or d.get("n_gpus") != n_gpus or not c.get("ga", True) \
                 or c.get("same_path"):
             continue
-        c = dict(c, dtype=c.get("dtype", "bf16"), lr=round(float(c.get("lr", 0.0)), 8))
+        c = dict(c, dtype=c.get("dtype", "bf16"), lr=round(float(c.get("lr", 0.0)), 8),
+                 rmsp_epsilon=c.get("rmsp_epsilon", 0.1))
         if any(c.get(k) != key[k] for k in SOLVE_KEYS):
             continue
         runs.append({"seed": c.get("seed"), "solved": bool(d.get("solved")),

