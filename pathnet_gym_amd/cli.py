@@ -54,6 +54,8 @@ def build_parser():
         p.add_argument("--backend", default=None, choices=["auto", "hip", "torch"])
         p.add_argument("--seed", type=int, default=None)
         p.add_argument("--use_lstm", type=int, default=None)
+        p.add_argument("--trunk_scale", default=None, choices=["M", "none"],
+                       help="divide the trunk output by M (reference FF net) or not (reference LSTM net)")
         p.add_argument("--no_graph", action="store_true")
         # RL constants (constants.py)
         p.add_argument("--t_max", type=int, default=None)
@@ -90,6 +92,8 @@ def build_parser():
     t.add_argument("--checkpoint", default=None, help="checkpoint path written at task ends / every --checkpoint_every")
     t.add_argument("--checkpoint_every", type=int, default=0, help="updates between checkpoints")
     t.add_argument("--resume", default=None)
+    t.add_argument("--init_from_tf", default=None,
+                   help="reference tf.train.Saver checkpoint prefix (model.ckpt-N) to start from (utils/tf_checkpoint.py)")
     t.add_argument("--graphs", action="store_true", help="dump path-graph PNGs per tournament (visualize.py)")
 
     e = sub.add_parser("eval")
@@ -150,6 +154,8 @@ def config_from_args(a):
         net.use_lstm = bool(a.use_lstm)
         if net.use_lstm:
             net.trunk_scale = "none"
+    if getattr(a, "trunk_scale", None):
+        net.trunk_scale = a.trunk_scale
     if a.B is not None:
         cfg.ga.B = a.B
     pop = a.paths if a.paths is not None else a.worker_hosts_num
@@ -215,6 +221,10 @@ def cmd_train(a):
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx, logger=logger)
     if a.resume:
         ckpt.load(tr, a.resume)
+    if getattr(a, "init_from_tf", None):
+        from .utils.tf_checkpoint import import_reference_checkpoint
+        info = import_reference_checkpoint(tr, a.init_from_tf)
+        logger.log("tf_import", **{k: v for k, v in info.items() if k != "genotypes"})
     if a.graphs and ctx.is_main:
         from .utils.visualize import GraphVisualize
         tr.visualizer = GraphVisualize([cfg.net.M] * cfg.net.L, out_dir=os.path.join(log_dir, "graphs"))
