@@ -102,23 +102,6 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
   const int tid = threadIdx.x;
   if (tid < MAXM_F) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
   __syncthreads();
-  for (int i = tid; i < nct * 16 * G::KC; i += 256) {
-    const int col = i / G::KC, kc = i - col * G::KC;
-    const int slot = col >> 3;
-    s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (slot < cnt) v = *reinterpret_cast<const s8v*>(Wc + ((long)(mods[slot] * 8 + (col & 7))) * G::KP + kc * 8);
-    *reinterpret_cast<s8v*>(Ws + col * KPs + kc * 8) = v;
-  }
-  if (tid < NCT * 16) {
-    float bv = 0.f;
-    if ((tid >> 3) < cnt) {
-      bv = flat[bias_off + (long)mods[tid >> 3] * chunk + (tid & 7)];
-      if constexpr (F16) bv -= 1024.f * in_scale * hcorr[mods[tid >> 3] * 8 + (tid & 7)];
-    }
-    bias_s[tid] = bv;
-  }
-  __syncthreads();
-
   // compile-time column-tile count per instantiation (see conv_wgrad_slab)
   auto run = [&](auto ncc) {
     constexpr int NC = decltype(ncc)::value;
@@ -212,7 +195,29 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
         }
       }
     };
-    load_tile(rfirst);
+    // uint8 first layer: the first tile's A loads do not depend on LDS, so they are issued before the
+    // weight staging and its barrier and their latency overlaps the Wc gather (nct is uniform over the
+    // block, so every thread reaches the barrier).  Not for the bf16 layers: at their 128-VGPR budget
+    // the longer live range spills, and that build wrote wrong ReLU bits for conv2
+    // (scripts/diag_conv_bits.py, docs/PERF.md).
+    if constexpr (G::U8) load_tile(rfirst);
+    for (int i = tid; i < NC * 16 * G::KC; i += 256) {
+      const int col = i / G::KC, kc = i - col * G::KC;
+      const int slot = col >> 3;
+      s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (slot < cnt) v = *reinterpret_cast<const s8v*>(Wc + ((long)(mods[slot] * 8 + (col & 7))) * G::KP + kc * 8);
+      *reinterpret_cast<s8v*>(Ws + col * KPs + kc * 8) = v;
+    }
+    if (tid < NCT * 16) {
+      float bv = 0.f;
+      if ((tid >> 3) < cnt) {
+        bv = flat[bias_off + (long)mods[tid >> 3] * chunk + (tid & 7)];
+        if constexpr (F16) bv -= 1024.f * in_scale * hcorr[mods[tid >> 3] * 8 + (tid & 7)];
+      }
+      bias_s[tid] = bv;
+    }
+    __syncthreads();
+    if constexpr (!G::U8) load_tile(rfirst);
     for (int tile = 0; tile < FF_ROWS / 128; ++tile) {
       const int rbase = rfirst + tile * 128;
       if (rbase >= Rtot) break;
