@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--ring", action="store_true", help="frame ring (single-frame writes) instead of packed stacks")
     ap.add_argument("--preset", default="pong")
+    ap.add_argument("--env", default=None, help="train this task of the preset's suite instead of its first task")
     ap.add_argument("--kernel-opt", action="append", default=[],
                     help="kernel switch NAME=VALUE (fast_conv_set_*), for A/B measurements")
     ap.add_argument("--ga-backend", default="device", choices=["device", "host"],
@@ -118,6 +119,9 @@ def main():
             (getattr(lib, k) if hasattr(lib, k) and "_set_" in k else getattr(lib, "fast_conv_set_" + k))(int(v))
     ctx = init_distributed()
     cfg = preset(args.preset)
+    if args.env:
+        cfg.env = args.env
+        cfg.tasks = [args.env] + [t for t in cfg.tasks if t != args.env]
     cfg.paths = args.paths
     cfg.envs_per_path = args.envs
     cfg.a2c.t_max = args.tmax
@@ -161,8 +165,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_STEPS_PER_SEC, 1),
-            "dtype": "bf16",
-            "data": "synthetic: on-device Atari-style Pong simulator (210x160 RGB -> gray 160x120 x4 stack), "
+            "dtype": tr.compute_dtype,
+            "data": f"synthetic: on-device Atari-style {cfg.tasks[0]} simulator (210x160 RGB -> gray 160x120 x4 stack), "
                     "random-init weights",
             "config": {
                 "model": f"PathNet {cfg.net.L} layers (3 conv 8-map + 2 fc 256) x M={cfg.net.M} modules, N={cfg.net.N}, "

@@ -71,6 +71,9 @@ class PathNetTrainer:
             device = self.ctx.device
         self.device = torch.device(device)
         self.backend = resolve_backend(cfg.backend, self.device)
+        # the torch backend always computes in fp32; the HIP engine uses bf16 (fp16 for the uint8 conv1
+        # operands) MFMA with fp32 accumulation and fp32 master weights
+        self.compute_dtype = cfg.compute_dtype if self.backend == "hip" else "fp32"
         self.logger = logger
         net = cfg.net
         self.P = cfg.paths

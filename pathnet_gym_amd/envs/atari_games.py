@@ -24,6 +24,12 @@ state in place, so the engine captures it in the rollout hipGraph like the
 HIP envs.  On the GPU the frame is not rendered by torch at all: each game
 describes its scene as a rectangle list (``Scene``) that one fused kernel
 rasterises, preprocesses and pushes into the frame stack.
+
+With ``backend="hip"`` on a GPU the game logic itself runs in ``csrc/games.hip``
+(one thread per env: physics sub-frames, reward/done, auto-reset and the scene),
+so an agent step is two launches; the torch code above stays the bit-exact
+oracle (``tests/test_games_hip.py``).  The packed int32 kernel state is then the
+source of truth and ``sync_from_device()`` refreshes the torch state tensors.
 """
 from __future__ import annotations
 
@@ -83,6 +89,10 @@ class PixelGameVec(VecEnv):
     graph_safe = True          # no host syncs / host->device copies inside a step; state updated in place
     n_actions = 4
     max_steps = 27000
+    HIP_GAME = None            # game id of csrc/games.hip (None: torch physics + HIP rasteriser)
+    # state fields in csrc/games.hip order ("i": one int, "vec": [N, k] ints, "mask": [N, k] bools as one
+    # bitmask int, "bits": bool grid bit-packed into 32-bit words); counter/steps/epret follow
+    HIP_FIELDS: tuple = ()
 
     def __init__(self, num_envs: int, device="cpu", seed: int = 0, frameskip: int = 4, gray: str = "rgb",
                  backend: str = "torch", no_op_max: int = 7):
@@ -111,13 +121,101 @@ class PixelGameVec(VecEnv):
         self._persist = {k: v for k, v in vars(self).items()
                          if isinstance(v, torch.Tensor) and v.dim() >= 1 and v.shape[0] == num_envs
                          and k not in ("obs", "env_id")}
+        self._hip = False
         self.seed(seed)
+        if self.backend == "hip" and self.device.type == "cuda" and self.HIP_GAME is not None:
+            self._hip_setup()
 
     # -- helpers -------------------------------------------------------------
     def seed(self, seed: int):
         self.seed_int = seed & 0xFFFFFFFF
         self._seed = torch.tensor(self.seed_int, dtype=torch.int64, device=self.device)
         self.counter.zero_()
+        if self._hip:
+            self._st32[:, self._st32.shape[1] - 3] = 0
+
+    # -- HIP game logic (csrc/games.hip) ------------------------------------------------
+    def _fields(self):
+        return tuple(self.HIP_FIELDS) + (("counter", "i"), ("steps", "i"), ("epret", "i"))
+
+    def _hip_pack(self) -> torch.Tensor:
+        """torch state -> int32 [N, NS] kernel state (bit-packed grids, two's-complement words)."""
+        N = self.num_envs
+        cols = []
+        for name, kind in self._fields():
+            t = getattr(self, name).reshape(N, -1).long()
+            if kind in ("i", "vec"):
+                cols.append(t)
+            elif kind == "mask":
+                cols.append((t << torch.arange(t.shape[1], device=self.device)).sum(1, keepdim=True))
+            else:                                           # bits
+                n = t.shape[1]
+                k = (n + 31) // 32
+                t = torch.nn.functional.pad(t, (0, 32 * k - n)).view(N, k, 32)
+                cols.append((t << torch.arange(32, device=self.device)).sum(2))
+        v = torch.cat(cols, 1) & 0xFFFFFFFF
+        return torch.where(v >= 2 ** 31, v - 2 ** 32, v).to(torch.int32).contiguous()
+
+    def sync_from_device(self):
+        """Refresh the torch state tensors from the HIP kernel state (no-op on the torch path)."""
+        if not self._hip:
+            return
+        N = self.num_envs
+        v = self._st32.long()
+        j = 0
+        for name, kind in self._fields():
+            t = getattr(self, name)
+            if kind == "i":
+                new = v[:, j]
+                j += 1
+            elif kind == "vec":
+                k = t.reshape(N, -1).shape[1]
+                new = v[:, j:j + k]
+                j += k
+            elif kind == "mask":
+                k = t.reshape(N, -1).shape[1]
+                new = (v[:, j:j + 1] >> torch.arange(k, device=self.device)) & 1
+                j += 1
+            else:
+                n = t.reshape(N, -1).shape[1]
+                k = (n + 31) // 32
+                w = v[:, j:j + k] & 0xFFFFFFFF
+                new = ((w[:, :, None] >> torch.arange(32, device=self.device)) & 1).reshape(N, 32 * k)[:, :n]
+                j += k
+            if name == "counter":
+                new = new & 0xFFFFFFFF
+            t.copy_(new.reshape(t.shape).to(t.dtype))
+
+    def _hip_setup(self):
+        from ..ops import envs as henv
+        from .pong import gray_weights
+        ns, nr = henv.game_layout(self.HIP_GAME)
+        self._st32 = self._hip_pack()
+        if self._st32.shape[1] != ns:
+            raise RuntimeError(f"{self.HIP_GAME}: HIP_FIELDS pack to {self._st32.shape[1]} ints, kernel expects {ns}")
+        colors = self.scene().colors
+        if len(colors) != nr:
+            raise RuntimeError(f"{self.HIP_GAME}: scene has {len(colors)} rectangles, kernel writes {nr}")
+        wr, wg, wb = gray_weights(self.gray)
+        lum = lambda c: (c[0] * wr + c[1] * wg + c[2] * wb + 8192) >> 14      # noqa: E731  cv2 fixed-point luma
+        self._gray_tab = torch.tensor([lum(c) for c in colors], dtype=torch.uint8, device=self.device)
+        self._bg_gray = int(lum(BG))
+        N = self.num_envs
+        self._rects = torch.zeros(N, nr, 4, dtype=torch.int16, device=self.device)
+        self._tab32 = self.tables.to(torch.int32).contiguous()
+        self._rw = torch.zeros(N, dtype=torch.float32, device=self.device)
+        self._dn = torch.zeros(N, dtype=torch.uint8, device=self.device)
+        self._ep = torch.zeros(N, dtype=torch.float32, device=self.device)
+        self._hip = True
+
+    def _hip_run(self, actions, mask, reward, done, epret):
+        from ..ops import envs as henv
+        henv.game_step(self.HIP_GAME, self._st32, actions, mask, self.num_actions, self.seed_int, self.frameskip,
+                       int(self.max_episode_steps), reward, done, epret, self._rects)
+
+    def _hip_push(self, obs_in, obs_out, reset_u8):
+        from ..ops import envs as henv
+        henv.rects16_stack_push(self._rects, self._gray_tab, self._bg_gray, obs_in, obs_out, reset_u8, self._tab32)
 
     def _commit(self):
         for k, p in self._persist.items():
@@ -186,6 +284,13 @@ class PixelGameVec(VecEnv):
         return self.obs.clone()
 
     def reset_where(self, mask):
+        if self._hip:
+            m8 = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            self._hip_run(None, m8, self._rw, self._dn, self._ep)
+            out = torch.empty_like(self.obs)
+            self._hip_push(self.obs, out, m8)
+            self.obs = out
+            return
         self.reset_state(mask)
         self.steps = torch.where(mask, torch.zeros_like(self.steps), self.steps)
         self.epret = torch.where(mask, torch.zeros_like(self.epret), self.epret)
@@ -229,13 +334,35 @@ class PixelGameVec(VecEnv):
         return reward, done, ep_return
 
     def step(self, actions):
+        if self._hip:
+            a = actions.to(device=self.device, dtype=torch.int32).contiguous()
+            self._hip_run(a, None, self._rw, self._dn, self._ep)
+            out = torch.empty_like(self.obs)
+            self._hip_push(self.obs, out, self._dn)
+            self.obs = out
+            return out.clone(), self._rw.clone(), self._dn.bool(), {"episode_return": self._ep.clone()}
         reward, done, ep_return = self._advance(actions)
         self.obs = self._push(self.obs, done)
         return self.obs.clone(), reward.float(), done, {"episode_return": ep_return}
 
     def step_into(self, actions, obs_in, obs_out, reward, done, epret):
         """Engine hook: torch physics + render, then (backend 'hip') ONE fused kernel that preprocesses the
-        frame and pushes it from the engine's obs slot t straight into slot t+1."""
+        frame and pushes it from the engine's obs slot t straight into slot t+1.  With the HIP game logic
+        the whole step is two launches writing the engine's reward/done/return rows directly."""
+        if self._hip:
+            a = actions if actions.dtype == torch.int32 and actions.is_contiguous() else \
+                actions.to(torch.int32).contiguous()
+            direct = (reward.dtype == torch.float32 and done.dtype == torch.uint8 and epret.dtype == torch.float32
+                      and reward.is_contiguous() and done.is_contiguous() and epret.is_contiguous())
+            rw, dn, ep = (reward, done, epret) if direct else (self._rw, self._dn, self._ep)
+            self._hip_run(a, None, rw, dn, ep)
+            self._hip_push(obs_in.view(self.obs.shape), obs_out.view(self.obs.shape), dn.reshape(-1))
+            if not direct:
+                reward.copy_(rw.view(reward.shape))
+                done.copy_(dn.view(done.shape).to(done.dtype))
+                epret.copy_(ep.view(epret.shape))
+            self.obs = obs_out.view(self.obs.shape)
+            return
         r, d, ep = self._advance(actions)
         self._push(obs_in.view(self.obs.shape), d, obs_out.view(self.obs.shape))
         self.obs = obs_out.view(self.obs.shape)
@@ -249,6 +376,9 @@ class BreakoutVec(PixelGameVec):
     id = "Breakout"
     n_actions = 4
     reward_threshold = 30.0
+    HIP_GAME = "Breakout"
+    HIP_FIELDS = (("px", "i"), ("bx", "i"), ("by", "i"), ("vx", "i"), ("vy", "i"), ("inplay", "i"), ("lives", "i"),
+                  ("bricks", "bits"))
     U = 16
     ROWS, COLS = 6, 18
     BRICK_Y0, BRICK_H, BRICK_W, BRICK_X0 = 57, 6, 8, 8
@@ -342,6 +472,9 @@ class SpaceInvadersVec(PixelGameVec):
     id = "SpaceInvaders"
     n_actions = 6
     reward_threshold = 300.0
+    HIP_GAME = "SpaceInvaders"
+    HIP_FIELDS = (("fx", "i"), ("fy", "i"), ("fdir", "i"), ("tick", "i"), ("px", "i"), ("lives", "i"), ("sx", "i"),
+                  ("sy", "i"), ("shot", "i"), ("bxp", "i"), ("byp", "i"), ("bomb", "i"), ("alive", "bits"))
     AR, AC = 6, 6
     ROW_REWARD = (30, 25, 20, 15, 10, 5)
 
@@ -457,6 +590,9 @@ class AlienVec(PixelGameVec):
     id = "Alien"
     n_actions = 18
     reward_threshold = 400.0
+    HIP_GAME = "Alien"
+    HIP_FIELDS = (("py", "i"), ("px", "i"), ("ay", "vec"), ("ax", "vec"), ("lives", "i"), ("tick", "i"),
+                  ("dots", "bits"))
     CW, CH, Y0, X0 = 12, 16, 20, 2
     NA = 3
     MOVE_EVERY = 2
@@ -558,6 +694,7 @@ class MsPacmanVec(AlienVec):
     id = "MsPacman"
     n_actions = 9
     reward_threshold = 500.0
+    HIP_GAME = "MsPacman"
 
 
 # ===========================================================================
@@ -565,6 +702,9 @@ class CentipedeVec(PixelGameVec):
     id = "Centipede"
     n_actions = 18
     reward_threshold = 3000.0
+    HIP_GAME = "Centipede"
+    HIP_FIELDS = (("mush", "bits"), ("sy", "vec"), ("sx", "vec"), ("sdir", "vec"), ("salive", "mask"), ("px", "i"),
+                  ("shot", "i"), ("shx", "i"), ("shy", "i"), ("lives", "i"), ("tick", "i"))
     NS = 10
     GH, GW = 20, 16          # mushroom grid (8 px rows x 10 px cols in the field rows 20..180)
 

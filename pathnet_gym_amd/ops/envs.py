@@ -8,6 +8,8 @@ Two entry points per env:
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -172,3 +174,50 @@ def rects_stack_push(geom: torch.Tensor, colors, bg, obs_in: torch.Tensor, obs_o
     r8 = None if reset is None else _lib.check(reset.to(torch.uint8).contiguous(), torch.uint8, numel=N, name="reset")
     _lib.call("launch_rects_stack_push", g16.data_ptr(), cache[key].data_ptr(), R, int(lum(bg)), obs_in.data_ptr(),
               obs_out.data_ptr(), _lib.ptr(r8), tab.data_ptr(), N, _lib.stream())
+
+
+# ------------------------------------------------------------------ synthetic Atari-style games (csrc/games.hip)
+GAME_IDS = {"Breakout": 0, "SpaceInvaders": 1, "Alien": 2, "MsPacman": 3, "Centipede": 4}
+
+
+def game_layout(game: str):
+    """(ints of state per env, rectangles per scene) of a HIP game."""
+    ns, nr = ctypes.c_int(0), ctypes.c_int(0)
+    _lib.call("game_layout", GAME_IDS[game], ctypes.byref(ns), ctypes.byref(nr))
+    return ns.value, nr.value
+
+
+def game_step(game: str, state: torch.Tensor, actions, mask, n_actions: int, seed: int, frameskip: int,
+              max_steps: int, reward: torch.Tensor, done: torch.Tensor, epret: torch.Tensor, rects: torch.Tensor):
+    """One launch: agent step of every env (``actions`` int32 [N]) or, with ``mask`` (uint8 [N]) instead,
+    ``reset_where``; writes reward/done/episode-return rows and the int16 scene [N, R, 4]."""
+    N = state.shape[0]
+    ns, nr = game_layout(game)
+    _lib.check(state, torch.int32, (N, ns), name="state")
+    _lib.check(rects, torch.int16, (N, nr, 4), name="rects")
+    _lib.check(reward, torch.float32, numel=N, name="reward")
+    _lib.check(done, torch.uint8, numel=N, name="done")
+    _lib.check(epret, torch.float32, numel=N, name="epret")
+    if actions is not None:
+        _lib.check(actions, torch.int32, (N,), name="actions")
+    if mask is not None:
+        _lib.check(mask, torch.uint8, (N,), name="mask")
+    _lib.call("launch_game_step", GAME_IDS[game], state.data_ptr(), _lib.ptr(actions), _lib.ptr(mask),
+              0 if mask is None else 1, n_actions, N, seed & 0xFFFFFFFF, frameskip, max_steps, reward.data_ptr(),
+              done.data_ptr(), epret.data_ptr(), rects.data_ptr(), _lib.stream())
+
+
+def rects16_stack_push(rects: torch.Tensor, gray_tab: torch.Tensor, bg_gray: int, obs_in: torch.Tensor,
+                       obs_out: torch.Tensor, reset, tables32: torch.Tensor):
+    """``rects_stack_push`` for a scene that is already int16 [N, R, 4] with a precomputed per-rectangle gray
+    table (the HIP games write their scene that way; no conversions, capturable)."""
+    N, R = rects.shape[0], rects.shape[1]
+    _lib.check(rects, torch.int16, (N, R, 4), name="rects")
+    _lib.check(gray_tab, torch.uint8, (R,), name="gray_tab")
+    _lib.check(obs_out, torch.uint8, numel=N * 160 * 120 * 4, name="obs_out")
+    _lib.check(obs_in, torch.uint8, numel=N * 160 * 120 * 4, name="obs_in")
+    _lib.check(tables32, torch.int32, name="tables")
+    if reset is not None:
+        _lib.check(reset, torch.uint8, numel=N, name="reset")
+    _lib.call("launch_rects_stack_push", rects.data_ptr(), gray_tab.data_ptr(), R, int(bg_gray), obs_in.data_ptr(),
+              obs_out.data_ptr(), _lib.ptr(reset), tables32.data_ptr(), N, _lib.stream())

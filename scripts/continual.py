@@ -38,8 +38,8 @@ def build_cfg(args, tasks):
     cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = args.paths, args.envs, args.tmax
     cfg.ga.backend = "device"
     cfg.ga.concurrent_tournaments = max(1, args.paths // 16)
-    cfg.steps_per_task = args.frames
-    cfg.a2c.max_time_step = args.frames
+    cfg.steps_per_task = 2 * args.frames          # task switches are driven by this script, never automatic
+    cfg.a2c.max_time_step = 2 * args.frames
     cfg.a2c.lr_anneal = "none"
     cfg.seed = cfg.ga.seed = args.seed
     return cfg
@@ -71,7 +71,8 @@ def train_task(tr, ti, args, label):
     ts = time.time()
     last = ts
     solved = None
-    while tr.global_step - tr.task_start_step < args.frames:
+    budget = args.frames_per_task[name]
+    while tr.global_step - tr.task_start_step < budget:
         st = tr.update()
         n += 1
         if not math.isnan(st.mean_return):
@@ -88,7 +89,7 @@ def train_task(tr, ti, args, label):
             curve.append(rec)
             print(json.dumps(rec), flush=True)
     tr.flush()
-    return {"task": name, "updates": n, "seconds": round(time.time() - ts, 1), "frames": args.frames,
+    return {"task": name, "updates": n, "seconds": round(time.time() - ts, 1), "frames": budget,
             "threshold": thr, "best_winner": best if math.isfinite(best) else None, "final_mean_return": ema, "solved": solved is not None,
             "generations_to_solve": solved and solved["generation"], "frames_to_solve": solved and solved["frames"],
             "generations": tr.pop.generation - tr._task_gen0, "curve": curve}
@@ -97,7 +98,8 @@ def train_task(tr, ti, args, label):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tasks", default="Pong,Breakout,SpaceInvaders,Alien")
-    ap.add_argument("--frames", type=int, default=25_000_000, help="agent frames per task")
+    ap.add_argument("--frames", default="25000000",
+                    help="agent frames per task: one number, or one per task (comma-separated)")
     ap.add_argument("--paths", type=int, default=16)
     ap.add_argument("--envs", type=int, default=16)
     ap.add_argument("--tmax", type=int, default=5)
@@ -120,6 +122,9 @@ def main():
         _build.build()
     dev = "cuda" if torch.cuda.is_available() else "cpu"
     tasks = [t.strip() for t in args.tasks.split(",")]
+    fr = [int(float(x)) for x in str(args.frames).split(",")]
+    args.frames_per_task = {t: fr[min(i, len(fr) - 1)] for i, t in enumerate(tasks)}
+    args.frames = max(fr)
     cfg = build_cfg(args, tasks)
     tr = PathNetTrainer(cfg, device=dev)
     t0 = time.time()
@@ -161,11 +166,11 @@ def main():
             del ctr
             torch.cuda.empty_cache() if dev == "cuda" else None
     out = {"experiment": "continual", "reference": "doom_pathnet.py:274-293, aliencentipede.txt:55-93",
-           "tasks": tasks, "frames_per_task": args.frames, "n_gpus": 1,
+           "tasks": tasks, "frames_per_task": args.frames_per_task, "n_gpus": 1,
            "config": {"paths": args.paths, "envs_per_path": args.envs, "t_max": args.tmax, "N": args.N,
                       "M": cfg.net.M, "B": cfg.ga.B, "trunk_scale": cfg.net.trunk_scale, "lr": cfg.a2c.lr,
                       "per_task_heads": True, "freeze_union": cfg.ga.freeze_union, "seed": args.seed,
-                      "env_reduction": cfg.a2c.env_reduction, "dtype": cfg.compute_dtype},
+                      "env_reduction": cfg.a2c.env_reduction, "dtype": tr.compute_dtype},
            "per_task": per_task, "scratch_control": controls, "seconds": round(time.time() - t0, 1)}
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     with open(args.out, "w") as f:

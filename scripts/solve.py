@@ -171,7 +171,7 @@ def main():
                           "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
                           "rmsp_epsilon": cfg.a2c.rmsp_epsilon,
                           "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
-                          "ga": not args.no_ga, "same_path": args.same_path, "dtype": cfg.compute_dtype}}
+                          "ga": not args.no_ga, "same_path": args.same_path, "dtype": tr.compute_dtype}}
         out["config"]["seed"] = cfg.seed
         print(json.dumps(out), flush=True)
         if args.out:
