@@ -195,12 +195,37 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
         }
       }
     };
+    // affine uint8 layer (conv1 on packed stacks): per-tile row addresses only, fragments loaded per k-step
+    constexpr bool AFF8 = !RING && G::U8 && G::KW * G::CIN == 32 && G::K == G::KP;
+    using El = typename std::conditional<G::U8, uint8_t, bf16_t>::type;
+    const El* asrc[2];
+    // rows past the end read row 0 of the path's first sample instead: their 16-row halves are never stored
+    auto aff_addr = [&]() {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool va = ait[i].r < Rtot;
+        const int oh = ait[i].pos / G::WO, ow = ait[i].pos - oh * G::WO;
+        const long xb = va ? rowit_sample(ait[i], p, E, PE, t0) * (long)G::IN_ELEMS +
+                                 (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN
+                           : rowit_sample(RowIt{0, 0, 0, 0}, p, E, PE, t0) * (long)G::IN_ELEMS;
+        asrc[i] = reinterpret_cast<const El*>(X) + xb + G::koff(grp);
+        rowit_adv(ait[i], 128, E, G::HOWO);
+      }
+    };
     // uint8 first layer: the first tile's A loads do not depend on LDS, so they are issued before the
     // weight staging and its barrier and their latency overlaps the Wc gather (nct is uniform over the
     // block, so every thread reaches the barrier).  Not for the bf16 layers: at their 128-VGPR budget
     // the longer live range spills, and that build wrote wrong ReLU bits for conv2
     // (scripts/diag_conv_bits.py, docs/PERF.md).
-    if constexpr (G::U8) load_tile(rfirst);
+    if constexpr (AFF8) {
+      aff_addr();
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) araw[i][kk] = *reinterpret_cast<const ARaw*>(asrc[i] + kk * G::WIN * G::CIN);
+    } else if constexpr (G::U8) {
+      load_tile(rfirst);
+    }
     for (int i = tid; i < NC * 16 * G::KC; i += 256) {
       const int col = i / G::KC, kc = i - col * G::KC;
       const int slot = col >> 3;
@@ -218,80 +243,178 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
     }
     __syncthreads();
     if constexpr (!G::U8) load_tile(rfirst);
-    for (int tile = 0; tile < FF_ROWS / 128; ++tile) {
-      const int rbase = rfirst + tile * 128;
-      if (rbase >= Rtot) break;
-      // raw fragments of this tile; the uint8 -> bf16 conversion happens per k-step next to its
-      // MFMAs (holding all converted fragments cost 64 VGPRs and capped occupancy at 2 waves)
-      ARaw cur[2][NK];
+    if constexpr (AFF8) {
+      // one 32-row tile; RELOAD (AFF8 only): the next tile's fragments are loaded into the same registers
+      auto do_tile = [&](const int tile, const int rbase, auto reload_c) {
+        constexpr bool RELOAD = decltype(reload_c)::value;
+        f4v acc[2][NC];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int kk = 0; kk < NK; ++kk) cur[i][kk] = araw[i][kk];
-      if (tile + 1 < FF_ROWS / 128) load_tile(rbase + 128);     // next tile in flight during MFMAs + epilogue
-      f4v acc[2][NC];
+          for (int ct = 0; ct < NC; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
+        // MFMAs of k-step kk on this tile's (converted) fragments
+        auto kstep = [&](const s8v& a0, const s8v& a1, int kk) {
+          const int kc = kk * 4 + grp;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int ct = 0; ct < NC; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        const int kc = kk * 4 + grp;
-        s8v a0, a1;
-        if constexpr (F16) {
-          a0 = u8x8_to_f16off(cur[0][kk]);
-          a1 = u8x8_to_f16off(cur[1][kk]);
-        } else if constexpr (G::U8) {
-          a0 = u8x8_to_bf16(cur[0][kk]);
-          a1 = u8x8_to_bf16(cur[1][kk]);
-        } else {
-          a0 = cur[0][kk];
-          a1 = cur[1][kk];
-        }
-#pragma unroll
-        for (int ct = 0; ct < NC; ++ct) {
-          const s8v b = *reinterpret_cast<const s8v*>(Ws + (ct * 16 + c16) * KPs + kc * 8);
-          if constexpr (F16) {
-            acc[0][ct] = mfma16_f16(a0, b, acc[0][ct]);
-            acc[1][ct] = mfma16_f16(a1, b, acc[1][ct]);
-          } else {
-            acc[0][ct] = mfma16(a0, b, acc[0][ct]);
-            acc[1][ct] = mfma16(a1, b, acc[1][ct]);
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r16 = rbase + i * 16;
-        const RowIt e0 = eit[i];
-        rowit_adv(eit[i], 128, E, G::HOWO);
-        if (r16 >= Rtot) continue;
-        float sum[4] = {0.f, 0.f, 0.f, 0.f};
-        const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
-#pragma unroll
-        for (int ct = 0; ct < NC; ++ct) {
-          {
-            const int slot = ct * 2 + h;
-            const bool sv = slot < cnt;
-            const float bb = bias_s[ct * 16 + c16];
-            uint32_t word = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float v = acc[i][ct][r] * in_scale + bb;
-              const bool pos = sv && v > 0.f;
-              sum[r] += pos ? v : 0.f;
-              const uint64_t bal = __ballot(pos);
-              word |= (uint32_t)((bal >> (16 * q + 8 * h)) & 0xFFull) << (8 * r);
+          for (int ct = 0; ct < NC; ++ct) {
+            const s8v b = *reinterpret_cast<const s8v*>(Ws + (ct * 16 + c16) * KPs + kc * 8);
+            if constexpr (F16) {
+              acc[0][ct] = mfma16_f16(a0, b, acc[0][ct]);
+              acc[1][ct] = mfma16_f16(a1, b, acc[1][ct]);
+            } else {
+              acc[0][ct] = mfma16(a0, b, acc[0][ct]);
+              acc[1][ct] = mfma16(a1, b, acc[1][ct]);
             }
-            if (ch == 0 && sv) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
+          }
+        };
+        // ONE register set: k-step kk's raw fragments are converted, then the same registers are
+        // reloaded with the NEXT tile's k-step kk before this step's MFMAs issue -- the loads stay in
+        // flight for the rest of the k loop and the epilogue, and no fragment is ever copied (the
+        // two-set pipeline below costs ~2 v_mov per fragment dword per tile)
+        if constexpr (RELOAD) aff_addr();
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          s8v a0, a1;
+          if constexpr (F16) {
+            a0 = u8x8_to_f16off(araw[0][kk]);
+            a1 = u8x8_to_f16off(araw[1][kk]);
+          } else {
+            a0 = u8x8_to_bf16(araw[0][kk]);
+            a1 = u8x8_to_bf16(araw[1][kk]);
+          }
+          if constexpr (RELOAD) {
+            araw[0][kk] = *reinterpret_cast<const ARaw*>(asrc[0] + kk * G::WIN * G::CIN);
+            araw[1][kk] = *reinterpret_cast<const ARaw*>(asrc[1] + kk * G::WIN * G::CIN);
+          }
+          kstep(a0, a1, kk);
+          // keep program order per k-step: the scheduler otherwise hoists every conversion to the top of
+          // the tile (one wait for all 16 fragments) and sinks every reload to its end
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r16 = rbase + i * 16;
+          const RowIt e0 = eit[i];
+          rowit_adv(eit[i], 128, E, G::HOWO);
+          if (r16 >= Rtot) continue;
+          float sum[4] = {0.f, 0.f, 0.f, 0.f};
+          const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) {
+            {
+              const int slot = ct * 2 + h;
+              const bool sv = slot < cnt;
+              const float bb = bias_s[ct * 16 + c16];
+              uint32_t word = 0;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float v = acc[i][ct][r] * in_scale + bb;
+                const bool pos = sv && v > 0.f;
+                sum[r] += pos ? v : 0.f;
+                const uint64_t bal = __ballot(pos);
+                word |= (uint32_t)((bal >> (16 * q + 8 * h)) & 0xFFull) << (8 * r);
+              }
+              if (ch == 0 && sv) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
+          if (h == 0) {
+            // rows 4q..4q+3 of this tile are consecutive global rows (E*HOWO % 16 == 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Y[(grow4 + r) * 8 + ch] = f2bf(sum[r] * out_scale);
+          }
+        }
+      };
+      // the reloading body runs while a next tile exists; the last tile is peeled (no reloads), so the
+      // fragment registers carry no conditional value across iterations (that cost a copy of the set)
+      // fully unrolled (NT - 1 reloading tiles): a rolled loop's back-edge made the wait-count pass drain
+      // every load in flight at the end of each tile
+      int tile = 0;
+#pragma unroll
+      for (; tile + 1 < FF_ROWS / 128; ++tile) {
+        const int rbase = rfirst + tile * 128;
+        if (rbase + 128 >= Rtot) break;
+        do_tile(tile, rbase, std::true_type{});
+      }
+      const int rbase = rfirst + tile * 128;
+      if (rbase < Rtot) do_tile(tile, rbase, std::false_type{});
+    } else {
+      for (int tile = 0; tile < FF_ROWS / 128; ++tile) {
+        const int rbase = rfirst + tile * 128;
+        if (rbase >= Rtot) break;
+        // raw fragments of this tile; the uint8 -> bf16 conversion happens per k-step next to its
+        // MFMAs (holding all converted fragments cost 64 VGPRs and capped occupancy at 2 waves)
+        ARaw cur[2][NK];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) cur[i][kk] = araw[i][kk];
+        if (tile + 1 < FF_ROWS / 128) load_tile(rbase + 128);     // next tile in flight during MFMAs + epilogue
+        f4v acc[2][NC];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const int kc = kk * 4 + grp;
+          s8v a0, a1;
+          if constexpr (F16) {
+            a0 = u8x8_to_f16off(cur[0][kk]);
+            a1 = u8x8_to_f16off(cur[1][kk]);
+          } else if constexpr (G::U8) {
+            a0 = u8x8_to_bf16(cur[0][kk]);
+            a1 = u8x8_to_bf16(cur[1][kk]);
+          } else {
+            a0 = cur[0][kk];
+            a1 = cur[1][kk];
+          }
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) {
+            const s8v b = *reinterpret_cast<const s8v*>(Ws + (ct * 16 + c16) * KPs + kc * 8);
+            if constexpr (F16) {
+              acc[0][ct] = mfma16_f16(a0, b, acc[0][ct]);
+              acc[1][ct] = mfma16_f16(a1, b, acc[1][ct]);
+            } else {
+              acc[0][ct] = mfma16(a0, b, acc[0][ct]);
+              acc[1][ct] = mfma16(a1, b, acc[1][ct]);
+            }
           }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
-        if (h == 0) {
-          // rows 4q..4q+3 of this tile are consecutive global rows (E*HOWO % 16 == 0)
+        for (int i = 0; i < 2; ++i) {
+          const int r16 = rbase + i * 16;
+          const RowIt e0 = eit[i];
+          rowit_adv(eit[i], 128, E, G::HOWO);
+          if (r16 >= Rtot) continue;
+          float sum[4] = {0.f, 0.f, 0.f, 0.f};
+          const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) Y[(grow4 + r) * 8 + ch] = f2bf(sum[r] * out_scale);
+          for (int ct = 0; ct < NC; ++ct) {
+            {
+              const int slot = ct * 2 + h;
+              const bool sv = slot < cnt;
+              const float bb = bias_s[ct * 16 + c16];
+              uint32_t word = 0;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float v = acc[i][ct][r] * in_scale + bb;
+                const bool pos = sv && v > 0.f;
+                sum[r] += pos ? v : 0.f;
+                const uint64_t bal = __ballot(pos);
+                word |= (uint32_t)((bal >> (16 * q + 8 * h)) & 0xFFull) << (8 * r);
+              }
+              if (ch == 0 && sv) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
+          if (h == 0) {
+            // rows 4q..4q+3 of this tile are consecutive global rows (E*HOWO % 16 == 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Y[(grow4 + r) * 8 + ch] = f2bf(sum[r] * out_scale);
+          }
         }
       }
     }

@@ -287,7 +287,10 @@ __global__ __launch_bounds__(256) void fc_fwd_kernel(
 // D = k-steps of A/B fragments in flight per wave.  The grid is one workgroup per (path, 64
 // columns) -- one wave per SIMD -- so registers are free and a deep prefetch ring cuts the
 // latency chain of the 44-step K loop (fc1: K = 1408) by D.
-template <int RT, int D>
+// NKS > 0: compile-time k-step count (fc1 / fc2 of the pixel trunk): the K loop is fully unrolled, so no
+// loop back-edge makes the wait-count pass drain the register ring (it emitted vmcnt(0) at the back-edge
+// of the rolled loop, which serialised one memory latency per D k-steps).
+template <int RT, int D, int NKS = 0>
 __global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
     const bf16_t* __restrict__ X, int ldx, bf16_t* __restrict__ Y, uint16_t* __restrict__ bits,
     const bf16_t* __restrict__ Wc, const float* __restrict__ flat, long bias_off, int chunk,
@@ -336,37 +339,52 @@ __global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
     s8v an[D][RT], bn[D][4];
+    // rows past Rtot read a valid row (their outputs are never stored); K padding (K < KP) reads zeros
     auto load = [&](s8v (&ad)[RT], s8v (&bd)[4], int kk) {
       const int k0 = kk + 8 * grp;
 #pragma unroll
       for (int i = 0; i < RT; ++i) {
-        ad[i] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
-        if (xv[i] && k0 < K) ad[i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+        if (K == KP) {
+          ad[i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+        } else {
+          ad[i] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+          if (k0 < K) ad[i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+        }
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) bd[j] = *reinterpret_cast<const s8v*>(Wm + (long)j * 16 * KP + kk);
     };
+    auto mma = [&](const s8v (&ad)[RT], const s8v (&bd)[4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < RT; ++i) acc[i][j] = mfma16(ad[i], bd[j], acc[i][j]);
+    };
+    // D-deep register ring WITHOUT copies: slot d's MFMAs issue, then the same registers are reloaded
+    // with k-step s + d + D.  The main loop reloads unconditionally (no loop-carried conditional value,
+    // which made the compiler copy the whole ring every step); the last < 2D k-steps are peeled.
+    const int nks = NKS > 0 ? NKS : KP / 32;
 #pragma unroll
     for (int d = 0; d < D; ++d)
-      if (d * 32 < KP) load(an[d], bn[d], d * 32);
-    for (int kk0 = 0; kk0 < KP; kk0 += 32 * D) {
+      if (d < nks) load(an[d], bn[d], d * 32);
+    int s = 0;
+#pragma unroll
+    for (; s + 2 * D <= nks; s += D) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        const int kk = kk0 + d * 32;
-        if (kk < KP) {
-          s8v ac[RT], bc[4];
-#pragma unroll
-          for (int i = 0; i < RT; ++i) ac[i] = an[d][i];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) bc[j] = bn[d][j];
-          if (kk + 32 * D < KP) load(an[d], bn[d], kk + 32 * D);
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int i = 0; i < RT; ++i) acc[i][j] = mfma16(ac[i], bc[j], acc[i][j]);
-        }
+        mma(an[d], bn[d]);
+        load(an[d], bn[d], (s + d + D) * 32);
       }
     }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (s + d < nks) {
+        mma(an[d], bn[d]);
+        if (s + d + D < nks) load(an[d], bn[d], (s + d + D) * 32);
+      }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (s + D + d < nks) mma(an[d], bn[d]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float bb = flat[bias_off + (long)mod * chunk + col0 + j * 16 + c16];
@@ -445,14 +463,19 @@ int launch_fc_fwd(const void* X, int ldx, void* Y, void* bits, const void* Wc, c
   const long rows = (long)T * E;
   if (rows <= 32 && Cout % 64 == 0) {
     dim3 grid(1, Cout / 64, P);
+#define FC_MW(RT_, NKS_)                                                                                       \
+  fc_fwd_mw_kernel<RT_, FC_MW_D, NKS_><<<grid, 256, 0, stream>>>(                                            \
+      (const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits, (const bf16_t*)Wc, flat, bias_off, chunk, act_idx,  \
+      act_cnt, layer, L, M, K, KP, Cout, P, E, T, t0, bits_rows, out_scale)
     if (rows <= 16)
-      fc_fwd_mw_kernel<1, FC_MW_D><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
-                                                    (const bf16_t*)Wc, flat, bias_off, chunk, act_idx, act_cnt, layer,
-                                                    L, M, K, KP, Cout, P, E, T, t0, bits_rows, out_scale);
+      FC_MW(1, 0);
+    else if (KP == 1408)
+      FC_MW(2, 44);          // fc1 of the pixel trunk (conv3 output 8 x 11 x 16)
+    else if (KP == 256)
+      FC_MW(2, 8);           // fc2 (256 -> 256)
     else
-      fc_fwd_mw_kernel<2, FC_MW_D><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
-                                                    (const bf16_t*)Wc, flat, bias_off, chunk, act_idx, act_cnt, layer,
-                                                    L, M, K, KP, Cout, P, E, T, t0, bits_rows, out_scale);
+      FC_MW(2, 0);
+#undef FC_MW
   } else if (rows <= 32) {
     dim3 grid((unsigned)((rows + 31) / 32), (Cout + 63) / 64, P);
     fc_fwd_kernel<32><<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (bf16_t*)Y, (uint16_t*)bits,
