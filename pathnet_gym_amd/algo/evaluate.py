@@ -16,8 +16,12 @@ from ..models.acnet import ACPathNet
 
 @torch.no_grad()
 def evaluate_model(model: ACPathNet, env_id: str, episodes: int = 1, max_steps: int = 2000, device="cpu",
-                   seed: int = 12345, frameskip: int = 4, gray: str = "rgb"):
+                   seed: int = 12345, frameskip: int = 4, gray: str = "rgb", sample: bool = False):
+    """Mean return per path over ``episodes`` episodes (NaN for a path that finished none in ``max_steps``).
+    ``sample=False`` plays the argmax action; ``sample=True`` samples the policy with a seeded generator,
+    so a repeated evaluation of unchanged parameters replays the same episodes."""
     P = model.P
+    gen = torch.Generator(device=device).manual_seed(seed) if sample else None
     kw = {} if env_id.startswith("CartPole") else dict(frameskip=frameskip, gray=gray)
     env = make(env_id, num_envs=P, device=device, seed=seed, backend="torch", **kw)
     obs = env.reset()
@@ -25,7 +29,10 @@ def evaluate_model(model: ACPathNet, env_id: str, episodes: int = 1, max_steps: 
     returns = [[] for _ in range(P)]
     for _ in range(max_steps):
         logits, value, state = model.forward(obs, 1, state)
-        a = logits.argmax(-1)
+        if sample:
+            a = torch.multinomial(torch.softmax(logits.float(), -1), 1, generator=gen).reshape(-1)
+        else:
+            a = logits.argmax(-1)
         obs, r, d, info = env.step(a)
         if state is not None:
             keep = (~d).float()[:, None]

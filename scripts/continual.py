@@ -45,7 +45,9 @@ def build_cfg(args, tasks):
     return cfg
 
 
-def greedy_eval(tr, ti, name, args, dev):
+def greedy_eval(tr, ti, name, args, dev, sample=False):
+    """Task ti's frozen path + head on a fresh env: argmax actions, or (sample=True) the seeded sampled policy
+    (a greedy Breakout policy may never press FIRE, so no episode ends)."""
     from pathnet_gym_amd.algo.evaluate import evaluate_model
     from pathnet_gym_amd.models.acnet import ACPathNet
     import torch
@@ -55,7 +57,7 @@ def greedy_eval(tr, ti, name, args, dev):
     m.set_paths(tr.task_paths[ti][None])
     m.task = ti
     r = evaluate_model(m, name, episodes=args.eval_episodes, max_steps=args.eval_steps, device=dev,
-                       frameskip=tr.cfg.frameskip, gray=tr.cfg.gray)
+                       frameskip=tr.cfg.frameskip, gray=tr.cfg.gray, sample=sample)
     return r[0] if math.isfinite(r[0]) else None
 
 
@@ -111,6 +113,8 @@ def main():
     ap.add_argument("--eval-steps", type=int, default=6000)
     ap.add_argument("--report-every", type=float, default=20.0)
     ap.add_argument("--control", action="store_true", help="also train tasks >= 2 from scratch (transfer control)")
+    ap.add_argument("--control-only", action="store_true",
+                    help="only the from-scratch control runs of tasks >= 2 (e.g. in a separate job)")
     ap.add_argument("--out", default="gpurun_out/continual.json")
     args = ap.parse_args()
     import numpy as np
@@ -126,16 +130,32 @@ def main():
     args.frames_per_task = {t: fr[min(i, len(fr) - 1)] for i, t in enumerate(tasks)}
     args.frames = max(fr)
     cfg = build_cfg(args, tasks)
-    tr = PathNetTrainer(cfg, device=dev)
+    tr = None if args.control_only else PathNetTrainer(cfg, device=dev)
     t0 = time.time()
     per_task = []
     frozen_snap = []
-    for ti, name in enumerate(tasks):
+    controls = []
+
+    def write_out(stage):
+        out = {"experiment": "continual", "reference": "doom_pathnet.py:274-293, aliencentipede.txt:55-93",
+               "stage": stage, "tasks": tasks, "frames_per_task": args.frames_per_task, "n_gpus": 1,
+               "config": {"paths": args.paths, "envs_per_path": args.envs, "t_max": args.tmax, "N": args.N,
+                          "M": cfg.net.M, "B": cfg.ga.B, "trunk_scale": cfg.net.trunk_scale, "lr": cfg.a2c.lr,
+                          "per_task_heads": True, "freeze_union": cfg.ga.freeze_union, "seed": args.seed,
+                          "env_reduction": cfg.a2c.env_reduction, "dtype": tr.compute_dtype if tr else None},
+               "per_task": per_task, "scratch_control": controls, "seconds": round(time.time() - t0, 1)}
+        os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+        with open(args.out, "w") as f:
+            json.dump(out, f, indent=1)
+        return out
+
+    for ti, name in enumerate([] if args.control_only else tasks):
         rec = train_task(tr, ti, args, "sequence")
         winner, frozen = tr.end_task()
         rec["frozen_path"] = [p.tolist() for p in decode_path(tr.task_paths[ti])]
         rec["frozen_modules_total"] = int(frozen.sum())
         rec["greedy_after_task"] = greedy_eval(tr, ti, name, args, dev)
+        rec["sampled_after_task"] = greedy_eval(tr, ti, name, args, dev, sample=True)
         # snapshot of this task's frozen parameters (its modules + its head) to prove they never change again
         lay = tr.model.store.layout
         keep = np.zeros(lay.numel, bool)
@@ -145,36 +165,35 @@ def main():
         frozen_snap.append((keep, tr.model.store.flat.detach().cpu().numpy()[keep].copy()))
         per_task.append(rec)
         print(json.dumps({k: v for k, v in rec.items() if k != "curve"}), flush=True)
-    flat_end = tr.model.store.flat.detach().cpu().numpy()
-    for ti, name in enumerate(tasks):
+        write_out("sequence")
+    flat_end = None if tr is None else tr.model.store.flat.detach().cpu().numpy()
+    for ti, name in enumerate([] if args.control_only else tasks):
         keep, vals = frozen_snap[ti]
         per_task[ti]["frozen_params_bit_identical_at_end"] = bool(np.array_equal(flat_end[keep], vals))
         per_task[ti]["greedy_after_sequence"] = greedy_eval(tr, ti, name, args, dev)
+        per_task[ti]["sampled_after_sequence"] = greedy_eval(tr, ti, name, args, dev, sample=True)
         a, b = per_task[ti]["greedy_after_task"], per_task[ti]["greedy_after_sequence"]
         per_task[ti]["forgetting"] = None if a is None or b is None else a - b
         print(json.dumps({"task": name, "greedy_after_task": per_task[ti]["greedy_after_task"],
                           "greedy_after_sequence": per_task[ti]["greedy_after_sequence"],
+                          "sampled_after_task": per_task[ti]["sampled_after_task"],
+                          "sampled_after_sequence": per_task[ti]["sampled_after_sequence"],
                           "frozen_params_bit_identical_at_end": per_task[ti]["frozen_params_bit_identical_at_end"]}),
               flush=True)
-    controls = []
-    if args.control:
+    if per_task:
+        write_out("sequence+evaluation")
+    if args.control or args.control_only:
         for name in tasks[1:]:
             ctr = PathNetTrainer(build_cfg(args, [name]), device=dev)
+            if tr is None:
+                tr = ctr
             rec = train_task(ctr, 0, args, "scratch")
             controls.append({k: v for k, v in rec.items()})
             print(json.dumps({k: v for k, v in rec.items() if k != "curve"}), flush=True)
+            write_out("control")
             del ctr
             torch.cuda.empty_cache() if dev == "cuda" else None
-    out = {"experiment": "continual", "reference": "doom_pathnet.py:274-293, aliencentipede.txt:55-93",
-           "tasks": tasks, "frames_per_task": args.frames_per_task, "n_gpus": 1,
-           "config": {"paths": args.paths, "envs_per_path": args.envs, "t_max": args.tmax, "N": args.N,
-                      "M": cfg.net.M, "B": cfg.ga.B, "trunk_scale": cfg.net.trunk_scale, "lr": cfg.a2c.lr,
-                      "per_task_heads": True, "freeze_union": cfg.ga.freeze_union, "seed": args.seed,
-                      "env_reduction": cfg.a2c.env_reduction, "dtype": tr.compute_dtype},
-           "per_task": per_task, "scratch_control": controls, "seconds": round(time.time() - t0, 1)}
-    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
-    with open(args.out, "w") as f:
-        json.dump(out, f, indent=1)
+    out = write_out("done")
     print(json.dumps({"done": True, "seconds": out["seconds"], "out": args.out}), flush=True)
 
 
