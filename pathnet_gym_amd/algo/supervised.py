@@ -103,6 +103,13 @@ def supervised_config(L=3, M=10, N=3, width=20, din=32 * 32 * 3, module2=True):
     return PathNetConfig(L=L, M=M, N=N, input_shape=(din,), layers=layers, trunk_scale="none", num_actions=10)
 
 
+def supervised_conv_config(M=10, N=3, width=64, maps=(16, 32)):
+    """conv_module PathNet (pathnet.py:170-183): conv 5x5/2 -> conv 3x3/2 -> fc, M modules per layer."""
+    layers = [LayerSpec("conv", maps[0], kernel=5, stride=2), LayerSpec("conv", maps[1], kernel=3, stride=2),
+              LayerSpec("fc", width)]
+    return PathNetConfig(L=3, M=M, N=N, input_shape=(32, 32, 3), layers=layers, trunk_scale="none", num_actions=10)
+
+
 class SupervisedPathNet:
     def __init__(self, cfg: PathNetConfig, population: int, num_tasks: int, device, seed=1, B=2, backend="auto"):
         self.cfg = cfg
@@ -132,7 +139,10 @@ class SupervisedPathNet:
         W, b = self.heads[task]
         return feat @ W + b
 
-    def train_generation(self, data, task, steps, batch, lr, gen):
+    def train_generation(self, data, task, steps, batch, lr, gen, clip: float = 0.0):
+        """``steps`` SGD steps of every path on its own minibatch.  ``clip`` > 0: clip the global gradient norm
+        (trunk + head) per step; without it the first steps of a later task can explode when frozen modules
+        meet the new input distribution."""
         X, y = data
         n = X.shape[0]
         P = self.P
@@ -149,15 +159,30 @@ class SupervisedPathNet:
             loss.backward()
             with torch.no_grad():
                 gflat = self.store.flat.grad.masked_fill(self.frozen_elems, 0.0)
-                self.store.flat.sub_(lr * gflat / P)
-                W.sub_(lr * W.grad / P)
-                b.sub_(lr * b.grad / P)
+                scale = lr / P
+                if clip > 0:
+                    norm = torch.sqrt(gflat.square().sum() + W.grad.square().sum() + b.grad.square().sum()) / P
+                    scale = scale * float(torch.clamp(clip / (norm + 1e-12), max=1.0))
+                self.store.flat.sub_(scale * gflat)
+                W.sub_(scale * W.grad)
+                b.sub_(scale * b.grad)
         # fitness: accuracy of every path on a fresh evaluation batch
         with torch.no_grad():
             idx = torch.randint(0, n, (P * batch * 4,), generator=g).to(self.device)
             pred = self.logits(X[idx], masks, batch * 4, task).argmax(-1)
             acc = (pred == y[idx]).float().view(P, -1).mean(1)
         return acc.cpu().numpy()
+
+    @torch.no_grad()
+    def test_accuracy(self, path: np.ndarray, data, task: int, chunk: int = 512) -> float:
+        """Accuracy of ONE path (expressed genotype [L, M]) on held-out data."""
+        X, y = data
+        m = torch.from_numpy(np.asarray(path, np.float32))[None].to(self.device)
+        correct = 0
+        for i in range(0, X.shape[0], chunk):
+            xb = X[i:i + chunk]
+            correct += int((self.logits(xb, m, xb.shape[0], task).argmax(-1) == y[i:i + chunk]).sum())
+        return correct / X.shape[0]
 
     def end_task(self, winner: int):
         frozen = self.pop.freeze(winner, union=True)
@@ -171,36 +196,79 @@ class SupervisedPathNet:
             self.store.flat.copy_(torch.where(keep, self.store.flat, self.init_flat))
 
 
+def _progress(task, gen, best, t0):
+    import sys
+    print(f"[supervised] {task} generation {gen} best path accuracy {best:.3f} t={time.time() - t0:.0f}s",
+          file=sys.stderr, flush=True)
+
+
 def run_supervised_transfer(a) -> Dict:
     device = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
     tasks = [t.strip() for t in a.tasks.split(",")]
-    cfg = supervised_config(a.L, a.M, a.N, a.width)
+    arch = getattr(a, "arch", "fc")
+    if arch == "conv":
+        cfg = supervised_conv_config(a.M, a.N, a.width)
+        cfg.input_shape = (32, 32, 3)
+    else:
+        cfg = supervised_config(a.L, a.M, a.N, a.width)
+    n_train = getattr(a, "train_size", 4096)
+    sizes = [int(v) for v in str(getattr(a, "train_sizes", "") or "").split(",") if v.strip()]
+    n_of = lambda ti: sizes[min(ti, len(sizes) - 1)] if sizes else n_train      # noqa: E731
     sp = SupervisedPathNet(cfg, a.population, len(tasks), device, a.seed, a.B)
-    out = {"tasks": tasks, "per_task": []}
+    out = {"tasks": tasks, "arch": arch, "train_sizes": [n_of(i) for i in range(len(tasks))], "per_task": [],
+           "config": {"L": cfg.L, "M": cfg.M, "N": cfg.N, "layers": [(sp_.kind, sp_.out, sp_.kernel, sp_.stride)
+                                                                     for sp_ in cfg.layers],
+                      "population": a.population, "B": a.B, "generations": a.generations,
+                      "steps_per_gen": a.steps_per_gen, "batch": a.batch, "lr": a.lr, "seed": a.seed,
+                      "backend": sp.backend}}
     t0 = time.time()
+
+    clip = getattr(a, "clip", 0.0)
+    standardize = getattr(a, "standardize", False)
+    out["config"].update(clip=clip, standardize=standardize)
+
+    def shaped(X):
+        return X.reshape(X.shape[0], 32, 32, 3) if arch == "conv" else X
+
+    def prep(train, test):
+        """Per-task, per-channel standardisation with the TRAINING set's statistics."""
+        (X, y), (Xt, yt) = train, test
+        if standardize:
+            c = X.reshape(X.shape[0], -1, 3)
+            mu, sd = c.mean((0, 1)), c.std((0, 1)) + 1e-6
+            X = ((c - mu) / sd).reshape(X.shape)
+            Xt = ((Xt.reshape(Xt.shape[0], -1, 3) - mu) / sd).reshape(Xt.shape)
+        return (shaped(X), y), (shaped(Xt), yt)
+
     for ti, name in enumerate(tasks):
-        data = make_digits(name, 4096, a.seed * 31 + ti, device)
+        data, test = prep(make_digits(name, n_of(ti), a.seed * 31 + ti, device),
+                          make_digits(name, 2048, a.seed * 31 + ti + 7919, device))
         if ti > 0:
             sp.pop.init_genotypes()
         best_hist = []
         for gen in range(a.generations):
-            acc = sp.train_generation(data, ti, a.steps_per_gen, a.batch, a.lr, gen)
+            acc = sp.train_generation(data, ti, a.steps_per_gen, a.batch, a.lr, gen, clip)
             sp.pop.step(acc.astype(np.float32), gen)
             best_hist.append(float(acc.max()))
+            _progress(name, gen, best_hist[-1], t0)
         winner = int(np.argmax(acc))
+        test_acc = sp.test_accuracy(sp.pop.expressed()[winner], test, ti)
         sp.end_task(winner)
-        out["per_task"].append({"task": name, "best_accuracy": best_hist[-1], "curve": best_hist,
-                                "frozen": sp.frozen.astype(int).tolist()})
+        out["per_task"].append({"task": name, "best_accuracy": best_hist[-1], "test_accuracy": test_acc,
+                                "curve": best_hist, "frozen": sp.frozen.astype(int).tolist()})
     if getattr(a, "control", False) and len(tasks) > 1:
         # transfer check: the last task learned from scratch (no frozen source path), same budget
         ctl = SupervisedPathNet(cfg, a.population, 1, device, a.seed + 1000, a.B)
-        data = make_digits(tasks[-1], 4096, a.seed * 31 + len(tasks) - 1, device)
+        data, test = prep(make_digits(tasks[-1], n_of(len(tasks) - 1), a.seed * 31 + len(tasks) - 1, device),
+                          make_digits(tasks[-1], 2048, a.seed * 31 + len(tasks) - 1 + 7919, device))
         hist = []
         for gen in range(a.generations):
-            acc = ctl.train_generation(data, 0, a.steps_per_gen, a.batch, a.lr, gen)
+            acc = ctl.train_generation(data, 0, a.steps_per_gen, a.batch, a.lr, gen, clip)
             ctl.pop.step(acc.astype(np.float32), gen)
             hist.append(float(acc.max()))
-        out["control"] = {"task": tasks[-1], "best_accuracy": hist[-1], "curve": hist}
+            _progress(tasks[-1] + " (scratch)", gen, hist[-1], t0)
+        out["control"] = {"task": tasks[-1], "best_accuracy": hist[-1], "curve": hist,
+                          "test_accuracy": ctl.test_accuracy(ctl.pop.expressed()[int(np.argmax(acc))], test, 0)}
         thr = getattr(a, "target_accuracy", 0.9)
         first = lambda c: next((i for i, v in enumerate(c) if v >= thr), None)     # noqa: E731
         out["generations_to_accuracy"] = {"threshold": thr, "transfer": first(out["per_task"][-1]["curve"]),

@@ -115,6 +115,11 @@ def build_parser():
     s.add_argument("--M", type=int, default=10)
     s.add_argument("--N", type=int, default=3)
     s.add_argument("--width", type=int, default=20)
+    s.add_argument("--arch", default="fc", choices=["fc", "conv"], help="fc: module2 FC modules; conv: conv_module")
+    s.add_argument("--train_size", type=int, default=4096, help="training samples per task")
+    s.add_argument("--train_sizes", default="", help="per-task training-set sizes, e.g. 4096,256 (overrides --train_size)")
+    s.add_argument("--clip", type=float, default=5.0, help="global gradient-norm clip per SGD step (0: off)")
+    s.add_argument("--standardize", type=int, default=1, help="per-task per-channel input standardisation")
     s.add_argument("--steps_per_gen", type=int, default=50)
     s.add_argument("--batch", type=int, default=16)
     s.add_argument("--lr", type=float, default=0.05)

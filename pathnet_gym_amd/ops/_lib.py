@@ -86,6 +86,9 @@ _SIGS = {
     "launch_typed_fc_fwd": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],
     "launch_typed_fc_dgrad": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],
     "launch_typed_fc_wgrad": [P, P, c_int, c_long, c_long, c_int, c_int, c_int, P, P, c_int, P, P, P],
+    "launch_typed_fc_fwd_mfma": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],
+    "launch_typed_fc_dgrad_mfma": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],
+    "launch_typed_fc_wgrad_mfma": [P, P, c_int, c_long, c_long, c_int, c_int, c_int, P, P, c_int, P, P, P],
     "launch_active_union": [P, P, c_int, c_int, c_int, P, P],
     "launch_pack_ranges": [P, P, P, c_int, c_long, c_int, P],
     "conv_fwd_smem": [c_int, c_int],

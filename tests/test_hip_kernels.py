@@ -994,17 +994,12 @@ def test_torch_game_step_replays_in_hipgraph(hip_lib, game):
         obs_in.copy_(obs_out)
 
 
-@pytest.mark.parametrize("rpp", [5, 16, 37])
-def test_typed_fc_trunk_matches_oracle(hip_lib, rpp):
-    """K19: skip / fc / residual module types (pathnet.py:122-196) vs trunk_forward_ref, fwd + grad."""
-    from pathnet_gym_amd.algo.supervised import supervised_config
+def _typed_vs_oracle(cfg, P, rpp, din_shape, seed, tol):
     from pathnet_gym_amd.models.pathnet import ParamStore
     from pathnet_gym_amd.ops.typed_fc import typed_trunk_forward
-    cfg = supervised_config(L=3, M=10, N=3, width=20, din=300)
-    P = 7
     st = ParamStore(cfg, torch.device(DEV), seed=3)
-    masks = torch.from_numpy(random_masks(P, cfg.L, cfg.M, cfg.N, seed=rpp)).float().to(DEV)
-    x = torch.rand(P * rpp, 300, device=DEV)
+    masks = torch.from_numpy(random_masks(P, cfg.L, cfg.M, cfg.N, seed=seed)).float().to(DEV)
+    x = torch.rand(P * rpp, *din_shape, device=DEV)
     flat_h = st.flat.detach().clone().requires_grad_(True)
     flat_r = st.flat.detach().clone().requires_grad_(True)
     st.flat = flat_h
@@ -1014,14 +1009,57 @@ def test_typed_fc_trunk_matches_oracle(hip_lib, rpp):
     st.flat = flat_r
     yr = trunk_forward_ref(st, x, masks.repeat_interleave(rpp, 0))
     (yr * w).sum().backward()
-    assert rel(yh, yr) < 1e-5
-    assert rel(flat_h.grad, flat_r.grad) < 1e-5
+    assert rel(yh, yr) < tol
+    assert rel(flat_h.grad, flat_r.grad) < tol
+    # per segment too: every active module's weight and bias gradient
+    for s in st.layout.segments:
+        if s.layer >= 0:
+            b = flat_r.grad[s.offset:s.offset + s.numel]
+            if float(b.norm()) > 0:
+                assert rel(flat_h.grad[s.offset:s.offset + s.numel], b) < 10 * tol, s.name
     # inactive modules get exactly zero gradient
-    lay = st.layout
     inactive = (masks.sum(0) == 0).cpu().numpy()
-    for s in lay.segments:
+    for s in st.layout.segments:
         if s.layer >= 0 and inactive[s.layer, s.module]:
             assert float(flat_h.grad[s.offset:s.offset + s.numel].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("mode", ["never", "always"], ids=["valu", "mfma"])
+@pytest.mark.parametrize("rpp", [5, 16, 37])
+def test_typed_fc_trunk_matches_oracle(hip_lib, rpp, mode):
+    """K19: skip / fc / residual module types (pathnet.py:122-196) vs trunk_forward_ref, fwd + grad, on the
+    VALU kernels and on the fp32-MFMA kernels."""
+    from pathnet_gym_amd.algo.supervised import supervised_config
+    from pathnet_gym_amd.ops import typed_fc
+    cfg = supervised_config(L=3, M=10, N=3, width=20, din=300)
+    typed_fc.set_mfma(mode)
+    try:
+        _typed_vs_oracle(cfg, 7, rpp, (300,), rpp, 1e-5 if mode == "never" else 2e-5)
+    finally:
+        typed_fc.set_mfma("auto")
+
+
+def test_typed_fc_wide_layers_use_mfma(hip_lib):
+    """Widths > 64 (beyond the VALU kernels): 3072 -> 160 -> 160 -> 160 with module2 types, MFMA path."""
+    from pathnet_gym_amd.algo.supervised import supervised_config
+    cfg = supervised_config(L=4, M=10, N=3, width=160, din=3072)
+    _typed_vs_oracle(cfg, 6, 24, (3072,), 2, 2e-5)
+
+
+def test_typed_conv_modules_match_oracle(hip_lib):
+    """conv_module (pathnet.py:170-183): VALID conv + bias + ReLU modules as typed GEMMs over im2col rows,
+    then an fc layer; fwd + grad vs trunk_forward_ref."""
+    from pathnet_gym_amd.config import LayerSpec, PathNetConfig
+    from pathnet_gym_amd.ops import typed_fc
+    cfg = PathNetConfig(L=3, M=6, N=2, input_shape=(32, 32, 3),
+                        layers=[LayerSpec("conv", 8, kernel=5, stride=2), LayerSpec("conv", 16, kernel=3, stride=2),
+                                LayerSpec("fc", 80)], trunk_scale="none", num_actions=10)
+    for mode in ("auto", "always"):
+        typed_fc.set_mfma(mode)
+        try:
+            _typed_vs_oracle(cfg, 5, 6, (32, 32, 3), 4, 2e-5)
+        finally:
+            typed_fc.set_mfma("auto")
 
 
 def test_supervised_hip_backend_trains(hip_lib):
