@@ -133,9 +133,11 @@ def main():
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
 
     def sync():
-        torch.cuda.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
         ctx.barrier()
-        torch.cuda.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         tr.update()
@@ -166,11 +168,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_STEPS_PER_SEC, 1),
             "dtype": tr.compute_dtype,
-            "data": f"synthetic: on-device Atari-style {cfg.tasks[0]} simulator (210x160 RGB -> gray 160x120 x4 stack), "
-                    "random-init weights",
+            "data": (f"synthetic: on-device Atari-style {cfg.tasks[0]} simulator (210x160 RGB -> gray 160x120 x4 "
+                     "stack), random-init weights") if len(cfg.net.input_shape) == 3 else
+                    f"synthetic: on-device {cfg.tasks[0]}, random-init weights",
             "config": {
-                "model": f"PathNet {cfg.net.L} layers (3 conv 8-map + 2 fc 256) x M={cfg.net.M} modules, N={cfg.net.N}, "
-                         f"A2C T={cfg.a2c.t_max}, B={cfg.ga.B} tournament",
+                "model": f"PathNet {cfg.net.L} layers ("
+                         + " + ".join(f"{sp.kind} {sp.out}" + (f" {sp.kernel}x{sp.kernel}/{sp.stride}"
+                                                                 if sp.kind == "conv" else "")
+                                      for sp in cfg.net.layers)
+                         + f") x M={cfg.net.M} modules, N={cfg.net.N}, A2C T={cfg.a2c.t_max}, B={cfg.ga.B} tournament",
                 "global_batch": B * ctx.world * cfg.a2c.t_max,
                 "seq_len": cfg.a2c.t_max,
                 "parallelism": f"dp{ctx.world} (population split: {cfg.paths} paths x {cfg.envs_per_path} envs per GPU)",

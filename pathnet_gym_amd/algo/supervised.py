@@ -111,7 +111,14 @@ def supervised_conv_config(M=10, N=3, width=64, maps=(16, 32)):
 
 
 class SupervisedPathNet:
-    def __init__(self, cfg: PathNetConfig, population: int, num_tasks: int, device, seed=1, B=2, backend="auto"):
+    def __init__(self, cfg: PathNetConfig, population: int, num_tasks: int, device, seed=1, B=2, backend="auto",
+                 frozen_mode: str = "or"):
+        """frozen_mode "or": frozen modules are always expressed (the reference's OR with fixed_path, as in RL);
+        "available": a later task's genotypes may or may not select them (the PathNet paper's transfer
+        setting); frozen parameters are never updated either way."""
+        if frozen_mode not in ("or", "available"):
+            raise ValueError(frozen_mode)
+        self.frozen_mode = frozen_mode
         self.cfg = cfg
         self.P = population
         self.device = torch.device(device)
@@ -146,7 +153,7 @@ class SupervisedPathNet:
         X, y = data
         n = X.shape[0]
         P = self.P
-        masks = torch.from_numpy(self.pop.expressed()).to(self.device)
+        masks = torch.from_numpy(self.paths()).to(self.device)
         g = torch.Generator(device="cpu").manual_seed(1000003 * gen + task)
         for _ in range(steps):
             idx = torch.randint(0, n, (P * batch,), generator=g).to(self.device)
@@ -172,6 +179,12 @@ class SupervisedPathNet:
             pred = self.logits(X[idx], masks, batch * 4, task).argmax(-1)
             acc = (pred == y[idx]).float().view(P, -1).mean(1)
         return acc.cpu().numpy()
+
+    def paths(self) -> np.ndarray:
+        """[P, L, M] module masks the population trains and is evaluated with."""
+        if self.frozen_mode == "or":
+            return self.pop.expressed()
+        return (self.pop.genotypes > 0.5).astype(np.float32)
 
     @torch.no_grad()
     def test_accuracy(self, path: np.ndarray, data, task: int, chunk: int = 512) -> float:
@@ -214,13 +227,14 @@ def run_supervised_transfer(a) -> Dict:
     n_train = getattr(a, "train_size", 4096)
     sizes = [int(v) for v in str(getattr(a, "train_sizes", "") or "").split(",") if v.strip()]
     n_of = lambda ti: sizes[min(ti, len(sizes) - 1)] if sizes else n_train      # noqa: E731
-    sp = SupervisedPathNet(cfg, a.population, len(tasks), device, a.seed, a.B)
+    frozen_mode = getattr(a, "frozen_mode", "or")
+    sp = SupervisedPathNet(cfg, a.population, len(tasks), device, a.seed, a.B, frozen_mode=frozen_mode)
     out = {"tasks": tasks, "arch": arch, "train_sizes": [n_of(i) for i in range(len(tasks))], "per_task": [],
            "config": {"L": cfg.L, "M": cfg.M, "N": cfg.N, "layers": [(sp_.kind, sp_.out, sp_.kernel, sp_.stride)
                                                                      for sp_ in cfg.layers],
                       "population": a.population, "B": a.B, "generations": a.generations,
                       "steps_per_gen": a.steps_per_gen, "batch": a.batch, "lr": a.lr, "seed": a.seed,
-                      "backend": sp.backend}}
+                      "backend": sp.backend, "frozen_mode": frozen_mode}}
     t0 = time.time()
 
     clip = getattr(a, "clip", 0.0)
@@ -252,7 +266,7 @@ def run_supervised_transfer(a) -> Dict:
             best_hist.append(float(acc.max()))
             _progress(name, gen, best_hist[-1], t0)
         winner = int(np.argmax(acc))
-        test_acc = sp.test_accuracy(sp.pop.expressed()[winner], test, ti)
+        test_acc = sp.test_accuracy(sp.paths()[winner], test, ti)
         sp.end_task(winner)
         out["per_task"].append({"task": name, "best_accuracy": best_hist[-1], "test_accuracy": test_acc,
                                 "curve": best_hist, "frozen": sp.frozen.astype(int).tolist()})
@@ -268,7 +282,7 @@ def run_supervised_transfer(a) -> Dict:
             hist.append(float(acc.max()))
             _progress(tasks[-1] + " (scratch)", gen, hist[-1], t0)
         out["control"] = {"task": tasks[-1], "best_accuracy": hist[-1], "curve": hist,
-                          "test_accuracy": ctl.test_accuracy(ctl.pop.expressed()[int(np.argmax(acc))], test, 0)}
+                          "test_accuracy": ctl.test_accuracy(ctl.paths()[int(np.argmax(acc))], test, 0)}
         thr = getattr(a, "target_accuracy", 0.9)
         first = lambda c: next((i for i, v in enumerate(c) if v >= thr), None)     # noqa: E731
         out["generations_to_accuracy"] = {"threshold": thr, "transfer": first(out["per_task"][-1]["curve"]),

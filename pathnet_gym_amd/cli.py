@@ -118,6 +118,8 @@ def build_parser():
     s.add_argument("--arch", default="fc", choices=["fc", "conv"], help="fc: module2 FC modules; conv: conv_module")
     s.add_argument("--train_size", type=int, default=4096, help="training samples per task")
     s.add_argument("--train_sizes", default="", help="per-task training-set sizes, e.g. 4096,256 (overrides --train_size)")
+    s.add_argument("--frozen_mode", default="or", choices=["or", "available"],
+                   help="or: frozen modules always expressed (reference RL semantics); available: selectable by later paths")
     s.add_argument("--clip", type=float, default=5.0, help="global gradient-norm clip per SGD step (0: off)")
     s.add_argument("--standardize", type=int, default=1, help="per-task per-channel input standardisation")
     s.add_argument("--steps_per_gen", type=int, default=50)
