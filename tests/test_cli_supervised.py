@@ -56,3 +56,25 @@ def test_cli_info_and_train_eval(tmp_path):
     assert len(out["returns"]) == 4
     png = _cli("visualize", "--checkpoint", ck, "--out", str(tmp_path / "g.png")).strip()
     assert png.endswith("g.png")
+
+
+def test_frozen_mode_available_lets_paths_skip_frozen_modules():
+    """frozen_mode 'or' expresses the frozen path in every task-2 path (reference RL semantics); 'available'
+    trains task-2 paths on their own genotypes only; frozen parameters stay fixed in both."""
+    cfg = supervised_config(L=2, M=6, N=2, width=16)
+    for mode in ("or", "available"):
+        sp = SupervisedPathNet(cfg, population=8, num_tasks=2, device="cpu", seed=0, frozen_mode=mode)
+        data = make_digits("mnist", 256, 0)
+        acc = sp.train_generation(data, 0, steps=2, batch=8, lr=0.05, gen=0)
+        before = sp.store.flat.detach().clone()
+        sp.end_task(int(np.argmax(acc)))
+        sp.pop.init_genotypes()
+        paths = sp.paths()
+        frozen = sp.frozen > 0.5
+        if mode == "or":
+            assert np.all(paths[:, frozen] == 1)
+        else:
+            assert np.array_equal(paths, (sp.pop.genotypes > 0.5).astype(np.float32))
+            assert not np.all(paths[:, frozen] == 1)
+        sp.train_generation(make_digits("svhn", 128, 1), 1, steps=2, batch=8, lr=0.05, gen=0, clip=5.0)
+        assert torch.equal(sp.store.flat.detach()[sp.frozen_elems], before[sp.frozen_elems])
