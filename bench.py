@@ -92,6 +92,9 @@ def main():
     ap.add_argument("--env", default=None, help="train this task of the preset's suite instead of its first task")
     ap.add_argument("--kernel-opt", action="append", default=[],
                     help="kernel switch NAME=VALUE (fast_conv_set_*), for A/B measurements")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="HIP engine compute dtype (fp32: the reference's precision, csrc/trunk_f32.hip)")
+    ap.add_argument("--deterministic", action="store_true", help="fixed-order gradient reductions (bit-reproducible)")
     ap.add_argument("--ga-backend", default="device", choices=["device", "host"],
                     help="device: GA kernels inside the update graph + pipelined host bookkeeping")
     ap.add_argument("--concurrent", type=int, default=None,
@@ -130,6 +133,8 @@ def main():
     cfg.frame_ring = args.ring
     cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
     cfg.ga.backend = args.ga_backend
+    cfg.compute_dtype = args.dtype
+    cfg.deterministic = args.deterministic
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
 
     def sync():
@@ -185,6 +190,7 @@ def main():
                 "frame_ring": bool(getattr(tr.engine, "ring", False)),
                 "ga": f"{cfg.ga.backend} (B={cfg.ga.B}, {cfg.ga.concurrent_tournaments} concurrent tournaments)",
                 "pipelined": bool(tr.pipelined),
+                "deterministic": bool(getattr(tr.model.hip, "deterministic", False)),
             },
             "generations_in_timed_window": int(tr.pop.generation - gen0),
             # the metric's second half is measured by scripts/solve.py (minutes of training, not a bench window)

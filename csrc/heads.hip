@@ -21,8 +21,13 @@ DEVI float u01(uint32_t seed, uint32_t stepkey, uint32_t b, uint32_t j) {
   return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
+// trunk features are bf16 (bf16 engine) or fp32 (compute_dtype = "fp32", csrc/trunk_f32.hip)
+DEVI float ldfeat(const bf16_t* p) { return bf2f(*p); }
+DEVI float ldfeat(const float* p) { return *p; }
+
+template <typename FT>
 __global__ __launch_bounds__(256) void heads_fwd_sample_kernel(
-    const bf16_t* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
+    const FT* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
     int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
     const long long* __restrict__ ctr, int t, int T, int greedy) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -33,7 +38,7 @@ __global__ __launch_bounds__(256) void heads_fwd_sample_kernel(
   for (int j = 0; j < AMAX; ++j) part[j] = 0.f;
   float pv = 0.f;
   for (int f = l; f < F; f += 64) {
-    const float x = bf2f(feat[(long)b * F + f]);
+    const float x = ldfeat(feat + (long)b * F + f);
 #pragma unroll
     for (int j = 0; j < AMAX; ++j)
       if (j < A) part[j] += x * flat[pw + (long)f * A + j];
@@ -152,12 +157,16 @@ __global__ __launch_bounds__(256) void a2c_grad_kernel(
 }
 
 // grid = ceil(N / ROWS), block 256 (thread = feature f, looping f += 256)
+// part == nullptr: the row-chunk partials meet in grad with fp32 atomics.  Deterministic mode: chunk c writes
+// its partials to part[c][F*A + F + A + 1] (dWp, dWv, dbp, dbv) and heads_reduce_kernel sums the chunks in order.
 #define HB_ROWS 128
-template <int AM>
+template <int AM, typename FT>
 __global__ __launch_bounds__(256) void heads_bwd_kernel(
-    const bf16_t* __restrict__ feat, int F, const float* __restrict__ dlogits, const float* __restrict__ dvalue,
+    const FT* __restrict__ feat, int F, const float* __restrict__ dlogits, const float* __restrict__ dvalue,
     int N, int A, const float* __restrict__ flat, long pw, long pb, long vw, long vb, float* __restrict__ grad,
-    float* __restrict__ dfeat) {
+    float* __restrict__ dfeat, float* __restrict__ part) {
+  const long PS = (long)F * A + F + A + 1;
+  float* pc = part ? part + blockIdx.x * PS : nullptr;
   const long r0 = (long)blockIdx.x * HB_ROWS;
   const long r1 = min((long)N, r0 + HB_ROWS);
   for (int f = threadIdx.x; f < F; f += 256) {
@@ -170,7 +179,7 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const float wv = flat[vw + f];
     float gv = 0.f;
     for (long r = r0; r < r1; ++r) {
-      const float x = bf2f(feat[r * F + f]);
+      const float x = ldfeat(feat + r * F + f);
       const float dv = dvalue[r];
       float d = dv * wv;
 #pragma unroll
@@ -183,10 +192,17 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
       gv += x * dv;
       dfeat[r * F + f] = d;
     }
+    if (pc) {
 #pragma unroll
-    for (int j = 0; j < AM; ++j)
-      if (j < A) atomicAdd(&grad[pw + (long)f * A + j], gw[j]);
-    atomicAdd(&grad[vw + f], gv);
+      for (int j = 0; j < AM; ++j)
+        if (j < A) pc[(long)f * A + j] = gw[j];
+      pc[(long)F * A + f] = gv;
+    } else {
+#pragma unroll
+      for (int j = 0; j < AM; ++j)
+        if (j < A) atomicAdd(&grad[pw + (long)f * A + j], gw[j]);
+      atomicAdd(&grad[vw + f], gv);
+    }
   }
   if (threadIdx.x < 64) {
     // bias grads: wave 0 reduces dz / dv over the chunk
@@ -205,11 +221,34 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     for (int j = 0; j < AM; ++j)
       if (j < A) {
         const float s = wave_sum(bz[j]);
-        if (l == 0) atomicAdd(&grad[pb + j], s);
+        if (l == 0) {
+          if (pc) pc[(long)F * A + F + j] = s;
+          else atomicAdd(&grad[pb + j], s);
+        }
       }
     bvv = wave_sum(bvv);
-    if (l == 0) atomicAdd(&grad[vb], bvv);
+    if (l == 0) {
+      if (pc) pc[PS - 1] = bvv;
+      else atomicAdd(&grad[vb], bvv);
+    }
   }
+}
+
+// deterministic mode: grad[head param e] += sum over the row chunks of part[c][e], in chunk order
+__global__ __launch_bounds__(256) void heads_reduce_kernel(const float* __restrict__ part, int nchunk, int F, int A,
+                                                           long pw, long pb, long vw, long vb,
+                                                           float* __restrict__ grad) {
+  const long PS = (long)F * A + F + A + 1;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= PS) return;
+  float s = 0.f;
+  for (int c = 0; c < nchunk; ++c) s += part[c * PS + e];
+  long dst;
+  if (e < (long)F * A) dst = pw + e;
+  else if (e < (long)F * A + F) dst = vw + (e - (long)F * A);
+  else if (e < PS - 1) dst = pb + (e - (long)F * A - F);
+  else dst = vb;
+  grad[dst] += s;
 }
 
 extern "C" {
@@ -218,8 +257,17 @@ int launch_heads_fwd_sample(const void* feat, int F, const float* flat, long pw,
                             int B, float* logits, float* value, int* actions, unsigned seed, const long long* ctr,
                             int t, int T, int greedy, hipStream_t stream) {
   if (A > AMAX || A < 1) return -1;
-  heads_fwd_sample_kernel<<<(B + 3) / 4, 256, 0, stream>>>((const bf16_t*)feat, F, flat, pw, pb, vw, vb, A, B, logits,
-                                                            value, actions, seed, ctr, t, T, greedy);
+  heads_fwd_sample_kernel<bf16_t><<<(B + 3) / 4, 256, 0, stream>>>((const bf16_t*)feat, F, flat, pw, pb, vw, vb, A,
+                                                                    B, logits, value, actions, seed, ctr, t, T, greedy);
+  return (int)hipGetLastError();
+}
+
+int launch_heads_fwd_sample_f32(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
+                                int A, int B, float* logits, float* value, int* actions, unsigned seed,
+                                const long long* ctr, int t, int T, int greedy, hipStream_t stream) {
+  if (A > AMAX || A < 1) return -1;
+  heads_fwd_sample_kernel<float><<<(B + 3) / 4, 256, 0, stream>>>((const float*)feat, F, flat, pw, pb, vw, vb, A, B,
+                                                                   logits, value, actions, seed, ctr, t, T, greedy);
   return (int)hipGetLastError();
 }
 
@@ -234,17 +282,54 @@ int launch_a2c_grad(const float* logits, const float* values, const int* actions
   return (int)hipGetLastError();
 }
 
+}  // extern "C"
+
+template <typename FT>
+static int heads_bwd_launch(const void* feat, int F, const float* dlogits, const float* dvalue, int N, int A,
+                            const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
+                            float* part, hipStream_t stream) {
+  if (A > AMAX) return -1;
+  const int nchunk = (N + HB_ROWS - 1) / HB_ROWS;
+  if (A <= 8)
+    heads_bwd_kernel<8, FT><<<nchunk, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw,
+                                                        vb, grad, dfeat, part);
+  else
+    heads_bwd_kernel<AMAX, FT><<<nchunk, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb,
+                                                           vw, vb, grad, dfeat, part);
+  if (part) {
+    const long PS = (long)F * A + F + A + 1;
+    heads_reduce_kernel<<<(unsigned)((PS + 255) / 256), 256, 0, stream>>>(part, nchunk, F, A, pw, pb, vw, vb, grad);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" {
 int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float* dvalue, int N, int A,
                      const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
                      hipStream_t stream) {
-  if (A > AMAX) return -1;
-  if (A <= 8)
-    heads_bwd_kernel<8><<<(N + HB_ROWS - 1) / HB_ROWS, 256, 0, stream>>>((const bf16_t*)feat, F, dlogits, dvalue, N,
-                                                                        A, flat, pw, pb, vw, vb, grad, dfeat);
-  else
-    heads_bwd_kernel<AMAX><<<(N + HB_ROWS - 1) / HB_ROWS, 256, 0, stream>>>((const bf16_t*)feat, F, dlogits, dvalue,
-                                                                           N, A, flat, pw, pb, vw, vb, grad, dfeat);
-  return (int)hipGetLastError();
+  return heads_bwd_launch<bf16_t>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, nullptr,
+                                  stream);
+}
+
+int launch_heads_bwd_f32(const void* feat, int F, const float* dlogits, const float* dvalue, int N, int A,
+                         const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
+                         hipStream_t stream) {
+  return heads_bwd_launch<float>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, nullptr,
+                                 stream);
+}
+
+// deterministic heads backward (fixed-order chunk reduction); part: ceil(N/128) * (F*A + F + A + 1) floats
+long heads_bwd_part_numel(int N, int F, int A) {
+  return (long)((N + HB_ROWS - 1) / HB_ROWS) * ((long)F * A + F + A + 1);
+}
+
+int launch_heads_bwd_det(const void* feat, int f32, int F, const float* dlogits, const float* dvalue, int N, int A,
+                         const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
+                         float* part, hipStream_t stream) {
+  if (!part) return -1;
+  if (f32) return heads_bwd_launch<float>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, part,
+                                          stream);
+  return heads_bwd_launch<bf16_t>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, part, stream);
 }
 }
 

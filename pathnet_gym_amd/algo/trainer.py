@@ -72,7 +72,9 @@ class PathNetTrainer:
         self.device = torch.device(device)
         self.backend = resolve_backend(cfg.backend, self.device)
         # the torch backend always computes in fp32; the HIP engine uses bf16 (fp16 for the uint8 conv1
-        # operands) MFMA with fp32 accumulation and fp32 master weights
+        # operands) MFMA with fp32 accumulation and fp32 master weights, or fp32 operands (compute_dtype="fp32")
+        if cfg.compute_dtype not in ("bf16", "fp32"):
+            raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'bf16' or 'fp32'")
         self.compute_dtype = cfg.compute_dtype if self.backend == "hip" else "fp32"
         self.logger = logger
         net = cfg.net
@@ -88,7 +90,7 @@ class PathNetTrainer:
         self.pop = pop_cls(self.P_total, net.L, net.M, net.N, cfg.ga.B, seed=cfg.ga.seed,
                            mutation_kind=cfg.ga.mutation, concurrent=cfg.ga.concurrent_tournaments)
         self.model = ACPathNet(net, self.P, self.device, self.backend, seed=cfg.seed,
-                               compute_dtype=cfg.compute_dtype)
+                               compute_dtype=self.compute_dtype, deterministic=cfg.deterministic)
         a2c = cfg.a2c
         self.opt = RMSPropTF(self.model.store.layout, self.model.store.flat, a2c.rmsp_alpha, a2c.rmsp_momentum,
                              a2c.rmsp_epsilon, a2c.grad_norm_clip,

@@ -57,6 +57,10 @@ def build_parser():
         p.add_argument("--trunk_scale", default=None, choices=["M", "none"],
                        help="divide the trunk output by M (reference FF net) or not (reference LSTM net)")
         p.add_argument("--no_graph", action="store_true")
+        p.add_argument("--compute_dtype", default=None, choices=["bf16", "fp32"],
+                       help="HIP engine operand precision (fp32 = the reference's precision, csrc/trunk_f32.hip)")
+        p.add_argument("--deterministic", type=int, default=None,
+                       help="1: fixed-order gradient reductions (bit-reproducible updates)")
         # RL constants (constants.py)
         p.add_argument("--t_max", type=int, default=None)
         p.add_argument("--gamma", type=float, default=None)
@@ -192,6 +196,10 @@ def config_from_args(a):
         cfg.ga.freeze_union = bool(a.freeze_union)
     if getattr(a, "no_graph", False):
         cfg.use_graph = False
+    if getattr(a, "compute_dtype", None):
+        cfg.compute_dtype = a.compute_dtype
+    if getattr(a, "deterministic", None) is not None:
+        cfg.deterministic = bool(a.deterministic)
     if getattr(a, "ga_sync", None):
         cfg.ga_sync = a.ga_sync
     if getattr(a, "steps_per_task", None):

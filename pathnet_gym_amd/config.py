@@ -187,7 +187,14 @@ class TrainConfig:
     a2c: A2CConfig = field(default_factory=A2CConfig)
     ga: GAConfig = field(default_factory=GAConfig)
     backend: str = "auto"               # "hip" | "torch" | "auto"
+    # HIP engine operand precision: "bf16" (bf16/fp16 MFMA operands, fp32 accumulation + master weights) or
+    # "fp32" (fp32 activations and operands on v_mfma_f32_16x16x4_f32, csrc/trunk_f32.hip) -- the reference
+    # computes in fp32 (game_ac_network.py:89-110)
     compute_dtype: str = "bf16"
+    # fixed-order gradient reductions everywhere (no fp32 atomics): one seed reproduces every update bit for
+    # bit.  Always on with compute_dtype="fp32"; in bf16 it routes the weight gradients through the ordered
+    # fp32 kernels (slower: see docs/PERF.md)
+    deterministic: bool = False
     use_graph: bool = True
     frame_ring: bool = False            # HIP Pong: single-frame ring instead of packed stacks (runtime/engine.py;
                                         # measured 13.06 vs 12.73 ms/update: the conv1 planar loads cost more than

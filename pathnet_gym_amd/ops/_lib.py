@@ -91,6 +91,26 @@ _SIGS = {
     "launch_typed_fc_wgrad_mfma": [P, P, c_int, c_long, c_long, c_int, c_int, c_int, P, P, c_int, P, P, P],
     "launch_active_union": [P, P, c_int, c_int, c_int, P, P],
     "launch_pack_ranges": [P, P, P, c_int, c_long, c_int, P],
+    "launch_heads_fwd_sample_f32": [P, c_int, P, c_long, c_long, c_long, c_long, c_int, c_int, P, P, P, c_uint, P,
+                                    c_int, c_int, c_int, P],
+    "launch_heads_bwd_f32": [P, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P],
+    "launch_conv_fwd_f32": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                            c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_long,
+                            c_float, c_float, P],
+    "launch_fc_fwd_f32": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                          c_int, c_int, c_int, c_int, c_long, c_float, P],
+    "launch_conv_wgrad_f32": [P, c_int, P, P, P, P, c_long, c_long, c_int, P, P, P, P, P, c_int, c_int, c_int, c_int,
+                              c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_long, c_int, c_float, c_float, P],
+    "launch_conv_dgrad_f32": [P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, P, P],
+    "launch_fc_dgrad_f32": [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_long,
+                            c_float, P, P],
+    "launch_fc_wgrad_f32": [P, c_int, c_int, P, P, P, c_long, c_long, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
+                            c_int, c_int, c_int, c_long, c_float, P],
+    "launch_refresh_weights_f32": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
+    "launch_heads_bwd_det": [P, c_int, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P, P],
+    "heads_bwd_part_numel": [c_int, c_int, c_int],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }
@@ -111,7 +131,7 @@ def lib():
         for name, args in _SIGS.items():
             fn = getattr(_lib, name)
             fn.argtypes = args
-            fn.restype = c_size_t if name.endswith("_smem") else (None if name.startswith("fast_conv_set_") else c_int)
+            fn.restype = c_size_t if name.endswith("_smem") else c_long if name.endswith("_numel") else (None if name.startswith("fast_conv_set_") else c_int)
     return _lib
 
 

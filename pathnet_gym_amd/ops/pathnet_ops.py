@@ -80,6 +80,15 @@ class HipPathNet:
         self.model = model
         cfg = model.cfg
         self.cfg = cfg
+        # compute_dtype "fp32": fp32 activations / operand copies on v_mfma_f32_16x16x4_f32 (csrc/trunk_f32.hip,
+        # every reduction in a fixed order); "bf16": the bf16/fp16-operand MFMA kernels with fp32 accumulation
+        self.f32 = getattr(model, "compute_dtype", "bf16") == "fp32"
+        self.act_dtype = torch.float32 if self.f32 else torch.bfloat16
+        # deterministic reductions (TrainConfig.deterministic; implied by fp32): every weight/bias gradient is
+        # summed in a fixed order (trunk_f32.hip ordered slabs, heads_reduce_kernel) instead of fp32 atomics,
+        # so one seed reproduces the update bit for bit
+        self.deterministic = self.f32 or bool(getattr(model, "deterministic", False))
+        self._hpart = None
         self.L, self.M = cfg.L, cfg.M
         lay = model.store.layout
         dev = model.device
@@ -104,7 +113,7 @@ class HipPathNet:
                     raise NotImplementedError("HIP fc layers implement fc+ReLU modules")
                 if cout % 32 != 0:
                     raise NotImplementedError("HIP fc modules need width % 32 == 0")
-                ldx = round_up(K, 8) if l > 0 else 8
+                ldx = round_up(K, 8) if l > 0 else (K if self.f32 else 8)
                 if l == 0 and K > 8:
                     raise NotImplementedError("vector observations up to 8 dims")
                 g = LayerGeom("fc", K, round_up(K, 32), cout, 1, cout, li["offset"], li["chunk"], ldx=ldx)
@@ -115,13 +124,14 @@ class HipPathNet:
             self.geoms.append(g)
         self.pixels = cfg.layers[0].kind == "conv"
         self.out_scale_last = (1.0 / cfg.M) if cfg.trunk_scale == "M" else 1.0
-        # bf16 operand copies
+        # MFMA operand copies (bf16, or fp32 in the fp32 mode)
         self.Wc = []
         self.WcT = []
         for l, g in enumerate(self.geoms):
-            self.Wc.append(torch.zeros(self.M, g.Cout, g.KP, dtype=torch.bfloat16, device=dev))
+            self.Wc.append(torch.zeros(self.M, g.Cout, g.KP, dtype=self.act_dtype, device=dev))
             need_t = g.kind == "fc" and l > 0
-            self.WcT.append(torch.zeros(self.M, g.KP, g.Cout, dtype=torch.bfloat16, device=dev) if need_t else None)
+            self.WcT.append(torch.zeros(self.M, g.KP, g.Cout, dtype=self.act_dtype, device=dev) if need_t else None)
+        self._part = None            # fp32 conv wgrad partial slabs (allocated on first use, before capture)
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
         self.inv_slot = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
@@ -130,7 +140,7 @@ class HipPathNet:
         self.heads_off = lay_h
         # fused LSTM cell (csrc/lstm.hip): bf16 copies of the fp32 master kernel
         self.lstm = None
-        if cfg.use_lstm:
+        if cfg.use_lstm and not self.deterministic:     # fp32 / deterministic: hybrid (autograd fp32) LSTM path
             ls = lay.lstm
             F, H = ls["din"], ls["H"]
             if F % 64 == 0 and H % 64 == 0:
@@ -139,13 +149,13 @@ class HipPathNet:
                                  Kb=torch.zeros(F + H, 4 * H, dtype=torch.bfloat16, device=dev))
         # frame-ring input for the first layer (runtime/engine.py): channel-major bf16 weights
         g0 = self.geoms[0]
-        self.ring_ok = (g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
+        self.ring_ok = (not self.deterministic and g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
                         and self.M <= 10 and g0.Cout == 8)
         self.Wc_ring = None
         # uint8 first conv layer: fp16 operand copy + per-column weight sums for the fp16-offset MFMA path
         # (conv_fwd_fast: pixels enter as fp16(1024 + v), built with one v_perm per two pixels)
         self.Wh0 = self.hcorr0 = None
-        if g0.kind == "conv" and g0.u8in:
+        if g0.kind == "conv" and g0.u8in and not self.f32:
             self.Wh0 = torch.zeros(self.M, g0.Cout, g0.KP, dtype=torch.float16, device=dev)
             self.hcorr0 = torch.zeros(self.M * g0.Cout, dtype=torch.float32, device=dev)
         self.refresh_weights()
@@ -185,7 +195,7 @@ class HipPathNet:
     def refresh_weights(self):
         flat = self.model.store.flat
         for l, g in enumerate(self.geoms):
-            _lib.call("launch_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
+            _lib.call("launch_refresh_weights_f32" if self.f32 else "launch_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
                       self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), _lib.stream())
         if self.Wh0 is not None:
             g = self.geoms[0]
@@ -240,6 +250,8 @@ class HipPathNet:
         flat = m.store.flat
         out_scale = self.out_scale_last if l == self.L - 1 else 1.0
         st = _lib.stream()
+        if self.f32:
+            return self._layer_fwd_f32(l, X, Y, bits, P, E, T, t0, bits_rows, out_scale, st)
         if g.kind == "conv":
             if (E * g.HWo) % 16 != 0:
                 raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
@@ -267,6 +279,10 @@ class HipPathNet:
         flat = m.store.flat
         g_scale = self.out_scale_last if l == self.L - 1 else 1.0
         st = _lib.stream()
+        if self.f32:
+            return self._layer_bwd_f32(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
+        if self.deterministic:
+            return self._layer_bwd_det(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
         if g.kind == "conv":
             fast_w = _lib.USE_FAST and _lib.call_fast(
                 "fast_conv_wgrad", X.data_ptr(), int(g.u8in), G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(),
@@ -311,6 +327,96 @@ class HipPathNet:
                 _lib.call("launch_fc_wgrad", X.data_ptr(), g.ldx, G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(),
                           g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(), self.inv_slot.data_ptr(),
                           self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T, bits_rows, g_scale, st)
+
+    # -- fp32 mode (csrc/trunk_f32.hip) ------------------------------------------
+    def _layer_fwd_f32(self, l, X, Y, bits, P, E, T, t0, bits_rows, out_scale, st):
+        g = self.geoms[l]
+        m = self.model
+        flat = m.store.flat
+        _lib.check(Y, torch.float32, name="Y")
+        if g.kind == "conv":
+            if (E * g.HWo) % 16 != 0:
+                raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
+            _lib.call("launch_conv_fwd_f32", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
+                      self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
+                      m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo,
+                      g.K, g.KP, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
+        else:
+            _lib.call("launch_fc_fwd_f32", X.data_ptr(), g.ldx, Y.data_ptr(), bits.data_ptr(), self.Wc[l].data_ptr(),
+                      flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L,
+                      self.M, g.K, g.KP, g.Cout, P, E, T, t0, bits_rows, out_scale, st)
+
+    def wgrad_chunks(self, l: int, P: int, E: int, T: int) -> int:
+        """Row chunks per path of the fp32 conv wgrad (>= ~1024 workgroups), matching the launcher's rounding."""
+        g = self.geoms[l]
+        rows = T * E * g.HWo
+        want = max(1, min(-(-rows // 32), -(-1024 // P)))
+        rpc = round_up(-(-rows // want), 32)
+        return -(-rows // rpc)
+
+    def _part_buffer(self, numel: int) -> torch.Tensor:
+        if self._part is None or self._part.numel() < numel:
+            self._part = torch.empty(numel, dtype=torch.float32, device=self.model.store.flat.device)
+        return self._part
+
+    def _conv_wgrad_ordered(self, l, X, G, bits, grad_flat, P, E, T, bits_rows, g_scale, st):
+        """Conv weight gradient with fixed-order reductions (uint8 / bf16 / fp32 input, fp32 MFMA)."""
+        g = self.geoms[l]
+        m = self.model
+        nch = self.wgrad_chunks(l, P, E, T)
+        part = self._part_buffer(P * nch * self.M * (g.K * 8 + 8))
+        xkind = 0 if g.u8in else (2 if X.dtype == torch.float32 else 1)
+        _lib.call("launch_conv_wgrad_f32", X.data_ptr(), xkind, G.data_ptr(), bits.data_ptr(),
+                  grad_flat.data_ptr(), part.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
+                  m.act_cnt.data_ptr(), self.inv_path.data_ptr(), self.inv_slot.data_ptr(),
+                  self.inv_cnt.data_ptr(), l, self.L, self.M, m.P, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho,
+                  g.Wo, g.K, g.KP, P, E, T, bits_rows, nch, g.in_scale, g_scale, st)
+
+    def _fc_wgrad_ordered(self, l, X, G, bits, grad_flat, P, E, T, bits_rows, g_scale, st):
+        g = self.geoms[l]
+        m = self.model
+        _lib.call("launch_fc_wgrad_f32", X.data_ptr(), 2 if X.dtype == torch.float32 else 1, g.ldx, G.data_ptr(),
+                  bits.data_ptr(), grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
+                  self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T, bits_rows,
+                  g_scale, st)
+
+    def _layer_bwd_det(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st):
+        """bf16 engine, deterministic mode: the bf16 dgrad kernels (no atomics) + ordered fp32 weight gradients."""
+        g = self.geoms[l]
+        m = self.model
+        flat = m.store.flat
+        if g.kind == "conv":
+            self._conv_wgrad_ordered(l, X, G, bits, grad_flat, P, E, T, bits_rows, g_scale, st)
+            if dX is not None and not (_lib.USE_FAST and _lib.call_fast(
+                    "fast_conv_dgrad", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
+                    m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW,
+                    g.S, P, E, T, bits_rows, g_scale, dX.data_ptr(), st)):
+                _lib.call("launch_conv_dgrad", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
+                          m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH,
+                          g.KW, g.S, g.Ho, g.Wo, P, E, T, bits_rows, g_scale, dX.data_ptr(), st)
+            return
+        if dX is not None:
+            _lib.call("launch_fc_dgrad", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
+                      m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.K, g.KP, g.Cout, P, E,
+                      T, bits_rows, g_scale, dX.data_ptr(), None, st)
+        self._fc_wgrad_ordered(l, X, G, bits, grad_flat, P, E, T, bits_rows, g_scale, st)
+
+    def _layer_bwd_f32(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st):
+        g = self.geoms[l]
+        m = self.model
+        flat = m.store.flat
+        if g.kind == "conv":
+            self._conv_wgrad_ordered(l, X, G, bits, grad_flat, P, E, T, bits_rows, g_scale, st)
+            if dX is not None:
+                _lib.call("launch_conv_dgrad_f32", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
+                          m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH,
+                          g.KW, g.S, g.Ho, g.Wo, P, E, T, bits_rows, g_scale, dX.data_ptr(), st)
+            return
+        if dX is not None:
+            _lib.call("launch_fc_dgrad_f32", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
+                      m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.K, g.KP, g.Cout, P, E, T,
+                      bits_rows, g_scale, dX.data_ptr(), st)
+        self._fc_wgrad_ordered(l, X, G, bits, grad_flat, P, E, T, bits_rows, g_scale, st)
 
     def _gm_buffer(self, bits_rows: int) -> torch.Tensor:
         """[M][bits_rows][256] bf16 scratch for the masked fc gradient (allocated before graph capture)."""
@@ -366,7 +472,8 @@ class HipPathNet:
         B = feat.shape[0]
         F = feat.shape[1]
         A = m.cfg.num_actions
-        _lib.call("launch_heads_fwd_sample", feat.data_ptr(), F, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"],
+        _lib.check(feat, self.act_dtype, name="feat")
+        _lib.call("launch_heads_fwd_sample_f32" if self.f32 else "launch_heads_fwd_sample", feat.data_ptr(), F, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"],
                   h["vb"], A, B, logits.data_ptr(), value.data_ptr(), actions.data_ptr(), seed & 0xFFFFFFFF,
                   ctr.data_ptr(), t, T, int(greedy), _lib.stream())
 
@@ -374,8 +481,18 @@ class HipPathNet:
         m = self.model
         h = m.store.layout.heads[task if m.cfg.per_task_heads else 0]
         N, F = feat.shape
-        _lib.call("launch_heads_bwd", feat.data_ptr(), F, dlogits.data_ptr(), dvalue.data_ptr(), N,
-                  m.cfg.num_actions, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"],
+        _lib.check(feat, self.act_dtype, name="feat")
+        A = m.cfg.num_actions
+        if self.deterministic:
+            n = _lib.lib().heads_bwd_part_numel(N, F, A)
+            if self._hpart is None or self._hpart.numel() < n:
+                self._hpart = torch.empty(n, dtype=torch.float32, device=feat.device)
+            _lib.call("launch_heads_bwd_det", feat.data_ptr(), int(self.f32), F, dlogits.data_ptr(),
+                      dvalue.data_ptr(), N, A, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"],
+                      grad_flat.data_ptr(), dfeat.data_ptr(), self._hpart.data_ptr(), _lib.stream())
+            return
+        _lib.call("launch_heads_bwd_f32" if self.f32 else "launch_heads_bwd", feat.data_ptr(), F, dlogits.data_ptr(),
+                  dvalue.data_ptr(), N, A, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"],
                   grad_flat.data_ptr(), dfeat.data_ptr(), _lib.stream())
 
     # -- standalone forward (tests / acting): obs [B, ...] -> feat [B, F] --------
@@ -386,7 +503,7 @@ class HipPathNet:
         x = self._prep_input(obs)
         out = None
         for l, g in enumerate(self.geoms):
-            Y = torch.empty(B, g.out_feat, dtype=torch.bfloat16, device=m.device)
+            Y = torch.empty(B, g.out_feat, dtype=self.act_dtype, device=m.device)
             bits, rows = self.alloc_bits(l, 1, B)
             self.layer_fwd(l, x, Y, bits, P, E, 1, 0, rows)
             x = Y
@@ -396,6 +513,8 @@ class HipPathNet:
     def _prep_input(self, obs):
         if self.pixels:
             return _lib.check(obs.contiguous(), torch.uint8, name="obs")
+        if self.f32:
+            return obs.float().reshape(obs.shape[0], -1).contiguous()
         if obs.dtype == torch.bfloat16 and obs.shape[-1] == 8:
             return obs.contiguous()
         from .envs import obs_to_bf16_padded

@@ -66,11 +66,13 @@ class HipEngine:
         elif self.pixels:
             H, W, C = model.cfg.input_shape
             self.obs = torch.zeros(T + 1, B, H * W * C, dtype=torch.uint8, device=dev)
+        elif hp.f32:
+            self.obs = torch.zeros(T + 1, B, hp.geoms[0].ldx, dtype=torch.float32, device=dev)
         else:
             self.obs = torch.zeros(T + 1, B, 8, dtype=torch.bfloat16, device=dev)
         self.acts, self.bits, self.bits_rows, self.grads = [], [], [], []
         for l, g in enumerate(hp.geoms):
-            self.acts.append(torch.zeros(T + 1, B, g.out_feat, dtype=torch.bfloat16, device=dev))
+            self.acts.append(torch.zeros(T + 1, B, g.out_feat, dtype=hp.act_dtype, device=dev))
             b, rows = hp.alloc_bits(l, T + 1, B)
             self.bits.append(b)
             self.bits_rows.append(rows)
@@ -126,6 +128,8 @@ class HipEngine:
         o = env.obs if self.pixels else None
         if self.pixels:
             self.set_obs_stack0(o.reshape(self.B, -1))
+        elif self.hip.f32:
+            self.obs[0].copy_(env.state.float().reshape(self.B, -1))
         else:
             self.obs[0].copy_(henv.obs_to_bf16_padded(env.state.float()))
 
@@ -200,6 +204,9 @@ class HipEngine:
         elif self.pixels:
             henv.pong_step_into(env, self.actions[t], self.obs[t], self.obs[t + 1], self.rewards[t], self.dones[t],
                                 self.epret[t])
+        elif self.hip.f32:
+            henv.cartpole_step_into(env, self.actions[t], None, self.rewards[t], self.dones[t], self.epret[t],
+                                    obs_f32_out=self.obs[t + 1])
         else:
             henv.cartpole_step_into(env, self.actions[t], self.obs[t + 1], self.rewards[t], self.dones[t],
                                     self.epret[t])
