@@ -71,6 +71,53 @@ DEVI void load_a8f(const void* X, long off, float* r) {
   }
 }
 
+// raw (unconverted) prefetch registers of 8 input values: 2 / 4 / 8 VGPRs for uint8 / bf16 / fp32
+template <int XK> struct XRaw { float4 a, b; };
+template <> struct XRaw<XU8> { uint2 a; };
+template <> struct XRaw<XBF16> { uint4 a; };
+
+template <int XK>
+DEVI XRaw<XK> load_raw8(const void* X, long off) {
+  XRaw<XK> r;
+  if constexpr (XK == XU8) r.a = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + off);
+  else if constexpr (XK == XBF16) r.a = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(X) + off);
+  else {
+    r.a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + off);
+    r.b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + off + 4);
+  }
+  return r;
+}
+
+template <int XK>
+DEVI XRaw<XK> zero_raw8() {
+  XRaw<XK> r;
+  if constexpr (XK == XU8) r.a = make_uint2(0, 0);
+  else if constexpr (XK == XBF16) r.a = make_uint4(0, 0, 0, 0);
+  else { r.a = make_float4(0.f, 0.f, 0.f, 0.f); r.b = r.a; }
+  return r;
+}
+
+template <int XK>
+DEVI void raw8_to_f(const XRaw<XK>& r, float* o) {
+  if constexpr (XK == XU8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (float)((r.a.x >> (8 * j)) & 0xFFu);
+      o[j + 4] = (float)((r.a.y >> (8 * j)) & 0xFFu);
+    }
+  } else if constexpr (XK == XBF16) {
+    const uint32_t u[4] = {r.a.x, r.a.y, r.a.z, r.a.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[2 * j] = __uint_as_float(u[j] << 16);
+      o[2 * j + 1] = __uint_as_float(u[j] & 0xFFFF0000u);
+    }
+  } else {
+    o[0] = r.a.x; o[1] = r.a.y; o[2] = r.a.z; o[3] = r.a.w;
+    o[4] = r.b.x; o[5] = r.b.y; o[6] = r.b.z; o[7] = r.b.w;
+  }
+}
+
 template <int XK>
 DEVI float load_a1f(const void* X, long off) {
   if constexpr (XK == XU8) return (float)reinterpret_cast<const uint8_t*>(X)[off];
@@ -141,16 +188,21 @@ __global__ __launch_bounds__(256) void conv_fwd_f32_kernel(
   for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int ct = 0; ct < MCT; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
+  // the next k-step's A fragments (raw: 2 VGPRs per row tile for uint8) are loaded before this step's MFMAs
+  constexpr int XK = U8IN ? XU8 : XF32;
+  XRaw<XK> an[RT];
+  auto aload = [&](int kk) {
+    const int off = koff[(kk + 8 * grp) >> 3];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) an[i] = (va[i] && off >= 0) ? load_raw8<XK>(X, xbase[i] + off) : zero_raw8<XK>();
+  };
+  aload(0);
   for (int kk = 0; kk < g.KP; kk += 32) {
     const int k0 = kk + 8 * grp;
-    const int off = koff[k0 >> 3];
     float a[RT][8];
 #pragma unroll
-    for (int i = 0; i < RT; ++i) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[i][j] = 0.f;
-      if (va[i] && off >= 0) load_a8f<U8IN ? XU8 : XF32>(X, xbase[i] + off, a[i]);
-    }
+    for (int i = 0; i < RT; ++i) raw8_to_f<XK>(an[i], a[i]);
+    if (kk + 32 < g.KP) aload(kk + 32);
 #pragma unroll
     for (int ct = 0; ct < MCT; ++ct) {
       if (ct < nct) {
@@ -259,29 +311,55 @@ __global__ __launch_bounds__(256) void fc_fwd_f32_kernel(
     f4v acc[RT][2];
 #pragma unroll
     for (int i = 0; i < RT; ++i) { acc[i][0] = {0.f, 0.f, 0.f, 0.f}; acc[i][1] = {0.f, 0.f, 0.f, 0.f}; }
-    for (int kk = 0; kk < KP; kk += 32) {
-      const int k0 = kk + 8 * grp;
-      float av[RT][8];
+    if (vec8) {
+      // register pipeline: the next k-step's A and B fragments load during this step's MFMAs
+      float an[RT][8], bn[2][8];
+      auto fload = [&](int kk) {
+        const int k0 = kk + 8 * grp;
 #pragma unroll
-      for (int i = 0; i < RT; ++i) {
+        for (int i = 0; i < RT; ++i) {
+          if (xv[i] && k0 < K) ld8f(X + xrow[i] + k0, an[i]);
+          else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) av[i][j] = 0.f;
-        if (xv[i] && k0 < K) {
-          if (vec8) {
-            ld8f(X + xrow[i] + k0, av[i]);
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (k0 + j < K) av[i][j] = X[xrow[i] + k0 + j];
+            for (int j = 0; j < 8; ++j) an[i][j] = 0.f;
           }
         }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) ld8f(Wm + (long)(col0 + j * 16 + c16) * KP + k0, bn[j]);
+      };
+      fload(0);
+      for (int kk = 0; kk < KP; kk += 32) {
+        float av[RT][8], bv[2][8];
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) av[i][j] = an[i][j];
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bv[jn][j] = bn[jn][j];
+        if (kk + 32 < KP) fload(kk + 32);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < RT; ++i) acc[i][j] = mfma_f32x8(av[i], bv[j], acc[i][j]);
       }
+    } else {
+      for (int kk = 0; kk < KP; kk += 32) {
+        const int k0 = kk + 8 * grp;
+        float av[RT][8];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float b[8];
-        ld8f(Wm + (long)(col0 + j * 16 + c16) * KP + k0, b);
+        for (int i = 0; i < RT; ++i) {
 #pragma unroll
-        for (int i = 0; i < RT; ++i) acc[i][j] = mfma_f32x8(av[i], b, acc[i][j]);
+          for (int j = 0; j < 8; ++j) av[i][j] = (xv[i] && k0 + j < K) ? X[xrow[i] + k0 + j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float b[8];
+          ld8f(Wm + (long)(col0 + j * 16 + c16) * KP + k0, b);
+#pragma unroll
+          for (int i = 0; i < RT; ++i) acc[i][j] = mfma_f32x8(av[i], b, acc[i][j]);
+        }
       }
     }
 #pragma unroll
@@ -375,6 +453,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32_kernel(
   float* pbase = part + ((long)(p * nch + blockIdx.x) * M) * pstride;
   // G staging: thread tid < 128 -> row gr = tid >> 2, slot (of the pass) gs = tid & 3
   const int gr = tid >> 2, gs = tid & 3;
+  // this thread's X items (stage-invariant): im2col row within the stage, input offset of the k chunk
+  // (-1: padding chunk or no item) and LDS offset (-1: no item)
+  int xrow[F32_WG_NX], xoff[F32_WG_NX], xsoff[F32_WG_NX];
+#pragma unroll
+  for (int q = 0; q < F32_WG_NX; ++q) {
+    const int it = tid + 256 * q;
+    xrow[q] = 0;
+    xoff[q] = -1;
+    xsoff[q] = -1;
+    if (it < nx) {
+      const int row = it / kvec, kc = it - row * kvec;
+      xrow[q] = row;
+      xoff[q] = koff[kc];
+      xsoff[q] = row * XS + kc * 8;
+    }
+  }
 
   for (int s0 = 0; s0 < cnt; s0 += 4) {
     const int ns = min(4, cnt - s0);
@@ -384,25 +478,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32_kernel(
     f4v acc[4][2];
 #pragma unroll
     for (int a = 0; a < 4; ++a) { acc[a][0] = {0.f, 0.f, 0.f, 0.f}; acc[a][1] = {0.f, 0.f, 0.f, 0.f}; }
-    float xr[F32_WG_NX][8];
+    XRaw<XK> xr[F32_WG_NX];
     float gvr[8];
     uint32_t gbits = 0;
     auto gload = [&](int rb) {
 #pragma unroll
       for (int q = 0; q < F32_WG_NX; ++q) {
-        const int it = tid + 256 * q;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) xr[q][c] = 0.f;
-        if (it < nx) {
-          const int row = it / kvec, kc = it - row * kvec;
-          const int r = rb + row;
-          const int off = koff[kc];
-          if (r < r_end && off >= 0) {
+        xr[q] = zero_raw8<XK>();
+        if (xoff[q] >= 0) {
+          const int r = rb + xrow[q];
+          if (r < r_end) {
             const int s = r / HoWo;
             const int pos = r - s * HoWo;
             const int oh = pos / g.Wo, ow = pos - oh * g.Wo;
-            const long xb = sample_global(p, s, E, PE, 0) * (long)HWC + (long)(oh * g.S * g.Win + ow * g.S) * g.Cin + off;
-            load_a8f<XK>(X, xb, xr[q]);
+            const long xb = sample_global(p, s, E, PE, 0) * (long)HWC + (long)(oh * g.S * g.Win + ow * g.S) * g.Cin +
+                            xoff[q];
+            xr[q] = load_raw8<XK>(X, xb);
           }
         }
       }
@@ -424,10 +515,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_f32_kernel(
       // registers -> LDS (masked G; bias partials accumulate per (row, slot) thread in stage order)
 #pragma unroll
       for (int q = 0; q < F32_WG_NX; ++q) {
-        const int it = tid + 256 * q;
-        if (it < nx) {
-          const int row = it / kvec, kc = it - row * kvec;
-          st8f(Xs + row * XS + kc * 8, xr[q]);
+        if (xsoff[q] >= 0) {
+          float v[8];
+          raw8_to_f<XK>(xr[q], v);
+          st8f(Xs + xsoff[q], v);
         }
       }
       if (tid < 128) {
