@@ -930,8 +930,9 @@ __global__ __launch_bounds__(WG_NT, 4) void conv_wgrad_fast(const void* __restri
 // RING: X is the frame ring (see conv_fwd_fast); a stage loads 8 pixels of each of the 4
 // channel planes per thread and interleaves them into the packed (pixel, channel) slab at
 // LDS-write time, so the slab layout and every MFMA operand read are unchanged.
-template <class G, int OB, int PF, bool RING = false>
-__global__ __launch_bounds__(256, 3) void conv_wgrad_slab(const void* __restrict__ X, const float* __restrict__ Gr,
+// GT = float, or bf16_t when the layer's output gradient was written in bf16 (conv_dgrad_mfma OT = bf16_t)
+template <class G, int OB, int PF, bool RING = false, typename GT = float>
+__global__ __launch_bounds__(256, 3) void conv_wgrad_slab(const void* __restrict__ X, const GT* __restrict__ Gr,
                                                           const uint8_t* __restrict__ bits, float* __restrict__ grad,
                                                           long w_off, long b_off, int chunk,
                                                           const int* __restrict__ act_idx,
@@ -1009,7 +1010,9 @@ __global__ __launch_bounds__(256, 3) void conv_wgrad_slab(const void* __restrict
     struct Regs {
       XRaw xr[RING ? 1 : SB::XIT];
       uint2 xq[RING ? XIT4 : 1][4];
-      float4 g0r[GIT], g1r[GIT];
+      // G rows: fp32 as two float4; bf16 kept raw (one uint4) until write_stage, so the load stays in flight
+      float4 g0r[sizeof(GT) == 2 ? 1 : GIT], g1r[sizeof(GT) == 2 ? 1 : GIT];
+      uint4 graw[sizeof(GT) == 2 ? GIT : 1];
       uint32_t gbr[GIT][3];
       bool gvr[GIT];
       int navail;
@@ -1072,8 +1075,12 @@ __global__ __launch_bounds__(256, 3) void conv_wgrad_slab(const void* __restrict
         Rg.gvr[j] = it < GROWS * 4 && rho < SB::NPOS && oh0 + ob < G::HO;
         if (Rg.gvr[j]) {
           const long go = sg * G::HOWO + (oh0 + ob) * G::WO + ow;
-          Rg.g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
-          Rg.g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+          if constexpr (sizeof(GT) == 2) {
+            Rg.graw[j] = *reinterpret_cast<const uint4*>(Gr + go * 8);
+          } else {
+            Rg.g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+            Rg.g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+          }
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
             const int slot = sub + 4 * k;
@@ -1130,8 +1137,18 @@ __global__ __launch_bounds__(256, 3) void conv_wgrad_slab(const void* __restrict
         const int it = tid + 256 * j;
         if (it >= GROWS * 4) continue;
         const int rho = it >> 2, sub = it & 3;
-        const float gg[8] = {Rg.g0r[j].x, Rg.g0r[j].y, Rg.g0r[j].z, Rg.g0r[j].w,
-                             Rg.g1r[j].x, Rg.g1r[j].y, Rg.g1r[j].z, Rg.g1r[j].w};
+        float gg[8];
+        if constexpr (sizeof(GT) == 2) {
+          const uint32_t u[4] = {Rg.graw[j].x, Rg.graw[j].y, Rg.graw[j].z, Rg.graw[j].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            gg[2 * e] = __uint_as_float(u[e] << 16);
+            gg[2 * e + 1] = __uint_as_float(u[e] & 0xFFFF0000u);
+          }
+        } else {
+          gg[0] = Rg.g0r[j].x; gg[1] = Rg.g0r[j].y; gg[2] = Rg.g0r[j].z; gg[3] = Rg.g0r[j].w;
+          gg[4] = Rg.g1r[j].x; gg[5] = Rg.g1r[j].y; gg[6] = Rg.g1r[j].z; gg[7] = Rg.g1r[j].w;
+        }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           const int slot = sub + 4 * k;
@@ -1332,13 +1349,16 @@ struct DGM {
   static constexpr int KSMAX = NTAP * DG_NSMAX / 4;         // 32-wide k-steps at 12 slots
 };
 
-template <class G>
+// OT = float, or bf16_t for the first layer's input gradient (read only by the slab wgrad, which rounds it to
+// bf16 for its MFMAs anyway): half of the largest activation-gradient stream of the update (1.48 GB fp32 at
+// the bench shape) is never written or re-read.
+template <class G, typename OT = float>
 __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
                                                           const float* __restrict__ flat, long w_off, int chunk,
                                                           const int* __restrict__ act_idx,
                                                           const int* __restrict__ act_cnt, int layer, int L, int M,
                                                           int P, int E, int T, long bits_rows, float g_scale,
-                                                          float* __restrict__ dX, int samples_per_wg) {
+                                                          OT* __restrict__ dX, int samples_per_wg) {
   using D = DGM<G>;
   constexpr int S = D::S;
   __shared__ __attribute__((aligned(16))) bf16_t Gs[G::HOWO * DG_PSTR];           // [pos][slot][c] + pad
@@ -1453,23 +1473,26 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
           if (spo >= D::NSP) continue;
           const int io = spo / D::NJ, jo = spo - io * D::NJ;
           const int ih = S * io + ph, iw = S * jo + pw;
-          if (ih < G::HIN && iw < G::WIN) dX[(sg * (G::HIN * G::WIN) + ih * G::WIN + iw) * 8 + ci] = acc[nt][r];
+          if (ih < G::HIN && iw < G::WIN) {
+            if constexpr (sizeof(OT) == 2) dX[(sg * (G::HIN * G::WIN) + ih * G::WIN + iw) * 8 + ci] = f2bf(acc[nt][r]);
+            else dX[(sg * (G::HIN * G::WIN) + ih * G::WIN + iw) * 8 + ci] = acc[nt][r];
+          }
         }
       }
     }
   }
 }
 
-template <class G>
+template <class G, typename OT = float>
 static int dgrad_mfma_t(const float* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,
-                        const int* ac, int layer, int L, int M, int P, int E, int T, long br, float gs, float* dX,
+                        const int* ac, int layer, int L, int M, int P, int E, int T, long br, float gs, OT* dX,
                         hipStream_t st) {
   const int nsamp = T * E;
   int spw = (nsamp + 31) / 32;                     // ~32 workgroups per path
   if (spw < 2) spw = 2;
   dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
-  conv_dgrad_mfma<G><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T,
-                                           br, gs, dX, spw);
+  conv_dgrad_mfma<G, OT><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E,
+                                               T, br, gs, dX, spw);
   return (int)hipGetLastError();
 }
 
@@ -1558,8 +1581,8 @@ static int fwd_slab_t(const void* X, void* Y, void* bits, const void* Wc, const 
   return (int)hipGetLastError();
 }
 
-template <class G, int OB, bool RING = false>
-static int wgrad_slab_t(const void* X, const float* Gr, const void* bits, float* grad, long w_off, long b_off,
+template <class G, int OB, bool RING = false, typename GT = float>
+static int wgrad_slab_t(const void* X, const GT* Gr, const void* bits, float* grad, long w_off, long b_off,
                         int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, long br,
                         float is, float gs, hipStream_t st, const uint8_t* fcv = nullptr, int nslots = 0) {
   using SB = Slab<G, OB>;
@@ -1569,10 +1592,10 @@ static int wgrad_slab_t(const void* X, const float* Gr, const void* bits, float*
   if (upw < 8) upw = 8;
   dim3 grid((unsigned)((units + upw - 1) / upw), P);
   if (WGRAD_PF >= 2)
-    conv_wgrad_slab<G, OB, 2, RING><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai,
+    conv_wgrad_slab<G, OB, 2, RING, GT><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai,
                                                           ac, layer, L, M, P, E, T, br, (int)upw, is, gs, fcv, nslots);
   else
-    conv_wgrad_slab<G, OB, 1, RING><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai,
+    conv_wgrad_slab<G, OB, 1, RING, GT><<<grid, 256, 0, st>>>(X, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai,
                                                           ac, layer, L, M, P, E, T, br, (int)upw, is, gs, fcv, nslots);
   return (int)hipGetLastError();
 }
@@ -1736,5 +1759,31 @@ int fast_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w
   DG(C2) DG(C3)
 #undef DG
   return 0;
+}
+
+// bf16 first-layer input gradient: the second layer's dgrad writes dX in bf16 and the first layer's slab
+// wgrad reads it (reference geometry only: 160x120x4 / 8x8 s4 -> 39x29x8 / 4x4 s2).  1: handled, 0: not
+// specialised (the caller must then keep that gradient in fp32), <0: error.
+int fast_conv_dgrad_bf16out(const float* Gr, const void* bits, const float* flat, long w_off, int chunk,
+                            const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH,
+                            int KW, int S, int P, int E, int T, long br, float gs, void* dX, hipStream_t st) {
+  if (M > 10 || !DGRAD_MFMA || !is_shape<C2>(Hin, Win, Cin, KH, KW, S, 0)) return 0;
+  const int rc = dgrad_mfma_t<C2, bf16_t>(Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs,
+                                          (bf16_t*)dX, st);
+  return rc ? -rc : 1;
+}
+
+int fast_conv_wgrad_bf16g(const void* X, int u8in, const void* Gr, const void* bits, float* grad, long w_off,
+                          long b_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin,
+                          int Win, int Cin, int KH, int KW, int S, int P, int E, int T, long br, float is, float gs,
+                          hipStream_t st) {
+  if (M > 2 * NCT || !SLAB_WGRAD || !is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) return 0;
+  const bf16_t* g = (const bf16_t*)Gr;
+  const int rc = WGRAD_OB == 3
+                     ? wgrad_slab_t<C1, 3, false, bf16_t>(X, g, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M,
+                                                          P, E, T, br, is, gs, st)
+                     : wgrad_slab_t<C1, 2, false, bf16_t>(X, g, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M,
+                                                          P, E, T, br, is, gs, st);
+  return rc ? -rc : 1;
 }
 }

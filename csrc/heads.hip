@@ -67,6 +67,103 @@ __global__ __launch_bounds__(256) void heads_fwd_sample_kernel(
   }
 }
 
+// Lane-per-sample variant (F % 32 == 0): a workgroup owns 64 samples, lane = sample; the policy and value
+// weights are staged once per workgroup in LDS as [F][AM+1] (broadcast reads), wave w sums the features
+// [w*F/4, (w+1)*F/4) of its lane's sample from 16-byte loads, the 4 partials meet in LDS in wave order
+// and wave 0 adds the biases and samples one action per lane.  (The wave-per-sample kernel spends most of
+// its time in A+1 cross-lane reductions per sample.)
+DEVI void ldfeat8(const bf16_t* p, float* x) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    x[2 * i] = __uint_as_float(u[i] << 16);
+    x[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+  }
+}
+DEVI void ldfeat8(const float* p, float* x) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+}
+
+template <int AM, typename FT>
+__global__ __launch_bounds__(256) void heads_fwd_lanes_kernel(
+    const FT* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
+    int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
+    const long long* __restrict__ ctr, int t, int T, int greedy) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  constexpr int AW = AM + 1;
+  float* Wl = hsm;                       // [F][AW]: policy weights (zero padded to AM) + value weight
+  float* red = hsm + F * AW;             // [3][AW][64]
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < F * AW; i += 256) {
+    const int f = i / AW, j = i - f * AW;
+    Wl[i] = j == AM ? flat[vw + f] : (j < A ? flat[pw + (long)f * A + j] : 0.f);
+  }
+  __syncthreads();
+  const int b = blockIdx.x * 64 + l;
+  const bool valid = b < B;
+  const int fq = F >> 2;
+  const int f0 = w * fq;
+  float acc[AW];
+#pragma unroll
+  for (int j = 0; j < AW; ++j) acc[j] = 0.f;
+  const FT* fr = feat + (long)(valid ? b : 0) * F;
+  for (int f = f0; f < f0 + fq; f += 8) {
+    float x[8];
+    ldfeat8(fr + f, x);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const float* wr = Wl + (f + jj) * AW;
+#pragma unroll
+      for (int j = 0; j < AW; ++j) acc[j] += x[jj] * wr[j];
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < AW; ++j) red[((w - 1) * AW + j) * 64 + l] = acc[j];
+  }
+  __syncthreads();
+  if (w != 0 || !valid) return;
+#pragma unroll
+  for (int j = 0; j < AW; ++j) acc[j] = ((acc[j] + red[j * 64 + l]) + red[(AW + j) * 64 + l]) + red[(2 * AW + j) * 64 + l];
+  const uint32_t stepkey = (uint32_t)(ctr[0] * T + t);
+  int best = 0;
+  float bv = -3.0e38f;
+#pragma unroll
+  for (int j = 0; j < AM; ++j) {
+    if (j < A) {
+      const float lg = acc[j] + flat[pb + j];
+      logits[(long)b * A + j] = lg;
+      float sc = lg;
+      if (!greedy) sc += -__logf(-__logf(u01(seed, stepkey, (uint32_t)b, (uint32_t)j)));
+      if (sc > bv) { bv = sc; best = j; }
+    }
+  }
+  value[b] = acc[AM] + flat[vb];
+  actions[b] = best;
+}
+
+template <typename FT>
+static bool heads_fwd_lanes_launch(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
+                                   int A, int B, float* logits, float* value, int* actions, unsigned seed,
+                                   const long long* ctr, int t, int T, int greedy, hipStream_t stream) {
+  if (F % 32 != 0 || A > 18) return false;
+  const unsigned g = (unsigned)((B + 63) / 64);
+  if (A <= 8) {
+    const size_t sm = (size_t)(F * 9 + 3 * 9 * 64) * 4;
+    if (sm > 64 * 1024) return false;
+    heads_fwd_lanes_kernel<8, FT><<<g, 256, sm, stream>>>((const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits,
+                                                          value, actions, seed, ctr, t, T, greedy);
+  } else {
+    const size_t sm = (size_t)(F * 19 + 3 * 19 * 64) * 4;
+    if (sm > 64 * 1024) return false;
+    heads_fwd_lanes_kernel<18, FT><<<g, 256, sm, stream>>>((const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits,
+                                                           value, actions, seed, ctr, t, T, greedy);
+  }
+  return true;
+}
+
 // logits/values/actions/rewards/dones: [T][B](...); vboot [B]
 __global__ __launch_bounds__(256) void a2c_grad_kernel(
     const float* __restrict__ logits, const float* __restrict__ values, const int* __restrict__ actions,
@@ -257,8 +354,11 @@ int launch_heads_fwd_sample(const void* feat, int F, const float* flat, long pw,
                             int B, float* logits, float* value, int* actions, unsigned seed, const long long* ctr,
                             int t, int T, int greedy, hipStream_t stream) {
   if (A > AMAX || A < 1) return -1;
-  heads_fwd_sample_kernel<bf16_t><<<(B + 3) / 4, 256, 0, stream>>>((const bf16_t*)feat, F, flat, pw, pb, vw, vb, A,
-                                                                    B, logits, value, actions, seed, ctr, t, T, greedy);
+  if (!heads_fwd_lanes_launch<bf16_t>(feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T,
+                                      greedy, stream))
+    heads_fwd_sample_kernel<bf16_t><<<(B + 3) / 4, 256, 0, stream>>>((const bf16_t*)feat, F, flat, pw, pb, vw, vb,
+                                                                      A, B, logits, value, actions, seed, ctr, t, T,
+                                                                      greedy);
   return (int)hipGetLastError();
 }
 
@@ -266,8 +366,11 @@ int launch_heads_fwd_sample_f32(const void* feat, int F, const float* flat, long
                                 int A, int B, float* logits, float* value, int* actions, unsigned seed,
                                 const long long* ctr, int t, int T, int greedy, hipStream_t stream) {
   if (A > AMAX || A < 1) return -1;
-  heads_fwd_sample_kernel<float><<<(B + 3) / 4, 256, 0, stream>>>((const float*)feat, F, flat, pw, pb, vw, vb, A, B,
-                                                                   logits, value, actions, seed, ctr, t, T, greedy);
+  if (!heads_fwd_lanes_launch<float>(feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T,
+                                     greedy, stream))
+    heads_fwd_sample_kernel<float><<<(B + 3) / 4, 256, 0, stream>>>((const float*)feat, F, flat, pw, pb, vw, vb, A,
+                                                                     B, logits, value, actions, seed, ctr, t, T,
+                                                                     greedy);
   return (int)hipGetLastError();
 }
 

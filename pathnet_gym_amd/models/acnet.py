@@ -29,12 +29,13 @@ from .pathnet import ParamStore, heads_ref, lstm_cell_ref, trunk_forward_ref
 
 class ACPathNet:
     def __init__(self, cfg: PathNetConfig, num_paths: int, device="cpu", backend: str = "torch",
-                 seed: int = 1, compute_dtype: str = "fp32", deterministic: bool = False):
+                 seed: int = 1, compute_dtype: Optional[str] = None, deterministic: bool = False):
         self.cfg = cfg
         self.P = num_paths
         self.device = torch.device(device)
         self.backend = backend
-        self.compute_dtype = compute_dtype
+        # HIP backend: "bf16" (default) or "fp32" operands; the torch backend always computes in fp32
+        self.compute_dtype = compute_dtype or ("bf16" if backend == "hip" else "fp32")
         self.deterministic = deterministic
         self.store = ParamStore(cfg, self.device, seed)
         self.store.flat.requires_grad_(True)

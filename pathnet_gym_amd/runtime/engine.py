@@ -76,7 +76,11 @@ class HipEngine:
             b, rows = hp.alloc_bits(l, T + 1, B)
             self.bits.append(b)
             self.bits_rows.append(rows)
-            self.grads.append(torch.zeros(T * B, g.out_feat, dtype=torch.float32, device=dev))
+            # grads[0] (first layer's output gradient, 1.5 GB fp32 at the bench shape) in bf16 where the
+            # specialised second-layer dgrad / first-layer wgrad handle it
+            g0_bf16 = l == 0 and hp.grad0_bf16_ok(self.ring)
+            self.grads.append(torch.zeros(T * B, g.out_feat, dtype=torch.bfloat16 if g0_bf16 else torch.float32,
+                                          device=dev))
         self.logits = torch.zeros(T + 1, B, A, device=dev)
         self.values = torch.zeros(T + 1, B, device=dev)
         self.actions = torch.zeros(T + 1, B, dtype=torch.int32, device=dev)

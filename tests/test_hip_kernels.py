@@ -261,6 +261,25 @@ def test_heads_and_a2c_grad(hip_lib):
         assert rel(gflat[s.offset:s.offset + s.numel], flat.grad[s.offset:s.offset + s.numel]) < 1e-4, name
 
 
+@pytest.mark.parametrize("A,F", [(18, 256), (6, 96), (3, 64)])
+def test_heads_fwd_action_and_feature_widths(hip_lib, A, F):
+    """Lane-per-sample heads forward for A <= 8 and A <= 18, a partial last workgroup, several F."""
+    cfg = PathNetConfig(L=2, M=4, N=2, input_shape=(4,), layers=[LayerSpec("fc", 64), LayerSpec("fc", F)],
+                        trunk_scale="none", num_actions=A)
+    P, E = 3, 16
+    m = make_model(cfg, P, random_masks(P, cfg.L, cfg.M, cfg.N, with_edge=False))
+    B = P * E + 5
+    feat = torch.randn(B, F, device=DEV).to(torch.bfloat16)
+    logits = torch.zeros(B, A, device=DEV)
+    values = torch.zeros(B, device=DEV)
+    actions = torch.zeros(B, dtype=torch.int32, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int64, device=DEV)
+    m.hip.heads_fwd(feat, logits, values, actions, 7, ctr, 0, 1, greedy=True)
+    lr_, vr_ = heads_ref(m.store, feat.float())
+    assert rel(logits, lr_.detach()) < 1e-4 and rel(values, vr_.detach()) < 1e-4
+    assert torch.equal(actions.long(), logits.argmax(-1))
+
+
 def test_rmsprop_kernel_matches_torch(hip_lib):
     from pathnet_gym_amd.algo.optim import RMSPropTF
     from pathnet_gym_amd.runtime.engine import HipEngine
@@ -554,6 +573,37 @@ def test_engine_gradient_vs_plain_fp32_oracle(hip_lib):
         assert v < FP32_SEG_BUDGET, (k, n, v)
 
 
+def test_bf16_first_layer_gradient_matches_fp32(hip_lib):
+    """engine.grads[0] in bf16 (second-layer MFMA dgrad writes it, first-layer slab wgrad reads it) vs the
+    fp32 buffer on the same rollout: only the bf16 rounding of dL/d(conv1 output) separates them."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 4
+    cfg.use_graph = False
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng = tr.engine
+    assert eng.grads[0].dtype == torch.bfloat16 and not eng.ring
+    tr.update()
+    eng._rollout_backward_body()
+    torch.cuda.synchronize()
+    g_bf = eng.grad_flat.clone()
+    g0_bf = eng.grads[0].float().clone()
+    eng.grads[0] = torch.zeros(eng.grads[0].shape, dtype=torch.float32, device=DEV)
+    eng.grad_flat.zero_()
+    T, B, L = eng.T, eng.B, len(tr.model.hip.geoms)
+    tr.model.hip.heads_bwd(eng.acts[L - 1][:T].reshape(T * B, -1), eng.dlogits.reshape(T * B, -1),
+                           eng.dvalue.reshape(-1), eng.grad_flat, eng.grads[L - 1], task=tr.model.task)
+    eng._layer_bwd_all(T)
+    torch.cuda.synchronize()
+    assert rel(g0_bf, eng.grads[0]) < 5e-3
+    for s in tr.model.store.layout.segments:
+        a, b = g_bf[s.offset:s.offset + s.numel], eng.grad_flat[s.offset:s.offset + s.numel]
+        if b.norm() < 1e-7:
+            assert a.norm() < 1e-5, s.name
+            continue
+        assert rel(a, b) < (2e-2 if s.layer == 0 else 1e-3), (s.name, rel(a, b))
+
+
 def test_frame_ring_stacks_match_packed_env(hip_lib):
     """Frame-ring rollout (single-frame writes + first-valid-channel bytes) reproduces, bit for bit,
     the packed 4-frame stacks the packed Pong kernel produces for the same actions, resets included."""
@@ -816,6 +866,28 @@ def test_device_ga_matches_host_mirror(hip_lib):
             assert int(ic[l, j]) == len(users)
             assert ip[l, j, :len(users)].tolist() == users
             assert isl[l, j, :len(users)].tolist() == [int(expr[p, l, :j].sum()) for p in users]
+    # more than one 64-path wave chunk per module (the inverse lists are built with ballots)
+    big = CounterPopulation(150, L, M, N, B, seed=5, concurrent=C)
+    gb = torch.from_numpy(big.genotypes.astype(np.uint8)).to(DEV)
+    fb = torch.from_numpy(big.frozen.astype(np.uint8)).to(DEV)
+    Pl = 150
+    mask = torch.zeros(Pl, L, M, device=DEV)
+    ai = torch.zeros(Pl, L, M, dtype=torch.int32, device=DEV)
+    ac = torch.zeros(Pl, L, dtype=torch.int32, device=DEV)
+    ip = torch.full((L, M, Pl), -5, dtype=torch.int32, device=DEV)
+    isl = torch.full_like(ip, -5)
+    ic = torch.zeros(L, M, dtype=torch.int32, device=DEV)
+    _lib.call("launch_ga_compact", gb.data_ptr(), fb.data_ptr(), 0, Pl, L, M, mask.data_ptr(), ai.data_ptr(),
+              ac.data_ptr(), ip.data_ptr(), isl.data_ptr(), ic.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    expr = big.expressed()
+    for l in range(L):
+        for j in range(M):
+            users = [p for p in range(Pl) if expr[p, l, j] > 0.5]
+            assert int(ic[l, j]) == len(users)
+            assert ip[l, j, :len(users)].tolist() == users
+            assert isl[l, j, :len(users)].tolist() == [int(expr[p, l, :j].sum()) for p in users]
+            assert (ip[l, j, len(users):] == 0).all() and (isl[l, j, len(users):] == 0).all()
 
 
 def test_trainer_device_ga_stays_in_sync(hip_lib):
