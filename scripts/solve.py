@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--same-path", action="store_true",
                     help="every path starts from the same random N-module genotype (ablation)")
     ap.add_argument("--out", default=None, help="also write the final JSON record to this file")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"], help="HIP engine compute dtype")
+    ap.add_argument("--deterministic", action="store_true", help="fixed-order gradient reductions")
     args = ap.parse_args()
 
     import torch
@@ -96,6 +98,9 @@ def main():
         cfg.ga.fitness_window = args.fitness_window
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
+    if args.dtype is not None:
+        cfg.compute_dtype = args.dtype
+    cfg.deterministic = bool(args.deterministic)
     cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
     if cfg.backend in ("hip", "auto") and ctx.device.type == "cuda":
         from pathnet_gym_amd import _build
