@@ -158,6 +158,154 @@ DEVI int scene_gray(const Scene& S, const uint8_t* band, int r, int c) {
 }
 }  // namespace pong
 
+namespace pong {
+// The 4 new-frame pixels of output quad (y, xq) (row word ri = rowinfo[y]): the row's static value, the
+// score-digit box from dlut, or -- on paddle / ball rows whose columns touch the same rectangle -- the 4 taps
+// evaluated analytically (all 4 pixels' taps and weights in 4 vector LDS reads, branch-free).
+DEVI void quad_gray(const Scene& S, int y, int xq, int ri, const int* tab, const int* colmask, const int* quadmask,
+                    const uint8_t* dlut, uint32_t* f4) {
+  const uint32_t vr = (uint32_t)(ri & 0xFF);
+  f4[0] = f4[1] = f4[2] = f4[3] = vr;
+  const int rm = ri >> 8;
+  const int dq = xq >= 4 && xq < 10 ? (xq - 4) * 4 : (xq >= 19 && xq < 25 ? 24 + (xq - 19) * 4 : -1);
+  if (y < DL_R && dq >= 0) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(&dlut[y * 48 + dq]);
+    f4[0] = w & 0xFFu; f4[1] = (w >> 8) & 0xFFu; f4[2] = (w >> 16) & 0xFFu; f4[3] = w >> 24;
+  } else if (rm && (rm & quadmask[xq])) {
+    const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
+    const int4 xs0v = *reinterpret_cast<const int4*>(&tab[4 * 160 + xq * 4]);
+    const int4 xs1v = *reinterpret_cast<const int4*>(&tab[5 * 160 + xq * 4]);
+    const int4 cx0v = *reinterpret_cast<const int4*>(&tab[6 * 160 + xq * 4]);
+    const int4 cx1v = *reinterpret_cast<const int4*>(&tab[7 * 160 + xq * 4]);
+    const int4 cmv = *reinterpret_cast<const int4*>(&colmask[xq * 4]);
+    const int xs0a[4] = {xs0v.x, xs0v.y, xs0v.z, xs0v.w}, xs1a[4] = {xs1v.x, xs1v.y, xs1v.z, xs1v.w};
+    const int cx0a[4] = {cx0v.x, cx0v.y, cx0v.z, cx0v.w}, cx1a[4] = {cx1v.x, cx1v.y, cx1v.z, cx1v.w};
+    const int cma[4] = {cmv.x, cmv.y, cmv.z, cmv.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ra = scene_gray_pf(S, ys0, xs0a[e]) * cx0a[e] + scene_gray_pf(S, ys0, xs1a[e]) * cx1a[e];
+      const int rb = scene_gray_pf(S, ys1, xs0a[e]) * cx0a[e] + scene_gray_pf(S, ys1, xs1a[e]) * cx1a[e];
+      int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+      v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      f4[e] = (rm & cma[e]) ? (uint32_t)v : f4[e];
+    }
+  }
+}
+
+// One env step's game physics on wave 0 of the env's workgroup (scalar code, frameskip sub-frames, reward,
+// done, auto-reset); publishes the new state + done flag to LDS phys[] and writes the per-env outputs.
+// fc_in != nullptr (frame ring): fc_out = done ? 3 : max(fc_in - 1, 0).
+DEVI void physics_wave0(int env, int* __restrict__ state, uint32_t* __restrict__ counter, const int* __restrict__ actions,
+                        int n_actions, uint32_t seed, int frameskip, int max_steps, int no_op_max, int* phys,
+                        float* __restrict__ reward_out, uint8_t* __restrict__ done_out,
+                        float* __restrict__ epret_out, const uint8_t* __restrict__ fc_in,
+                        uint8_t* __restrict__ fc_out) {
+  St st;
+#pragma unroll
+  for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
+  uint32_t ctr = (uint32_t)__builtin_amdgcn_readfirstlane((int)counter[env]);
+  int a = __builtin_amdgcn_readfirstlane(actions[env]);
+  if (a >= n_actions || a < 0) a = 0;                    // game_state.py:38-39
+  const int up = (a == 2 || a == 4), down = (a == 3 || a == 5);
+  int reward = 0;
+  for (int f = 0; f < frameskip; ++f) reward += subframe(st, up, down, seed, (uint32_t)env, ctr);
+  ctr += 1;
+  st.s[STEPS] += 1;
+  st.s[EPRET] += reward;
+  const bool done = st.s[PS] >= WIN_SCORE || st.s[CS] >= WIN_SCORE || st.s[STEPS] >= max_steps;
+  const int epret = st.s[EPRET];
+  if (done) {
+    reset_state(st, seed, (uint32_t)env, ctr, no_op_max, frameskip);
+    ctr += 1;
+  }
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NSTATE; ++i) {
+      state[env * NSTATE + i] = st.s[i];
+      phys[i] = st.s[i];
+    }
+    phys[NSTATE] = done ? 1 : 0;
+    counter[env] = ctr;
+    reward_out[env] = (float)reward;
+    done_out[env] = done ? 1 : 0;
+    epret_out[env] = done ? (float)epret : 0.f;
+    if (fc_in) fc_out[env] = done ? 3 : (uint8_t)max((int)fc_in[env] - 1, 0);
+  }
+}
+
+// Per-workgroup scene tables of the fused render (pong_step_kernel): the row / column
+// rectangle masks, per-row static colour, score band and score-digit box.  Contains two barriers.
+template <int NTH>
+DEVI void scene_tables(const St& st, Scene& S, const int* tab, int* rowinfo, int* colmask, int* quadmask,
+                       uint8_t* band, uint8_t* dlut, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball) {
+  S.cy = st.s[CY] >> 4;   // floor division by U=16 (values are non-negative)
+  S.py = st.s[PY] >> 4;
+  S.bx = st.s[BX] >= 0 ? st.s[BX] / U : -((-st.s[BX] + U - 1) / U);   // floor
+  S.by = st.s[BY] >= 0 ? st.s[BY] / U : -((-st.s[BY] + U - 1) / U);
+  S.vis = st.s[SERVE] == 0;
+  {
+    const int cs_t = st.s[CS] / 10, cs_o = st.s[CS] % 10, ps_t = st.s[PS] / 10, ps_o = st.s[PS] % 10;
+    S.dmask[0] = cs_t > 0 ? DIGITS[cs_t] : 0;        // tens digit only when non-zero
+    S.dmask[1] = DIGITS[cs_o];
+    S.dmask[2] = ps_t > 0 ? DIGITS[ps_t] : 0;
+    S.dmask[3] = DIGITS[ps_o];
+  }
+  S.g_bg = g_bg; S.g_wall = g_wall; S.g_cpu = g_cpu; S.g_player = g_player; S.g_ball = g_ball;
+  // source rectangles [r0, r1) x [c0, c1): cpu digits, player digits, ball, player, cpu
+  const int by0 = S.vis ? S.by : -1000, by1 = S.vis ? S.by + BALL_H : -1000;   // matches no row when hidden
+  const int R0[5] = {SCORE_ROW0, SCORE_ROW0, by0, S.py, S.cy};
+  const int R1[5] = {SCORE_ROW0 + 5 * DIGIT_SCALE, SCORE_ROW0 + 5 * DIGIT_SCALE, by1, S.py + PADDLE_H,
+                     S.cy + PADDLE_H};
+  const int C0[5] = {24, 104, S.bx, PLAYER_X, CPU_X};
+  const int C1[5] = {40 + 3 * DIGIT_SCALE, 120 + 3 * DIGIT_SCALE, S.bx + BALL_W, PLAYER_X + PADDLE_W,
+                     CPU_X + PADDLE_W};
+  for (int i = threadIdx.x; i < BAND_R * BAND_C; i += NTH) {
+    const int r = SCORE_ROW0 + i / BAND_C, bc = i - (i / BAND_C) * BAND_C;
+    const int c = bc < 28 ? 24 + bc : 104 + (bc - 28);
+    int g = S.g_bg;
+    if (digit_lit(S.dmask[0], r, c, 24) || digit_lit(S.dmask[1], r, c, 40)) g = S.g_cpu;
+    else if (digit_lit(S.dmask[2], r, c, 104) || digit_lit(S.dmask[3], r, c, 120)) g = S.g_player;
+    band[i] = (uint8_t)g;
+  }
+  for (int i = threadIdx.x; i < OBS_H + OBS_W; i += NTH) {
+    if (i < OBS_H) {
+      const int ys0 = tab[0 * 160 + i], ys1 = tab[1 * 160 + i], cy0 = tab[2 * 160 + i], cy1 = tab[3 * 160 + i];
+      int m = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) m |= (ys1 >= R0[k] && ys0 < R1[k]) ? (1 << k) : 0;
+      int v = (static_gray(S, ys0) * cy0 + static_gray(S, ys1) * cy1 + 1024) >> 11;
+      v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      rowinfo[i] = v | (m << 8);
+    } else {
+      const int x = i - OBS_H;
+      const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x];
+      int m = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) m |= (xs1 >= C0[k] && xs0 < C1[k]) ? (1 << k) : 0;
+      colmask[x] = m;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < OBS_W / 4)
+    quadmask[threadIdx.x] = colmask[4 * threadIdx.x] | colmask[4 * threadIdx.x + 1] | colmask[4 * threadIdx.x + 2] |
+                            colmask[4 * threadIdx.x + 3];
+  // score-digit output box (rows < DL_R, quads 4..9 and 19..24 = x 16..39 and 76..99: every output
+  // pixel whose taps can reach a digit), each pixel evaluated once per workgroup from the LDS band
+  // map instead of inside the (divergent) quad loop
+  for (int i = threadIdx.x; i < DL_R * 48; i += NTH) {
+    const int yy = i / 48, lx = i - yy * 48;
+    const int x = lx < 24 ? 16 + lx : 76 + (lx - 24);
+    const int ys0 = tab[0 * 160 + yy], ys1 = tab[1 * 160 + yy], cy0 = tab[2 * 160 + yy], cy1 = tab[3 * 160 + yy];
+    const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x], cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
+    const int ra = scene_gray(S, band, ys0, xs0) * cx0 + scene_gray(S, band, ys0, xs1) * cx1;
+    const int rb = scene_gray(S, band, ys1, xs0) * cx0 + scene_gray(S, band, ys1, xs1) * cx1;
+    const int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+    dlut[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+  }
+  __syncthreads();
+}
+}  // namespace pong
+
 // state [B][12] int32, counter [B] uint32, actions [B] int32 (any int; >= n_actions remapped to 0)
 // obs_in/obs_out [B][160*120] uint32 (4 stacked uint8 frames), tables [8][160] int32
 //
@@ -186,39 +334,9 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   // CU with the other workgroups there, so running it redundantly in every wave made the SALU the
   // kernel's bottleneck), published through LDS ---
   __shared__ int phys[NSTATE + 4];
-  if (threadIdx.x < 64) {
-    St st;
-#pragma unroll
-    for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
-    uint32_t ctr = (uint32_t)__builtin_amdgcn_readfirstlane((int)counter[env]);
-    int a = __builtin_amdgcn_readfirstlane(actions[env]);
-    if (a >= n_actions || a < 0) a = 0;                    // game_state.py:38-39
-    const int up = (a == 2 || a == 4), down = (a == 3 || a == 5);
-    int reward = 0;
-    for (int f = 0; f < frameskip; ++f) reward += subframe(st, up, down, seed, (uint32_t)env, ctr);
-    ctr += 1;
-    st.s[STEPS] += 1;
-    st.s[EPRET] += reward;
-    const bool done = st.s[PS] >= WIN_SCORE || st.s[CS] >= WIN_SCORE || st.s[STEPS] >= max_steps;
-    const int epret = st.s[EPRET];
-    if (done) {
-      reset_state(st, seed, (uint32_t)env, ctr, no_op_max, frameskip);
-      ctr += 1;
-    }
-    if (threadIdx.x == 0) {
-#pragma unroll
-      for (int i = 0; i < NSTATE; ++i) {
-        state[env * NSTATE + i] = st.s[i];
-        phys[i] = st.s[i];
-      }
-      phys[NSTATE] = done ? 1 : 0;
-      counter[env] = ctr;
-      reward_out[env] = (float)reward;
-      done_out[env] = done ? 1 : 0;
-      epret_out[env] = done ? (float)epret : 0.f;
-      if constexpr (RING) fc_out[env] = done ? 3 : (uint8_t)max((int)fc_in[env] - 1, 0);
-    }
-  }
+  if (threadIdx.x < 64)
+    physics_wave0(env, state, counter, actions, n_actions, seed, frameskip, max_steps, no_op_max, phys, reward_out,
+                  done_out, epret_out, RING ? fc_in : nullptr, fc_out);
   PONG_STAMP(1);
   __syncthreads();    // tab[] staged and the new state published
   PONG_STAMP(2);
@@ -239,74 +357,10 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   __shared__ int rowinfo[OBS_H];     // vrow | (rect mask << 8)
   __shared__ __attribute__((aligned(16))) int colmask[OBS_W];
   __shared__ int quadmask[OBS_W / 4];    // OR of the 4 columns' masks per quad
-  Scene S;
-  S.cy = st.s[CY] >> 4;   // floor division by U=16 (values are non-negative)
-  S.py = st.s[PY] >> 4;
-  S.bx = st.s[BX] >= 0 ? st.s[BX] / U : -((-st.s[BX] + U - 1) / U);   // floor
-  S.by = st.s[BY] >= 0 ? st.s[BY] / U : -((-st.s[BY] + U - 1) / U);
-  S.vis = st.s[SERVE] == 0;
-  {
-    const int cs_t = st.s[CS] / 10, cs_o = st.s[CS] % 10, ps_t = st.s[PS] / 10, ps_o = st.s[PS] % 10;
-    S.dmask[0] = cs_t > 0 ? DIGITS[cs_t] : 0;        // tens digit only when non-zero
-    S.dmask[1] = DIGITS[cs_o];
-    S.dmask[2] = ps_t > 0 ? DIGITS[ps_t] : 0;
-    S.dmask[3] = DIGITS[ps_o];
-  }
-  S.g_bg = g_bg; S.g_wall = g_wall; S.g_cpu = g_cpu; S.g_player = g_player; S.g_ball = g_ball;
-  // source rectangles [r0, r1) x [c0, c1): cpu digits, player digits, ball, player, cpu
-  const int by0 = S.vis ? S.by : -1000, by1 = S.vis ? S.by + BALL_H : -1000;   // matches no row when hidden
-  const int R0[5] = {SCORE_ROW0, SCORE_ROW0, by0, S.py, S.cy};
-  const int R1[5] = {SCORE_ROW0 + 5 * DIGIT_SCALE, SCORE_ROW0 + 5 * DIGIT_SCALE, by1, S.py + PADDLE_H,
-                     S.cy + PADDLE_H};
-  const int C0[5] = {24, 104, S.bx, PLAYER_X, CPU_X};
-  const int C1[5] = {40 + 3 * DIGIT_SCALE, 120 + 3 * DIGIT_SCALE, S.bx + BALL_W, PLAYER_X + PADDLE_W,
-                     CPU_X + PADDLE_W};
   __shared__ uint8_t band[BAND_R * BAND_C];
-  for (int i = threadIdx.x; i < BAND_R * BAND_C; i += 256) {
-    const int r = SCORE_ROW0 + i / BAND_C, bc = i - (i / BAND_C) * BAND_C;
-    const int c = bc < 28 ? 24 + bc : 104 + (bc - 28);
-    int g = S.g_bg;
-    if (digit_lit(S.dmask[0], r, c, 24) || digit_lit(S.dmask[1], r, c, 40)) g = S.g_cpu;
-    else if (digit_lit(S.dmask[2], r, c, 104) || digit_lit(S.dmask[3], r, c, 120)) g = S.g_player;
-    band[i] = (uint8_t)g;
-  }
-  for (int i = threadIdx.x; i < OBS_H + OBS_W; i += 256) {
-    if (i < OBS_H) {
-      const int ys0 = tab[0 * 160 + i], ys1 = tab[1 * 160 + i], cy0 = tab[2 * 160 + i], cy1 = tab[3 * 160 + i];
-      int m = 0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) m |= (ys1 >= R0[k] && ys0 < R1[k]) ? (1 << k) : 0;
-      int v = (static_gray(S, ys0) * cy0 + static_gray(S, ys1) * cy1 + 1024) >> 11;
-      v = v < 0 ? 0 : (v > 255 ? 255 : v);
-      rowinfo[i] = v | (m << 8);
-    } else {
-      const int x = i - OBS_H;
-      const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x];
-      int m = 0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) m |= (xs1 >= C0[k] && xs0 < C1[k]) ? (1 << k) : 0;
-      colmask[x] = m;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < OBS_W / 4)
-    quadmask[threadIdx.x] = colmask[4 * threadIdx.x] | colmask[4 * threadIdx.x + 1] | colmask[4 * threadIdx.x + 2] |
-                            colmask[4 * threadIdx.x + 3];
-  // score-digit output box (rows < DL_R, quads 4..9 and 19..24 = x 16..39 and 76..99: every output
-  // pixel whose taps can reach a digit), each pixel evaluated once per workgroup from the LDS band
-  // map instead of inside the (divergent) quad loop
   __shared__ __attribute__((aligned(4))) uint8_t dlut[DL_R * 48];
-  for (int i = threadIdx.x; i < DL_R * 48; i += 256) {
-    const int yy = i / 48, lx = i - yy * 48;
-    const int x = lx < 24 ? 16 + lx : 76 + (lx - 24);
-    const int ys0 = tab[0 * 160 + yy], ys1 = tab[1 * 160 + yy], cy0 = tab[2 * 160 + yy], cy1 = tab[3 * 160 + yy];
-    const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x], cx0 = tab[6 * 160 + x], cx1 = tab[7 * 160 + x];
-    const int ra = scene_gray(S, band, ys0, xs0) * cx0 + scene_gray(S, band, ys0, xs1) * cx1;
-    const int rb = scene_gray(S, band, ys1, xs0) * cx0 + scene_gray(S, band, ys1, xs1) * cx1;
-    const int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
-    dlut[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
-  }
-  __syncthreads();
+  Scene S;
+  scene_tables<256>(st, S, tab, rowinfo, colmask, quadmask, band, dlut, g_bg, g_wall, g_cpu, g_player, g_ball);
   PONG_STAMP(3);
   const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OBS_H * OBS_W / 4);
   uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OBS_H * OBS_W / 4);
@@ -328,34 +382,8 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
       int yn = y + 8 + (xq + 16 >= QR ? 1 : 0);
       ri_next = rowinfo[yn < OBS_H ? yn : OBS_H - 1];
     }
-    const uint32_t vr = (uint32_t)(ri & 0xFF);
-    uint32_t f4[4] = {vr, vr, vr, vr};
-    const int rm = ri >> 8;
-    const int dq = xq >= 4 && xq < 10 ? (xq - 4) * 4 : (xq >= 19 && xq < 25 ? 24 + (xq - 19) * 4 : -1);
-    if (y < DL_R && dq >= 0) {
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(&dlut[y * 48 + dq]);
-      f4[0] = w & 0xFFu; f4[1] = (w >> 8) & 0xFFu; f4[2] = (w >> 16) & 0xFFu; f4[3] = w >> 24;
-    } else if (rm && (rm & quadmask[xq])) {
-      // paddle / ball rows: all 4 pixels' taps and weights in 4 vector LDS reads, branch-free
-      // scene evaluation, result kept only where the row AND column touch the same rectangle
-      const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
-      const int4 xs0v = *reinterpret_cast<const int4*>(&tab[4 * 160 + xq * 4]);
-      const int4 xs1v = *reinterpret_cast<const int4*>(&tab[5 * 160 + xq * 4]);
-      const int4 cx0v = *reinterpret_cast<const int4*>(&tab[6 * 160 + xq * 4]);
-      const int4 cx1v = *reinterpret_cast<const int4*>(&tab[7 * 160 + xq * 4]);
-      const int4 cmv = *reinterpret_cast<const int4*>(&colmask[xq * 4]);
-      const int xs0a[4] = {xs0v.x, xs0v.y, xs0v.z, xs0v.w}, xs1a[4] = {xs1v.x, xs1v.y, xs1v.z, xs1v.w};
-      const int cx0a[4] = {cx0v.x, cx0v.y, cx0v.z, cx0v.w}, cx1a[4] = {cx1v.x, cx1v.y, cx1v.z, cx1v.w};
-      const int cma[4] = {cmv.x, cmv.y, cmv.z, cmv.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ra = scene_gray_pf(S, ys0, xs0a[e]) * cx0a[e] + scene_gray_pf(S, ys0, xs1a[e]) * cx1a[e];
-        const int rb = scene_gray_pf(S, ys1, xs0a[e]) * cx0a[e] + scene_gray_pf(S, ys1, xs1a[e]) * cx1a[e];
-        int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
-        v = v < 0 ? 0 : (v > 255 ? 255 : v);
-        f4[e] = (rm & cma[e]) ? (uint32_t)v : f4[e];
-      }
-    }
+    uint32_t f4[4];
+    quad_gray(S, y, xq, ri, tab, colmask, quadmask, dlut, f4);
     if constexpr (RING) {
       outw[q] = f4[0] | (f4[1] << 8) | (f4[2] << 16) | (f4[3] << 24);
     } else {
@@ -427,6 +455,8 @@ __global__ void cartpole_step_kernel(float* __restrict__ state, int* __restrict_
     *reinterpret_cast<uint4*>(obs_bf16 + (long)b * 8) = o;
   }
 }
+
+
 
 extern "C" {
 int launch_pong_step(void* state, void* counter, const int* actions, int n_actions, const void* obs_in, void* obs_out,
