@@ -1352,8 +1352,9 @@ struct DGM {
 // OT = float, or bf16_t for the first layer's input gradient (read only by the slab wgrad, which rounds it to
 // bf16 for its MFMAs anyway): half of the largest activation-gradient stream of the update (1.48 GB fp32 at
 // the bench shape) is never written or re-read.
-template <class G, typename OT = float>
-__global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
+// GT = float, or bf16_t when this layer's output gradient was itself stored in bf16 by the next layer's dgrad.
+template <class G, typename OT = float, typename GT = float>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__ Gr, const uint8_t* __restrict__ bits,
                                                           const float* __restrict__ flat, long w_off, int chunk,
                                                           const int* __restrict__ act_idx,
                                                           const int* __restrict__ act_cnt, int layer, int L, int M,
@@ -1396,7 +1397,9 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
   // staging role: one thread per output position (the G row is shared by all slots), all slots' bits
   const int nslot = ns4 * 4;
   constexpr int GIT = (G::HOWO + 255) / 256;
-  float4 g0r[GIT], g1r[GIT];
+  // G rows: fp32 as two float4; bf16 kept raw (one uint4) and converted at staging time
+  float4 g0r[sizeof(GT) == 2 ? 1 : GIT], g1r[sizeof(GT) == 2 ? 1 : GIT];
+  uint4 graw[sizeof(GT) == 2 ? GIT : 1];
   uint8_t gbr[GIT][DG_NSMAX];
   auto load_sample = [&](int s) {
     const long sg = sample_global(p, s, E, PE, 0);
@@ -1405,8 +1408,12 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
       const int pos = tid + 256 * j;
       if (pos < G::HOWO) {
         const long go = sg * G::HOWO + pos;
-        g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
-        g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+        if constexpr (sizeof(GT) == 2) {
+          graw[j] = *reinterpret_cast<const uint4*>(Gr + go * 8);
+        } else {
+          g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+          g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+        }
 #pragma unroll
         for (int a = 0; a < DG_NSMAX; ++a) gbr[j][a] = a < cnt ? bits[(long)a * bits_rows + go] : (uint8_t)0;
       }
@@ -1419,8 +1426,19 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
     for (int j = 0; j < GIT; ++j) {
       const int pos = tid + 256 * j;
       if (pos < G::HOWO) {
-        const float gg[8] = {g0r[j].x * g_scale, g0r[j].y * g_scale, g0r[j].z * g_scale, g0r[j].w * g_scale,
-                             g1r[j].x * g_scale, g1r[j].y * g_scale, g1r[j].z * g_scale, g1r[j].w * g_scale};
+        float gg[8];
+        if constexpr (sizeof(GT) == 2) {
+          const uint32_t u[4] = {graw[j].x, graw[j].y, graw[j].z, graw[j].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            gg[2 * e] = __uint_as_float(u[e] << 16) * g_scale;
+            gg[2 * e + 1] = __uint_as_float(u[e] & 0xFFFF0000u) * g_scale;
+          }
+        } else {
+          gg[0] = g0r[j].x * g_scale; gg[1] = g0r[j].y * g_scale; gg[2] = g0r[j].z * g_scale;
+          gg[3] = g0r[j].w * g_scale; gg[4] = g1r[j].x * g_scale; gg[5] = g1r[j].y * g_scale;
+          gg[6] = g1r[j].z * g_scale; gg[7] = g1r[j].w * g_scale;
+        }
 #pragma unroll
         for (int a = 0; a < DG_NSMAX; ++a) {
           if (a < nslot) {
@@ -1483,15 +1501,15 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const float* __restric
   }
 }
 
-template <class G, typename OT = float>
-static int dgrad_mfma_t(const float* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,
+template <class G, typename OT = float, typename GT = float>
+static int dgrad_mfma_t(const GT* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,
                         const int* ac, int layer, int L, int M, int P, int E, int T, long br, float gs, OT* dX,
                         hipStream_t st) {
   const int nsamp = T * E;
   int spw = (nsamp + 31) / 32;                     // ~32 workgroups per path
   if (spw < 2) spw = 2;
   dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
-  conv_dgrad_mfma<G, OT><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E,
+  conv_dgrad_mfma<G, OT, GT><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E,
                                                T, br, gs, dX, spw);
   return (int)hipGetLastError();
 }
@@ -1761,24 +1779,49 @@ int fast_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w
   return 0;
 }
 
-// bf16 first-layer input gradient: the second layer's dgrad writes dX in bf16 and the first layer's slab
-// wgrad reads it (reference geometry only: 160x120x4 / 8x8 s4 -> 39x29x8 / 4x4 s2).  1: handled, 0: not
-// specialised (the caller must then keep that gradient in fp32), <0: error.
-int fast_conv_dgrad_bf16out(const float* Gr, const void* bits, const float* flat, long w_off, int chunk,
-                            const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH,
-                            int KW, int S, int P, int E, int T, long br, float gs, void* dX, hipStream_t st) {
-  if (M > 10 || !DGRAD_MFMA || !is_shape<C2>(Hin, Win, Cin, KH, KW, S, 0)) return 0;
-  const int rc = dgrad_mfma_t<C2, bf16_t>(Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs,
-                                          (bf16_t*)dX, st);
-  return rc ? -rc : 1;
+// bf16 activation gradients between the conv layers: the MFMA dgrad reads its G and writes its dX in fp32
+// or bf16 (flags), the slab wgrad reads a bf16 G (reference geometries only: 160x120x4 / 8x8 s4,
+// 39x29x8 / 4x4 s2, 18x13x8 / 3x3 s1).  1: handled, 0: not specialised (the caller must then keep that
+// gradient in fp32), <0: error.
+int fast_conv_dgrad_bf16(const void* Gr, int g_bf16, const void* bits, const float* flat, long w_off, int chunk,
+                         const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH,
+                         int KW, int S, int P, int E, int T, long br, float gs, void* dX, int dx_bf16,
+                         hipStream_t st) {
+  if (M > 10 || !DGRAD_MFMA) return 0;
+#define DGB(Gx)                                                                                               \
+  if (is_shape<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                            \
+    int rc;                                                                                                   \
+    if (g_bf16 && dx_bf16)                                                                                    \
+      rc = dgrad_mfma_t<Gx, bf16_t, bf16_t>((const bf16_t*)Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, \
+                                            br, gs, (bf16_t*)dX, st);                                         \
+    else if (g_bf16)                                                                                          \
+      rc = dgrad_mfma_t<Gx, float, bf16_t>((const bf16_t*)Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, \
+                                           br, gs, (float*)dX, st);                                           \
+    else if (dx_bf16)                                                                                         \
+      rc = dgrad_mfma_t<Gx, bf16_t, float>((const float*)Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, \
+                                           br, gs, (bf16_t*)dX, st);                                          \
+    else                                                                                                      \
+      rc = dgrad_mfma_t<Gx, float, float>((const float*)Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, \
+                                          gs, (float*)dX, st);                                                \
+    return rc ? -rc : 1;                                                                                      \
+  }
+  DGB(C2) DGB(C3)
+#undef DGB
+  return 0;
 }
 
 int fast_conv_wgrad_bf16g(const void* X, int u8in, const void* Gr, const void* bits, float* grad, long w_off,
                           long b_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin,
                           int Win, int Cin, int KH, int KW, int S, int P, int E, int T, long br, float is, float gs,
                           hipStream_t st) {
-  if (M > 2 * NCT || !SLAB_WGRAD || !is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) return 0;
+  if (M > 2 * NCT || !SLAB_WGRAD) return 0;
   const bf16_t* g = (const bf16_t*)Gr;
+  if (is_shape<C2>(Hin, Win, Cin, KH, KW, S, u8in)) {
+    const int rc = wgrad_slab_t<C2, 7, false, bf16_t>(X, g, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E,
+                                                       T, br, is, gs, st);
+    return rc ? -rc : 1;
+  }
+  if (!is_shape<C1>(Hin, Win, Cin, KH, KW, S, u8in)) return 0;
   const int rc = WGRAD_OB == 3
                      ? wgrad_slab_t<C1, 3, false, bf16_t>(X, g, bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M,
                                                           P, E, T, br, is, gs, st)

@@ -284,7 +284,7 @@ class HipPathNet:
         if self.deterministic:
             return self._layer_bwd_det(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
         if (G.dtype == torch.bfloat16) or (dX is not None and dX.dtype == torch.bfloat16):
-            return self._layer_bwd_grad0_bf16(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
+            return self._layer_bwd_bf16_grads(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
         if g.kind == "conv":
             fast_w = _lib.USE_FAST and _lib.call_fast(
                 "fast_conv_wgrad", X.data_ptr(), int(g.u8in), G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(),
@@ -330,15 +330,25 @@ class HipPathNet:
                           g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(), self.inv_slot.data_ptr(),
                           self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T, bits_rows, g_scale, st)
 
-    def grad0_bf16_ok(self, ring: bool) -> bool:
-        """Can the first layer's output gradient (engine.grads[0]) be kept in bf16?  The second layer's MFMA
-        dgrad writes it and the first layer's slab wgrad reads it (csrc/conv_fast.hip *_bf16out / *_bf16g);
-        only those reference-geometry kernels take bf16, so every other configuration keeps fp32."""
-        if self.f32 or self.deterministic or ring or not _lib.USE_FAST or len(self.geoms) < 2 or self.M > 10:
-            return False
-        g0, g1 = self.geoms[0], self.geoms[1]
-        return (g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
-                and g1.kind == "conv" and (g1.Hin, g1.Win, g1.Cin, g1.KH, g1.S) == (39, 29, 8, 4, 2))
+    # reference conv geometries (Hin, Win, Cin, KH, S) of the specialised kernels
+    _C1 = (160, 120, 4, 8, 4)
+    _C2 = (39, 29, 8, 4, 2)
+    _C3 = (18, 13, 8, 3, 1)
+
+    def grad_bf16_layers(self, ring: bool) -> set:
+        """Layers l whose output gradient engine.grads[l] is kept in bf16: written by layer l+1's MFMA dgrad and
+        read by layer l's slab wgrad (and, for l >= 1, by layer l's MFMA dgrad), all of which round it to bf16
+        for their MFMAs anyway (csrc/conv_fast.hip fast_conv_dgrad_bf16 / fast_conv_wgrad_bf16g).  Only those
+        reference-geometry kernels take bf16, so every other layer / configuration keeps fp32."""
+        if self.f32 or self.deterministic or ring or not _lib.USE_FAST or self.M > 10:
+            return set()
+        geo = [(g.Hin, g.Win, g.Cin, g.KH, g.S) if g.kind == "conv" else None for g in self.geoms]
+        out = set()
+        if len(geo) > 1 and geo[0] == self._C1 and self.geoms[0].u8in and geo[1] == self._C2:
+            out.add(0)
+        if len(geo) > 2 and geo[1] == self._C2 and geo[2] == self._C3:
+            out.add(1)
+        return out
 
     # -- fp32 mode (csrc/trunk_f32.hip) ------------------------------------------
     def _layer_fwd_f32(self, l, X, Y, bits, P, E, T, t0, bits_rows, out_scale, st):
@@ -371,30 +381,27 @@ class HipPathNet:
             self._part = torch.empty(numel, dtype=torch.float32, device=self.model.store.flat.device)
         return self._part
 
-    def _layer_bwd_grad0_bf16(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st):
-        """Layers 0 / 1 when grads[0] is bf16 (grad0_bf16_ok): no fallback kernel reads or writes it."""
+    def _layer_bwd_bf16_grads(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st):
+        """Conv layer with a bf16 output gradient G and/or a bf16 input gradient dX (grad_bf16_layers): no
+        fallback kernel reads or writes those, so an unspecialised shape raises."""
         g = self.geoms[l]
         m = self.model
         flat = m.store.flat
-        if l == 0 and G.dtype == torch.bfloat16 and dX is None:
-            ok = _lib.call_fast("fast_conv_wgrad_bf16g", X.data_ptr(), int(g.u8in), G.data_ptr(), bits.data_ptr(),
-                                grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
-                                m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T,
-                                bits_rows, g.in_scale, g_scale, st)
-        elif l == 1 and G.dtype == torch.float32 and dX is not None and dX.dtype == torch.bfloat16:
-            ok = _lib.call_fast("fast_conv_wgrad", X.data_ptr(), int(g.u8in), G.data_ptr(), bits.data_ptr(),
-                                grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
-                                m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T,
-                                bits_rows, g.in_scale, g_scale, st)
-            ok = ok and _lib.call_fast("fast_conv_dgrad_bf16out", G.data_ptr(), bits.data_ptr(), flat.data_ptr(),
-                                       g.w_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M,
-                                       g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T, bits_rows, g_scale, dX.data_ptr(),
-                                       st)
-        else:
-            ok = False
+        if g.kind != "conv":
+            raise RuntimeError(f"layer {l}: bf16 activation gradients are for the conv layers")
+        args = (g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin,
+                g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T, bits_rows, g.in_scale, g_scale, st)
+        g_bf = G.dtype == torch.bfloat16
+        ok = _lib.call_fast("fast_conv_wgrad_bf16g" if g_bf else "fast_conv_wgrad", X.data_ptr(), int(g.u8in),
+                            G.data_ptr(), bits.data_ptr(), grad_flat.data_ptr(), *args)
+        if ok and dX is not None:
+            ok = _lib.call_fast("fast_conv_dgrad_bf16", G.data_ptr(), int(g_bf), bits.data_ptr(), flat.data_ptr(),
+                                g.w_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin,
+                                g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T, bits_rows, g_scale, dX.data_ptr(),
+                                int(dX.dtype == torch.bfloat16), st)
         if not ok:
-            raise RuntimeError(f"layer {l}: bf16 first-layer gradient needs the specialised kernels "
-                               "(HipPathNet.grad0_bf16_ok)")
+            raise RuntimeError(f"layer {l}: bf16 activation gradients need the specialised kernels "
+                               "(HipPathNet.grad_bf16_layers)")
 
     def _conv_wgrad_ordered(self, l, X, G, bits, grad_flat, P, E, T, bits_rows, g_scale, st):
         """Conv weight gradient with fixed-order reductions (uint8 / bf16 / fp32 input, fp32 MFMA)."""

@@ -71,15 +71,15 @@ class HipEngine:
         else:
             self.obs = torch.zeros(T + 1, B, 8, dtype=torch.bfloat16, device=dev)
         self.acts, self.bits, self.bits_rows, self.grads = [], [], [], []
+        # conv-layer output gradients kept in bf16 where the specialised dgrad / wgrad kernels take them
+        # (grads[0] is 1.5 GB and grads[1] 0.3 GB in fp32 at the bench shape)
+        bf16_grads = hp.grad_bf16_layers(self.ring)
         for l, g in enumerate(hp.geoms):
             self.acts.append(torch.zeros(T + 1, B, g.out_feat, dtype=hp.act_dtype, device=dev))
             b, rows = hp.alloc_bits(l, T + 1, B)
             self.bits.append(b)
             self.bits_rows.append(rows)
-            # grads[0] (first layer's output gradient, 1.5 GB fp32 at the bench shape) in bf16 where the
-            # specialised second-layer dgrad / first-layer wgrad handle it
-            g0_bf16 = l == 0 and hp.grad0_bf16_ok(self.ring)
-            self.grads.append(torch.zeros(T * B, g.out_feat, dtype=torch.bfloat16 if g0_bf16 else torch.float32,
+            self.grads.append(torch.zeros(T * B, g.out_feat, dtype=torch.bfloat16 if l in bf16_grads else torch.float32,
                                           device=dev))
         self.logits = torch.zeros(T + 1, B, A, device=dev)
         self.values = torch.zeros(T + 1, B, device=dev)

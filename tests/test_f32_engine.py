@@ -167,8 +167,8 @@ def test_bf16_deterministic_gradient_matches_default_path(hip_lib):
     torch.cuda.synchronize()
     g_default = eng.grad_flat.clone()
     hp.deterministic = True
-    # the default engine keeps the first layer's output gradient in bf16; the ordered kernels take fp32
-    eng.grads[0] = torch.zeros(eng.grads[0].shape, dtype=torch.float32, device=DEV)
+    # the default engine keeps the conv1 / conv2 output gradients in bf16; the ordered kernels take fp32
+    eng.grads = [torch.zeros(g.shape, dtype=torch.float32, device=DEV) for g in eng.grads]
     try:
         eng.grad_flat.zero_()
         L = len(hp.geoms)
