@@ -167,3 +167,23 @@ def test_windowed_fitness_windows_restart_only_for_tournament_candidates():
                 else:
                     assert float(tr.fit_cnt[p]) == 0.0
     assert fired_any
+
+
+def test_compute_dtype_and_deterministic_flags():
+    """--compute_dtype / --deterministic reach the config, survive the checkpoint JSON, and bad dtypes fail early;
+    the torch backend always computes in fp32."""
+    import pytest
+    from pathnet_gym_amd.cli import build_parser, config_from_args
+    from pathnet_gym_amd.config import TrainConfig
+    a = build_parser().parse_args(["train", "--preset", "pong", "--compute_dtype", "fp32", "--deterministic", "1"])
+    cfg = config_from_args(a)
+    assert cfg.compute_dtype == "fp32" and cfg.deterministic
+    c2 = TrainConfig.from_json(cfg.to_json())
+    assert c2.compute_dtype == "fp32" and c2.deterministic
+    bad = preset("cartpole-cpu")
+    bad.compute_dtype = "fp16"
+    with pytest.raises(ValueError):
+        PathNetTrainer(bad, device="cpu")
+    ok = preset("cartpole-cpu")
+    ok.compute_dtype = "bf16"
+    assert PathNetTrainer(ok, device="cpu").compute_dtype == "fp32"
