@@ -6,11 +6,14 @@
 // accumulation, 64 FLOP/clk/SIMD -- 1/16 of the bf16 rate, so this mode is the precision reference, not
 // the throughput mode).
 //
-// Tiling follows the bf16 generic kernels (trunk_fwd.hip / trunk_bwd.hip) so the epilogues (bias, ReLU,
-// ReLU bits by ballot, per-layer module sum) are shared in form.  A 32-wide k chunk per lane group keeps
-// the bf16 kernels' load shape: lane group g = l>>4 holds k = kk+8g .. kk+8g+7 and the chunk is eight
-// 16x16x4 MFMAs, sub-step j feeding k-slot g with element kk+8g+j (A and B use the same permutation of
-// k, so the sum is unchanged).
+// The epilogues (bias, ReLU, ReLU bits by ballot, per-layer module sum) have the form of the bf16 kernels'
+// (trunk_fwd.hip / trunk_bwd.hip).  A 32-wide k chunk per lane group keeps the bf16 kernels' load shape:
+// lane group g = l>>4 holds k = kk+8g .. kk+8g+7 and the chunk is eight 16x16x4 MFMAs, sub-step j feeding
+// k-slot g with element kk+8g+j (A and B use the same permutation of k, so the sum is unchanged).
+//   conv fwd   : B fragments straight from the L1-resident weight copy (no LDS staging), RT = 2 row tiles
+//                per wave, raw (uint8) A fragments of the next k-step prefetched during this step's MFMAs.
+//   conv dgrad : one thread per input pixel, weights in LDS as [slot][tap][c][ci] (two ds_read_b128 per 8 FMAs).
+//   fc fwd     : register pipeline (next k-step's A and B loaded during this step's MFMAs).
 //
 // Every reduction is in a FIXED order -- no float atomics anywhere in this file:
 //   conv wgrad : each (path, row chunk) workgroup writes its partial dW/db of every active slot to a
