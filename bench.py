@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="HIP engine compute dtype (fp32: the reference's precision, csrc/trunk_f32.hip)")
     ap.add_argument("--deterministic", action="store_true", help="fixed-order gradient reductions (bit-reproducible)")
+    ap.add_argument("--rollout-groups", type=int, default=0,
+                    help="path groups stepped on their own streams in the rollout (0 = auto, 1 = one stream)")
     ap.add_argument("--ga-backend", default="device", choices=["device", "host"],
                     help="device: GA kernels inside the update graph + pipelined host bookkeeping")
     ap.add_argument("--concurrent", type=int, default=None,
@@ -135,6 +137,7 @@ def main():
     cfg.ga.backend = args.ga_backend
     cfg.compute_dtype = args.dtype
     cfg.deterministic = args.deterministic
+    cfg.rollout_groups = args.rollout_groups
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
 
     def sync():
@@ -188,6 +191,7 @@ def main():
                 "backend": args.backend,
                 "hipgraph": cfg.use_graph,
                 "frame_ring": bool(getattr(tr.engine, "ring", False)),
+                "rollout_groups": int(getattr(tr.engine, "groups", 1)),
                 "ga": f"{cfg.ga.backend} (B={cfg.ga.B}, {cfg.ga.concurrent_tournaments} concurrent tournaments)",
                 "pipelined": bool(tr.pipelined),
                 "deterministic": bool(getattr(tr.model.hip, "deterministic", False)),

@@ -324,10 +324,10 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
                                                         int g_player, int g_ball,
                                                         const uint8_t* __restrict__ fc_in = nullptr,
                                                         uint8_t* __restrict__ fc_out = nullptr,
-                                                        long out_stride = 0) {
+                                                        long out_stride = 0, int b0 = 0) {
   using namespace pong;
   __shared__ __attribute__((aligned(16))) int tab[8 * 160];
-  const int env = blockIdx.x;
+  const int env = b0 + blockIdx.x;
   PONG_STAMP(0);
   for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
   // --- physics: wave 0 only (scalar code; the 4 waves of a workgroup share ONE scalar unit per
@@ -462,11 +462,13 @@ extern "C" {
 int launch_pong_step(void* state, void* counter, const int* actions, int n_actions, const void* obs_in, void* obs_out,
                      const int* tables, float* reward, void* done, float* epret, int B, unsigned seed, int frameskip,
                      int max_steps, int no_op_max, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
-                     hipStream_t stream) {
-  pong_step_kernel<false><<<B, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions,
-                                                 (const uint32_t*)obs_in, (uint32_t*)obs_out, tables, reward,
-                                                 (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max, g_bg,
-                                                 g_wall, g_cpu, g_player, g_ball);
+                     int b0, hipStream_t stream) {
+  // envs [b0, B): one path group of the split rollout (runtime/engine.py); per-env state and RNG keys are global
+  if (b0 < 0 || b0 >= B) return -22;
+  pong_step_kernel<false><<<B - b0, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions,
+                                                      (const uint32_t*)obs_in, (uint32_t*)obs_out, tables, reward,
+                                                      (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max,
+                                                      g_bg, g_wall, g_cpu, g_player, g_ball, nullptr, nullptr, 0, b0);
   return (int)hipGetLastError();
 }
 

@@ -29,9 +29,9 @@ template <typename FT>
 __global__ __launch_bounds__(256) void heads_fwd_sample_kernel(
     const FT* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
     int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
-    const long long* __restrict__ ctr, int t, int T, int greedy) {
+    const long long* __restrict__ ctr, int t, int T, int greedy, int b0) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + w;
+  const int b = b0 + blockIdx.x * 4 + w;
   if (b >= B) return;
   float part[AMAX];
 #pragma unroll
@@ -90,7 +90,7 @@ template <int AM, typename FT>
 __global__ __launch_bounds__(256) void heads_fwd_lanes_kernel(
     const FT* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
     int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
-    const long long* __restrict__ ctr, int t, int T, int greedy) {
+    const long long* __restrict__ ctr, int t, int T, int greedy, int b0) {
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   constexpr int AW = AM + 1;
   float* Wl = hsm;                       // [F][AW]: policy weights (zero padded to AM) + value weight
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void heads_fwd_lanes_kernel(
     Wl[i] = j == AM ? flat[vw + f] : (j < A ? flat[pw + (long)f * A + j] : 0.f);
   }
   __syncthreads();
-  const int b = blockIdx.x * 64 + l;
+  const int b = b0 + blockIdx.x * 64 + l;
   const bool valid = b < B;
   const int fq = F >> 2;
   const int f0 = w * fq;
@@ -147,19 +147,19 @@ __global__ __launch_bounds__(256) void heads_fwd_lanes_kernel(
 template <typename FT>
 static bool heads_fwd_lanes_launch(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
                                    int A, int B, float* logits, float* value, int* actions, unsigned seed,
-                                   const long long* ctr, int t, int T, int greedy, hipStream_t stream) {
+                                   const long long* ctr, int t, int T, int greedy, int b0, hipStream_t stream) {
   if (F % 32 != 0 || A > 18) return false;
-  const unsigned g = (unsigned)((B + 63) / 64);
+  const unsigned g = (unsigned)((B - b0 + 63) / 64);
   if (A <= 8) {
     const size_t sm = (size_t)(F * 9 + 3 * 9 * 64) * 4;
     if (sm > 64 * 1024) return false;
     heads_fwd_lanes_kernel<8, FT><<<g, 256, sm, stream>>>((const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits,
-                                                          value, actions, seed, ctr, t, T, greedy);
+                                                          value, actions, seed, ctr, t, T, greedy, b0);
   } else {
     const size_t sm = (size_t)(F * 19 + 3 * 19 * 64) * 4;
     if (sm > 64 * 1024) return false;
     heads_fwd_lanes_kernel<18, FT><<<g, 256, sm, stream>>>((const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits,
-                                                           value, actions, seed, ctr, t, T, greedy);
+                                                           value, actions, seed, ctr, t, T, greedy, b0);
   }
   return true;
 }
@@ -360,27 +360,28 @@ __global__ __launch_bounds__(256) void heads_reduce_kernel(const float* __restri
 
 extern "C" {
 
+// samples [b0, B) (a path group of the split rollout, runtime/engine.py); RNG keys use the global sample index
 int launch_heads_fwd_sample(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb, int A,
                             int B, float* logits, float* value, int* actions, unsigned seed, const long long* ctr,
-                            int t, int T, int greedy, hipStream_t stream) {
-  if (A > AMAX || A < 1) return -1;
+                            int t, int T, int greedy, int b0, hipStream_t stream) {
+  if (A > AMAX || A < 1 || b0 < 0 || b0 >= B) return -1;
   if (!heads_fwd_lanes_launch<bf16_t>(feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T,
-                                      greedy, stream))
-    heads_fwd_sample_kernel<bf16_t><<<(B + 3) / 4, 256, 0, stream>>>((const bf16_t*)feat, F, flat, pw, pb, vw, vb,
-                                                                      A, B, logits, value, actions, seed, ctr, t, T,
-                                                                      greedy);
+                                      greedy, b0, stream))
+    heads_fwd_sample_kernel<bf16_t><<<(B - b0 + 3) / 4, 256, 0, stream>>>((const bf16_t*)feat, F, flat, pw, pb, vw,
+                                                                           vb, A, B, logits, value, actions, seed, ctr,
+                                                                           t, T, greedy, b0);
   return (int)hipGetLastError();
 }
 
 int launch_heads_fwd_sample_f32(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
                                 int A, int B, float* logits, float* value, int* actions, unsigned seed,
-                                const long long* ctr, int t, int T, int greedy, hipStream_t stream) {
-  if (A > AMAX || A < 1) return -1;
+                                const long long* ctr, int t, int T, int greedy, int b0, hipStream_t stream) {
+  if (A > AMAX || A < 1 || b0 < 0 || b0 >= B) return -1;
   if (!heads_fwd_lanes_launch<float>(feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T,
-                                     greedy, stream))
-    heads_fwd_sample_kernel<float><<<(B + 3) / 4, 256, 0, stream>>>((const float*)feat, F, flat, pw, pb, vw, vb, A,
-                                                                     B, logits, value, actions, seed, ctr, t, T,
-                                                                     greedy);
+                                     greedy, b0, stream))
+    heads_fwd_sample_kernel<float><<<(B - b0 + 3) / 4, 256, 0, stream>>>((const float*)feat, F, flat, pw, pb, vw, vb,
+                                                                          A, B, logits, value, actions, seed, ctr, t,
+                                                                          T, greedy, b0);
   return (int)hipGetLastError();
 }
 

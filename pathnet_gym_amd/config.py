@@ -199,6 +199,12 @@ class TrainConfig:
     frame_ring: bool = False            # HIP Pong: single-frame ring instead of packed stacks (runtime/engine.py;
                                         # measured 13.06 vs 12.73 ms/update: the conv1 planar loads cost more than
                                         # the env saves)
+    # HIP engine rollout: the population is stepped as this many path groups on their own HIP streams (one
+    # branch each inside the rollout hipGraph) so one group's latency-bound fc / heads launches can overlap
+    # the other group's env / conv1 launches (runtime/engine.py; packed-stack pixel envs without LSTM).
+    # Bit-identical to one stream.  Measured at the bench shape: 9.70 (1) vs 10.00 (2) vs 10.81 (4) ms per
+    # update -- every rollout kernel already fills the GPU -- so 0 (auto) = 1.
+    rollout_groups: int = 0
     seed: int = 1
     log_dir: str = "./data/tensorboard/"
     steps_per_task: int = MAX_TIME_STEP

@@ -39,7 +39,7 @@ _SIGS = {
     "launch_fc_wgrad": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_long, c_float, P],
     "launch_heads_fwd_sample": [P, c_int, P, c_long, c_long, c_long, c_long, c_int, c_int, P, P, P, c_uint, P, c_int,
-                                c_int, c_int, P],
+                                c_int, c_int, c_int, P],
     "launch_a2c_grad": [P, P, P, P, P, P, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_float, c_float,
                         P, P, P, P],
     "launch_heads_bwd": [P, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P],
@@ -47,7 +47,7 @@ _SIGS = {
     "launch_rmsprop": [P, P, P, P, P, P, P, c_int, P, P, P, P, P, c_float, c_float, c_float, c_float, P],
     "launch_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
     "launch_pong_step": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int, c_int, c_int,
-                         c_int, c_int, P],
+                         c_int, c_int, c_int, P],
     "launch_refresh_weights_cmajor": [P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P],
     "fast_conv1_ring_fwd": [P, P, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_int, c_long, c_float, c_float, P, P, P],
@@ -92,7 +92,7 @@ _SIGS = {
     "launch_active_union": [P, P, c_int, c_int, c_int, P, P],
     "launch_pack_ranges": [P, P, P, c_int, c_long, c_int, P],
     "launch_heads_fwd_sample_f32": [P, c_int, P, c_long, c_long, c_long, c_long, c_int, c_int, P, P, P, c_uint, P,
-                                    c_int, c_int, c_int, P],
+                                    c_int, c_int, c_int, c_int, P],
     "launch_heads_bwd_f32": [P, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P],
     "launch_conv_fwd_f32": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_long,

@@ -37,8 +37,12 @@ def _gray_consts(env):
     return [g(pg.COLOR_BG), g(pg.COLOR_WALL), g(pg.COLOR_CPU), g(pg.COLOR_PLAYER), g(pg.COLOR_BALL)]
 
 
-def pong_step_into(env, actions, obs_in, obs_out, reward, done, epret):
+def pong_step_into(env, actions, obs_in, obs_out, reward, done, epret, b0: int = 0, b1=None):
+    """One step of envs [b0, b1) (default all; the split rollout steps one path group per call)."""
     B = env.num_envs
+    b1 = B if b1 is None else b1
+    if not 0 <= b0 < b1 <= B:
+        raise ValueError(f"pong_step_into: env range [{b0}, {b1}) outside [0, {B})")
     if not hasattr(env, "_st32"):
         pong_sync_to_device(env)
     _lib.check(actions, torch.int32, (B,), name="actions")
@@ -52,8 +56,8 @@ def pong_step_into(env, actions, obs_in, obs_out, reward, done, epret):
     g = env._gray
     _lib.call("launch_pong_step", env._st32.data_ptr(), env._ctr32.data_ptr(), actions.data_ptr(), env.num_actions,
               obs_in.data_ptr(), obs_out.data_ptr(), env._tab32.data_ptr(), reward.data_ptr(), done.data_ptr(),
-              epret.data_ptr(), B, env.seed_int, env.frameskip, env.max_episode_steps,
-              env.no_op_max, g[0], g[1], g[2], g[3], g[4], _lib.stream())
+              epret.data_ptr(), b1, env.seed_int, env.frameskip, env.max_episode_steps,
+              env.no_op_max, g[0], g[1], g[2], g[3], g[4], b0, _lib.stream())
 
 
 def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done, epret):

@@ -243,33 +243,60 @@ class HipPathNet:
                   c0.data_ptr(), self.lstm["H"], h0.shape[0], _lib.stream())
 
     # ------------------------------------------------------------------
+    def _fwd_ptrs(self, l: int, X, Y, bits, row0: int, p0: int, xrow0: int):
+        """Device pointers of a forward launch.  row0 > 0 / p0 > 0 (one path group of the split rollout,
+        runtime/engine.py): X, Y and the ReLU bits start at global sample row row0 and the active-module
+        tables at path p0, so the kernel sees a population of its own group's paths at t0 = 0 (every kernel
+        addresses rows as sample_global(p, s, E, P*E, t0) and bits as [slot][bits_rows] from these bases)."""
+        m = self.model
+        g = self.geoms[l]
+        if row0 == 0 and p0 == 0 and xrow0 == 0:
+            return X.data_ptr(), Y.data_ptr(), bits.data_ptr(), m.act_idx.data_ptr(), m.act_cnt.data_ptr()
+        xrow = X.shape[-1] * X.element_size()
+        yrow = Y.shape[-1] * Y.element_size()
+        brow = g.HWo * bits.element_size() if g.kind == "conv" else bits.shape[-1] * bits.element_size()
+        i4 = m.act_idx.element_size()
+        return (X.data_ptr() + xrow0 * xrow, Y.data_ptr() + row0 * yrow, bits.data_ptr() + row0 * brow,
+                m.act_idx.data_ptr() + p0 * self.L * self.M * i4, m.act_cnt.data_ptr() + p0 * self.L * i4)
+
     def layer_fwd(self, l: int, X: torch.Tensor, Y: torch.Tensor, bits: torch.Tensor, P: int, E: int, T: int,
-                  t0: int, bits_rows: int):
+                  t0: int, bits_rows: int, row0: int = 0, p0: int = 0, xrow0: Optional[int] = None):
+        """Forward of layer l for P paths x E envs x T steps from step t0.  row0/p0/xrow0: a one-step window of
+        paths p0..p0+P-1 whose outputs (Y, ReLU bits) start at global sample row row0 and whose inputs start at
+        row xrow0 of X (default row0; runtime/engine.py passes the other observation buffer for the bootstrap
+        step).  The caller then passes t0 = 0 and T = 1 (see _fwd_ptrs)."""
         g = self.geoms[l]
         m = self.model
         flat = m.store.flat
         out_scale = self.out_scale_last if l == self.L - 1 else 1.0
         st = _lib.stream()
+        xrow0 = row0 if xrow0 is None else xrow0
+        if (row0 or p0 or xrow0) and (t0 != 0 or T != 1 or p0 + P > m.P or
+                                      xrow0 + P * E > X.numel() // X.shape[-1] or
+                                      row0 + P * E > Y.numel() // Y.shape[-1]):
+            raise ValueError(f"layer {l}: path-group window (row0={row0}, xrow0={xrow0}, p0={p0}, P={P}) out of range")
+        xp, yp, bp, aip, acp = self._fwd_ptrs(l, X, Y, bits, row0, p0, xrow0)
         if self.f32:
-            return self._layer_fwd_f32(l, X, Y, bits, P, E, T, t0, bits_rows, out_scale, st)
+            _lib.check(Y, torch.float32, name="Y")
+            return self._layer_fwd_f32(l, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st)
         if g.kind == "conv":
             if (E * g.HWo) % 16 != 0:
                 raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
             f16 = g.u8in and self.Wh0 is not None
             if _lib.USE_FAST and _lib.call_fast(
-                    "fast_conv_fwd", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
+                    "fast_conv_fwd", xp, int(g.u8in), yp, bp,
                     (self.Wh0 if f16 else self.Wc[l]).data_ptr(), flat.data_ptr(), g.b_off, g.chunk,
-                    m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW,
+                    aip, acp, l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW,
                     g.S, P, E, T, t0, bits_rows, g.in_scale, out_scale, _lib.ptr(self.hcorr0 if f16 else None),
                     self.Wc[l].data_ptr(), st):
                 return
-            _lib.call("launch_conv_fwd", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
-                      self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
-                      m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo,
+            _lib.call("launch_conv_fwd", xp, int(g.u8in), yp, bp,
+                      self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, aip,
+                      acp, l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo,
                       g.K, g.KP, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
         else:
-            _lib.call("launch_fc_fwd", X.data_ptr(), g.ldx, Y.data_ptr(), bits.data_ptr(), self.Wc[l].data_ptr(),
-                      flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L,
+            _lib.call("launch_fc_fwd", xp, g.ldx, yp, bp, self.Wc[l].data_ptr(),
+                      flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L,
                       self.M, g.K, g.KP, g.Cout, P, E, T, t0, bits_rows, out_scale, st)
 
     def layer_bwd(self, l: int, X: torch.Tensor, G: torch.Tensor, bits: torch.Tensor, grad_flat: torch.Tensor,
@@ -351,21 +378,19 @@ class HipPathNet:
         return out
 
     # -- fp32 mode (csrc/trunk_f32.hip) ------------------------------------------
-    def _layer_fwd_f32(self, l, X, Y, bits, P, E, T, t0, bits_rows, out_scale, st):
+    def _layer_fwd_f32(self, l, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st):
         g = self.geoms[l]
-        m = self.model
-        flat = m.store.flat
-        _lib.check(Y, torch.float32, name="Y")
+        flat = self.model.store.flat
         if g.kind == "conv":
             if (E * g.HWo) % 16 != 0:
                 raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
-            _lib.call("launch_conv_fwd_f32", X.data_ptr(), int(g.u8in), Y.data_ptr(), bits.data_ptr(),
-                      self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
-                      m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo,
+            _lib.call("launch_conv_fwd_f32", xp, int(g.u8in), yp, bp,
+                      self.Wc[l].data_ptr(), flat.data_ptr(), g.b_off, g.chunk, aip,
+                      acp, l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, g.Ho, g.Wo,
                       g.K, g.KP, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
         else:
-            _lib.call("launch_fc_fwd_f32", X.data_ptr(), g.ldx, Y.data_ptr(), bits.data_ptr(), self.Wc[l].data_ptr(),
-                      flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L,
+            _lib.call("launch_fc_fwd_f32", xp, g.ldx, yp, bp, self.Wc[l].data_ptr(),
+                      flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L,
                       self.M, g.K, g.KP, g.Cout, P, E, T, t0, bits_rows, out_scale, st)
 
     def wgrad_chunks(self, l: int, P: int, E: int, T: int) -> int:
@@ -512,16 +537,21 @@ class HipPathNet:
         rows = steps * B
         return torch.zeros(self.M, rows, g.Cout // 16, dtype=torch.int16, device=dev), rows
 
-    def heads_fwd(self, feat, logits, value, actions, seed, ctr, t, T, greedy=False, task=0):
+    def heads_fwd(self, feat, logits, value, actions, seed, ctr, t, T, greedy=False, task=0, b0=0, b1=None):
+        """Heads + Gumbel-max sampling of samples [b0, b1) of feat [B, F] (default all; the split rollout
+        passes one path group's rows, runtime/engine.py)."""
         m = self.model
         h = m.store.layout.heads[task if m.cfg.per_task_heads else 0]
-        B = feat.shape[0]
+        B = feat.shape[0] if b1 is None else b1
         F = feat.shape[1]
         A = m.cfg.num_actions
         _lib.check(feat, self.act_dtype, name="feat")
-        _lib.call("launch_heads_fwd_sample_f32" if self.f32 else "launch_heads_fwd_sample", feat.data_ptr(), F, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"],
-                  h["vb"], A, B, logits.data_ptr(), value.data_ptr(), actions.data_ptr(), seed & 0xFFFFFFFF,
-                  ctr.data_ptr(), t, T, int(greedy), _lib.stream())
+        if not 0 <= b0 < B <= feat.shape[0]:
+            raise ValueError(f"heads_fwd: sample range [{b0}, {B}) outside [0, {feat.shape[0]})")
+        _lib.call("launch_heads_fwd_sample_f32" if self.f32 else "launch_heads_fwd_sample", feat.data_ptr(), F,
+                  m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"], A, B, logits.data_ptr(),
+                  value.data_ptr(), actions.data_ptr(), seed & 0xFFFFFFFF, ctr.data_ptr(), t, T, int(greedy), b0,
+                  _lib.stream())
 
     def heads_bwd(self, feat, dlogits, dvalue, grad_flat, dfeat, task=0):
         m = self.model

@@ -56,7 +56,12 @@ class HipEngine:
         # step writes 19.2 KB per env instead of reading + writing a 77 KB stack.
         self.ring = bool(self.pixels and getattr(cfg, "frame_ring", True) and hp.ring_ok and _lib.USE_FAST
                          and hasattr(env, "step_ring_into"))
-        self.obs = None
+        # observation double buffer (non-ring): the rollout of parity q reads bufs[q][0..T-1] and its last
+        # env step writes the NEXT rollout's step-0 input straight into bufs[1-q][0] (the bootstrap forward
+        # reads it there), so no obs[0] <- obs[T] copy of the whole stack batch (157 MB at the bench shape)
+        # runs per update; one rollout hipGraph per parity, the parity flips after every optimizer step
+        self._obs_bufs = None
+        self._par = 0
         if self.ring:
             H, W, C = model.cfg.input_shape
             hp.enable_ring()
@@ -65,11 +70,11 @@ class HipEngine:
             self.fc = torch.zeros(T + 1, B, dtype=torch.uint8, device=dev)
         elif self.pixels:
             H, W, C = model.cfg.input_shape
-            self.obs = torch.zeros(T + 1, B, H * W * C, dtype=torch.uint8, device=dev)
+            self._obs_bufs = [torch.zeros(T, B, H * W * C, dtype=torch.uint8, device=dev) for _ in range(2)]
         elif hp.f32:
-            self.obs = torch.zeros(T + 1, B, hp.geoms[0].ldx, dtype=torch.float32, device=dev)
+            self._obs_bufs = [torch.zeros(T, B, hp.geoms[0].ldx, dtype=torch.float32, device=dev) for _ in range(2)]
         else:
-            self.obs = torch.zeros(T + 1, B, 8, dtype=torch.bfloat16, device=dev)
+            self._obs_bufs = [torch.zeros(T, B, 8, dtype=torch.bfloat16, device=dev) for _ in range(2)]
         self.acts, self.bits, self.bits_rows, self.grads = [], [], [], []
         # conv-layer output gradients kept in bf16 where the specialised dgrad / wgrad kernels take them
         # (grads[0] is 1.5 GB and grads[1] 0.3 GB in fp32 at the bench shape)
@@ -124,7 +129,38 @@ class HipEngine:
         # torch-implemented games (envs/atari_games.py) are stepped eagerly, outside hipGraphs
         self.env_graph_safe = getattr(env, "graph_safe", True)
         self.use_graph = bool(cfg.use_graph) and not self.hybrid and self.env_graph_safe
+        self.groups = self._rollout_groups(getattr(cfg, "rollout_groups", 0))
+        self.side_streams = [torch.cuda.Stream(device=dev) for _ in range(self.groups - 1)]
         self.load_obs(env)
+
+    def _rollout_groups(self, want: int) -> int:
+        """Path groups of the split rollout (TrainConfig.rollout_groups): each group's forward + env step chain
+        runs on its own stream.  Needs per-range launches: the packed-stack Pong kernel (pong_step_into b0/b1),
+        the trunk forward (HipPathNet.layer_fwd row0/p0) and the heads (heads_fwd b0/b1)."""
+        ok = (self.pixels and not self.ring and not self.lstm_hip and not self.hybrid
+              and not hasattr(self.env, "step_into") and self.env_graph_safe)
+        if want == 0:
+            want = 1       # measured: two groups 3 % slower at the bench shape (TrainConfig.rollout_groups)
+        if want > 1 and (not ok or self.P % want != 0):
+            raise ValueError(f"rollout_groups={want} needs a packed-stack pixel env without LSTM and paths "
+                             f"({self.P}) divisible by it")
+        return max(1, want)
+
+    # -- observation double buffer -------------------------------------------
+    @property
+    def obs(self):
+        """[T, B, ...] observations of the current rollout (steps 0..T-1); None with the frame ring."""
+        return None if self._obs_bufs is None else self._obs_bufs[self._par]
+
+    def _obs_at(self, t: int) -> torch.Tensor:
+        """Input of step t (t == T: the bootstrap input = the next rollout's step 0, in the other buffer)."""
+        return self._obs_bufs[self._par][t] if t < self.T else self._obs_bufs[1 - self._par][0]
+
+    def _obs_x(self, t: int):
+        """(buffer, first global row) of step t's observations for a trunk launch."""
+        if t < self.T:
+            return self._obs_bufs[self._par], t * self.B
+        return self._obs_bufs[1 - self._par], 0
 
     # ------------------------------------------------------------------
     def load_obs(self, env):
@@ -141,7 +177,7 @@ class HipEngine:
     def obs_stack(self, t: int) -> torch.Tensor:
         """Stack of step t as [B, H*W*4] uint8 (pixel-major, channel-minor, newest frame last)."""
         if not self.ring:
-            return self.obs[t]
+            return self._obs_at(t)
         B = self.B
         dev = self.device
         c = torch.arange(4, device=dev)
@@ -153,7 +189,7 @@ class HipEngine:
         """Stacks of steps 0..n-1 (default T+1) as [n, B, H*W*4] uint8 (or the vector obs)."""
         n = self.T + 1 if n is None else n
         if not self.ring:
-            return self.obs[:n]
+            return self.obs[:n] if n <= self.T else torch.cat([self.obs, self._obs_at(self.T)[None]])[:n]
         return torch.stack([self.obs_stack(t) for t in range(n)])
 
     def set_obs_stack0(self, stack: torch.Tensor):
@@ -197,32 +233,49 @@ class HipEngine:
         self.trainable_u8.copy_(self.opt.seg_trainable.to(torch.uint8))
 
     # ------------------------------------------------------------------
-    def _env_step(self, t):
+    def _group_range(self, grp):
+        """(first path, path count) of path group grp (None: the whole population)."""
+        if grp is None:
+            return 0, self.P
+        pg = self.P // self.groups
+        return grp * pg, pg
+
+    def _env_step(self, t, grp=None):
         env = self.env
+        if grp is not None:
+            p0, np_ = self._group_range(grp)
+            henv.pong_step_into(env, self.actions[t], self._obs_at(t), self._obs_at(t + 1), self.rewards[t],
+                                self.dones[t], self.epret[t], b0=p0 * self.E, b1=(p0 + np_) * self.E)
+            return
         if self.ring:
             env.step_ring_into(self.actions[t], self.frames, t + 4, self.fc[t], self.fc[t + 1], self.rewards[t],
                                self.dones[t], self.epret[t])
         elif hasattr(env, "step_into"):
-            env.step_into(self.actions[t], self.obs[t], self.obs[t + 1], self.rewards[t], self.dones[t],
+            env.step_into(self.actions[t], self._obs_at(t), self._obs_at(t + 1), self.rewards[t], self.dones[t],
                           self.epret[t])
         elif self.pixels:
-            henv.pong_step_into(env, self.actions[t], self.obs[t], self.obs[t + 1], self.rewards[t], self.dones[t],
-                                self.epret[t])
+            henv.pong_step_into(env, self.actions[t], self._obs_at(t), self._obs_at(t + 1), self.rewards[t],
+                                self.dones[t], self.epret[t])
         elif self.hip.f32:
             henv.cartpole_step_into(env, self.actions[t], None, self.rewards[t], self.dones[t], self.epret[t],
-                                    obs_f32_out=self.obs[t + 1])
+                                    obs_f32_out=self._obs_at(t + 1))
         else:
-            henv.cartpole_step_into(env, self.actions[t], self.obs[t + 1], self.rewards[t], self.dones[t],
+            henv.cartpole_step_into(env, self.actions[t], self._obs_at(t + 1), self.rewards[t], self.dones[t],
                                     self.epret[t])
 
-    def _trunk_step(self, t):
+    def _trunk_step(self, t, grp=None):
         hp = self.hip
-        x = self.obs
+        if self.ring:
+            hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0])
+            for l in range(1, len(hp.geoms)):
+                hp.layer_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l], self.P, self.E, 1, t, self.bits_rows[l])
+            return
+        p0, np_ = self._group_range(grp)
+        x, xrow0 = self._obs_x(t)
+        row0 = t * self.B + p0 * self.E
         for l in range(len(hp.geoms)):
-            if l == 0 and self.ring:
-                hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0])
-            else:
-                hp.layer_fwd(l, x, self.acts[l], self.bits[l], self.P, self.E, 1, t, self.bits_rows[l])
+            hp.layer_fwd(l, x, self.acts[l], self.bits[l], np_, self.E, 1, 0, self.bits_rows[l], row0=row0, p0=p0,
+                         xrow0=xrow0 + p0 * self.E if l == 0 else None)
             x = self.acts[l]
 
     def _layer_bwd_all(self, T):
@@ -237,10 +290,15 @@ class HipEngine:
             dX = self.grads[l - 1] if l > 0 else None
             hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
 
-    def _forward_step(self, t, greedy=False):
+    def _forward_step(self, t, greedy=False, grp=None):
         hp = self.hip
-        self._trunk_step(t)
+        self._trunk_step(t, grp)
         feat = self.acts[-1][t]
+        if grp is not None:
+            p0, np_ = self._group_range(grp)
+            hp.heads_fwd(feat, self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t, self.T + 1,
+                         greedy=greedy, task=self.model.task, b0=p0 * self.E, b1=(p0 + np_) * self.E)
+            return
         if self.lstm_hip:
             # state entering step t: slot t, reset where the previous step ended an episode
             # (slot 0 is pre-masked by the carry at the end of the previous update)
@@ -305,10 +363,13 @@ class HipEngine:
         T, P, E, B = self.T, self.P, self.E, self.B
         a2c = self.cfg.a2c
         hp = self.hip
-        for t in range(T):
-            self._forward_step(t)
-            self._env_step(t)
-        self._forward_step(T, greedy=True)
+        if self.groups > 1:
+            self._rollout_split()
+        else:
+            for t in range(T):
+                self._forward_step(t)
+                self._env_step(t)
+            self._forward_step(T, greedy=True)
         self._fitness_update()
         self.stats.zero_()
         _lib.call("launch_a2c_grad", self.logits.data_ptr(), self.values.data_ptr(), self.actions.data_ptr(),
@@ -324,6 +385,26 @@ class HipEngine:
             hp.heads_bwd(feat, self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1), self.grad_flat,
                          self.grads[L - 1], task=self.model.task)
         self._layer_bwd_all(T)
+
+    def _rollout_split(self):
+        """The rollout as independent per-path-group chains (forward -> sample -> env step, T times, then the
+        bootstrap forward), group g on stream g, forked from and joined back into the current stream.  Under
+        graph capture each chain is a branch of the rollout hipGraph.  Every kernel computes exactly what the
+        single-stream rollout does for its rows (global RNG keys, same tiling per path), so the result is
+        bit-identical; only the overlap changes."""
+        T = self.T
+        cur = torch.cuda.current_stream()
+        streams = [cur] + self.side_streams
+        for s in self.side_streams:
+            s.wait_stream(cur)
+        for t in range(T + 1):
+            for g, s in enumerate(streams):
+                with torch.cuda.stream(s):
+                    self._forward_step(t, greedy=(t == T), grp=g)
+                    if t < T:
+                        self._env_step(t, grp=g)
+        for s in self.side_streams:
+            cur.wait_stream(s)
 
     def _fitness_update(self):
         _lib.call("launch_fitness_update", self.dones.data_ptr(), self.epret.data_ptr(), self.T, self.P, self.E,
@@ -461,8 +542,6 @@ class HipEngine:
             src = self.frames[:, self.T:self.T + 4]
             self.frames[:, 0:4].copy_(src if self.T >= 4 else src.clone())   # T < 4: the slot ranges overlap
             self.fc[0].copy_(self.fc[self.T])
-        else:
-            self.obs[0].copy_(self.obs[self.T])
         self.ctr.add_(1)
 
     # ------------------------------------------------------------------
@@ -471,9 +550,16 @@ class HipEngine:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.synchronize()
-        self.g_rollout = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_rollout):
-            self._rollout_backward_body()
+        par = self._par
+        self.g_rollouts = []
+        for q in ((0, 1) if self._obs_bufs is not None else (par,)):      # one rollout graph per obs parity
+            self._par = q
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._rollout_backward_body()
+            self.g_rollouts.append(g)
+        self._par = par
+        self.g_rollout = self.g_rollouts[0]
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt):
             self._optimizer_body()
@@ -486,7 +572,7 @@ class HipEngine:
                 self._rollout_backward_body()
                 self._pending_capture = True
                 return
-            self.g_rollout.replay()
+            self.g_rollouts[self._par if self._obs_bufs is not None else 0].replay()
         else:
             self._rollout_backward_body()
 
@@ -501,6 +587,8 @@ class HipEngine:
             if self.use_graph and getattr(self, "_pending_capture", False):
                 self._pending_capture = False
                 self._capture()
+        if self._obs_bufs is not None:
+            self._par ^= 1          # the next rollout starts from the buffer this one's last env step wrote
         self._read_union()
 
     def stats_host(self):
