@@ -43,6 +43,7 @@ __global__ __launch_bounds__(256) void pack_ranges_kernel(float* __restrict__ fl
 
 extern "C" {
 int launch_active_union(const void* geno, const void* frozen, int P, int L, int M, void* out, hipStream_t stream) {
+  if (P <= 0 || L <= 0 || M <= 0) return -22;
   if (P <= 0 || L <= 0 || M <= 0) return -1;
   active_union_kernel<<<L * M, 256, 0, stream>>>((const uint8_t*)geno, (const uint8_t*)frozen, P, L * M,
                                                  (uint8_t*)out);
@@ -51,6 +52,7 @@ int launch_active_union(const void* geno, const void* frozen, int P, int L, int 
 
 int launch_pack_ranges(float* flat, float* packed, const long long* table, int nr, long n, int unpack,
                        hipStream_t stream) {
+  if (nr < 0 || n < 0 || unpack < 0) return -22;
   if (nr <= 0 || n < 0) return -1;
   if (n == 0) return 0;
   long blocks = (n + 255) / 256;

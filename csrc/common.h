@@ -85,6 +85,9 @@ DEVI s4v lds_tr16(const bf16_t* p) {
 DEVI int lane_id() { return threadIdx.x & 63; }
 
 // sample index (in the [T][P*E] batch) of path-local sample s
+// Every exported launcher starts with a guard that returns -22 (EINVAL; 0 for the *_smem sizes) when a size
+// argument is <= 0 or an offset / index argument is negative, so invalid arguments never reach the host-side
+// grid and shared-memory arithmetic (checked by the host ASan/UBSan harness, pathnet_gym_amd/_sanitize.py).
 DEVI long sample_global(int p, int s, int E, int PE, int t0) {
   int t = s / E;
   int e = s - t * E;

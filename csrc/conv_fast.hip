@@ -1368,7 +1368,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__
                                                           OT* __restrict__ dX, int samples_per_wg) {
   using D = DGM<G>;
   constexpr int S = D::S;
-  __shared__ __attribute__((aligned(16))) bf16_t Gs[G::HOWO * DG_PSTR];           // [pos][slot (swizzled)][c]
+  // [pos][slot (swizzled)][c], plus one zeroed block read by out-of-image taps
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[(G::HOWO + 1) * DG_PSTR];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[D::KSMAX * D::NT * 16 * 32];   // [ks][n][k (32), swizzled]
   __shared__ int mods[MAXM_F];
   __shared__ int atab[D::NRT * 16];
@@ -1449,6 +1450,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__
                                         ((S * jj + 1 < G::WIN) << 15))
                            : (uint16_t)0xFFFF;
   }
+  for (int i = tid; i < DG_PSTR; i += 256) Gs[G::HOWO * DG_PSTR + i] = 0;
   // the lane's columns n = nt*16 + c16 -> (ph*WIN + pw)*8 + ci and its class offsets (ph, pw)
   int nofs[D::NT], nph[D::NT], npw[D::NT];
 #pragma unroll
@@ -1466,6 +1468,28 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__
     for (int j = 0; j < GIT; ++j) {
       const int pos = tid + 256 * j;
       if (pos < G::HOWO) {
+        if (sizeof(GT) == 2 && g_scale == 1.f) {
+          // bf16 G, unit scale: mask the raw bf16 words with the ReLU bits directly (v_bfe_i32 sign-extends a
+          // bit to 0 / ~0, v_bfi merges the two halves) -- 4 VALU per channel pair instead of unpack, select,
+          // repack
+          const uint32_t u[4] = {graw[j].x, graw[j].y, graw[j].z, graw[j].w};
+#pragma unroll
+          for (int a = 0; a < DG_NSMAX; ++a) {
+            if (a < nslot) {
+              const uint32_t b = gbr[j][a];
+              uint4 o;
+              uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)b, 2 * e, 1);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)b, 2 * e + 1, 1);
+                ow[e] = u[e] & ((lo & 0xFFFFu) | (hi & 0xFFFF0000u));
+              }
+              *reinterpret_cast<uint4*>(Gs + pos * DG_PSTR + (a ^ dg_swz(pos)) * 8) = o;
+            }
+          }
+          continue;
+        }
         float gg[8];
         if constexpr (sizeof(GT) == 2) {
           const uint32_t u[4] = {graw[j].x, graw[j].y, graw[j].z, graw[j].w};
@@ -1482,9 +1506,11 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__
 #pragma unroll
         for (int a = 0; a < DG_NSMAX; ++a) {
           if (a < nslot) {
+            const int b = (int)gbr[j][a];
             float m[8];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) m[c] = ((gbr[j][a] >> c) & 1u) ? gg[c] : 0.f;
+            for (int c = 0; c < 8; ++c)
+              m[c] = __uint_as_float(__float_as_uint(gg[c]) & (uint32_t)__builtin_amdgcn_sbfe(b, c, 1));
             *reinterpret_cast<s8v*>(Gs + pos * DG_PSTR + (a ^ dg_swz(pos)) * 8) = f32x8_to_bf16(m);
           }
         }
@@ -1507,12 +1533,12 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__
       for (int tap = 0; tap < D::NTAP; ++tap) {
         const int ta = tap / D::NA, tb = tap - ta * D::NA;
         const bool ok = (amask >> tap) & 1;
-        const int apos = ok ? ab - (ta * G::WO + tb) : 0;
+        // out-of-image taps read the zeroed position block HOWO (one select per tap, none per fragment)
+        const int apos = ok ? ab - (ta * G::WO + tb) : G::HOWO;
         const bf16_t* ap = Gs + apos * DG_PSTR + (grp ^ dg_swz(apos)) * 8;
         const bf16_t* bp = Bs + (tap * ns4 * D::NT * 16 + c16) * 32 + (grp ^ dg_swz(c16)) * 8;
         for (int a4 = 0; a4 < ns4; ++a4) {
-          s8v af = *reinterpret_cast<const s8v*>(ap + a4 * 32);
-          if (!ok) af = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+          const s8v af = *reinterpret_cast<const s8v*>(ap + a4 * 32);
 #pragma unroll
           for (int nt = 0; nt < D::NT; ++nt) {
             const s8v bf = *reinterpret_cast<const s8v*>(bp + (a4 * D::NT * 16 + nt * 16) * 32);
@@ -1704,6 +1730,8 @@ int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, 
                   int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH,
                   int KW, int S, int P, int E, int T, int t0, long br, float is, float os, const float* hcorr,
                   const void* Wc_bf16, hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      P <= 0 || E <= 0 || T <= 0 || br <= 0 || u8in < 0 || bias_off < 0 || layer < 0 || t0 < 0) return -22;
   if (M > 2 * NCT) return 0;
   if (u8in && (!F16_FWD || !hcorr)) {      // bf16 operands: the bf16 weight copy, no offset correction
     Wc = Wc_bf16;
@@ -1734,6 +1762,8 @@ int fast_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc, 
 int fast_conv_wgrad(const void* X, int u8in, const float* Gr, const void* bits, float* grad, long w_off, long b_off,
                     int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win, int Cin,
                     int KH, int KW, int S, int P, int E, int T, long br, float is, float gs, hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      P <= 0 || E <= 0 || T <= 0 || br <= 0 || u8in < 0 || w_off < 0 || b_off < 0 || layer < 0) return -22;
   if (M > 2 * NCT) return 0;
 #define WG(Gx)                                                                                                 \
   if (is_shape<Gx>(Hin, Win, Cin, KH, KW, S, u8in)) {                                                          \
@@ -1766,6 +1796,8 @@ int fast_conv1_ring_fwd(const void* frames, const void* fc, void* Y, void* bits,
                         long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int P, int E,
                         int T, int t0, int nslots, long br, float is, float os, const float* hcorr,
                         const void* Wc_bf16, hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || P <= 0 || E <= 0 || T <= 0 || nslots <= 0 || br <= 0 || bias_off < 0 ||
+      layer < 0 || t0 < 0) return -22;
   if (M > 2 * NCT) return -22;
   if ((E * C1::HOWO) % 16) return -2;
   if (nslots < t0 + T + 3) return -33;
@@ -1786,6 +1818,8 @@ int fast_conv1_ring_fwd(const void* frames, const void* fc, void* Y, void* bits,
 int fast_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, const void* bits, float* grad,
                           long w_off, long b_off, int chunk, const int* ai, const int* ac, int layer, int L, int M,
                           int P, int E, int T, int nslots, long br, float is, float gs, hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || P <= 0 || E <= 0 || T <= 0 || nslots <= 0 || br <= 0 || w_off < 0 ||
+      b_off < 0 || layer < 0) return -22;
   if (M > 2 * NCT) return -22;
   if (nslots < T + 3) return -33;
   if ((long)T * E / 24 + 3 > 1024) return -34;   // samples per workgroup vs the LDS first-channel table
@@ -1800,6 +1834,8 @@ int fast_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, c
 int fast_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,
                     const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH, int KW, int S, int P,
                     int E, int T, long br, float gs, float* dX, hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      P <= 0 || E <= 0 || T <= 0 || br <= 0 || w_off < 0 || layer < 0) return -22;
 #define DG(Gx)                                                                                          \
   if (is_shape<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                      \
     const int rc = dgrad_t<Gx>(Gr, bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs, dX, st); \
@@ -1828,6 +1864,8 @@ int fast_conv_dgrad_bf16(const void* Gr, int g_bf16, const void* bits, const flo
                          const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH,
                          int KW, int S, int P, int E, int T, long br, float gs, void* dX, int dx_bf16,
                          hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      P <= 0 || E <= 0 || T <= 0 || br <= 0 || g_bf16 < 0 || w_off < 0 || layer < 0 || dx_bf16 < 0) return -22;
   if (M > 10 || !DGRAD_MFMA) return 0;
 #define DGB(Gx)                                                                                               \
   if (is_shape<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                            \
@@ -1855,6 +1893,8 @@ int fast_conv_wgrad_bf16g(const void* X, int u8in, const void* Gr, const void* b
                           long b_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin,
                           int Win, int Cin, int KH, int KW, int S, int P, int E, int T, long br, float is, float gs,
                           hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      P <= 0 || E <= 0 || T <= 0 || br <= 0 || u8in < 0 || w_off < 0 || b_off < 0 || layer < 0) return -22;
   if (M > 2 * NCT || !SLAB_WGRAD) return 0;
   const bf16_t* g = (const bf16_t*)Gr;
   if (is_shape<C2>(Hin, Win, Cin, KH, KW, S, u8in)) {

@@ -463,6 +463,8 @@ int launch_pong_step(void* state, void* counter, const int* actions, int n_actio
                      const int* tables, float* reward, void* done, float* epret, int B, unsigned seed, int frameskip,
                      int max_steps, int no_op_max, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
                      int b0, hipStream_t stream) {
+  if (n_actions <= 0 || B <= 0 || frameskip < 0 || max_steps < 0 || no_op_max < 0 || g_bg < 0 || g_wall < 0 ||
+      g_cpu < 0 || g_player < 0 || g_ball < 0 || b0 < 0) return -22;
   // envs [b0, B): one path group of the split rollout (runtime/engine.py); per-env state and RNG keys are global
   if (b0 < 0 || b0 >= B) return -22;
   pong_step_kernel<false><<<B - b0, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions,
@@ -478,6 +480,8 @@ int launch_pong_step_ring(void* state, void* counter, const int* actions, int n_
                           long out_stride, const void* fc_in, void* fc_out, const int* tables, float* reward,
                           void* done, float* epret, int B, unsigned seed, int frameskip, int max_steps, int no_op_max,
                           int g_bg, int g_wall, int g_cpu, int g_player, int g_ball, hipStream_t stream) {
+  if (n_actions <= 0 || out_stride <= 0 || B <= 0 || frameskip < 0 || max_steps < 0 || no_op_max < 0 || g_bg < 0 ||
+      g_wall < 0 || g_cpu < 0 || g_player < 0 || g_ball < 0) return -22;
   if (out_stride < 160 * 120 || out_stride % 16) return -22;
   pong_step_kernel<true><<<B, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions, nullptr,
                                                 (uint32_t*)frame_out, tables, reward, (uint8_t*)done, epret, seed,
@@ -489,6 +493,7 @@ int launch_pong_step_ring(void* state, void* counter, const int* actions, int n_
 int launch_cartpole_step(float* state, int* steps, float* epret, void* counter, const int* actions, int B,
                          unsigned seed, int max_steps, float* obs_f32, void* obs_bf16, float* reward, void* done,
                          float* epret_out, hipStream_t stream) {
+  if (B <= 0 || max_steps < 0) return -22;
   cartpole_step_kernel<<<(B + 255) / 256, 256, 0, stream>>>(state, steps, epret, (uint32_t*)counter, actions, B, seed,
                                                             max_steps, obs_f32, (bf16_t*)obs_bf16, reward,
                                                             (uint8_t*)done, epret_out);

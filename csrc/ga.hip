@@ -184,6 +184,7 @@ __global__ __launch_bounds__(64) void ga_compact_inverse_kernel(const float* __r
 extern "C" {
 int launch_ga_step(void* geno, float* fitness, int* slots, long long* gen_ctr, int* events, int P, int L, int M,
                    int N, int B, int C, unsigned seed, void* reset, hipStream_t stream) {
+  if (P <= 0 || L <= 0 || M <= 0 || N <= 0 || B <= 0 || C <= 0) return -22;
   if (C > GA_MAXC || B > GA_MAXB || L > GA_MAXL || M > GA_MAXM || C < 1) return -1;
   ga_step_kernel<<<1, 256, (size_t)P, stream>>>((uint8_t*)geno, fitness, slots, gen_ctr, events, P, L, M, N, B, C,
                                                 seed, (uint8_t*)reset);
@@ -192,6 +193,7 @@ int launch_ga_step(void* geno, float* fitness, int* slots, long long* gen_ctr, i
 
 int launch_ga_compact(const void* geno, const void* frozen, int p_off, int P_local, int L, int M, float* mask,
                       int* act_idx, int* act_cnt, int* inv_path, int* inv_slot, int* inv_cnt, hipStream_t stream) {
+  if (P_local <= 0 || L <= 0 || M <= 0 || p_off < 0) return -22;
   if (M > GA_MAXM) return -1;
   const int n1 = P_local * L;
   ga_compact_paths_kernel<<<(n1 + 255) / 256, 256, 0, stream>>>((const uint8_t*)geno, (const uint8_t*)frozen, p_off,

@@ -364,6 +364,8 @@ extern "C" {
 int launch_heads_fwd_sample(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb, int A,
                             int B, float* logits, float* value, int* actions, unsigned seed, const long long* ctr,
                             int t, int T, int greedy, int b0, hipStream_t stream) {
+  if (F <= 0 || A <= 0 || B <= 0 || T <= 0 || pw < 0 || pb < 0 || vw < 0 || vb < 0 || t < 0 || greedy < 0 ||
+      b0 < 0) return -22;
   if (A > AMAX || A < 1 || b0 < 0 || b0 >= B) return -1;
   if (!heads_fwd_lanes_launch<bf16_t>(feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T,
                                       greedy, b0, stream))
@@ -376,6 +378,8 @@ int launch_heads_fwd_sample(const void* feat, int F, const float* flat, long pw,
 int launch_heads_fwd_sample_f32(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
                                 int A, int B, float* logits, float* value, int* actions, unsigned seed,
                                 const long long* ctr, int t, int T, int greedy, int b0, hipStream_t stream) {
+  if (F <= 0 || A <= 0 || B <= 0 || T <= 0 || pw < 0 || pb < 0 || vw < 0 || vb < 0 || t < 0 || greedy < 0 ||
+      b0 < 0) return -22;
   if (A > AMAX || A < 1 || b0 < 0 || b0 >= B) return -1;
   if (!heads_fwd_lanes_launch<float>(feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T,
                                      greedy, b0, stream))
@@ -389,6 +393,7 @@ int launch_a2c_grad(const float* logits, const float* values, const int* actions
                     const void* dones, const float* vboot, int T, int B, int A, float gamma, float lam, float rclip,
                     float beta, float vcoef, float weight, float* dlogits, float* dvalue, float* stats,
                     hipStream_t stream) {
+  if (T <= 0 || B <= 0 || A <= 0) return -22;
   if (A > AMAX) return -1;
   a2c_grad_kernel<<<(unsigned)(((long)T * B + 255) / 256), 256, 0, stream>>>(logits, values, actions, rewards, (const uint8_t*)dones,
                                                         vboot, T, B, A, gamma, lam, rclip, beta, vcoef, weight,
@@ -421,6 +426,7 @@ extern "C" {
 int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float* dvalue, int N, int A,
                      const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
                      hipStream_t stream) {
+  if (F <= 0 || N <= 0 || A <= 0 || pw < 0 || pb < 0 || vw < 0 || vb < 0) return -22;
   return heads_bwd_launch<bf16_t>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, nullptr,
                                   stream);
 }
@@ -428,18 +434,21 @@ int launch_heads_bwd(const void* feat, int F, const float* dlogits, const float*
 int launch_heads_bwd_f32(const void* feat, int F, const float* dlogits, const float* dvalue, int N, int A,
                          const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
                          hipStream_t stream) {
+  if (F <= 0 || N <= 0 || A <= 0 || pw < 0 || pb < 0 || vw < 0 || vb < 0) return -22;
   return heads_bwd_launch<float>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, nullptr,
                                  stream);
 }
 
 // deterministic heads backward (fixed-order chunk reduction); part: ceil(N/128) * (F*A + F + A + 1) floats
 long heads_bwd_part_numel(int N, int F, int A) {
+  if (N <= 0 || F <= 0 || A <= 0) return -1;
   return (long)((N + HB_ROWS - 1) / HB_ROWS) * ((long)F * A + F + A + 1);
 }
 
 int launch_heads_bwd_det(const void* feat, int f32, int F, const float* dlogits, const float* dvalue, int N, int A,
                          const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
                          float* part, hipStream_t stream) {
+  if (F <= 0 || N <= 0 || A <= 0 || f32 < 0 || pw < 0 || pb < 0 || vw < 0 || vb < 0) return -22;
   if (!part) return -1;
   if (f32) return heads_bwd_launch<float>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, part,
                                           stream);

@@ -273,6 +273,7 @@ extern "C" {
 int launch_lstm_fwd(const void* X, int ldx, const void* hprev, const float* cprev, const uint8_t* prev_done,
                     const void* KpT, const float* flat, long b_off, void* hout, float* cout, float* gates, void* xh,
                     int F, int H, int B, hipStream_t stream) {
+  if (ldx <= 0 || F <= 0 || H <= 0 || B <= 0 || b_off < 0) return -22;
   if (F % 64 != 0 || H % 64 != 0 || ldx % 8 != 0) return -1;
   dim3 grid((B + 63) / 64, H / 16);
   lstm_fwd_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)X, ldx, (const bf16_t*)hprev, cprev, prev_done,
@@ -284,6 +285,7 @@ int launch_lstm_fwd(const void* X, int ldx, const void* hprev, const float* cpre
 int launch_lstm_bwd_point(const float* dh_heads, const float* dh_rec, const float* dc_rec, const uint8_t* done_t,
                           const float* gates, const float* c_t, const float* c_prev, const uint8_t* prev_done,
                           float* dz, float* dc_out, int H, int B, hipStream_t stream) {
+  if (H <= 0 || B <= 0) return -22;
   const long n = (long)B * H;
   lstm_bwd_point_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(dh_heads, dh_rec, dc_rec, done_t, gates,
                                                                          c_t, c_prev, prev_done, dz, dc_out, H, B);
@@ -292,6 +294,7 @@ int launch_lstm_bwd_point(const float* dh_heads, const float* dh_rec, const floa
 
 int launch_lstm_bwd_gemm(const float* dz, const void* Kb, float* dx, int lddx, float* dh_prev, int F, int H, int B,
                          hipStream_t stream) {
+  if (lddx <= 0 || F <= 0 || H <= 0 || B <= 0) return -22;
   if (F % 64 != 0 || H % 64 != 0) return -1;
   dim3 grid((B + 63) / 64, (F + H) / 64);
   lstm_bwd_gemm_kernel<<<grid, 256, 0, stream>>>(dz, (const bf16_t*)Kb, dx, lddx, dh_prev, F, H, B);
@@ -300,6 +303,7 @@ int launch_lstm_bwd_gemm(const float* dz, const void* Kb, float* dx, int lddx, f
 
 int launch_lstm_wgrad(const void* xh, const float* dz, float* grad, long k_off, long b_off, int F, int H, long R,
                       int rows_per_chunk, hipStream_t stream) {
+  if (F <= 0 || H <= 0 || R <= 0 || rows_per_chunk <= 0 || k_off < 0 || b_off < 0) return -22;
   if (F % 64 != 0 || H % 64 != 0 || rows_per_chunk % 32 != 0) return -1;
   dim3 grid((F + H) / 64, (4 * H) / 64, (unsigned)((R + rows_per_chunk - 1) / rows_per_chunk));
   lstm_wgrad_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)xh, dz, grad, k_off, b_off, F, H, R, rows_per_chunk);
@@ -307,6 +311,7 @@ int launch_lstm_wgrad(const void* xh, const float* dz, float* grad, long k_off, 
 }
 
 int launch_lstm_refresh(const float* flat, long k_off, int F, int H, void* KpT, void* Kb, hipStream_t stream) {
+  if (F <= 0 || H <= 0 || k_off < 0) return -22;
   const long n = (long)(F + H) * 4 * H;
   lstm_refresh_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(flat, k_off, F, H, (bf16_t*)KpT,
                                                                        (bf16_t*)Kb);
@@ -315,6 +320,7 @@ int launch_lstm_refresh(const float* flat, long k_off, int F, int H, void* KpT, 
 
 int launch_lstm_carry(const void* hT, const float* cT, const uint8_t* done_last, void* h0, float* c0, int H, int B,
                       hipStream_t stream) {
+  if (H <= 0 || B <= 0) return -22;
   const long n = (long)B * H;
   lstm_carry_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>((const bf16_t*)hT, cT, done_last,
                                                                      (bf16_t*)h0, c0, H, B);

@@ -132,7 +132,8 @@ extern "C" {
 
 int launch_refresh_weights_cmajor(const float* flat, long w_off, int chunk, int KH, int KW, int CIN, int Cout, int M,
                                   void* Wc, int f16, hipStream_t stream) {
-  if ((KH * KW * CIN) % 32) return -22;
+  if (chunk <= 0 || KH <= 0 || KW <= 0 || CIN <= 0 || Cout <= 0 || M <= 0 || w_off < 0 || f16 < 0) return -22;
+  if (((long)KH * KW * CIN) % 32) return -22;
   const long n = (long)M * KH * KW * CIN * Cout;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;
@@ -146,6 +147,7 @@ int launch_rmsprop(float* w, const float* g, float* ms, float* mom, const int* b
                    const long long* blk_end, int nblk, float* partial, const int* seg_blk0, const void* trainable,
                    const float* lr_ptr, float* status, float decay, float momentum, float eps, float clip,
                    hipStream_t stream) {
+  if (nblk < 0) return -22;
   if (nblk <= 0) return -1;
   seg_sqnorm_kernel<<<nblk, 256, 0, stream>>>(g, blk_beg, blk_end, partial);
   rmsprop_apply_kernel<<<nblk, 256, 0, stream>>>(w, g, ms, mom, blk_seg, blk_beg, blk_end, partial, seg_blk0, nblk,
@@ -156,6 +158,7 @@ int launch_rmsprop(float* w, const float* g, float* ms, float* mom, const int* b
 
 int launch_refresh_weights_f16(const float* flat, long w_off, int chunk, int K, int KP, int Cout, int M, void* Wh,
                                float* hcorr, hipStream_t stream) {
+  if (chunk <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || M <= 0 || w_off < 0) return -22;
   if (M <= 0 || Cout <= 0 || KP < K) return -1;
   refresh_f16_kernel<<<M * Cout, 256, 0, stream>>>(flat, w_off, chunk, K, KP, Cout, (uint16_t*)Wh, hcorr);
   return (int)hipGetLastError();
@@ -163,6 +166,7 @@ int launch_refresh_weights_f16(const float* flat, long w_off, int chunk, int K, 
 
 int launch_refresh_weights(const float* flat, long w_off, int chunk, int K, int KP, int Cout, int M, void* Wc,
                            void* WcT, hipStream_t stream) {
+  if (chunk <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || M <= 0 || w_off < 0) return -22;
   const long n = (long)M * KP * Cout;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;

@@ -680,6 +680,7 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_kernel(
 extern "C" {
 
 size_t conv_wgrad_smem(int KP) {
+  if (KP <= 0) return 0;
   return (size_t)32 * (KP + 8) * 2 + 32 * (16 * 8 + 8) * 2 + 128 * 4 + (KP / 8) * 4 + MAXM * 4;
 }
 
@@ -687,6 +688,9 @@ int launch_conv_wgrad(const void* X, int u8in, const float* G, const void* bits,
                       long b_off, int chunk, const int* act_idx, const int* act_cnt, int layer, int L, int M,
                       int Hin, int Win, int Cin, int KH, int KW, int S, int Ho, int Wo, int K, int KP, int P, int E,
                       int T, long bits_rows, int rows_per_chunk, float in_scale, float g_scale, hipStream_t stream) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      Ho <= 0 || Wo <= 0 || K <= 0 || KP <= 0 || P <= 0 || E <= 0 || T <= 0 || bits_rows <= 0 ||
+      rows_per_chunk <= 0 || u8in < 0 || w_off < 0 || b_off < 0 || layer < 0) return -22;
   if (M > MAXM || KP % 32 != 0 || KP > 512 || rows_per_chunk % 32 != 0) return -1;
   ConvGeomB g{Hin, Win, Cin, KH, KW, S, Ho, Wo, K, KP};
   const long rows = (long)T * E * Ho * Wo;
@@ -707,6 +711,8 @@ int launch_conv_dgrad(const float* G, const void* bits, const float* flat, long 
                       const int* act_idx, const int* act_cnt, int layer, int L, int M, int Hin, int Win, int Cin,
                       int KH, int KW, int S, int Ho, int Wo, int P, int E, int T, long bits_rows, float g_scale,
                       float* dX, hipStream_t stream) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      Ho <= 0 || Wo <= 0 || P <= 0 || E <= 0 || T <= 0 || bits_rows <= 0 || w_off < 0 || layer < 0) return -22;
   if (Cin != 8 || M > MAXM) return -1;
   ConvGeomB g{Hin, Win, Cin, KH, KW, S, Ho, Wo, KH * KW * Cin, 0};
   const long npix = (long)T * E * Hin * Win;
@@ -720,6 +726,8 @@ int launch_conv_dgrad(const float* G, const void* bits, const float* flat, long 
 int launch_fc_dgrad(const float* G, const void* bits, const void* WcT, const int* act_idx, const int* act_cnt,
                     int layer, int L, int M, int K, int KP, int Cout, int P, int E, int T, long bits_rows,
                     float g_scale, float* dX, void* Gm, hipStream_t stream) {
+  if (L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || bits_rows <= 0 ||
+      layer < 0) return -22;
   if (M > MAXM || Cout % 32 != 0) return -1;
   if (Cout == 256) {
     const int nchunks = (K + 127) / 128;
@@ -741,6 +749,8 @@ int launch_fc_dgrad(const float* G, const void* bits, const void* WcT, const int
 int launch_fc_wgrad_gm(const void* X, int ldx, const void* Gm, float* grad, long w_off, long b_off, int chunk,
                        const int* inv_path, const int* inv_slot, const int* inv_cnt, int layer, int M, int Pmax,
                        int K, int Cout, int P, int E, int T, long bits_rows, int nsplit, hipStream_t stream) {
+  if (ldx <= 0 || chunk <= 0 || M <= 0 || Pmax <= 0 || K <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 ||
+      bits_rows <= 0 || nsplit <= 0 || w_off < 0 || b_off < 0 || layer < 0) return -22;
   if (Cout != 256 || ldx % 8 != 0 || K % 8 != 0 || nsplit < 1) return -1;
   const int kt = (K + 127) / 128;
   fc_wgrad_gm_kernel<256><<<kt * M * nsplit, 512, 0, stream>>>((const bf16_t*)X, ldx, (const bf16_t*)Gm, grad, w_off,
@@ -753,6 +763,8 @@ int launch_fc_wgrad(const void* X, int ldx, const float* G, const void* bits, fl
                     int chunk, const int* inv_path, const int* inv_slot, const int* inv_cnt, int layer, int M,
                     int Pmax, int K, int Cout, int P, int E, int T, long bits_rows, float g_scale,
                     hipStream_t stream) {
+  if (ldx <= 0 || chunk <= 0 || M <= 0 || Pmax <= 0 || K <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 ||
+      bits_rows <= 0 || w_off < 0 || b_off < 0 || layer < 0) return -22;
   if (Cout % 16 != 0 || ldx % 8 != 0) return -1;
   // split the users of each module so the grid covers >= ~2K workgroups
   const int tiles = ((K + 63) / 64) * ((Cout + 63) / 64) * M;

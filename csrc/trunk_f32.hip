@@ -866,6 +866,7 @@ __global__ __launch_bounds__(256) void refresh_weights_f32_kernel(const float* _
 extern "C" {
 
 size_t conv_wgrad_f32_smem(int KP) {
+  if (KP <= 0) return 0;
   return (size_t)32 * (KP + 16) * 4 + 32 * F32_WG_GS * 4 + 32 * 4 * 8 * 4 + (KP / 8) * 4;
 }
 
@@ -873,6 +874,9 @@ int launch_conv_fwd_f32(const void* X, int u8in, void* Y, void* bits, const void
                         long bias_off, int chunk, const int* act_idx, const int* act_cnt, int layer, int L, int M,
                         int Hin, int Win, int Cin, int KH, int KW, int S, int Ho, int Wo, int K, int KP, int P, int E,
                         int T, int t0, long bits_rows, float in_scale, float out_scale, hipStream_t stream) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      Ho <= 0 || Wo <= 0 || K <= 0 || KP <= 0 || P <= 0 || E <= 0 || T <= 0 || bits_rows <= 0 || u8in < 0 ||
+      bias_off < 0 || layer < 0 || t0 < 0) return -22;
   if (M > F32_MAXM || KP % 32 != 0 || KP > 512 || (E * Ho * Wo) % 16 != 0 || (KW * Cin) % 8 != 0) return -1;
   ConvGeomF g{Hin, Win, Cin, KH, KW, S, Ho, Wo, K, KP};
   constexpr int RT = 2;
@@ -895,6 +899,8 @@ int launch_conv_fwd_f32(const void* X, int u8in, void* Y, void* bits, const void
 int launch_fc_fwd_f32(const void* X, int ldx, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
                       int chunk, const int* act_idx, const int* act_cnt, int layer, int L, int M, int K, int KP,
                       int Cout, int P, int E, int T, int t0, long bits_rows, float out_scale, hipStream_t stream) {
+  if (ldx <= 0 || chunk <= 0 || L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 ||
+      bits_rows <= 0 || bias_off < 0 || layer < 0 || t0 < 0) return -22;
   if (M > F32_MAXM || KP % 32 != 0 || Cout % 32 != 0 || ldx < K) return -1;
   const long rows = (long)T * E;
   if (rows <= 32) {
@@ -922,6 +928,9 @@ int launch_conv_wgrad_f32(const void* X, int xkind, const float* G, const void* 
                           int Pmax, int Hin, int Win, int Cin, int KH, int KW, int S, int Ho, int Wo, int K, int KP,
                           int P, int E, int T, long bits_rows, int nch, float in_scale, float g_scale,
                           hipStream_t stream) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Pmax <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 ||
+      S <= 0 || Ho <= 0 || Wo <= 0 || K <= 0 || KP <= 0 || P <= 0 || E <= 0 || T <= 0 || bits_rows <= 0 ||
+      nch <= 0 || xkind < 0 || w_off < 0 || b_off < 0 || layer < 0) return -22;
   if (M > F32_MAXM || KP % 32 != 0 || KP > 256 || nch < 1 || (KW * Cin) % 8 != 0) return -1;
   if ((long)T * E * Ho * Wo >= (1L << 31)) return -1;
   ConvGeomF g{Hin, Win, Cin, KH, KW, S, Ho, Wo, K, KP};
@@ -951,6 +960,8 @@ int launch_conv_dgrad_f32(const float* G, const void* bits, const float* flat, l
                           const int* act_idx, const int* act_cnt, int layer, int L, int M, int Hin, int Win, int Cin,
                           int KH, int KW, int S, int Ho, int Wo, int P, int E, int T, long bits_rows, float g_scale,
                           float* dX, hipStream_t stream) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      Ho <= 0 || Wo <= 0 || P <= 0 || E <= 0 || T <= 0 || bits_rows <= 0 || w_off < 0 || layer < 0) return -22;
   if (Cin != 8 || M > F32_MAXM) return -1;
   const long npix = (long)T * E * Hin * Win;
   if (npix >= (1L << 31)) return -1;
@@ -966,6 +977,8 @@ int launch_conv_dgrad_f32(const float* G, const void* bits, const float* flat, l
 int launch_fc_dgrad_f32(const float* G, const void* bits, const void* WcT, const int* act_idx, const int* act_cnt,
                         int layer, int L, int M, int K, int KP, int Cout, int P, int E, int T, long bits_rows,
                         float g_scale, float* dX, hipStream_t stream) {
+  if (L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || bits_rows <= 0 ||
+      layer < 0) return -22;
   if (M > F32_MAXM || Cout % 32 != 0) return -1;
   dim3 grid((unsigned)(((long)T * E + 63) / 64), (K + 63) / 64, P);
   fc_dgrad_f32_kernel<<<grid, 256, 0, stream>>>(G, (const uint16_t*)bits, (const float*)WcT, act_idx, act_cnt, layer,
@@ -977,6 +990,8 @@ int launch_fc_wgrad_f32(const void* X, int xkind, int ldx, const float* G, const
                         int chunk, const int* inv_path, const int* inv_slot, const int* inv_cnt, int layer, int M,
                         int Pmax, int K, int Cout, int P, int E, int T, long bits_rows, float g_scale,
                         hipStream_t stream) {
+  if (ldx <= 0 || chunk <= 0 || M <= 0 || Pmax <= 0 || K <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 ||
+      bits_rows <= 0 || xkind < 0 || w_off < 0 || b_off < 0 || layer < 0) return -22;
   if (Cout % 16 != 0 || ldx < K || (xkind != XBF16 && xkind != XF32)) return -1;
   dim3 grid((K + 63) / 64, (Cout + 63) / 64, M);
   if (xkind == XBF16)
@@ -992,6 +1007,7 @@ int launch_fc_wgrad_f32(const void* X, int xkind, int ldx, const float* G, const
 
 int launch_refresh_weights_f32(const float* flat, long w_off, int chunk, int K, int KP, int Cout, int M, void* Wc,
                                void* WcT, hipStream_t stream) {
+  if (chunk <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || M <= 0 || w_off < 0) return -22;
   const long n = (long)M * KP * Cout;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;

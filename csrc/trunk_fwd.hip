@@ -432,6 +432,7 @@ __global__ __launch_bounds__(256) void fc_fwd_mw_kernel(
 extern "C" {
 
 size_t conv_fwd_smem(int KP, int M) {
+  if (KP <= 0 || M <= 0) return 0;
   const int ncap = ((M + 1) >> 1) * 16;
   return (size_t)ncap * (KP + 8) * 2 + (KP / 8) * 4 + ncap * 4 + MAXM * 4;
 }
@@ -440,6 +441,9 @@ int launch_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc
                     int chunk, const int* act_idx, const int* act_cnt, int layer, int L, int M, int Hin, int Win,
                     int Cin, int KH, int KW, int S, int Ho, int Wo, int K, int KP, int P, int E, int T, int t0,
                     long bits_rows, float in_scale, float out_scale, hipStream_t stream) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 ||
+      Ho <= 0 || Wo <= 0 || K <= 0 || KP <= 0 || P <= 0 || E <= 0 || T <= 0 || bits_rows <= 0 || u8in < 0 ||
+      bias_off < 0 || layer < 0 || t0 < 0) return -22;
   if (M > MAXM || KP % 32 != 0 || (E * Ho * Wo) % 16 != 0) return -1;
   ConvGeom g{Hin, Win, Cin, KH, KW, S, Ho, Wo, K, KP};
   const long rows = (long)T * E * Ho * Wo;
@@ -459,6 +463,8 @@ int launch_conv_fwd(const void* X, int u8in, void* Y, void* bits, const void* Wc
 int launch_fc_fwd(const void* X, int ldx, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,
                   int chunk, const int* act_idx, const int* act_cnt, int layer, int L, int M, int K, int KP, int Cout,
                   int P, int E, int T, int t0, long bits_rows, float out_scale, hipStream_t stream) {
+  if (ldx <= 0 || chunk <= 0 || L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 ||
+      bits_rows <= 0 || bias_off < 0 || layer < 0 || t0 < 0) return -22;
   if (M > MAXM || KP % 32 != 0 || Cout % 32 != 0 || ldx % 8 != 0) return -1;
   const long rows = (long)T * E;
   if (rows <= 32 && Cout % 64 == 0) {

@@ -216,6 +216,7 @@ extern "C" {
 int launch_typed_fc_fwd(const float* x, int K, const float* flat, long off, long chunk, int C, int M,
                         const float* mask, const int* types, int P, int rpp, float* out, void* relu,
                         hipStream_t stream) {
+  if (K <= 0 || chunk <= 0 || C <= 0 || M <= 0 || P <= 0 || rpp <= 0 || off < 0) return -22;
   if (C > TF_MAXC || M > TF_MAXM || TF_RT * C > 256 * TF_PPT || P < 1 || rpp < 1) return -1;
   dim3 grid(P, (rpp + TF_RT - 1) / TF_RT);
   typed_fc_fwd_kernel<<<grid, 256, 0, stream>>>(x, K, flat, off, chunk, C, M, mask, types, rpp, out,
@@ -226,6 +227,7 @@ int launch_typed_fc_fwd(const float* x, int K, const float* flat, long off, long
 int launch_typed_fc_dgrad(const float* dy, int K, const float* flat, long off, long chunk, int C, int M,
                           const float* mask, const int* types, int P, int rpp, const void* relu, float* dx,
                           hipStream_t stream) {
+  if (K <= 0 || chunk <= 0 || C <= 0 || M <= 0 || P <= 0 || rpp <= 0 || off < 0) return -22;
   if (C > TF_MAXC || M > TF_MAXM || P < 1 || rpp < 1) return -1;
   dim3 grid(P, (rpp + TF_RT - 1) / TF_RT);
   const size_t lds = (size_t)M * TF_RT * C * sizeof(float);
@@ -237,6 +239,7 @@ int launch_typed_fc_dgrad(const float* dy, int K, const float* flat, long off, l
 int launch_typed_fc_wgrad(const float* x, const float* dy, int K, long off, long chunk, int C, int M, int P,
                           const float* mask, const int* types, int rpp, const void* relu, float* gflat,
                           hipStream_t stream) {
+  if (K <= 0 || chunk <= 0 || C <= 0 || M <= 0 || P <= 0 || rpp <= 0 || off < 0) return -22;
   if (C > TF_MAXC || M > TF_MAXM || 16 * C > 256 * TF_PPT || P < 1 || rpp < 1) return -1;
   dim3 grid(M, (K + 15) / 16);
   typed_fc_wgrad_kernel<<<grid, 256, 0, stream>>>(x, dy, K, off, chunk, C, M, P, mask, types, rpp,
@@ -468,6 +471,7 @@ extern "C" {
 int launch_typed_fc_fwd_mfma(const float* x, int K, const float* flat, long off, long chunk, int C, int M,
                              const float* mask, const int* types, int P, int rpp, float* out, void* relu,
                              hipStream_t stream) {
+  if (K <= 0 || chunk <= 0 || C <= 0 || M <= 0 || P <= 0 || rpp <= 0 || off < 0) return -22;
   if (M > TF_MAXM || P < 1 || rpp < 1 || K < 1 || C < 1) return -1;
   dim3 grid(P, (rpp + TM_T - 1) / TM_T, (C + TM_T - 1) / TM_T);
   typed_fc_fwd_mfma_kernel<<<grid, 256, 0, stream>>>(x, K, flat, off, chunk, C, M, mask, types, rpp, out,
@@ -478,6 +482,7 @@ int launch_typed_fc_fwd_mfma(const float* x, int K, const float* flat, long off,
 int launch_typed_fc_dgrad_mfma(const float* dy, int K, const float* flat, long off, long chunk, int C, int M,
                                const float* mask, const int* types, int P, int rpp, const void* relu, float* dx,
                                hipStream_t stream) {
+  if (K <= 0 || chunk <= 0 || C <= 0 || M <= 0 || P <= 0 || rpp <= 0 || off < 0) return -22;
   if (M > TF_MAXM || P < 1 || rpp < 1 || K < 1 || C < 1) return -1;
   dim3 grid(P, (rpp + TM_T - 1) / TM_T, (K + TM_T - 1) / TM_T);
   typed_fc_dgrad_mfma_kernel<<<grid, 256, 0, stream>>>(dy, K, flat, off, chunk, C, M, mask, types, rpp,
@@ -488,6 +493,7 @@ int launch_typed_fc_dgrad_mfma(const float* dy, int K, const float* flat, long o
 int launch_typed_fc_wgrad_mfma(const float* x, const float* dy, int K, long off, long chunk, int C, int M, int P,
                                const float* mask, const int* types, int rpp, const void* relu, float* gflat,
                                hipStream_t stream) {
+  if (K <= 0 || chunk <= 0 || C <= 0 || M <= 0 || P <= 0 || rpp <= 0 || off < 0) return -22;
   if (M > TF_MAXM || P < 1 || rpp < 1 || K < 1 || C < 1) return -1;
   dim3 grid(M, (K + TM_T - 1) / TM_T, (C + TM_T - 1) / TM_T);
   typed_fc_wgrad_mfma_kernel<<<grid, 256, 0, stream>>>(x, dy, K, off, chunk, C, M, P, mask, types, rpp,
