@@ -56,6 +56,19 @@ DEVI long rowit_sample(const RowIt& it, int p, int E, int PE, int t0) {
   return (long)(t0 + it.t) * PE + (long)p * E + it.e;
 }
 
+// The ReLU-bit word of a lane: byte r = byte k of row r's 64-lane ballot.  One v_perm_b32 per row on the SGPR
+// ballot pair, its selector (byte k into byte r, 0x0C -> 0x00 elsewhere) one v_lshl_or_b32 -- instead of a
+// 64-bit shift, mask, shift and or per row.  Selectors are formed at use: holding them cost the bf16 conv layers
+// (128-VGPR budget at 4 waves/SIMD) 40 spilled VGPRs.
+DEVI uint32_t relu_bits_word(const uint64_t (&bal)[4], uint32_t k) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    w |= __builtin_amdgcn_perm((uint32_t)(bal[r] >> 32), (uint32_t)bal[r],
+                               (k << (8 * r)) | (0x0C0C0C0Cu & ~(0xFFu << (8 * r))));
+  return w;
+}
+
 template <bool U8IN>
 DEVI s8v ld8(const void* X, long off) {
   s8v r;
@@ -109,6 +122,12 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
     const int PE = P * E;
     const int w = tid >> 6, l = tid & 63;
     const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
+    // ReLU-bit byte of this lane's (row quad q, slot half h) in each row's 64-lane ballot: byte 2q + h
+    const uint32_t bkey = (uint32_t)(2 * q + h);
+    // one step per launch (the rollout, trunk()): global row = rowbase + path-local row, no iterator needed
+    // (uint8 affine path only: in the bf16 layers' 128-VGPR budget the extra live values spilled)
+    const bool lin = T == 1;
+    const long rowbase = ((long)t0 * PE + (long)p * E) * G::HOWO;
     // lane rows: A-operand rows (rbase + 16i + c16) and epilogue rows (rbase + 16i + 4q + r)
     constexpr int FF_ROWS = NT * 128;
     const int rfirst = blockIdx.x * FF_ROWS + w * 32;
@@ -294,28 +313,31 @@ __global__ __launch_bounds__(256, G::U8 ? 3 : 4) void conv_fwd_fast(const void* 
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int r16 = rbase + i * 16;
-          const RowIt e0 = eit[i];
-          rowit_adv(eit[i], 128, E, G::HOWO);
+          long grow4;
+          if (lin) {
+            grow4 = rowbase + r16 + 4 * q;
+          } else {
+            const RowIt e0 = eit[i];
+            rowit_adv(eit[i], 128, E, G::HOWO);
+            grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
+          }
           if (r16 >= Rtot) continue;
           float sum[4] = {0.f, 0.f, 0.f, 0.f};
-          const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
 #pragma unroll
           for (int ct = 0; ct < NC; ++ct) {
-            {
-              const int slot = ct * 2 + h;
-              const bool sv = slot < cnt;
-              const float bb = bias_s[ct * 16 + c16];
-              uint32_t word = 0;
+            // slots >= cnt have zero weights and bias (staged that way), so v == 0 and they never fire
+            const int slot = ct * 2 + h;
+            const float bb = bias_s[ct * 16 + c16];
+            uint64_t bal[4];
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float v = acc[i][ct][r] * in_scale + bb;
-                const bool pos = sv && v > 0.f;
-                sum[r] += pos ? v : 0.f;
-                const uint64_t bal = __ballot(pos);
-                word |= (uint32_t)((bal >> (16 * q + 8 * h)) & 0xFFull) << (8 * r);
-              }
-              if (ch == 0 && sv) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[i][ct][r] * in_scale + bb;
+              const bool pos = v > 0.f;
+              sum[r] += pos ? v : 0.f;
+              bal[r] = __ballot(pos);
             }
+            const uint32_t word = relu_bits_word(bal, bkey);
+            if (ch == 0 && slot < cnt) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);

@@ -93,6 +93,35 @@ def test_conv1_fp16_offset_forward_is_tight(hip_lib):
     assert rel(Y.float(), ref) < 4e-3, rel(Y.float(), ref)
 
 
+def test_conv_forward_multi_step_launch_matches_per_step(hip_lib):
+    """A T=2 forward launch (row iterators across the step boundary) writes exactly what two T=1 launches write
+    (the one-step fast path computes global rows linearly, csrc/conv_fast.hip conv_fwd_fast `lin`)."""
+    cfg = small_pixel_cfg()
+    P, E, T = 4, 16, 2
+    masks = random_masks(P, cfg.L, cfg.M, cfg.N, seed=5)
+    m = make_model(cfg, P, masks, seed=4)
+    hp = m.hip
+    B = P * E
+    g = torch.Generator().manual_seed(8)
+    x = torch.randint(0, 256, (T, B, 160 * 120 * 4), generator=g, dtype=torch.uint8).to(DEV)
+    for l in range(3):                         # conv1 (uint8, affine path), conv2, conv3 (bf16 inputs)
+        gl = hp.geoms[l]
+        outs = []
+        for mode in ("multi", "single"):
+            Y = torch.zeros(T + 1, B, gl.out_feat, dtype=torch.bfloat16, device=DEV)
+            bits, rows = hp.alloc_bits(l, T + 1, B)
+            if mode == "multi":
+                hp.layer_fwd(l, x, Y, bits, P, E, T, 0, rows)
+            else:
+                for t in range(T):
+                    hp.layer_fwd(l, x, Y, bits, P, E, 1, t, rows)
+            torch.cuda.synchronize()
+            outs.append((Y, bits))
+        assert torch.equal(outs[0][0], outs[1][0]), l
+        assert torch.equal(outs[0][1], outs[1][1]), l
+        x = outs[0][0]
+
+
 def test_fc_trunk_forward_vector_input(hip_lib):
     cfg = preset("cartpole").net
     P, E = 6, 16
