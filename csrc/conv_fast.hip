@@ -1211,28 +1211,54 @@ __global__ __launch_bounds__(256, 3) void conv_wgrad_slab(const void* __restrict
     };
     __syncthreads();
     if constexpr (PF == 1) {
+      // the last stage is peeled so the reload in the loop body is unconditional: a conditional reload is a
+      // loop-carried phi and the compiler copied the whole register set (~140 v_mov per stage) to merge it
       if (u_beg < u_end) load_stage(R[0], u_beg);
-      int buf = 0;
-      for (int u = u_beg; u < u_end; ++u, buf ^= 1) {
+      int u = u_beg, buf = 0;
+      for (; u + 1 < u_end; ++u, buf ^= 1) {
         write_stage(R[0], buf);
         __syncthreads();
-        if (u + 1 < u_end) load_stage(R[0], u + 1);
+        load_stage(R[0], u + 1);
+        compute_stage(buf);
+      }
+      if (u < u_end) {
+        write_stage(R[0], buf);
+        __syncthreads();
         compute_stage(buf);
       }
     } else {
-      // stage u lives in register set (u - u_beg) & 1 and LDS buffer (u - u_beg) & 1
+      // stage u lives in register set (u - u_beg) & 1 and LDS buffer (u - u_beg) & 1.  The main loop reloads
+      // unconditionally (a conditional reload is a loop-carried phi: the compiler copied both register sets
+      // every stage); the last 0-3 stages run in the straight-line tail.
       if (u_beg < u_end) load_stage(R[0], u_beg);
       if (u_beg + 1 < u_end) load_stage(R[1], u_beg + 1);
-      for (int u = u_beg; u < u_end; u += 2) {
+      int u = u_beg;
+      for (; u + 3 < u_end; u += 2) {
         write_stage(R[0], 0);
         __syncthreads();
-        if (u + 2 < u_end) load_stage(R[0], u + 2);
+        load_stage(R[0], u + 2);
         compute_stage(0);
-        if (u + 1 >= u_end) break;
         write_stage(R[1], 1);
         __syncthreads();
-        if (u + 3 < u_end) load_stage(R[1], u + 3);
+        load_stage(R[1], u + 3);
         compute_stage(1);
+      }
+      const int rem = u_end - u;
+      if (rem >= 1) {
+        write_stage(R[0], 0);
+        __syncthreads();
+        if (rem >= 3) load_stage(R[0], u + 2);
+        compute_stage(0);
+      }
+      if (rem >= 2) {
+        write_stage(R[1], 1);
+        __syncthreads();
+        compute_stage(1);
+      }
+      if (rem >= 3) {
+        write_stage(R[0], 0);
+        __syncthreads();
+        compute_stage(0);
       }
     }
     const int h = i16 >> 3, ch = l & 7;
