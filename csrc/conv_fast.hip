@@ -1210,7 +1210,8 @@ __global__ __launch_bounds__(256, 3) void conv_wgrad_slab(const void* __restrict
       }
     };
     __syncthreads();
-    if constexpr (PF == 1) {
+    // PF=2 only for <= 4 active modules (NC <= 2): with the NC=5 accumulators two register sets spilled
+    if constexpr (PF == 1 || NC > 2) {
       // the last stage is peeled so the reload in the loop body is unconditional: a conditional reload is a
       // loop-carried phi and the compiler copied the whole register set (~140 v_mov per stage) to merge it
       if (u_beg < u_end) load_stage(R[0], u_beg);
@@ -1634,7 +1635,7 @@ static int FWD_NT = 4;         // 32-row tiles per wave in conv_fwd_fast (4 -> 5
 // uint8 first layer: fp16-offset MFMA operands (1 v_perm per 2 pixels) instead of u8 -> f32 -> bf16 converts.
 // Off only for A/B runs and for the exact-equality tests against the bf16 alternative kernels.
 static int F16_FWD = 1;
-static int WGRAD_PF = 1;       // register sets of slab-wgrad loads in flight (1 or 2)
+static int WGRAD_PF = 2;       // register sets of slab-wgrad loads in flight (1 or 2; 2: 1617 -> 1464 us conv1)
 
 template <class G, int NT, bool RING = false>
 static void fwd_launch(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off,

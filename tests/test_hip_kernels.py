@@ -811,7 +811,7 @@ def test_slab_conv_kernels_match_fast(hip_lib, E):
 
 @pytest.mark.parametrize("nt,pf", [(2, 2), (8, 1), (16, 2)])
 def test_conv_pipeline_variants_match_default(hip_lib, nt, pf):
-    """conv_fwd_fast with 2/8/16 row tiles per wave and the 2-deep-prefetch slab wgrad == the default kernels."""
+    """conv_fwd_fast with 2/8/16 row tiles per wave and the 1- / 2-deep-prefetch slab wgrad == the default kernels."""
     from pathnet_gym_amd.ops import _lib
     cfg = small_pixel_cfg()
     P, T, E = 3, 3, 16
@@ -829,7 +829,7 @@ def test_conv_pipeline_variants_match_default(hip_lib, nt, pf):
         f1, g1 = _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E)
     finally:
         lib.fast_conv_set_fwd_nt(4)
-        lib.fast_conv_set_wgrad_pf(1)
+        lib.fast_conv_set_wgrad_pf(2)     # the default (csrc/conv_fast.hip WGRAD_PF)
     assert rel(f1, f0) < 1e-5
     for s in m.store.layout.segments:
         if s.layer < 0 or s.layer > 2:
