@@ -1421,7 +1421,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__
   __shared__ __attribute__((aligned(16))) bf16_t Gs[(G::HOWO + 1) * DG_PSTR];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[D::KSMAX * D::NT * 16 * 32];   // [ks][n][k (32), swizzled]
   __shared__ int mods[MAXM_F];
-  __shared__ int atab[D::NRT * 16];
+  constexpr int NTAPP = (D::NTAP + 3) & ~3;
+  __shared__ __attribute__((aligned(16))) uint16_t atap[D::NRT * 16 * NTAPP];
   __shared__ __attribute__((aligned(8))) uint16_t etab[D::NRT * 16];
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
@@ -1479,22 +1480,24 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__
   };
   // Sample-independent geometry, formed once per workgroup in two small LDS tables instead of once per sample
   // in registers (that per-sample index math was ~3/4 of this kernel's VALU work):
-  //   atab[sp]: A-operand superpixel sp -> position base ii*WO + jj, bit 16+tap set when the tap's output
-  //             position lies inside the image
+  //   atap[sp][tap]: LDS element offset of the A fragment of superpixel row sp and tap for k-chunk 0, with the
+  //             position's swizzle in bits 3-4 (position blocks are 96 elements, so those bits are free): the
+  //             lane's k-chunk grp is then one XOR (grp << 3).  Out-of-image taps point at the zero block HOWO.
   //   etab[sp]: epilogue superpixel sp -> dX offset S*(io*WIN + jo)*8, bit 14 / 15 set when class offset
   //             ph = 1 / pw = 1 stays inside the image; 0xFFFF past the last superpixel
   static_assert(S <= 2, "dgrad class limits are packed for strides 1 and 2");
+  static_assert((G::HOWO + 1) * DG_PSTR < (1 << 16) && DG_PSTR % 32 == 0, "atap offset / swizzle fields");
   static_assert((S * (D::NI - 1) * G::WIN + S * (D::NJ - 1)) * 8 < (1 << 14), "etab offset field");
   for (int sp = tid; sp < D::NRT * 16; sp += 256) {
     const int ii = sp / D::NJ, jj = sp - ii * D::NJ;
-    int m = 0;
 #pragma unroll
-    for (int tap = 0; tap < D::NTAP; ++tap) {
+    for (int tap = 0; tap < NTAPP; ++tap) {
       const int ta = tap / D::NA, tb = tap - ta * D::NA;
       const int oh = ii - ta, ow = jj - tb;
-      if (sp < D::NSP && oh >= 0 && oh < G::HO && ow >= 0 && ow < G::WO) m |= 1 << tap;
+      const bool ok = tap < D::NTAP && sp < D::NSP && oh >= 0 && oh < G::HO && ow >= 0 && ow < G::WO;
+      const int apos = ok ? oh * G::WO + ow : G::HOWO;
+      atap[sp * NTAPP + tap] = (uint16_t)(apos * DG_PSTR + (dg_swz(apos) << 3));
     }
-    atab[sp] = (ii * G::WO + jj) | (m << 16);
     etab[sp] = sp < D::NSP ? (uint16_t)((S * ii * G::WIN + S * jj) * 8 | ((S * ii + 1 < G::HIN) << 14) |
                                         ((S * jj + 1 < G::WIN) << 15))
                            : (uint16_t)0xFFFF;
@@ -1570,21 +1573,15 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_mfma(const GT* __restrict__
     const long sg = sample_global(p, s, E, PE, 0);
     OT* __restrict__ dXs = dX + sg * (long)(G::HIN * G::WIN * 8);
     for (int rt = w; rt < D::NRT; rt += 4) {
-      const int av = atab[rt * 16 + c16];
-      const int ab = av & 0xFFFF, amask = av >> 16;
+      const uint16_t* tp = atap + (rt * 16 + c16) * NTAPP;
       f4v acc[D::NT];
 #pragma unroll
       for (int nt = 0; nt < D::NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
-      // k = (tap, slot group): the tap loop is compile-time (no per-step divisions by the
-      // runtime slot count -- they made this kernel SALU-bound), the A address is formed once
-      // per tap and out-of-image taps read position 0 and are zeroed by a select
+      // k = (tap, slot group): the tap loop is compile-time (no per-step divisions by the runtime slot count --
+      // they made this kernel SALU-bound); the A address of a tap is one table entry XOR the lane's k-chunk
 #pragma unroll
       for (int tap = 0; tap < D::NTAP; ++tap) {
-        const int ta = tap / D::NA, tb = tap - ta * D::NA;
-        const bool ok = (amask >> tap) & 1;
-        // out-of-image taps read the zeroed position block HOWO (one select per tap, none per fragment)
-        const int apos = ok ? ab - (ta * G::WO + tb) : G::HOWO;
-        const bf16_t* ap = Gs + apos * DG_PSTR + (grp ^ dg_swz(apos)) * 8;
+        const bf16_t* ap = Gs + ((int)tp[tap] ^ (grp << 3));
         const bf16_t* bp = Bs + (tap * ns4 * D::NT * 16 + c16) * 32 + (grp ^ dg_swz(c16)) * 8;
         for (int a4 = 0; a4 < ns4; ++a4) {
           const s8v af = *reinterpret_cast<const s8v*>(ap + a4 * 32);
