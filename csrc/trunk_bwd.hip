@@ -405,7 +405,10 @@ __global__ __launch_bounds__(512) void fc_dgrad_lds_kernel(
     }
     const int n_it = (ch_end - ch_beg) * ng;
     const int* aidx = act_idx + (p * L + layer) * M + g0;
-    s8v bcur[COUT / 32], bnxt[COUT / 32];
+    // two weight-fragment register sets used alternately (no bcur = bnxt copy), and the in-loop prefetch is
+    // unconditional (the last 1-2 iterations are peeled): a conditional prefetch is a loop-carried phi that
+    // made the compiler copy register sets every iteration
+    s8v b0[COUT / 32], b1[COUT / 32];
     auto wload = [&](s8v* b, int it) {
       const int ch = ch_beg + it / ng, a = it - (it / ng) * ng;
       const int kc = ch * 128 + w * 16 + c16;
@@ -414,11 +417,9 @@ __global__ __launch_bounds__(512) void fc_dgrad_lds_kernel(
       for (int c = 0; c < COUT / 32; ++c)
         b[c] = kc < KP ? *reinterpret_cast<const s8v*>(Wm + 32 * c) : (s8v){0, 0, 0, 0, 0, 0, 0, 0};
     };
-    wload(bcur, 0);
     f4v acc[4];
-    for (int it = 0; it < n_it; ++it) {
+    auto body = [&](const s8v* bc, int it) {
       const int ch = ch_beg + it / ng, a = it - (it / ng) * ng;
-      if (it + 1 < n_it) wload(bnxt, it + 1);
       if (a == 0) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) acc[rb] = {0.f, 0.f, 0.f, 0.f};
@@ -429,10 +430,8 @@ __global__ __launch_bounds__(512) void fc_dgrad_lds_kernel(
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
           const s8v af = *reinterpret_cast<const s8v*>(As + rb * 16 * CS + 32 * c);
-          acc[rb] = mfma16(af, bcur[c], acc[rb]);
+          acc[rb] = mfma16(af, bc[c], acc[rb]);
         }
-#pragma unroll
-      for (int c = 0; c < COUT / 32; ++c) bcur[c] = bnxt[c];
       const int kcol = ch * 128 + w * 16 + c16;
       if (a == ng - 1 && kcol < K) {
 #pragma unroll
@@ -446,6 +445,21 @@ __global__ __launch_bounds__(512) void fc_dgrad_lds_kernel(
             }
           }
       }
+    };
+    wload(b0, 0);
+    int it = 0;
+    for (; it + 2 < n_it; it += 2) {
+      wload(b1, it + 1);
+      body(b0, it);
+      wload(b0, it + 2);
+      body(b1, it + 1);
+    }
+    if (it + 1 < n_it) {
+      wload(b1, it + 1);
+      body(b0, it);
+      body(b1, it + 1);
+    } else {
+      body(b0, it);
     }
   }
 }
