@@ -1628,7 +1628,9 @@ static int dgrad_mfma_t(const GT* Gr, const void* bits, const float* flat, long 
 }
 
 // ---------------------------------------------------------------------------
-static int FWD_NT = 4;         // 32-row tiles per wave in conv_fwd_fast (4 -> 512 rows per workgroup)
+static int FWD_NT = 4;         // 32-row tiles per wave in conv_fwd_fast (4 -> 512 rows per workgroup); the uint8
+                               // first layer uses twice as many (capped at 16): conv1 85.3 -> 82.6 us per step at 8,
+                               // while conv2 / conv3 lose at 8 (18.0 -> 22.6, 14.8 -> 20.7 us: too few workgroups)
 // uint8 first layer: fp16-offset MFMA operands (1 v_perm per 2 pixels) instead of u8 -> f32 -> bf16 converts.
 // Off only for A/B runs and for the exact-equality tests against the bf16 alternative kernels.
 static int F16_FWD = 1;
@@ -1658,13 +1660,14 @@ template <class G>
 static int fwd_t(const void* X, void* Y, void* bits, const void* Wc, const float* flat, long bias_off, int chunk,
                  const int* ai, const int* ac, int layer, int L, int M, int P, int E, int T, int t0, long br,
                  float is, float os, hipStream_t st, const float* hcorr = nullptr) {
-  if (FWD_NT >= 16)
+  const int nt = G::U8 ? (FWD_NT >= 8 ? 16 : 2 * FWD_NT) : FWD_NT;
+  if (nt >= 16)
     fwd_launch<G, 16>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st,
                       nullptr, 0, hcorr);
-  else if (FWD_NT >= 8)
+  else if (nt >= 8)
     fwd_launch<G, 8>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st,
                      nullptr, 0, hcorr);
-  else if (FWD_NT >= 4)
+  else if (nt >= 4)
     fwd_launch<G, 4>(X, Y, bits, Wc, flat, bias_off, chunk, ai, ac, layer, L, M, P, E, T, t0, br, is, os, st,
                      nullptr, 0, hcorr);
   else
