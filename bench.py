@@ -92,7 +92,7 @@ def main():
     ap.add_argument("--env", default=None, help="train this task of the preset's suite instead of its first task")
     ap.add_argument("--kernel-opt", action="append", default=[],
                     help="kernel switch NAME=VALUE (fast_conv_set_*), for A/B measurements")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x"],
                     help="HIP engine compute dtype (fp32: the reference's precision, csrc/trunk_f32.hip)")
     ap.add_argument("--deterministic", action="store_true", help="fixed-order gradient reductions (bit-reproducible)")
     ap.add_argument("--rollout-groups", type=int, default=0,
@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--concurrent", type=int, default=None,
                     help="concurrent tournaments (default paths/16 -- per rank count, NOT scaled by the world size, so "
                          "the GA takes the same number of tournaments per update on 1, 2, 4 and 8 GPUs)")
+    ap.add_argument("--prof-window", action="store_true",
+                    help="launch marker kernels around the timed updates (scripts/prof_window.py summarises the "
+                         "rocprofv3 kernel trace between them)")
     args = ap.parse_args()
 
     import numpy as np
@@ -153,10 +156,15 @@ def main():
     sync()
     gen0 = tr.pop.generation
     step0 = tr.global_step
+    if args.prof_window:
+        from pathnet_gym_amd.ops import _lib as _plib
+        _plib.call("launch_prof_marker", 1, _plib.stream())
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.update()
     tr.flush()                               # drain the pipelined host bookkeeping of the last update
+    if args.prof_window:
+        _plib.call("launch_prof_marker", 2, _plib.stream())
     sync()
     dt = time.perf_counter() - t0
     dt = ctx.max_scalar(dt)

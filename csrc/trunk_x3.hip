@@ -1,0 +1,1860 @@
+// PathNet trunk in the fp32-accurate split-bf16 mode (TrainConfig.compute_dtype = "fp32x").
+//
+// The reference computes in fp32 (TF default dtype, game_ac_network.py:89-110).  gfx950 has no xf32 MFMA and its
+// fp32-input MFMA runs at 1/16 of the bf16 rate, so this mode keeps every value the bf16 engine keeps in bf16 as a
+// PAIR of bf16 values: x = hi + lo, hi = bf16(x), lo = bf16(x - hi), which represents x to 2^-17 relative.  A product
+// is then three bf16 MFMAs into one fp32 accumulator,
+//     a*b ~ a_hi*b_hi + a_hi*b_lo + a_lo*b_hi          (the dropped a_lo*b_lo term is <= 2^-16 |a*b|)
+// so each MFMA k-step costs 3x the bf16 engine's, against 16x for v_mfma_f32_16x16x4_f32 (csrc/trunk_f32.hip).
+// Inputs that are exact in 16 bits need two: the uint8 frame stack (exact in fp16) against the fp16 hi/lo pair of
+// the first layer's weights (scaled by 2^X3_W0_SHIFT so the lo half stays out of the fp16 subnormal range), and the
+// same uint8 stack (exact in bf16) against the hi/lo output gradient in that layer's weight gradient.
+//
+// Storage (pathnet_gym_amd/ops/pathnet_ops.py allocates it):
+//   activations between layers : two bf16 planes [hi | lo] of the bf16 engine's layout; kernels take the hi base
+//                                and the element offset of the lo plane (xlo / ylo).  The last layer writes fp32
+//                                (its only consumers are the fp32 heads kernels).
+//   activation gradients       : fp32 (masked and split into hi/lo while staging into LDS).
+//   weight operand copies      : [2][M][Cout][KP] (hi plane, lo plane), WcT likewise; conv1 [2][M][8][KP] fp16.
+// Kernel structure follows the bf16 engine (conv_fast.hip, trunk_fwd.hip, trunk_bwd.hip): the same row tilings,
+// LDS layouts and epilogues (bias + ReLU + ReLU bits + module sum), with the B operand and the masked-G staging
+// doubled.  LDS holds X3_NCX column tiles (6 modules) per pass; a path with more active modules in a layer runs
+// further passes over the same rows (forward: the epilogue adds into the output; weight gradients: separate
+// accumulation passes; conv dgrad: 4 slots per pass), so occupancy is sized for the common N = 4 genotypes.
+#include "common.h"
+#include <type_traits>
+
+namespace x3 {
+
+#define X3_NCX 3          // column tiles (16 = 2 modules x 8 maps) of B / masked G in LDS per pass
+#define X3_MAXM 16
+#define X3_NCT 5          // column tiles of a full layer (M <= 10)
+#define X3_W0_SHIFT 8     // first-layer weights enter the fp16 MFMA as W * 2^8 (hi/lo pair)
+
+template <int HIN_, int WIN_, int CIN_, int KH_, int KW_, int S_, bool U8_>
+struct CG {
+  static constexpr int HIN = HIN_, WIN = WIN_, CIN = CIN_, KH = KH_, KW = KW_, S = S_;
+  static constexpr bool U8 = U8_;
+  static constexpr int HO = (HIN - KH) / S + 1, WO = (WIN - KW) / S + 1, HOWO = HO * WO;
+  static constexpr int K = KH * KW * CIN, KP = (K + 31) / 32 * 32, KC = KP / 8;
+  static constexpr int IN_ELEMS = HIN * WIN * CIN;
+  static constexpr __host__ __device__ int koff(int kc) {
+    return kc * 8 >= K ? -1
+                       : ((kc * 8 / CIN) / KW * WIN + (kc * 8 / CIN) % KW) * CIN + (kc * 8) % CIN;
+  }
+};
+using C1 = CG<160, 120, 4, 8, 8, 4, true>;
+using C2 = CG<39, 29, 8, 4, 4, 2, false>;
+using C3 = CG<18, 13, 8, 3, 3, 1, false>;
+
+struct RowIt {
+  int r, t, e, pos;
+};
+DEVI void rowit_init(RowIt& it, int r, int E, int howo) {
+  it.r = r;
+  const int s = r / howo;
+  it.pos = r - s * howo;
+  it.t = s / E;
+  it.e = s - it.t * E;
+}
+DEVI void rowit_adv(RowIt& it, int n, int E, int howo) {
+  it.r += n;
+  it.pos += n;
+  while (it.pos >= howo) {
+    it.pos -= howo;
+    if (++it.e == E) { it.e = 0; ++it.t; }
+  }
+}
+DEVI long rowit_sample(const RowIt& it, int p, int E, int PE, int t0) {
+  return (long)(t0 + it.t) * PE + (long)p * E + it.e;
+}
+
+DEVI uint32_t relu_bits_word(const uint64_t (&bal)[4], uint32_t k) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    w |= __builtin_amdgcn_perm((uint32_t)(bal[r] >> 32), (uint32_t)bal[r],
+                               (k << (8 * r)) | (0x0C0C0C0Cu & ~(0xFFu << (8 * r))));
+  return w;
+}
+
+// ---- split-bf16 helpers ----
+DEVI void split8(const float (&v)[8], s8v& hi, s8v& lo) {
+  __bf16 h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = (__bf16)v[j];
+    l[j] = (__bf16)(v[j] - (float)h[j]);
+  }
+  __builtin_memcpy(&hi, h, 16);
+  __builtin_memcpy(&lo, l, 16);
+}
+// hi/lo pair of one value into two planes
+DEVI void st_x2(bf16_t* Y, long ylo, long i, float v) {
+  const bf16_t h = f2bf(v);
+  Y[i] = h;
+  Y[i + ylo] = f2bf(v - bf2f(h));
+}
+DEVI float ld_x2(const bf16_t* Y, long ylo, long i) { return bf2f(Y[i]) + bf2f(Y[i + ylo]); }
+// a*b over one 32-wide k-step from hi/lo operands: the two small cross terms first
+DEVI f4v mma3(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
+  c = mfma16(al, bh, c);
+  c = mfma16(ah, bl, c);
+  return mfma16(ah, bh, c);
+}
+// exact operand a (uint8 pixels in bf16) against a hi/lo pair b
+DEVI f4v mma2(const s8v& a, const s8v& bh, const s8v& bl, f4v c) {
+  c = mfma16(a, bl, c);
+  return mfma16(a, bh, c);
+}
+// 8 x uint8 -> 8 x fp16 holding the exact pixel value: fp16(1024 + v) built by v_perm, minus 1024 (exact)
+DEVI s8v u8x8_to_f16(uint2 v) {
+  h8v x = __builtin_bit_cast(h8v, u8x8_to_f16off(v));
+  x = x - (h8v){(_Float16)1024.f, (_Float16)1024.f, (_Float16)1024.f, (_Float16)1024.f,
+                (_Float16)1024.f, (_Float16)1024.f, (_Float16)1024.f, (_Float16)1024.f};
+  return __builtin_bit_cast(s8v, x);
+}
+
+// ===========================================================================
+// first layer forward (uint8 frame stack, 8x8/s4, 160x120x4): fp16 MFMA, exact pixels x (W*2^8) hi/lo pair.
+// grid = (ceil(T*E*HOWO / (NT*128)), P), 256 threads; each wave owns 32-row tiles (2 MFMA row tiles) and walks
+// NT of them with the bf16 engine's one-register-set reload pipeline (conv_fast.hip conv_fwd_fast AFF8 path):
+// a k-step's raw bytes are converted, the same registers are reloaded with the next tile's k-step, then the MFMAs.
+// Wh: [2][M][8][KP] fp16 (hi plane, lo plane at +wlo).  Y: two bf16 planes (lo at +ylo).
+// ===========================================================================
+template <class G, int NT>
+__global__ __launch_bounds__(256, 2) void conv1_fwd_x2(const uint8_t* __restrict__ X, bf16_t* __restrict__ Y,
+                                                      long ylo, uint8_t* __restrict__ bits,
+                                                      const uint16_t* __restrict__ Wh, long wlo,
+                                                      const float* __restrict__ flat, long bias_off, int chunk,
+                                                      const int* __restrict__ act_idx,
+                                                      const int* __restrict__ act_cnt, int layer, int L, int M, int P,
+                                                      int E, int T, int t0, long bits_rows, float in_scale,
+                                                      float out_scale) {
+  static_assert(G::U8 && G::KW * G::CIN == 32 && G::K == G::KP, "affine uint8 first-layer geometry");
+  constexpr int KPs = G::KP + 8;
+  constexpr int NK = G::KP / 32;
+  constexpr int FF_ROWS = NT * 128;
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[2][X3_NCX * 16 * KPs];
+  __shared__ float bias_s[X3_NCX * 16];
+  __shared__ int mods[X3_MAXM];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  const int Rtot = T * E * G::HOWO;
+  const int PE = P * E;
+  const int w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
+  const uint32_t bkey = (uint32_t)(2 * q + h);
+  const bool lin = T == 1;
+  const long rowbase = ((long)t0 * PE + (long)p * E) * G::HOWO;
+  const int rfirst = blockIdx.x * FF_ROWS + w * 32;
+  const int npass = nct > X3_NCX ? (nct + X3_NCX - 1) / X3_NCX : 1;
+  RowIt ait[2], eit[2];
+  uint2 araw[2][NK];
+  const uint8_t* asrc[2];
+  // rows past the end read row 0 of the path's first sample: their 16-row halves are never stored
+  auto aff_addr = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool va = ait[i].r < Rtot;
+      const int oh = ait[i].pos / G::WO, ow = ait[i].pos - oh * G::WO;
+      const long xb = va ? rowit_sample(ait[i], p, E, PE, t0) * (long)G::IN_ELEMS +
+                               (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN
+                         : rowit_sample(RowIt{0, 0, 0, 0}, p, E, PE, t0) * (long)G::IN_ELEMS;
+      asrc[i] = X + xb + G::koff(grp);
+      rowit_adv(ait[i], 128, E, G::HOWO);
+    }
+  };
+  for (int pass = 0; pass < npass; ++pass) {
+    const int ct0 = pass * X3_NCX;
+    const int ncg = nct == 0 ? 1 : min(X3_NCX, nct - ct0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      rowit_init(ait[i], rfirst + i * 16 + c16, E, G::HOWO);
+      rowit_init(eit[i], rfirst + i * 16 + 4 * q, E, G::HOWO);
+    }
+    // the first tile's A loads do not depend on LDS: issued before the staging barriers
+    aff_addr();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) araw[i][kk] = *reinterpret_cast<const uint2*>(asrc[i] + kk * G::WIN * G::CIN);
+    __syncthreads();       // mods visible / the previous pass's LDS reads done
+    for (int i = tid; i < ncg * 16 * G::KC; i += 256) {
+      const int col = i / G::KC, kc = i - col * G::KC;
+      const int slot = ct0 * 2 + (col >> 3);
+      s8v vh = {0, 0, 0, 0, 0, 0, 0, 0}, vl = vh;
+      if (slot < cnt) {
+        const long o = ((long)(mods[slot] * 8 + (col & 7))) * G::KP + kc * 8;
+        vh = *reinterpret_cast<const s8v*>(Wh + o);
+        vl = *reinterpret_cast<const s8v*>(Wh + wlo + o);
+      }
+      *reinterpret_cast<s8v*>(Ws[0] + col * KPs + kc * 8) = vh;
+      *reinterpret_cast<s8v*>(Ws[1] + col * KPs + kc * 8) = vl;
+    }
+    if (tid < ncg * 16) {
+      const int slot = ct0 * 2 + (tid >> 3);
+      bias_s[tid] = slot < cnt ? flat[bias_off + (long)mods[slot] * chunk + (tid & 7)] : 0.f;
+    }
+    __syncthreads();
+    auto run = [&](auto ncc) {
+      constexpr int NC = decltype(ncc)::value;
+      auto do_tile = [&](const int rbase, auto reload_c) {
+        constexpr bool RELOAD = decltype(reload_c)::value;
+        f4v acc[2][NC];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (RELOAD) aff_addr();
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const s8v a0 = u8x8_to_f16(araw[0][kk]);
+          const s8v a1 = u8x8_to_f16(araw[1][kk]);
+          if constexpr (RELOAD) {
+            araw[0][kk] = *reinterpret_cast<const uint2*>(asrc[0] + kk * G::WIN * G::CIN);
+            araw[1][kk] = *reinterpret_cast<const uint2*>(asrc[1] + kk * G::WIN * G::CIN);
+          }
+          const int kc = kk * 4 + grp;
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) {
+            const s8v bh = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
+            const s8v bl = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
+            acc[0][ct] = mfma16_f16(a0, bl, acc[0][ct]);
+            acc[0][ct] = mfma16_f16(a0, bh, acc[0][ct]);
+            acc[1][ct] = mfma16_f16(a1, bl, acc[1][ct]);
+            acc[1][ct] = mfma16_f16(a1, bh, acc[1][ct]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r16 = rbase + i * 16;
+          long grow4;
+          if (lin) {
+            grow4 = rowbase + r16 + 4 * q;
+          } else {
+            const RowIt e0 = eit[i];
+            rowit_adv(eit[i], 128, E, G::HOWO);
+            grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
+          }
+          if (r16 >= Rtot) continue;
+          float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) {
+            const int slot = (ct0 + ct) * 2 + h;
+            const float bb = bias_s[ct * 16 + c16];
+            uint64_t bal[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[i][ct][r] * in_scale + bb;
+              const bool pos = v > 0.f;
+              sum[r] += pos ? v : 0.f;
+              bal[r] = __ballot(pos);
+            }
+            const uint32_t word = relu_bits_word(bal, bkey);
+            if (ch == 0 && slot < cnt) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
+          if (h == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const long o = (grow4 + r) * 8 + ch;
+              float y = sum[r] * out_scale;
+              if (pass > 0) y += ld_x2(Y, ylo, o);
+              st_x2(Y, ylo, o, y);
+            }
+          }
+        }
+      };
+      int tile = 0;
+#pragma unroll
+      for (; tile + 1 < NT; ++tile) {
+        const int rbase = rfirst + tile * 128;
+        if (rbase + 128 >= Rtot) break;
+        do_tile(rbase, std::true_type{});
+      }
+      const int rbase = rfirst + tile * 128;
+      if (rbase < Rtot) do_tile(rbase, std::false_type{});
+    };
+    switch (ncg) {
+      case 1: run(std::integral_constant<int, 1>{}); break;
+      case 2: run(std::integral_constant<int, 2>{}); break;
+      default: run(std::integral_constant<int, 3>{}); break;
+    }
+  }
+}
+
+// ===========================================================================
+// forward of the bf16-activation conv layers (39x29x8 4x4/s2, 18x13x8 3x3/s1): A hi/lo planes, B hi/lo in LDS,
+// three MFMAs per (row tile, column tile, k-step).  grid = (ceil(T*E*HOWO / (NT*128)), P).  The next 32-row
+// tile's A fragments (both planes) are loaded while this tile's MFMAs run.
+// ===========================================================================
+template <class G, int NT>
+__global__ __launch_bounds__(256, 2) void conv_fwd_x3(const bf16_t* __restrict__ X, long xlo, bf16_t* __restrict__ Y,
+                                                     long ylo, uint8_t* __restrict__ bits,
+                                                     const bf16_t* __restrict__ Wc, long wlo,
+                                                     const float* __restrict__ flat, long bias_off, int chunk,
+                                                     const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
+                                                     int layer, int L, int M, int P, int E, int T, int t0,
+                                                     long bits_rows, float out_scale) {
+  static_assert(!G::U8, "bf16-activation layers");
+  constexpr int KPs = G::KP + 8;
+  constexpr int NK = G::KP / 32;
+  constexpr int FF_ROWS = NT * 128;
+  __shared__ __attribute__((aligned(16))) bf16_t Ws[2][X3_NCX * 16 * KPs];
+  __shared__ float bias_s[X3_NCX * 16];
+  __shared__ int mods[X3_MAXM];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  const int Rtot = T * E * G::HOWO;
+  const int PE = P * E;
+  const int w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
+  const uint32_t bkey = (uint32_t)(2 * q + h);
+  const int rfirst = blockIdx.x * FF_ROWS + w * 32;
+  const int npass = nct > X3_NCX ? (nct + X3_NCX - 1) / X3_NCX : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+    const int ct0 = pass * X3_NCX;
+    const int ncg = nct == 0 ? 1 : min(X3_NCX, nct - ct0);
+    __syncthreads();
+    for (int i = tid; i < ncg * 16 * G::KC; i += 256) {
+      const int col = i / G::KC, kc = i - col * G::KC;
+      const int slot = ct0 * 2 + (col >> 3);
+      s8v vh = {0, 0, 0, 0, 0, 0, 0, 0}, vl = vh;
+      if (slot < cnt) {
+        const long o = ((long)(mods[slot] * 8 + (col & 7))) * G::KP + kc * 8;
+        vh = *reinterpret_cast<const s8v*>(Wc + o);
+        vl = *reinterpret_cast<const s8v*>(Wc + wlo + o);
+      }
+      *reinterpret_cast<s8v*>(Ws[0] + col * KPs + kc * 8) = vh;
+      *reinterpret_cast<s8v*>(Ws[1] + col * KPs + kc * 8) = vl;
+    }
+    if (tid < ncg * 16) {
+      const int slot = ct0 * 2 + (tid >> 3);
+      bias_s[tid] = slot < cnt ? flat[bias_off + (long)mods[slot] * chunk + (tid & 7)] : 0.f;
+    }
+    __syncthreads();
+    auto run = [&](auto ncc) {
+      constexpr int NC = decltype(ncc)::value;
+      RowIt ait[2], eit[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        rowit_init(ait[i], rfirst + i * 16 + c16, E, G::HOWO);
+        rowit_init(eit[i], rfirst + i * 16 + 4 * q, E, G::HOWO);
+      }
+      s8v ah[2][NK], al[2][NK];
+      auto load_tile = [&](int rbase) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bool va = rbase < Rtot && ait[i].r < Rtot;
+          const int oh = ait[i].pos / G::WO, ow = ait[i].pos - oh * G::WO;
+          const long xb = rowit_sample(ait[i], p, E, PE, t0) * (long)G::IN_ELEMS +
+                          (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN;
+          rowit_adv(ait[i], 128, E, G::HOWO);
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            const int off = G::koff(kk * 4 + grp);
+            ah[i][kk] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+            al[i][kk] = ah[i][kk];
+            if (va && off >= 0) {
+              ah[i][kk] = *reinterpret_cast<const s8v*>(X + xb + off);
+              al[i][kk] = *reinterpret_cast<const s8v*>(X + xlo + xb + off);
+            }
+          }
+        }
+      };
+      load_tile(rfirst);
+      for (int tile = 0; tile < NT; ++tile) {
+        const int rbase = rfirst + tile * 128;
+        if (rbase >= Rtot) break;
+        s8v ch_[2][NK], cl_[2][NK];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) { ch_[i][kk] = ah[i][kk]; cl_[i][kk] = al[i][kk]; }
+        if (tile + 1 < NT) load_tile(rbase + 128);
+        f4v acc[2][NC];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) acc[i][ct] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const int kc = kk * 4 + grp;
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) {
+            const s8v bh = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
+            const s8v bl = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
+            acc[0][ct] = mma3(ch_[0][kk], cl_[0][kk], bh, bl, acc[0][ct]);
+            acc[1][ct] = mma3(ch_[1][kk], cl_[1][kk], bh, bl, acc[1][ct]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r16 = rbase + i * 16;
+          const RowIt e0 = eit[i];
+          rowit_adv(eit[i], 128, E, G::HOWO);
+          if (r16 >= Rtot) continue;
+          const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
+          float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) {
+            const int slot = (ct0 + ct) * 2 + h;
+            const float bb = bias_s[ct * 16 + c16];
+            uint64_t bal[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[i][ct][r] + bb;
+              const bool pos = v > 0.f;
+              sum[r] += pos ? v : 0.f;
+              bal[r] = __ballot(pos);
+            }
+            const uint32_t word = relu_bits_word(bal, bkey);
+            if (ch == 0 && slot < cnt) *reinterpret_cast<uint32_t*>(bits + (long)slot * bits_rows + grow4) = word;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 8, 64);
+          if (h == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const long o = (grow4 + r) * 8 + ch;
+              float y = sum[r] * out_scale;
+              if (pass > 0) y += ld_x2(Y, ylo, o);
+              st_x2(Y, ylo, o, y);
+            }
+          }
+        }
+      }
+    };
+    switch (ncg) {
+      case 1: run(std::integral_constant<int, 1>{}); break;
+      case 2: run(std::integral_constant<int, 2>{}); break;
+      default: run(std::integral_constant<int, 3>{}); break;
+    }
+  }
+}
+
+// ===========================================================================
+// weight gradient, LDS-slab implicit im2col (KW*CIN == 32, S*CIN == 16: the 160x120x4 8x8/s4 and 39x29x8 4x4/s2
+// layers; conv_fast.hip conv_wgrad_slab describes the slab).  A stage is a band of OB output rows of one sample:
+// its input rows are copied once into LDS (uint8 -> bf16 exact, or the hi and lo planes), the MFMA A operand
+// (im2col^T) is read from the slab with ds_read_b64_tr_b16; the fp32 output gradient is masked by the ReLU bits and
+// split into hi/lo rows of Gs.  uint8 input: 2 MFMAs (X exact), bf16 input: 3.  Register prefetch of the next stage
+// + double-buffered LDS; passes of X3_NCX column tiles.  grid = (chunks, P).
+// ===========================================================================
+template <class G, int OB>
+struct Slab {
+  static constexpr int RL = G::WIN * G::CIN;
+  static constexpr int PS = G::S * G::CIN;
+  static constexpr int SEG = G::KW * G::CIN;
+  static constexpr int NB = (G::HO + OB - 1) / OB;
+  static constexpr int NPOS = OB * G::WO;
+  static constexpr int KS = (NPOS + 31) / 32;
+  static constexpr int SR = (OB - 1) * G::S + G::KH;
+  static constexpr int SLAB = SR * RL;
+  static constexpr int SLABP = SLAB + 64;
+  static constexpr int NG8 = SLAB / 8;
+  static constexpr int XIT = (NG8 + 255) / 256;
+  static_assert(SEG == 32 && PS == 16, "slab wgrad needs KW*CIN == 32 and S*CIN == 16");
+  static_assert(SLAB % 8 == 0, "slab must be a whole number of 8-element groups");
+};
+
+DEVI s8v tr8(const bf16_t* p0, const bf16_t* p1) {
+  const s4v v0 = lds_tr16(p0);
+  const s4v v1 = lds_tr16(p1);
+  return (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+}
+
+template <class G, int OB>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restrict__ X, long xlo,
+                                                            const float* __restrict__ Gr,
+                                                            const uint8_t* __restrict__ bits, float* __restrict__ grad,
+                                                            long w_off, long b_off, int chunk,
+                                                            const int* __restrict__ act_idx,
+                                                            const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                            int P, int E, int T, long bits_rows, int units_per_wg,
+                                                            float in_scale, float g_scale) {
+  using SB = Slab<G, OB>;
+  constexpr bool XL = !G::U8;                       // bf16 input: lo plane too
+  constexpr int NXP = XL ? 2 : 1;
+  constexpr int GS = X3_NCX * 16 + 8;
+  constexpr int NMT = G::KP / 16;
+  constexpr int MPW = NMT / 4;
+  constexpr int GROWS = SB::KS * 32;
+  constexpr int GIT = (GROWS * 4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][NXP][SB::SLABP];
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][2][GROWS * GS];
+  __shared__ float dbias[X3_NCT * 16];
+  __shared__ int mods[X3_MAXM];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  if (cnt == 0) return;
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  if (tid < X3_NCT * 16) dbias[tid] = 0.f;
+  for (int i = tid; i < 2 * NXP * 64; i += 256) Xs[i / (NXP * 64)][(i / 64) % NXP][SB::SLAB + (i & 63)] = 0;
+  const int PE = P * E;
+  const int nunits = T * E * SB::NB;
+  const int u_beg = blockIdx.x * units_per_wg;
+  const int u_end = min(nunits, u_beg + units_per_wg);
+  int aoff[SB::KS][2];
+#pragma unroll
+  for (int ks = 0; ks < SB::KS; ++ks)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      int rho = ks * 32 + 8 * grp + 4 * hf + q;
+      if (rho >= SB::NPOS) rho = 0;                     // padded position: its G row is zero
+      const int ob = rho / G::WO, ow = rho - ob * G::WO;
+      aoff[ks][hf] = ob * G::S * SB::RL + ow * SB::PS + 4 * pp;
+    }
+  const int npass = (nct + X3_NCX - 1) / X3_NCX;
+  using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
+  auto run = [&](auto ncc, const int ct0) {
+    constexpr int NC = decltype(ncc)::value;
+    float acc_b[2][8];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc_b[k][c] = 0.f;
+    f4v acc[MPW][NC];
+#pragma unroll
+    for (int a = 0; a < MPW; ++a)
+#pragma unroll
+      for (int b = 0; b < NC; ++b) acc[a][b] = {0.f, 0.f, 0.f, 0.f};
+    XRaw xr[SB::XIT];
+    s8v xl[XL ? SB::XIT : 1];
+    float4 g0r[GIT], g1r[GIT];
+    uint32_t gbr[GIT][2];
+    bool gvr[GIT];
+    int navail = 0;
+    int it_band, it_e, it_t;
+    {
+      const int s0 = u_beg / SB::NB;
+      it_band = u_beg - s0 * SB::NB;
+      it_t = s0 / E;
+      it_e = s0 - it_t * E;
+    }
+    auto load_stage = [&]() {
+      const int band = it_band, ut = it_t, ue = it_e;
+      const long sg = (long)ut * PE + (long)p * E + ue;
+      if (++it_band == SB::NB) {
+        it_band = 0;
+        if (++it_e == E) { it_e = 0; ++it_t; }
+      }
+      const int ih0 = band * OB * G::S;
+      navail = min(SB::SR, G::HIN - ih0) * SB::RL;
+      const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
+#pragma unroll
+      for (int j = 0; j < SB::XIT; ++j) {
+        const int gi = tid + 256 * j;
+        const int e0 = (gi < SB::NG8 && gi * 8 < navail) ? gi * 8 : 0;   // clamped, zeroed at write time
+        if constexpr (G::U8) {
+          xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xbase + e0);
+        } else {
+          xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xbase + e0);
+          xl[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xlo + xbase + e0);
+        }
+      }
+      const int oh0 = band * OB;
+#pragma unroll
+      for (int j = 0; j < GIT; ++j) {
+        const int it = tid + 256 * j;
+        const int rho = it >> 2, sub = it & 3;
+        const int ob = rho / G::WO, ow = rho - ob * G::WO;
+        gvr[j] = it < GROWS * 4 && rho < SB::NPOS && oh0 + ob < G::HO;
+        if (gvr[j]) {
+          const long go = sg * G::HOWO + (oh0 + ob) * G::WO + ow;
+          g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+          g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int slot = 2 * ct0 + sub + 4 * k;
+            gbr[j][k] = (sub + 4 * k < 2 * NC && slot < cnt) ? bits[(long)slot * bits_rows + go] : 0u;
+          }
+        }
+      }
+    };
+    auto write_stage = [&](int buf) {
+#pragma unroll
+      for (int j = 0; j < SB::XIT; ++j) {
+        const int gi = tid + 256 * j;
+        if (gi < SB::NG8) {
+          const bool ok = gi * 8 < navail;
+          s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
+          if constexpr (G::U8) {
+            if (ok) v = u8x8_to_bf16(xr[j]);
+          } else {
+            if (ok) v = xr[j];
+          }
+          *reinterpret_cast<s8v*>(&Xs[buf][0][gi * 8]) = v;
+          if constexpr (XL) {
+            s8v vl = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (ok) vl = xl[j];
+            *reinterpret_cast<s8v*>(&Xs[buf][XL ? 1 : 0][gi * 8]) = vl;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < GIT; ++j) {
+        const int it = tid + 256 * j;
+        if (it >= GROWS * 4) continue;
+        const int rho = it >> 2, sub = it & 3;
+        const float gg[8] = {g0r[j].x, g0r[j].y, g0r[j].z, g0r[j].w, g1r[j].x, g1r[j].y, g1r[j].z, g1r[j].w};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int rel = sub + 4 * k;
+          if (rel < 2 * NC) {
+            float m[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) m[c] = (gvr[j] && ((gbr[j][k] >> c) & 1u)) ? gg[c] : 0.f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc_b[k][c] += m[c];
+            s8v hi, lo;
+            split8(m, hi, lo);
+            *reinterpret_cast<s8v*>(&Gs[buf][0][rho * GS + rel * 8]) = hi;
+            *reinterpret_cast<s8v*>(&Gs[buf][1][rho * GS + rel * 8]) = lo;
+          }
+        }
+      }
+    };
+    auto compute_stage = [&](int buf) {
+      const bf16_t* xh = Xs[buf][0];
+      const bf16_t* xlp = Xs[buf][XL ? 1 : 0];
+#pragma unroll
+      for (int ks = 0; ks < SB::KS; ++ks) {
+        s8v bh[NC], bl[NC];
+#pragma unroll
+        for (int nt = 0; nt < NC; ++nt) {
+          const int o0 = (ks * 32 + 8 * grp + q) * GS + nt * 16 + 4 * pp;
+          const int o1 = (ks * 32 + 8 * grp + 4 + q) * GS + nt * 16 + 4 * pp;
+          bh[nt] = tr8(Gs[buf][0] + o0, Gs[buf][0] + o1);
+          bl[nt] = tr8(Gs[buf][1] + o0, Gs[buf][1] + o1);
+        }
+#pragma unroll
+        for (int mi = 0; mi < MPW; ++mi) {
+          const int mt = w * MPW + mi;
+          const int kb = (mt * 16 / SB::SEG) * SB::RL + (mt * 16) % SB::SEG;
+          const s8v ah = tr8(xh + kb + aoff[ks][0], xh + kb + aoff[ks][1]);
+          if constexpr (XL) {
+            const s8v al = tr8(xlp + kb + aoff[ks][0], xlp + kb + aoff[ks][1]);
+#pragma unroll
+            for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma3(ah, al, bh[nt], bl[nt], acc[mi][nt]);
+          } else {
+#pragma unroll
+            for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma2(ah, bh[nt], bl[nt], acc[mi][nt]);
+          }
+        }
+      }
+    };
+    __syncthreads();     // the previous pass's LDS reads are done (and the init above is visible)
+    if (u_beg < u_end) load_stage();
+    int u = u_beg, buf = 0;
+    for (; u + 1 < u_end; ++u, buf ^= 1) {
+      write_stage(buf);
+      __syncthreads();
+      load_stage();
+      compute_stage(buf);
+    }
+    if (u < u_end) {
+      write_stage(buf);
+      __syncthreads();
+      compute_stage(buf);
+    }
+    const int h = i16 >> 3, ch = l & 7;
+#pragma unroll
+    for (int mi = 0; mi < MPW; ++mi) {
+      const int mt = w * MPW + mi;
+#pragma unroll
+      for (int nt = 0; nt < NC; ++nt) {
+        const int slot = (ct0 + nt) * 2 + h;
+        if (slot < cnt) {
+          const long base = w_off + (long)mods[slot] * chunk;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = mt * 16 + 4 * grp + r;
+            if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int rel = (tid & 3) + 4 * k;
+      const int slot = 2 * ct0 + rel;
+      if (rel < 2 * NC && slot < cnt) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) atomicAdd(&dbias[slot * 8 + c], acc_b[k][c] * g_scale);
+      }
+    }
+  };
+  for (int pass = 0; pass < npass; ++pass) {
+    const int ct0 = pass * X3_NCX;
+    switch (min(X3_NCX, nct - ct0)) {
+      case 1: run(std::integral_constant<int, 1>{}, ct0); break;
+      case 2: run(std::integral_constant<int, 2>{}, ct0); break;
+      default: run(std::integral_constant<int, 3>{}, ct0); break;
+    }
+  }
+  __syncthreads();
+  if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
+}
+
+// ===========================================================================
+// weight gradient of the 18x13x8 3x3/s1 layer (KW*CIN = 24: no slab): 512 threads, 32-row stages of im2col rows
+// (hi and lo planes) + masked, split G in double-buffered LDS, one register set of next-stage loads in flight.
+// grid = (chunks, P) (conv_fast.hip conv_wgrad_fast is the bf16 form).
+// ===========================================================================
+#define X3_WG_RB 32
+template <class G>
+__global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict__ X, long xlo,
+                                                       const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
+                                                       float* __restrict__ grad, long w_off, long b_off, int chunk,
+                                                       const int* __restrict__ act_idx,
+                                                       const int* __restrict__ act_cnt, int layer, int L, int M, int P,
+                                                       int E, int T, long bits_rows, int rows_per_chunk,
+                                                       float in_scale, float g_scale) {
+  static_assert(!G::U8 && G::HOWO > X3_WG_RB, "bf16 input; one row wrap per stage");
+  constexpr int XS = G::KP + 8;
+  constexpr int GS = X3_NCX * 16 + 8;
+  constexpr int NMT = G::KP / 16;
+  constexpr int NW = 8;
+  constexpr int MPW = (NMT + NW - 1) / NW;
+  constexpr int XIT = (X3_WG_RB * G::KC + 511) / 512;
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][2][X3_WG_RB * XS];
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][2][X3_WG_RB * GS];
+  __shared__ float dbias[X3_NCT * 16];
+  __shared__ int mods[X3_MAXM];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  if (cnt == 0) return;
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  if (tid < X3_NCT * 16) dbias[tid] = 0.f;
+  const int Rtot = T * E * G::HOWO;
+  const int PE = P * E;
+  const int r_begin = blockIdx.x * rows_per_chunk;
+  const int r_end = min(Rtot, r_begin + rows_per_chunk);
+  const int w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
+  const int grow = tid >> 3, gsl = tid & 7;       // G staging role (threads < 256): row, slot of the pass
+  const int npass = (nct + X3_NCX - 1) / X3_NCX;
+  int xkoff[XIT];
+#pragma unroll
+  for (int j = 0; j < XIT; ++j) {
+    const int it = tid + 512 * j;
+    xkoff[j] = it < X3_WG_RB * G::KC ? G::koff(it % G::KC) : -1;
+  }
+  auto run = [&](auto ncc, const int ct0) {
+    constexpr int NC = decltype(ncc)::value;
+    const bool gact = tid < 256 && gsl < 2 * NC && 2 * ct0 + gsl < cnt;
+    float bpart[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    f4v acc[MPW][NC];
+#pragma unroll
+    for (int a = 0; a < MPW; ++a)
+#pragma unroll
+      for (int b = 0; b < NC; ++b) acc[a][b] = {0.f, 0.f, 0.f, 0.f};
+    RowIt xit[XIT], git;
+#pragma unroll
+    for (int j = 0; j < XIT; ++j) rowit_init(xit[j], r_begin + (tid + 512 * j) / G::KC, E, G::HOWO);
+    rowit_init(git, r_begin + grow, E, G::HOWO);
+    s8v xh[XIT], xlr[XIT];
+    bool xv[XIT];
+    float4 g0r, g1r;
+    uint32_t gbr = 0;
+    bool gv = false;
+    auto load_stage = [&]() {
+#pragma unroll
+      for (int j = 0; j < XIT; ++j) {
+        xv[j] = xkoff[j] >= 0 && xit[j].r < r_end;
+        if (xv[j]) {
+          const int oh = xit[j].pos / G::WO, ow = xit[j].pos - oh * G::WO;
+          const long xo = rowit_sample(xit[j], p, E, PE, 0) * (long)G::IN_ELEMS +
+                          (long)(oh * G::S * G::WIN + ow * G::S) * G::CIN + xkoff[j];
+          xh[j] = *reinterpret_cast<const s8v*>(X + xo);
+          xlr[j] = *reinterpret_cast<const s8v*>(X + xlo + xo);
+        }
+        rowit_adv(xit[j], X3_WG_RB, E, G::HOWO);
+      }
+      gv = gact && git.r < r_end;
+      if (gv) {
+        const long go = rowit_sample(git, p, E, PE, 0) * G::HOWO + git.pos;
+        g0r = *reinterpret_cast<const float4*>(Gr + go * 8);
+        g1r = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+        gbr = bits[(long)(2 * ct0 + gsl) * bits_rows + go];
+      }
+      rowit_adv(git, X3_WG_RB, E, G::HOWO);
+    };
+    auto write_stage = [&](int buf) {
+#pragma unroll
+      for (int j = 0; j < XIT; ++j) {
+        const int it = tid + 512 * j;
+        if (it < X3_WG_RB * G::KC) {
+          const int row = it / G::KC, kc = it - row * G::KC;
+          const s8v z = {0, 0, 0, 0, 0, 0, 0, 0};
+          *reinterpret_cast<s8v*>(&Xs[buf][0][row * XS + kc * 8]) = xv[j] ? xh[j] : z;
+          *reinterpret_cast<s8v*>(&Xs[buf][1][row * XS + kc * 8]) = xv[j] ? xlr[j] : z;
+        }
+      }
+      if (tid < 256 && gsl < 2 * NC) {
+        float m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (gv) {
+          const float gg[8] = {g0r.x, g0r.y, g0r.z, g0r.w, g1r.x, g1r.y, g1r.z, g1r.w};
+#pragma unroll
+          for (int c = 0; c < 8; ++c) m[c] = ((gbr >> c) & 1u) ? gg[c] : 0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) bpart[c] += m[c];
+        s8v hi, lo;
+        split8(m, hi, lo);
+        *reinterpret_cast<s8v*>(&Gs[buf][0][grow * GS + gsl * 8]) = hi;
+        *reinterpret_cast<s8v*>(&Gs[buf][1][grow * GS + gsl * 8]) = lo;
+      }
+    };
+    auto compute = [&](int buf) {
+      s8v bh[NC], bl[NC];
+#pragma unroll
+      for (int nt = 0; nt < NC; ++nt) {
+        const int o0 = (8 * grp + q) * GS + nt * 16 + 4 * pp, o1 = (8 * grp + 4 + q) * GS + nt * 16 + 4 * pp;
+        bh[nt] = tr8(Gs[buf][0] + o0, Gs[buf][0] + o1);
+        bl[nt] = tr8(Gs[buf][1] + o0, Gs[buf][1] + o1);
+      }
+#pragma unroll
+      for (int mi = 0; mi < MPW; ++mi) {
+        const int mt = w + NW * mi;
+        if (mt < NMT) {
+          const int o0 = (8 * grp + q) * XS + mt * 16 + 4 * pp, o1 = (8 * grp + 4 + q) * XS + mt * 16 + 4 * pp;
+          const s8v ah = tr8(Xs[buf][0] + o0, Xs[buf][0] + o1);
+          const s8v al = tr8(Xs[buf][1] + o0, Xs[buf][1] + o1);
+#pragma unroll
+          for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma3(ah, al, bh[nt], bl[nt], acc[mi][nt]);
+        }
+      }
+    };
+    __syncthreads();
+    if (r_begin < r_end) load_stage();
+    int rb = r_begin, buf = 0;
+    for (; rb + X3_WG_RB < r_end; rb += X3_WG_RB, buf ^= 1) {
+      write_stage(buf);
+      __syncthreads();
+      load_stage();
+      compute(buf);
+    }
+    if (rb < r_end) {
+      write_stage(buf);
+      __syncthreads();
+      compute(buf);
+    }
+    const int h = i16 >> 3, ch = l & 7;
+#pragma unroll
+    for (int mi = 0; mi < MPW; ++mi) {
+      const int mt = w + NW * mi;
+      if (mt < NMT) {
+#pragma unroll
+        for (int nt = 0; nt < NC; ++nt) {
+          const int slot = (ct0 + nt) * 2 + h;
+          if (slot < cnt) {
+            const long base = w_off + (long)mods[slot] * chunk;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = mt * 16 + 4 * grp + r;
+              if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale));
+            }
+          }
+        }
+      }
+    }
+    if (gact) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) atomicAdd(&dbias[(2 * ct0 + gsl) * 8 + c], bpart[c] * g_scale);
+    }
+  };
+  for (int pass = 0; pass < npass; ++pass) {
+    const int ct0 = pass * X3_NCX;
+    switch (min(X3_NCX, nct - ct0)) {
+      case 1: run(std::integral_constant<int, 1>{}, ct0); break;
+      case 2: run(std::integral_constant<int, 2>{}, ct0); break;
+      default: run(std::integral_constant<int, 3>{}, ct0); break;
+    }
+  }
+  __syncthreads();
+  if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
+}
+
+// ===========================================================================
+// input gradient of the bf16-activation conv layers on MFMA, "superpixel" implicit GEMM (conv_fast.hip
+// conv_dgrad_mfma describes the geometry): one GEMM row = one superpixel (the S x S input pixels that read the
+// same output positions through different taps), N = (ph, pw, ci), K = (tap, slot, c).  Per sample the masked
+// output gradient of 4 active slots is split into hi/lo planes in LDS (a path with more active slots runs a pass
+// per group of 4, adding into dX); B = the hi/lo weights of those slots.  fp32 dX.  grid = (chunks, P).
+// ===========================================================================
+#define X3_DG_PSTR 32        // one position's 4 slots x 8 maps
+DEVI int dg_swz(int i) { return (i >> 1) & 3; }
+template <class G>
+struct DGM {
+  static constexpr int S = G::S;
+  static constexpr int NA = (G::KH + S - 1) / S;
+  static constexpr int NTAP = NA * NA;
+  static constexpr int NI = (G::HIN + S - 1) / S, NJ = (G::WIN + S - 1) / S;
+  static constexpr int NSP = NI * NJ;
+  static constexpr int NRT = (NSP + 15) / 16;
+  static constexpr int NN = 8 * S * S;
+  static constexpr int NT = (NN + 15) / 16;
+};
+
+template <class G>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
+                                                       const float* __restrict__ flat, long w_off, int chunk,
+                                                       const int* __restrict__ act_idx,
+                                                       const int* __restrict__ act_cnt, int layer, int L, int M, int P,
+                                                       int E, int T, long bits_rows, float g_scale,
+                                                       float* __restrict__ dX, int samples_per_wg) {
+  using D = DGM<G>;
+  constexpr int S = D::S;
+  constexpr int NTAPP = (D::NTAP + 3) & ~3;
+  constexpr int GPL = (G::HOWO + 1) * X3_DG_PSTR;
+  constexpr int BPL = D::NTAP * D::NT * 16 * 32;
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][GPL];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BPL];
+  __shared__ int mods[X3_MAXM];
+  __shared__ __attribute__((aligned(16))) uint16_t atap[D::NRT * 16 * NTAPP];
+  __shared__ __attribute__((aligned(8))) uint16_t etab[D::NRT * 16];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int PE = P * E;
+  const int nsamp = T * E;
+  const int s_beg = blockIdx.x * samples_per_wg;
+  const int s_end = min(nsamp, s_beg + samples_per_wg);
+  if (s_beg >= s_end) return;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  __syncthreads();
+  const int ngroup = cnt > 4 ? (cnt + 3) >> 2 : 1;
+  // B[k][n] of slot group g: k = (tap, slot a4, c), n = (ph*S + pw)*8 + ci  ->  W_a[kh][kw][ci][c], hi/lo
+  auto stage_b = [&](int g) {
+    for (int it = tid; it < D::NTAP * D::NT * 16 * 4; it += 256) {
+      const int a4 = it & 3, rest = it >> 2;
+      const int n = rest % (D::NT * 16), tap = rest / (D::NT * 16);
+      const int a = 4 * g + a4;
+      const int ta = tap / D::NA, tb = tap - ta * D::NA;
+      const int cls = n >> 3, ci = n & 7, ph = cls / S, pw = cls - ph * S;
+      const int kh = ph + S * ta, kw = pw + S * tb;
+      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (n < D::NN && a < cnt && kh < G::KH && kw < G::KW) {
+        const float* wp = flat + w_off + (long)mods[a] * chunk + ((kh * G::KW + kw) * 8 + ci) * 8;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = wp[c];
+      }
+      s8v hi, lo;
+      split8(v, hi, lo);
+      const int o = (tap * D::NT * 16 + n) * 32 + (a4 ^ dg_swz(n)) * 8;
+      *reinterpret_cast<s8v*>(Bs[0] + o) = hi;
+      *reinterpret_cast<s8v*>(Bs[1] + o) = lo;
+    }
+  };
+  constexpr int GIT = (G::HOWO + 255) / 256;
+  float4 g0r[GIT], g1r[GIT];
+  uint8_t gbr[GIT][12];
+  auto load_sample = [&](int s) {
+    const long sg = sample_global(p, s, E, PE, 0);
+#pragma unroll
+    for (int j = 0; j < GIT; ++j) {
+      const int pos = tid + 256 * j;
+      if (pos < G::HOWO) {
+        const long go = sg * G::HOWO + pos;
+        g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+        g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+#pragma unroll
+        for (int a = 0; a < 12; ++a) gbr[j][a] = a < cnt ? bits[(long)a * bits_rows + go] : (uint8_t)0;
+      }
+    }
+  };
+  static_assert(S <= 2, "dgrad class limits are packed for strides 1 and 2");
+  static_assert((G::HOWO + 1) * X3_DG_PSTR < (1 << 16), "atap offset field");
+  static_assert((S * (D::NI - 1) * G::WIN + S * (D::NJ - 1)) * 8 < (1 << 14), "etab offset field");
+  for (int sp = tid; sp < D::NRT * 16; sp += 256) {
+    const int ii = sp / D::NJ, jj = sp - ii * D::NJ;
+#pragma unroll
+    for (int tap = 0; tap < NTAPP; ++tap) {
+      const int ta = tap / D::NA, tb = tap - ta * D::NA;
+      const int oh = ii - ta, ow = jj - tb;
+      const bool ok = tap < D::NTAP && sp < D::NSP && oh >= 0 && oh < G::HO && ow >= 0 && ow < G::WO;
+      const int apos = ok ? oh * G::WO + ow : G::HOWO;
+      atap[sp * NTAPP + tap] = (uint16_t)(apos * X3_DG_PSTR + (dg_swz(apos) << 3));
+    }
+    etab[sp] = sp < D::NSP ? (uint16_t)((S * ii * G::WIN + S * jj) * 8 | ((S * ii + 1 < G::HIN) << 14) |
+                                        ((S * jj + 1 < G::WIN) << 15))
+                           : (uint16_t)0xFFFF;
+  }
+  for (int i = tid; i < 2 * X3_DG_PSTR; i += 256) Gs[i / X3_DG_PSTR][G::HOWO * X3_DG_PSTR + (i % X3_DG_PSTR)] = 0;
+  int nofs[D::NT], nph[D::NT], npw[D::NT];
+#pragma unroll
+  for (int nt = 0; nt < D::NT; ++nt) {
+    const int n = nt * 16 + c16;
+    const int cls = n >> 3, ci = n & 7;
+    nph[nt] = n < D::NN ? cls / S : 9;
+    npw[nt] = cls - (cls / S) * S;
+    nofs[nt] = ((cls / S) * G::WIN + npw[nt]) * 8 + ci;
+  }
+  if (ngroup == 1) stage_b(0);
+  load_sample(s_beg);
+  for (int s = s_beg; s < s_end; ++s) {
+    const long sg = sample_global(p, s, E, PE, 0);
+    float* __restrict__ dXs = dX + sg * (long)(G::HIN * G::WIN * 8);
+    for (int g = 0; g < ngroup; ++g) {
+      __syncthreads();                             // previous LDS reads done
+      if (ngroup > 1) stage_b(g);
+#pragma unroll
+      for (int j = 0; j < GIT; ++j) {
+        const int pos = tid + 256 * j;
+        if (pos < G::HOWO) {
+          const float gg[8] = {g0r[j].x * g_scale, g0r[j].y * g_scale, g0r[j].z * g_scale, g0r[j].w * g_scale,
+                               g1r[j].x * g_scale, g1r[j].y * g_scale, g1r[j].z * g_scale, g1r[j].w * g_scale};
+#pragma unroll
+          for (int a4 = 0; a4 < 4; ++a4) {
+            const int b = (int)gbr[j][(4 * g + a4) < 12 ? 4 * g + a4 : 0] * (4 * g + a4 < cnt ? 1 : 0);
+            float m[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) m[c] = ((b >> c) & 1) ? gg[c] : 0.f;
+            s8v hi, lo;
+            split8(m, hi, lo);
+            const int o = pos * X3_DG_PSTR + (a4 ^ dg_swz(pos)) * 8;
+            *reinterpret_cast<s8v*>(Gs[0] + o) = hi;
+            *reinterpret_cast<s8v*>(Gs[1] + o) = lo;
+          }
+        }
+      }
+      __syncthreads();
+      if (g == ngroup - 1 && s + 1 < s_end) load_sample(s + 1);
+      for (int rt = w; rt < D::NRT; rt += 4) {
+        const uint16_t* tp = atap + (rt * 16 + c16) * NTAPP;
+        f4v acc[D::NT];
+#pragma unroll
+        for (int nt = 0; nt < D::NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tap = 0; tap < D::NTAP; ++tap) {
+          const int ao = (int)tp[tap] ^ (grp << 3);
+          const s8v ah = *reinterpret_cast<const s8v*>(Gs[0] + ao);
+          const s8v al = *reinterpret_cast<const s8v*>(Gs[1] + ao);
+          const int bo = (tap * D::NT * 16 + c16) * 32 + (grp ^ dg_swz(c16)) * 8;
+#pragma unroll
+          for (int nt = 0; nt < D::NT; ++nt) {
+            const s8v bh = *reinterpret_cast<const s8v*>(Bs[0] + bo + nt * 16 * 32);
+            const s8v bl = *reinterpret_cast<const s8v*>(Bs[1] + bo + nt * 16 * 32);
+            acc[nt] = mma3(ah, al, bh, bl, acc[nt]);
+          }
+        }
+        const uint2 e4 = *reinterpret_cast<const uint2*>(etab + rt * 16 + 4 * grp);
+        const uint32_t ev[4] = {e4.x & 0xFFFFu, e4.x >> 16, e4.y & 0xFFFFu, e4.y >> 16};
+#pragma unroll
+        for (int nt = 0; nt < D::NT; ++nt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t v = ev[r];
+            const bool okh = nph[nt] == 0 || (nph[nt] == 1 && ((v >> 14) & 1u));
+            const bool okw = npw[nt] == 0 || ((v >> 15) & 1u);
+            if (v != 0xFFFFu && okh && okw) {
+              float* o = dXs + (int)(v & 0x3FFFu) + nofs[nt];
+              *o = g == 0 ? acc[nt][r] : *o + acc[nt][r];
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// ===========================================================================
+// fc forward for the rollout (<= 32 rows per path), module per wave (trunk_fwd.hip fc_fwd_mw_kernel): A hi/lo
+// planes and B hi/lo from the [2][M][Cout][KP] weight copy, a D-deep register ring, three MFMAs per k-step.
+// OF32: the last layer writes fp32 (heads input); otherwise two bf16 planes.  grid = (1, Cout/64, P).
+// ===========================================================================
+template <int RT, int D, int NKS, bool OF32>
+__global__ __launch_bounds__(256) void fc_fwd_x3(const bf16_t* __restrict__ X, long xlo, int ldx,
+                                                 void* __restrict__ Yv, long ylo, uint16_t* __restrict__ bits,
+                                                 const bf16_t* __restrict__ Wc, long wlo,
+                                                 const float* __restrict__ flat, long bias_off, int chunk,
+                                                 const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
+                                                 int layer, int L, int M, int K, int KP, int Cout, int P, int E, int T,
+                                                 int t0, long bits_rows, float out_scale) {
+  __shared__ float part[4][32][64 + 1];
+  const int p = blockIdx.z;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const long Rtot = (long)T * E;
+  const int PE = P * E;
+  const long row0 = (long)blockIdx.x * 32;
+  const int col0 = blockIdx.y * 64;
+  long xrow[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) {
+    const long r = row0 + i * 16 + c16;
+    xrow[i] = sample_global(p, (int)(r < Rtot ? r : row0), E, PE, t0) * ldx;
+  }
+  float sum[RT][4][4];
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sum[i][j][r] = 0.f;
+  const int nwords = Cout / 16;
+  long sgb[RT][4];
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long row = row0 + i * 16 + 4 * grp + r;
+      sgb[i][r] = sample_global(p, (int)(row < Rtot ? row : row0), E, PE, t0);
+    }
+  for (int a = w; a < cnt; a += 4) {
+    const int mod = act_idx[(p * L + layer) * M + a];
+    const bf16_t* Wm = Wc + (long)mod * Cout * KP + (long)(col0 + c16) * KP + 8 * grp;
+    f4v acc[RT][4];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+    s8v ah[D][RT], al[D][RT], bh[D][4], bl[D][4];
+    auto load = [&](int d, int kk) {
+      const int k0 = kk + 8 * grp;
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+        if (K == KP) {
+          ah[d][i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+          al[d][i] = *reinterpret_cast<const s8v*>(X + xlo + xrow[i] + k0);
+        } else {
+          ah[d][i] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+          al[d][i] = ah[d][i];
+          if (k0 < K) {
+            ah[d][i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+            al[d][i] = *reinterpret_cast<const s8v*>(X + xlo + xrow[i] + k0);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bh[d][j] = *reinterpret_cast<const s8v*>(Wm + (long)j * 16 * KP + kk);
+        bl[d][j] = *reinterpret_cast<const s8v*>(Wm + wlo + (long)j * 16 * KP + kk);
+      }
+    };
+    auto mma = [&](int d) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < RT; ++i) acc[i][j] = mma3(ah[d][i], al[d][i], bh[d][j], bl[d][j], acc[i][j]);
+    };
+    const int nks = NKS > 0 ? NKS : KP / 32;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (d < nks) load(d, d * 32);
+    int s = 0;
+#pragma unroll
+    for (; s + 2 * D <= nks; s += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        mma(d);
+        load(d, (s + d + D) * 32);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (s + d < nks) {
+        mma(d);
+        if (s + d + D < nks) load(d, (s + d + D) * 32);
+      }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (s + D + d < nks) mma(d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float bb = flat[bias_off + (long)mod * chunk + col0 + j * 16 + c16];
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r] + bb;
+          const bool pos = v > 0.f;
+          sum[i][j][r] += pos ? v : 0.f;
+          const uint64_t bal = __ballot(pos);
+          if (c16 == 0 && row0 + i * 16 + 4 * grp + r < Rtot)
+            bits[((long)a * bits_rows + sgb[i][r]) * nwords + (col0 + j * 16) / 16] =
+                (uint16_t)((bal >> (16 * grp)) & 0xFFFFull);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[w][i * 16 + 4 * grp + r][j * 16 + c16] = sum[i][j][r];
+  __syncthreads();
+  const int orow = tid >> 3, oc = (tid & 7) * 8;
+  const long row = row0 + orow;
+  if (orow < RT * 16 && row < Rtot) {
+    const long sg = sample_global(p, (int)row, E, PE, t0);
+    float o[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      o[c] = (part[0][orow][oc + c] + part[1][orow][oc + c] + part[2][orow][oc + c] + part[3][orow][oc + c]) *
+             out_scale;
+    if constexpr (OF32) {
+      float* Y = reinterpret_cast<float*>(Yv) + sg * Cout + col0 + oc;
+      *reinterpret_cast<float4*>(Y) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(Y + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+      bf16_t* Y = reinterpret_cast<bf16_t*>(Yv) + sg * Cout + col0 + oc;
+      s8v hi, lo;
+      split8(o, hi, lo);
+      *reinterpret_cast<s8v*>(Y) = hi;
+      *reinterpret_cast<s8v*>(Y + ylo) = lo;
+    }
+  }
+}
+
+// ===========================================================================
+// fc input gradient (trunk_bwd.hip fc_dgrad_lds_kernel): per workgroup 64 rows; the masked gradient of 2 active
+// slots is split into hi/lo planes in LDS (135 KB: 1 workgroup of 512 threads per CU), every 128-column chunk of
+// dX is swept with the hi/lo weight fragments of WcT [2][M][KP][COUT] in registers (next iteration's prefetched).
+// Slot groups beyond the first add into dX.  Gm (optional): the masked hi/lo gradient per slot for the weight
+// gradient, [2][M][bits_rows][COUT] (lo plane at +gmlo).  1-D grid (split, path, row block), XCD-aware order.
+// ===========================================================================
+template <int COUT>
+__global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, const uint16_t* __restrict__ bits,
+                                                   const bf16_t* __restrict__ WcT, long wlo,
+                                                   const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
+                                                   int layer, int L, int M, int K, int KP, int P, int E, int T,
+                                                   long bits_rows, float g_scale, float* __restrict__ dX,
+                                                   int chunks_per_split, int nrowb, int nsplit,
+                                                   bf16_t* __restrict__ Gm, long gmlo) {
+  constexpr int CS = COUT + 8;
+  constexpr int NW = COUT / 16;
+  constexpr int NSL = 2;                               // slots per group
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][NSL * 64 * CS];
+  const int seq = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (seq >= nrowb * P * nsplit) return;
+  const int bz = seq / (nrowb * P), sr_ = seq - bz * (nrowb * P);
+  const int p = sr_ / nrowb, bx = sr_ - p * nrowb;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const long R = (long)T * E;
+  const int PE = P * E;
+  const long row0 = (long)bx * 64;
+  const int nchunks = (K + 127) / 128;
+  const int ch_beg = bz * chunks_per_split;
+  const int ch_end = min(nchunks, ch_beg + chunks_per_split);
+  if (ch_beg >= ch_end) return;
+  long sg_out[4][4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long row = row0 + rb * 16 + 4 * grp + r;
+      sg_out[rb][r] = row < R ? sample_global(p, (int)row, E, PE, 0) : -1;
+    }
+  const int ngroups = cnt > 0 ? (cnt + NSL - 1) / NSL : 1;
+  for (int gi = 0; gi < ngroups; ++gi) {
+    const int g0 = gi * NSL;
+    const int ng = min(NSL, cnt - g0);
+    __syncthreads();
+    {
+      constexpr int SEG = COUT / 8;
+      const int sr = tid >> 3, c0 = (tid & 7) * SEG;
+      const long r = row0 + sr;
+      const bool v = r < R;
+      const long sg = v ? sample_global(p, (int)r, E, PE, 0) : 0;
+#pragma unroll
+      for (int cc = 0; cc < SEG; cc += 8) {
+        const int c = c0 + cc;
+        float gv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (v) {
+          const float4 a0 = *reinterpret_cast<const float4*>(G + sg * COUT + c);
+          const float4 a1 = *reinterpret_cast<const float4*>(G + sg * COUT + c + 4);
+          gv[0] = a0.x * g_scale; gv[1] = a0.y * g_scale; gv[2] = a0.z * g_scale; gv[3] = a0.w * g_scale;
+          gv[4] = a1.x * g_scale; gv[5] = a1.y * g_scale; gv[6] = a1.z * g_scale; gv[7] = a1.w * g_scale;
+        }
+        for (int a = 0; a < ng; ++a) {
+          const uint32_t bw = v ? ((uint32_t)bits[((long)(g0 + a) * bits_rows + sg) * NW + (c >> 4)] >> (c & 15)) : 0u;
+          float m[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[j] = ((bw >> j) & 1u) ? gv[j] : 0.f;
+          s8v hi, lo;
+          split8(m, hi, lo);
+          *reinterpret_cast<s8v*>(Gs[0] + (a * 64 + sr) * CS + c) = hi;
+          *reinterpret_cast<s8v*>(Gs[1] + (a * 64 + sr) * CS + c) = lo;
+          if (Gm != nullptr && v && (tid & 7) % nsplit == bz) {
+            bf16_t* gp = Gm + ((long)(g0 + a) * bits_rows + sg) * COUT + c;
+            *reinterpret_cast<s8v*>(gp) = hi;
+            *reinterpret_cast<s8v*>(gp + gmlo) = lo;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (ng <= 0) {
+      for (int ch = ch_beg; ch < ch_end; ++ch) {
+        const int kcol = ch * 128 + w * 16 + c16;
+        if (kcol < K)
+          for (int rb = 0; rb < 4; ++rb)
+            for (int r = 0; r < 4; ++r)
+              if (sg_out[rb][r] >= 0) dX[sg_out[rb][r] * K + kcol] = 0.f;
+      }
+      continue;
+    }
+    const int n_it = (ch_end - ch_beg) * ng;
+    const int* aidx = act_idx + (p * L + layer) * M + g0;
+    s8v b0h[COUT / 32], b0l[COUT / 32], b1h[COUT / 32], b1l[COUT / 32];
+    auto wload = [&](s8v* bh, s8v* bl, int it) {
+      const int ch = ch_beg + it / ng, a = it - (it / ng) * ng;
+      const int kc = ch * 128 + w * 16 + c16;
+      const bf16_t* Wm = WcT + (long)aidx[a] * KP * COUT + (long)kc * COUT + 8 * grp;
+#pragma unroll
+      for (int c = 0; c < COUT / 32; ++c) {
+        bh[c] = kc < KP ? *reinterpret_cast<const s8v*>(Wm + 32 * c) : (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+        bl[c] = kc < KP ? *reinterpret_cast<const s8v*>(Wm + wlo + 32 * c) : (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    };
+    f4v acc[4];
+    auto body = [&](const s8v* bh, const s8v* bl, int it) {
+      const int ch = ch_beg + it / ng, a = it - (it / ng) * ng;
+      if (a == 0) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) acc[rb] = {0.f, 0.f, 0.f, 0.f};
+      }
+      const int ao = (a * 64 + c16) * CS + 8 * grp;
+#pragma unroll
+      for (int c = 0; c < COUT / 32; ++c)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const s8v fh = *reinterpret_cast<const s8v*>(Gs[0] + ao + rb * 16 * CS + 32 * c);
+          const s8v fl = *reinterpret_cast<const s8v*>(Gs[1] + ao + rb * 16 * CS + 32 * c);
+          acc[rb] = mma3(fh, fl, bh[c], bl[c], acc[rb]);
+        }
+      const int kcol = ch * 128 + w * 16 + c16;
+      if (a == ng - 1 && kcol < K) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const long sg = sg_out[rb][r];
+            if (sg >= 0) {
+              float* o = dX + sg * K + kcol;
+              *o = gi == 0 ? acc[rb][r] : *o + acc[rb][r];
+            }
+          }
+      }
+    };
+    wload(b0h, b0l, 0);
+    int it = 0;
+    for (; it + 2 < n_it; it += 2) {
+      wload(b1h, b1l, it + 1);
+      body(b0h, b0l, it);
+      wload(b0h, b0l, it + 2);
+      body(b1h, b1l, it + 1);
+    }
+    if (it + 1 < n_it) {
+      wload(b1h, b1l, it + 1);
+      body(b0h, b0l, it);
+      body(b1h, b1l, it + 1);
+    } else {
+      body(b0h, b0l, it);
+    }
+  }
+}
+
+// ===========================================================================
+// fc weight gradient from the masked hi/lo gradient Gm written by fc_dgrad_x3 (trunk_bwd.hip fc_wgrad_gm_kernel):
+// 128 x COUT tiles, module-major users, 32-row stages of X (hi/lo) and Gm (hi/lo) double-buffered in LDS.
+// ===========================================================================
+template <int COUT>
+__global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__ X, long xlo, int ldx,
+                                                      const bf16_t* __restrict__ Gm, long gmlo,
+                                                      float* __restrict__ grad, long w_off, long b_off, int chunk,
+                                                      const int* __restrict__ inv_path,
+                                                      const int* __restrict__ inv_slot,
+                                                      const int* __restrict__ inv_cnt, int layer, int M, int Pmax,
+                                                      int K, int P, int E, int T, long bits_rows, int nsplit) {
+  constexpr int XS = 128 + 8;
+  constexpr int GS = COUT + 8;
+  constexpr int NT = COUT / 32;
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][2][32 * XS];
+  __shared__ __attribute__((aligned(16))) bf16_t Gsh[2][2][32 * GS];
+  const int kt = (K + 127) / 128;
+  const int zt = blockIdx.x / kt, tile_k = blockIdx.x - zt * kt;
+  const int j = zt / nsplit, split = zt - j * nsplit;
+  const int n_all = inv_cnt[layer * M + j];
+  const int u_beg = (int)((long)n_all * split / nsplit), u_end = (int)((long)n_all * (split + 1) / nsplit);
+  if (u_beg >= u_end) return;
+  const int k0 = tile_k * 128;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
+  const int wk = w >> 1, wn = w & 1;
+  const int Rtot = T * E, PE = P * E;
+  const int nrb = (Rtot + 31) / 32;
+  const int n_it = (u_end - u_beg) * nrb;
+  const int* ip = inv_path + (layer * M + j) * Pmax;
+  const int* is = inv_slot + (layer * M + j) * Pmax;
+  constexpr int GSEG = COUT / 16;
+  const int lr = tid >> 4, lxs = (tid & 15) * 8, lgs = (tid & 15) * GSEG;
+  const bool xin = k0 + lxs < K;
+  s8v xrh, xrl, grh[GSEG / 8], grl[GSEG / 8];
+  auto gload = [&](int it) {
+    const int ui = it / nrb;
+    const int r = (it - ui * nrb) * 32 + lr;
+    const int p = ip[u_beg + ui], a = is[u_beg + ui];
+    xrh = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+    xrl = xrh;
+#pragma unroll
+    for (int h = 0; h < GSEG / 8; ++h) { grh[h] = xrh; grl[h] = xrh; }
+    if (r < Rtot) {
+      const long sg = sample_global(p, r, E, PE, 0);
+      if (xin) {
+        xrh = *reinterpret_cast<const s8v*>(X + sg * ldx + k0 + lxs);
+        xrl = *reinterpret_cast<const s8v*>(X + xlo + sg * ldx + k0 + lxs);
+      }
+      const bf16_t* gp = Gm + ((long)a * bits_rows + sg) * COUT + lgs;
+#pragma unroll
+      for (int h = 0; h < GSEG / 8; ++h) {
+        grh[h] = *reinterpret_cast<const s8v*>(gp + 8 * h);
+        grl[h] = *reinterpret_cast<const s8v*>(gp + gmlo + 8 * h);
+      }
+    }
+  };
+  f4v acc[2][NT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
+  float bsum[NT];
+#pragma unroll
+  for (int jj = 0; jj < NT; ++jj) bsum[jj] = 0.f;
+  const bool do_bias = tile_k == 0 && wk == 0;
+  gload(0);
+  for (int it = 0; it < n_it; ++it) {
+    const int buf = it & 1;
+    *reinterpret_cast<s8v*>(Xs[buf][0] + lr * XS + lxs) = xrh;
+    *reinterpret_cast<s8v*>(Xs[buf][1] + lr * XS + lxs) = xrl;
+#pragma unroll
+    for (int h = 0; h < GSEG / 8; ++h) {
+      *reinterpret_cast<s8v*>(Gsh[buf][0] + lr * GS + lgs + 8 * h) = grh[h];
+      *reinterpret_cast<s8v*>(Gsh[buf][1] + lr * GS + lgs + 8 * h) = grl[h];
+    }
+    __syncthreads();
+    if (it + 1 < n_it) gload(it + 1);
+    s8v afh[2], afl[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int o0 = (8 * grp + q) * XS + 32 * wk + 16 * i + 4 * pp;
+      const int o1 = (8 * grp + 4 + q) * XS + 32 * wk + 16 * i + 4 * pp;
+      afh[i] = tr8(Xs[buf][0] + o0, Xs[buf][0] + o1);
+      afl[i] = tr8(Xs[buf][1] + o0, Xs[buf][1] + o1);
+    }
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj) {
+      const int nb = (COUT / 2) * wn + 16 * jj;
+      const int o0 = (8 * grp + q) * GS + nb + 4 * pp, o1 = (8 * grp + 4 + q) * GS + nb + 4 * pp;
+      const s8v bh = tr8(Gsh[buf][0] + o0, Gsh[buf][0] + o1);
+      const s8v bl = tr8(Gsh[buf][1] + o0, Gsh[buf][1] + o1);
+      acc[0][jj] = mma3(afh[0], afl[0], bh, bl, acc[0][jj]);
+      acc[1][jj] = mma3(afh[1], afl[1], bh, bl, acc[1][jj]);
+      if (do_bias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum[jj] += bf2f((uint16_t)bh[e]) + bf2f((uint16_t)bl[e]);
+      }
+    }
+  }
+  const long base = w_off + (long)j * chunk;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + 32 * wk + 16 * i + 4 * grp + r;
+        const int n = (COUT / 2) * wn + 16 * jj + i16;
+        if (k < K) {
+          if (nsplit == 1) grad[base + (long)k * COUT + n] = acc[i][jj][r];
+          else atomicAdd(&grad[base + (long)k * COUT + n], acc[i][jj][r]);
+        }
+      }
+  if (do_bias) {
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj) {
+      float v = bsum[jj];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (grp == 0) {
+        const long o = b_off + (long)j * chunk + (COUT / 2) * wn + 16 * jj + i16;
+        if (nsplit == 1) grad[o] = v;
+        else atomicAdd(&grad[o], v);
+      }
+    }
+  }
+}
+
+// ===========================================================================
+// fc weight gradient, 64 x 64 tiles (trunk_bwd.hip fc_wgrad_kernel) for the narrow fc layers: X hi/lo planes,
+// fp32 G masked by the ReLU bits and split into hi/lo while staging.  grid = (K/64, Cout/64, M * nsplit).
+// ===========================================================================
+__global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X, long xlo, int ldx,
+                                                   const float* __restrict__ G, const uint16_t* __restrict__ bits,
+                                                   float* __restrict__ grad, long w_off, long b_off, int chunk,
+                                                   const int* __restrict__ inv_path, const int* __restrict__ inv_slot,
+                                                   const int* __restrict__ inv_cnt, int layer, int M, int Pmax, int K,
+                                                   int Cout, int P, int E, int T, long bits_rows, float g_scale,
+                                                   int nsplit) {
+  constexpr int S = 64 + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][32 * S];
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][32 * S];
+  __shared__ float dbias[64];
+  const int j = blockIdx.z / nsplit, split = blockIdx.z - j * nsplit;
+  const int n_all = inv_cnt[layer * M + j];
+  const int u_beg = (int)((long)n_all * split / nsplit), u_end = (int)((long)n_all * (split + 1) / nsplit);
+  if (u_beg >= u_end) return;
+  const int k0b = blockIdx.x * 64, n0b = blockIdx.y * 64;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
+  const bool do_bias = blockIdx.x == 0;
+  if (tid < 64) dbias[tid] = 0.f;
+  const long Rtot = (long)T * E;
+  const int PE = P * E;
+  const int nwords = Cout / 16;
+  f4v acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) { acc[a][0] = {0.f, 0.f, 0.f, 0.f}; acc[a][1] = {0.f, 0.f, 0.f, 0.f}; }
+  float bpart[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int srow = tid >> 3, sc = (tid & 7) * 8;
+  const int mt0 = 2 * (w >> 1), nt0 = 2 * (w & 1);
+  for (int u = u_beg; u < u_end; ++u) {
+    const int p = inv_path[(layer * M + j) * Pmax + u];
+    const int a = inv_slot[(layer * M + j) * Pmax + u];
+    for (long rb = 0; rb < Rtot; rb += 32) {
+      const long r = rb + srow;
+      s8v xh = {0, 0, 0, 0, 0, 0, 0, 0}, xl = xh;
+      float m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (r < Rtot) {
+        const long sg = sample_global(p, (int)r, E, PE, 0);
+        if (k0b + sc < K) {
+          xh = *reinterpret_cast<const s8v*>(X + sg * ldx + k0b + sc);
+          xl = *reinterpret_cast<const s8v*>(X + xlo + sg * ldx + k0b + sc);
+        }
+        const int n = n0b + sc;
+        if (n < Cout) {
+          const float4 g0 = *reinterpret_cast<const float4*>(G + sg * Cout + n);
+          const float4 g1 = *reinterpret_cast<const float4*>(G + sg * Cout + n + 4);
+          const uint32_t bw = bits[((long)a * bits_rows + sg) * nwords + (n >> 4)] >> (n & 15);
+          const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            m[c] = ((bw >> c) & 1u) ? gg[c] * g_scale : 0.f;
+            bpart[c] += m[c];
+          }
+        }
+      }
+      s8v gh, gl;
+      split8(m, gh, gl);
+      *reinterpret_cast<s8v*>(Xs[0] + srow * S + sc) = xh;
+      *reinterpret_cast<s8v*>(Xs[1] + srow * S + sc) = xl;
+      *reinterpret_cast<s8v*>(Gs[0] + srow * S + sc) = gh;
+      *reinterpret_cast<s8v*>(Gs[1] + srow * S + sc) = gl;
+      __syncthreads();
+      s8v afh[2], afl[2], bfh[2], bfl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int xo0 = (8 * grp + q) * S + (mt0 + i) * 16 + 4 * pp, xo1 = (8 * grp + 4 + q) * S + (mt0 + i) * 16 + 4 * pp;
+        afh[i] = tr8(Xs[0] + xo0, Xs[0] + xo1);
+        afl[i] = tr8(Xs[1] + xo0, Xs[1] + xo1);
+        const int go0 = (8 * grp + q) * S + (nt0 + i) * 16 + 4 * pp, go1 = (8 * grp + 4 + q) * S + (nt0 + i) * 16 + 4 * pp;
+        bfh[i] = tr8(Gs[0] + go0, Gs[0] + go1);
+        bfl[i] = tr8(Gs[1] + go0, Gs[1] + go1);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma3(afh[i], afl[i], bfh[jj], bfl[jj], acc[i][jj]);
+      __syncthreads();
+    }
+  }
+  const long base = w_off + (long)j * chunk;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0b + (mt0 + i) * 16 + 4 * grp + r;
+        const int n = n0b + (nt0 + jj) * 16 + i16;
+        if (k < K && n < Cout) {
+          if (nsplit == 1) grad[base + (long)k * Cout + n] = acc[i][jj][r];
+          else atomicAdd(&grad[base + (long)k * Cout + n], acc[i][jj][r]);
+        }
+      }
+  if (do_bias) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) atomicAdd(&dbias[sc + c], bpart[c]);
+    __syncthreads();
+    if (tid < 64 && n0b + tid < Cout) {
+      if (nsplit == 1) grad[b_off + (long)j * chunk + n0b + tid] = dbias[tid];
+      else atomicAdd(&grad[b_off + (long)j * chunk + n0b + tid], dbias[tid]);
+    }
+  }
+}
+
+// hi/lo operand copies of one layer's weights: Wc [2][M][Cout][KP] (k contiguous, zero padded) and optionally
+// WcT [2][M][KP][Cout].  f16: fp16 pair of W * 2^X3_W0_SHIFT (uint8 first layer); *status = 1 when a scaled weight
+// leaves the fp16 range (checked by the host, runtime/guard.py)
+__global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict__ flat, long w_off, int chunk, int K,
+                                                         int KP, int Cout, int M, uint16_t* __restrict__ Wc,
+                                                         uint16_t* __restrict__ WcT, int f16,
+                                                         uint32_t* __restrict__ status) {
+  const long n = (long)M * KP * Cout;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int j = (int)(i / ((long)KP * Cout));
+    const int rem = (int)(i - (long)j * KP * Cout);
+    const int k = rem / Cout, c = rem - k * Cout;
+    const float v = k < K ? flat[w_off + (long)j * chunk + (long)k * Cout + c] : 0.f;
+    uint16_t hi, lo;
+    if (f16) {
+      const float x = v * (float)(1 << X3_W0_SHIFT);
+      const _Float16 h = (_Float16)x;
+      const _Float16 lw = (_Float16)(x - (float)h);
+      hi = __builtin_bit_cast(uint16_t, h);
+      lo = __builtin_bit_cast(uint16_t, lw);
+      if (!(fabsf(x) < 32768.f) && status) *status = 1u;
+    } else {
+      hi = f2bf(v);
+      lo = f2bf(v - bf2f(hi));
+    }
+    const long wi = ((long)j * Cout + c) * KP + k;
+    Wc[wi] = hi;
+    Wc[n + wi] = lo;
+    if (WcT) {
+      WcT[i] = hi;
+      WcT[n + i] = lo;
+    }
+  }
+}
+
+}  // namespace x3
+
+// ---------------------------------------------------------------------------
+// C ABI.  Every launcher returns 1 when it handled the call, 0 when the shape is not one of the specialised
+// geometries (the caller must not run the fp32x mode for it), <0 on invalid arguments (-22) or launch errors.
+// ---------------------------------------------------------------------------
+using namespace x3;
+
+template <class G>
+struct Tag {
+  using type = G;
+};
+
+template <class G>
+static bool x3_is(int Hin, int Win, int Cin, int KH, int KW, int S, int u8) {
+  return Hin == G::HIN && Win == G::WIN && Cin == G::CIN && KH == G::KH && KW == G::KW && S == G::S &&
+         (u8 != 0) == G::U8;
+}
+
+static int X3_FWD_NT = 8;      // 32-row tiles per wave in the first-layer forward (4 for the bf16-input layers)
+
+extern "C" {
+
+void fast_conv_set_x3_fwd_nt(int nt) { X3_FWD_NT = nt; }
+
+int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits, const void* Wc, long wlo,
+                const float* flat, long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M,
+                int Hin, int Win, int Cin, int KH, int KW, int S, int P, int E, int T, int t0, long br, float is,
+                float os, hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 || P <= 0 ||
+      E <= 0 || T <= 0 || br <= 0 || u8in < 0 || bias_off < 0 || layer < 0 || t0 < 0 || xlo < 0 || ylo <= 0 ||
+      wlo <= 0) return -22;
+  if (M > 2 * X3_NCT) return 0;
+  if (x3_is<C1>(Hin, Win, Cin, KH, KW, S, u8in)) {
+    if ((E * C1::HOWO) % 16) return -2;
+    const long rows = (long)T * E * C1::HOWO;
+    const float isc = is / (float)(1 << X3_W0_SHIFT);
+#define C1L(NT_)                                                                                                \
+  conv1_fwd_x2<C1, NT_><<<dim3((unsigned)((rows + NT_ * 128 - 1) / (NT_ * 128)), P), 256, 0, st>>>(             \
+      (const uint8_t*)X, (bf16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, \
+      layer, L, M, P, E, T, t0, br, isc, os)
+    if (X3_FWD_NT >= 8) C1L(8); else C1L(4);
+#undef C1L
+    const int rc = (int)hipGetLastError();
+    return rc ? -rc : 1;
+  }
+#define CFX(Gx)                                                                                                   \
+  if (x3_is<Gx>(Hin, Win, Cin, KH, KW, S, u8in)) {                                                                \
+    if ((E * Gx::HOWO) % 16) return -2;                                                                           \
+    const long rows = (long)T * E * Gx::HOWO;                                                                     \
+    conv_fwd_x3<Gx, 4><<<dim3((unsigned)((rows + 511) / 512), P), 256, 0, st>>>(                                  \
+        (const bf16_t*)X, xlo, (bf16_t*)Y, ylo, (uint8_t*)bits, (const bf16_t*)Wc, wlo, flat, bias_off, chunk, ai,  \
+        ac, layer, L, M, P, E, T, t0, br, os);                                                                    \
+    const int rc = (int)hipGetLastError();                                                                        \
+    return rc ? -rc : 1;                                                                                          \
+  }
+  if (xlo <= 0) return -22;
+  CFX(C2) CFX(C3)
+#undef CFX
+  return 0;
+}
+
+int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void* bits, float* grad, long w_off,
+                  long b_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win,
+                  int Cin, int KH, int KW, int S, int P, int E, int T, long br, float is, float gs, hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 || P <= 0 ||
+      E <= 0 || T <= 0 || br <= 0 || u8in < 0 || w_off < 0 || b_off < 0 || layer < 0 || xlo < 0) return -22;
+  if (M > 2 * X3_NCT) return 0;
+  auto slab = [&](auto gc, auto obc) {
+    using Gx = typename decltype(gc)::type;
+    constexpr int OB = decltype(obc)::value;
+    using SB = Slab<Gx, OB>;
+    const long units = (long)T * E * SB::NB;
+    long upw = (units + 23) / 24;
+    if (upw < 8) upw = 8;
+    conv_wgrad_slab_x3<Gx, OB><<<dim3((unsigned)((units + upw - 1) / upw), P), 256, 0, st>>>(
+        X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, (int)upw, is,
+        gs);
+    const int rc = (int)hipGetLastError();
+    return rc ? -rc : 1;
+  };
+  if (x3_is<C1>(Hin, Win, Cin, KH, KW, S, u8in)) return slab(Tag<C1>{}, std::integral_constant<int, 2>{});
+  if (x3_is<C2>(Hin, Win, Cin, KH, KW, S, u8in)) {
+    if (xlo <= 0) return -22;
+    return slab(Tag<C2>{}, std::integral_constant<int, 7>{});
+  }
+  if (x3_is<C3>(Hin, Win, Cin, KH, KW, S, u8in)) {
+    if (xlo <= 0) return -22;
+    const long rows = (long)T * E * C3::HOWO;
+    long rpc = (rows + 15) / 16;
+    rpc = (rpc + X3_WG_RB - 1) / X3_WG_RB * X3_WG_RB;
+    if (rpc < X3_WG_RB * 4) rpc = X3_WG_RB * 4;
+    conv_wgrad_x3<C3><<<dim3((unsigned)((rows + rpc - 1) / rpc), P), 512, 0, st>>>(
+        (const bf16_t*)X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br,
+        (int)rpc, is, gs);
+    const int rc = (int)hipGetLastError();
+    return rc ? -rc : 1;
+  }
+  return 0;
+}
+
+int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,
+                  const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH, int KW, int S, int P,
+                  int E, int T, long br, float gs, float* dX, hipStream_t st) {
+  if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 || P <= 0 ||
+      E <= 0 || T <= 0 || br <= 0 || w_off < 0 || layer < 0) return -22;
+  if (M > 2 * X3_NCT) return 0;
+  const int nsamp = T * E;
+  int spw = (nsamp + 31) / 32;
+  if (spw < 2) spw = 2;
+  const dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
+#define DGX(Gx)                                                                                                    \
+  if (x3_is<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                                    \
+    conv_dgrad_x3<Gx><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, \
+                                            T, br, gs, dX, spw);                                                   \
+    const int rc = (int)hipGetLastError();                                                                         \
+    return rc ? -rc : 1;                                                                                           \
+  }
+  DGX(C2) DGX(C3)
+#undef DGX
+  return 0;
+}
+
+// ylo = 0: fp32 output (last layer); > 0: bf16 hi/lo planes
+int x3_fc_fwd(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, const void* Wc, long wlo,
+              const float* flat, long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int K,
+              int KP, int Cout, int P, int E, int T, int t0, long br, float os, hipStream_t st) {
+  if (ldx <= 0 || chunk <= 0 || L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 ||
+      br <= 0 || bias_off < 0 || layer < 0 || t0 < 0 || xlo <= 0 || ylo < 0 || wlo <= 0) return -22;
+  if (M > X3_MAXM || KP % 32 != 0 || Cout % 64 != 0 || ldx % 8 != 0 || ldx < K || (long)T * E > 32) return 0;
+  const dim3 grid(1, Cout / 64, P);
+#define FCX(RT_, D_, NKS_, OF_)                                                                                      \
+  fc_fwd_x3<RT_, D_, NKS_, OF_><<<grid, 256, 0, st>>>((const bf16_t*)X, xlo, ldx, Y, ylo, (uint16_t*)bits,          \
+                                                      (const bf16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, layer, L, \
+                                                      M, K, KP, Cout, P, E, T, t0, br, os)
+  const bool of = ylo == 0;
+  if ((long)T * E <= 16) {
+    if (of) FCX(1, 4, 0, true); else FCX(1, 4, 0, false);
+  } else if (KP == 1408) {
+    if (of) FCX(2, 4, 44, true); else FCX(2, 4, 44, false);
+  } else if (KP == 256) {
+    if (of) FCX(2, 4, 8, true); else FCX(2, 4, 8, false);
+  } else {
+    if (of) FCX(2, 4, 0, true); else FCX(2, 4, 0, false);
+  }
+#undef FCX
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
+int x3_fc_dgrad(const float* G, const void* bits, const void* WcT, long wlo, const int* ai, const int* ac, int layer,
+                int L, int M, int K, int KP, int Cout, int P, int E, int T, long br, float gs, float* dX, void* Gm,
+                long gmlo, hipStream_t st) {
+  if (L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 || layer < 0 ||
+      wlo <= 0 || gmlo < 0 || (Gm && gmlo <= 0)) return -22;
+  if (M > X3_MAXM || Cout != 256) return 0;
+  const int nchunks = (K + 127) / 128;
+  const int split = nchunks >= 8 ? 2 : 1;
+  const int per = (nchunks + split - 1) / split;
+  const int nrowb = (int)(((long)T * E + 63) / 64);
+  const int nwg = (nrowb * P * split + 7) / 8 * 8;
+  fc_dgrad_x3<256><<<nwg, 512, 0, st>>>(G, (const uint16_t*)bits, (const bf16_t*)WcT, wlo, ai, ac, layer, L, M, K, KP,
+                                        P, E, T, br, gs, dX, per, nrowb, split, (bf16_t*)Gm, gmlo);
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
+int x3_fc_wgrad_gm(const void* X, long xlo, int ldx, const void* Gm, long gmlo, float* grad, long w_off, long b_off,
+                   int chunk, const int* inv_path, const int* inv_slot, const int* inv_cnt, int layer, int M, int Pmax,
+                   int K, int Cout, int P, int E, int T, long br, int nsplit, hipStream_t st) {
+  if (ldx <= 0 || chunk <= 0 || M <= 0 || Pmax <= 0 || K <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 ||
+      nsplit <= 0 || w_off < 0 || b_off < 0 || layer < 0 || xlo <= 0 || gmlo <= 0) return -22;
+  if (Cout != 256 || ldx % 8 != 0 || K % 8 != 0) return 0;
+  const int kt = (K + 127) / 128;
+  fc_wgrad_gm_x3<256><<<kt * M * nsplit, 512, 0, st>>>((const bf16_t*)X, xlo, ldx, (const bf16_t*)Gm, gmlo, grad,
+                                                       w_off, b_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, Pmax,
+                                                       K, P, E, T, br, nsplit);
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
+int x3_fc_wgrad(const void* X, long xlo, int ldx, const float* G, const void* bits, float* grad, long w_off,
+                long b_off, int chunk, const int* inv_path, const int* inv_slot, const int* inv_cnt, int layer, int M,
+                int Pmax, int K, int Cout, int P, int E, int T, long br, float gs, hipStream_t st) {
+  if (ldx <= 0 || chunk <= 0 || M <= 0 || Pmax <= 0 || K <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 ||
+      w_off < 0 || b_off < 0 || layer < 0 || xlo <= 0) return -22;
+  if (Cout % 16 != 0 || ldx % 8 != 0) return 0;
+  const int tiles = ((K + 63) / 64) * ((Cout + 63) / 64) * M;
+  int nsplit = (2048 + tiles - 1) / tiles;
+  nsplit = nsplit < 1 ? 1 : (nsplit > Pmax ? Pmax : nsplit);
+  fc_wgrad_x3<<<dim3((K + 63) / 64, (Cout + 63) / 64, M * nsplit), 256, 0, st>>>(
+      (const bf16_t*)X, xlo, ldx, G, (const uint16_t*)bits, grad, w_off, b_off, chunk, inv_path, inv_slot, inv_cnt,
+      layer, M, Pmax, K, Cout, P, E, T, br, gs, nsplit);
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
+int x3_refresh_weights(const float* flat, long w_off, int chunk, int K, int KP, int Cout, int M, void* Wc, void* WcT,
+                       int f16, void* status, hipStream_t st) {
+  if (chunk <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || M <= 0 || w_off < 0 || f16 < 0 || KP < K) return -22;
+  const long n = (long)M * KP * Cout;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  refresh_x3_kernel<<<blocks, 256, 0, st>>>(flat, w_off, chunk, K, KP, Cout, M, (uint16_t*)Wc, (uint16_t*)WcT, f16,
+                                            (uint32_t*)status);
+  return (int)hipGetLastError();
+}
+}

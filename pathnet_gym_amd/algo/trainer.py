@@ -73,8 +73,8 @@ class PathNetTrainer:
         self.backend = resolve_backend(cfg.backend, self.device)
         # the torch backend always computes in fp32; the HIP engine uses bf16 (fp16 for the uint8 conv1
         # operands) MFMA with fp32 accumulation and fp32 master weights, or fp32 operands (compute_dtype="fp32")
-        if cfg.compute_dtype not in ("bf16", "fp32"):
-            raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'bf16' or 'fp32'")
+        if cfg.compute_dtype not in ("bf16", "fp32", "fp32x"):
+            raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'bf16', 'fp32' or 'fp32x'")
         self.compute_dtype = cfg.compute_dtype if self.backend == "hip" else "fp32"
         self.logger = logger
         net = cfg.net

@@ -90,6 +90,7 @@ _SIGS = {
     "launch_typed_fc_dgrad_mfma": [P, c_int, P, c_long, c_long, c_int, c_int, P, P, c_int, c_int, P, P, P],
     "launch_typed_fc_wgrad_mfma": [P, P, c_int, c_long, c_long, c_int, c_int, c_int, P, P, c_int, P, P, P],
     "launch_active_union": [P, P, c_int, c_int, c_int, P, P],
+    "launch_prof_marker": [c_int, P],
     "launch_pack_ranges": [P, P, P, c_int, c_long, c_int, P],
     "launch_heads_fwd_sample_f32": [P, c_int, P, c_long, c_long, c_long, c_long, c_int, c_int, P, P, P, c_uint, P,
                                     c_int, c_int, c_int, c_int, P],
@@ -115,6 +116,19 @@ _SIGS = {
                              c_int, c_int, c_int, c_int, c_int, c_long, c_float, P, c_int, P],
     "fast_conv_wgrad_bf16g": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P],
+    "x3_conv_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 13
+                   + [c_long, c_float, c_float, P],
+    "x3_conv_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 12
+                     + [c_long, c_float, c_float, P],
+    "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P],
+    "x3_fc_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 10
+                 + [c_long, c_float, P],
+    "x3_fc_dgrad": [P, P, P, c_long, P, P] + [c_int] * 9 + [c_long, c_float, P, P, c_long, P],
+    "x3_fc_wgrad_gm": [P, c_long, c_int, P, c_long, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8
+                      + [c_long, c_int, P],
+    "x3_fc_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8 + [c_long, c_float, P],
+    "x3_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
+    "fast_conv_set_x3_fwd_nt": [c_int],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }

@@ -38,6 +38,29 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
+# -- split-bf16 ("fp32x") activation storage: a value is the pair (hi, lo) of bf16 planes, hi + lo == fp32 value to
+# 2^-17 relative (csrc/trunk_x3.hip).  A tensor of the pair is the hi plane viewed out of a [2, ...] allocation; the
+# lo plane of any view starts a fixed number of elements further on (half the storage).
+def x2_alloc(shape, device) -> torch.Tensor:
+    """Hi plane of a zeroed [2, *shape] bf16 pair allocation."""
+    return torch.zeros((2,) + tuple(shape), dtype=torch.bfloat16, device=device)[0]
+
+
+def x2_lo(t: torch.Tensor) -> int:
+    """Element offset from any element of a pair tensor's hi plane to the same element of its lo plane."""
+    nb = t.untyped_storage().nbytes()
+    if t.dtype != torch.bfloat16 or nb % 4 != 0 or t.storage_offset() + t.numel() > nb // 4:
+        raise ValueError("not the hi plane of a split-bf16 pair allocation (x2_alloc)")
+    return nb // 4
+
+
+def x2_value(t: torch.Tensor) -> torch.Tensor:
+    """fp32 value hi + lo of a pair tensor (tests, checkpoints, the torch fallback)."""
+    lo = torch.empty(0, dtype=t.dtype, device=t.device).set_(t.untyped_storage(), t.storage_offset() + x2_lo(t),
+                                                            t.size(), t.stride())
+    return t.float() + lo.float()
+
+
 @dataclass
 class LayerGeom:
     kind: str
@@ -83,6 +106,12 @@ class HipPathNet:
         # compute_dtype "fp32": fp32 activations / operand copies on v_mfma_f32_16x16x4_f32 (csrc/trunk_f32.hip,
         # every reduction in a fixed order); "bf16": the bf16/fp16-operand MFMA kernels with fp32 accumulation
         self.f32 = getattr(model, "compute_dtype", "bf16") == "fp32"
+        # compute_dtype "fp32x": fp32-accurate split-bf16 operands (csrc/trunk_x3.hip): every activation between
+        # layers is a (hi, lo) bf16 pair, every MFMA product hi*hi + hi*lo + lo*hi, the last layer's output fp32
+        self.x3 = getattr(model, "compute_dtype", "bf16") == "fp32x"
+        if self.x3 and getattr(model, "deterministic", False):
+            raise NotImplementedError("compute_dtype='fp32x' reduces weight gradients with fp32 atomics; use 'fp32' "
+                                      "for bit-reproducible updates")
         self.act_dtype = torch.float32 if self.f32 else torch.bfloat16
         # deterministic reductions (TrainConfig.deterministic; implied by fp32): every weight/bias gradient is
         # summed in a fixed order (trunk_f32.hip ordered slabs, heads_reduce_kernel) instead of fp32 atomics,
@@ -124,13 +153,20 @@ class HipPathNet:
             self.geoms.append(g)
         self.pixels = cfg.layers[0].kind == "conv"
         self.out_scale_last = (1.0 / cfg.M) if cfg.trunk_scale == "M" else 1.0
-        # MFMA operand copies (bf16, or fp32 in the fp32 mode)
+        if self.x3:
+            self._check_x3()
+        # MFMA operand copies (bf16, or fp32 in the fp32 mode; fp32x: [2, ...] hi/lo planes, the uint8 first
+        # layer's as the fp16 pair of W * 2^8)
         self.Wc = []
         self.WcT = []
+        npl = (2,) if self.x3 else ()
         for l, g in enumerate(self.geoms):
-            self.Wc.append(torch.zeros(self.M, g.Cout, g.KP, dtype=self.act_dtype, device=dev))
+            wdt = torch.float16 if (self.x3 and g.u8in) else self.act_dtype
+            self.Wc.append(torch.zeros(npl + (self.M, g.Cout, g.KP), dtype=wdt, device=dev))
             need_t = g.kind == "fc" and l > 0
-            self.WcT.append(torch.zeros(self.M, g.KP, g.Cout, dtype=self.act_dtype, device=dev) if need_t else None)
+            self.WcT.append(torch.zeros(npl + (self.M, g.KP, g.Cout), dtype=self.act_dtype, device=dev)
+                            if need_t else None)
+        self.x3_status = torch.zeros(1, dtype=torch.int32, device=dev)   # fp16 range overflow of the scaled conv1 pair
         self._part = None            # fp32 conv wgrad partial slabs (allocated on first use, before capture)
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
@@ -140,7 +176,7 @@ class HipPathNet:
         self.heads_off = lay_h
         # fused LSTM cell (csrc/lstm.hip): bf16 copies of the fp32 master kernel
         self.lstm = None
-        if cfg.use_lstm and not self.deterministic:     # fp32 / deterministic: hybrid (autograd fp32) LSTM path
+        if cfg.use_lstm and not self.deterministic and not self.x3:   # fp32 / fp32x / deterministic: hybrid LSTM
             ls = lay.lstm
             F, H = ls["din"], ls["H"]
             if F % 64 == 0 and H % 64 == 0:
@@ -149,13 +185,13 @@ class HipPathNet:
                                  Kb=torch.zeros(F + H, 4 * H, dtype=torch.bfloat16, device=dev))
         # frame-ring input for the first layer (runtime/engine.py): channel-major bf16 weights
         g0 = self.geoms[0]
-        self.ring_ok = (not self.deterministic and g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
+        self.ring_ok = (not self.deterministic and not self.x3 and g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
                         and self.M <= 10 and g0.Cout == 8)
         self.Wc_ring = None
         # uint8 first conv layer: fp16 operand copy + per-column weight sums for the fp16-offset MFMA path
         # (conv_fwd_fast: pixels enter as fp16(1024 + v), built with one v_perm per two pixels)
         self.Wh0 = self.hcorr0 = None
-        if g0.kind == "conv" and g0.u8in and not self.f32:
+        if g0.kind == "conv" and g0.u8in and not self.f32 and not self.x3:
             self.Wh0 = torch.zeros(self.M, g0.Cout, g0.KP, dtype=torch.float16, device=dev)
             self.hcorr0 = torch.zeros(self.M * g0.Cout, dtype=torch.float32, device=dev)
         self.refresh_weights()
@@ -170,6 +206,34 @@ class HipPathNet:
             self.Wc_ring = torch.zeros(self.M, g.Cout, g.KP, dtype=torch.bfloat16, device=dev)
             self.Wh_ring = torch.zeros(self.M, g.Cout, g.KP, dtype=torch.float16, device=dev)     # fp16-offset path
             self.refresh_weights()
+
+    _X3_CONV = ((160, 120, 4, 8, 4, True), (39, 29, 8, 4, 2, False), (18, 13, 8, 3, 1, False))
+
+    def _check_x3(self):
+        """fp32x kernels exist for the reference pixel trunk geometries (csrc/trunk_x3.hip): uint8 160x120x4 8x8/s4,
+        then 39x29x8 4x4/s2 and 18x13x8 3x3/s1 conv layers, fc layers of 64k outputs over >= 8-aligned inputs."""
+        if self.M > 10:
+            raise NotImplementedError("fp32x kernels hold up to 10 modules per layer")
+        for l, g in enumerate(self.geoms):
+            if g.kind == "conv":
+                if (g.Hin, g.Win, g.Cin, g.KH, g.S, g.u8in) not in self._X3_CONV or g.u8in != (l == 0):
+                    raise NotImplementedError(f"fp32x: conv layer {l} geometry {(g.Hin, g.Win, g.Cin, g.KH, g.S)} "
+                                              "has no split-bf16 kernel")
+            elif l == 0 or g.Cout % 64 != 0 or g.ldx % 8 != 0:
+                raise NotImplementedError(f"fp32x: fc layer {l} needs a conv input and width % 64 == 0")
+
+    def alloc_act(self, l: int, shape) -> torch.Tensor:
+        """Output buffer of layer l: bf16 (bf16 mode), fp32 (fp32 mode, and the last layer in fp32x), or the hi plane
+        of a split-bf16 pair (fp32x, between layers)."""
+        dev = self.model.device
+        if self.x3 and l < self.L - 1:
+            return x2_alloc(shape, dev)
+        dt = torch.float32 if (self.f32 or self.x3) else torch.bfloat16
+        return torch.zeros(tuple(shape), dtype=dt, device=dev)
+
+    @property
+    def feat_dtype(self):
+        return torch.float32 if (self.f32 or self.x3) else torch.bfloat16
 
     # ------------------------------------------------------------------
     def set_paths(self, expressed: np.ndarray):
@@ -194,6 +258,14 @@ class HipPathNet:
 
     def refresh_weights(self):
         flat = self.model.store.flat
+        if self.x3:
+            for l, g in enumerate(self.geoms):
+                _lib.call("x3_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
+                          self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), int(g.u8in), self.x3_status.data_ptr(),
+                          _lib.stream())
+            if self.lstm is not None:
+                raise RuntimeError("fp32x runs the LSTM on the hybrid path")
+            return
         for l, g in enumerate(self.geoms):
             _lib.call("launch_refresh_weights_f32" if self.f32 else "launch_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
                       self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), _lib.stream())
@@ -279,6 +351,8 @@ class HipPathNet:
         if self.f32:
             _lib.check(Y, torch.float32, name="Y")
             return self._layer_fwd_f32(l, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st)
+        if self.x3:
+            return self._layer_fwd_x3(l, X, Y, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st)
         if g.kind == "conv":
             if (E * g.HWo) % 16 != 0:
                 raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
@@ -308,6 +382,8 @@ class HipPathNet:
         st = _lib.stream()
         if self.f32:
             return self._layer_bwd_f32(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
+        if self.x3:
+            return self._layer_bwd_x3(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
         if self.deterministic:
             return self._layer_bwd_det(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
         if (G.dtype == torch.bfloat16) or (dX is not None and dX.dtype == torch.bfloat16):
@@ -367,7 +443,7 @@ class HipPathNet:
         read by layer l's slab wgrad (and, for l >= 1, by layer l's MFMA dgrad), all of which round it to bf16
         for their MFMAs anyway (csrc/conv_fast.hip fast_conv_dgrad_bf16 / fast_conv_wgrad_bf16g).  Only those
         reference-geometry kernels take bf16, so every other layer / configuration keeps fp32."""
-        if self.f32 or self.deterministic or ring or not _lib.USE_FAST or self.M > 10:
+        if self.f32 or self.x3 or self.deterministic or ring or not _lib.USE_FAST or self.M > 10:
             return set()
         geo = [(g.Hin, g.Win, g.Cin, g.KH, g.S) if g.kind == "conv" else None for g in self.geoms]
         out = set()
@@ -376,6 +452,82 @@ class HipPathNet:
         if len(geo) > 2 and geo[1] == self._C2 and geo[2] == self._C3:
             out.add(1)
         return out
+
+    # -- fp32x mode (csrc/trunk_x3.hip) -------------------------------------------
+    def _x3_lo(self, t: torch.Tensor) -> int:
+        return 0 if t.dtype == torch.uint8 else x2_lo(t)
+
+    def _layer_fwd_x3(self, l, X, Y, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st):
+        g = self.geoms[l]
+        flat = self.model.store.flat
+        last = l == self.L - 1
+        _lib.check(Y, torch.float32 if last else torch.bfloat16, name="Y")
+        ylo = 0 if last else x2_lo(Y)
+        wlo = self.Wc[l][0].numel()
+        if g.kind == "conv":
+            if last:
+                raise NotImplementedError("fp32x: a conv layer cannot be the last trunk layer")
+            ok = _lib.call_fast("x3_conv_fwd", xp, self._x3_lo(X), int(g.u8in), yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
+                                flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L, self.M, g.Hin, g.Win, g.Cin,
+                                g.KH, g.KW, g.S, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
+        else:
+            ok = _lib.call_fast("x3_fc_fwd", xp, x2_lo(X), g.ldx, yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
+                                flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L, self.M, g.K, g.KP, g.Cout, P, E,
+                                T, t0, bits_rows, out_scale, st)
+        if not ok:
+            raise RuntimeError(f"fp32x: layer {l} forward shape (P={P}, E={E}, T={T}) has no split-bf16 kernel "
+                               "(fc layers take <= 32 rows per path and launch)")
+
+    def _layer_bwd_x3(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st):
+        g = self.geoms[l]
+        m = self.model
+        flat = m.store.flat
+        _lib.check(G, torch.float32, name="G")
+        if dX is not None:
+            _lib.check(dX, torch.float32, name="dX")
+        if g.kind == "conv":
+            ok = _lib.call_fast("x3_conv_wgrad", X.data_ptr(), self._x3_lo(X), int(g.u8in), G.data_ptr(),
+                                bits.data_ptr(), grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
+                                m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T,
+                                bits_rows, g.in_scale, g_scale, st)
+            if ok and dX is not None:
+                ok = _lib.call_fast("x3_conv_dgrad", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
+                                    m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin,
+                                    g.KH, g.KW, g.S, P, E, T, bits_rows, g_scale, dX.data_ptr(), st)
+            if not ok:
+                raise RuntimeError(f"fp32x: conv layer {l} backward has no split-bf16 kernel")
+            return
+        gm = self._gm_buffer_x3(bits_rows) if (dX is not None and g.Cout == 256 and g.K >= self.fc_wgrad_gm_min_k
+                                              and self.fc_wgrad_gm) else None
+        gmlo = gm.numel() // 2 if gm is not None else 0
+        ok = True
+        if dX is not None:
+            ok = _lib.call_fast("x3_fc_dgrad", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
+                                self.WcT[l][0].numel(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M,
+                                g.K, g.KP, g.Cout, P, E, T, bits_rows, g_scale, dX.data_ptr(), _lib.ptr(gm), gmlo, st)
+        if ok and gm is not None:
+            tiles = ((g.K + 127) // 128) * self.M
+            nsplit = max(1, min(m.P, -(-512 // tiles)))
+            ok = _lib.call_fast("x3_fc_wgrad_gm", X.data_ptr(), x2_lo(X), g.ldx, gm.data_ptr(), gmlo,
+                                grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
+                                self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T,
+                                bits_rows, nsplit, st)
+        elif ok:
+            ok = _lib.call_fast("x3_fc_wgrad", X.data_ptr(), x2_lo(X), g.ldx, G.data_ptr(), bits.data_ptr(),
+                                grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
+                                self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T,
+                                bits_rows, g_scale, st)
+        if not ok:
+            raise RuntimeError(f"fp32x: fc layer {l} backward has no split-bf16 kernel")
+
+    def _gm_buffer_x3(self, bits_rows: int) -> torch.Tensor:
+        """[2][M][bits_rows][256] bf16 hi/lo scratch for the masked fc gradient (allocated before graph capture)."""
+        n = 2 * self.M * bits_rows * 256
+        buf = getattr(self, "_gm", None)
+        if buf is None or buf.numel() != n:
+            buf = torch.empty(n, dtype=torch.bfloat16, device=self.model.store.flat.device)
+            self._gm = buf
+        return buf
 
     # -- fp32 mode (csrc/trunk_f32.hip) ------------------------------------------
     def _layer_fwd_f32(self, l, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st):
@@ -545,10 +697,11 @@ class HipPathNet:
         B = feat.shape[0] if b1 is None else b1
         F = feat.shape[1]
         A = m.cfg.num_actions
-        _lib.check(feat, self.act_dtype, name="feat")
+        _lib.check(feat, self.feat_dtype, name="feat")
         if not 0 <= b0 < B <= feat.shape[0]:
             raise ValueError(f"heads_fwd: sample range [{b0}, {B}) outside [0, {feat.shape[0]})")
-        _lib.call("launch_heads_fwd_sample_f32" if self.f32 else "launch_heads_fwd_sample", feat.data_ptr(), F,
+        _lib.call("launch_heads_fwd_sample_f32" if self.feat_dtype == torch.float32 else "launch_heads_fwd_sample",
+                  feat.data_ptr(), F,
                   m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"], A, B, logits.data_ptr(),
                   value.data_ptr(), actions.data_ptr(), seed & 0xFFFFFFFF, ctr.data_ptr(), t, T, int(greedy), b0,
                   _lib.stream())
@@ -557,7 +710,7 @@ class HipPathNet:
         m = self.model
         h = m.store.layout.heads[task if m.cfg.per_task_heads else 0]
         N, F = feat.shape
-        _lib.check(feat, self.act_dtype, name="feat")
+        _lib.check(feat, self.feat_dtype, name="feat")
         A = m.cfg.num_actions
         if self.deterministic:
             n = _lib.lib().heads_bwd_part_numel(N, F, A)
@@ -567,7 +720,8 @@ class HipPathNet:
                       dvalue.data_ptr(), N, A, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"],
                       grad_flat.data_ptr(), dfeat.data_ptr(), self._hpart.data_ptr(), _lib.stream())
             return
-        _lib.call("launch_heads_bwd_f32" if self.f32 else "launch_heads_bwd", feat.data_ptr(), F, dlogits.data_ptr(),
+        _lib.call("launch_heads_bwd_f32" if self.feat_dtype == torch.float32 else "launch_heads_bwd", feat.data_ptr(), F,
+                  dlogits.data_ptr(),
                   dvalue.data_ptr(), N, A, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"],
                   grad_flat.data_ptr(), dfeat.data_ptr(), _lib.stream())
 
@@ -579,7 +733,7 @@ class HipPathNet:
         x = self._prep_input(obs)
         out = None
         for l, g in enumerate(self.geoms):
-            Y = torch.empty(B, g.out_feat, dtype=self.act_dtype, device=m.device)
+            Y = self.alloc_act(l, (B, g.out_feat))
             bits, rows = self.alloc_bits(l, 1, B)
             self.layer_fwd(l, x, Y, bits, P, E, 1, 0, rows)
             x = Y

@@ -80,7 +80,7 @@ class HipEngine:
         # (grads[0] is 1.5 GB and grads[1] 0.3 GB in fp32 at the bench shape)
         bf16_grads = hp.grad_bf16_layers(self.ring)
         for l, g in enumerate(hp.geoms):
-            self.acts.append(torch.zeros(T + 1, B, g.out_feat, dtype=hp.act_dtype, device=dev))
+            self.acts.append(hp.alloc_act(l, (T + 1, B, g.out_feat)))
             b, rows = hp.alloc_bits(l, T + 1, B)
             self.bits.append(b)
             self.bits_rows.append(rows)

@@ -1,0 +1,43 @@
+"""Per-kernel summary of the steady-state window of a rocprofv3 kernel trace (bench.py --prof-window).
+
+Only dispatches between the two ``prof_window_marker_kernel`` launches count: setup, warm-up, graph capture
+and the post-window bookkeeping are excluded, so the table sums to the timed updates' GPU time.
+
+    python scripts/prof_window.py <kernel_trace.csv> <updates in the window> <title>
+"""
+import csv
+import sys
+from collections import defaultdict
+
+
+def main(path, updates, title):
+    rows = list(csv.DictReader(open(path)))
+    key = next(k for k in rows[0] if k.lower().replace("_", "") in ("kernelname", "name"))
+    t0k = next(k for k in rows[0] if "start" in k.lower())
+    t1k = next(k for k in rows[0] if "end" in k.lower())
+    rows.sort(key=lambda r: int(r[t0k]))
+    marks = [int(r[t0k]) for r in rows if "prof_window_marker" in r[key]]
+    if len(marks) < 2:
+        raise SystemExit("no prof_window markers in the trace (run bench.py --prof-window)")
+    lo, hi = marks[0], marks[-1]
+    tot = defaultdict(float)
+    calls = defaultdict(int)
+    for r in rows:
+        t = int(r[t0k])
+        if lo < t < hi and "prof_window_marker" not in r[key]:
+            name = r[key].split("(")[0].replace("void ", "")
+            tot[name] += int(r[t1k]) - t
+            calls[name] += 1
+    total = sum(tot.values())
+    out = [f"# {title}", "", f"source: `{path}` (rocprofv3 --kernel-trace); {updates} timed updates between the "
+           f"bench.py --prof-window markers; wall between markers {(hi - lo) / 1e6 / updates:.3f} ms per update", "",
+           "| kernel | calls/update | avg us | ms/update | % |", "|---|---:|---:|---:|---:|"]
+    for name in sorted(tot, key=lambda n: -tot[n])[:30]:
+        out.append(f"| `{name[:70]}` | {calls[name] / updates:.1f} | {tot[name] / calls[name] / 1e3:.1f} | "
+                   f"{tot[name] / 1e6 / updates:.3f} | {100 * tot[name] / total:.1f} |")
+    out.append(f"| **total GPU kernel time** | | | **{total / 1e6 / updates:.2f}** | 100 |")
+    return "\n".join(out) + "\n"
+
+
+if __name__ == "__main__":
+    print(main(sys.argv[1], float(sys.argv[2]), sys.argv[3]))

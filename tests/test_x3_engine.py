@@ -1,0 +1,170 @@
+"""fp32x engine mode (split-bf16 operands, csrc/trunk_x3.hip) on an MI355X.
+
+The reference computes in fp32 (TF default dtype, game_ac_network.py:89-110).  The fp32x mode keeps every activation
+as a (hi, lo) bf16 pair and every product as three bf16 MFMAs; it must match a PLAIN fp32 PyTorch oracle to <= 2e-5
+relative per layer (forward and whole-update gradient), and a gradient wiring error of 2 % in a single module must
+be detected by the same comparison.
+"""
+import numpy as np
+import pytest
+import torch
+
+from pathnet_gym_amd.algo.a2c_math import a2c_loss, nstep_returns
+from pathnet_gym_amd.algo.ga import get_geopath
+from pathnet_gym_amd.config import LayerSpec, PathNetConfig, preset
+from pathnet_gym_amd.models.acnet import ACPathNet
+from pathnet_gym_amd.models.pathnet import ParamStore, heads_ref, trunk_forward_ref
+from pathnet_gym_amd.ops.pathnet_ops import x2_alloc, x2_lo, x2_value
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+X3_LAYER_TOL = 2e-5
+
+
+def rel(a, b):
+    a = a.float().flatten()
+    b = b.float().flatten()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def masks_with_edges(P, L, M, N, seed=0):
+    rng = np.random.RandomState(seed)
+    m = np.stack([get_geopath(L, M, N, rng) for _ in range(P)])
+    m[0, 1, :] = 0          # empty layer
+    m[1, :, :] = 1          # every module active: 5 column tiles -> two LDS passes per layer
+    m[2, 0, :] = 0
+    m[2, 0, M - 1] = 1      # one (odd) module
+    return m
+
+
+def pixel_cfg(scale="M"):
+    return PathNetConfig(L=5, M=10, N=4, input_shape=(160, 120, 4),
+                         layers=[LayerSpec("conv", 8, 8, 4), LayerSpec("conv", 8, 4, 2), LayerSpec("conv", 8, 3, 1),
+                                 LayerSpec("fc", 256), LayerSpec("fc", 256)],
+                         trunk_scale=scale, num_actions=6)
+
+
+def test_x2_pair_helpers(hip_lib):
+    t = x2_alloc((3, 5), DEV)
+    assert x2_lo(t) == 15 and x2_lo(t[1]) == 15
+    v = torch.randn(3, 5, device=DEV)
+    hi = v.to(torch.bfloat16)
+    t.copy_(hi)
+    lo = torch.empty(0, dtype=torch.bfloat16, device=DEV).set_(t.untyped_storage(), 15, (3, 5), (5, 1))
+    lo.copy_((v - hi.float()).to(torch.bfloat16))
+    assert rel(x2_value(t), v) < 1e-5
+    with pytest.raises(ValueError):
+        x2_lo(torch.zeros(4, dtype=torch.bfloat16, device=DEV)[:1].expand(4))
+
+
+def test_x3_weight_pairs_reconstruct_fp32(hip_lib):
+    cfg = pixel_cfg()
+    m = ACPathNet(cfg, 2, DEV, "hip", seed=5, compute_dtype="fp32x")
+    hp = m.hip
+    st = m.store
+    flat = st.flat.detach()
+    for l, g in enumerate(hp.geoms):
+        W = flat[g.w_off:g.w_off + hp.M * g.chunk].view(hp.M, g.chunk)[:, :g.K * g.Cout].view(hp.M, g.K, g.Cout)
+        pair = hp.Wc[l].float()
+        rec = (pair[0] + pair[1])[:, :, :g.K].transpose(1, 2)
+        # bf16 pair: 16 significant bits (~2.6e-6 rms); fp16 pair of W * 2^8: 22 bits
+        tol = 1e-7 if g.u8in else 4e-6
+        if g.u8in:
+            rec = rec / 256.0
+        assert rel(rec, W) < tol, (l, rel(rec, W))
+        if hp.WcT[l] is not None:
+            pt = hp.WcT[l].float()
+            assert rel((pt[0] + pt[1])[:, :g.K], W) < tol
+    assert int(hp.x3_status.item()) == 0
+
+
+def test_x3_trunk_forward_matches_plain_fp32_oracle(hip_lib):
+    cfg = pixel_cfg()
+    P, E = 4, 16
+    m = ACPathNet(cfg, P, DEV, "hip", seed=3, compute_dtype="fp32x")
+    m.set_paths(masks_with_edges(P, cfg.L, cfg.M, cfg.N))
+    assert m.hip.x3 and m.hip.Wc[1].shape[0] == 2
+    g = torch.Generator(device="cpu").manual_seed(0)
+    obs = torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+    feat = m.hip.trunk(obs, E)
+    with torch.no_grad():
+        ref = trunk_forward_ref(m.store, obs.float() / 255.0, m.mask.repeat_interleave(E, 0))
+    errs = []
+    for p in range(P):
+        sl = slice(p * E, (p + 1) * E)
+        if ref[sl].norm() == 0:
+            assert feat[sl].norm() == 0, p
+            continue
+        errs.append(rel(feat[sl], ref[sl]))
+    print("fp32x trunk forward vs fp32 oracle, per path:", [f"{e:.2e}" for e in errs])
+    assert max(errs) < X3_LAYER_TOL, errs
+
+
+def _oracle_grad(tr, eng):
+    """Autograd of the A2C loss over the engine's stored rollout, plain fp32."""
+    cfg = tr.cfg
+    T, B = eng.T, eng.B
+    a2c = cfg.a2c
+    flat = tr.model.store.flat.detach().clone().requires_grad_(True)
+    st = ParamStore(cfg.net, DEV, flat=flat)
+    x = eng.obs_stacks().reshape((T + 1) * B, 160, 120, 4).float() / 255.0
+    mask = tr.model.mask.repeat_interleave(eng.E, 0).repeat(T + 1, 1, 1)
+    feat = trunk_forward_ref(st, x, mask)
+    logits, values = heads_ref(st, feat)
+    assert rel(logits[:T * B], eng.logits[:T].reshape(-1, eng.A)) < 1e-5
+    assert rel(values, eng.values[:T + 1].reshape(-1)) < 1e-5
+    R, adv = nstep_returns(eng.rewards, eng.values[:T], eng.dones.bool(), eng.values[T], a2c.gamma,
+                           a2c.gae_lambda, a2c.reward_clip)
+    loss, _, _, _ = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(), R.reshape(-1),
+                             adv.reshape(-1), a2c.entropy_beta, a2c.value_coef,
+                             torch.full((T * B,), eng.weight, device=DEV))
+    loss.backward()
+    return flat.grad
+
+
+def layer_errors(tr, g_hip, g_ref):
+    parts = {}
+    for s in tr.model.store.layout.segments:
+        key = s.layer if s.layer >= 0 else s.name.split(".")[0]
+        parts.setdefault(key, []).append((g_hip[s.offset:s.offset + s.numel], g_ref[s.offset:s.offset + s.numel]))
+    return {k: rel(torch.cat([a for a, _ in v]), torch.cat([b for _, b in v])) for k, v in parts.items()}
+
+
+@pytest.fixture(scope="module")
+def x3_rollout(hip_lib):
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 4
+    cfg.use_graph = False
+    cfg.compute_dtype = "fp32x"
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng = tr.engine
+    assert tr.compute_dtype == "fp32x" and eng.acts[-1].dtype == torch.float32 and not eng.ring
+    tr.env.max_episode_steps = 5
+    tr.update()
+    tr.model.set_paths(masks_with_edges(3, cfg.net.L, cfg.net.M, cfg.net.N, seed=2))
+    eng._rollout_backward_body()
+    torch.cuda.synchronize()
+    return tr, eng, _oracle_grad(tr, eng), eng.grad_flat.clone()
+
+
+def test_x3_engine_gradient_vs_plain_fp32_oracle(x3_rollout):
+    tr, eng, g_ref, g_hip = x3_rollout
+    err = layer_errors(tr, g_hip, g_ref)
+    print("fp32x engine vs fp32 oracle, per layer:", {k: f"{v:.2e}" for k, v in err.items()})
+    for k, v in err.items():
+        assert v < X3_LAYER_TOL, (k, v)
+
+
+def test_x3_gradient_check_detects_a_two_percent_module_error(x3_rollout):
+    """Negative control: one active module's weight gradient scaled by 1.02 must fail the per-layer budget."""
+    tr, eng, g_ref, g_hip = x3_rollout
+    hp = tr.model.hip
+    for l, g in enumerate(hp.geoms):
+        act = np.nonzero(tr.model.mask[0, l].cpu().numpy() > 0.5)[0]
+        j = int(act[0]) if len(act) else int(np.nonzero(tr.model.mask[1, l].cpu().numpy() > 0.5)[0][0])
+        bad = g_hip.clone()
+        seg = slice(g.w_off + j * g.chunk, g.w_off + j * g.chunk + g.K * g.Cout)
+        bad[seg] *= 1.02
+        err = layer_errors(tr, bad, g_ref)[l]
+        assert err > X3_LAYER_TOL, (l, err)
