@@ -17,6 +17,19 @@ unit as the reference's 63 global steps/s (BASELINE.md, aliencentipede.txt);
 the synthetic Pong repeats each action for `frameskip`=4 emulator sub-frames
 that are NOT counted.  Weak scaling: P paths per GPU, fixed.
 
+Precision: the headline runs the fp32x engine (``--dtype fp32x``, reported as
+"dtype": "fp32"): the reference trains in fp32 (game_ac_network.py:89-110) and
+fp32x matches a plain fp32 oracle to <= 2e-5 per layer (fp16 / bf16 hi+lo
+operand pairs, three MFMAs per product, csrc/trunk_x3.hip).  The bf16 engine
+is timed on the same config as ``value_bf16``.
+
+Steady state: every env's first episode starts at a random late score
+(PongVec.stagger_scores), so fitness windows fill and tournaments fire inside
+the timed window (``generations_in_timed_window``).  After it, one
+generations-to-solve seed runs on a fresh trainer under a hard wall cap
+(``generations_to_solve_in_run``); ``generations_to_solve`` lists every
+committed multi-seed record of exactly this config (scripts/solve.py).
+
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 """
@@ -24,6 +37,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -77,6 +91,85 @@ def solve_records(key: dict, n_gpus: int):
             "solved_seeds": len(gens), "seeds": len(runs), "runs": runs, "config": key}
 
 
+def build_trainer(args, ctx, dtype: str, stagger: bool):
+    from pathnet_gym_amd.config import preset
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset(args.preset)
+    if args.env:
+        cfg.env = args.env
+        cfg.tasks = [args.env] + [t for t in cfg.tasks if t != args.env]
+    cfg.paths = args.paths
+    cfg.envs_per_path = args.envs
+    cfg.a2c.t_max = args.tmax
+    cfg.backend = args.backend
+    cfg.use_graph = not args.no_graph
+    cfg.frame_ring = args.ring
+    cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
+    cfg.ga.backend = args.ga_backend
+    cfg.compute_dtype = dtype
+    cfg.deterministic = args.deterministic
+    cfg.rollout_groups = args.rollout_groups
+    tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
+    if stagger and hasattr(tr.env, "stagger_scores"):
+        tr.env.stagger_scores()
+    return cfg, tr
+
+
+def timed_window(tr, ctx, steps: int, warmup: int, markers: bool = False):
+    """W untimed updates, then EXACTLY K updates between barrier + synchronize on both sides; max over ranks."""
+    import torch
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        ctx.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    for _ in range(warmup):
+        tr.update()
+    tr.flush()
+    sync()
+    gen0 = tr.pop.generation
+    step0 = tr.global_step
+    if markers:
+        from pathnet_gym_amd.ops import _lib as _plib
+        _plib.call("launch_prof_marker", 1, _plib.stream())
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.update()
+    tr.flush()                               # drain the pipelined host bookkeeping of the last update
+    if markers:
+        _plib.call("launch_prof_marker", 2, _plib.stream())
+    sync()
+    dt = ctx.max_scalar(time.perf_counter() - t0)
+    return dt, tr.global_step - step0, tr.pop.generation - gen0   # whole-job agent steps (fused all-reduce)
+
+
+def in_run_solve(args, ctx, dtype: str, cap_s: float) -> dict:
+    """One seed of generations-to-solve on a FRESH trainer of the bench config, observed inside this run (hard wall
+    cap; scripts/solve.py is the multi-seed version): the first tournament whose winner fitness reaches the task's
+    reward threshold."""
+    from pathnet_gym_amd.envs.registry import reward_threshold
+    cfg, tr = build_trainer(args, ctx, dtype, stagger=False)
+    thr = reward_threshold(cfg.tasks[0])
+    t0 = time.time()
+    best = -math.inf
+    out = {"seed": cfg.seed, "threshold": thr, "cap_s": cap_s, "solved": False}
+    while time.time() - t0 < cap_s:
+        st = tr.update()
+        if st.tournaments:
+            best = max(best, st.best_winner)
+            if st.best_winner >= thr:
+                out.update(solved=True, generations=tr.pop.generation, frames=tr.global_step,
+                           seconds=round(time.time() - t0, 1))
+                break
+    tr.flush()
+    out.update(best_winner=best if best > -math.inf else None, generations_run=tr.pop.generation,
+               frames_run=tr.global_step, wall_s=round(time.time() - t0, 1))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -92,8 +185,10 @@ def main():
     ap.add_argument("--env", default=None, help="train this task of the preset's suite instead of its first task")
     ap.add_argument("--kernel-opt", action="append", default=[],
                     help="kernel switch NAME=VALUE (fast_conv_set_*), for A/B measurements")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x"],
-                    help="HIP engine compute dtype (fp32: the reference's precision, csrc/trunk_f32.hip)")
+    ap.add_argument("--dtype", default="fp32x", choices=["bf16", "fp32", "fp32x"],
+                    help="HIP engine compute dtype.  fp32x (headline): fp32-accurate split operands (fp16 / bf16 "
+                         "hi+lo pairs, 3 MFMAs per product, <= 2e-5 per layer vs a plain fp32 oracle, "
+                         "csrc/trunk_x3.hip); fp32: fp32 MFMA operands (csrc/trunk_f32.hip); bf16: bf16 operands")
     ap.add_argument("--deterministic", action="store_true", help="fixed-order gradient reductions (bit-reproducible)")
     ap.add_argument("--rollout-groups", type=int, default=0,
                     help="path groups stepped on their own streams in the rollout (0 = auto, 1 = one stream)")
@@ -102,18 +197,21 @@ def main():
     ap.add_argument("--concurrent", type=int, default=None,
                     help="concurrent tournaments (default paths/16 -- per rank count, NOT scaled by the world size, so "
                          "the GA takes the same number of tournaments per update on 1, 2, 4 and 8 GPUs)")
+    ap.add_argument("--no-stagger", action="store_true",
+                    help="start every env at 0-0 (default: random late scores, so tournaments fire inside the window)")
+    ap.add_argument("--solve-seconds", type=float, default=None,
+                    help="after the timed window, run one generations-to-solve seed on a fresh trainer for at most "
+                         "this long (default 330 s on one GPU, 0 = off; multi-GPU runs skip it)")
+    ap.add_argument("--compare-bf16", type=int, default=None,
+                    help="also time the bf16 engine on the same config (default: on for one GPU)")
     ap.add_argument("--prof-window", action="store_true",
                     help="launch marker kernels around the timed updates (scripts/prof_window.py summarises the "
                          "rocprofv3 kernel trace between them)")
     args = ap.parse_args()
 
-    import numpy as np
     import torch
-    import torch.distributed as dist
 
-    from pathnet_gym_amd.config import preset
     from pathnet_gym_amd.parallel.dist import init_distributed
-    from pathnet_gym_amd.algo.trainer import PathNetTrainer
 
     if args.backend == "hip":
         from pathnet_gym_amd import _build
@@ -126,88 +224,68 @@ def main():
             lib = _lib.lib()
             (getattr(lib, k) if hasattr(lib, k) and "_set_" in k else getattr(lib, "fast_conv_set_" + k))(int(v))
     ctx = init_distributed()
-    cfg = preset(args.preset)
-    if args.env:
-        cfg.env = args.env
-        cfg.tasks = [args.env] + [t for t in cfg.tasks if t != args.env]
-    cfg.paths = args.paths
-    cfg.envs_per_path = args.envs
-    cfg.a2c.t_max = args.tmax
-    cfg.backend = args.backend
-    cfg.use_graph = not args.no_graph
-    cfg.frame_ring = args.ring
-    cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
-    cfg.ga.backend = args.ga_backend
-    cfg.compute_dtype = args.dtype
-    cfg.deterministic = args.deterministic
-    cfg.rollout_groups = args.rollout_groups
-    tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
-
-    def sync():
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-        ctx.barrier()
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        tr.update()
-    tr.flush()
-    sync()
-    gen0 = tr.pop.generation
-    step0 = tr.global_step
-    if args.prof_window:
-        from pathnet_gym_amd.ops import _lib as _plib
-        _plib.call("launch_prof_marker", 1, _plib.stream())
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tr.update()
-    tr.flush()                               # drain the pipelined host bookkeeping of the last update
-    if args.prof_window:
-        _plib.call("launch_prof_marker", 2, _plib.stream())
-    sync()
-    dt = time.perf_counter() - t0
-    dt = ctx.max_scalar(dt)
-    frames = tr.global_step - step0          # whole-job agent steps (all ranks, from the fused all-reduce)
+    single = ctx.world == 1 and not args.prof_window
+    solve_s = args.solve_seconds if args.solve_seconds is not None else (330.0 if single else 0.0)
+    compare = args.compare_bf16 if args.compare_bf16 is not None else int(single and args.dtype != "bf16")
+    stagger = not args.no_stagger
+    cfg, tr = build_trainer(args, ctx, args.dtype, stagger)
+    dt, frames, gens = timed_window(tr, ctx, args.steps, args.warmup, markers=args.prof_window)
     value = frames / dt
+    rec = {
+        "metric": "env_frames_per_sec_whole_node_pong_pathnet",
+        "value": round(value, 1),
+        "unit": "env frames/s (agent steps, all GPUs)",
+        "n_gpus": ctx.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_STEPS_PER_SEC, 1),
+        "dtype": "fp32" if tr.compute_dtype == "fp32x" else tr.compute_dtype,
+        "compute": {"fp32x": "fp32-accurate split operands: fp16 hi+lo pairs (forward), bf16 hi+lo pairs (gradients), "
+                             "3 MFMAs per product, fp32 accumulation and master weights; <= 2e-5 relative per layer "
+                             "vs a plain fp32 PyTorch oracle (tests/test_x3_engine.py)",
+                    "fp32": "fp32 MFMA operands (v_mfma_f32_16x16x4_f32)",
+                    "bf16": "bf16/fp16 MFMA operands, fp32 accumulation (reduced precision)"}[tr.compute_dtype],
+        "data": (f"synthetic: on-device Atari-style {cfg.tasks[0]} simulator (210x160 RGB -> gray 160x120 x4 "
+                 "stack), random-init weights") if len(cfg.net.input_shape) == 3 else
+                f"synthetic: on-device {cfg.tasks[0]}, random-init weights",
+        "config": {
+            "model": f"PathNet {cfg.net.L} layers ("
+                     + " + ".join(f"{sp.kind} {sp.out}" + (f" {sp.kernel}x{sp.kernel}/{sp.stride}"
+                                                             if sp.kind == "conv" else "")
+                                  for sp in cfg.net.layers)
+                     + f") x M={cfg.net.M} modules, N={cfg.net.N}, A2C T={cfg.a2c.t_max}, B={cfg.ga.B} tournament",
+            "global_batch": cfg.paths * cfg.envs_per_path * ctx.world * cfg.a2c.t_max,
+            "seq_len": cfg.a2c.t_max,
+            "parallelism": f"dp{ctx.world} (population split: {cfg.paths} paths x {cfg.envs_per_path} envs per GPU)",
+            "backend": args.backend,
+            "hipgraph": cfg.use_graph,
+            "frame_ring": bool(getattr(tr.engine, "ring", False)),
+            "rollout_groups": int(getattr(tr.engine, "groups", 1)),
+            "ga": f"{cfg.ga.backend} (B={cfg.ga.B}, {cfg.ga.concurrent_tournaments} concurrent tournaments, "
+                  f"fitness {cfg.ga.fitness} over {cfg.ga.window_for(cfg.envs_per_path)} episodes)",
+            "pipelined": bool(tr.pipelined),
+            "deterministic": bool(getattr(tr.model.hip, "deterministic", False)),
+            "episode_stagger": stagger,
+        },
+        "generations_in_timed_window": int(gens),
+    }
+    del tr
+    if compare:
+        _, trb = build_trainer(args, ctx, "bf16", stagger)
+        dtb, fb, _ = timed_window(trb, ctx, args.steps, args.warmup)
+        rec["value_bf16"] = round(fb / dtb, 1)
+        rec["ms_per_step_bf16"] = round(dtb / args.steps * 1e3, 3)
+        del trb
+    torch.cuda.empty_cache() if torch.cuda.is_available() else None
+    # the metric's second half: one seed observed in this run, plus every committed multi-seed record of exactly
+    # this config (scripts/solve.py --out profiles/solve/*.json)
+    if solve_s > 0:
+        rec["generations_to_solve_in_run"] = in_run_solve(args, ctx, args.dtype, solve_s)
     if ctx.is_main:
-        B = cfg.paths * cfg.envs_per_path
-        rec = {
-            "metric": "env_frames_per_sec_whole_node_pong_pathnet",
-            "value": round(value, 1),
-            "unit": "env frames/s (agent steps, all GPUs)",
-            "n_gpus": ctx.world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_STEPS_PER_SEC, 1),
-            "dtype": tr.compute_dtype,
-            "data": (f"synthetic: on-device Atari-style {cfg.tasks[0]} simulator (210x160 RGB -> gray 160x120 x4 "
-                     "stack), random-init weights") if len(cfg.net.input_shape) == 3 else
-                    f"synthetic: on-device {cfg.tasks[0]}, random-init weights",
-            "config": {
-                "model": f"PathNet {cfg.net.L} layers ("
-                         + " + ".join(f"{sp.kind} {sp.out}" + (f" {sp.kernel}x{sp.kernel}/{sp.stride}"
-                                                                 if sp.kind == "conv" else "")
-                                      for sp in cfg.net.layers)
-                         + f") x M={cfg.net.M} modules, N={cfg.net.N}, A2C T={cfg.a2c.t_max}, B={cfg.ga.B} tournament",
-                "global_batch": B * ctx.world * cfg.a2c.t_max,
-                "seq_len": cfg.a2c.t_max,
-                "parallelism": f"dp{ctx.world} (population split: {cfg.paths} paths x {cfg.envs_per_path} envs per GPU)",
-                "backend": args.backend,
-                "hipgraph": cfg.use_graph,
-                "frame_ring": bool(getattr(tr.engine, "ring", False)),
-                "rollout_groups": int(getattr(tr.engine, "groups", 1)),
-                "ga": f"{cfg.ga.backend} (B={cfg.ga.B}, {cfg.ga.concurrent_tournaments} concurrent tournaments)",
-                "pipelined": bool(tr.pipelined),
-                "deterministic": bool(getattr(tr.model.hip, "deterministic", False)),
-            },
-            "generations_in_timed_window": int(tr.pop.generation - gen0),
-            # the metric's second half is measured by scripts/solve.py (minutes of training, not a bench window)
-            "generations_to_solve": solve_records(solve_key(cfg, args.preset), ctx.world),
-        }
+        rec["generations_to_solve"] = solve_records(solve_key(cfg, args.preset), ctx.world)
         print(json.dumps(rec), flush=True)
     ctx.destroy()
 

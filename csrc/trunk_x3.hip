@@ -89,18 +89,50 @@ DEVI void split8(const float (&v)[8], s8v& hi, s8v& lo) {
   __builtin_memcpy(&hi, h, 16);
   __builtin_memcpy(&lo, l, 16);
 }
-// hi/lo pair of one value into two planes
-DEVI void st_x2(bf16_t* Y, long ylo, long i, float v) {
-  const bf16_t h = f2bf(v);
-  Y[i] = h;
-  Y[i + ylo] = f2bf(v - bf2f(h));
+DEVI void split8h(const float (&v)[8], s8v& hi, s8v& lo) {
+  _Float16 h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = (_Float16)v[j];
+    l[j] = (_Float16)(v[j] - (float)h[j]);
+  }
+  __builtin_memcpy(&hi, h, 16);
+  __builtin_memcpy(&lo, l, 16);
 }
-DEVI float ld_x2(const bf16_t* Y, long ylo, long i) { return bf2f(Y[i]) + bf2f(Y[i + ylo]); }
+DEVI uint16_t f2h(float v) { return __builtin_bit_cast(uint16_t, (_Float16)v); }
+DEVI float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+// An activation between layers is stored in FOUR 16-bit planes, ylo elements apart: the fp16 pair (planes 0, 1:
+// 22 significant bits, read by the next layer's forward) and the bf16 pair (planes 2, 3: 16 bits, exponent range
+// of the output gradients it meets in the weight-gradient MFMAs).
+DEVI void st_x4(uint16_t* Y, long ylo, long i, float v) {
+  const uint16_t h = f2h(v);
+  Y[i] = h;
+  Y[i + ylo] = f2h(v - h2f(h));
+  const bf16_t b = f2bf(v);
+  Y[i + 2 * ylo] = b;
+  Y[i + 3 * ylo] = f2bf(v - bf2f(b));
+}
+DEVI float ld_x4(const uint16_t* Y, long ylo, long i) { return h2f(Y[i]) + h2f(Y[i + ylo]); }
+DEVI void st8_x4(uint16_t* Y, long ylo, const float (&o)[8]) {
+  s8v a, b;
+  split8h(o, a, b);
+  *reinterpret_cast<s8v*>(Y) = a;
+  *reinterpret_cast<s8v*>(Y + ylo) = b;
+  split8(o, a, b);
+  *reinterpret_cast<s8v*>(Y + 2 * ylo) = a;
+  *reinterpret_cast<s8v*>(Y + 3 * ylo) = b;
+}
 // a*b over one 32-wide k-step from hi/lo operands: the two small cross terms first
 DEVI f4v mma3(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
   c = mfma16(al, bh, c);
   c = mfma16(ah, bl, c);
   return mfma16(ah, bh, c);
+}
+// the same on fp16 pairs (forward: activations x weights * 2^8)
+DEVI f4v mma3h(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
+  c = mfma16_f16(al, bh, c);
+  c = mfma16_f16(ah, bl, c);
+  return mfma16_f16(ah, bh, c);
 }
 // exact operand a (uint8 pixels in bf16) against a hi/lo pair b
 DEVI f4v mma2(const s8v& a, const s8v& bh, const s8v& bl, f4v c) {
@@ -123,7 +155,7 @@ DEVI s8v u8x8_to_f16(uint2 v) {
 // Wh: [2][M][8][KP] fp16 (hi plane, lo plane at +wlo).  Y: two bf16 planes (lo at +ylo).
 // ===========================================================================
 template <class G, int NT>
-__global__ __launch_bounds__(256, 2) void conv1_fwd_x2(const uint8_t* __restrict__ X, bf16_t* __restrict__ Y,
+__global__ __launch_bounds__(256, 2) void conv1_fwd_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                       long ylo, uint8_t* __restrict__ bits,
                                                       const uint16_t* __restrict__ Wh, long wlo,
                                                       const float* __restrict__ flat, long bias_off, int chunk,
@@ -265,8 +297,8 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x2(const uint8_t* __restrict
             for (int r = 0; r < 4; ++r) {
               const long o = (grow4 + r) * 8 + ch;
               float y = sum[r] * out_scale;
-              if (pass > 0) y += ld_x2(Y, ylo, o);
-              st_x2(Y, ylo, o, y);
+              if (pass > 0) y += ld_x4(Y, ylo, o);
+              st_x4(Y, ylo, o, y);
             }
           }
         }
@@ -295,18 +327,18 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x2(const uint8_t* __restrict
 // tile's A fragments (both planes) are loaded while this tile's MFMAs run.
 // ===========================================================================
 template <class G, int NT>
-__global__ __launch_bounds__(256, 2) void conv_fwd_x3(const bf16_t* __restrict__ X, long xlo, bf16_t* __restrict__ Y,
-                                                     long ylo, uint8_t* __restrict__ bits,
-                                                     const bf16_t* __restrict__ Wc, long wlo,
+__global__ __launch_bounds__(256, 2) void conv_fwd_x3(const uint16_t* __restrict__ X, long xlo,
+                                                     uint16_t* __restrict__ Y, long ylo, uint8_t* __restrict__ bits,
+                                                     const uint16_t* __restrict__ Wc, long wlo,
                                                      const float* __restrict__ flat, long bias_off, int chunk,
                                                      const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
                                                      int layer, int L, int M, int P, int E, int T, int t0,
-                                                     long bits_rows, float out_scale) {
+                                                     long bits_rows, float in_scale, float out_scale) {
   static_assert(!G::U8, "bf16-activation layers");
   constexpr int KPs = G::KP + 8;
   constexpr int NK = G::KP / 32;
   constexpr int FF_ROWS = NT * 128;
-  __shared__ __attribute__((aligned(16))) bf16_t Ws[2][X3_NCX * 16 * KPs];
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[2][X3_NCX * 16 * KPs];
   __shared__ float bias_s[X3_NCX * 16];
   __shared__ int mods[X3_MAXM];
   const int p = blockIdx.y;
@@ -393,8 +425,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_x3(const bf16_t* __restrict__
           for (int ct = 0; ct < NC; ++ct) {
             const s8v bh = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
             const s8v bl = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
-            acc[0][ct] = mma3(ch_[0][kk], cl_[0][kk], bh, bl, acc[0][ct]);
-            acc[1][ct] = mma3(ch_[1][kk], cl_[1][kk], bh, bl, acc[1][ct]);
+            acc[0][ct] = mma3h(ch_[0][kk], cl_[0][kk], bh, bl, acc[0][ct]);
+            acc[1][ct] = mma3h(ch_[1][kk], cl_[1][kk], bh, bl, acc[1][ct]);
           }
         }
 #pragma unroll
@@ -427,8 +459,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_x3(const bf16_t* __restrict__
             for (int r = 0; r < 4; ++r) {
               const long o = (grow4 + r) * 8 + ch;
               float y = sum[r] * out_scale;
-              if (pass > 0) y += ld_x2(Y, ylo, o);
-              st_x2(Y, ylo, o, y);
+              if (pass > 0) y += ld_x4(Y, ylo, o);
+              st_x4(Y, ylo, o, y);
             }
           }
         }
@@ -1081,13 +1113,13 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
 // OF32: the last layer writes fp32 (heads input); otherwise two bf16 planes.  grid = (1, Cout/64, P).
 // ===========================================================================
 template <int RT, int D, int NKS, bool OF32>
-__global__ __launch_bounds__(256) void fc_fwd_x3(const bf16_t* __restrict__ X, long xlo, int ldx,
+__global__ __launch_bounds__(256) void fc_fwd_x3(const uint16_t* __restrict__ X, long xlo, int ldx,
                                                  void* __restrict__ Yv, long ylo, uint16_t* __restrict__ bits,
-                                                 const bf16_t* __restrict__ Wc, long wlo,
+                                                 const uint16_t* __restrict__ Wc, long wlo,
                                                  const float* __restrict__ flat, long bias_off, int chunk,
                                                  const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
                                                  int layer, int L, int M, int K, int KP, int Cout, int P, int E, int T,
-                                                 int t0, long bits_rows, float out_scale) {
+                                                 int t0, long bits_rows, float in_scale, float out_scale) {
   __shared__ float part[4][32][64 + 1];
   const int p = blockIdx.z;
   const int cnt = act_cnt[p * L + layer];
@@ -1121,7 +1153,7 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const bf16_t* __restrict__ X, l
     }
   for (int a = w; a < cnt; a += 4) {
     const int mod = act_idx[(p * L + layer) * M + a];
-    const bf16_t* Wm = Wc + (long)mod * Cout * KP + (long)(col0 + c16) * KP + 8 * grp;
+    const uint16_t* Wm = Wc + (long)mod * Cout * KP + (long)(col0 + c16) * KP + 8 * grp;
     f4v acc[RT][4];
 #pragma unroll
     for (int i = 0; i < RT; ++i)
@@ -1154,7 +1186,7 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const bf16_t* __restrict__ X, l
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int i = 0; i < RT; ++i) acc[i][j] = mma3(ah[d][i], al[d][i], bh[d][j], bl[d][j], acc[i][j]);
+        for (int i = 0; i < RT; ++i) acc[i][j] = mma3h(ah[d][i], al[d][i], bh[d][j], bl[d][j], acc[i][j]);
     };
     const int nks = NKS > 0 ? NKS : KP / 32;
 #pragma unroll
@@ -1185,7 +1217,7 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const bf16_t* __restrict__ X, l
       for (int i = 0; i < RT; ++i) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float v = acc[i][j][r] + bb;
+          const float v = acc[i][j][r] * in_scale + bb;
           const bool pos = v > 0.f;
           sum[i][j][r] += pos ? v : 0.f;
           const uint64_t bal = __ballot(pos);
@@ -1217,11 +1249,7 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const bf16_t* __restrict__ X, l
       *reinterpret_cast<float4*>(Y) = make_float4(o[0], o[1], o[2], o[3]);
       *reinterpret_cast<float4*>(Y + 4) = make_float4(o[4], o[5], o[6], o[7]);
     } else {
-      bf16_t* Y = reinterpret_cast<bf16_t*>(Yv) + sg * Cout + col0 + oc;
-      s8v hi, lo;
-      split8(o, hi, lo);
-      *reinterpret_cast<s8v*>(Y) = hi;
-      *reinterpret_cast<s8v*>(Y + ylo) = lo;
+      st8_x4(reinterpret_cast<uint16_t*>(Yv) + sg * Cout + col0 + oc, ylo, o);
     }
   }
 }
@@ -1615,9 +1643,10 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
   }
 }
 
-// hi/lo operand copies of one layer's weights: Wc [2][M][Cout][KP] (k contiguous, zero padded) and optionally
-// WcT [2][M][KP][Cout].  f16: fp16 pair of W * 2^X3_W0_SHIFT (uint8 first layer); *status = 1 when a scaled weight
-// leaves the fp16 range (checked by the host, runtime/guard.py)
+// hi/lo operand copies of one layer's weights: Wc [2][M][Cout][KP] (forward B operand, k contiguous, zero padded):
+// the fp16 pair of W * 2^X3_W0_SHIFT (f16 != 0) or the bf16 pair of W; optionally WcT [2][M][KP][Cout] (the fc input
+// gradient's B operand): always the bf16 pair, as the output gradients it meets.  *status = 1 when a scaled weight
+// leaves the fp16 range (the host checks it, HipPathNet.check_x3_status)
 __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict__ flat, long w_off, int chunk, int K,
                                                          int KP, int Cout, int M, uint16_t* __restrict__ Wc,
                                                          uint16_t* __restrict__ WcT, int f16,
@@ -1628,24 +1657,21 @@ __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict
     const int rem = (int)(i - (long)j * KP * Cout);
     const int k = rem / Cout, c = rem - k * Cout;
     const float v = k < K ? flat[w_off + (long)j * chunk + (long)k * Cout + c] : 0.f;
-    uint16_t hi, lo;
+    const bf16_t bh = f2bf(v);
+    const bf16_t bl = f2bf(v - bf2f(bh));
+    uint16_t hi = bh, lo = bl;
     if (f16) {
       const float x = v * (float)(1 << X3_W0_SHIFT);
-      const _Float16 h = (_Float16)x;
-      const _Float16 lw = (_Float16)(x - (float)h);
-      hi = __builtin_bit_cast(uint16_t, h);
-      lo = __builtin_bit_cast(uint16_t, lw);
+      hi = f2h(x);
+      lo = f2h(x - h2f(hi));
       if (!(fabsf(x) < 32768.f) && status) *status = 1u;
-    } else {
-      hi = f2bf(v);
-      lo = f2bf(v - bf2f(hi));
     }
     const long wi = ((long)j * Cout + c) * KP + k;
     Wc[wi] = hi;
     Wc[n + wi] = lo;
     if (WcT) {
-      WcT[i] = hi;
-      WcT[n + i] = lo;
+      WcT[i] = bh;
+      WcT[n + i] = bl;
     }
   }
 }
@@ -1689,7 +1715,7 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
     const float isc = is / (float)(1 << X3_W0_SHIFT);
 #define C1L(NT_)                                                                                                \
   conv1_fwd_x2<C1, NT_><<<dim3((unsigned)((rows + NT_ * 128 - 1) / (NT_ * 128)), P), 256, 0, st>>>(             \
-      (const uint8_t*)X, (bf16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, \
+      (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, \
       layer, L, M, P, E, T, t0, br, isc, os)
     if (X3_FWD_NT >= 8) C1L(8); else C1L(4);
 #undef C1L
@@ -1701,8 +1727,8 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
     if ((E * Gx::HOWO) % 16) return -2;                                                                           \
     const long rows = (long)T * E * Gx::HOWO;                                                                     \
     conv_fwd_x3<Gx, 4><<<dim3((unsigned)((rows + 511) / 512), P), 256, 0, st>>>(                                  \
-        (const bf16_t*)X, xlo, (bf16_t*)Y, ylo, (uint8_t*)bits, (const bf16_t*)Wc, wlo, flat, bias_off, chunk, ai,  \
-        ac, layer, L, M, P, E, T, t0, br, os);                                                                    \
+        (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,       \
+        chunk, ai, ac, layer, L, M, P, E, T, t0, br, is / (float)(1 << X3_W0_SHIFT), os);                         \
     const int rc = (int)hipGetLastError();                                                                        \
     return rc ? -rc : 1;                                                                                          \
   }
@@ -1782,9 +1808,10 @@ int x3_fc_fwd(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, c
   if (M > X3_MAXM || KP % 32 != 0 || Cout % 64 != 0 || ldx % 8 != 0 || ldx < K || (long)T * E > 32) return 0;
   const dim3 grid(1, Cout / 64, P);
 #define FCX(RT_, D_, NKS_, OF_)                                                                                      \
-  fc_fwd_x3<RT_, D_, NKS_, OF_><<<grid, 256, 0, st>>>((const bf16_t*)X, xlo, ldx, Y, ylo, (uint16_t*)bits,          \
-                                                      (const bf16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, layer, L, \
-                                                      M, K, KP, Cout, P, E, T, t0, br, os)
+  fc_fwd_x3<RT_, D_, NKS_, OF_><<<grid, 256, 0, st>>>((const uint16_t*)X, xlo, ldx, Y, ylo, (uint16_t*)bits,        \
+                                                      (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, layer, \
+                                                      L, M, K, KP, Cout, P, E, T, t0, br,                               \
+                                                      1.f / (float)(1 << X3_W0_SHIFT), os)
   const bool of = ylo == 0;
   if ((long)T * E <= 16) {
     if (of) FCX(1, 4, 0, true); else FCX(1, 4, 0, false);

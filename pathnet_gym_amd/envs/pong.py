@@ -299,6 +299,24 @@ class PongVec(VecEnv):
         """RGB frames [N,210,160,3] (gym ``render('rgb_array')``)."""
         return render_rgb(self.state)
 
+    def stagger_scores(self, max_left: int = 3):
+        """Benchmark helper (bench.py): start every env's CURRENT episode at a random late score -- the CPU needs
+        1..max_left more points and the player has a random 0..20 -- so episodes end, fitness windows fill and GA
+        tournaments fire within the first few hundred agent steps instead of after a whole 21-point game.  Frame
+        work per step is unchanged; only the first episode of each env is shortened.  Call before the first
+        engine update (the HIP state buffer is updated in place, its address stays the one the graphs use)."""
+        if hasattr(self, "_st32"):
+            from ..ops import envs as henv
+            henv.pong_sync_from_device(self)
+        left = self._rand(7, max_left) + 1
+        self.state[:, CS] = WIN_SCORE - left
+        self.state[:, PS] = self._rand(8, WIN_SCORE)
+        self.state[:, EPRET] = self.state[:, PS] - self.state[:, CS]
+        self.counter += 1
+        if hasattr(self, "_st32"):
+            self._st32.copy_(self.state.to(torch.int32))
+            self._ctr32.copy_(self.counter.to(torch.int32))
+
     def reset(self):
         allm = torch.ones(self.num_envs, dtype=torch.bool, device=self.device)
         self.reset_where(allm)

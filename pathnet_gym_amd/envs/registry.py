@@ -15,7 +15,17 @@ ids (``gym_doom/__init__.py:18-91``).  Three kinds of env live here:
 * user envs: ``register_gym_env(id, entry_point)`` puts any class with the
   classic gym API behind the same bridge.
 
-Doom ids resolve to the ``envs/doom`` package (needs the ViZDoom engine).
+Doom ids (``gym_doom/DoomBasic-v0`` ... ``gym_doom/meta-Doom-v0``, with the reference's step limits and
+reward thresholds) resolve to ``envs/doom``: N engine-backed ``DoomEnv`` / ``MetaDoomEnv`` instances wrapped
+in ``ToDiscrete('minimal')`` (the level's allowed buttons + NOOP, reference
+``gym_doom/wrappers/action_space.py:20-66``) behind the batched host bridge, exactly the stack the reference
+builds in ``game_state.py:16-27``.  Construction needs the ViZDoom engine (``vizdoom`` / ``doom_py``), which is
+not installed in this image, and raises ``DependencyNotInstalled`` without it.
+
+Renamed ids (breaking change of round 2): the synthetic games answered to ``Pong-v0``,
+``PongNoFrameskip-v4`` and ``<Game>-v0`` in round 1; those ids now mean the REAL gym games (bridge).  The
+synthetic ones are ``Synth<Game>-v0`` or the short ``<Game>`` aliases; ``legacy_synth_id`` maps an old id
+found in a round-1 config/checkpoint to its synthetic equivalent.
 """
 from __future__ import annotations
 
@@ -66,6 +76,15 @@ def make(env_id: str, num_envs: int = 1, device="cpu", seed: int = 0, backend: s
     return env
 
 
+def legacy_synth_id(env_id: str):
+    """Round-1 id of a synthetic game (``Pong-v0``, ``PongNoFrameskip-v4``, ``Breakout-v0`` ...) -> the synthetic
+    id it meant then (``SynthPong-v0`` ...), or None when ``env_id`` never named a synthetic game."""
+    base = env_id.split("-")[0].replace("NoFrameskip", "").replace("Deterministic", "")
+    if base in REAL_ATARI_THRESHOLDS and env_id != base and not env_id.startswith("Synth"):
+        return "Synth" + base + "-v0"
+    return None
+
+
 def reward_threshold(env_id: str) -> float:
     if env_id in _THRESHOLDS:
         return _THRESHOLDS[env_id]
@@ -99,6 +118,25 @@ for _g, _thr in REAL_ATARI_THRESHOLDS.items():
     for _id in ("Synth" + _g + "-v0", _g):
         register(_id, _f, _thr)
         _SYNTH_ALIASES[_id] = _g
+
+
+def _doom(env_id: str):
+    def f(num_envs: int = 1, device="cpu", seed: int = 0, backend: str = "torch", **kw):
+        from .doom import ToDiscrete, make_doom
+        from .gym_bridge import GymVecEnv
+        kw.pop("frameskip", None)                   # ViZDoom tics are the env's own
+        envs = [ToDiscrete("minimal")(make_doom(env_id)) for _ in range(num_envs)]
+        return GymVecEnv(envs, device=device, seed=seed, backend=backend, env_id=env_id, **kw)
+    return f
+
+
+def _register_doom():
+    from .doom.constants import REGISTRY as DOOM_IDS
+    for _id, (_level, _steps, _thr) in DOOM_IDS.items():
+        register(_id, _doom(_id), _thr)
+
+
+_register_doom()
 
 
 def _register_bridge_examples():

@@ -38,27 +38,35 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
-# -- split-bf16 ("fp32x") activation storage: a value is the pair (hi, lo) of bf16 planes, hi + lo == fp32 value to
-# 2^-17 relative (csrc/trunk_x3.hip).  A tensor of the pair is the hi plane viewed out of a [2, ...] allocation; the
-# lo plane of any view starts a fixed number of elements further on (half the storage).
+# -- fp32x activation storage (csrc/trunk_x3.hip): an activation between layers is kept in four 16-bit planes of one
+# [4, ...] allocation: its fp16 pair (planes 0, 1: hi + lo == the fp32 value to 2^-22, read by the next layer's
+# forward) and its bf16 pair (planes 2, 3: 2^-16, read by the weight gradients, whose other operand -- the output
+# gradient -- needs bf16's exponent range).  The tensor handle is plane 0 (fp16); plane k of any view starts k
+# plane-lengths further on.
 def x2_alloc(shape, device) -> torch.Tensor:
-    """Hi plane of a zeroed [2, *shape] bf16 pair allocation."""
-    return torch.zeros((2,) + tuple(shape), dtype=torch.bfloat16, device=device)[0]
+    """Plane 0 (fp16 hi) of a zeroed [4, *shape] split-pair allocation."""
+    return torch.zeros((4,) + tuple(shape), dtype=torch.float16, device=device)[0]
 
 
 def x2_lo(t: torch.Tensor) -> int:
-    """Element offset from any element of a pair tensor's hi plane to the same element of its lo plane."""
+    """Elements from any element of plane 0 of a split-pair tensor to the same element of plane 1 (plane length)."""
     nb = t.untyped_storage().nbytes()
-    if t.dtype != torch.bfloat16 or nb % 4 != 0 or t.storage_offset() + t.numel() > nb // 4:
-        raise ValueError("not the hi plane of a split-bf16 pair allocation (x2_alloc)")
-    return nb // 4
+    if t.dtype != torch.float16 or nb % 8 != 0 or t.storage_offset() + t.numel() > nb // 8:
+        raise ValueError("not plane 0 of a split-pair allocation (x2_alloc)")
+    return nb // 8
 
 
-def x2_value(t: torch.Tensor) -> torch.Tensor:
-    """fp32 value hi + lo of a pair tensor (tests, checkpoints, the torch fallback)."""
-    lo = torch.empty(0, dtype=t.dtype, device=t.device).set_(t.untyped_storage(), t.storage_offset() + x2_lo(t),
-                                                            t.size(), t.stride())
-    return t.float() + lo.float()
+def _plane(t: torch.Tensor, k: int, dtype) -> torch.Tensor:
+    v = torch.empty(0, dtype=torch.float16, device=t.device).set_(t.untyped_storage(), t.storage_offset() + k * x2_lo(t),
+                                                                 t.size(), t.stride())
+    return v if dtype == torch.float16 else v.view(dtype)
+
+
+def x2_value(t: torch.Tensor, pair: str = "fp16") -> torch.Tensor:
+    """fp32 value hi + lo of a split-pair tensor: the fp16 pair (default) or the bf16 pair."""
+    if pair == "fp16":
+        return t.float() + _plane(t, 1, torch.float16).float()
+    return _plane(t, 2, torch.bfloat16).float() + _plane(t, 3, torch.bfloat16).float()
 
 
 @dataclass
@@ -161,7 +169,7 @@ class HipPathNet:
         self.WcT = []
         npl = (2,) if self.x3 else ()
         for l, g in enumerate(self.geoms):
-            wdt = torch.float16 if (self.x3 and g.u8in) else self.act_dtype
+            wdt = torch.float16 if self.x3 else self.act_dtype
             self.Wc.append(torch.zeros(npl + (self.M, g.Cout, g.KP), dtype=wdt, device=dev))
             need_t = g.kind == "fc" and l > 0
             self.WcT.append(torch.zeros(npl + (self.M, g.KP, g.Cout), dtype=self.act_dtype, device=dev)
@@ -261,8 +269,7 @@ class HipPathNet:
         if self.x3:
             for l, g in enumerate(self.geoms):
                 _lib.call("x3_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
-                          self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), int(g.u8in), self.x3_status.data_ptr(),
-                          _lib.stream())
+                          self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), 1, self.x3_status.data_ptr(), _lib.stream())
             if self.lstm is not None:
                 raise RuntimeError("fp32x runs the LSTM on the hybrid path")
             return
@@ -457,11 +464,18 @@ class HipPathNet:
     def _x3_lo(self, t: torch.Tensor) -> int:
         return 0 if t.dtype == torch.uint8 else x2_lo(t)
 
+    def _x3_bf16(self, t: torch.Tensor):
+        """(pointer, lo offset) of the bf16 pair planes (2, 3) of a split-pair tensor; uint8 frames as they are."""
+        if t.dtype == torch.uint8:
+            return t.data_ptr(), 0
+        lo = x2_lo(t)
+        return t.data_ptr() + 2 * lo * t.element_size(), lo
+
     def _layer_fwd_x3(self, l, X, Y, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st):
         g = self.geoms[l]
         flat = self.model.store.flat
         last = l == self.L - 1
-        _lib.check(Y, torch.float32 if last else torch.bfloat16, name="Y")
+        _lib.check(Y, torch.float32 if last else torch.float16, name="Y")
         ylo = 0 if last else x2_lo(Y)
         wlo = self.Wc[l][0].numel()
         if g.kind == "conv":
@@ -485,8 +499,9 @@ class HipPathNet:
         _lib.check(G, torch.float32, name="G")
         if dX is not None:
             _lib.check(dX, torch.float32, name="dX")
+        xb, xblo = self._x3_bf16(X)
         if g.kind == "conv":
-            ok = _lib.call_fast("x3_conv_wgrad", X.data_ptr(), self._x3_lo(X), int(g.u8in), G.data_ptr(),
+            ok = _lib.call_fast("x3_conv_wgrad", xb, xblo, int(g.u8in), G.data_ptr(),
                                 bits.data_ptr(), grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
                                 m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T,
                                 bits_rows, g.in_scale, g_scale, st)
@@ -508,12 +523,12 @@ class HipPathNet:
         if ok and gm is not None:
             tiles = ((g.K + 127) // 128) * self.M
             nsplit = max(1, min(m.P, -(-512 // tiles)))
-            ok = _lib.call_fast("x3_fc_wgrad_gm", X.data_ptr(), x2_lo(X), g.ldx, gm.data_ptr(), gmlo,
+            ok = _lib.call_fast("x3_fc_wgrad_gm", xb, xblo, g.ldx, gm.data_ptr(), gmlo,
                                 grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
                                 self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T,
                                 bits_rows, nsplit, st)
         elif ok:
-            ok = _lib.call_fast("x3_fc_wgrad", X.data_ptr(), x2_lo(X), g.ldx, G.data_ptr(), bits.data_ptr(),
+            ok = _lib.call_fast("x3_fc_wgrad", xb, xblo, g.ldx, G.data_ptr(), bits.data_ptr(),
                                 grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
                                 self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T,
                                 bits_rows, g_scale, st)

@@ -202,6 +202,21 @@ def read_metadata(path: str) -> dict:
         return dict(f.metadata() or {})
 
 
+def read_config(path: str):
+    """The TrainConfig stored in a checkpoint.  Task ids of the round-1 synthetic games (``Pong-v0`` ...: those ids
+    now mean the real gym games, envs/registry.py) are mapped to their ``Synth*`` equivalents with a warning."""
+    import warnings
+    from ..config import TrainConfig
+    from ..envs.registry import legacy_synth_id
+    cfg = TrainConfig.from_json(read_metadata(path)["config"])
+    new = [legacy_synth_id(t) or t for t in cfg.tasks]
+    if new != list(cfg.tasks):
+        warnings.warn(f"checkpoint tasks {cfg.tasks} use round-1 synthetic ids; mapped to {new}")
+        cfg.tasks = new
+        cfg.env = legacy_synth_id(cfg.env) or cfg.env
+    return cfg
+
+
 # ---------------------------------------------------------------------------
 # TF1 creation-order importer (SURVEY.md Appendix A)
 # ---------------------------------------------------------------------------

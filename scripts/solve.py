@@ -54,7 +54,7 @@ def main():
     ap.add_argument("--same-path", action="store_true",
                     help="every path starts from the same random N-module genotype (ablation)")
     ap.add_argument("--out", default=None, help="also write the final JSON record to this file")
-    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"], help="HIP engine compute dtype")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp32x"], help="HIP engine compute dtype")
     ap.add_argument("--deterministic", action="store_true", help="fixed-order gradient reductions")
     args = ap.parse_args()
 

@@ -47,14 +47,18 @@ def pixel_cfg(scale="M"):
 def test_x2_pair_helpers(hip_lib):
     t = x2_alloc((3, 5), DEV)
     assert x2_lo(t) == 15 and x2_lo(t[1]) == 15
-    v = torch.randn(3, 5, device=DEV)
-    hi = v.to(torch.bfloat16)
-    t.copy_(hi)
-    lo = torch.empty(0, dtype=torch.bfloat16, device=DEV).set_(t.untyped_storage(), 15, (3, 5), (5, 1))
-    lo.copy_((v - hi.float()).to(torch.bfloat16))
-    assert rel(x2_value(t), v) < 1e-5
+    v = torch.rand(3, 5, device=DEV)
+    full = torch.empty(0, dtype=torch.float16, device=DEV).set_(t.untyped_storage(), 0, (4, 3, 5), (15, 5, 1))
+    hi = v.half()
+    full[0].copy_(hi)
+    full[1].copy_((v - hi.float()).half())
+    bh = v.bfloat16()
+    full[2].copy_(bh.view(torch.float16))
+    full[3].copy_((v - bh.float()).bfloat16().view(torch.float16))
+    assert rel(x2_value(t), v) < 1e-6
+    assert rel(x2_value(t, "bf16"), v) < 2e-5
     with pytest.raises(ValueError):
-        x2_lo(torch.zeros(4, dtype=torch.bfloat16, device=DEV)[:1].expand(4))
+        x2_lo(torch.zeros(4, dtype=torch.float16, device=DEV)[:1].expand(4))
 
 
 def test_x3_weight_pairs_reconstruct_fp32(hip_lib):
@@ -67,14 +71,12 @@ def test_x3_weight_pairs_reconstruct_fp32(hip_lib):
         W = flat[g.w_off:g.w_off + hp.M * g.chunk].view(hp.M, g.chunk)[:, :g.K * g.Cout].view(hp.M, g.K, g.Cout)
         pair = hp.Wc[l].float()
         rec = (pair[0] + pair[1])[:, :, :g.K].transpose(1, 2)
-        # bf16 pair: 16 significant bits (~2.6e-6 rms); fp16 pair of W * 2^8: 22 bits
-        tol = 1e-7 if g.u8in else 4e-6
-        if g.u8in:
-            rec = rec / 256.0
-        assert rel(rec, W) < tol, (l, rel(rec, W))
+        # forward copy: fp16 pair of W * 2^8 (22 significant bits); WcT: bf16 pair (16 bits, ~2.6e-6 rms)
+        rec = rec / 256.0
+        assert rel(rec, W) < 1e-7, (l, rel(rec, W))
         if hp.WcT[l] is not None:
             pt = hp.WcT[l].float()
-            assert rel((pt[0] + pt[1])[:, :g.K], W) < tol
+            assert rel((pt[0] + pt[1])[:, :g.K], W) < 4e-6
     assert int(hp.x3_status.item()) == 0
 
 
