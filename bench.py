@@ -154,10 +154,16 @@ def in_run_solve(args, ctx, dtype: str, cap_s: float) -> dict:
     cfg, tr = build_trainer(args, ctx, dtype, stagger=False)
     thr = reward_threshold(cfg.tasks[0])
     t0 = time.time()
+    last = t0
     best = -math.inf
     out = {"seed": cfg.seed, "threshold": thr, "cap_s": cap_s, "solved": False}
     while time.time() - t0 < cap_s:
         st = tr.update()
+        now = time.time()
+        if now - last > 30 and ctx.is_main:      # progress on stderr (the JSON line stays the only stdout line)
+            last = now
+            print(f"[bench] solve t={now - t0:.0f}s generation={tr.pop.generation} frames={tr.global_step} "
+                  f"best_winner={best:.2f}", file=sys.stderr, flush=True)
         if st.tournaments:
             best = max(best, st.best_winner)
             if st.best_winner >= thr:

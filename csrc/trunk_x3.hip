@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_x3(const uint16_t* __restrict
             uint64_t bal[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float v = acc[i][ct][r] + bb;
+              const float v = acc[i][ct][r] * in_scale + bb;
               const bool pos = v > 0.f;
               sum[r] += pos ? v : 0.f;
               bal[r] = __ballot(pos);
