@@ -5,13 +5,16 @@
 // var -= mom.  A "variable" is a segment of the flat buffer; frozen segments
 // are skipped (no apply op in the reference, a3c_training_thread.py:190-216).
 //
-// Two launches, no atomics and no memset (both deterministic and safe inside a hipGraph replayed
+// Three launches, no atomics and no memset (deterministic and safe inside a hipGraph replayed
 // back-to-back -- see profiles/r2_graph_fence.md for what a captured hipMemsetAsync did):
-//  (1) seg_sqnorm: every <= 8192-element block of a segment writes its partial sum of squares;
-//  (2) rmsprop_apply: every block first checks the partials of all TRAINABLE blocks for a non-finite
-//      value (the update is then skipped on every rank alike: the partials come from the all-reduced
-//      gradient) and records that in status[0]; then sums its segment's partials in a fixed order
-//      (identical in every block of the segment, bit-reproducible) for clip_by_norm, and applies.
+//  (1) seg_sqnorm: every <= 8192-element block of a segment writes its partial sum of squares, or NaN when
+//      one of its gradient entries is not finite (a finite gradient whose square sum overflows writes +inf:
+//      clip_by_norm then scales it to 0, as tf.clip_by_norm does -- it is not skipped);
+//  (2) nonfinite_flag (one workgroup): partial[nblk] = 1 if a TRAINABLE block's partial is NaN -- the update
+//      is then skipped on every rank alike (the partials come from the all-reduced gradient); status[0] too;
+//  (3) rmsprop_apply: reads that flag, sums its segment's partials in a fixed order (identical in every block
+//      of the segment, bit-reproducible) for clip_by_norm, and applies.
+// ``partial`` holds nblk + 1 floats.
 // A third kernel refreshes the bf16 MFMA operand copies of the trunk weights (Wc [M][Cout][KP],
 // WcT [M][KP][Cout]).
 #include "common.h"
@@ -23,15 +26,31 @@ __global__ __launch_bounds__(256) void seg_sqnorm_kernel(const float* __restrict
   const int blk = blockIdx.x;
   const long b0 = blk_beg[blk], b1 = blk_end[blk];
   float s = 0.f;
+  int nf = 0;
   for (long i = b0 + threadIdx.x; i < b1; i += 256) {
     const float v = g[i];
+    nf |= !isfinite(v);
     s += v * v;
   }
   __shared__ float red[4];
+  nf = __syncthreads_or(nf);
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) partial[blk] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) partial[blk] = nf ? __builtin_nanf("") : (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void nonfinite_flag_kernel(float* __restrict__ partial, const int* __restrict__ blk_seg,
+                                                             int nblk, const uint8_t* __restrict__ trainable,
+                                                             float* __restrict__ status) {
+  int bad = 0;
+  for (int i = threadIdx.x; i < nblk; i += 256)
+    if (trainable[blk_seg[i]] && isnan(partial[i])) bad = 1;
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) {
+    partial[nblk] = bad ? 1.f : 0.f;
+    if (status) status[0] = bad ? 1.f : 0.f;
+  }
 }
 
 __global__ __launch_bounds__(256) void rmsprop_apply_kernel(float* __restrict__ w, const float* __restrict__ g,
@@ -42,16 +61,12 @@ __global__ __launch_bounds__(256) void rmsprop_apply_kernel(float* __restrict__ 
                                                             const float* __restrict__ partial,
                                                             const int* __restrict__ seg_blk0, int nblk,
                                                             const uint8_t* __restrict__ trainable,
-                                                            const float* __restrict__ lr_ptr, float* __restrict__ status,
+                                                            const float* __restrict__ lr_ptr,
                                                             float decay, float momentum, float eps, float clip) {
   const int blk = blockIdx.x, tid = threadIdx.x;
-  int bad = 0;
-  for (int i = tid; i < nblk; i += 256)
-    if (trainable[blk_seg[i]] && !isfinite(partial[i])) bad = 1;
-  bad = __syncthreads_or(bad);
-  if (blk == 0 && tid == 0 && status) status[0] = bad ? 1.f : 0.f;
   const int seg = blk_seg[blk];
-  if (bad || !trainable[seg] || lr_ptr[1] != 0.f) return;      // lr_ptr = {lr, skip}: skip = host-decided skip
+  // partial[nblk]: non-finite flag of nonfinite_flag_kernel; lr_ptr = {lr, skip}: skip = host-decided skip
+  if (partial[nblk] != 0.f || !trainable[seg] || lr_ptr[1] != 0.f) return;
   __shared__ float segsq;
   if (tid == 0) {
     float s = 0.f;
@@ -141,7 +156,7 @@ int launch_refresh_weights_cmajor(const float* flat, long w_off, int chunk, int 
   return (int)hipGetLastError();
 }
 
-// partial: float [nblk] scratch; seg_blk0: int [nseg + 1] first block of every segment (blocks are
+// partial: float [nblk + 1] scratch; seg_blk0: int [nseg + 1] first block of every segment (blocks are
 // segment-ordered); status: float [1] <- 1 if the (reduced) gradient held a non-finite value (update skipped)
 int launch_rmsprop(float* w, const float* g, float* ms, float* mom, const int* blk_seg, const long long* blk_beg,
                    const long long* blk_end, int nblk, float* partial, const int* seg_blk0, const void* trainable,
@@ -150,9 +165,9 @@ int launch_rmsprop(float* w, const float* g, float* ms, float* mom, const int* b
   if (nblk < 0) return -22;
   if (nblk <= 0) return -1;
   seg_sqnorm_kernel<<<nblk, 256, 0, stream>>>(g, blk_beg, blk_end, partial);
+  nonfinite_flag_kernel<<<1, 256, 0, stream>>>(partial, blk_seg, nblk, (const uint8_t*)trainable, status);
   rmsprop_apply_kernel<<<nblk, 256, 0, stream>>>(w, g, ms, mom, blk_seg, blk_beg, blk_end, partial, seg_blk0, nblk,
-                                                 (const uint8_t*)trainable, lr_ptr, status, decay, momentum, eps,
-                                                 clip);
+                                                 (const uint8_t*)trainable, lr_ptr, decay, momentum, eps, clip);
   return (int)hipGetLastError();
 }
 

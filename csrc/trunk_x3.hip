@@ -1,19 +1,21 @@
 // PathNet trunk in the fp32-accurate split-bf16 mode (TrainConfig.compute_dtype = "fp32x").
 //
 // The reference computes in fp32 (TF default dtype, game_ac_network.py:89-110).  gfx950 has no xf32 MFMA and its
-// fp32-input MFMA runs at 1/16 of the bf16 rate, so this mode keeps every value the bf16 engine keeps in bf16 as a
-// PAIR of bf16 values: x = hi + lo, hi = bf16(x), lo = bf16(x - hi), which represents x to 2^-17 relative.  A product
-// is then three bf16 MFMAs into one fp32 accumulator,
-//     a*b ~ a_hi*b_hi + a_hi*b_lo + a_lo*b_hi          (the dropped a_lo*b_lo term is <= 2^-16 |a*b|)
+// fp32-input MFMA runs at 1/16 of the bf16 rate, so this mode keeps every value the bf16 engine keeps in 16 bits as
+// a PAIR: x = hi + lo, hi = rnd(x), lo = rnd(x - hi).  The forward uses fp16 pairs (22 significant bits; activations
+// are ReLU sums, weights enter as W * 2^8, both far inside fp16's range); the gradient side uses bf16 pairs (16 bits,
+// bf16's exponent range for the output gradients).  A product is three MFMAs into one fp32 accumulator,
+//     a*b ~ a_hi*b_hi + a_hi*b_lo + a_lo*b_hi          (the dropped a_lo*b_lo term is <= 2^-16 |a*b| in bf16)
 // so each MFMA k-step costs 3x the bf16 engine's, against 16x for v_mfma_f32_16x16x4_f32 (csrc/trunk_f32.hip).
 // Inputs that are exact in 16 bits need two: the uint8 frame stack (exact in fp16) against the fp16 hi/lo pair of
 // the first layer's weights (scaled by 2^X3_W0_SHIFT so the lo half stays out of the fp16 subnormal range), and the
 // same uint8 stack (exact in bf16) against the hi/lo output gradient in that layer's weight gradient.
 //
 // Storage (pathnet_gym_amd/ops/pathnet_ops.py allocates it):
-//   activations between layers : two bf16 planes [hi | lo] of the bf16 engine's layout; kernels take the hi base
-//                                and the element offset of the lo plane (xlo / ylo).  The last layer writes fp32
-//                                (its only consumers are the fp32 heads kernels).
+//   activations between layers : the fp16 pair (hi | lo planes of the bf16 engine's layout; kernels take the hi
+//                                base and the element offset of the lo plane, xlo / ylo); the forward reads it as
+//                                is, the weight gradients convert it to the bf16 pair while staging.  The last
+//                                layer writes fp32 (its only consumers are the fp32 heads kernels).
 //   activation gradients       : fp32 (masked and split into hi/lo while staging into LDS).
 //   weight operand copies      : [2][M][Cout][KP] (hi plane, lo plane), WcT likewise; conv1 [2][M][8][KP] fp16.
 // Kernel structure follows the bf16 engine (conv_fast.hip, trunk_fwd.hip, trunk_bwd.hip): the same row tilings,
@@ -101,16 +103,13 @@ DEVI void split8h(const float (&v)[8], s8v& hi, s8v& lo) {
 }
 DEVI uint16_t f2h(float v) { return __builtin_bit_cast(uint16_t, (_Float16)v); }
 DEVI float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
-// An activation between layers is stored in FOUR 16-bit planes, ylo elements apart: the fp16 pair (planes 0, 1:
-// 22 significant bits, read by the next layer's forward) and the bf16 pair (planes 2, 3: 16 bits, exponent range
-// of the output gradients it meets in the weight-gradient MFMAs).
+// An activation between layers is stored as its fp16 pair in two 16-bit planes, ylo elements apart (22 significant
+// bits; the next layer's forward reads it as is).  The weight gradients meet it with the output gradient, which needs
+// bf16's exponent range, so they convert it to the bf16 pair while staging (x16pair_to_bf16pair).
 DEVI void st_x4(uint16_t* Y, long ylo, long i, float v) {
   const uint16_t h = f2h(v);
   Y[i] = h;
   Y[i + ylo] = f2h(v - h2f(h));
-  const bf16_t b = f2bf(v);
-  Y[i + 2 * ylo] = b;
-  Y[i + 3 * ylo] = f2bf(v - bf2f(b));
 }
 DEVI float ld_x4(const uint16_t* Y, long ylo, long i) { return h2f(Y[i]) + h2f(Y[i + ylo]); }
 DEVI void st8_x4(uint16_t* Y, long ylo, const float (&o)[8]) {
@@ -118,9 +117,14 @@ DEVI void st8_x4(uint16_t* Y, long ylo, const float (&o)[8]) {
   split8h(o, a, b);
   *reinterpret_cast<s8v*>(Y) = a;
   *reinterpret_cast<s8v*>(Y + ylo) = b;
-  split8(o, a, b);
-  *reinterpret_cast<s8v*>(Y + 2 * ylo) = a;
-  *reinterpret_cast<s8v*>(Y + 3 * ylo) = b;
+}
+// 8 values as an fp16 pair (hi, lo) -> the bf16 pair of their fp32 sum
+DEVI void x16pair_to_bf16pair(const s8v& h, const s8v& l, s8v& bh, s8v& bl) {
+  const h8v hh = __builtin_bit_cast(h8v, h), ll = __builtin_bit_cast(h8v, l);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)hh[j] + (float)ll[j];
+  split8(v, bh, bl);
 }
 // a*b over one 32-wide k-step from hi/lo operands: the two small cross terms first
 DEVI f4v mma3(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
@@ -154,8 +158,8 @@ DEVI s8v u8x8_to_f16(uint2 v) {
 // a k-step's raw bytes are converted, the same registers are reloaded with the next tile's k-step, then the MFMAs.
 // Wh: [2][M][8][KP] fp16 (hi plane, lo plane at +wlo).  Y: two bf16 planes (lo at +ylo).
 // ===========================================================================
-template <class G, int NT>
-__global__ __launch_bounds__(256, 2) void conv1_fwd_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
+template <class G, int NT, int LB>
+__global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                       long ylo, uint8_t* __restrict__ bits,
                                                       const uint16_t* __restrict__ Wh, long wlo,
                                                       const float* __restrict__ flat, long bias_off, int chunk,
@@ -326,8 +330,8 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_x2(const uint8_t* __restrict
 // three MFMAs per (row tile, column tile, k-step).  grid = (ceil(T*E*HOWO / (NT*128)), P).  The next 32-row
 // tile's A fragments (both planes) are loaded while this tile's MFMAs run.
 // ===========================================================================
-template <class G, int NT>
-__global__ __launch_bounds__(256, 2) void conv_fwd_x3(const uint16_t* __restrict__ X, long xlo,
+template <class G, int NT, int LB, bool DB>
+__global__ __launch_bounds__(256, LB) void conv_fwd_x3(const uint16_t* __restrict__ X, long xlo,
                                                      uint16_t* __restrict__ Y, long ylo, uint8_t* __restrict__ bits,
                                                      const uint16_t* __restrict__ Wc, long wlo,
                                                      const float* __restrict__ flat, long bias_off, int chunk,
@@ -403,16 +407,26 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_x3(const uint16_t* __restrict
           }
         }
       };
-      load_tile(rfirst);
+      // DB: the next tile's A fragments load into a second register set during this tile's MFMAs (2 waves/SIMD);
+      // otherwise one set, loaded at the top of each tile, and latency is hidden by occupancy (3 waves/SIMD)
+      if constexpr (DB) load_tile(rfirst);
       for (int tile = 0; tile < NT; ++tile) {
         const int rbase = rfirst + tile * 128;
         if (rbase >= Rtot) break;
         s8v ch_[2][NK], cl_[2][NK];
+        if constexpr (DB) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int kk = 0; kk < NK; ++kk) { ch_[i][kk] = ah[i][kk]; cl_[i][kk] = al[i][kk]; }
-        if (tile + 1 < NT) load_tile(rbase + 128);
+            for (int kk = 0; kk < NK; ++kk) { ch_[i][kk] = ah[i][kk]; cl_[i][kk] = al[i][kk]; }
+          if (tile + 1 < NT) load_tile(rbase + 128);
+        } else {
+          load_tile(rbase);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int kk = 0; kk < NK; ++kk) { ch_[i][kk] = ah[i][kk]; cl_[i][kk] = al[i][kk]; }
+        }
         f4v acc[2][NC];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -505,7 +519,7 @@ DEVI s8v tr8(const bf16_t* p0, const bf16_t* p1) {
   return (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 }
 
-template <class G, int OB>
+template <class G, int OB, int PFM>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restrict__ X, long xlo,
                                                             const float* __restrict__ Gr,
                                                             const uint8_t* __restrict__ bits, float* __restrict__ grad,
@@ -563,12 +577,18 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
     for (int a = 0; a < MPW; ++a)
 #pragma unroll
       for (int b = 0; b < NC; ++b) acc[a][b] = {0.f, 0.f, 0.f, 0.f};
-    XRaw xr[SB::XIT];
-    s8v xl[XL ? SB::XIT : 1];
-    float4 g0r[GIT], g1r[GIT];
-    uint32_t gbr[GIT][2];
-    bool gvr[GIT];
-    int navail = 0;
+    // PF register sets of stage loads in flight (PFM = 2 for paths of <= 2 column tiles: a second set beside the
+    // 3-tile accumulators would cap occupancy); stages load strictly in unit order
+    constexpr int PF = (PFM >= 2 && NC <= 2) ? 2 : 1;
+    struct Regs {
+      XRaw xr[SB::XIT];
+      s8v xl[XL ? SB::XIT : 1];
+      float4 g0r[GIT], g1r[GIT];
+      uint32_t gbr[GIT][2];
+      bool gvr[GIT];
+      int navail;
+    };
+    Regs R[PF];
     int it_band, it_e, it_t;
     {
       const int s0 = u_beg / SB::NB;
@@ -576,7 +596,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
       it_t = s0 / E;
       it_e = s0 - it_t * E;
     }
-    auto load_stage = [&]() {
+    auto load_stage = [&](Regs& Rg) {
       const int band = it_band, ut = it_t, ue = it_e;
       const long sg = (long)ut * PE + (long)p * E + ue;
       if (++it_band == SB::NB) {
@@ -584,17 +604,18 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
         if (++it_e == E) { it_e = 0; ++it_t; }
       }
       const int ih0 = band * OB * G::S;
-      navail = min(SB::SR, G::HIN - ih0) * SB::RL;
+      const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;
+      Rg.navail = navail;
       const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
 #pragma unroll
       for (int j = 0; j < SB::XIT; ++j) {
         const int gi = tid + 256 * j;
         const int e0 = (gi < SB::NG8 && gi * 8 < navail) ? gi * 8 : 0;   // clamped, zeroed at write time
         if constexpr (G::U8) {
-          xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xbase + e0);
+          Rg.xr[j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(X) + xbase + e0);
         } else {
-          xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xbase + e0);
-          xl[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xlo + xbase + e0);
+          Rg.xr[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xbase + e0);
+          Rg.xl[j] = *reinterpret_cast<const s8v*>(reinterpret_cast<const bf16_t*>(X) + xlo + xbase + e0);
         }
       }
       const int oh0 = band * OB;
@@ -603,37 +624,34 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
         const int it = tid + 256 * j;
         const int rho = it >> 2, sub = it & 3;
         const int ob = rho / G::WO, ow = rho - ob * G::WO;
-        gvr[j] = it < GROWS * 4 && rho < SB::NPOS && oh0 + ob < G::HO;
-        if (gvr[j]) {
+        Rg.gvr[j] = it < GROWS * 4 && rho < SB::NPOS && oh0 + ob < G::HO;
+        if (Rg.gvr[j]) {
           const long go = sg * G::HOWO + (oh0 + ob) * G::WO + ow;
-          g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
-          g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+          Rg.g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+          Rg.g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
 #pragma unroll
           for (int k = 0; k < 2; ++k) {
             const int slot = 2 * ct0 + sub + 4 * k;
-            gbr[j][k] = (sub + 4 * k < 2 * NC && slot < cnt) ? bits[(long)slot * bits_rows + go] : 0u;
+            Rg.gbr[j][k] = (sub + 4 * k < 2 * NC && slot < cnt) ? bits[(long)slot * bits_rows + go] : 0u;
           }
         }
       }
     };
-    auto write_stage = [&](int buf) {
+    auto write_stage = [&](const Regs& Rg, int buf) {
 #pragma unroll
       for (int j = 0; j < SB::XIT; ++j) {
         const int gi = tid + 256 * j;
         if (gi < SB::NG8) {
-          const bool ok = gi * 8 < navail;
+          const bool ok = gi * 8 < Rg.navail;
           s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
           if constexpr (G::U8) {
-            if (ok) v = u8x8_to_bf16(xr[j]);
+            if (ok) v = u8x8_to_bf16(Rg.xr[j]);
           } else {
-            if (ok) v = xr[j];
-          }
-          *reinterpret_cast<s8v*>(&Xs[buf][0][gi * 8]) = v;
-          if constexpr (XL) {
-            s8v vl = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (ok) vl = xl[j];
+            s8v vl = v;
+            if (ok) x16pair_to_bf16pair(Rg.xr[j], Rg.xl[j], v, vl);      // fp16 pair -> bf16 pair
             *reinterpret_cast<s8v*>(&Xs[buf][XL ? 1 : 0][gi * 8]) = vl;
           }
+          *reinterpret_cast<s8v*>(&Xs[buf][0][gi * 8]) = v;
         }
       }
 #pragma unroll
@@ -641,14 +659,15 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
         const int it = tid + 256 * j;
         if (it >= GROWS * 4) continue;
         const int rho = it >> 2, sub = it & 3;
-        const float gg[8] = {g0r[j].x, g0r[j].y, g0r[j].z, g0r[j].w, g1r[j].x, g1r[j].y, g1r[j].z, g1r[j].w};
+        const float gg[8] = {Rg.g0r[j].x, Rg.g0r[j].y, Rg.g0r[j].z, Rg.g0r[j].w,
+                             Rg.g1r[j].x, Rg.g1r[j].y, Rg.g1r[j].z, Rg.g1r[j].w};
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           const int rel = sub + 4 * k;
           if (rel < 2 * NC) {
             float m[8];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) m[c] = (gvr[j] && ((gbr[j][k] >> c) & 1u)) ? gg[c] : 0.f;
+            for (int c = 0; c < 8; ++c) m[c] = (Rg.gvr[j] && ((Rg.gbr[j][k] >> c) & 1u)) ? gg[c] : 0.f;
 #pragma unroll
             for (int c = 0; c < 8; ++c) acc_b[k][c] += m[c];
             s8v hi, lo;
@@ -689,18 +708,54 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
       }
     };
     __syncthreads();     // the previous pass's LDS reads are done (and the init above is visible)
-    if (u_beg < u_end) load_stage();
-    int u = u_beg, buf = 0;
-    for (; u + 1 < u_end; ++u, buf ^= 1) {
-      write_stage(buf);
-      __syncthreads();
-      load_stage();
-      compute_stage(buf);
-    }
-    if (u < u_end) {
-      write_stage(buf);
-      __syncthreads();
-      compute_stage(buf);
+    // the last stage(s) are peeled so every in-loop reload is unconditional (a conditional reload is a loop-carried
+    // phi: the compiler copied the register set to merge it, conv_fast.hip conv_wgrad_slab)
+    if constexpr (PF == 1) {
+      if (u_beg < u_end) load_stage(R[0]);
+      int u = u_beg, buf = 0;
+      for (; u + 1 < u_end; ++u, buf ^= 1) {
+        write_stage(R[0], buf);
+        __syncthreads();
+        load_stage(R[0]);
+        compute_stage(buf);
+      }
+      if (u < u_end) {
+        write_stage(R[0], buf);
+        __syncthreads();
+        compute_stage(buf);
+      }
+    } else {
+      // stage u lives in register set and LDS buffer (u - u_beg) & 1: stage u+2's loads fly during stage u
+      if (u_beg < u_end) load_stage(R[0]);
+      if (u_beg + 1 < u_end) load_stage(R[PF - 1]);
+      int u = u_beg;
+      for (; u + 3 < u_end; u += 2) {
+        write_stage(R[0], 0);
+        __syncthreads();
+        load_stage(R[0]);
+        compute_stage(0);
+        write_stage(R[PF - 1], 1);
+        __syncthreads();
+        load_stage(R[PF - 1]);
+        compute_stage(1);
+      }
+      const int rem = u_end - u;
+      if (rem >= 1) {
+        write_stage(R[0], 0);
+        __syncthreads();
+        if (rem >= 3) load_stage(R[0]);
+        compute_stage(0);
+      }
+      if (rem >= 2) {
+        write_stage(R[PF - 1], 1);
+        __syncthreads();
+        compute_stage(1);
+      }
+      if (rem >= 3) {
+        write_stage(R[0], 0);
+        __syncthreads();
+        compute_stage(0);
+      }
     }
     const int h = i16 >> 3, ch = l & 7;
 #pragma unroll
@@ -833,9 +888,10 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
         const int it = tid + 512 * j;
         if (it < X3_WG_RB * G::KC) {
           const int row = it / G::KC, kc = it - row * G::KC;
-          const s8v z = {0, 0, 0, 0, 0, 0, 0, 0};
-          *reinterpret_cast<s8v*>(&Xs[buf][0][row * XS + kc * 8]) = xv[j] ? xh[j] : z;
-          *reinterpret_cast<s8v*>(&Xs[buf][1][row * XS + kc * 8]) = xv[j] ? xlr[j] : z;
+          s8v bh = {0, 0, 0, 0, 0, 0, 0, 0}, bl = bh;
+          if (xv[j]) x16pair_to_bf16pair(xh[j], xlr[j], bh, bl);     // fp16 pair -> bf16 pair
+          *reinterpret_cast<s8v*>(&Xs[buf][0][row * XS + kc * 8]) = bh;
+          *reinterpret_cast<s8v*>(&Xs[buf][1][row * XS + kc * 8]) = bl;
         }
       }
       if (tid < 256 && gsl < 2 * NC) {
@@ -1475,8 +1531,12 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
   gload(0);
   for (int it = 0; it < n_it; ++it) {
     const int buf = it & 1;
-    *reinterpret_cast<s8v*>(Xs[buf][0] + lr * XS + lxs) = xrh;
-    *reinterpret_cast<s8v*>(Xs[buf][1] + lr * XS + lxs) = xrl;
+    {
+      s8v bh, bl;
+      x16pair_to_bf16pair(xrh, xrl, bh, bl);          // fp16 pair -> bf16 pair (zeros stay zeros)
+      *reinterpret_cast<s8v*>(Xs[buf][0] + lr * XS + lxs) = bh;
+      *reinterpret_cast<s8v*>(Xs[buf][1] + lr * XS + lxs) = bl;
+    }
 #pragma unroll
     for (int h = 0; h < GSEG / 8; ++h) {
       *reinterpret_cast<s8v*>(Gsh[buf][0] + lr * GS + lgs + 8 * h) = grh[h];
@@ -1594,10 +1654,11 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
           }
         }
       }
-      s8v gh, gl;
+      s8v gh, gl, bh, bl;
       split8(m, gh, gl);
-      *reinterpret_cast<s8v*>(Xs[0] + srow * S + sc) = xh;
-      *reinterpret_cast<s8v*>(Xs[1] + srow * S + sc) = xl;
+      x16pair_to_bf16pair(xh, xl, bh, bl);            // fp16 pair -> bf16 pair
+      *reinterpret_cast<s8v*>(Xs[0] + srow * S + sc) = bh;
+      *reinterpret_cast<s8v*>(Xs[1] + srow * S + sc) = bl;
       *reinterpret_cast<s8v*>(Gs[0] + srow * S + sc) = gh;
       *reinterpret_cast<s8v*>(Gs[1] + srow * S + sc) = gl;
       __syncthreads();
@@ -1696,10 +1757,22 @@ static bool x3_is(int Hin, int Win, int Cin, int KH, int KW, int S, int u8) {
 }
 
 static int X3_FWD_NT = 8;      // 32-row tiles per wave in the first-layer forward (4 for the bf16-input layers)
+static int X3_FWD_LB = 2;      // first-layer forward: min waves/SIMD (2: 194 VGPRs, no spill; 3: 168 with spills)
+static int X3_FWD_DB = 0;      // bf16-activation conv forward: 1 = double-buffered A registers (2 waves/SIMD),
+                               // 0 = one register set at 3 waves/SIMD (measured: conv3 24.6 -> 16.9 us, conv2 31.1 -> 30.3)
+// slab weight gradient: stages of loads in flight for <= 2 column tiles: 1, 2, or 3 = 2 for the bf16-input layers
+// and 1 for the uint8 first layer (measured, steady-state window: conv1 2.63 (2) -> 2.32 ms (1), conv2 0.50 (2) vs
+// 0.52 ms (1); profiles/r3/kwin_x3_v4*.md)
+static int X3_WGRAD_PF = 3;
+static int X3_FC_D = 4;        // fc forward register ring depth (k-steps of hi/lo A and B fragments in flight)
 
 extern "C" {
 
 void fast_conv_set_x3_fwd_nt(int nt) { X3_FWD_NT = nt; }
+void fast_conv_set_x3_fwd_lb(int lb) { X3_FWD_LB = lb; }
+void fast_conv_set_x3_fwd_db(int db) { X3_FWD_DB = db; }
+void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
+void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
 
 int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits, const void* Wc, long wlo,
                 const float* flat, long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M,
@@ -1713,11 +1786,15 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
     if ((E * C1::HOWO) % 16) return -2;
     const long rows = (long)T * E * C1::HOWO;
     const float isc = is / (float)(1 << X3_W0_SHIFT);
-#define C1L(NT_)                                                                                                \
-  conv1_fwd_x2<C1, NT_><<<dim3((unsigned)((rows + NT_ * 128 - 1) / (NT_ * 128)), P), 256, 0, st>>>(             \
+#define C1L(NT_, LB_)                                                                                           \
+  conv1_fwd_x2<C1, NT_, LB_><<<dim3((unsigned)((rows + NT_ * 128 - 1) / (NT_ * 128)), P), 256, 0, st>>>(             \
       (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, \
       layer, L, M, P, E, T, t0, br, isc, os)
-    if (X3_FWD_NT >= 8) C1L(8); else C1L(4);
+    if (X3_FWD_LB >= 3) {
+      if (X3_FWD_NT >= 8) C1L(8, 3); else C1L(4, 3);
+    } else {
+      if (X3_FWD_NT >= 8) C1L(8, 2); else C1L(4, 2);
+    }
 #undef C1L
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
@@ -1726,9 +1803,16 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
   if (x3_is<Gx>(Hin, Win, Cin, KH, KW, S, u8in)) {                                                                \
     if ((E * Gx::HOWO) % 16) return -2;                                                                           \
     const long rows = (long)T * E * Gx::HOWO;                                                                     \
-    conv_fwd_x3<Gx, 4><<<dim3((unsigned)((rows + 511) / 512), P), 256, 0, st>>>(                                  \
-        (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,       \
-        chunk, ai, ac, layer, L, M, P, E, T, t0, br, is / (float)(1 << X3_W0_SHIFT), os);                         \
+    const dim3 grid((unsigned)((rows + 511) / 512), P);                                                           \
+    const float isc = is / (float)(1 << X3_W0_SHIFT);                                                             \
+    if (X3_FWD_DB)                                                                                                \
+      conv_fwd_x3<Gx, 4, 2, true><<<grid, 256, 0, st>>>(                                                          \
+          (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \
+          chunk, ai, ac, layer, L, M, P, E, T, t0, br, isc, os);                                                  \
+    else                                                                                                          \
+      conv_fwd_x3<Gx, 4, 3, false><<<grid, 256, 0, st>>>(                                                         \
+          (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \
+          chunk, ai, ac, layer, L, M, P, E, T, t0, br, isc, os);                                                  \
     const int rc = (int)hipGetLastError();                                                                        \
     return rc ? -rc : 1;                                                                                          \
   }
@@ -1751,9 +1835,14 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     const long units = (long)T * E * SB::NB;
     long upw = (units + 23) / 24;
     if (upw < 8) upw = 8;
-    conv_wgrad_slab_x3<Gx, OB><<<dim3((unsigned)((units + upw - 1) / upw), P), 256, 0, st>>>(
-        X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br, (int)upw, is,
-        gs);
+    const dim3 grid((unsigned)((units + upw - 1) / upw), P);
+    const int pf = Gx::U8 ? (X3_WGRAD_PF == 2 ? 2 : 1) : (X3_WGRAD_PF >= 2 ? 2 : 1);
+    if (pf == 2)
+      conv_wgrad_slab_x3<Gx, OB, 2><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
+                                                          ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs);
+    else
+      conv_wgrad_slab_x3<Gx, OB, 1><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
+                                                          ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   };
@@ -1815,6 +1904,8 @@ int x3_fc_fwd(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, c
   const bool of = ylo == 0;
   if ((long)T * E <= 16) {
     if (of) FCX(1, 4, 0, true); else FCX(1, 4, 0, false);
+  } else if (KP == 1408 && X3_FC_D <= 2) {
+    if (of) FCX(2, 2, 44, true); else FCX(2, 2, 44, false);
   } else if (KP == 1408) {
     if (of) FCX(2, 4, 44, true); else FCX(2, 4, 44, false);
   } else if (KP == 256) {

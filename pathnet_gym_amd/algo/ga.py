@@ -230,7 +230,7 @@ class Population:
         self.frozen = np.asarray(d["frozen"]).astype(np.float32)
         self.fitness = np.asarray(d["fitness"]).astype(np.float32).copy()
         self.candidates = [list(map(int, c)) for c in np.asarray(d["candidates"])]
-        self.generation = int(np.asarray(d["generation"]))
+        self.generation = int(np.asarray(d["generation"]).reshape(-1)[0])
         pos = np.asarray(d["rng_pos"])
         self.rng.set_state(("MT19937", np.asarray(d["rng_keys"]).astype(np.uint32), int(pos[0]), int(pos[1]),
                             float(np.asarray(d["rng_gauss"])[0])))

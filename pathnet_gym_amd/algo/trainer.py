@@ -60,6 +60,9 @@ class UpdateStats:
     best_winner: float = float("nan")
     steps: int = 0
     skipped: bool = False
+    # the update (1-based count) whose optimizer step ``skipped`` refers to: this one when not pipelined; with the
+    # pipeline the status arrives one update late, so it names the previous update (flush() reports the last)
+    skipped_update: int = -1
 
 
 class PathNetTrainer:
@@ -147,6 +150,7 @@ class PathNetTrainer:
             self.fitness_local = self.engine.fitness
             if self.device_ga:
                 self.engine.enable_device_ga(self.pop, self.comm, self.path_offset)
+            self._enable_overlap()
         else:
             self.fitness_local = torch.full((self.P,), FITNESS_PENDING, device=self.device)
             self.fit_cnt = torch.zeros(self.P, device=self.device)
@@ -154,6 +158,22 @@ class PathNetTrainer:
         self.task_start_step = self.global_step
         self.solved_generation.setdefault(task_idx, None)
         self._task_gen0 = self.pop.generation
+
+    def _enable_overlap(self):
+        """TrainConfig.overlap_allreduce: split the HIP update at the first layer so the all-reduce of everything
+        else runs during the first layer's weight gradient (parallel/comm.py exchange_async_split)."""
+        eng = self.engine
+        if not (getattr(self.cfg, "overlap_allreduce", True) and self.ctx.enabled and self.pipelined
+                and isinstance(self.comm, FusedUpdateComm) and type(self.comm) is FusedUpdateComm
+                and not eng.hybrid and not eng.lstm_hip and self.device.type == "cuda"):
+            return
+        segs = self.model.store.layout.segments
+        split_off = max(s.offset + s.numel for s in segs if s.layer == 0)
+        if any(s.offset < split_off for s in segs if s.layer != 0):
+            return                               # layout does not put the first layer first: keep one bucket
+        if self.comm.split_off is None:
+            self.comm.enable_overlap(split_off)
+        eng.split = True
 
     def _push_genotypes(self):
         expr = self.pop.expressed()
@@ -282,14 +302,16 @@ class PathNetTrainer:
                     self.opt.step(grad, lr)
         self.global_step += int(csum[0])
         self.updates += 1
-        return self._finish_update(fit_all, csum, (lp, lv, ent), skip, self.global_step)
+        st = self._finish_update(fit_all, csum, (lp, lv, ent), skip, self.global_step)
+        st.skipped_update = self.updates if skip else -1
+        return st
 
     def _update_pipelined(self, lr) -> UpdateStats:
         """Enqueue update u (rollout graph, fused reduce, optimizer+GA graph, async D2H), then finish u-1."""
         tr = self.tracer
         eng = self.engine
         with tr.phase("rollout_backward"):
-            eng.rollout_backward()
+            eng.rollout_backward("head" if eng.split else None)
         with tr.phase("allreduce"):
             if self.ctx.enabled:
                 # modules the running rollout uses, from the device GA of the previous optimizer step (the GPU is
@@ -297,32 +319,56 @@ class PathNetTrainer:
                 union = eng.active_union()
                 if union is not None:
                     self.comm.plan_union(union)
-            handle = self.comm.exchange_async(eng.grad_flat, eng.fitness, eng.counters, extra=eng.report_tensor())
+            if eng.split:
+                # bucket 1 (layers >= 1, heads, fitness, counters) is reduced while the first layer's weight
+                # gradient runs; bucket 2 (the first layer) after it
+                handle = self.comm.exchange_async_split(eng.grad_flat, eng.fitness, eng.counters,
+                                                        run_tail=lambda: eng.rollout_backward("tail"),
+                                                        extra=eng.report_tensor())
+            else:
+                handle = self.comm.exchange_async(eng.grad_flat, eng.fitness, eng.counters,
+                                                  extra=eng.report_tensor())
         with tr.phase("optimizer"):
             eng.optimizer_step(lr)              # non-finite reduced gradient: skipped on device, on every rank
         self.global_step += self.cfg.a2c.t_max * self.P * self.E * self.ctx.world
         self.updates += 1
-        prev, self._pending = getattr(self, "_pending", None), (handle, self.global_step)
+        prev, self._pending = getattr(self, "_pending", None), (handle, self.global_step, self.updates)
         if prev is None:
             return UpdateStats(float("nan"), float("nan"), float("nan"), 0, float("nan"),
                                steps=self.cfg.a2c.t_max * self.P * self.E * self.ctx.world)
         return self._collect(prev)
 
+    def _guard_opt(self, flag: float, update: int) -> bool:
+        """Feed the device optimizer status of ``update`` to the guard once (pipelined: it arrives late)."""
+        if update <= getattr(self, "_opt_checked", 0):
+            return False
+        self._opt_checked = update
+        return self.guard.check(flag, update)
+
     def _collect(self, pending) -> UpdateStats:
-        handle, step_at = pending
+        handle, step_at, u = pending
         fit_all, csum, stats = self.comm.collect(handle)
-        # stats[4]: whether the optimizer step BEFORE this update skipped a non-finite gradient (one-update lag)
-        skip = self.guard.check(float(stats[4]), self.updates)
+        # stats[4]: whether the optimizer step of update u-1 skipped a non-finite gradient (read before the
+        # optimizer of update u ran: one-update lag)
+        skip = self._guard_opt(float(stats[4]), u - 1) if u > 1 else False
         ent = float(stats[2]) / max(1, self.cfg.a2c.t_max * self.P * self.E)
-        return self._finish_update(fit_all, csum, (float(stats[0]), float(stats[1]), ent), skip, step_at)
+        st = self._finish_update(fit_all, csum, (float(stats[0]), float(stats[1]), ent), skip, step_at)
+        st.skipped_update = u - 1 if skip else -1
+        return st
 
     def flush(self) -> Optional[UpdateStats]:
-        """Drain the pipelined update still in flight (task end, checkpoint, end of run)."""
+        """Drain the pipelined update still in flight (task end, checkpoint, end of run); the status of its
+        optimizer step (the last one) is read here, so it reaches the guard too."""
         pending = getattr(self, "_pending", None)
         self._pending = None
         if pending is None:
             return None
-        return self._collect(pending)
+        st = self._collect(pending)
+        u = pending[2]
+        if self.engine is not None and getattr(self.engine, "opt_status", None) is not None:
+            if self._guard_opt(float(self.engine.opt_status), u):
+                st.skipped, st.skipped_update = True, u
+        return st
 
     def _finish_update(self, fit_all, csum, losses, skip, step_at) -> UpdateStats:
         tr = self.tracer

@@ -219,6 +219,9 @@ class TrainConfig:
     # HIP engine + device GA: overlap the host bookkeeping of update u-1 with the GPU work of update u
     # (stats / tournament events are reported one update late; flush() drains the last one)
     pipeline: bool = True
+    # multi-rank HIP engine: all-reduce everything but the first layer's gradient while that layer's weight-gradient
+    # kernel runs (two async buckets, parallel/comm.py); False = one bucket after the whole backward
+    overlap_allreduce: bool = True
 
     def to_json(self):
         return json.dumps(dataclasses.asdict(self))
@@ -279,7 +282,13 @@ def preset(name: str) -> TrainConfig:
                            ga=GAConfig(B=3, fitness="mean"),
                            a2c=A2CConfig(max_time_step=DEVICE_TASK_STEPS))
     if name in ("reference", "ref"):
-        # the reference's own default network: L=4 (3 conv + 1 linear), M=10, N=4, LSTM
+        # the reference's own default network and experiment: L=4 (3 conv + 1 linear 1408->256), M=10, N=4,
+        # BasicLSTMCell(256) (USE_LSTM=True, constants.py:30; game_ac_network.py:303-521), 18-way head
+        # (ACTION_SIZEZ, constants.py:15), LOCAL_T_MAX=20 (constants.py:4), Alien -> Centipede
+        # (aliencentipede.txt:55-93).  The reference's 9 one-env workers become 64 paths x 16 envs, the HIP
+        # engine's shape (runtime/engine.py, csrc/lstm.hip); the same GA fitness as "pong" (mean of the last E).
         net = PathNetConfig(L=4, M=10, N=4, use_lstm=True, trunk_scale="none", num_actions=18)
-        return TrainConfig(env="Pong", tasks=["Pong", "Breakout"], paths=9, envs_per_path=1, net=net)
+        return TrainConfig(env="Alien", tasks=["Alien", "Centipede"], paths=64, envs_per_path=16, net=net,
+                           ga=GAConfig(B=3, fitness="mean"), steps_per_task=DEVICE_TASK_STEPS,
+                           a2c=A2CConfig(t_max=20, max_time_step=DEVICE_TASK_STEPS))
     raise KeyError(name)

@@ -129,6 +129,10 @@ _SIGS = {
     "x3_fc_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8 + [c_long, c_float, P],
     "x3_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
     "fast_conv_set_x3_fwd_nt": [c_int],
+    "fast_conv_set_x3_fwd_lb": [c_int],
+    "fast_conv_set_x3_fwd_db": [c_int],
+    "fast_conv_set_x3_fc_d": [c_int],
+    "fast_conv_set_x3_wgrad_pf": [c_int],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }

@@ -34,7 +34,7 @@ def _tables(opt):
              beg=torch.tensor(beg, dtype=torch.int64, device=dev),
              end=torch.tensor(end, dtype=torch.int64, device=dev),
              blk0=torch.tensor(blk0, dtype=torch.int32, device=dev),
-             partial=torch.zeros(len(seg_id), dtype=torch.float32, device=dev),
+             partial=torch.zeros(len(seg_id) + 1, dtype=torch.float32, device=dev),
              status=torch.zeros(1, dtype=torch.float32, device=dev),
              lr=torch.zeros(2, dtype=torch.float32, device=dev))
     opt._hip_tables = t

@@ -38,22 +38,21 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
-# -- fp32x activation storage (csrc/trunk_x3.hip): an activation between layers is kept in four 16-bit planes of one
-# [4, ...] allocation: its fp16 pair (planes 0, 1: hi + lo == the fp32 value to 2^-22, read by the next layer's
-# forward) and its bf16 pair (planes 2, 3: 2^-16, read by the weight gradients, whose other operand -- the output
-# gradient -- needs bf16's exponent range).  The tensor handle is plane 0 (fp16); plane k of any view starts k
-# plane-lengths further on.
+# -- fp32x activation storage (csrc/trunk_x3.hip): an activation between layers is kept as its fp16 pair in two
+# 16-bit planes of one [2, ...] allocation (hi + lo == the fp32 value to 2^-22; the weight-gradient kernels convert it
+# to the bf16 pair while staging).  The tensor handle is plane 0 (fp16 hi); plane 1 of any view starts one plane
+# length further on.
 def x2_alloc(shape, device) -> torch.Tensor:
-    """Plane 0 (fp16 hi) of a zeroed [4, *shape] split-pair allocation."""
-    return torch.zeros((4,) + tuple(shape), dtype=torch.float16, device=device)[0]
+    """Plane 0 (fp16 hi) of a zeroed [2, *shape] fp16-pair allocation."""
+    return torch.zeros((2,) + tuple(shape), dtype=torch.float16, device=device)[0]
 
 
 def x2_lo(t: torch.Tensor) -> int:
-    """Elements from any element of plane 0 of a split-pair tensor to the same element of plane 1 (plane length)."""
+    """Elements from any element of plane 0 of a pair tensor to the same element of plane 1 (plane length)."""
     nb = t.untyped_storage().nbytes()
-    if t.dtype != torch.float16 or nb % 8 != 0 or t.storage_offset() + t.numel() > nb // 8:
-        raise ValueError("not plane 0 of a split-pair allocation (x2_alloc)")
-    return nb // 8
+    if t.dtype != torch.float16 or nb % 4 != 0 or t.storage_offset() + t.numel() > nb // 4:
+        raise ValueError("not plane 0 of a fp16-pair allocation (x2_alloc)")
+    return nb // 4
 
 
 def _plane(t: torch.Tensor, k: int, dtype) -> torch.Tensor:
@@ -62,11 +61,9 @@ def _plane(t: torch.Tensor, k: int, dtype) -> torch.Tensor:
     return v if dtype == torch.float16 else v.view(dtype)
 
 
-def x2_value(t: torch.Tensor, pair: str = "fp16") -> torch.Tensor:
-    """fp32 value hi + lo of a split-pair tensor: the fp16 pair (default) or the bf16 pair."""
-    if pair == "fp16":
-        return t.float() + _plane(t, 1, torch.float16).float()
-    return _plane(t, 2, torch.bfloat16).float() + _plane(t, 3, torch.bfloat16).float()
+def x2_value(t: torch.Tensor) -> torch.Tensor:
+    """fp32 value hi + lo of an fp16-pair tensor."""
+    return t.float() + _plane(t, 1, torch.float16).float()
 
 
 @dataclass
@@ -465,11 +462,10 @@ class HipPathNet:
         return 0 if t.dtype == torch.uint8 else x2_lo(t)
 
     def _x3_bf16(self, t: torch.Tensor):
-        """(pointer, lo offset) of the bf16 pair planes (2, 3) of a split-pair tensor; uint8 frames as they are."""
+        """(pointer, lo offset) of a weight-gradient X operand: an fp16 pair (converted in-kernel), or uint8 frames."""
         if t.dtype == torch.uint8:
             return t.data_ptr(), 0
-        lo = x2_lo(t)
-        return t.data_ptr() + 2 * lo * t.element_size(), lo
+        return t.data_ptr(), x2_lo(t)
 
     def _layer_fwd_x3(self, l, X, Y, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st):
         g = self.geoms[l]

@@ -26,7 +26,16 @@ fitness + RCCL broadcast of the winner genotype table from rank 0), used by
 
 Bucket sizing for xGMI: the whole buffer is <= 17 MB, a single ring
 all-reduce moves 2*(w-1)/w*S per GPU, ~0.2 ms at 153 GB/s per link, so one
-bucket (no splitting) minimises the latency-dominated cost.
+bucket minimises the latency-dominated cost -- except that it would wait for
+the LAST backward kernel.  With ``enable_overlap(split_off)`` (HIP engine,
+pipelined, world > 1) the update is split at the first layer: bucket 1 =
+[gradients at offsets >= split_off (layers 1..L-1 + heads) | fitness |
+counters] is all-reduced asynchronously (RCCL runs it on its own stream)
+while the first layer's weight-gradient kernel -- the longest backward
+kernel, 1.5-2.4 ms at the bench shape -- runs on the compute stream; bucket 2
+(the first layer's active modules) follows.  Per element the sums are the
+same two-way additions as the single bucket, so at two ranks the result is
+bit-identical (tests/test_dist_hip.py).
 """
 from __future__ import annotations
 
@@ -100,6 +109,26 @@ class FusedUpdateComm:
         self.nranges = 0
         self._union_key = None
         self.plans = 0              # number of distinct plans built (diagnostics)
+        # split (overlapped) exchange: bucket tables for offsets >= split_off / < split_off
+        self.split_off = None
+        self.n1 = self.n2 = 0
+        self.tab1 = self.tab2 = None
+        self.nr1 = self.nr2 = 0
+        self.overlap_log = None     # list of per-update timing records when tracing (utils/tracing.py)
+
+    def enable_overlap(self, split_off: int):
+        """Split every exchange at flat offset ``split_off`` (the first layer's end) into two async buckets."""
+        if not self._gpu_pack:
+            raise RuntimeError("the overlapped exchange packs on the GPU (HIP engine)")
+        self.split_off = int(split_off)
+        self._split_tabs = [[torch.zeros(self.layout.cfg.L * self.layout.cfg.M + 1, 3, dtype=torch.int64,
+                                         device=self.device) for _ in range(2)] for _ in range(2)]
+        self._split_host = [[torch.zeros(self.layout.cfg.L * self.layout.cfg.M + 1, 3, dtype=torch.int64,
+                                          pin_memory=True) for _ in range(2)] for _ in range(2)]
+        self._split_ev = [None, None]
+        self._split_flip = 0
+        self._union_key = None
+        self._plan_split([(0, self.layout.numel)])      # dense until the first module union arrives
 
     # -- planning ---------------------------------------------------------------
     def plan(self, expressed_all: np.ndarray, frozen: np.ndarray):
@@ -116,6 +145,9 @@ class FusedUpdateComm:
         self.plans += 1
         rng = union_ranges(self.layout, union)
         n = sum(e - s for s, e in rng)
+        if self.split_off is not None:
+            self._plan_split(rng if not self.force_dense else [(0, self.layout.numel)])
+            return
         if self.force_dense or n >= self.dense_threshold * self.layout.numel:
             self.ranges = [(0, self.layout.numel)]
             self.index = None
@@ -145,6 +177,99 @@ class FusedUpdateComm:
         else:
             idx = np.concatenate([np.arange(s, e, dtype=np.int64) for s, e in rng])
             self.index = torch.from_numpy(idx).to(self.device)
+
+    def _plan_split(self, rng):
+        so = self.split_off
+        r1 = [(max(s, so), e) for s, e in rng if e > so]
+        r2 = [(s, min(e, so)) for s, e in rng if s < so]
+        self.ranges = rng
+        self.n1 = sum(e - s for s, e in r1)
+        self.n2 = sum(e - s for s, e in r2)
+        self.ngrad = self.n1 + self.n2
+        f = self._split_flip
+        self._split_flip ^= 1
+        if self._split_ev[f] is not None:
+            self._split_ev[f].synchronize()
+        for b, rr in enumerate((r1, r2)):
+            tab = np.zeros((max(1, len(rr)), 3), np.int64)
+            d = 0
+            for i, (s, e) in enumerate(rr):
+                tab[i] = (s, e - s, d)
+                d += e - s
+            self._split_host[f][b][:len(tab)].copy_(torch.from_numpy(tab))
+            self._split_tabs[f][b].copy_(self._split_host[f][b], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._split_ev[f] = ev
+        self.tab1, self.tab2 = self._split_tabs[f]
+        self.nr1, self.nr2 = len(r1), len(r2)
+
+    def _pack_tab(self, grad, packed_off: int, tab, nr: int, n: int, unpack: int):
+        if n == 0 or nr == 0:
+            return
+        from ..ops import _lib
+        _lib.call("launch_pack_ranges", grad.data_ptr(), self.buf.data_ptr() + packed_off * 4, tab.data_ptr(), nr, n,
+                  unpack, _lib.stream())
+
+    def exchange_async_split(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor,
+                             run_tail, extra=None):
+        """Overlapped form of ``exchange_async``: bucket 1 (offsets >= split_off, fitness, counters) goes out
+        asynchronously, then ``run_tail()`` enqueues the first layer's backward on the compute stream (it runs while
+        bucket 1 is reduced), then bucket 2 (offsets < split_off).  Both are waited for before unpacking."""
+        import time
+        import torch.distributed as dist
+        P = self.P_total
+        n1, n2 = self.n1, self.n2
+        m = n1 + P + self.NCOUNTERS
+        buf = self.buf
+        rec = {} if self.overlap_log is not None else None
+        self._pack_tab(grad, 0, self.tab1, self.nr1, n1, 0)
+        fit = buf[n1:n1 + P]
+        fit.zero_()
+        fit[self.offset:self.offset + self.P_local].copy_(fitness_local)
+        buf[n1 + P:m].copy_(counters)
+        if rec is not None:
+            rec["b1_issue"] = time.perf_counter()
+        w1 = dist.all_reduce(buf[:m], op=dist.ReduceOp.SUM, async_op=True)
+        if rec is not None:
+            fut = w1.get_future()
+            fut.then(lambda _f: rec.__setitem__("b1_done", time.perf_counter()))
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rec["tail_enqueue"] = time.perf_counter()
+        run_tail()
+        if rec is not None:
+            e1.record()
+        self._pack_tab(grad, m, self.tab2, self.nr2, n2, 0)
+        w2 = dist.all_reduce(buf[m:m + n2], op=dist.ReduceOp.SUM, async_op=True) if n2 > 0 else None
+        w1.wait()
+        self._pack_tab(grad, 0, self.tab1, self.nr1, n1, 1)
+        self.small_dev.copy_(buf[n1:m])
+        if w2 is not None:
+            w2.wait()
+            self._pack_tab(grad, m, self.tab2, self.nr2, n2, 1)
+        self.bytes_last = (m + n2) * 4
+        if rec is not None:
+            e1.synchronize()
+            rec["b_all_done"] = time.perf_counter()
+            rec["tail_gpu_ms"] = e0.elapsed_time(e1)
+            rec["n1"], rec["n2"] = n1, n2
+            self.overlap_log.append(rec)
+        hb = self.host_small[self._flip]
+        ex = None
+        if extra is not None:
+            if getattr(self, "_extra_host", None) is None or self._extra_host[0].shape != extra.shape:
+                self._extra_host = [torch.zeros(extra.shape, dtype=extra.dtype, pin_memory=hb.is_pinned())
+                                    for _ in range(2)]
+            ex = self._extra_host[self._flip]
+            ex.copy_(extra, non_blocking=True)
+        self._flip ^= 1
+        hb.copy_(self.small_dev, non_blocking=True)
+        ev = torch.cuda.Event() if hb.is_pinned() else None
+        if ev is not None:
+            ev.record()
+        return (ev, hb, ex)
 
     @property
     def dense(self) -> bool:

@@ -111,6 +111,10 @@ class HipEngine:
         self.g_rollout = None
         self.g_opt = None
         self.ga_dev = None
+        # overlapped all-reduce (TrainConfig.overlap_allreduce, world > 1): the rollout graph is captured as a head
+        # (everything but the first layer's backward) and a tail (that backward), replayed around the bucket-1
+        # all-reduce (parallel/comm.py exchange_async_split)
+        self.split = False
         # LSTM nets: fused HIP LSTM cell (csrc/lstm.hip) when the widths are multiples of 64; otherwise
         # the hybrid path (HIP trunk + autograd LSTM/heads/loss, dL/dfeat fed back to the HIP trunk backward)
         self.lstm_hip = hp.lstm is not None
@@ -222,7 +226,7 @@ class HipEngine:
         self.blk_end = torch.tensor(end, dtype=torch.int64, device=dev)
         self.seg_blk0 = torch.tensor(blk0, dtype=torch.int32, device=dev)
         self.nblk = len(seg_id)
-        self.partial = torch.zeros(self.nblk, dtype=torch.float32, device=dev)
+        self.partial = torch.zeros(self.nblk + 1, dtype=torch.float32, device=dev)
         # 1.0 when the last optimizer step found a non-finite (all-reduced) gradient and skipped itself
         self.opt_status = torch.zeros(1, dtype=torch.float32, device=dev)
         # [loss_pi, loss_v, entropy, spare, previous optimizer step skipped] read back per update (pipelined mode)
@@ -278,10 +282,12 @@ class HipEngine:
                          xrow0=xrow0 + p0 * self.E if l == 0 else None)
             x = self.acts[l]
 
-    def _layer_bwd_all(self, T):
+    def _layer_bwd_all(self, T, lo: int = 0, hi: Optional[int] = None):
+        """Backward of layers hi-1 .. lo (default: all)."""
         hp = self.hip
         P, E = self.P, self.E
-        for l in range(len(hp.geoms) - 1, -1, -1):
+        hi = len(hp.geoms) if hi is None else hi
+        for l in range(hi - 1, lo - 1, -1):
             if l == 0 and self.ring:
                 hp.ring_wgrad(self.frames, self.fc, self.grads[0], self.bits[0], self.grad_flat, P, E, T,
                               self.bits_rows[0])
@@ -357,7 +363,12 @@ class HipEngine:
         self._fitness_update()
         self.lstm_state = (h.detach(), c.detach())
 
-    def _rollout_backward_body(self):
+    def _rollout_backward_body(self, part: Optional[str] = None):
+        """part None: the whole rollout + backward; "head": all of it except the first layer's backward; "tail":
+        the first layer's backward only (the overlapped all-reduce runs between them, parallel/comm.py)."""
+        if part == "tail":
+            self._layer_bwd_all(self.T, 0, 1)
+            return
         if self.hybrid:
             return self._rollout_backward_hybrid()
         T, P, E, B = self.T, self.P, self.E, self.B
@@ -384,7 +395,7 @@ class HipEngine:
             feat = self.acts[L - 1][:T].reshape(T * B, -1)
             hp.heads_bwd(feat, self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1), self.grad_flat,
                          self.grads[L - 1], task=self.model.task)
-        self._layer_bwd_all(T)
+        self._layer_bwd_all(T, 1 if part == "head" else 0)
 
     def _rollout_split(self):
         """The rollout as independent per-path-group chains (forward -> sample -> env step, T times, then the
@@ -552,12 +563,18 @@ class HipEngine:
         torch.cuda.synchronize()
         par = self._par
         self.g_rollouts = []
+        self.g_tails = []
         for q in ((0, 1) if self._obs_bufs is not None else (par,)):      # one rollout graph per obs parity
             self._par = q
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._rollout_backward_body()
+                self._rollout_backward_body("head" if self.split else None)
             self.g_rollouts.append(g)
+            if self.split:
+                gt = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gt):
+                    self._rollout_backward_body("tail")
+                self.g_tails.append(gt)
         self._par = par
         self.g_rollout = self.g_rollouts[0]
         self.g_opt = torch.cuda.CUDAGraph()
@@ -565,16 +582,22 @@ class HipEngine:
             self._optimizer_body()
         torch.cuda.synchronize()
 
-    def rollout_backward(self):
+    def rollout_backward(self, part: Optional[str] = None):
+        """Replay (or run) the rollout + backward; with ``split``, part "head" then part "tail"."""
+        if part is None and self.split:
+            self.rollout_backward("head")
+            self.rollout_backward("tail")
+            return
         if self.use_graph:
             if self.g_rollout is None:
                 # first update eagerly (validates every launch), capture for the next ones
-                self._rollout_backward_body()
+                self._rollout_backward_body(part)
                 self._pending_capture = True
                 return
-            self.g_rollouts[self._par if self._obs_bufs is not None else 0].replay()
+            gi = self._par if self._obs_bufs is not None else 0
+            (self.g_tails[gi] if part == "tail" else self.g_rollouts[gi]).replay()
         else:
-            self._rollout_backward_body()
+            self._rollout_backward_body(part)
 
     def optimizer_step(self, lr: float, skip: bool = False):
         """``skip``: host-decided skip (tests); non-finite gradients are skipped by the kernel itself."""

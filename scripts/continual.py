@@ -26,8 +26,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def build_cfg(args, tasks):
     from pathnet_gym_amd.config import preset
-    cfg = preset("atari4")
+    cfg = preset(args.preset)
     cfg.tasks = list(tasks)
+    cfg.env = cfg.tasks[0]
+    if args.paths is None:
+        args.paths = cfg.paths
+    if args.envs is None:
+        args.envs = cfg.envs_per_path
+    if args.tmax is None:
+        args.tmax = cfg.a2c.t_max
     cfg.net.num_tasks = len(cfg.tasks)
     cfg.net.per_task_heads = True
     cfg.net.N = args.N
@@ -102,9 +109,11 @@ def main():
     ap.add_argument("--tasks", default="Pong,Breakout,SpaceInvaders,Alien")
     ap.add_argument("--frames", default="25000000",
                     help="agent frames per task: one number, or one per task (comma-separated)")
-    ap.add_argument("--paths", type=int, default=16)
-    ap.add_argument("--envs", type=int, default=16)
-    ap.add_argument("--tmax", type=int, default=5)
+    ap.add_argument("--preset", default="atari4",
+                    help="atari4 (FF 5-layer trunk) | reference (L=4 + LSTM 256, T=20: the reference's own network)")
+    ap.add_argument("--paths", type=int, default=None, help="default: 16 (atari4), the preset's (reference)")
+    ap.add_argument("--envs", type=int, default=None, help="default: 16 (atari4), the preset's (reference)")
+    ap.add_argument("--tmax", type=int, default=None, help="default: 5 (atari4), the preset's (reference)")
     ap.add_argument("--N", type=int, default=4)
     ap.add_argument("--trunk-scale", default=None, choices=["M", "none"])
     ap.add_argument("--lr", type=float, default=None)
@@ -117,6 +126,10 @@ def main():
                     help="only the from-scratch control runs of tasks >= 2 (e.g. in a separate job)")
     ap.add_argument("--out", default="gpurun_out/continual.json")
     args = ap.parse_args()
+    if args.preset == "atari4":
+        args.paths = args.paths or 16
+        args.envs = args.envs or 16
+        args.tmax = args.tmax or 5
     import numpy as np
     import torch
     from pathnet_gym_amd import _build
@@ -139,7 +152,7 @@ def main():
     def write_out(stage):
         out = {"experiment": "continual", "reference": "doom_pathnet.py:274-293, aliencentipede.txt:55-93",
                "stage": stage, "tasks": tasks, "frames_per_task": args.frames_per_task, "n_gpus": 1,
-               "config": {"paths": args.paths, "envs_per_path": args.envs, "t_max": args.tmax, "N": args.N,
+               "config": {"preset": args.preset, "use_lstm": cfg.net.use_lstm, "L": cfg.net.L, "paths": args.paths, "envs_per_path": args.envs, "t_max": args.tmax, "N": args.N,
                           "M": cfg.net.M, "B": cfg.ga.B, "trunk_scale": cfg.net.trunk_scale, "lr": cfg.a2c.lr,
                           "per_task_heads": True, "freeze_union": cfg.ga.freeze_union, "seed": args.seed,
                           "env_reduction": cfg.a2c.env_reduction, "dtype": tr.compute_dtype if tr else None},

@@ -45,6 +45,7 @@ def _worker(rank, world, port, q):
         cfg.net.N = 2                         # sparse unions at this small population size
         cfg.check_every = 1
         cfg.tasks = ["Pong", "Pong"]
+        cfg.overlap_allreduce = False         # the single-bucket exchange (the split one: tests below)
         tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
         assert tr.pipelined and tr.engine.use_graph and not tr.comm.force_dense
         out = {"grad_checks": 0, "grad_ok": True}
@@ -59,9 +60,26 @@ def _worker(rank, world, port, q):
             dist.all_gather(parts, local)
             tot = parts[0] + parts[1]
             red = grad.detach().cpu()
+            inside = torch.zeros(local.numel(), dtype=torch.bool)
             for s, e in comm.ranges:
+                inside[s:e] = True
                 if not torch.equal(red[s:e], tot[s:e]):
                     out["grad_ok"] = False
+            # outside the plan: untouched by the reduce, and zero unless the module is frozen (a frozen module on a
+            # path still gets a local gradient that the optimizer discards); a plan lagging the rollout fails here
+            if not torch.equal(red[~inside], local[~inside]):
+                out["grad_ok"] = False
+            frozen_mask = torch.zeros(local.numel(), dtype=torch.bool)
+            fz = tr.pop.frozen > 0.5
+            lay = tr.model.store.layout
+            for l in range(cfg.net.L):
+                for j in range(cfg.net.M):
+                    if fz[l, j]:
+                        s, e = lay.module_range(l, j)
+                        frozen_mask[s:e] = True
+            if torch.count_nonzero(local[~inside & ~frozen_mask]) != 0:
+                out["grad_ok"] = False
+                out["stray"] = int(torch.count_nonzero(local[~inside & ~frozen_mask]))
             out["grad_checks"] += 1
             return n
         comm._reduce = checked
@@ -116,3 +134,106 @@ def test_two_gloo_ranks_on_one_gpu_hip_engine_device_ga_pipelined(hip_lib):
         assert not o["dense_task1"] and o["frozen_excluded"]
         assert o["bytes_task1"] < o["dense_bytes"]
     assert np.array_equal(a["flat"], b["flat"]) and a["gen"] == b["gen"]
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# overlapped all-reduce (TrainConfig.overlap_allreduce) and 4 ranks with tournaments firing
+# ---------------------------------------------------------------------------------------------------------------
+def _overlap_worker(rank, world, port, q, updates, trace_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), PATHNET_DIST_BACKEND="gloo")
+    torch.set_num_threads(2)
+    try:
+        from pathnet_gym_amd.algo.trainer import PathNetTrainer
+        from pathnet_gym_amd.config import preset
+        from pathnet_gym_amd.parallel.dist import init_distributed
+        ctx = init_distributed()
+        out = {}
+        for mode in ("overlap", "serial"):
+            cfg = preset("pong")
+            cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 4
+            cfg.ga.backend = "device"
+            cfg.ga.concurrent_tournaments = 2
+            cfg.ga.fitness_window = 2           # small window: tournaments fire during the run
+            cfg.net.N = 2
+            cfg.compute_dtype = "fp32"          # fixed-order reductions: bit-reproducible, so the modes compare bitwise
+            cfg.overlap_allreduce = mode == "overlap"
+            tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
+            tr.env.max_episode_steps = 6
+            assert tr.engine.split == (mode == "overlap")
+            if mode == "overlap":
+                tr.comm.overlap_log = []
+            for _ in range(updates):
+                tr.update()
+            tr.flush()
+            torch.cuda.synchronize()
+            out[mode] = dict(flat=tr.model.store.flat.detach().cpu().numpy().copy(), gen=tr.pop.generation,
+                             geno=tr.pop.genotypes.copy(), ms=tr.opt.ms.detach().cpu().numpy().copy())
+            if mode == "overlap":
+                log = tr.comm.overlap_log
+                out["log"] = log
+                out["split_n"] = (tr.comm.n1, tr.comm.n2)
+                if trace_path and rank == 0:
+                    import json
+                    ev = []
+                    t0 = log[0]["b1_issue"]
+                    for i, r in enumerate(log[1:], 1):
+                        us = lambda t: (t - t0) * 1e6
+                        ev.append(dict(name=f"bucket-1 all-reduce (u{i}, {r['n1']} grads + fitness + counters)",
+                                       ph="X", pid=rank, tid="comm (gloo)", ts=us(r["b1_issue"]),
+                                       dur=us(r["b1_done"]) - us(r["b1_issue"])))
+                        ev.append(dict(name=f"first-layer backward graph (u{i}, {r['tail_gpu_ms']:.3f} ms on the GPU)",
+                                       ph="X", pid=rank, tid="compute stream", ts=us(r["tail_enqueue"]),
+                                       dur=r["tail_gpu_ms"] * 1e3))
+                        ev.append(dict(name=f"bucket-2 all-reduce + unpack (u{i}, {r['n2']} grads)", ph="X", pid=rank,
+                                       tid="comm (gloo)", ts=us(r["b1_done"]),
+                                       dur=max(0.0, us(r["b_all_done"]) - us(r["b1_done"]))))
+                    with open(trace_path, "w") as f:
+                        json.dump({"traceEvents": ev}, f)
+        q.put((rank, out))
+        ctx.destroy()
+    except Exception:   # pragma: no cover
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+def _run_ranks(world, updates, trace_path=None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_overlap_worker, args=(r, world, port, q, updates, trace_path)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+    return res
+
+
+def test_overlapped_allreduce_is_bit_equal_to_serial(hip_lib):
+    """Two gloo ranks: the split exchange (bucket 1 reduced while the first layer's weight gradient runs) gives
+    bit-identical weights, RMSProp slots and GA state to the single-bucket exchange; bucket 1 is still in flight
+    when the first-layer backward is enqueued (the overlap)."""
+    res = _run_ranks(2, 10, os.environ.get("PATHNET_OVERLAP_TRACE"))
+    for r in range(2):
+        o, s = res[r]["overlap"], res[r]["serial"]
+        assert np.array_equal(o["flat"], s["flat"]) and np.array_equal(o["ms"], s["ms"])
+        assert o["gen"] == s["gen"] and np.array_equal(o["geno"], s["geno"])
+        n1, n2 = res[r]["split_n"]
+        assert n1 > 0 and n2 > 0
+        log = res[r]["log"]
+        assert len(log) == 10
+        assert all(x["b1_issue"] <= x["tail_enqueue"] <= x["b_all_done"] for x in log)
+        assert sum(x["tail_enqueue"] < x["b1_done"] for x in log) >= 5      # tail issued before bucket 1 finished
+    assert np.array_equal(res[0]["overlap"]["flat"], res[1]["overlap"]["flat"])
+
+
+def test_four_gloo_ranks_tournaments_fire_and_replicas_agree(hip_lib):
+    res = _run_ranks(4, 12)
+    gens = [res[r]["overlap"]["gen"] for r in range(4)]
+    assert gens[0] > 0 and len(set(gens)) == 1, gens
+    for r in range(1, 4):
+        assert np.array_equal(res[0]["overlap"]["flat"], res[r]["overlap"]["flat"])
+        assert np.array_equal(res[0]["overlap"]["geno"], res[r]["overlap"]["geno"])

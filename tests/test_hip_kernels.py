@@ -3,12 +3,16 @@
 Every test compares a hand-written gfx950 kernel against a plain PyTorch
 fp32 implementation of the same op (``models/pathnet.py``,
 ``algo/a2c_math.py``, ``algo/optim.py``, ``envs/*.py``).  bf16 MFMA operands
-give ~1e-2 relative error; envs are integer/bit exact.
+give ~1e-3 .. 1e-2 relative error: every budget is 3x the measured error of that layer / segment / path
+(tests/numerics_budget.py, tests/data/numerics_measured.json); envs are integer/bit exact.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
+import numerics_budget as budget
 from pathnet_gym_amd.algo.a2c_math import a2c_loss, nstep_returns
 from pathnet_gym_amd.algo.ga import Population, get_geopath
 from pathnet_gym_amd.config import LayerSpec, PathNetConfig, preset
@@ -62,9 +66,15 @@ def test_trunk_forward_matches_oracle(hip_lib):
         ref = trunk_forward_ref(m.store, obs.float() / 255.0, m.mask.repeat_interleave(E, 0))
     assert feat.shape == ref.shape
     # path 0 has an empty layer 1 -> every later layer sees zeros
+    errs = {}
     for p in range(P):
         sl = slice(p * E, (p + 1) * E)
-        assert rel(feat[sl], ref[sl]) < 3e-2, (p, rel(feat[sl], ref[sl]))
+        if ref[sl].norm() == 0:
+            assert feat[sl].norm() == 0, p
+            continue
+        errs[f"path{p}"] = rel(feat[sl], ref[sl])
+    print("bf16 trunk forward vs fp32 oracle:", errs)
+    budget.check("trunk_forward_bf16", errs, 3e-2)
 
 
 def test_conv1_fp16_offset_forward_is_tight(hip_lib):
@@ -131,7 +141,7 @@ def test_fc_trunk_forward_vector_input(hip_lib):
     feat = m.hip.trunk(x, E)
     with torch.no_grad():
         ref = trunk_forward_ref(m.store, x.to(torch.bfloat16).float(), m.mask.repeat_interleave(E, 0))
-    assert rel(feat, ref) < 3e-2
+    budget.check("fc_trunk_forward_bf16", {"all": rel(feat, ref)}, 3e-2)
 
 
 def _hip_trunk_fwd_bwd(m, obs_steps, dfeat, P, E):
@@ -184,7 +194,8 @@ def test_trunk_backward_matches_autograd(hip_lib, wgrad_gm):
     feat_ref = trunk_forward_ref(st, x, mask, emulate_bf16=True)
     (feat_ref * dfeat).sum().backward()
     gref = flat.grad
-    assert rel(feat_hip, feat_ref.detach()) < 1e-2
+    test = f"trunk_backward_bf16_{'gm' if wgrad_gm else 'tiles'}"
+    budget.check(test + "_fwd", {"feat": rel(feat_hip, feat_ref.detach())}, 1e-2)
     lay = m.store.layout
     errs = {}
     for s in lay.segments:
@@ -198,15 +209,15 @@ def test_trunk_backward_matches_autograd(hip_lib, wgrad_gm):
         errs[s.name] = rel(a, b)
     print({k: round(v, 4) for k, v in errs.items()})
     assert len(errs) > 20
-    # a wiring error is systematic: every layer's WHOLE gradient (all modules) must match tightly;
-    # single sparse modules (few contributing rows, cancelling random dfeat) may show more bf16 noise
+    # every layer's WHOLE gradient (all modules) and every segment, each within 3x its measured error
+    layer = {}
     for l in range(cfg.L):
         segs = [x for x in lay.segments if x.layer == l]
         a = torch.cat([grad_hip[x.offset:x.offset + x.numel] for x in segs])
         b = torch.cat([gref[x.offset:x.offset + x.numel] for x in segs])
-        assert rel(a, b) < 3e-2, (l, rel(a, b))
-    worst = max(errs, key=errs.get)
-    assert errs[worst] < 6e-2, (worst, errs[worst])
+        layer[f"layer{l}"] = rel(a, b)
+    budget.check(test + "_layers", layer, 3e-2)
+    budget.check(test + "_segments", errs, 6e-2)
 
 
 def test_fc_backward_vector(hip_lib):
@@ -358,6 +369,21 @@ def test_rmsprop_kernel_matches_torch(hip_lib):
     eng._optimizer_body()
     torch.cuda.synchronize()
     assert torch.equal(tr.model.store.flat.detach(), w1) and torch.equal(tr.opt.ms, m1)
+    # finite entries whose sum of squares overflows fp32: NOT skipped -- clip_by_norm scales that segment to 0
+    # (tf.clip_by_norm's t * clip / max(inf, clip)) and every other segment steps normally
+    s1 = tr.model.store.layout.by_name["layer1.module0.weight"]
+    gbig = g.clone()
+    gbig[s1.offset:s1.offset + 64] = 1e30
+    with torch.no_grad():
+        tr.model.store.flat.copy_(flat0)
+    tr.opt.ms.copy_(ms_before)
+    eng.grad_flat.copy_(gbig)
+    eng._optimizer_body()
+    torch.cuda.synchronize()
+    assert float(eng.opt_status) == 0.0 and torch.isfinite(tr.model.store.flat).all()
+    seg1 = slice(s1.offset, s1.offset + s1.numel)
+    assert torch.equal(tr.model.store.flat[seg1], flat0[seg1])          # zero gradient, zero momentum
+    assert torch.equal(tr.model.store.flat[:s1.offset], w1[:s1.offset])
 
 
 def test_pong_env_hip_bit_exact_vs_torch(hip_lib):
@@ -520,8 +546,9 @@ def test_engine_gradient_matches_oracle(hip_lib, graph, ring):
     mask = tr.model.mask.repeat_interleave(E, 0).repeat(T + 1, 1, 1)
     feat = trunk_forward_ref(st, x, mask, emulate_bf16=True)
     logits, values = heads_ref(st, feat)
-    assert rel(logits[:T * B], eng.logits[:T].reshape(-1, A)) < 3e-2
-    assert rel(values, eng.values[:T + 1].reshape(-1)) < 3e-2
+    test = f"engine_bf16_vs_emulated_{'graph' if graph else 'eager'}_{'ring' if ring else 'packed'}"
+    budget.check(test + "_fwd", {"logits": rel(logits[:T * B], eng.logits[:T].reshape(-1, A)),
+                                 "values": rel(values, eng.values[:T + 1].reshape(-1))}, 3e-2)
     R, adv = nstep_returns(eng.rewards, eng.values[:T], eng.dones.bool(), eng.values[T], a2c.gamma,
                            a2c.gae_lambda, a2c.reward_clip)
     loss, lp, lv, ent = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(), R.reshape(-1),
@@ -529,29 +556,51 @@ def test_engine_gradient_matches_oracle(hip_lib, graph, ring):
                                  torch.full((T * B,), eng.weight, device=DEV))
     loss.backward()
     g_ref, g_hip = flat.grad, eng.grad_flat
-    errs = {}
-    for s in tr.model.store.layout.segments:
+    errs = grad_errors(tr, g_hip, g_ref)
+    print({k: round(v, 4) for k, v in sorted(errs.items(), key=lambda kv: -kv[1])[:8]})
+    budget.check(test, errs, 6e-2)
+
+
+def grad_errors(tr, g_hip, g_ref, big=0.2):
+    """{"layer<l>" / "policy" / "value": error of the group's whole gradient} + {segment: error} for segments
+    carrying >= ``big`` x the largest segment gradient of their group (a module few rows reach is dominated by
+    bf16 noise: its share of the layer error is what the layer key bounds)."""
+    segs = tr.model.store.layout.segments
+    key_of = lambda s: f"layer{s.layer}" if s.layer >= 0 else s.name.split(".")[0]      # noqa: E731
+    top, parts, errs = {}, {}, {}
+    for s in segs:
+        top[key_of(s)] = max(top.get(key_of(s), 0.0), float(g_ref[s.offset:s.offset + s.numel].norm()))
+    for s in segs:
         a, b = g_hip[s.offset:s.offset + s.numel], g_ref[s.offset:s.offset + s.numel]
+        parts.setdefault(key_of(s), []).append((a, b))
         if b.norm() < 1e-7:
             assert a.norm() < 1e-4 * max(1.0, float(g_ref.norm())), s.name
             continue
-        errs[s.name] = rel(a, b)
-    worst = max(errs, key=errs.get)
-    print({k: round(v, 4) for k, v in sorted(errs.items(), key=lambda kv: -kv[1])[:8]})
-    assert errs[worst] < 6e-2, (worst, errs[worst])
+        if float(b.norm()) >= big * top[key_of(s)]:
+            errs[s.name] = rel(a, b)
+    for k, v in parts.items():
+        errs[k] = rel(torch.cat([a for a, _ in v]), torch.cat([b for _, b in v]))
+    return errs
 
 
-# relative-error budget of the engine gradient vs a PLAIN fp32 oracle (no bf16 emulation), per layer
-# (all modules of the layer together) and per single segment: heads see bf16 features only; earlier layers
-# accumulate the bf16 rounding of every activation and weight operand on the way back (measured values:
-# profiles/r2_engine_fp32_oracle.md)
-FP32_LAYER_BUDGET = {"policy": 1e-2, "value": 3e-2, 4: 5e-2, 3: 5e-2, 2: 8e-2, 1: 7e-2, 0: 6e-2}
-FP32_SEG_BUDGET = 2.5e-1      # for segments carrying >= 20 % of the largest segment gradient of their layer
+def scaled_module_violations(tr, g_hip, g_ref, test, fallback, factor=1.02):
+    """Negative control: per layer, the largest active module's weight gradient x ``factor`` -> the budget
+    violations it causes (must be non-empty for every layer)."""
+    out = {}
+    lay = tr.model.store.layout
+    for l in range(tr.cfg.net.L):
+        ws = [s for s in lay.segments if s.layer == l and s.name.endswith(".weight")]
+        s = max(ws, key=lambda x: float(g_ref[x.offset:x.offset + x.numel].norm()))
+        bad = g_hip.clone()
+        bad[s.offset:s.offset + s.numel] *= factor
+        out[s.name] = budget.violations(test, grad_errors(tr, bad, g_ref), fallback)
+    return out
 
 
 def test_engine_gradient_vs_plain_fp32_oracle(hip_lib):
-    """Whole-update gradient of the bf16 HIP engine vs the fp32 autograd oracle WITHOUT bf16 emulation,
-    at a small shape, with an explicit error budget per segment group."""
+    """Whole-update gradient of the bf16 HIP engine vs the fp32 autograd oracle WITHOUT bf16 emulation, at a
+    small shape: every layer and every major segment within 3x its measured error (tests/numerics_budget.py);
+    a 2 % error in any layer's largest module must break that budget (negative control)."""
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     from pathnet_gym_amd.models.pathnet import ParamStore
     cfg = preset("pong")
@@ -578,28 +627,14 @@ def test_engine_gradient_vs_plain_fp32_oracle(hip_lib):
                                  torch.full((T * B,), eng.weight, device=DEV))
     loss.backward()
     g_ref, g_hip = flat.grad, eng.grad_flat
-    worst, parts = {}, {}
-    segs = tr.model.store.layout.segments
-    key_of = lambda s: s.layer if s.layer >= 0 else s.name.split(".")[0]      # noqa: E731
-    top = {}
-    for s in segs:
-        top[key_of(s)] = max(top.get(key_of(s), 0.0), float(g_ref[s.offset:s.offset + s.numel].norm()))
-    for s in segs:
-        a, b = g_hip[s.offset:s.offset + s.numel], g_ref[s.offset:s.offset + s.numel]
-        key = key_of(s)
-        parts.setdefault(key, []).append((a, b))
-        if b.norm() < 1e-7:
-            assert a.norm() < 1e-4 * max(1.0, float(g_ref.norm())), s.name
-            continue
-        if float(b.norm()) >= 0.2 * top[key]:      # sparse modules (a few rows) are bf16-noise dominated
-            worst[key] = max(worst.get(key, (0.0, "")), (rel(a, b), s.name))
-    layer_err = {k: rel(torch.cat([a for a, _ in v]), torch.cat([b for _, b in v])) for k, v in parts.items()}
-    print("layer", {k: round(v, 4) for k, v in layer_err.items()},
-          "worst segment", {k: (round(v, 4), n) for k, (v, n) in worst.items()})
-    for k, v in layer_err.items():
-        assert v < FP32_LAYER_BUDGET[k], (k, v)
-    for k, (v, n) in worst.items():
-        assert v < FP32_SEG_BUDGET, (k, n, v)
+    errs = grad_errors(tr, g_hip, g_ref)
+    print("bf16 engine vs plain fp32 oracle:", {k: round(v, 5) for k, v in errs.items()})
+    test = "engine_bf16_vs_plain_fp32"
+    budget.check(test, errs, 2.5e-1)
+    if not os.environ.get("PATHNET_RECORD_NUMERICS") and budget._load(budget.MEASURED).get(test):
+        neg = scaled_module_violations(tr, g_hip, g_ref, test, 2.5e-1)
+        print("1.02-scaled module -> violations:", {k: len(v) for k, v in neg.items()})
+        assert all(len(v) > 0 for v in neg.values()), neg
 
 
 def test_bf16_conv_gradients_match_fp32(hip_lib):
@@ -625,14 +660,16 @@ def test_bf16_conv_gradients_match_fp32(hip_lib):
                            eng.dvalue.reshape(-1), eng.grad_flat, eng.grads[L - 1], task=tr.model.task)
     eng._layer_bwd_all(T)
     torch.cuda.synchronize()
-    assert rel(acts_bf[1], eng.grads[1]) < 5e-3
-    assert rel(acts_bf[0], eng.grads[0]) < 1e-2
+    budget.check("bf16_conv_act_grads", {"grads1": rel(acts_bf[1], eng.grads[1]),
+                                         "grads0": rel(acts_bf[0], eng.grads[0])}, 1e-2)
+    errs = {}
     for s in tr.model.store.layout.segments:
         a, b = g_bf[s.offset:s.offset + s.numel], eng.grad_flat[s.offset:s.offset + s.numel]
         if b.norm() < 1e-7:
             assert a.norm() < 1e-5, s.name
             continue
-        assert rel(a, b) < (2e-2 if s.layer in (0, 1) else 1e-3), (s.name, rel(a, b))
+        errs[s.name] = rel(a, b)
+    budget.check("bf16_conv_act_grads_wgrad", errs, 2e-2)
 
 
 def test_frame_ring_stacks_match_packed_env(hip_lib):
@@ -701,8 +738,7 @@ def test_lstm_cell_kernels_match_autograd(hip_lib):
     xr = x.float().requires_grad_(True)
     hin = (h.float() * keep).requires_grad_(True)
     h2, c2 = lstm_cell_ref(xr, hin, c * keep, bf16_ste(k), b)
-    assert rel(hout.float(), h2.detach()) < 1e-2
-    assert rel(cout, c2.detach()) < 1e-2
+    errs = {"h": rel(hout.float(), h2.detach()), "c": rel(cout, c2.detach())}
     assert torch.equal(xh[:, :F], x) and torch.equal(xh[:, F:].float(), hin.detach().to(torch.bfloat16).float())
     dh = torch.randn(B, H, generator=g).to(DEV)
     (h2 * dh).sum().backward()
@@ -714,12 +750,14 @@ def test_lstm_cell_kernels_match_autograd(hip_lib):
     hp.lstm_bwd_step(dh, None, None, None, gates, cout, c, done, dz, dc_out, dx, dh_prev)
     hp.lstm_wgrad(xh, dz, gflat, rows_per_chunk=32)
     torch.cuda.synchronize()
-    assert rel(dx, xr.grad) < 2e-2
-    assert rel(dh_prev, hin.grad) < 2e-2
+    errs["dx"] = rel(dx, xr.grad)
+    errs["dh_prev"] = rel(dh_prev, hin.grad)
     lay = m.store.layout
     for name in ("lstm.kernel", "lstm.bias"):
         s_ = lay.by_name[name]
-        assert rel(gflat[s_.offset:s_.offset + s_.numel], flat.grad[s_.offset:s_.offset + s_.numel]) < 2e-2, name
+        errs[name] = rel(gflat[s_.offset:s_.offset + s_.numel], flat.grad[s_.offset:s_.offset + s_.numel])
+    print("lstm cell kernels:", errs)
+    budget.check("lstm_cell_kernels", errs, 2e-2)
 
 
 def test_engine_lstm_gradient_matches_oracle(hip_lib):
@@ -755,22 +793,16 @@ def test_engine_lstm_gradient_matches_oracle(hip_lib):
         h, c = lstm_cell_ref(bf16_ste(feat[t]), bf16_ste(h), c, kq, bb)
         hs.append(h)
     logits, values = heads_ref(st, bf16_ste(torch.stack(hs)).reshape((T + 1) * B, -1))
-    assert rel(logits[:T * B], eng.logits[:T].reshape(-1, A)) < 3e-2
+    budget.check("engine_lstm_fwd", {"logits": rel(logits[:T * B], eng.logits[:T].reshape(-1, A))}, 3e-2)
     R, adv = nstep_returns(eng.rewards, eng.values[:T], eng.dones.bool(), eng.values[T], a2c.gamma,
                            a2c.gae_lambda, a2c.reward_clip)
     loss, _, _, _ = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(), R.reshape(-1),
                              adv.reshape(-1), a2c.entropy_beta, a2c.value_coef,
                              torch.full((T * B,), 1.0 / E, device=DEV))
     loss.backward()
-    errs = {}
-    for s_ in tr.model.store.layout.segments:
-        a, b = eng.grad_flat[s_.offset:s_.offset + s_.numel], flat.grad[s_.offset:s_.offset + s_.numel]
-        if b.norm() < 1e-7:
-            continue
-        errs[s_.name] = rel(a, b)
-    worst = max(errs, key=errs.get)
+    errs = grad_errors(tr, eng.grad_flat, flat.grad)
     print({k_: round(v, 4) for k_, v in sorted(errs.items(), key=lambda kv: -kv[1])[:8]})
-    assert errs[worst] < 8e-2, (worst, errs[worst])
+    budget.check("engine_lstm", errs, 8e-2)
 
 
 @pytest.mark.parametrize("E", [16, 32])

@@ -48,15 +48,11 @@ def test_x2_pair_helpers(hip_lib):
     t = x2_alloc((3, 5), DEV)
     assert x2_lo(t) == 15 and x2_lo(t[1]) == 15
     v = torch.rand(3, 5, device=DEV)
-    full = torch.empty(0, dtype=torch.float16, device=DEV).set_(t.untyped_storage(), 0, (4, 3, 5), (15, 5, 1))
+    full = torch.empty(0, dtype=torch.float16, device=DEV).set_(t.untyped_storage(), 0, (2, 3, 5), (15, 5, 1))
     hi = v.half()
     full[0].copy_(hi)
     full[1].copy_((v - hi.float()).half())
-    bh = v.bfloat16()
-    full[2].copy_(bh.view(torch.float16))
-    full[3].copy_((v - bh.float()).bfloat16().view(torch.float16))
     assert rel(x2_value(t), v) < 1e-6
-    assert rel(x2_value(t, "bf16"), v) < 2e-5
     with pytest.raises(ValueError):
         x2_lo(torch.zeros(4, dtype=torch.float16, device=DEV)[:1].expand(4))
 
