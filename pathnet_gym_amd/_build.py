@@ -7,8 +7,11 @@ loaded with ctypes after torch, so it shares torch's HIP runtime
 (libamdhip64.so.7).  An object is rebuilt when the SHA-256 of its source,
 the shared headers and the compile flags differs from the stamp written next
 to it (``<obj>.sha``); the library is relinked when the combined stamp of
-its objects changes.  File mtimes are never trusted: a snapshot pushed to a
-GPU box with skewed mtimes still rebuilds exactly what changed.
+its objects changes.  The stamp also records the SHA-256 of the built file itself,
+which is re-verified before the file is trusted: an object or library that does not
+match its stamp (e.g. a stale file shipped next to a fresh stamp) is rebuilt.  File
+mtimes are never trusted: a snapshot pushed to a GPU box with skewed mtimes still
+rebuilds exactly what changed.
 """
 from __future__ import annotations
 
@@ -40,16 +43,34 @@ def _digest(paths, extra=()) -> str:
     return h.hexdigest()
 
 
-def _stamp(path) -> str:
+def _file_sha(path) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def _stamp(path):
+    """(input digest, sha256 of the built file) recorded next to ``path``."""
     try:
         with open(path + ".sha") as f:
-            return f.read().strip()
+            lines = f.read().split()
     except OSError:
-        return ""
+        return "", ""
+    return (lines + ["", ""])[0], (lines + ["", ""])[1]
+
+
+def _write_stamp(path, digest):
+    with open(path + ".sha", "w") as f:
+        f.write(digest + "\n" + _file_sha(path) + "\n")
 
 
 def _needs(obj, digest) -> bool:
-    return not os.path.exists(obj) or _stamp(obj) != digest
+    if not os.path.exists(obj):
+        return True
+    d, fsha = _stamp(obj)
+    return d != digest or fsha != _file_sha(obj)
 
 
 def build(verbose: bool = False, jobs: int = 0) -> str:
@@ -75,8 +96,7 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {s}:\n{r.stderr}")
-        with open(o + ".sha", "w") as f:
-            f.write(d)
+        _write_stamp(o, d)
         return o
 
     n = jobs or min(8, max(1, (os.cpu_count() or 2)))
@@ -89,8 +109,7 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
-        with open(LIB + ".sha", "w") as f:
-            f.write(lib_digest)
+        _write_stamp(LIB, lib_digest)
     return LIB
 
 

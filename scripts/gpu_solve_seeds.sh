@@ -13,9 +13,10 @@ grep -E "FAILED|^E  " gpurun_out/pytest_gpu.log | head -20; tail -1 gpurun_out/p
 grep -E "^layer" gpurun_out/pytest_gpu.log | head -3
 fi
 for seed in ${SEEDS:-2 3}; do
+  NAME=pong_bench${DT:+_$DT}_seed$seed
   timeout -k 10 $((${SECS:-480} + 120)) python -u scripts/solve.py --preset pong --ga-backend device --seed $seed \
-      --report-every 30 --minutes $(python3 -c "print(${SECS:-480}/60)") \
-      --curve gpurun_out/solve/pong_bench_seed$seed.jsonl --out gpurun_out/solve/pong_bench_seed$seed.json \
-      > gpurun_out/solve/seed$seed.log 2>&1 || { echo "SOLVE FAIL seed $seed"; tail -5 gpurun_out/solve/seed$seed.log; exit 1; }
-  echo "== seed $seed"; tail -1 gpurun_out/solve/pong_bench_seed$seed.json | cut -c1-330
+      ${DT:+--dtype $DT} --report-every 30 --minutes $(python3 -c "print(${SECS:-480}/60)") \
+      --curve gpurun_out/solve/$NAME.jsonl --out gpurun_out/solve/$NAME.json \
+      > gpurun_out/solve/$NAME.log 2>&1 || { echo "SOLVE FAIL seed $seed"; tail -5 gpurun_out/solve/$NAME.log; exit 1; }
+  echo "== seed $seed"; tail -1 gpurun_out/solve/$NAME.json | cut -c1-330
 done

@@ -2,7 +2,8 @@
 
 Each numerics test reports a dict ``{key: relative error}`` (per layer, per segment, per path ...).  The measured
 values of the committed MI355X runs live in ``tests/data/numerics_measured.json`` ({test: {key: error}}); a key's
-budget is ``HEADROOM`` x its measured error.  A key that was never measured falls back to the test's old loose
+budget is ``HEADROOM`` x its measured error (at least ``HEADROOM`` x 1e-5: a key measured at 0 -- bit-identical
+-- still tolerates the atomic-order noise of the bf16 engine).  A key that was never measured falls back to the test's old loose
 budget.  ``PATHNET_RECORD_NUMERICS=<file>`` records instead of checking (still against the loose fallback, so a
 broken kernel is never recorded): the file keeps the MAX over recording runs, since the bf16 engine's atomic
 weight-gradient reductions make repeated runs differ in the last bits.
@@ -21,7 +22,7 @@ def _load(path):
         return json.load(f)
 
 
-def violations(test, errs, fallback, floor=1e-7):
+def violations(test, errs, fallback, floor=1e-5):
     """[(key, error, budget)] of every key over its budget (the recorded table, else ``fallback``)."""
     table = _load(MEASURED).get(test, {})
     out = []
@@ -33,7 +34,7 @@ def violations(test, errs, fallback, floor=1e-7):
     return out
 
 
-def check(test, errs, fallback, floor=1e-7):
+def check(test, errs, fallback, floor=1e-5):
     """Assert every error in ``errs`` is within budget; in record mode, merge them into the record file."""
     rec = os.environ.get("PATHNET_RECORD_NUMERICS")
     if rec:

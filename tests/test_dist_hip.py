@@ -237,3 +237,75 @@ def test_four_gloo_ranks_tournaments_fire_and_replicas_agree(hip_lib):
     for r in range(1, 4):
         assert np.array_equal(res[0]["overlap"]["flat"], res[r]["overlap"]["flat"])
         assert np.array_equal(res[0]["overlap"]["geno"], res[r]["overlap"]["geno"])
+
+
+def _resume_worker(rank, world, port, q, path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), PATHNET_DIST_BACKEND="gloo")
+    torch.set_num_threads(2)
+    try:
+        from pathnet_gym_amd.algo.trainer import PathNetTrainer
+        from pathnet_gym_amd.config import preset
+        from pathnet_gym_amd.parallel.dist import init_distributed
+        from pathnet_gym_amd.utils import checkpoint as ckpt
+        ctx = init_distributed()
+
+        def make():
+            cfg = preset("pong")
+            cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 4
+            cfg.ga.backend = "device"
+            cfg.ga.concurrent_tournaments = 2
+            cfg.ga.fitness_window = 2
+            cfg.net.N = 2
+            cfg.compute_dtype = "fp32"
+            tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
+            tr.env.max_episode_steps = 6
+            return tr
+        a = make()
+        for _ in range(6):
+            a.update()
+        a.flush()
+        ckpt.save(a, path)
+        ctx.barrier()
+        for _ in range(6):
+            a.update()
+        a.flush()
+        torch.cuda.synchronize()
+        out = {"flat_a": a.model.store.flat.detach().cpu().numpy().copy(), "gen_a": a.pop.generation,
+               "geno_a": a.pop.genotypes.copy()}
+        del a
+        b = make()
+        ckpt.load(b, path)
+        for _ in range(6):
+            b.update()
+        b.flush()
+        torch.cuda.synchronize()
+        out.update(flat_b=b.model.store.flat.detach().cpu().numpy().copy(), gen_b=b.pop.generation,
+                   geno_b=b.pop.genotypes.copy())
+        q.put((rank, out))
+        ctx.destroy()
+    except Exception:   # pragma: no cover
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+def test_two_gloo_ranks_checkpoint_resume_is_exact(hip_lib, tmp_path):
+    """Multi-rank checkpoint -> resume (rank-0 global state + one file per rank: env, engine counters, fitness
+    windows): 6 updates, save, 6 more == a fresh trainer that loads the checkpoint and runs the same 6 (fp32 engine,
+    device GA with tournaments firing, pipelined, overlapped all-reduce)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    path = str(tmp_path / "ck.safetensors")
+    ps = [ctx.Process(target=_resume_worker, args=(r, 2, port, q, path)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r in range(2):
+        o = res[r]
+        assert "error" not in o, o.get("error")
+        assert o["gen_a"] > 0 and o["gen_a"] == o["gen_b"]
+        assert np.array_equal(o["geno_a"], o["geno_b"])
+        assert np.array_equal(o["flat_a"], o["flat_b"])

@@ -559,6 +559,12 @@ def test_engine_gradient_matches_oracle(hip_lib, graph, ring):
     errs = grad_errors(tr, g_hip, g_ref)
     print({k: round(v, 4) for k, v in sorted(errs.items(), key=lambda kv: -kv[1])[:8]})
     budget.check(test, errs, 6e-2)
+    if not graph and not ring and not os.environ.get("PATHNET_RECORD_NUMERICS") \
+            and budget._load(budget.MEASURED).get(test):
+        # negative control: a 2 % error in any layer's largest module breaks the budget
+        neg = scaled_module_violations(tr, g_hip, g_ref, test, 6e-2)
+        print("1.02-scaled module -> violations:", {k: len(v) for k, v in neg.items()})
+        assert all(len(v) > 0 for v in neg.values()), neg
 
 
 def grad_errors(tr, g_hip, g_ref, big=0.2):
@@ -599,8 +605,7 @@ def scaled_module_violations(tr, g_hip, g_ref, test, fallback, factor=1.02):
 
 def test_engine_gradient_vs_plain_fp32_oracle(hip_lib):
     """Whole-update gradient of the bf16 HIP engine vs the fp32 autograd oracle WITHOUT bf16 emulation, at a
-    small shape: every layer and every major segment within 3x its measured error (tests/numerics_budget.py);
-    a 2 % error in any layer's largest module must break that budget (negative control)."""
+    small shape: every layer and every major segment within 3x its measured error (tests/numerics_budget.py)."""
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     from pathnet_gym_amd.models.pathnet import ParamStore
     cfg = preset("pong")
@@ -629,12 +634,11 @@ def test_engine_gradient_vs_plain_fp32_oracle(hip_lib):
     g_ref, g_hip = flat.grad, eng.grad_flat
     errs = grad_errors(tr, g_hip, g_ref)
     print("bf16 engine vs plain fp32 oracle:", {k: round(v, 5) for k, v in errs.items()})
-    test = "engine_bf16_vs_plain_fp32"
-    budget.check(test, errs, 2.5e-1)
-    if not os.environ.get("PATHNET_RECORD_NUMERICS") and budget._load(budget.MEASURED).get(test):
-        neg = scaled_module_violations(tr, g_hip, g_ref, test, 2.5e-1)
-        print("1.02-scaled module -> violations:", {k: len(v) for k, v in neg.items()})
-        assert all(len(v) > 0 for v in neg.values()), neg
+    # bf16 rounding amplified through R - V makes some modules 5-20 % off the PLAIN fp32 gradient (measured,
+    # tests/data/numerics_measured.json): this budget bounds that drift; the wiring check with a 2 % negative
+    # control runs against the bf16-emulating oracle (test_engine_gradient_matches_oracle) and, for fp32-accurate
+    # numbers, in tests/test_x3_engine.py / tests/test_f32_engine.py
+    budget.check("engine_bf16_vs_plain_fp32", errs, 2.5e-1)
 
 
 def test_bf16_conv_gradients_match_fp32(hip_lib):
