@@ -205,6 +205,12 @@ struct SpaceInvaders {
     s[LIVES] -= hitp;
     s[BOMB] = bomb && !hitp && s[BYP] < 196;
     s[SHOT] = shot;
+    if (!any_bits(s + ALIVE, AR * AC)) {      // wave cleared: a new formation marches in from the top
+      fill_bits(s + ALIVE, AR * AC);
+      s[FX] = 22;
+      s[FY] = 40;
+      s[FDIR] = 1;
+    }
     return reward;
   }
   static DEVI bool over(const int* s) {
@@ -213,7 +219,7 @@ struct SpaceInvaders {
       for (int c = 0; c < AC; ++c)
         if (alive(s, r, c)) lowest_row = r;
     const bool invaded = s[FY] + 18 * lowest_row + 10 >= 180;
-    return s[LIVES] <= 0 || !any_bits(s + ALIVE, AR * AC) || invaded;
+    return s[LIVES] <= 0 || invaded;
   }
   static DEVI void scene(const int* s, int16_t* r) {
     rect(r, 0, 195, 0, 2, 160);

@@ -1311,6 +1311,182 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const uint16_t* __restrict__ X,
 }
 
 // ===========================================================================
+// fc forward, MODULE-MAJOR (share each module's weight slice across the paths that use it).
+// The path-major kernel above re-reads a module's [Cout][KP] hi/lo slice once per (path, 64-column tile): 553 MB
+// of L2/MALL traffic per fc1 launch at the bench shape.  Here one workgroup = one active module j x 64 rows (4 row
+// tiles of 16 taken from the paths on j's inverse list, ga.hip ga_compact_inverse_kernel) x all 256 columns, so
+// the slice is read once per 64 rows; 8 waves: wave w owns column quarter w & 3 and k half w >> 2 (split-K, the
+// halves meet in LDS).  relu(W_j x + b_j) goes to the path's slot plane Ys[slot][p*R + r][256] (fp32), the relu
+// bits straight to `bits`; fc_slot_sum_x3 sums every path's slots in slot order (deterministic) into Y.  The
+// (module, chunk) units are walked XCD-major -- XCD x takes the x-th contiguous eighth of the unit list -- so an
+// XCD's L2 holds the slices of ~2 modules rather than all of them.
+// ===========================================================================
+template <int NKS>
+__global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__ X, long xlo, int ldx,
+                                                    float* __restrict__ Ys, uint16_t* __restrict__ bits,
+                                                    const uint16_t* __restrict__ Wc, long wlo,
+                                                    const float* __restrict__ flat, long bias_off, int chunk,
+                                                    const int* __restrict__ inv_path, const int* __restrict__ inv_slot,
+                                                    const int* __restrict__ inv_cnt, int layer, int M, int KP, int P,
+                                                    int E, int T, int t0, long bits_rows, float in_scale) {
+  constexpr int COUT = 256, RTW = 4, D = 2, NWORDS = COUT / 16;
+  __shared__ float red[4][64][64 + 4];                 // k-half-1 partials per column quarter (69.6 KB)
+  const int R = T * E, tpp = (R + 15) / 16;
+  int U = 0;
+  for (int j = 0; j < M; ++j) U += (inv_cnt[layer * M + j] * tpp + RTW - 1) / RTW;
+  const int per = (U + 7) >> 3;
+  const int kx = (int)(blockIdx.x >> 3);
+  int u = (int)(blockIdx.x & 7) * per + kx;
+  if (kx >= per || u >= U) return;
+  int j = 0, ncnt = 0;
+  for (; j < M; ++j) {
+    ncnt = inv_cnt[layer * M + j];
+    const int n = (ncnt * tpp + RTW - 1) / RTW;
+    if (u < n) break;
+    u -= n;
+  }
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int cq = w & 3, kh = w >> 2;
+  const int PE = P * E;
+  const long lbase = ((long)layer * M + j) * P;
+  int xrow[RTW];                                       // element offsets (the activation buffer is < 2^31)
+#pragma unroll
+  for (int i = 0; i < RTW; ++i) {
+    const int tile = u * RTW + i;
+    const int q = tile / tpp, lt = tile - q * tpp;
+    const bool tv = q < ncnt;
+    const int r = lt * 16 + c16;
+    xrow[i] = (int)sample_global(inv_path[lbase + (tv ? q : 0)], tv && r < R ? r : 0, E, PE, t0) * ldx;
+  }
+  const uint16_t* Wm = Wc + (long)j * COUT * KP + (long)(cq * 64 + c16) * KP + 8 * grp;
+  f4v acc[RTW][4];
+#pragma unroll
+  for (int i = 0; i < RTW; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
+  s8v ah[D][RTW], al[D][RTW], bh[D][4], bl[D][4];
+  auto load = [&](int d, int kk) {
+    const int k0 = kk + 8 * grp;
+#pragma unroll
+    for (int i = 0; i < RTW; ++i) {
+      ah[d][i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+      al[d][i] = *reinterpret_cast<const s8v*>(X + xlo + xrow[i] + k0);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      bh[d][jj] = *reinterpret_cast<const s8v*>(Wm + (long)jj * 16 * KP + kk);
+      bl[d][jj] = *reinterpret_cast<const s8v*>(Wm + wlo + (long)jj * 16 * KP + kk);
+    }
+  };
+  auto mma = [&](int d) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int i = 0; i < RTW; ++i) acc[i][jj] = mma3h(ah[d][i], al[d][i], bh[d][jj], bl[d][jj], acc[i][jj]);
+  };
+  const int nks = NKS > 0 ? NKS : KP / 32;
+  const int ks0 = kh ? nks / 2 : 0, nk = kh ? nks - nks / 2 : nks / 2;
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < nk) load(d, (ks0 + d) * 32);
+  int s = 0;
+#pragma unroll 1
+  for (; s + 2 * D <= nk; s += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      mma(d);
+      load(d, (ks0 + s + d + D) * 32);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (s + d < nk) {
+      mma(d);
+      if (s + d + D < nk) load(d, (ks0 + s + d + D) * 32);
+    }
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (s + D + d < nk) mma(d);
+  if (kh) {
+#pragma unroll
+    for (int i = 0; i < RTW; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[cq][i * 16 + 4 * grp + r][jj * 16 + c16] = acc[i][jj][r];
+  }
+  __syncthreads();
+  if (kh) return;
+  const long PR = (long)P * R;
+  int pth[RTW], slot[RTW], rbase[RTW];
+#pragma unroll
+  for (int i = 0; i < RTW; ++i) {
+    const int tile = u * RTW + i;
+    const int q = tile / tpp;
+    const bool tv = q < ncnt;
+    pth[i] = tv ? inv_path[lbase + q] : -1;
+    slot[i] = tv ? inv_slot[lbase + q] : 0;
+    rbase[i] = (tile - q * tpp) * 16;
+  }
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int col = cq * 64 + jj * 16;
+    const float bb = flat[bias_off + (long)j * chunk + col + c16];
+#pragma unroll
+    for (int i = 0; i < RTW; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase[i] + 4 * grp + r;
+        const bool ok = pth[i] >= 0 && row < R;
+        const float v = (acc[i][jj][r] + red[cq][i * 16 + 4 * grp + r][jj * 16 + c16]) * in_scale + bb;
+        const bool pos = v > 0.f;
+        const uint64_t bal = __ballot(pos);
+        if (ok) {
+          Ys[((long)slot[i] * PR + (long)pth[i] * R + row) * COUT + col + c16] = pos ? v : 0.f;
+          if (c16 == 0)
+            bits[((long)slot[i] * bits_rows + sample_global(pth[i], row, E, PE, t0)) * NWORDS + col / 16] =
+                (uint16_t)((bal >> (16 * grp)) & 0xFFFFull);
+        }
+      }
+    }
+  }
+}
+
+// sum every path's module slots in slot order (one thread per row x 8 columns) -> Y (fp32, or an fp16 pair)
+template <bool OF32>
+__global__ __launch_bounds__(256) void fc_slot_sum_x3(const float* __restrict__ Ys, const int* __restrict__ act_cnt,
+                                                      int layer, int L, int P, int E, int T, int t0,
+                                                      void* __restrict__ Yv, long ylo, float out_scale) {
+  constexpr int COUT = 256;
+  const int R = T * E;
+  const long PR = (long)P * R;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long row = idx >> 5;
+  const int c8 = (int)(idx & 31) * 8;
+  if (row >= PR) return;
+  const int p = (int)(row / R), r = (int)(row - (long)p * R);
+  const int cnt = act_cnt[p * L + layer];
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int a = 0; a < cnt; ++a) {
+    const float4* src = reinterpret_cast<const float4*>(Ys + ((long)a * PR + row) * COUT + c8);
+    const float4 x = src[0], y = src[1];
+    o[0] += x.x; o[1] += x.y; o[2] += x.z; o[3] += x.w;
+    o[4] += y.x; o[5] += y.y; o[6] += y.z; o[7] += y.w;
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) o[c] *= out_scale;
+  const long sg = sample_global(p, r, E, P * E, t0);
+  if constexpr (OF32) {
+    float* Y = reinterpret_cast<float*>(Yv) + sg * COUT + c8;
+    *reinterpret_cast<float4*>(Y) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(Y + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  } else {
+    st8_x4(reinterpret_cast<uint16_t*>(Yv) + sg * COUT + c8, ylo, o);
+  }
+}
+
+// ===========================================================================
 // fc input gradient (trunk_bwd.hip fc_dgrad_lds_kernel): per workgroup 64 rows; the masked gradient of 2 active
 // slots is split into hi/lo planes in LDS (135 KB: 1 workgroup of 512 threads per CU), every 128-column chunk of
 // dX is swept with the hi/lo weight fragments of WcT [2][M][KP][COUT] in registers (next iteration's prefetched).
@@ -1915,6 +2091,37 @@ int x3_fc_fwd(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, c
   }
 #undef FCX
   const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
+// module-major fc forward (fc_fwd_mm_x3 + fc_slot_sum_x3); Ys: fp32 [M][P*T*E][256] slot planes
+int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, const void* Wc, long wlo,
+                 const float* flat, long bias_off, int chunk, const int* ac, const int* inv_path, const int* inv_slot,
+                 const int* inv_cnt, float* Ys, int layer, int L, int M, int K, int KP, int Cout, int P, int E, int T,
+                 int t0, long br, float os, hipStream_t st) {
+  if (ldx <= 0 || chunk <= 0 || L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 ||
+      br <= 0 || bias_off < 0 || layer < 0 || t0 < 0 || xlo <= 0 || ylo < 0 || wlo <= 0 || !Ys || !inv_path ||
+      !inv_slot || !inv_cnt) return -22;
+  if (M > X3_MAXM || KP % 32 != 0 || Cout != 256 || ldx % 8 != 0 || ldx < KP || (long)T * E > 32) return 0;
+  const int R = T * E, tpp = (R + 15) / 16;
+  const int umax = M * ((P * tpp + 3) / 4);
+  const int nwg = (umax + 7) / 8 * 8;
+  const float isc = 1.f / (float)(1 << X3_W0_SHIFT);
+#define FMM(NKS_)                                                                                                 \
+  fc_fwd_mm_x3<NKS_><<<nwg, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits, (const uint16_t*)Wc, \
+                                          wlo, flat, bias_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, KP, P, E, \
+                                          T, t0, br, isc)
+  if (KP == 256) FMM(8); else FMM(0);        // (a constant 44-step loop spills: runtime count for fc1)
+#undef FMM
+  int rc = (int)hipGetLastError();
+  if (rc) return -rc;
+  const long thr = (long)P * R * 32;
+  const unsigned g2 = (unsigned)((thr + 255) / 256);
+  if (ylo == 0)
+    fc_slot_sum_x3<true><<<g2, 256, 0, st>>>(Ys, ac, layer, L, P, E, T, t0, Y, 0, os);
+  else
+    fc_slot_sum_x3<false><<<g2, 256, 0, st>>>(Ys, ac, layer, L, P, E, T, t0, Y, ylo, os);
+  rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
 

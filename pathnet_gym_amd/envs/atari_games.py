@@ -11,7 +11,10 @@ and the same preprocessing/stacking pipeline as Pong
                     7/7/4/4/1/1 by row, 5 lives, FIRE serves.
 * ``SpaceInvaders`` 6 actions (NOOP, FIRE, RIGHT, LEFT, RIGHTFIRE, LEFTFIRE);
                     6x6 marching formation worth 30..5 by row, one player
-                    shot and one alien bomb in flight, 3 lives.
+                    shot and one alien bomb in flight, 3 lives; a cleared
+                    wave is followed by a new one (the game ends on lives, an
+                    invasion or 4500 agent steps: one wave alone was cleared by
+                    a random policy).
 * ``Alien`` / ``MsPacman``  18 / 9 actions; 13x11 maze with eggs (+10) and
                     three chasing aliens, 3 lives, clearing the maze +500.
 * ``Centipede``     18 actions; a 10-segment centipede snaking down through
@@ -472,6 +475,9 @@ class SpaceInvadersVec(PixelGameVec):
     id = "SpaceInvaders"
     n_actions = 6
     reward_threshold = 300.0
+    # waves repeat, so a good player's episode is unbounded: 4500 agent steps (18000 frames, 5 minutes of play)
+    # bound it, as ALE's frame limit bounds the real game
+    max_steps = 4500
     HIP_GAME = "SpaceInvaders"
     HIP_FIELDS = (("fx", "i"), ("fy", "i"), ("fdir", "i"), ("tick", "i"), ("px", "i"), ("lives", "i"), ("sx", "i"),
                   ("sy", "i"), ("shot", "i"), ("bxp", "i"), ("byp", "i"), ("bomb", "i"), ("alive", "bits"))
@@ -547,12 +553,18 @@ class SpaceInvadersVec(PixelGameVec):
         hitp = self.bomb & (self.byp >= 185) & (self.byp < 193) & (self.bxp >= self.px) & (self.bxp < self.px + 7)
         self.lives = self.lives - hitp.long()
         self.bomb = self.bomb & ~hitp & (self.byp < 196)
+        # wave cleared: a new formation marches in from the top (the game ends on lives or an invasion only)
+        cleared = ~self.alive.view(N, -1).any(1)
+        self.alive = torch.where(cleared[:, None, None], torch.ones_like(self.alive), self.alive)
+        self.fx = self.where_set(self.fx, cleared, 22)
+        self.fy = self.where_set(self.fy, cleared, 40)
+        self.fdir = self.where_set(self.fdir, cleared, 1)
         return reward
 
     def game_over(self):
         lowest_row = torch.where(self.alive.any(2), torch.arange(self.AR, device=self.device)[None], -1).max(1).values
         invaded = (self.fy + 18 * lowest_row + 10) >= 180
-        return (self.lives <= 0) | (~self.alive.view(self.num_envs, -1).any(1)) | invaded
+        return (self.lives <= 0) | invaded
 
     def scene(self) -> Scene:
         sc = Scene(self.num_envs, self.device)

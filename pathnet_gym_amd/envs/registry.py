@@ -73,6 +73,8 @@ def make(env_id: str, num_envs: int = 1, device="cpu", seed: int = 0, backend: s
         kw.pop("frameskip", None)                   # gym envs apply their own frame skip
     env = factory(num_envs=num_envs, device=device, seed=seed, backend=backend, **kw)
     env.id = env_id
+    if is_synthetic(env_id):
+        env.reward_threshold = reward_threshold(env_id)     # the calibrated one (envs/thresholds.json)
     return env
 
 
@@ -112,8 +114,23 @@ def _atari_game(name):
     return f
 
 
+def synthetic_thresholds() -> Dict[str, float]:
+    """Solve thresholds of the synthetic games, calibrated by ``scripts/calibrate_thresholds.py`` from a measured
+    random-policy return and a scripted expert's (``envs/thresholds.json``: random + 0.75 (expert - random); Pong
+    keeps the ALE 18).  Real gym ids keep ``REAL_ATARI_THRESHOLDS``."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "thresholds.json")
+    out = dict(REAL_ATARI_THRESHOLDS)
+    if os.path.exists(path):
+        with open(path) as f:
+            for g, rec in json.load(f)["games"].items():
+                out[g] = float(rec["threshold"])
+    return out
+
+
 register("CartPole-v1", _cartpole, 475.0)
-for _g, _thr in REAL_ATARI_THRESHOLDS.items():
+for _g, _thr in synthetic_thresholds().items():
     _f = _pong if _g == "Pong" else _atari_game(_g)
     for _id in ("Synth" + _g + "-v0", _g):
         register(_id, _f, _thr)

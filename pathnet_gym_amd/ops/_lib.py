@@ -123,6 +123,8 @@ _SIGS = {
     "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P],
     "x3_fc_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 10
                  + [c_long, c_float, P],
+    "x3_fc_fwd_mm": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P, P, P, P] + [c_int] * 10
+                    + [c_long, c_float, P],
     "x3_fc_dgrad": [P, P, P, c_long, P, P] + [c_int] * 9 + [c_long, c_float, P, P, c_long, P],
     "x3_fc_wgrad_gm": [P, c_long, c_int, P, c_long, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8
                       + [c_long, c_int, P],

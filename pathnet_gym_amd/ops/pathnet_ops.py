@@ -173,6 +173,10 @@ class HipPathNet:
                             if need_t else None)
         self.x3_status = torch.zeros(1, dtype=torch.int32, device=dev)   # fp16 range overflow of the scaled conv1 pair
         self._part = None            # fp32 conv wgrad partial slabs (allocated on first use, before capture)
+        self._ys = None              # fp32x module-major fc forward: per-slot fp32 output planes
+        # fp32x fc forward: module-major (one workgroup per module x 64 rows of its paths, csrc/trunk_x3.hip
+        # fc_fwd_mm_x3) instead of path-major (fc_fwd_x3)
+        self.fc_fwd_mm = os.environ.get("PATHNET_X3_FC_MM", "1") != "0"
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
         self.inv_slot = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
@@ -480,6 +484,13 @@ class HipPathNet:
             ok = _lib.call_fast("x3_conv_fwd", xp, self._x3_lo(X), int(g.u8in), yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
                                 flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L, self.M, g.Hin, g.Win, g.Cin,
                                 g.KH, g.KW, g.S, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
+        elif self.fc_fwd_mm and g.Cout == 256 and P == self.model.P and aip == self.model.act_idx.data_ptr():
+            # module-major: each module's weight slice read once per 64 rows of the paths using it
+            ys = self._ys_buffer_x3(P * T * E)
+            ok = _lib.call_fast("x3_fc_fwd_mm", xp, x2_lo(X), g.ldx, yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
+                                flat.data_ptr(), g.b_off, g.chunk, acp, self.inv_path.data_ptr(),
+                                self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), ys.data_ptr(), l, self.L, self.M,
+                                g.K, g.KP, g.Cout, P, E, T, t0, bits_rows, out_scale, st)
         else:
             ok = _lib.call_fast("x3_fc_fwd", xp, x2_lo(X), g.ldx, yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
                                 flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L, self.M, g.K, g.KP, g.Cout, P, E,
@@ -487,6 +498,15 @@ class HipPathNet:
         if not ok:
             raise RuntimeError(f"fp32x: layer {l} forward shape (P={P}, E={E}, T={T}) has no split-bf16 kernel "
                                "(fc layers take <= 32 rows per path and launch)")
+
+    def _ys_buffer_x3(self, rows: int) -> torch.Tensor:
+        """fp32 module-slot planes [M][rows][256] of the module-major fc forward (grown before graph capture)."""
+        need = self.M * rows * 256
+        if self._ys is None or self._ys.numel() < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("fp32x: fc slot buffer first needed inside a graph capture")
+            self._ys = torch.empty(need, dtype=torch.float32, device=self.model.device)
+        return self._ys
 
     def _layer_bwd_x3(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st):
         g = self.geoms[l]

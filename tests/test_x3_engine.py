@@ -166,3 +166,36 @@ def test_x3_gradient_check_detects_a_two_percent_module_error(x3_rollout):
         bad[seg] *= 1.02
         err = layer_errors(tr, bad, g_ref)[l]
         assert err > X3_LAYER_TOL, (l, err)
+
+
+@pytest.mark.parametrize("E", [16, 32])
+def test_x3_fc_forward_module_major_matches_path_major(hip_lib, E):
+    """fc_fwd_mm_x3 (one workgroup per module x 64 rows, split-K, slot planes summed in slot order) == the
+    path-major fc_fwd_x3 up to summation order: outputs to fp32 rounding, relu bits equal but for exact ties."""
+    cfg = pixel_cfg()
+    P = 5
+    m = ACPathNet(cfg, P, DEV, "hip", seed=7, compute_dtype="fp32x")
+    m.set_paths(masks_with_edges(P, cfg.L, cfg.M, cfg.N, seed=4))
+    hp = m.hip
+    g = torch.Generator(device="cpu").manual_seed(2)
+    obs = torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+    outs = []
+    for mm in (True, False):
+        hp.fc_fwd_mm = mm
+        acts, bits = [], []
+        x = obs
+        for l, geo in enumerate(hp.geoms):
+            Y = hp.alloc_act(l, (1, P * E, geo.out_feat))
+            b, rows = hp.alloc_bits(l, 1, P * E)
+            hp.layer_fwd(l, x, Y, b, P, E, 1, 0, rows)
+            acts.append(Y)
+            bits.append(b)
+            x = Y
+        torch.cuda.synchronize()
+        outs.append(([x2_value(a) if a.dtype == torch.float16 else a.clone() for a in acts], [b.clone() for b in bits]))
+    hp.fc_fwd_mm = True
+    for l in (3, 4):
+        a, b = outs[0][0][l], outs[1][0][l]
+        assert rel(a, b) < 1e-6, (l, rel(a, b))
+        same = (outs[0][1][l] == outs[1][1][l]).float().mean().item()
+        assert same > 0.999, (l, same)
