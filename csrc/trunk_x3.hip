@@ -1311,6 +1311,162 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const uint16_t* __restrict__ X,
 }
 
 // ===========================================================================
+// fc forward, split-K: fc_fwd_x3 with KS waves per module (KS x 256 threads), each summing 1/KS of the k-steps;
+// the partial accumulators of a module meet in LDS before its bias + ReLU.  The rollout's fc launches have one
+// workgroup per (path, 64 columns) -- 256 workgroups at the bench shape -- so the module-per-wave kernel runs one
+// wave per SIMD and waits on its weight loads; KS multiplies the waves in flight on the same traffic.
+// ===========================================================================
+template <int RT, int D, int NKS, bool OF32, int KS>
+__global__ __launch_bounds__(256 * KS) void fc_fwd_ks_x3(const uint16_t* __restrict__ X, long xlo, int ldx,
+                                                         void* __restrict__ Yv, long ylo, uint16_t* __restrict__ bits,
+                                                         const uint16_t* __restrict__ Wc, long wlo,
+                                                         const float* __restrict__ flat, long bias_off, int chunk,
+                                                         const int* __restrict__ act_idx,
+                                                         const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                         int K, int KP, int Cout, int P, int E, int T, int t0,
+                                                         long bits_rows, float in_scale, float out_scale) {
+  static_assert(KS >= 2 && KS <= 4, "split-K 2..4");
+  __shared__ float kpart[KS - 1][4][RT * 16][64 + 4];
+  __shared__ float part[4][32][64 + 1];
+  const int p = blockIdx.z;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int mw = w & 3, kp = w >> 2;
+  const int grp = l >> 4, c16 = l & 15;
+  const long Rtot = (long)T * E;
+  const int PE = P * E;
+  const long row0 = (long)blockIdx.x * 32;
+  const int col0 = blockIdx.y * 64;
+  long xrow[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) {
+    const long r = row0 + i * 16 + c16;
+    xrow[i] = sample_global(p, (int)(r < Rtot ? r : row0), E, PE, t0) * ldx;
+  }
+  // per-module-lane ReLU sums live in LDS (part[mw]: only the k-part-0 wave of lane mw writes it), not in VGPRs
+  for (int x = tid; x < 4 * 32 * 65; x += 256 * KS) (&part[0][0][0])[x] = 0.f;
+  const int nwords = Cout / 16;
+  const int nks = NKS > 0 ? NKS : KP / 32;
+  const int kb = kp * nks / KS, nk = (kp + 1) * nks / KS - kb;
+  const int nit = (cnt + 3) >> 2;
+  __syncthreads();
+  for (int it = 0; it < nit; ++it) {
+    const int a = mw + 4 * it;
+    const bool act = a < cnt;
+    f4v acc[RT][4];
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+    const int mod = act ? act_idx[(p * L + layer) * M + a] : 0;
+    if (act) {
+      const uint16_t* Wm = Wc + (long)mod * Cout * KP + (long)(col0 + c16) * KP + 8 * grp;
+      s8v ah[D][RT], al[D][RT], bh[D][4], bl[D][4];
+      auto load = [&](int d, int ks) {
+        const int kk = (kb + ks) * 32;
+        const int k0 = kk + 8 * grp;
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+          if (K == KP) {
+            ah[d][i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+            al[d][i] = *reinterpret_cast<const s8v*>(X + xlo + xrow[i] + k0);
+          } else {
+            ah[d][i] = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
+            al[d][i] = ah[d][i];
+            if (k0 < K) {
+              ah[d][i] = *reinterpret_cast<const s8v*>(X + xrow[i] + k0);
+              al[d][i] = *reinterpret_cast<const s8v*>(X + xlo + xrow[i] + k0);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bh[d][j] = *reinterpret_cast<const s8v*>(Wm + (long)j * 16 * KP + kk);
+          bl[d][j] = *reinterpret_cast<const s8v*>(Wm + wlo + (long)j * 16 * KP + kk);
+        }
+      };
+      auto mma = [&](int d) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < RT; ++i) acc[i][j] = mma3h(ah[d][i], al[d][i], bh[d][j], bl[d][j], acc[i][j]);
+      };
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (d < nk) load(d, d);
+      int s = 0;
+      for (; s + 2 * D <= nk; s += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          mma(d);
+          load(d, s + d + D);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (s + d < nk) {
+          mma(d);
+          if (s + d + D < nk) load(d, s + d + D);
+        }
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (s + D + d < nk) mma(d);
+      if (kp > 0) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) kpart[kp - 1][mw][i * 16 + 4 * grp + r][j * 16 + c16] = acc[i][j][r];
+      }
+    }
+    __syncthreads();
+    if (kp == 0 && act) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float bb = flat[bias_off + (long)mod * chunk + col0 + j * 16 + c16];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[i][j][r];
+#pragma unroll
+            for (int q = 0; q < KS - 1; ++q) v += kpart[q][mw][i * 16 + 4 * grp + r][j * 16 + c16];
+            v = v * in_scale + bb;
+            const bool pos = v > 0.f;
+            part[mw][i * 16 + 4 * grp + r][j * 16 + c16] += pos ? v : 0.f;
+            const uint64_t bal = __ballot(pos);
+            const long row = row0 + i * 16 + 4 * grp + r;
+            if (c16 == 0 && row < Rtot)
+              bits[((long)a * bits_rows + sample_global(p, (int)row, E, PE, t0)) * nwords + (col0 + j * 16) / 16] =
+                  (uint16_t)((bal >> (16 * grp)) & 0xFFFFull);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (tid >= 256) return;
+  const int orow = tid >> 3, oc = (tid & 7) * 8;
+  const long row = row0 + orow;
+  if (orow < RT * 16 && row < Rtot) {
+    const long sg = sample_global(p, (int)row, E, PE, t0);
+    float o[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      o[c] = (part[0][orow][oc + c] + part[1][orow][oc + c] + part[2][orow][oc + c] + part[3][orow][oc + c]) *
+             out_scale;
+    if constexpr (OF32) {
+      float* Y = reinterpret_cast<float*>(Yv) + sg * Cout + col0 + oc;
+      *reinterpret_cast<float4*>(Y) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(Y + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+      st8_x4(reinterpret_cast<uint16_t*>(Yv) + sg * Cout + col0 + oc, ylo, o);
+    }
+  }
+}
+
+// ===========================================================================
 // fc forward, MODULE-MAJOR (share each module's weight slice across the paths that use it).
 // The path-major kernel above re-reads a module's [Cout][KP] hi/lo slice once per (path, 64-column tile): 553 MB
 // of L2/MALL traffic per fc1 launch at the bench shape.  Here one workgroup = one active module j x 64 rows (4 row
@@ -1330,10 +1486,12 @@ __global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__
                                                     const int* __restrict__ inv_cnt, int layer, int M, int KP, int P,
                                                     int E, int T, int t0, long bits_rows, float in_scale) {
   constexpr int COUT = 256, RTW = 4, D = 2, NWORDS = COUT / 16;
-  __shared__ float red[4][64][64 + 4];                 // k-half-1 partials per column quarter (69.6 KB)
+  constexpr int CPW = 2;                               // 16-column tiles per wave
+  constexpr int NH = COUT / (4 * 16 * CPW);            // column slices per (module, 64 rows): units = chunks x NH
+  __shared__ float red[4][64][16 * CPW + 4];           // k-half-1 partials per wave column slice
   const int R = T * E, tpp = (R + 15) / 16;
   int U = 0;
-  for (int j = 0; j < M; ++j) U += (inv_cnt[layer * M + j] * tpp + RTW - 1) / RTW;
+  for (int j = 0; j < M; ++j) U += NH * ((inv_cnt[layer * M + j] * tpp + RTW - 1) / RTW);
   const int per = (U + 7) >> 3;
   const int kx = (int)(blockIdx.x >> 3);
   int u = (int)(blockIdx.x & 7) * per + kx;
@@ -1341,13 +1499,16 @@ __global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__
   int j = 0, ncnt = 0;
   for (; j < M; ++j) {
     ncnt = inv_cnt[layer * M + j];
-    const int n = (ncnt * tpp + RTW - 1) / RTW;
+    const int n = NH * ((ncnt * tpp + RTW - 1) / RTW);
     if (u < n) break;
     u -= n;
   }
+  const int hslice = u % NH;
+  u /= NH;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
   const int cq = w & 3, kh = w >> 2;
+  const int cbase = (hslice * 4 + cq) * 16 * CPW;      // first output column of this wave
   const int PE = P * E;
   const long lbase = ((long)layer * M + j) * P;
   int xrow[RTW];                                       // element offsets (the activation buffer is < 2^31)
@@ -1359,13 +1520,13 @@ __global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__
     const int r = lt * 16 + c16;
     xrow[i] = (int)sample_global(inv_path[lbase + (tv ? q : 0)], tv && r < R ? r : 0, E, PE, t0) * ldx;
   }
-  const uint16_t* Wm = Wc + (long)j * COUT * KP + (long)(cq * 64 + c16) * KP + 8 * grp;
-  f4v acc[RTW][4];
+  const uint16_t* Wm = Wc + (long)j * COUT * KP + (long)(cbase + c16) * KP + 8 * grp;
+  f4v acc[RTW][CPW];
 #pragma unroll
   for (int i = 0; i < RTW; ++i)
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
-  s8v ah[D][RTW], al[D][RTW], bh[D][4], bl[D][4];
+    for (int jj = 0; jj < CPW; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
+  s8v ah[D][RTW], al[D][RTW], bh[D][CPW], bl[D][CPW];
   auto load = [&](int d, int kk) {
     const int k0 = kk + 8 * grp;
 #pragma unroll
@@ -1374,14 +1535,14 @@ __global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__
       al[d][i] = *reinterpret_cast<const s8v*>(X + xlo + xrow[i] + k0);
     }
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
+    for (int jj = 0; jj < CPW; ++jj) {
       bh[d][jj] = *reinterpret_cast<const s8v*>(Wm + (long)jj * 16 * KP + kk);
       bl[d][jj] = *reinterpret_cast<const s8v*>(Wm + wlo + (long)jj * 16 * KP + kk);
     }
   };
   auto mma = [&](int d) {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj)
+    for (int jj = 0; jj < CPW; ++jj)
 #pragma unroll
       for (int i = 0; i < RTW; ++i) acc[i][jj] = mma3h(ah[d][i], al[d][i], bh[d][jj], bl[d][jj], acc[i][jj]);
   };
@@ -1412,7 +1573,7 @@ __global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__
 #pragma unroll
     for (int i = 0; i < RTW; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
+      for (int jj = 0; jj < CPW; ++jj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[cq][i * 16 + 4 * grp + r][jj * 16 + c16] = acc[i][jj][r];
   }
@@ -1430,8 +1591,8 @@ __global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__
     rbase[i] = (tile - q * tpp) * 16;
   }
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    const int col = cq * 64 + jj * 16;
+  for (int jj = 0; jj < CPW; ++jj) {
+    const int col = cbase + jj * 16;
     const float bb = flat[bias_off + (long)j * chunk + col + c16];
 #pragma unroll
     for (int i = 0; i < RTW; ++i) {
@@ -1941,6 +2102,10 @@ static int X3_FWD_DB = 0;      // bf16-activation conv forward: 1 = double-buffe
 // 0.52 ms (1); profiles/r3/kwin_x3_v4*.md)
 static int X3_WGRAD_PF = 3;
 static int X3_FC_D = 4;        // fc forward register ring depth (k-steps of hi/lo A and B fragments in flight)
+// fc forward split-K waves per module (1 = fc_fwd_x3, 2 = fc_fwd_ks_x3).  Measured: fc1 66.4 (2) vs 65.1 us (1),
+// fc2 19.7 vs 17.4 (profiles/r3/kwin_x3_v7*.md): more waves on the same weight traffic do not help -- the launch
+// is bound by its L2/MALL traffic, not by load latency
+static int X3_FC_KS = 1;
 
 extern "C" {
 
@@ -1948,6 +2113,7 @@ void fast_conv_set_x3_fwd_nt(int nt) { X3_FWD_NT = nt; }
 void fast_conv_set_x3_fwd_lb(int lb) { X3_FWD_LB = lb; }
 void fast_conv_set_x3_fwd_db(int db) { X3_FWD_DB = db; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
+void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
 
 int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits, const void* Wc, long wlo,
@@ -2078,6 +2244,16 @@ int x3_fc_fwd(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, c
                                                       L, M, K, KP, Cout, P, E, T, t0, br,                               \
                                                       1.f / (float)(1 << X3_W0_SHIFT), os)
   const bool of = ylo == 0;
+  if (X3_FC_KS >= 2 && (long)T * E > 16) {
+#define FKS(D_, NKS_, OF_, KS_)                                                                                      \
+  fc_fwd_ks_x3<2, D_, NKS_, OF_, KS_><<<grid, 256 * KS_, 0, st>>>(                                                  \
+      (const uint16_t*)X, xlo, ldx, Y, ylo, (uint16_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, \
+      layer, L, M, K, KP, Cout, P, E, T, t0, br, 1.f / (float)(1 << X3_W0_SHIFT), os)
+    if (of) FKS(2, 0, true, 2); else FKS(2, 0, false, 2);     // (KS = 4 needs <= 128 VGPRs: spills)
+#undef FKS
+    const int rc = (int)hipGetLastError();
+    return rc ? -rc : 1;
+  }
   if ((long)T * E <= 16) {
     if (of) FCX(1, 4, 0, true); else FCX(1, 4, 0, false);
   } else if (KP == 1408 && X3_FC_D <= 2) {
@@ -2104,7 +2280,7 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
       !inv_slot || !inv_cnt) return -22;
   if (M > X3_MAXM || KP % 32 != 0 || Cout != 256 || ldx % 8 != 0 || ldx < KP || (long)T * E > 32) return 0;
   const int R = T * E, tpp = (R + 15) / 16;
-  const int umax = M * ((P * tpp + 3) / 4);
+  const int umax = M * ((P * tpp + 3) / 4) * 2;      // x 2 column slices (fc_fwd_mm_x3 NH)
   const int nwg = (umax + 7) / 8 * 8;
   const float isc = 1.f / (float)(1 << X3_W0_SHIFT);
 #define FMM(NKS_)                                                                                                 \

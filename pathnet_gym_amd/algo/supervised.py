@@ -258,6 +258,7 @@ def run_supervised_transfer(a) -> Dict:
         data, test = prep(make_digits(name, n_of(ti), a.seed * 31 + ti, device),
                           make_digits(name, 2048, a.seed * 31 + ti + 7919, device))
         if ti > 0:
+            sp.pop.rng = np.random.RandomState(a.seed * 7919 + ti)     # the paired control replays this draw
             sp.pop.init_genotypes()
         best_hist = []
         for gen in range(a.generations):
@@ -271,18 +272,30 @@ def run_supervised_transfer(a) -> Dict:
         out["per_task"].append({"task": name, "best_accuracy": best_hist[-1], "test_accuracy": test_acc,
                                 "curve": best_hist, "frozen": sp.frozen.astype(int).tolist()})
     if getattr(a, "control", False) and len(tasks) > 1:
-        # transfer check: the last task learned from scratch (no frozen source path), same budget
-        ctl = SupervisedPathNet(cfg, a.population, 1, device, a.seed + 1000, a.B)
-        data, test = prep(make_digits(tasks[-1], n_of(len(tasks) - 1), a.seed * 31 + len(tasks) - 1, device),
-                          make_digits(tasks[-1], 2048, a.seed * 31 + len(tasks) - 1 + 7919, device))
+        # transfer check: the last task learned from scratch (no frozen source path), same budget.  paired (default):
+        # common random numbers -- the same initial parameters and task head, the same minibatch and GA random
+        # streams and the same initial genotypes as the transfer run's last task, so the ONLY difference is the
+        # frozen source modules; otherwise an independent seed (seed + 1000)
+        last = len(tasks) - 1
+        paired = bool(getattr(a, "paired_control", 1))
+        if paired:
+            ctl = SupervisedPathNet(cfg, a.population, len(tasks), device, a.seed, a.B)
+            ctl.pop.rng = np.random.RandomState(a.seed * 7919 + last)
+            ctl.pop.init_genotypes()
+            task_c = last
+        else:
+            ctl = SupervisedPathNet(cfg, a.population, 1, device, a.seed + 1000, a.B)
+            task_c = 0
+        data, test = prep(make_digits(tasks[-1], n_of(last), a.seed * 31 + last, device),
+                          make_digits(tasks[-1], 2048, a.seed * 31 + last + 7919, device))
         hist = []
         for gen in range(a.generations):
-            acc = ctl.train_generation(data, 0, a.steps_per_gen, a.batch, a.lr, gen, clip)
+            acc = ctl.train_generation(data, task_c, a.steps_per_gen, a.batch, a.lr, gen, clip)
             ctl.pop.step(acc.astype(np.float32), gen)
             hist.append(float(acc.max()))
             _progress(tasks[-1] + " (scratch)", gen, hist[-1], t0)
-        out["control"] = {"task": tasks[-1], "best_accuracy": hist[-1], "curve": hist,
-                          "test_accuracy": ctl.test_accuracy(ctl.paths()[int(np.argmax(acc))], test, 0)}
+        out["control"] = {"task": tasks[-1], "best_accuracy": hist[-1], "curve": hist, "paired": paired,
+                          "test_accuracy": ctl.test_accuracy(ctl.paths()[int(np.argmax(acc))], test, task_c)}
         thr = getattr(a, "target_accuracy", 0.9)
         first = lambda c: next((i for i, v in enumerate(c) if v >= thr), None)     # noqa: E731
         out["generations_to_accuracy"] = {"threshold": thr, "transfer": first(out["per_task"][-1]["curve"]),

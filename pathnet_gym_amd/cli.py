@@ -132,6 +132,9 @@ def build_parser():
     s.add_argument("--seed", type=int, default=1)
     s.add_argument("--device", default=None)
     s.add_argument("--control", action="store_true", help="also learn the last task from scratch (transfer check)")
+    s.add_argument("--paired_control", type=int, default=1,
+                   help="1: the control replays the transfer run's last-task random streams (same init, head, "
+                        "minibatches, GA draws): only the frozen source modules differ; 0: independent seed")
     s.add_argument("--target_accuracy", type=float, default=0.9)
     s.add_argument("--log_dir", default=None)
 

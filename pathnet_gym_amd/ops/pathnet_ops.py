@@ -175,8 +175,9 @@ class HipPathNet:
         self._part = None            # fp32 conv wgrad partial slabs (allocated on first use, before capture)
         self._ys = None              # fp32x module-major fc forward: per-slot fp32 output planes
         # fp32x fc forward: module-major (one workgroup per module x 64 rows of its paths, csrc/trunk_x3.hip
-        # fc_fwd_mm_x3) instead of path-major (fc_fwd_x3)
-        self.fc_fwd_mm = os.environ.get("PATHNET_X3_FC_MM", "1") != "0"
+        # fc_fwd_mm_x3) instead of path-major.  Measured slower at the bench shape (fc1 95.6 vs 70.3 us: 128
+        # workgroups leave half the CUs idle; profiles/r3/kwin_x3_v6*.md), so off unless PATHNET_X3_FC_MM=1
+        self.fc_fwd_mm = os.environ.get("PATHNET_X3_FC_MM", "0") == "1"
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
         self.inv_slot = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
