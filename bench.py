@@ -207,13 +207,15 @@ def main():
                     help="start every env at 0-0 (default: random late scores, so tournaments fire inside the window)")
     ap.add_argument("--solve-seconds", type=float, default=None,
                     help="after the timed window, run one generations-to-solve seed on a fresh trainer for at most "
-                         "this long (default 330 s on one GPU, 0 = off; multi-GPU runs skip it)")
+                         "this long (default: up to 420 s on one GPU, within a 540 s total; 0 = off; multi-GPU "
+                         "runs skip it)")
     ap.add_argument("--compare-bf16", type=int, default=None,
                     help="also time the bf16 engine on the same config (default: on for one GPU)")
     ap.add_argument("--prof-window", action="store_true",
                     help="launch marker kernels around the timed updates (scripts/prof_window.py summarises the "
                          "rocprofv3 kernel trace between them)")
     args = ap.parse_args()
+    t_start = time.time()
 
     import torch
 
@@ -231,7 +233,9 @@ def main():
             (getattr(lib, k) if hasattr(lib, k) and "_set_" in k else getattr(lib, "fast_conv_set_" + k))(int(v))
     ctx = init_distributed()
     single = ctx.world == 1 and not args.prof_window
-    solve_s = args.solve_seconds if args.solve_seconds is not None else (330.0 if single else 0.0)
+    # the in-run solve may use what is left of a ~540 s budget (the driver allows 600 s for the whole bench; a fresh
+    # box can spend a minute or two importing torch), at most 420 s
+    solve_s = args.solve_seconds if args.solve_seconds is not None else (420.0 if single else 0.0)
     compare = args.compare_bf16 if args.compare_bf16 is not None else int(single and args.dtype != "bf16")
     stagger = not args.no_stagger
     cfg, tr = build_trainer(args, ctx, args.dtype, stagger)
@@ -288,6 +292,8 @@ def main():
     torch.cuda.empty_cache() if torch.cuda.is_available() else None
     # the metric's second half: one seed observed in this run, plus every committed multi-seed record of exactly
     # this config (scripts/solve.py --out profiles/solve/*.json)
+    if solve_s > 0 and args.solve_seconds is None:
+        solve_s = max(0.0, min(solve_s, 540.0 - (time.time() - t_start)))
     if solve_s > 0:
         rec["generations_to_solve_in_run"] = in_run_solve(args, ctx, args.dtype, solve_s)
     if ctx.is_main:
