@@ -81,12 +81,18 @@ DEVI uint32_t relu_bits_word(const uint64_t (&bal)[4], uint32_t k) {
 }
 
 // ---- split-bf16 helpers ----
+typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+typedef float f2v_ __attribute__((ext_vector_type(2)));
+// hi = RNE bf16(v), lo = RNE bf16(v - hi): one v_cvt_pk_bf16_f32 per PAIR for hi (the scalar form converted each
+// value twice: once alone for the residual, once paired for the store), the residual's operand rebuilt from the
+// packed word by a shift / mask
 DEVI void split8(const float (&v)[8], s8v& hi, s8v& lo) {
-  __bf16 h[8], l[8];
+  uint32_t h[4], l[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    h[j] = (__bf16)v[j];
-    l[j] = (__bf16)(v[j] - (float)h[j]);
+  for (int j = 0; j < 4; ++j) {
+    h[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v_){v[2 * j], v[2 * j + 1]}, b2v));
+    const float b0 = __builtin_bit_cast(float, h[j] << 16), b1 = __builtin_bit_cast(float, h[j] & 0xFFFF0000u);
+    l[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v_){v[2 * j] - b0, v[2 * j + 1] - b1}, b2v));
   }
   __builtin_memcpy(&hi, h, 16);
   __builtin_memcpy(&lo, l, 16);
@@ -138,6 +144,12 @@ DEVI f4v mma3h(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c
   c = mfma16_f16(ah, bl, c);
   return mfma16_f16(ah, bh, c);
 }
+// the same products with the weights as the A operand (D = [columns][rows], conv_epi_sw), in mma3h's order
+DEVI f4v mma3h_t(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
+  c = mfma16_f16(bh, al, c);
+  c = mfma16_f16(bl, ah, c);
+  return mfma16_f16(bh, ah, c);
+}
 // exact operand a (uint8 pixels in bf16) against a hi/lo pair b
 DEVI f4v mma2(const s8v& a, const s8v& bh, const s8v& bl, f4v c) {
   c = mfma16(a, bl, c);
@@ -151,6 +163,63 @@ DEVI s8v u8x8_to_f16(uint2 v) {
   return __builtin_bit_cast(s8v, x);
 }
 
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// ---- conv forward epilogue, swapped MFMA orientation (weights as the A operand, im2col rows as B) ----
+// acc[ct] = D[16 output columns][16 rows]: lane (q, c16) holds columns 4q..4q+3 of column tile ct -- slot
+// 2*(ct0+ct) + (q>>1), channels 4*(q&1) + r -- for row c16, i.e. four consecutive channels of one row.  Compared with
+// rows-as-A (lane = one channel of four rows) the module-pair sum is one xor-32 exchange, the ReLU-bit byte of a
+// (slot, row) is two lanes' nibbles (no ballot transposes), and each lane writes its four channels of one plane as
+// one 8-byte store (hi plane: q < 2, lo plane: q >= 2) instead of 16 two-byte stores.  Same arithmetic and summation
+// order as the rows-as-A epilogue: bit-identical outputs.
+template <int NC>
+DEVI void conv_epi_sw(const f4v (&acc)[NC], const float* bias_s, int ct0, int cnt, int q, float in_scale,
+                      float out_scale, long grow, uint8_t* __restrict__ bits, long bits_rows,
+                      uint16_t* __restrict__ Y, long ylo, bool accumulate) {
+  float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ct = 0; ct < NC; ++ct) {
+    const float4 bb = *reinterpret_cast<const float4*>(bias_s + ct * 16 + 4 * q);
+    const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+    uint32_t nib = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = acc[ct][r] * in_scale + bv[r];
+      const bool pos = v > 0.f;
+      sum[r] += pos ? v : 0.f;
+      nib |= pos ? (1u << r) : 0u;
+    }
+    const uint32_t hi4 = (uint32_t)__shfl_xor((int)nib, 16, 64);      // channels 4..7 of the same slot and row
+    const int slot = (ct0 + ct) * 2 + (q >> 1);
+    if ((q & 1) == 0 && slot < cnt) bits[(long)slot * bits_rows + grow] = (uint8_t)(nib | (hi4 << 4));
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 32, 64);   // + the other slot of each pair
+  float y[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) y[r] = sum[r] * out_scale;
+  const long o = grow * 8 + 4 * (q & 1);
+  if (accumulate) {
+    const uint2 ph = *reinterpret_cast<const uint2*>(Y + o), pl = *reinterpret_cast<const uint2*>(Y + ylo + o);
+    const uint32_t hw[4] = {ph.x & 0xFFFFu, ph.x >> 16, ph.y & 0xFFFFu, ph.y >> 16};
+    const uint32_t lw[4] = {pl.x & 0xFFFFu, pl.x >> 16, pl.y & 0xFFFFu, pl.y >> 16};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] += h2f((uint16_t)hw[r]) + h2f((uint16_t)lw[r]);
+  }
+  const h2v h01 = __builtin_convertvector((f2v){y[0], y[1]}, h2v);
+  const h2v h23 = __builtin_convertvector((f2v){y[2], y[3]}, h2v);
+  uint2 out;
+  if (q < 2) {
+    out = make_uint2(__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23));
+  } else {
+    const h2v l01 = __builtin_convertvector((f2v){y[0] - (float)h01[0], y[1] - (float)h01[1]}, h2v);
+    const h2v l23 = __builtin_convertvector((f2v){y[2] - (float)h23[0], y[3] - (float)h23[1]}, h2v);
+    out = make_uint2(__builtin_bit_cast(uint32_t, l01), __builtin_bit_cast(uint32_t, l23));
+  }
+  *reinterpret_cast<uint2*>(Y + (q < 2 ? 0 : ylo) + o) = out;
+}
+
 // ===========================================================================
 // first layer forward (uint8 frame stack, 8x8/s4, 160x120x4): fp16 MFMA, exact pixels x (W*2^8) hi/lo pair.
 // grid = (ceil(T*E*HOWO / (NT*128)), P), 256 threads; each wave owns 32-row tiles (2 MFMA row tiles) and walks
@@ -158,7 +227,7 @@ DEVI s8v u8x8_to_f16(uint2 v) {
 // a k-step's raw bytes are converted, the same registers are reloaded with the next tile's k-step, then the MFMAs.
 // Wh: [2][M][8][KP] fp16 (hi plane, lo plane at +wlo).  Y: two bf16 planes (lo at +ylo).
 // ===========================================================================
-template <class G, int NT, int LB>
+template <class G, int NT, int LB, bool SW>
 __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                       long ylo, uint8_t* __restrict__ bits,
                                                       const uint16_t* __restrict__ Wh, long wlo,
@@ -172,7 +241,8 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
   constexpr int NK = G::KP / 32;
   constexpr int FF_ROWS = NT * 128;
   __shared__ __attribute__((aligned(16))) uint16_t Ws[2][X3_NCX * 16 * KPs];
-  __shared__ float bias_s[X3_NCX * 16];
+  __shared__ __attribute__((aligned(16))) float bias_s[X3_NCX * 16];
+  __shared__ float wsum_s[X3_NCX * 16];
   __shared__ int mods[X3_MAXM];
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
@@ -185,6 +255,9 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
   const int grp = l >> 4, c16 = l & 15, q = grp, h = c16 >> 3, ch = l & 7;
   const uint32_t bkey = (uint32_t)(2 * q + h);
   const bool lin = T == 1;
+  // SW: pixels enter the MFMA as fp16(1024 + v) straight from v_perm (no per-element subtraction); the offset's
+  // contribution 1024 * sum_k W[col][k] is taken out of the bias (wsum_s: the fp32 sum of the staged fp16 pair)
+  static_assert(!SW || G::KC == 32, "SW weight-sum reduction: one column per 32 lanes");
   const long rowbase = ((long)t0 * PE + (long)p * E) * G::HOWO;
   const int rfirst = blockIdx.x * FF_ROWS + w * 32;
   const int npass = nct > X3_NCX ? (nct + X3_NCX - 1) / X3_NCX : 1;
@@ -210,7 +283,7 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       rowit_init(ait[i], rfirst + i * 16 + c16, E, G::HOWO);
-      rowit_init(eit[i], rfirst + i * 16 + 4 * q, E, G::HOWO);
+      rowit_init(eit[i], rfirst + i * 16 + (SW ? c16 : 4 * q), E, G::HOWO);
     }
     // the first tile's A loads do not depend on LDS: issued before the staging barriers
     aff_addr();
@@ -230,10 +303,21 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
       }
       *reinterpret_cast<s8v*>(Ws[0] + col * KPs + kc * 8) = vh;
       *reinterpret_cast<s8v*>(Ws[1] + col * KPs + kc * 8) = vl;
+      if constexpr (SW) {
+        const h8v hh = __builtin_bit_cast(h8v, vh), ll = __builtin_bit_cast(h8v, vl);
+        float ws = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ws += (float)hh[j] + (float)ll[j];
+#pragma unroll
+        for (int m = 16; m >= 1; m >>= 1) ws += __shfl_xor(ws, m, 64);
+        if (kc == 0) wsum_s[col] = ws;
+      }
     }
+    __syncthreads();
     if (tid < ncg * 16) {
       const int slot = ct0 * 2 + (tid >> 3);
-      bias_s[tid] = slot < cnt ? flat[bias_off + (long)mods[slot] * chunk + (tid & 7)] : 0.f;
+      const float b = slot < cnt ? flat[bias_off + (long)mods[slot] * chunk + (tid & 7)] : 0.f;
+      bias_s[tid] = SW ? b - in_scale * 1024.f * wsum_s[tid] : b;
     }
     __syncthreads();
     auto run = [&](auto ncc) {
@@ -248,8 +332,8 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
         if constexpr (RELOAD) aff_addr();
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) {
-          const s8v a0 = u8x8_to_f16(araw[0][kk]);
-          const s8v a1 = u8x8_to_f16(araw[1][kk]);
+          const s8v a0 = SW ? u8x8_to_f16off(araw[0][kk]) : u8x8_to_f16(araw[0][kk]);
+          const s8v a1 = SW ? u8x8_to_f16off(araw[1][kk]) : u8x8_to_f16(araw[1][kk]);
           if constexpr (RELOAD) {
             araw[0][kk] = *reinterpret_cast<const uint2*>(asrc[0] + kk * G::WIN * G::CIN);
             araw[1][kk] = *reinterpret_cast<const uint2*>(asrc[1] + kk * G::WIN * G::CIN);
@@ -259,10 +343,17 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
           for (int ct = 0; ct < NC; ++ct) {
             const s8v bh = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
             const s8v bl = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
-            acc[0][ct] = mfma16_f16(a0, bl, acc[0][ct]);
-            acc[0][ct] = mfma16_f16(a0, bh, acc[0][ct]);
-            acc[1][ct] = mfma16_f16(a1, bl, acc[1][ct]);
-            acc[1][ct] = mfma16_f16(a1, bh, acc[1][ct]);
+            if constexpr (SW) {
+              acc[0][ct] = mfma16_f16(bl, a0, acc[0][ct]);
+              acc[0][ct] = mfma16_f16(bh, a0, acc[0][ct]);
+              acc[1][ct] = mfma16_f16(bl, a1, acc[1][ct]);
+              acc[1][ct] = mfma16_f16(bh, a1, acc[1][ct]);
+            } else {
+              acc[0][ct] = mfma16_f16(a0, bl, acc[0][ct]);
+              acc[0][ct] = mfma16_f16(a0, bh, acc[0][ct]);
+              acc[1][ct] = mfma16_f16(a1, bl, acc[1][ct]);
+              acc[1][ct] = mfma16_f16(a1, bh, acc[1][ct]);
+            }
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -271,13 +362,17 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
           const int r16 = rbase + i * 16;
           long grow4;
           if (lin) {
-            grow4 = rowbase + r16 + 4 * q;
+            grow4 = rowbase + r16 + (SW ? c16 : 4 * q);
           } else {
             const RowIt e0 = eit[i];
             rowit_adv(eit[i], 128, E, G::HOWO);
             grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
           }
           if (r16 >= Rtot) continue;
+          if constexpr (SW) {
+            conv_epi_sw<NC>(acc[i], bias_s, ct0, cnt, q, in_scale, out_scale, grow4, bits, bits_rows, Y, ylo, pass > 0);
+            continue;
+          }
           float sum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int ct = 0; ct < NC; ++ct) {
@@ -330,7 +425,7 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
 // three MFMAs per (row tile, column tile, k-step).  grid = (ceil(T*E*HOWO / (NT*128)), P).  The next 32-row
 // tile's A fragments (both planes) are loaded while this tile's MFMAs run.
 // ===========================================================================
-template <class G, int NT, int LB, bool DB>
+template <class G, int NT, int LB, bool DB, bool SW>
 __global__ __launch_bounds__(256, LB) void conv_fwd_x3(const uint16_t* __restrict__ X, long xlo,
                                                      uint16_t* __restrict__ Y, long ylo, uint8_t* __restrict__ bits,
                                                      const uint16_t* __restrict__ Wc, long wlo,
@@ -343,7 +438,7 @@ __global__ __launch_bounds__(256, LB) void conv_fwd_x3(const uint16_t* __restric
   constexpr int NK = G::KP / 32;
   constexpr int FF_ROWS = NT * 128;
   __shared__ __attribute__((aligned(16))) uint16_t Ws[2][X3_NCX * 16 * KPs];
-  __shared__ float bias_s[X3_NCX * 16];
+  __shared__ __attribute__((aligned(16))) float bias_s[X3_NCX * 16];
   __shared__ int mods[X3_MAXM];
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
@@ -384,7 +479,7 @@ __global__ __launch_bounds__(256, LB) void conv_fwd_x3(const uint16_t* __restric
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         rowit_init(ait[i], rfirst + i * 16 + c16, E, G::HOWO);
-        rowit_init(eit[i], rfirst + i * 16 + 4 * q, E, G::HOWO);
+        rowit_init(eit[i], rfirst + i * 16 + (SW ? c16 : 4 * q), E, G::HOWO);
       }
       s8v ah[2][NK], al[2][NK];
       auto load_tile = [&](int rbase) {
@@ -439,8 +534,13 @@ __global__ __launch_bounds__(256, LB) void conv_fwd_x3(const uint16_t* __restric
           for (int ct = 0; ct < NC; ++ct) {
             const s8v bh = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
             const s8v bl = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
-            acc[0][ct] = mma3h(ch_[0][kk], cl_[0][kk], bh, bl, acc[0][ct]);
-            acc[1][ct] = mma3h(ch_[1][kk], cl_[1][kk], bh, bl, acc[1][ct]);
+            if constexpr (SW) {
+              acc[0][ct] = mma3h_t(ch_[0][kk], cl_[0][kk], bh, bl, acc[0][ct]);
+              acc[1][ct] = mma3h_t(ch_[1][kk], cl_[1][kk], bh, bl, acc[1][ct]);
+            } else {
+              acc[0][ct] = mma3h(ch_[0][kk], cl_[0][kk], bh, bl, acc[0][ct]);
+              acc[1][ct] = mma3h(ch_[1][kk], cl_[1][kk], bh, bl, acc[1][ct]);
+            }
           }
         }
 #pragma unroll
@@ -450,6 +550,10 @@ __global__ __launch_bounds__(256, LB) void conv_fwd_x3(const uint16_t* __restric
           rowit_adv(eit[i], 128, E, G::HOWO);
           if (r16 >= Rtot) continue;
           const long grow4 = rowit_sample(e0, p, E, PE, t0) * G::HOWO + e0.pos;
+          if constexpr (SW) {
+            conv_epi_sw<NC>(acc[i], bias_s, ct0, cnt, q, in_scale, out_scale, grow4, bits, bits_rows, Y, ylo, pass > 0);
+            continue;
+          }
           float sum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int ct = 0; ct < NC; ++ct) {
@@ -973,6 +1077,195 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
       case 1: run(std::integral_constant<int, 1>{}, ct0); break;
       case 2: run(std::integral_constant<int, 2>{}, ct0); break;
       default: run(std::integral_constant<int, 3>{}, ct0); break;
+    }
+  }
+  __syncthreads();
+  if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
+}
+
+// ===========================================================================
+// weight gradient of the 18x13x8 3x3/s1 layer, one SAMPLE per stage: the sample's fp16-pair input tile is converted
+// to a bf16 pair ONCE into LDS (1872 elements, instead of 9 im2col copies of each element as in conv_wgrad_x3), and
+// the MFMA A operand (im2col^T: k = (kh, kw, ci) x 8 positions) is read straight from the tile with
+// ds_read_b64_tr_b16 -- a lane's address is (position offset) + (tap/channel-chunk offset), both precomputed, so
+// there is no im2col staging at all.  B = the masked, split output gradient of <= 4 slots [192 positions][32].
+// 5 waves: wave w owns k rows 16w..16w+15 (the fifth tile is half padding) for every position step and column tile.
+// Double-buffered LDS, one register set of next-sample loads in flight.  grid = (chunks, P).
+// ===========================================================================
+template <class G>
+struct WT3 {
+  static constexpr int NPOS = G::HOWO;                   // 176 output positions
+  static constexpr int NKS = (NPOS + 31) / 32;           // 6 position steps (192 rows, 16 zero)
+  static constexpr int NPP = NKS * 32;
+  static constexpr int NMT = (G::K + 15) / 16;           // 5 k tiles
+  static constexpr int NW = NMT;
+  static constexpr int NT = NW * 64;
+  static constexpr int TILE = G::IN_ELEMS;               // 1872
+  static constexpr int TILEP = (TILE + 8 + 7) / 8 * 8;   // + a zero pad chunk
+  static constexpr int NXC = TILE / 8;                   // 234 8-element chunks
+  static constexpr int GS = 2 * 16 + 8;                  // 4 slots x 8 maps + pad (bf16)
+  static constexpr int NGI = NPOS * 4;                   // (position, slot) staging items
+  static constexpr int GIT = (NGI + NT - 1) / NT;
+  static_assert(G::S == 1 && G::CIN == 8 && TILE % 8 == 0, "3x3/s1 8-channel layer");
+  static_assert(NT % 4 == 0, "a thread's staging items share one slot");
+};
+
+template <class G>
+__global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16_t* __restrict__ X, long xlo,
+                                                                   const float* __restrict__ Gr,
+                                                                   const uint8_t* __restrict__ bits,
+                                                                   float* __restrict__ grad, long w_off, long b_off,
+                                                                   int chunk, const int* __restrict__ act_idx,
+                                                                   const int* __restrict__ act_cnt, int layer, int L,
+                                                                   int M, int P, int E, int T, long bits_rows,
+                                                                   int samples_per_wg, float in_scale, float g_scale) {
+  using W = WT3<G>;
+  __shared__ __attribute__((aligned(16))) bf16_t Xt[2][2][W::TILEP];
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][2][W::NPP * W::GS];
+  __shared__ float dbias[X3_NCT * 16];
+  __shared__ int mods[X3_MAXM];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  if (cnt == 0) return;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
+  const int PE = P * E;
+  const int nsamp = T * E;
+  const int s_beg = blockIdx.x * samples_per_wg;
+  const int s_end = min(nsamp, s_beg + samples_per_wg);
+  if (s_beg >= s_end) return;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  if (tid < X3_NCT * 16) dbias[tid] = 0.f;
+  // zero rows 176..191 of both G buffers and the tile pad chunk (never rewritten)
+  for (int i = tid; i < 2 * 2 * (W::NPP - W::NPOS) * W::GS; i += W::NT) {
+    const int per = (W::NPP - W::NPOS) * W::GS;
+    Gs[i / (2 * per)][(i / per) & 1][W::NPOS * W::GS + i % per] = 0;
+  }
+  for (int i = tid; i < 2 * 2 * (W::TILEP - W::TILE); i += W::NT) {
+    const int per = W::TILEP - W::TILE;
+    Xt[i / (2 * per)][(i / per) & 1][W::TILE + i % per] = 0;
+  }
+  // A addresses: lane 4q+pp of a 16-lane group supplies (position 8*grp + 4*hf + q of step ks, k chunk 4*pp of the
+  // wave's k tile); out-of-range positions / k read the zero pad chunk (their G rows / D rows are zero / dropped)
+  int posoff[W::NKS][2];
+#pragma unroll
+  for (int ks = 0; ks < W::NKS; ++ks)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int pos = ks * 32 + 8 * grp + 4 * hf + q;
+      const int oh = pos / G::WO, ow = pos - (pos / G::WO) * G::WO;
+      posoff[ks][hf] = pos < W::NPOS ? (oh * G::WIN + ow) * 8 : -1;
+    }
+  int koff;
+  {
+    const int k = w * 16 + 4 * pp;
+    const int tap = k >> 3, kh = tap / G::KW, kw = tap - (tap / G::KW) * G::KW;
+    koff = k < G::K ? (kh * G::WIN + kw) * 8 + (k & 7) : -1;
+  }
+#pragma unroll
+  for (int ks = 0; ks < W::NKS; ++ks)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) posoff[ks][hf] = (posoff[ks][hf] < 0 || koff < 0) ? W::TILE : posoff[ks][hf] + koff;
+  const int nct = (cnt + 1) >> 1;
+  const int npass = (nct + 1) / 2;
+  const int a_my = tid & 3;                       // the slot (within the pass) of every staging item of this thread
+  for (int pass = 0; pass < npass; ++pass) {
+    const int ct0 = pass * 2;
+    const int nc = min(2, nct - ct0);
+    const bool slot_ok = a_my < 2 * nc && 2 * ct0 + a_my < cnt;
+    float bpart[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    f4v acc[2];
+    acc[0] = acc[1] = (f4v){0.f, 0.f, 0.f, 0.f};
+    float4 g0r[W::GIT], g1r[W::GIT];
+    uint32_t gb[W::GIT];
+    s8v xh, xl;
+    auto load_sample = [&](int s) {
+      const long sg = sample_global(p, s, E, PE, 0);
+#pragma unroll
+      for (int j = 0; j < W::GIT; ++j) {
+        const int it = tid + W::NT * j;
+        gb[j] = 0;
+        if (it < W::NGI) {
+          const long go = sg * G::HOWO + (it >> 2);
+          g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+          g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+          if (slot_ok) gb[j] = bits[(long)(2 * ct0 + a_my) * bits_rows + go];
+        }
+      }
+      if (tid < W::NXC) {
+        const long xo = sg * (long)W::TILE + tid * 8;
+        xh = *reinterpret_cast<const s8v*>(X + xo);
+        xl = *reinterpret_cast<const s8v*>(X + xlo + xo);
+      }
+    };
+    auto write_sample = [&](int buf) {
+      if (tid < W::NXC) {
+        s8v bh, bl;
+        x16pair_to_bf16pair(xh, xl, bh, bl);
+        *reinterpret_cast<s8v*>(&Xt[buf][0][tid * 8]) = bh;
+        *reinterpret_cast<s8v*>(&Xt[buf][1][tid * 8]) = bl;
+      }
+#pragma unroll
+      for (int j = 0; j < W::GIT; ++j) {
+        const int it = tid + W::NT * j;
+        if (it < W::NGI) {
+          const float gg[8] = {g0r[j].x, g0r[j].y, g0r[j].z, g0r[j].w, g1r[j].x, g1r[j].y, g1r[j].z, g1r[j].w};
+          float m[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            m[c] = ((gb[j] >> c) & 1u) ? gg[c] : 0.f;
+            bpart[c] += m[c];
+          }
+          s8v hi, lo;
+          split8(m, hi, lo);
+          const int o = (it >> 2) * W::GS + a_my * 8;
+          *reinterpret_cast<s8v*>(&Gs[buf][0][o]) = hi;
+          *reinterpret_cast<s8v*>(&Gs[buf][1][o]) = lo;
+        }
+      }
+    };
+    auto compute = [&](int buf, auto ncc) {
+      constexpr int NC = decltype(ncc)::value;
+#pragma unroll
+      for (int ks = 0; ks < W::NKS; ++ks) {
+        const s8v ah = tr8(Xt[buf][0] + posoff[ks][0], Xt[buf][0] + posoff[ks][1]);
+        const s8v al = tr8(Xt[buf][1] + posoff[ks][0], Xt[buf][1] + posoff[ks][1]);
+#pragma unroll
+        for (int nt = 0; nt < NC; ++nt) {
+          const int o0 = (ks * 32 + 8 * grp + q) * W::GS + nt * 16 + 4 * pp;
+          const int o1 = (ks * 32 + 8 * grp + 4 + q) * W::GS + nt * 16 + 4 * pp;
+          const s8v bh = tr8(Gs[buf][0] + o0, Gs[buf][0] + o1);
+          const s8v bl = tr8(Gs[buf][1] + o0, Gs[buf][1] + o1);
+          acc[nt] = mma3(ah, al, bh, bl, acc[nt]);
+        }
+      }
+    };
+    __syncthreads();     // mods / dbias / pads visible; the previous pass's LDS reads done
+    load_sample(s_beg);
+    int buf = 0;
+    for (int s = s_beg; s < s_end; ++s, buf ^= 1) {
+      write_sample(buf);
+      __syncthreads();
+      if (s + 1 < s_end) load_sample(s + 1);
+      if (nc == 2) compute(buf, std::integral_constant<int, 2>{});
+      else compute(buf, std::integral_constant<int, 1>{});
+    }
+    const int h = i16 >> 3, ch = l & 7;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int slot = (ct0 + nt) * 2 + h;
+      if (nt < nc && slot < cnt) {
+        const long base = w_off + (long)mods[slot] * chunk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = w * 16 + 4 * grp + r;
+          if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[nt][r] * (in_scale * g_scale));
+        }
+      }
+    }
+    if (slot_ok) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) atomicAdd(&dbias[(2 * ct0 + a_my) * 8 + c], bpart[c] * g_scale);
     }
   }
   __syncthreads();
@@ -2101,17 +2394,23 @@ static int X3_FWD_DB = 0;      // bf16-activation conv forward: 1 = double-buffe
 // and 1 for the uint8 first layer (measured, steady-state window: conv1 2.63 (2) -> 2.32 ms (1), conv2 0.50 (2) vs
 // 0.52 ms (1); profiles/r3/kwin_x3_v4*.md)
 static int X3_WGRAD_PF = 3;
+// conv forward epilogue, bit 0: first layer, bit 1: the bf16-activation layers; set = swapped MFMA orientation
+// (conv_epi_sw; first layer also with the 1024-offset pixels folded into the bias), clear = rows-as-A
+static int X3_FWD_SW = 1;
 static int X3_FC_D = 4;        // fc forward register ring depth (k-steps of hi/lo A and B fragments in flight)
 // fc forward split-K waves per module (1 = fc_fwd_x3, 2 = fc_fwd_ks_x3).  Measured: fc1 66.4 (2) vs 65.1 us (1),
 // fc2 19.7 vs 17.4 (profiles/r3/kwin_x3_v7*.md): more waves on the same weight traffic do not help -- the launch
 // is bound by its L2/MALL traffic, not by load latency
 static int X3_FC_KS = 1;
+static int X3_WG3_TILE = 1;    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
 extern "C" {
 
 void fast_conv_set_x3_fwd_nt(int nt) { X3_FWD_NT = nt; }
 void fast_conv_set_x3_fwd_lb(int lb) { X3_FWD_LB = lb; }
 void fast_conv_set_x3_fwd_db(int db) { X3_FWD_DB = db; }
+void fast_conv_set_x3_fwd_sw(int sw) { X3_FWD_SW = sw; }
+void fast_conv_set_x3_wg3_tile(int t) { X3_WG3_TILE = t; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
@@ -2129,7 +2428,9 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
     const long rows = (long)T * E * C1::HOWO;
     const float isc = is / (float)(1 << X3_W0_SHIFT);
 #define C1L(NT_, LB_)                                                                                           \
-  conv1_fwd_x2<C1, NT_, LB_><<<dim3((unsigned)((rows + NT_ * 128 - 1) / (NT_ * 128)), P), 256, 0, st>>>(             \
+  if (X3_FWD_SW & 1) C1LS(NT_, LB_, true); else C1LS(NT_, LB_, false)
+#define C1LS(NT_, LB_, SW_)                                                                                     \
+  conv1_fwd_x2<C1, NT_, LB_, SW_><<<dim3((unsigned)((rows + NT_ * 128 - 1) / (NT_ * 128)), P), 256, 0, st>>>(             \
       (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, \
       layer, L, M, P, E, T, t0, br, isc, os)
     if (X3_FWD_LB >= 3) {
@@ -2138,6 +2439,7 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
       if (X3_FWD_NT >= 8) C1L(8, 2); else C1L(4, 2);
     }
 #undef C1L
+#undef C1LS
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   }
@@ -2148,11 +2450,15 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
     const dim3 grid((unsigned)((rows + 511) / 512), P);                                                           \
     const float isc = is / (float)(1 << X3_W0_SHIFT);                                                             \
     if (X3_FWD_DB)                                                                                                \
-      conv_fwd_x3<Gx, 4, 2, true><<<grid, 256, 0, st>>>(                                                          \
+      conv_fwd_x3<Gx, 4, 2, true, false><<<grid, 256, 0, st>>>(                                                   \
+          (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \
+          chunk, ai, ac, layer, L, M, P, E, T, t0, br, isc, os);                                                  \
+    else if (X3_FWD_SW & 2)                                                                                       \
+      conv_fwd_x3<Gx, 4, 3, false, true><<<grid, 256, 0, st>>>(                                                   \
           (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \
           chunk, ai, ac, layer, L, M, P, E, T, t0, br, isc, os);                                                  \
     else                                                                                                          \
-      conv_fwd_x3<Gx, 4, 3, false><<<grid, 256, 0, st>>>(                                                         \
+      conv_fwd_x3<Gx, 4, 3, false, false><<<grid, 256, 0, st>>>(                                                  \
           (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \
           chunk, ai, ac, layer, L, M, P, E, T, t0, br, isc, os);                                                  \
     const int rc = (int)hipGetLastError();                                                                        \
@@ -2192,6 +2498,17 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
   if (x3_is<C2>(Hin, Win, Cin, KH, KW, S, u8in)) {
     if (xlo <= 0) return -22;
     return slab(Tag<C2>{}, std::integral_constant<int, 7>{});
+  }
+  if (x3_is<C3>(Hin, Win, Cin, KH, KW, S, u8in) && X3_WG3_TILE) {
+    if (xlo <= 0) return -22;
+    const long nsamp = (long)T * E;
+    long spw = (nsamp * P + 511) / 512;            // ~2 workgroups per CU over the whole launch
+    if (spw < 4) spw = 4;
+    conv_wgrad_tile_x3<C3><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), WT3<C3>::NT, 0, st>>>(
+        (const uint16_t*)X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br,
+        (int)spw, is, gs);
+    const int rc = (int)hipGetLastError();
+    return rc ? -rc : 1;
   }
   if (x3_is<C3>(Hin, Win, Cin, KH, KW, S, u8in)) {
     if (xlo <= 0) return -22;

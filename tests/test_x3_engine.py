@@ -205,3 +205,69 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
         assert rel(a, b) < 1e-6, (l, rel(a, b))
         same = (outs[0][1][l] == outs[1][1][l]).float().mean().item()
         assert same > 0.999, (l, same)
+
+
+@pytest.mark.parametrize("T", [1, 2])
+def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T):
+    """conv_epi_sw (weights as the MFMA A operand: one xor-32 module-pair sum, nibble ReLU bits, 8-byte stores; the
+    first layer with fp16(1024 + v) pixels and the offset folded into the bias) == the rows-as-A epilogue: conv2/3
+    bit-identical, conv1 to fp32 rounding of the offset sum; ReLU bits equal but for near-zero ties.  T = 2 runs the
+    multi-step row walk (backward-style launches), T = 1 the rollout's linear rows."""
+    from pathnet_gym_amd.ops import _lib
+    cfg = pixel_cfg()
+    P, E = 5, 16
+    m = ACPathNet(cfg, P, DEV, "hip", seed=11, compute_dtype="fp32x")
+    m.set_paths(masks_with_edges(P, cfg.L, cfg.M, cfg.N, seed=6))
+    hp = m.hip
+    g = torch.Generator(device="cpu").manual_seed(5)
+    obs = torch.randint(0, 256, (T * P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+    lib = _lib.lib()
+    outs = []
+    for sw in (0, 3):
+        lib.fast_conv_set_x3_fwd_sw(sw)
+        acts, bits = [], []
+        x = obs
+        for l in range(3):
+            geo = hp.geoms[l]
+            Y = hp.alloc_act(l, (T, P * E, geo.out_feat))
+            b, rows = hp.alloc_bits(l, T, P * E)
+            hp.layer_fwd(l, x, Y, b, P, E, T, 0, rows)
+            acts.append(Y)
+            bits.append(b)
+            x = Y
+        torch.cuda.synchronize()
+        outs.append(([x2_value(a) for a in acts], [b.clone() for b in bits]))
+    lib.fast_conv_set_x3_fwd_sw(1)
+    for l in range(3):
+        a, b = outs[0][0][l], outs[1][0][l]
+        e = rel(b, a)
+        same = (outs[0][1][l] == outs[1][1][l]).float().mean().item()
+        print(f"layer {l}: rel {e:.2e}, relu-bit bytes equal {same:.6f}")
+        assert e < 3e-6, (l, e)
+        assert same > 0.999, (l, same)
+
+
+def test_x3_conv3_wgrad_tile_matches_im2col_rows(x3_rollout):
+    """conv_wgrad_tile_x3 (one sample per stage: the input tile converted once, im2col^T read straight from it with
+    transposed LDS reads) == conv_wgrad_x3 (32-row im2col stages) up to fp32 summation order, weights and biases."""
+    from pathnet_gym_amd.ops import _lib
+    tr, eng, g_ref, g_hip = x3_rollout
+    hp = tr.model.hip
+    lib = _lib.lib()
+    l = 2
+    g = hp.geoms[l]
+    seg = slice(g.w_off, g.w_off + hp.M * g.chunk)
+    outs = []
+    for tile in (0, 1):
+        lib.fast_conv_set_x3_wg3_tile(tile)
+        eng.grad_flat.zero_()
+        hp.layer_bwd(l, eng.acts[l - 1], eng.grads[l], eng.bits[l], eng.grad_flat, eng.grads[l - 1], eng.P, eng.E,
+                     eng.T, eng.bits_rows[l])
+        torch.cuda.synchronize()
+        outs.append(eng.grad_flat[seg].clone())
+    lib.fast_conv_set_x3_wg3_tile(1)
+    assert outs[0].norm() > 0
+    e = rel(outs[1], outs[0])
+    print(f"conv3 wgrad tile vs im2col rows: rel {e:.2e}")
+    assert e < 1e-6, e
+    assert rel(outs[1], g_hip[seg]) < 1e-6
