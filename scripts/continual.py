@@ -53,19 +53,24 @@ def build_cfg(args, tasks):
 
 
 def greedy_eval(tr, ti, name, args, dev, sample=False):
-    """Task ti's frozen path + head on a fresh env: argmax actions, or (sample=True) the seeded sampled policy
-    (a greedy Breakout policy may never press FIRE, so no episode ends)."""
+    """Task ti's frozen path + head on fresh envs: argmax actions, or (sample=True) the seeded sampled policy
+    (a greedy Breakout policy may never press FIRE, so no episode ends).  The ``eval_episodes`` episodes run as
+    that many differently seeded envs in one batch (one episode each), so an evaluation costs one episode's steps."""
     from pathnet_gym_amd.algo.evaluate import evaluate_model
     from pathnet_gym_amd.models.acnet import ACPathNet
+    import numpy as np
     import torch
-    m = ACPathNet(tr.cfg.net, 1, dev, "torch")
+    n = max(1, args.eval_episodes)
+    print(json.dumps({"eval": name, "task": ti, "sample": sample, "envs": n}), flush=True)   # progress heartbeat
+    m = ACPathNet(tr.cfg.net, n, dev, "torch")
     with torch.no_grad():
         m.store.flat.copy_(tr.model.store.flat.detach())
-    m.set_paths(tr.task_paths[ti][None])
+    m.set_paths(np.repeat(tr.task_paths[ti][None], n, axis=0))
     m.task = ti
-    r = evaluate_model(m, name, episodes=args.eval_episodes, max_steps=args.eval_steps, device=dev,
+    r = evaluate_model(m, name, episodes=1, max_steps=args.eval_steps, device=dev,
                        frameskip=tr.cfg.frameskip, gray=tr.cfg.gray, sample=sample)
-    return r[0] if math.isfinite(r[0]) else None
+    r = [x for x in r if math.isfinite(x)]
+    return float(np.mean(r)) if r else None
 
 
 def train_task(tr, ti, args, label):
