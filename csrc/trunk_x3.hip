@@ -1907,6 +1907,161 @@ __global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__
   }
 }
 
+// ===========================================================================
+// fc forward, module-major with LDS-staged tiles.  fc_fwd_mm_x3 above shares a module's weights across paths but
+// keeps the path-major kernel's ratio of global fragment loads to MFMAs (12 16-byte loads per 24 MFMAs per wave),
+// and that ratio is what bounds both: the kernel waits on its L1/L2 fragment traffic, not on HBM.  Here a
+// workgroup = one active module j x 128 rows (taken from the paths on j's inverse list) x 128 columns; each k-step
+// stages the A tile [128 rows][32] and B tile [128 columns][32] (fp16 hi/lo planes, 32 KB) once in LDS with four
+// 16-byte loads per thread, and 8 waves (2 x 4, wave tile 64 rows x 32 columns) read them: 12 ds_read_b128 per
+// 24 MFMAs, each global byte read once per workgroup.  Double-buffered LDS, next k-step's loads in registers.  LDS
+// rows are 64 B with the 16-byte chunk index XORed by (-(row >> 2)) & 3, conflict-free for the ds_read_b128 lane
+// groups of the MFMA operand reads.  relu(W_j x + b_j) -> slot plane Ys, bits -> `bits`; fc_slot_sum_x3 sums.
+// ===========================================================================
+DEVI int mm2_sw(int row, int ch) { return (row << 2) + (ch ^ ((-(row >> 2)) & 3)); }   // 16-byte chunk index
+
+template <int NKS, int PF>
+__global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restrict__ X, long xlo, int ldx,
+                                                       float* __restrict__ Ys, uint16_t* __restrict__ bits,
+                                                       const uint16_t* __restrict__ Wc, long wlo,
+                                                       const float* __restrict__ flat, long bias_off, int chunk,
+                                                       const int* __restrict__ inv_path,
+                                                       const int* __restrict__ inv_slot,
+                                                       const int* __restrict__ inv_cnt, int layer, int M, int KP, int P,
+                                                       int E, int T, int t0, long bits_rows, float in_scale) {
+  constexpr int COUT = 256, BR = 128, BC = 128, NCS = COUT / BC, NWORDS = COUT / 16;
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][2][BR * 32];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][2][BC * 32];
+  const int R = T * E;
+  // unit -> (module j, row block, column half); units of module j = ceil(inv_cnt[j] * R / 128) x NCS
+  int u = (int)blockIdx.x, j = 0, ncnt = 0;
+  for (; j < M; ++j) {
+    ncnt = inv_cnt[layer * M + j];
+    const int n = NCS * ((ncnt * R + BR - 1) / BR);
+    if (u < n) break;
+    u -= n;
+  }
+  if (j >= M) return;                                    // grid is an upper bound on the unit count
+  const int chalf = u % NCS, rb = u / NCS;
+  const int nrows = ncnt * R;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int wr = w >> 2, wc = w & 3;                     // wave tile: rows 64*wr.., columns 32*wc.. of the block
+  const int PE = P * E;
+  const long lbase = ((long)layer * M + j) * P;
+  const int col0 = chalf * BC;
+  // staging role: thread -> (row / column srow, 16-byte chunk skc) of the 128 x 32 tiles
+  const int srow = tid >> 2, skc = tid & 3;
+  long xoff;
+  {
+    const int gr = rb * BR + srow;
+    const int q = gr < nrows ? gr / R : 0, rr = gr < nrows ? gr - q * R : 0;
+    xoff = sample_global(inv_path[lbase + q], rr, E, PE, t0) * (long)ldx + skc * 8;
+  }
+  const uint16_t* wsrc = Wc + ((long)j * COUT + col0 + srow) * KP + skc * 8;
+  const int sdst = mm2_sw(srow, skc) * 8;
+  // PF register sets of k-step loads in flight (a k-step's MFMA work is ~400 cycles per wave, far below the
+  // L2/MALL latency of its loads: one step of lookahead left the kernel waiting on every step).  Plain vector
+  // registers (a struct array captured by the lambdas went to scratch).
+  static_assert(PF == 3, "three named register sets (an indexed array of them went to scratch)");
+  uint4 ga0, gx0, gb0, gy0, ga1, gx1, gb1, gy1, ga2, gx2, gb2, gy2;
+#define MM2_GLOAD(d, ks)                                                     \
+  do {                                                                       \
+    const int k0_ = (ks) * 32;                                               \
+    ga##d = *reinterpret_cast<const uint4*>(X + xoff + k0_);                 \
+    gx##d = *reinterpret_cast<const uint4*>(X + xlo + xoff + k0_);           \
+    gb##d = *reinterpret_cast<const uint4*>(wsrc + k0_);                     \
+    gy##d = *reinterpret_cast<const uint4*>(wsrc + wlo + k0_);               \
+  } while (0)
+#define MM2_LSTORE(d, buf)                                                   \
+  do {                                                                       \
+    *reinterpret_cast<uint4*>(&As[buf][0][sdst]) = ga##d;                    \
+    *reinterpret_cast<uint4*>(&As[buf][1][sdst]) = gx##d;                    \
+    *reinterpret_cast<uint4*>(&Bs[buf][0][sdst]) = gb##d;                    \
+    *reinterpret_cast<uint4*>(&Bs[buf][1][sdst]) = gy##d;                    \
+  } while (0)
+  f4v acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = (f4v){0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) {
+    s8v bh[2], bl[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int o = mm2_sw(wc * 32 + jj * 16 + c16, grp) * 8;
+      bh[jj] = *reinterpret_cast<const s8v*>(&Bs[buf][0][o]);
+      bl[jj] = *reinterpret_cast<const s8v*>(&Bs[buf][1][o]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int o = mm2_sw(wr * 64 + i * 16 + c16, grp) * 8;
+      const s8v ah = *reinterpret_cast<const s8v*>(&As[buf][0][o]);
+      const s8v al = *reinterpret_cast<const s8v*>(&As[buf][1][o]);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma3h(ah, al, bh[jj], bl[jj], acc[i][jj]);
+    }
+  };
+  const int nks = NKS > 0 ? NKS : KP / 32;
+  MM2_GLOAD(0, 0);
+  MM2_LSTORE(0, 0);
+  if (1 < nks) MM2_GLOAD(0, 1);                    // set d holds k-step d + 1, then d + 1 + PF, ...
+  if (2 < nks) MM2_GLOAD(1, 2);
+  if (3 < nks) MM2_GLOAD(2, 3);
+  __syncthreads();
+  // full groups of PF steps: every reload unconditional (clamped to the last k-step; a conditional reload is a
+  // loop-carried phi), the remainder peeled.  Buffer (ks + 1) & 1 was last read in step ks - 1, before the
+  // barrier that ended it; after the last step the store is dead (nothing reads that buffer again).
+#define MM2_STEP(d, ks)                                                      \
+  do {                                                                       \
+    compute((ks) & 1);                                                       \
+    MM2_LSTORE(d, ((ks) + 1) & 1);                                           \
+    MM2_GLOAD(d, min((ks) + 1 + PF, nks - 1));                               \
+    __syncthreads();                                                         \
+  } while (0)
+  int k0 = 0;
+  for (; k0 + PF <= nks; k0 += PF) {
+    MM2_STEP(0, k0);
+    MM2_STEP(1, k0 + 1);
+    MM2_STEP(2, k0 + 2);
+  }
+  if (k0 < nks) { compute(k0 & 1); MM2_LSTORE(0, (k0 + 1) & 1); __syncthreads(); }
+  if (k0 + 1 < nks) { compute((k0 + 1) & 1); MM2_LSTORE(1, (k0 + 2) & 1); __syncthreads(); }
+#undef MM2_STEP
+#undef MM2_GLOAD
+#undef MM2_LSTORE
+  // epilogue: rows-as-A D layout (lane: rows 4*grp + r of each 16-row tile, column c16), bits as 16-bit ballots
+  const long PR = (long)P * R;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gr0 = rb * BR + wr * 64 + i * 16 + 4 * grp;
+    int pth[4], slt[4], rr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gr = gr0 + r;
+      const int q = gr < nrows ? gr / R : -1;
+      pth[r] = q >= 0 ? inv_path[lbase + q] : -1;
+      slt[r] = q >= 0 ? inv_slot[lbase + q] : 0;
+      rr[r] = q >= 0 ? gr - q * R : 0;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int col = col0 + wc * 32 + jj * 16;
+      const float bb = flat[bias_off + (long)j * chunk + col + c16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[i][jj][r] * in_scale + bb;
+        const bool pos = v > 0.f;
+        const uint64_t bal = __ballot(pos);
+        if (pth[r] >= 0) {
+          Ys[((long)slt[r] * PR + (long)pth[r] * R + rr[r]) * COUT + col + c16] = pos ? v : 0.f;
+          if (c16 == 0)
+            bits[((long)slt[r] * bits_rows + sample_global(pth[r], rr[r], E, PE, t0)) * NWORDS + col / 16] =
+                (uint16_t)((bal >> (16 * grp)) & 0xFFFFull);
+        }
+      }
+    }
+  }
+}
+
 // sum every path's module slots in slot order (one thread per row x 8 columns) -> Y (fp32, or an fp16 pair)
 template <bool OF32>
 __global__ __launch_bounds__(256) void fc_slot_sum_x3(const float* __restrict__ Ys, const int* __restrict__ act_cnt,
@@ -2402,6 +2557,9 @@ static int X3_FC_D = 4;        // fc forward register ring depth (k-steps of hi/
 // fc2 19.7 vs 17.4 (profiles/r3/kwin_x3_v7*.md): more waves on the same weight traffic do not help -- the launch
 // is bound by its L2/MALL traffic, not by load latency
 static int X3_FC_KS = 1;
+// module-major fc forward kernel (when the Python side selects module-major): 1 = fc_fwd_mm_x3 (register
+// fragments), 2 = fc_fwd_mm2_x3 (LDS-staged 128 x 128 tiles)
+static int X3_FC_MMV = 2;
 static int X3_WG3_TILE = 1;    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
 extern "C" {
@@ -2411,6 +2569,7 @@ void fast_conv_set_x3_fwd_lb(int lb) { X3_FWD_LB = lb; }
 void fast_conv_set_x3_fwd_db(int db) { X3_FWD_DB = db; }
 void fast_conv_set_x3_fwd_sw(int sw) { X3_FWD_SW = sw; }
 void fast_conv_set_x3_wg3_tile(int t) { X3_WG3_TILE = t; }
+void fast_conv_set_x3_fc_mmv(int v) { X3_FC_MMV = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
@@ -2597,15 +2756,27 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
       !inv_slot || !inv_cnt) return -22;
   if (M > X3_MAXM || KP % 32 != 0 || Cout != 256 || ldx % 8 != 0 || ldx < KP || (long)T * E > 32) return 0;
   const int R = T * E, tpp = (R + 15) / 16;
-  const int umax = M * ((P * tpp + 3) / 4) * 2;      // x 2 column slices (fc_fwd_mm_x3 NH)
-  const int nwg = (umax + 7) / 8 * 8;
   const float isc = 1.f / (float)(1 << X3_W0_SHIFT);
+  if (X3_FC_MMV >= 2) {
+    const int umax = M * 2 * ((P * R + 127) / 128);    // every module on every path: an upper bound
+    if (KP == 256)
+      fc_fwd_mm2_x3<8, 3><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits, (const uint16_t*)Wc,
+                                             wlo, flat, bias_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, KP, P,
+                                             E, T, t0, br, isc);
+    else
+      fc_fwd_mm2_x3<0, 3><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits, (const uint16_t*)Wc,
+                                             wlo, flat, bias_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, KP, P,
+                                             E, T, t0, br, isc);
+  } else {
+    const int umax = M * ((P * tpp + 3) / 4) * 2;    // x 2 column slices (fc_fwd_mm_x3 NH)
+    const int nwg = (umax + 7) / 8 * 8;
 #define FMM(NKS_)                                                                                                 \
   fc_fwd_mm_x3<NKS_><<<nwg, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits, (const uint16_t*)Wc, \
                                           wlo, flat, bias_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, KP, P, E, \
                                           T, t0, br, isc)
-  if (KP == 256) FMM(8); else FMM(0);        // (a constant 44-step loop spills: runtime count for fc1)
+    if (KP == 256) FMM(8); else FMM(0);      // (a constant 44-step loop spills: runtime count for fc1)
 #undef FMM
+  }
   int rc = (int)hipGetLastError();
   if (rc) return -rc;
   const long thr = (long)P * R * 32;

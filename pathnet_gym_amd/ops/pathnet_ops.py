@@ -174,10 +174,13 @@ class HipPathNet:
         self.x3_status = torch.zeros(1, dtype=torch.int32, device=dev)   # fp16 range overflow of the scaled conv1 pair
         self._part = None            # fp32 conv wgrad partial slabs (allocated on first use, before capture)
         self._ys = None              # fp32x module-major fc forward: per-slot fp32 output planes
-        # fp32x fc forward: module-major (one workgroup per module x 64 rows of its paths, csrc/trunk_x3.hip
-        # fc_fwd_mm_x3) instead of path-major.  Measured slower at the bench shape (fc1 95.6 vs 70.3 us: 128
-        # workgroups leave half the CUs idle; profiles/r3/kwin_x3_v6*.md), so off unless PATHNET_X3_FC_MM=1
-        self.fc_fwd_mm = os.environ.get("PATHNET_X3_FC_MM", "0") == "1"
+        # fp32x fc forward: module-major (csrc/trunk_x3.hip fc_fwd_mm2_x3: one workgroup per module x 128 rows of
+        # its paths x 128 columns, LDS-staged tiles, then fc_slot_sum_x3) instead of path-major (fc_fwd_x3, which
+        # re-reads a module's weights per path and is bound by its fragment loads).  The first module-major kernel
+        # (register fragments, fast_conv_set_x3_fc_mmv(1)) measured slower (fc1 95.6 vs 70.3 us,
+        # profiles/r3/kwin_x3_v6*.md).  PATHNET_X3_FC_MM=0 selects path-major.
+        self.fc_fwd_mm = os.environ.get("PATHNET_X3_FC_MM", "1") == "1"
+        self.fc_fwd_mm_min_k = int(os.environ.get("PATHNET_X3_FC_MM_MIN_K", "1024"))   # fc2 (K = 256): path-major
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
         self.inv_slot = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
@@ -485,7 +488,8 @@ class HipPathNet:
             ok = _lib.call_fast("x3_conv_fwd", xp, self._x3_lo(X), int(g.u8in), yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
                                 flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L, self.M, g.Hin, g.Win, g.Cin,
                                 g.KH, g.KW, g.S, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
-        elif self.fc_fwd_mm and g.Cout == 256 and P == self.model.P and aip == self.model.act_idx.data_ptr():
+        elif self.fc_fwd_mm and g.Cout == 256 and g.K >= self.fc_fwd_mm_min_k and P == self.model.P \
+                and aip == self.model.act_idx.data_ptr():
             # module-major: each module's weight slice read once per 64 rows of the paths using it
             ys = self._ys_buffer_x3(P * T * E)
             ok = _lib.call_fast("x3_fc_fwd_mm", xp, x2_lo(X), g.ldx, yp, ylo, bp, self.Wc[l].data_ptr(), wlo,

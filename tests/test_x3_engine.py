@@ -169,7 +169,7 @@ def test_x3_gradient_check_detects_a_two_percent_module_error(x3_rollout):
 
 
 @pytest.mark.parametrize("E", [16, 32])
-@pytest.mark.parametrize("variant", ["split_k", "module_major"])
+@pytest.mark.parametrize("variant", ["split_k", "module_major", "module_major_regs"])
 def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     """fc_fwd_ks_x3 (two waves per module, partial sums meet in LDS) and fc_fwd_mm_x3 (one workgroup per module
     x 64 rows, slot planes summed in slot order) == the path-major fc_fwd_x3 up to summation order: outputs to
@@ -184,9 +184,11 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     obs = torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
     outs = []
     lib = _lib.lib()
+    lib.fast_conv_set_x3_fc_mmv(1 if variant == "module_major_regs" else 2)
+    hp.fc_fwd_mm_min_k = 0
     for ref in (False, True):
-        hp.fc_fwd_mm = variant == "module_major" and not ref
-        lib.fast_conv_set_x3_fc_ks(1 if ref or variant == "module_major" else 2)
+        hp.fc_fwd_mm = variant.startswith("module_major") and not ref
+        lib.fast_conv_set_x3_fc_ks(1 if ref or variant.startswith("module_major") else 2)
         acts, bits = [], []
         x = obs
         for l, geo in enumerate(hp.geoms):
@@ -198,8 +200,9 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
             x = Y
         torch.cuda.synchronize()
         outs.append(([x2_value(a) if a.dtype == torch.float16 else a.clone() for a in acts], [b.clone() for b in bits]))
-    hp.fc_fwd_mm = False
-    lib.fast_conv_set_x3_fc_ks(2)
+    hp.fc_fwd_mm = True
+    lib.fast_conv_set_x3_fc_mmv(2)
+    lib.fast_conv_set_x3_fc_ks(1)
     for l in (3, 4):
         a, b = outs[0][0][l], outs[1][0][l]
         assert rel(a, b) < 1e-6, (l, rel(a, b))
