@@ -52,7 +52,7 @@ def build_cfg(args, tasks):
     return cfg
 
 
-def greedy_eval(tr, ti, name, args, dev, sample=False):
+def greedy_eval(tr, ti, name, args, dev, sample=False, flat=None):
     """Task ti's frozen path + head on fresh envs: argmax actions, or (sample=True) the seeded sampled policy
     (a greedy Breakout policy may never press FIRE, so no episode ends).  The ``eval_episodes`` episodes run as
     that many differently seeded envs in one batch (one episode each), so an evaluation costs one episode's steps."""
@@ -64,7 +64,7 @@ def greedy_eval(tr, ti, name, args, dev, sample=False):
     print(json.dumps({"eval": name, "task": ti, "sample": sample, "envs": n}), flush=True)   # progress heartbeat
     m = ACPathNet(tr.cfg.net, n, dev, "torch")
     with torch.no_grad():
-        m.store.flat.copy_(tr.model.store.flat.detach())
+        m.store.flat.copy_(tr.model.store.flat.detach() if flat is None else flat)
     m.set_paths(np.repeat(tr.task_paths[ti][None], n, axis=0))
     m.task = ti
     r = evaluate_model(m, name, episodes=1, max_steps=args.eval_steps, device=dev,
@@ -169,11 +169,16 @@ def main():
 
     for ti, name in enumerate([] if args.control_only else tasks):
         rec = train_task(tr, ti, args, "sequence")
+        # the parameters as the task left them: end_task re-initialises everything outside the frozen paths and
+        # heads, which includes the shared LSTM cell of the reference's default network (its modules are frozen,
+        # its LSTM is not -- game_ac_network.py:303-521), so "after task" is evaluated on this snapshot
+        flat_task_end = tr.model.store.flat.detach().clone()
         winner, frozen = tr.end_task()
         rec["frozen_path"] = [p.tolist() for p in decode_path(tr.task_paths[ti])]
         rec["frozen_modules_total"] = int(frozen.sum())
-        rec["greedy_after_task"] = greedy_eval(tr, ti, name, args, dev)
-        rec["sampled_after_task"] = greedy_eval(tr, ti, name, args, dev, sample=True)
+        rec["greedy_after_task"] = greedy_eval(tr, ti, name, args, dev, flat=flat_task_end)
+        rec["sampled_after_task"] = greedy_eval(tr, ti, name, args, dev, sample=True, flat=flat_task_end)
+        del flat_task_end
         # snapshot of this task's frozen parameters (its modules + its head) to prove they never change again
         lay = tr.model.store.layout
         keep = np.zeros(lay.numel, bool)

@@ -6,6 +6,7 @@ and the post-window bookkeeping are excluded, so the table sums to the timed upd
     python scripts/prof_window.py <kernel_trace.csv> <updates in the window> <title>
 """
 import csv
+import os
 import sys
 from collections import defaultdict
 
@@ -20,12 +21,17 @@ def main(path, updates, title):
     if len(marks) < 2:
         raise SystemExit("no prof_window markers in the trace (run bench.py --prof-window)")
     lo, hi = marks[0], marks[-1]
+    # PROF_BY_GRID=1: separate dispatches of one kernel by grid size (e.g. the fc1 and fc2 launches of a template)
+    gkey = next((k for k in rows[0] if k.lower().replace("_", "") == "gridsize"), None)
+    by_grid = os.environ.get("PROF_BY_GRID") == "1" and gkey is not None
     tot = defaultdict(float)
     calls = defaultdict(int)
     for r in rows:
         t = int(r[t0k])
         if lo < t < hi and "prof_window_marker" not in r[key]:
             name = r[key].split("(")[0].replace("void ", "")
+            if by_grid:
+                name += f" [grid {r[gkey]}]"
             tot[name] += int(r[t1k]) - t
             calls[name] += 1
     total = sum(tot.values())
@@ -33,7 +39,7 @@ def main(path, updates, title):
            f"bench.py --prof-window markers; wall between markers {(hi - lo) / 1e6 / updates:.3f} ms per update", "",
            "| kernel | calls/update | avg us | ms/update | % |", "|---|---:|---:|---:|---:|"]
     for name in sorted(tot, key=lambda n: -tot[n])[:30]:
-        out.append(f"| `{name[:70]}` | {calls[name] / updates:.1f} | {tot[name] / calls[name] / 1e3:.1f} | "
+        out.append(f"| `{name[:70] if not by_grid else name[:50] + name[name.rfind(' ['):]}` | {calls[name] / updates:.1f} | {tot[name] / calls[name] / 1e3:.1f} | "
                    f"{tot[name] / 1e6 / updates:.3f} | {100 * tot[name] / total:.1f} |")
     out.append(f"| **total GPU kernel time** | | | **{total / 1e6 / updates:.2f}** | 100 |")
     return "\n".join(out) + "\n"
