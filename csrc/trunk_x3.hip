@@ -1920,7 +1920,7 @@ __global__ __launch_bounds__(512) void fc_fwd_mm_x3(const uint16_t* __restrict__
 // ===========================================================================
 DEVI int mm2_sw(int row, int ch) { return (row << 2) + (ch ^ ((-(row >> 2)) & 3)); }   // 16-byte chunk index
 
-template <int NKS, int PF>
+template <int NKS, int PF, int KS>
 __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restrict__ X, long xlo, int ldx,
                                                        float* __restrict__ Ys, uint16_t* __restrict__ bits,
                                                        const uint16_t* __restrict__ Wc, long wlo,
@@ -1933,15 +1933,17 @@ __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restri
   __shared__ __attribute__((aligned(16))) uint16_t As[2][2][BR * 32];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[2][2][BC * 32];
   const int R = T * E;
-  // unit -> (module j, row block, column half); units of module j = ceil(inv_cnt[j] * R / 128) x NCS
+  // unit -> (module j, row block, column half, k part); units of module j = ceil(inv_cnt[j] * R / 128) x NCS x KS
   int u = (int)blockIdx.x, j = 0, ncnt = 0;
   for (; j < M; ++j) {
     ncnt = inv_cnt[layer * M + j];
-    const int n = NCS * ((ncnt * R + BR - 1) / BR);
+    const int n = KS * NCS * ((ncnt * R + BR - 1) / BR);
     if (u < n) break;
     u -= n;
   }
   if (j >= M) return;                                    // grid is an upper bound on the unit count
+  const int kpart = u % KS;
+  u /= KS;
   const int chalf = u % NCS, rb = u / NCS;
   const int nrows = ncnt * R;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -1958,7 +1960,13 @@ __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restri
     const int q = gr < nrows ? gr / R : 0, rr = gr < nrows ? gr - q * R : 0;
     xoff = sample_global(inv_path[lbase + q], rr, E, PE, t0) * (long)ldx + skc * 8;
   }
-  const uint16_t* wsrc = Wc + ((long)j * COUT + col0 + srow) * KP + skc * 8;
+  // KS > 1: this workgroup sums k-steps [ks_beg, ks_beg + nks) only; the pre-activation partials of the parts go
+  // to separate planes of Ys and fc_slot_sum2_x3 adds them, then bias, ReLU, bits and the module sum
+  const int nks_all = NKS > 0 ? NKS : KP / 32;
+  const int ks_beg = kpart * (nks_all / KS) + min(kpart, nks_all % KS);
+  const int nks = nks_all / KS + (kpart < nks_all % KS ? 1 : 0);
+  xoff += (long)ks_beg * 32;
+  const uint16_t* wsrc = Wc + ((long)j * COUT + col0 + srow) * KP + skc * 8 + ks_beg * 32;
   const int sdst = mm2_sw(srow, skc) * 8;
   // PF register sets of k-step loads in flight (a k-step's MFMA work is ~400 cycles per wave, far below the
   // L2/MALL latency of its loads: one step of lookahead left the kernel waiting on every step).  Plain vector
@@ -2000,7 +2008,6 @@ __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restri
       for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma3h(ah, al, bh[jj], bl[jj], acc[i][jj]);
     }
   };
-  const int nks = NKS > 0 ? NKS : KP / 32;
   MM2_GLOAD(0, 0);
   MM2_LSTORE(0, 0);
   if (1 < nks) MM2_GLOAD(0, 1);                    // set d holds k-step d + 1, then d + 1 + PF, ...
@@ -2030,6 +2037,23 @@ __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restri
 #undef MM2_LSTORE
   // epilogue: rows-as-A D layout (lane: rows 4*grp + r of each 16-row tile, column c16), bits as 16-bit ballots
   const long PR = (long)P * R;
+  if constexpr (KS > 1) {
+    float* Yp = Ys + (long)kpart * M * PR * COUT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gr0 = rb * BR + wr * 64 + i * 16 + 4 * grp;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gr = gr0 + r;
+        if (gr >= nrows) continue;
+        const int q = gr / R;
+        const long o = ((long)inv_slot[lbase + q] * PR + (long)inv_path[lbase + q] * R + (gr - q * R)) * COUT;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) Yp[o + col0 + wc * 32 + jj * 16 + c16] = acc[i][jj][r] * in_scale;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int gr0 = rb * BR + wr * 64 + i * 16 + 4 * grp;
@@ -2058,6 +2082,69 @@ __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restri
                 (uint16_t)((bal >> (16 * grp)) & 0xFFFFull);
         }
       }
+    }
+  }
+}
+
+// KS-part partials of the module-major fc forward -> per slot: sum of the parts + bias, ReLU, the 16-bit ReLU word
+// of (slot, row, 16 columns); the slots summed in slot order -> Y.  One thread per (row, 16 columns).
+template <bool OF32, int KS>
+__global__ __launch_bounds__(256) void fc_slot_sum2_x3(const float* __restrict__ Ys, const int* __restrict__ act_idx,
+                                                       const int* __restrict__ act_cnt, const float* __restrict__ flat,
+                                                       long bias_off, int chunk, uint16_t* __restrict__ bits,
+                                                       long bits_rows, int layer, int L, int M, int P, int E, int T,
+                                                       int t0, void* __restrict__ Yv, long ylo, float out_scale) {
+  constexpr int COUT = 256, NWORDS = COUT / 16;
+  const int R = T * E;
+  const long PR = (long)P * R;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long row = idx >> 4;
+  const int w16 = (int)(idx & 15), c0 = w16 * 16;
+  if (row >= PR) return;
+  const int p = (int)(row / R), r = (int)(row - (long)p * R);
+  const int cnt = act_cnt[p * L + layer];
+  const long sg = sample_global(p, r, E, P * E, t0);
+  float o[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) o[c] = 0.f;
+  for (int a = 0; a < cnt; ++a) {
+    const int mod = act_idx[(p * L + layer) * M + a];
+    const float* bsrc = flat + bias_off + (long)mod * chunk + c0;     // (no alignment assumed)
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = bsrc[c];
+#pragma unroll
+    for (int kp = 0; kp < KS; ++kp) {
+      const float* src = Ys + (((long)kp * M + a) * PR + row) * COUT + c0;
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(src + c);
+        v[c] += x.x; v[c + 1] += x.y; v[c + 2] += x.z; v[c + 3] += x.w;
+      }
+    }
+    uint32_t word = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const bool pos = v[c] > 0.f;
+      word |= pos ? (1u << c) : 0u;
+      o[c] += pos ? v[c] : 0.f;
+    }
+    bits[((long)a * bits_rows + sg) * NWORDS + w16] = (uint16_t)word;
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) o[c] *= out_scale;
+  if constexpr (OF32) {
+    float* Y = reinterpret_cast<float*>(Yv) + sg * COUT + c0;
+#pragma unroll
+    for (int c = 0; c < 16; c += 4) *reinterpret_cast<float4*>(Y + c) = make_float4(o[c], o[c + 1], o[c + 2], o[c + 3]);
+  } else {
+    uint16_t* Y = reinterpret_cast<uint16_t*>(Yv) + sg * COUT + c0;
+    float o8[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o8[c] = o[h * 8 + c];
+      st8_x4(Y + h * 8, ylo, o8);
     }
   }
 }
@@ -2242,6 +2329,156 @@ __global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, 
       body(b1h, b1l, it + 1);
     } else {
       body(b0h, b0l, it);
+    }
+  }
+}
+
+// ===========================================================================
+// fc input gradient as a per-path GEMM with LDS-staged 128 x 256 tiles.  fc_dgrad_x3 above gives a workgroup 64
+// rows and streams the path's whole weight set past them (~2.9 MB per workgroup, ~3.6 GB of L2/MALL traffic per
+// fc1 backward).  Here the masked, split gradient of every active slot is written once by fc_gm_x3 (the same Gm the
+// weight gradient reads), and dX[rows][K] = sum over (slot a, c) Gm[a][row][c] * W_a[k][c] runs as a GEMM with the
+// reduction over (a, c) in steps of 32: a workgroup = path x 128 rows x 256 columns of dX, 8 waves (2 x 4, wave
+// tile 64 x 64), A [128][32] and B [256][32] hi/lo tiles staged per step (6 16-byte loads per thread, 48 MFMAs per
+// wave), two steps of loads in flight, double-buffered LDS with the XOR-swizzled 64-byte rows of fc_fwd_mm2_x3.
+// ===========================================================================
+template <int COUT>
+__global__ __launch_bounds__(256) void fc_gm_x3(const float* __restrict__ G, const uint16_t* __restrict__ bits,
+                                                const int* __restrict__ act_cnt, int layer, int L, int P, int E, int T,
+                                                long bits_rows, float g_scale, bf16_t* __restrict__ Gm, long gmlo) {
+  constexpr int NW = COUT / 16, C8 = COUT / 8;
+  const int R = T * E;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long row = idx / C8;
+  const int c = (int)(idx - row * C8) * 8;
+  if (row >= (long)P * R) return;
+  const int p = (int)(row / R), r = (int)(row - (long)p * R);
+  const int cnt = act_cnt[p * L + layer];
+  const long sg = sample_global(p, r, E, P * E, 0);
+  const float4 a0 = *reinterpret_cast<const float4*>(G + sg * COUT + c);
+  const float4 a1 = *reinterpret_cast<const float4*>(G + sg * COUT + c + 4);
+  const float gv[8] = {a0.x * g_scale, a0.y * g_scale, a0.z * g_scale, a0.w * g_scale,
+                       a1.x * g_scale, a1.y * g_scale, a1.z * g_scale, a1.w * g_scale};
+  for (int a = 0; a < cnt; ++a) {
+    const uint32_t bw = (uint32_t)bits[((long)a * bits_rows + sg) * NW + (c >> 4)] >> (c & 15);
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = ((bw >> j) & 1u) ? gv[j] : 0.f;
+    s8v hi, lo;
+    split8(m, hi, lo);
+    bf16_t* gp = Gm + ((long)a * bits_rows + sg) * COUT + c;
+    *reinterpret_cast<s8v*>(gp) = hi;
+    *reinterpret_cast<s8v*>(gp + gmlo) = lo;
+  }
+}
+
+template <int COUT>
+__global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict__ Gm, long gmlo,
+                                                        const bf16_t* __restrict__ WcT, long wlo,
+                                                        const int* __restrict__ act_idx,
+                                                        const int* __restrict__ act_cnt, int layer, int L, int M, int K,
+                                                        int KP, int P, int E, int T, long bits_rows,
+                                                        float* __restrict__ dX, int nrb, int ncb) {
+  constexpr int BM = 128, BN = 256, CS = COUT / 32;                 // reduction steps per slot
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][2][BM * 32];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][2][BN * 32];
+  const int bid = (int)blockIdx.x;
+  const int p = bid / (nrb * ncb), rem = bid - p * (nrb * ncb);
+  const int rbk = rem / ncb, cb = rem - rbk * ncb;
+  const int R = T * E, PE = P * E;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int wm = w >> 2, wn = w & 3;                                 // wave tile: rows 64*wm.., columns 64*wn..
+  const int row0 = rbk * BM, col0 = cb * BN;
+  const int nsteps = cnt * CS;
+  f4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (f4v){0.f, 0.f, 0.f, 0.f};
+  if (nsteps > 0) {
+    // staging roles: A: thread -> (row tid >> 2, chunk tid & 3), both planes; B: two columns (tid >> 2, + 128)
+    const int sr = tid >> 2, sk = tid & 3;
+    const int ra = min(row0 + sr, R - 1);
+    const long asg = sample_global(p, ra, E, PE, 0);
+    const int kb0 = min(col0 + sr, K - 1), kb1 = min(col0 + 128 + sr, K - 1);
+    const int* aidx = act_idx + (p * L + layer) * M;
+    const int sdA = mm2_sw(sr, sk) * 8, sdB0 = sdA, sdB1 = mm2_sw(sr + 128, sk) * 8;
+    uint4 x0, x1, y0, y1, z0, z1, u0, u1, v0, v1, t0_, t1_;     // two sets: A hi/lo, B col hi/lo, B col+128 hi/lo
+#define DG_LOAD(S, st)                                                                                      \
+    do {                                                                                                    \
+      const int a_ = (st) / CS, c_ = ((st) - a_ * CS) * 32 + sk * 8;                                        \
+      const bf16_t* ga_ = Gm + ((long)a_ * bits_rows + asg) * COUT + c_;                                    \
+      const bf16_t* wb_ = WcT + (long)aidx[a_] * KP * COUT + c_;                                            \
+      x##S = *reinterpret_cast<const uint4*>(ga_);                                                          \
+      y##S = *reinterpret_cast<const uint4*>(ga_ + gmlo);                                                   \
+      z##S = *reinterpret_cast<const uint4*>(wb_ + (long)kb0 * COUT);                                       \
+      u##S = *reinterpret_cast<const uint4*>(wb_ + wlo + (long)kb0 * COUT);                                 \
+      v##S = *reinterpret_cast<const uint4*>(wb_ + (long)kb1 * COUT);                                       \
+      t##S##_ = *reinterpret_cast<const uint4*>(wb_ + wlo + (long)kb1 * COUT);                              \
+    } while (0)
+#define DG_STORE(S, buf)                                                                                    \
+    do {                                                                                                    \
+      *reinterpret_cast<uint4*>(&As[buf][0][sdA]) = x##S;                                                   \
+      *reinterpret_cast<uint4*>(&As[buf][1][sdA]) = y##S;                                                   \
+      *reinterpret_cast<uint4*>(&Bs[buf][0][sdB0]) = z##S;                                                  \
+      *reinterpret_cast<uint4*>(&Bs[buf][1][sdB0]) = u##S;                                                  \
+      *reinterpret_cast<uint4*>(&Bs[buf][0][sdB1]) = v##S;                                                  \
+      *reinterpret_cast<uint4*>(&Bs[buf][1][sdB1]) = t##S##_;                                               \
+    } while (0)
+    auto compute = [&](int buf) {
+      s8v bh[4], bl[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int o = mm2_sw(wn * 64 + jj * 16 + c16, grp) * 8;
+        bh[jj] = *reinterpret_cast<const s8v*>(&Bs[buf][0][o]);
+        bl[jj] = *reinterpret_cast<const s8v*>(&Bs[buf][1][o]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = mm2_sw(wm * 64 + i * 16 + c16, grp) * 8;
+        const s8v ah = *reinterpret_cast<const s8v*>(&As[buf][0][o]);
+        const s8v al = *reinterpret_cast<const s8v*>(&As[buf][1][o]);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mma3(ah, al, bh[jj], bl[jj], acc[i][jj]);
+      }
+    };
+    // set 0 holds the even steps' loads, set 1 the odd ones; step s stores step s + 1's set, then reloads it with
+    // step s + 3 (clamped: a conditional reload is a loop-carried phi); the remainder step is peeled
+    DG_LOAD(0, 0);
+    DG_STORE(0, 0);
+    DG_LOAD(1, min(1, nsteps - 1));
+    DG_LOAD(0, min(2, nsteps - 1));
+    __syncthreads();
+    int s = 0;
+    for (; s + 2 <= nsteps; s += 2) {
+      compute(0);
+      DG_STORE(1, 1);
+      DG_LOAD(1, min(s + 3, nsteps - 1));
+      __syncthreads();
+      compute(1);
+      DG_STORE(0, 0);
+      DG_LOAD(0, min(s + 4, nsteps - 1));
+      __syncthreads();
+    }
+    if (s < nsteps) compute(0);
+#undef DG_LOAD
+#undef DG_STORE
+  }
+  // epilogue: rows-as-A D layout, fp32 dX (zeros for a path with no active slot)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + wm * 64 + i * 16 + 4 * grp + r;
+      if (row >= R) continue;
+      float* o = dX + sample_global(p, row, E, PE, 0) * (long)K;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int k = col0 + wn * 64 + jj * 16 + c16;
+        if (k < K) o[k] = acc[i][jj][r];
+      }
     }
   }
 }
@@ -2558,9 +2795,11 @@ static int X3_FC_D = 4;        // fc forward register ring depth (k-steps of hi/
 // is bound by its L2/MALL traffic, not by load latency
 static int X3_FC_KS = 1;
 // module-major fc forward kernel (when the Python side selects module-major): 1 = fc_fwd_mm_x3 (register
-// fragments), 2 = fc_fwd_mm2_x3 (LDS-staged 128 x 128 tiles)
-static int X3_FC_MMV = 2;
-static int X3_WG3_TILE = 1;    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
+// fragments), 2 = fc_fwd_mm2_x3 (LDS-staged 128 x 128 tiles), 3 = the same with k split in two workgroups
+// (pre-activation planes; bias, ReLU, bits and the slot sum in fc_slot_sum2_x3)
+static int X3_FC_MMV = 3;
+static int X3_WG3_TILE = 1;
+static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
 extern "C" {
 
@@ -2570,6 +2809,7 @@ void fast_conv_set_x3_fwd_db(int db) { X3_FWD_DB = db; }
 void fast_conv_set_x3_fwd_sw(int sw) { X3_FWD_SW = sw; }
 void fast_conv_set_x3_wg3_tile(int t) { X3_WG3_TILE = t; }
 void fast_conv_set_x3_fc_mmv(int v) { X3_FC_MMV = v; }
+void fast_conv_set_x3_fc_dg_gemm(int v) { X3_FC_DG_GEMM = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
@@ -2748,25 +2988,48 @@ int x3_fc_fwd(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, c
 
 // module-major fc forward (fc_fwd_mm_x3 + fc_slot_sum_x3); Ys: fp32 [M][P*T*E][256] slot planes
 int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, const void* Wc, long wlo,
-                 const float* flat, long bias_off, int chunk, const int* ac, const int* inv_path, const int* inv_slot,
+                 const float* flat, long bias_off, int chunk, const int* ac, const int* ai, const int* inv_path,
+                 const int* inv_slot,
                  const int* inv_cnt, float* Ys, int layer, int L, int M, int K, int KP, int Cout, int P, int E, int T,
                  int t0, long br, float os, hipStream_t st) {
   if (ldx <= 0 || chunk <= 0 || L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 ||
       br <= 0 || bias_off < 0 || layer < 0 || t0 < 0 || xlo <= 0 || ylo < 0 || wlo <= 0 || !Ys || !inv_path ||
-      !inv_slot || !inv_cnt) return -22;
+      !inv_slot || !inv_cnt || !ai || !ac) return -22;
   if (M > X3_MAXM || KP % 32 != 0 || Cout != 256 || ldx % 8 != 0 || ldx < KP || (long)T * E > 32) return 0;
   const int R = T * E, tpp = (R + 15) / 16;
   const float isc = 1.f / (float)(1 << X3_W0_SHIFT);
-  if (X3_FC_MMV >= 2) {
+  if (X3_FC_MMV >= 3) {
+    // k split in two: partial planes Ys[2][M][P*R][256], then bias + ReLU + bits + slot sum in fc_slot_sum2_x3
+    const int umax = 2 * M * 2 * ((P * R + 127) / 128);
+    if (KP == 256)
+      fc_fwd_mm2_x3<8, 3, 2><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,
+                                                   (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path, inv_slot,
+                                                   inv_cnt, layer, M, KP, P, E, T, t0, br, isc);
+    else
+      fc_fwd_mm2_x3<0, 3, 2><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,
+                                                   (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path, inv_slot,
+                                                   inv_cnt, layer, M, KP, P, E, T, t0, br, isc);
+    int rc = (int)hipGetLastError();
+    if (rc) return -rc;
+    const unsigned g2 = (unsigned)(((long)P * R * 16 + 255) / 256);
+    if (ylo == 0)
+      fc_slot_sum2_x3<true, 2><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br, layer, L,
+                                                   M, P, E, T, t0, Y, 0, os);
+    else
+      fc_slot_sum2_x3<false, 2><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br, layer, L,
+                                                    M, P, E, T, t0, Y, ylo, os);
+    rc = (int)hipGetLastError();
+    return rc ? -rc : 1;
+  } else if (X3_FC_MMV >= 2) {
     const int umax = M * 2 * ((P * R + 127) / 128);    // every module on every path: an upper bound
     if (KP == 256)
-      fc_fwd_mm2_x3<8, 3><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits, (const uint16_t*)Wc,
-                                             wlo, flat, bias_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, KP, P,
-                                             E, T, t0, br, isc);
+      fc_fwd_mm2_x3<8, 3, 1><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,
+                                                   (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path, inv_slot,
+                                                   inv_cnt, layer, M, KP, P, E, T, t0, br, isc);
     else
-      fc_fwd_mm2_x3<0, 3><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits, (const uint16_t*)Wc,
-                                             wlo, flat, bias_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, KP, P,
-                                             E, T, t0, br, isc);
+      fc_fwd_mm2_x3<0, 3, 1><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,
+                                                   (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path, inv_slot,
+                                                   inv_cnt, layer, M, KP, P, E, T, t0, br, isc);
   } else {
     const int umax = M * ((P * tpp + 3) / 4) * 2;    // x 2 column slices (fc_fwd_mm_x3 NH)
     const int nwg = (umax + 7) / 8 * 8;
@@ -2795,6 +3058,20 @@ int x3_fc_dgrad(const float* G, const void* bits, const void* WcT, long wlo, con
   if (L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 || layer < 0 ||
       wlo <= 0 || gmlo < 0 || (Gm && gmlo <= 0)) return -22;
   if (M > X3_MAXM || Cout != 256) return 0;
+  if (X3_FC_DG_GEMM && Gm != nullptr) {
+    const int R = T * E;
+    const long thr = (long)P * R * (256 / 8);
+    fc_gm_x3<256><<<(unsigned)((thr + 255) / 256), 256, 0, st>>>(G, (const uint16_t*)bits, ac, layer, L, P, E, T, br,
+                                                                  gs, (bf16_t*)Gm, gmlo);
+    int rc = (int)hipGetLastError();
+    if (rc) return -rc;
+    const int nrb = (R + 127) / 128, ncb = (K + 255) / 256;
+    fc_dgrad_gemm_x3<256><<<(unsigned)(P * nrb * ncb), 512, 0, st>>>((const bf16_t*)Gm, gmlo, (const bf16_t*)WcT, wlo,
+                                                                     ai, ac, layer, L, M, K, KP, P, E, T, br, dX, nrb,
+                                                                     ncb);
+    rc = (int)hipGetLastError();
+    return rc ? -rc : 1;
+  }
   const int nchunks = (K + 127) / 128;
   const int split = nchunks >= 8 ? 2 : 1;
   const int per = (nchunks + split - 1) / split;

@@ -123,7 +123,7 @@ _SIGS = {
     "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P],
     "x3_fc_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 10
                  + [c_long, c_float, P],
-    "x3_fc_fwd_mm": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P, P, P, P] + [c_int] * 10
+    "x3_fc_fwd_mm": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P, P, P, P, P] + [c_int] * 10
                     + [c_long, c_float, P],
     "x3_fc_dgrad": [P, P, P, c_long, P, P] + [c_int] * 9 + [c_long, c_float, P, P, c_long, P],
     "x3_fc_wgrad_gm": [P, c_long, c_int, P, c_long, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8
@@ -136,6 +136,7 @@ _SIGS = {
     "fast_conv_set_x3_fwd_sw": [c_int],
     "fast_conv_set_x3_wg3_tile": [c_int],
     "fast_conv_set_x3_fc_mmv": [c_int],
+    "fast_conv_set_x3_fc_dg_gemm": [c_int],
     "fast_conv_set_x3_fc_d": [c_int],
     "fast_conv_set_x3_fc_ks": [c_int],
     "fast_conv_set_x3_wgrad_pf": [c_int],

@@ -493,7 +493,7 @@ class HipPathNet:
             # module-major: each module's weight slice read once per 64 rows of the paths using it
             ys = self._ys_buffer_x3(P * T * E)
             ok = _lib.call_fast("x3_fc_fwd_mm", xp, x2_lo(X), g.ldx, yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
-                                flat.data_ptr(), g.b_off, g.chunk, acp, self.inv_path.data_ptr(),
+                                flat.data_ptr(), g.b_off, g.chunk, acp, aip, self.inv_path.data_ptr(),
                                 self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), ys.data_ptr(), l, self.L, self.M,
                                 g.K, g.KP, g.Cout, P, E, T, t0, bits_rows, out_scale, st)
         else:
@@ -505,8 +505,9 @@ class HipPathNet:
                                "(fc layers take <= 32 rows per path and launch)")
 
     def _ys_buffer_x3(self, rows: int) -> torch.Tensor:
-        """fp32 module-slot planes [M][rows][256] of the module-major fc forward (grown before graph capture)."""
-        need = self.M * rows * 256
+        """fp32 module-slot planes [2][M][rows][256] of the module-major fc forward (two k-part planes of
+        pre-activations, or one plane of activations; grown before graph capture)."""
+        need = 2 * self.M * rows * 256
         if self._ys is None or self._ys.numel() < need:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("fp32x: fc slot buffer first needed inside a graph capture")
@@ -533,15 +534,17 @@ class HipPathNet:
             if not ok:
                 raise RuntimeError(f"fp32x: conv layer {l} backward has no split-bf16 kernel")
             return
-        gm = self._gm_buffer_x3(bits_rows) if (dX is not None and g.Cout == 256 and g.K >= self.fc_wgrad_gm_min_k
-                                              and self.fc_wgrad_gm) else None
+        # Gm: the masked hi/lo output gradient per active slot -- read by the GEMM input gradient (every fc layer
+        # with an input gradient) and by the Gm weight gradient (K >= fc_wgrad_gm_min_k)
+        use_gm_wgrad = dX is not None and g.Cout == 256 and g.K >= self.fc_wgrad_gm_min_k and self.fc_wgrad_gm
+        gm = self._gm_buffer_x3(bits_rows) if (dX is not None and g.Cout == 256) else None
         gmlo = gm.numel() // 2 if gm is not None else 0
         ok = True
         if dX is not None:
             ok = _lib.call_fast("x3_fc_dgrad", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
                                 self.WcT[l][0].numel(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M,
                                 g.K, g.KP, g.Cout, P, E, T, bits_rows, g_scale, dX.data_ptr(), _lib.ptr(gm), gmlo, st)
-        if ok and gm is not None:
+        if ok and use_gm_wgrad:
             tiles = ((g.K + 127) // 128) * self.M
             nsplit = max(1, min(m.P, -(-512 // tiles)))
             ok = _lib.call_fast("x3_fc_wgrad_gm", xb, xblo, g.ldx, gm.data_ptr(), gmlo,

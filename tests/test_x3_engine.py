@@ -169,9 +169,10 @@ def test_x3_gradient_check_detects_a_two_percent_module_error(x3_rollout):
 
 
 @pytest.mark.parametrize("E", [16, 32])
-@pytest.mark.parametrize("variant", ["split_k", "module_major", "module_major_regs"])
+@pytest.mark.parametrize("variant", ["split_k", "module_major", "module_major_ks1", "module_major_regs"])
 def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
-    """fc_fwd_ks_x3 (two waves per module, partial sums meet in LDS) and fc_fwd_mm_x3 (one workgroup per module
+    """fc_fwd_ks_x3 (two waves per module, partial sums meet in LDS), fc_fwd_mm2_x3 (module-major LDS tiles, one or
+    two k parts; the two-part form leaves bias / ReLU / bits to fc_slot_sum2_x3) and fc_fwd_mm_x3 (one workgroup per module
     x 64 rows, slot planes summed in slot order) == the path-major fc_fwd_x3 up to summation order: outputs to
     fp32 rounding, relu bits equal but for exact ties."""
     from pathnet_gym_amd.ops import _lib
@@ -184,7 +185,7 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     obs = torch.randint(0, 256, (P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
     outs = []
     lib = _lib.lib()
-    lib.fast_conv_set_x3_fc_mmv(1 if variant == "module_major_regs" else 2)
+    lib.fast_conv_set_x3_fc_mmv({"module_major_regs": 1, "module_major_ks1": 2}.get(variant, 3))
     hp.fc_fwd_mm_min_k = 0
     for ref in (False, True):
         hp.fc_fwd_mm = variant.startswith("module_major") and not ref
@@ -201,7 +202,8 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
         torch.cuda.synchronize()
         outs.append(([x2_value(a) if a.dtype == torch.float16 else a.clone() for a in acts], [b.clone() for b in bits]))
     hp.fc_fwd_mm = True
-    lib.fast_conv_set_x3_fc_mmv(2)
+    hp.fc_fwd_mm_min_k = 1024
+    lib.fast_conv_set_x3_fc_mmv(3)
     lib.fast_conv_set_x3_fc_ks(1)
     for l in (3, 4):
         a, b = outs[0][0][l], outs[1][0][l]
@@ -274,3 +276,33 @@ def test_x3_conv3_wgrad_tile_matches_im2col_rows(x3_rollout):
     print(f"conv3 wgrad tile vs im2col rows: rel {e:.2e}")
     assert e < 1e-6, e
     assert rel(outs[1], g_hip[seg]) < 1e-6
+
+
+@pytest.mark.parametrize("l", [3, 4])
+def test_x3_fc_dgrad_gemm_matches_streaming_kernel(x3_rollout, l):
+    """fc_gm_x3 + fc_dgrad_gemm_x3 (per-path GEMM over (slot, column) with LDS-staged 128 x 256 tiles) == fc_dgrad_x3
+    (64-row workgroups streaming the weights): input gradient to fp32 summation order, weight gradient (which reads
+    the same Gm) equal up to its own float atomics."""
+    from pathnet_gym_amd.ops import _lib
+    tr, eng, g_ref, g_hip = x3_rollout
+    hp = tr.model.hip
+    lib = _lib.lib()
+    g = hp.geoms[l]
+    seg = slice(g.w_off, g.w_off + hp.M * g.chunk)
+    dxs, gws = [], []
+    for gemm in (0, 1):
+        lib.fast_conv_set_x3_fc_dg_gemm(gemm)
+        eng.grad_flat.zero_()
+        dX = eng.grads[l - 1]
+        dX.fill_(float("nan"))
+        hp.layer_bwd(l, eng.acts[l - 1], eng.grads[l], eng.bits[l], eng.grad_flat, dX, eng.P, eng.E, eng.T,
+                     eng.bits_rows[l])
+        torch.cuda.synchronize()
+        dxs.append(dX[:eng.T].clone())
+        gws.append(eng.grad_flat[seg].clone())
+    lib.fast_conv_set_x3_fc_dg_gemm(1)
+    assert torch.isfinite(dxs[1]).all() and dxs[0].norm() > 0
+    e = rel(dxs[1], dxs[0])
+    print(f"fc layer {l} dgrad GEMM vs streaming: rel {e:.2e}, weight gradient rel {rel(gws[1], gws[0]):.2e}")
+    assert e < 1e-6, e
+    assert rel(gws[1], gws[0]) < 1e-6
