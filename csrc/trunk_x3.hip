@@ -176,7 +176,7 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 template <int NC>
 DEVI void conv_epi_sw(const f4v (&acc)[NC], const float* bias_s, int ct0, int cnt, int q, float in_scale,
                       float out_scale, long grow, uint8_t* __restrict__ bits, long bits_rows,
-                      uint16_t* __restrict__ Y, long ylo, bool accumulate) {
+                      uint16_t* __restrict__ Y, long ylo, bool accumulate, bool valid = true) {
   float sum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ct = 0; ct < NC; ++ct) {
@@ -192,13 +192,14 @@ DEVI void conv_epi_sw(const f4v (&acc)[NC], const float* bias_s, int ct0, int cn
     }
     const uint32_t hi4 = (uint32_t)__shfl_xor((int)nib, 16, 64);      // channels 4..7 of the same slot and row
     const int slot = (ct0 + ct) * 2 + (q >> 1);
-    if ((q & 1) == 0 && slot < cnt) bits[(long)slot * bits_rows + grow] = (uint8_t)(nib | (hi4 << 4));
+    if ((q & 1) == 0 && slot < cnt && valid) bits[(long)slot * bits_rows + grow] = (uint8_t)(nib | (hi4 << 4));
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 32, 64);   // + the other slot of each pair
   float y[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) y[r] = sum[r] * out_scale;
+  if (!valid) return;                            // (after the exchanges: every lane took part in them)
   const long o = grow * 8 + 4 * (q & 1);
   if (accumulate) {
     const uint2 ph = *reinterpret_cast<const uint2*>(Y + o), pl = *reinterpret_cast<const uint2*>(Y + ylo + o);
@@ -589,6 +590,141 @@ __global__ __launch_bounds__(256, LB) void conv_fwd_x3(const uint16_t* __restric
       case 2: run(std::integral_constant<int, 2>{}); break;
       default: run(std::integral_constant<int, 3>{}); break;
     }
+  }
+}
+
+// ===========================================================================
+// forward of the bf16-activation conv layers, one SAMPLE per stage: the sample's fp16-pair input (39x29x8 or
+// 18x13x8, 36 / 7.5 KB) is staged in LDS once and every im2col fragment is a ds_read_b128 of one pixel's 8 channels
+// at (position offset) + (tap offset), instead of conv_fwd_x3's 16-byte global fragment loads that read each input
+// element KH*KW/S^2 times through L2.  Weights as the MFMA A operand (conv_epi_sw epilogue, rows past the
+// sample's positions masked).  Next sample's tile in registers while this one computes.  grid = (chunks, P).
+// ===========================================================================
+template <class G>
+struct FT3 {
+  static constexpr int NRT = (G::HOWO + 15) / 16;              // 16-row position tiles per sample
+  static constexpr int NK = G::KP / 32;
+  static constexpr int NXC = G::IN_ELEMS / 8;                  // 8-channel pixel chunks per plane
+  static constexpr int XIT = (NXC + 255) / 256;
+  static constexpr int TILEP = G::IN_ELEMS + 8;                // + a zero chunk for padded taps
+  static_assert(G::CIN == 8 && !G::U8 && G::IN_ELEMS % 8 == 0, "8-channel fp16-pair input");
+};
+
+template <class G>
+__global__ __launch_bounds__(256, 2) void conv_fwd_tile_x3(const uint16_t* __restrict__ X, long xlo,
+                                                          uint16_t* __restrict__ Y, long ylo,
+                                                          uint8_t* __restrict__ bits, const uint16_t* __restrict__ Wc,
+                                                          long wlo, const float* __restrict__ flat, long bias_off,
+                                                          int chunk, const int* __restrict__ act_idx,
+                                                          const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                          int P, int E, int T, int t0, long bits_rows,
+                                                          int samples_per_wg, float in_scale, float out_scale) {
+  using F = FT3<G>;
+  constexpr int KPs = G::KP + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Xt[2][F::TILEP];
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[2][2 * 16 * KPs];
+  __shared__ __attribute__((aligned(16))) float bias_s[2 * 16];
+  __shared__ int mods[X3_MAXM];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15, q = grp;
+  const int PE = P * E, nsamp = T * E;
+  const int s_beg = blockIdx.x * samples_per_wg;
+  const int s_end = min(nsamp, s_beg + samples_per_wg);
+  if (s_beg >= s_end) return;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  if (tid < 16) Xt[tid >> 3][G::IN_ELEMS + (tid & 7)] = 0;
+  // B (pixel) fragment addresses: lane c16 = position in the tile, grp = 8-element k chunk of the k-step
+  int koffs[F::NK];
+#pragma unroll
+  for (int kk = 0; kk < F::NK; ++kk) {
+    const int kc = kk * 4 + grp;                                   // pixel chunk = tap (kh, kw)
+    koffs[kk] = kc * 8 < G::K ? ((kc / G::KW) * G::WIN + kc % G::KW) * 8 : -1;
+  }
+  constexpr int NCXT = 2;                          // column tiles per pass (a third set of accumulators spilled)
+  const int npass = nct > NCXT ? (nct + NCXT - 1) / NCXT : 1;
+  s8v xh[F::XIT], xl[F::XIT];
+  auto load_sample = [&](int s) {
+    const long xb = sample_global(p, s, E, PE, t0) * (long)G::IN_ELEMS;
+#pragma unroll
+    for (int j = 0; j < F::XIT; ++j) {
+      const int c = tid + 256 * j;
+      if (c < F::NXC) {
+        xh[j] = *reinterpret_cast<const s8v*>(X + xb + c * 8);
+        xl[j] = *reinterpret_cast<const s8v*>(X + xlo + xb + c * 8);
+      }
+    }
+  };
+  for (int pass = 0; pass < npass; ++pass) {
+    const int ct0 = pass * NCXT;
+    const int ncg = nct == 0 ? 1 : min(NCXT, nct - ct0);
+    __syncthreads();
+    for (int i = tid; i < ncg * 16 * G::KC; i += 256) {
+      const int col = i / G::KC, kc = i - col * G::KC;
+      const int slot = ct0 * 2 + (col >> 3);
+      s8v vh = {0, 0, 0, 0, 0, 0, 0, 0}, vl = vh;
+      if (slot < cnt) {
+        const long o = ((long)(mods[slot] * 8 + (col & 7))) * G::KP + kc * 8;
+        vh = *reinterpret_cast<const s8v*>(Wc + o);
+        vl = *reinterpret_cast<const s8v*>(Wc + wlo + o);
+      }
+      *reinterpret_cast<s8v*>(Ws[0] + col * KPs + kc * 8) = vh;
+      *reinterpret_cast<s8v*>(Ws[1] + col * KPs + kc * 8) = vl;
+    }
+    if (tid < ncg * 16) {
+      const int slot = ct0 * 2 + (tid >> 3);
+      bias_s[tid] = slot < cnt ? flat[bias_off + (long)mods[slot] * chunk + (tid & 7)] : 0.f;
+    }
+    load_sample(s_beg);
+    auto run = [&](auto ncc) {
+      constexpr int NC = decltype(ncc)::value;
+      for (int s = s_beg; s < s_end; ++s) {
+        __syncthreads();                           // previous sample's tile reads (and the staging above) done
+#pragma unroll
+        for (int j = 0; j < F::XIT; ++j) {
+          const int c = tid + 256 * j;
+          if (c < F::NXC) {
+            *reinterpret_cast<s8v*>(&Xt[0][c * 8]) = xh[j];
+            *reinterpret_cast<s8v*>(&Xt[1][c * 8]) = xl[j];
+          }
+        }
+        __syncthreads();
+        if (s + 1 < s_end) load_sample(s + 1);
+        const long growb = sample_global(p, s, E, PE, t0) * G::HOWO;
+#pragma unroll 1
+        for (int rt = w; rt < F::NRT; rt += 4) {                    // wave-uniform
+          int poff;
+          {
+            const int pos = rt * 16 + c16;
+            const int oh = pos / G::WO, ow = pos - (pos / G::WO) * G::WO;
+            poff = pos < G::HOWO ? (oh * G::S * G::WIN + ow * G::S) * 8 : -1;
+          }
+          f4v acc[NC];
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) acc[ct] = (f4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < F::NK; ++kk) {
+            const int a = (poff < 0 || koffs[kk] < 0) ? G::IN_ELEMS : poff + koffs[kk];
+            const s8v ph = *reinterpret_cast<const s8v*>(&Xt[0][a]);
+            const s8v pl = *reinterpret_cast<const s8v*>(&Xt[1][a]);
+            const int kc = kk * 4 + grp;
+#pragma unroll
+            for (int ct = 0; ct < NC; ++ct) {
+              const s8v bh = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
+              const s8v bl = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
+              acc[ct] = mma3h_t(ph, pl, bh, bl, acc[ct]);
+            }
+          }
+          const int pos = rt * 16 + c16;
+          conv_epi_sw<NC>(acc, bias_s, ct0, cnt, q, in_scale, out_scale, growb + pos, bits, bits_rows, Y, ylo,
+                          pass > 0, pos < G::HOWO);
+        }
+      }
+    };
+    if (ncg == 1) run(std::integral_constant<int, 1>{});
+    else run(std::integral_constant<int, 2>{});
   }
 }
 
@@ -2087,7 +2223,8 @@ __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restri
 }
 
 // KS-part partials of the module-major fc forward -> per slot: sum of the parts + bias, ReLU, the 16-bit ReLU word
-// of (slot, row, 16 columns); the slots summed in slot order -> Y.  One thread per (row, 16 columns).
+// of (slot, row, 16 columns); the slots summed in slot order -> Y.  One thread per (row, 8 columns); the two threads
+// of a 16-column word (adjacent lanes) join their ReLU bytes with one xor-1 exchange.
 template <bool OF32, int KS>
 __global__ __launch_bounds__(256) void fc_slot_sum2_x3(const float* __restrict__ Ys, const int* __restrict__ act_idx,
                                                        const int* __restrict__ act_cnt, const float* __restrict__ flat,
@@ -2098,54 +2235,49 @@ __global__ __launch_bounds__(256) void fc_slot_sum2_x3(const float* __restrict__
   const int R = T * E;
   const long PR = (long)P * R;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  const long row = idx >> 4;
-  const int w16 = (int)(idx & 15), c0 = w16 * 16;
-  if (row >= PR) return;
-  const int p = (int)(row / R), r = (int)(row - (long)p * R);
-  const int cnt = act_cnt[p * L + layer];
+  const long row = idx >> 5;                                   // 32 threads per row: whole waves share 2 rows
+  const int c0 = (int)(idx & 31) * 8;
+  const bool live = row < PR;
+  const long rowc = live ? row : 0;
+  const int p = (int)(rowc / R), r = (int)(rowc - (long)p * R);
+  const int cnt = live ? act_cnt[p * L + layer] : 0;
   const long sg = sample_global(p, r, E, P * E, t0);
-  float o[16];
+  float o[8];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) o[c] = 0.f;
+  for (int c = 0; c < 8; ++c) o[c] = 0.f;
+  // the xor-1 partner is in the same row (32 lanes per row), so it runs the same slot count
   for (int a = 0; a < cnt; ++a) {
+    float v[8];
     const int mod = act_idx[(p * L + layer) * M + a];
-    const float* bsrc = flat + bias_off + (long)mod * chunk + c0;     // (no alignment assumed)
-    float v[16];
+    const float* bsrc = flat + bias_off + (long)mod * chunk + c0;      // (no alignment assumed)
 #pragma unroll
-    for (int c = 0; c < 16; ++c) v[c] = bsrc[c];
+    for (int c = 0; c < 8; ++c) v[c] = bsrc[c];
 #pragma unroll
     for (int kp = 0; kp < KS; ++kp) {
       const float* src = Ys + (((long)kp * M + a) * PR + row) * COUT + c0;
-#pragma unroll
-      for (int c = 0; c < 16; c += 4) {
-        const float4 x = *reinterpret_cast<const float4*>(src + c);
-        v[c] += x.x; v[c + 1] += x.y; v[c + 2] += x.z; v[c + 3] += x.w;
-      }
+      const float4 x = *reinterpret_cast<const float4*>(src), y = *reinterpret_cast<const float4*>(src + 4);
+      v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
+      v[4] += y.x; v[5] += y.y; v[6] += y.z; v[7] += y.w;
     }
-    uint32_t word = 0;
+    uint32_t byte = 0;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
+    for (int c = 0; c < 8; ++c) {
       const bool pos = v[c] > 0.f;
-      word |= pos ? (1u << c) : 0u;
+      byte |= pos ? (1u << c) : 0u;
       o[c] += pos ? v[c] : 0.f;
     }
-    bits[((long)a * bits_rows + sg) * NWORDS + w16] = (uint16_t)word;
+    const uint32_t other = (uint32_t)__shfl_xor((int)byte, 1, 64);
+    if ((c0 & 8) == 0) bits[((long)a * bits_rows + sg) * NWORDS + (c0 >> 4)] = (uint16_t)(byte | (other << 8));
   }
+  if (!live) return;
 #pragma unroll
-  for (int c = 0; c < 16; ++c) o[c] *= out_scale;
+  for (int c = 0; c < 8; ++c) o[c] *= out_scale;
   if constexpr (OF32) {
     float* Y = reinterpret_cast<float*>(Yv) + sg * COUT + c0;
-#pragma unroll
-    for (int c = 0; c < 16; c += 4) *reinterpret_cast<float4*>(Y + c) = make_float4(o[c], o[c + 1], o[c + 2], o[c + 3]);
+    *reinterpret_cast<float4*>(Y) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(Y + 4) = make_float4(o[4], o[5], o[6], o[7]);
   } else {
-    uint16_t* Y = reinterpret_cast<uint16_t*>(Yv) + sg * COUT + c0;
-    float o8[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int c = 0; c < 8; ++c) o8[c] = o[h * 8 + c];
-      st8_x4(Y + h * 8, ylo, o8);
-    }
+    st8_x4(reinterpret_cast<uint16_t*>(Yv) + sg * COUT + c0, ylo, o);
   }
 }
 
@@ -2799,6 +2931,7 @@ static int X3_FC_KS = 1;
 // (pre-activation planes; bias, ReLU, bits and the slot sum in fc_slot_sum2_x3)
 static int X3_FC_MMV = 3;
 static int X3_WG3_TILE = 1;
+static int X3_FWD_TILE = 1;    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
 extern "C" {
@@ -2810,6 +2943,7 @@ void fast_conv_set_x3_fwd_sw(int sw) { X3_FWD_SW = sw; }
 void fast_conv_set_x3_wg3_tile(int t) { X3_WG3_TILE = t; }
 void fast_conv_set_x3_fc_mmv(int v) { X3_FC_MMV = v; }
 void fast_conv_set_x3_fc_dg_gemm(int v) { X3_FC_DG_GEMM = v; }
+void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
@@ -2848,7 +2982,14 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
     const long rows = (long)T * E * Gx::HOWO;                                                                     \
     const dim3 grid((unsigned)((rows + 511) / 512), P);                                                           \
     const float isc = is / (float)(1 << X3_W0_SHIFT);                                                             \
-    if (X3_FWD_DB)                                                                                                \
+    if (X3_FWD_TILE) {                                                                                            \
+      const long nsamp = (long)T * E;                                                                             \
+      long spw = (nsamp * P + 511) / 512;                                                                         \
+      if (spw < 2) spw = 2;                                                                                       \
+      conv_fwd_tile_x3<Gx><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), 256, 0, st>>>(                         \
+          (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \
+          chunk, ai, ac, layer, L, M, P, E, T, t0, br, (int)spw, isc, os);                                        \
+    } else if (X3_FWD_DB)                                                                                         \
       conv_fwd_x3<Gx, 4, 2, true, false><<<grid, 256, 0, st>>>(                                                   \
           (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \
           chunk, ai, ac, layer, L, M, P, E, T, t0, br, isc, os);                                                  \
@@ -3011,7 +3152,7 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
                                                    inv_cnt, layer, M, KP, P, E, T, t0, br, isc);
     int rc = (int)hipGetLastError();
     if (rc) return -rc;
-    const unsigned g2 = (unsigned)(((long)P * R * 16 + 255) / 256);
+    const unsigned g2 = (unsigned)(((long)P * R * 32 + 255) / 256);
     if (ylo == 0)
       fc_slot_sum2_x3<true, 2><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br, layer, L,
                                                    M, P, E, T, t0, Y, 0, os);

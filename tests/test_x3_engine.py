@@ -212,12 +212,14 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
         assert same > 0.999, (l, same)
 
 
+@pytest.mark.parametrize("arm", ["swapped", "tile"])
 @pytest.mark.parametrize("T", [1, 2])
-def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T):
+def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T, arm):
     """conv_epi_sw (weights as the MFMA A operand: one xor-32 module-pair sum, nibble ReLU bits, 8-byte stores; the
     first layer with fp16(1024 + v) pixels and the offset folded into the bias) == the rows-as-A epilogue: conv2/3
     bit-identical, conv1 to fp32 rounding of the offset sum; ReLU bits equal but for near-zero ties.  T = 2 runs the
-    multi-step row walk (backward-style launches), T = 1 the rollout's linear rows."""
+    multi-step row walk (backward-style launches), T = 1 the rollout's linear rows.  arm "tile": conv_fwd_tile_x3
+    (one sample's input staged in LDS, im2col fragments read from it) against conv_fwd_x3 for conv2/conv3."""
     from pathnet_gym_amd.ops import _lib
     cfg = pixel_cfg()
     P, E = 5, 16
@@ -229,7 +231,12 @@ def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T):
     lib = _lib.lib()
     outs = []
     for sw in (0, 3):
-        lib.fast_conv_set_x3_fwd_sw(sw)
+        if arm == "tile":
+            lib.fast_conv_set_x3_fwd_sw(0)
+            lib.fast_conv_set_x3_fwd_tile(1 if sw else 0)
+        else:
+            lib.fast_conv_set_x3_fwd_tile(0)
+            lib.fast_conv_set_x3_fwd_sw(sw)
         acts, bits = [], []
         x = obs
         for l in range(3):
@@ -243,6 +250,7 @@ def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T):
         torch.cuda.synchronize()
         outs.append(([x2_value(a) for a in acts], [b.clone() for b in bits]))
     lib.fast_conv_set_x3_fwd_sw(1)
+    lib.fast_conv_set_x3_fwd_tile(1)
     for l in range(3):
         a, b = outs[0][0][l], outs[1][0][l]
         e = rel(b, a)
