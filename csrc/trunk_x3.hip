@@ -2969,7 +2969,7 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
     if (X3_FWD_LB >= 3) {
       if (X3_FWD_NT >= 8) C1L(8, 3); else C1L(4, 3);
     } else {
-      if (X3_FWD_NT >= 8) C1L(8, 2); else C1L(4, 2);
+      if (X3_FWD_NT >= 9) C1L(9, 2); else if (X3_FWD_NT >= 8) C1L(8, 2); else C1L(4, 2);
     }
 #undef C1L
 #undef C1LS

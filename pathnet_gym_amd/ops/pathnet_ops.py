@@ -181,6 +181,7 @@ class HipPathNet:
         # profiles/r3/kwin_x3_v6*.md).  PATHNET_X3_FC_MM=0 selects path-major.
         self.fc_fwd_mm = os.environ.get("PATHNET_X3_FC_MM", "1") == "1"
         self.fc_fwd_mm_min_k = int(os.environ.get("PATHNET_X3_FC_MM_MIN_K", "1024"))   # fc2 (K = 256): path-major
+        self.fc_wgrad_gm_wgs = int(os.environ.get("PATHNET_X3_FC_WGRAD_WGS", "768"))    # target workgroup count
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
         self.inv_slot = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
@@ -546,7 +547,9 @@ class HipPathNet:
                                 g.K, g.KP, g.Cout, P, E, T, bits_rows, g_scale, dX.data_ptr(), _lib.ptr(gm), gmlo, st)
         if ok and use_gm_wgrad:
             tiles = ((g.K + 127) // 128) * self.M
-            nsplit = max(1, min(m.P, -(-512 // tiles)))
+            # workgroups ~ a whole number of rounds of one per CU (fc_wgrad_gm_x3 holds 102 KB of LDS): 110 tiles x 7
+            # = 770 = 3.0 rounds on 256 CUs, where 110 x 5 = 550 left the third round 15 % full
+            nsplit = max(1, min(m.P, -(-self.fc_wgrad_gm_wgs // tiles)))
             ok = _lib.call_fast("x3_fc_wgrad_gm", xb, xblo, g.ldx, gm.data_ptr(), gmlo,
                                 grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
                                 self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T,
