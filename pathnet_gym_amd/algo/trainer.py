@@ -252,9 +252,12 @@ class PathNetTrainer:
         values = torch.stack(values_l)
         R, adv = nstep_returns(torch.stack(rewards_l), values.detach().float(), torch.stack(dones_l),
                                v_boot.float(), a2c.gamma, a2c.gae_lambda, a2c.reward_clip)
+        from ..runtime.engine import loss_scale
         weight = None
-        if a2c.env_reduction == "mean_env":
-            weight = torch.full((T * B,), 1.0 / E, device=self.device)
+        ls = loss_scale(cfg)
+        if a2c.env_reduction == "mean_env" or ls != 1.0:
+            weight = torch.full((T * B,), (1.0 / E if a2c.env_reduction == "mean_env" else 1.0) * ls,
+                                device=self.device)
         loss, lp, lv, ent = a2c_loss(torch.cat(logits_l), values.reshape(-1), torch.cat(actions_l),
                                      R.reshape(-1), adv.reshape(-1), a2c.entropy_beta, a2c.value_coef, weight)
         flat = model.store.flat

@@ -73,6 +73,8 @@ def build_parser():
         p.add_argument("--grad_norm_clip", type=float, default=None)
         p.add_argument("--max_time_step", type=int, default=None)
         p.add_argument("--env_reduction", default=None, choices=["sum", "mean_env"])
+        p.add_argument("--rank_reduction", default=None, choices=["sum", "mean"])
+        p.add_argument("--grad_scale", type=float, default=None)
         p.add_argument("--mutation", default=None, choices=["ref", "down"])
         p.add_argument("--concurrent_tournaments", type=int, default=None)
         p.add_argument("--freeze_union", type=int, default=None)
@@ -187,7 +189,8 @@ def config_from_args(a):
                     ("entropy_beta", "entropy_beta"), ("lr", "lr"), ("lr_anneal", "lr_anneal"),
                     ("rmsp_alpha", "rmsp_alpha"), ("rmsp_epsilon", "rmsp_epsilon"),
                     ("grad_norm_clip", "grad_norm_clip"), ("max_time_step", "max_time_step"),
-                    ("env_reduction", "env_reduction")):
+                    ("env_reduction", "env_reduction"), ("rank_reduction", "rank_reduction"),
+                    ("grad_scale", "grad_scale")):
         v = getattr(a, k, None)
         if v is not None:
             setattr(cfg.a2c, attr, v)

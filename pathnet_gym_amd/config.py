@@ -150,6 +150,11 @@ class A2CConfig:
     # loss reduction over envs of one path: "sum" (ref: sum over everything)
     # or "mean_env" (sum over time, mean over the E envs of a path, sum over paths)
     env_reduction: str = "mean_env"
+    # gradient reduction over ranks: "sum" (each rank's paths count like the reference's Hogwild workers: the update
+    # grows with the population) or "mean" (the all-reduced gradient is divided by the world size, so an 8-GPU
+    # update has the scale of a 1-GPU one -- measured: profiles/solve/README.md, "8-GPU population on one GPU")
+    rank_reduction: str = "sum"
+    grad_scale: float = 1.0            # extra factor on the loss weight (1 / world emulates "mean" on one GPU)
     lr: float = log_uniform(INITIAL_ALPHA_LOW, INITIAL_ALPHA_HIGH, INITIAL_ALPHA_LOG_RATE)
     lr_anneal: str = "per_task"        # "per_task" | "global" (ref quirk) | "none"
     max_time_step: int = MAX_TIME_STEP

@@ -32,6 +32,16 @@ from ..ops import _lib
 from ..ops import envs as henv
 
 
+def loss_scale(cfg) -> float:
+    """grad_scale x (1 / world size when rank_reduction == "mean"): the factor on every sample's loss weight."""
+    a2c = cfg.a2c
+    world = 1
+    if getattr(a2c, "rank_reduction", "sum") == "mean":
+        import torch.distributed as dist
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    return float(getattr(a2c, "grad_scale", 1.0)) / world
+
+
 class HipEngine:
     def __init__(self, model, env, cfg, opt, seed: int = 1):
         self.model = model
@@ -105,7 +115,7 @@ class HipEngine:
         self.path_part = torch.zeros(P, 2, device=dev)     # per-path (episodes, return sum) of the last rollout
         self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.zeros(2, dtype=torch.float32, device=dev)      # {lr, skip}
-        self.weight = (1.0 / E) if a2c.env_reduction == "mean_env" else 1.0
+        self.weight = ((1.0 / E) if a2c.env_reduction == "mean_env" else 1.0) * loss_scale(cfg)
         # optimizer block table (segments split into <= 8192-element blocks)
         self._build_opt_tables()
         self.g_rollout = None

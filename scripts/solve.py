@@ -37,6 +37,10 @@ def main():
     ap.add_argument("--trunk-scale", default=None, choices=["M", "none"])
     ap.add_argument("--gae-lambda", type=float, default=None)
     ap.add_argument("--rmsp-eps", type=float, default=None, help="RMSProp epsilon (reference 0.1, inside the sqrt)")
+    ap.add_argument("--grad-scale", type=float, default=None,
+                    help="factor on the loss weight; 1/8 with --paths 512 emulates 8 ranks whose all-reduced "
+                         "gradient is averaged (--rank-reduction mean) on one GPU")
+    ap.add_argument("--rank-reduction", default=None, choices=["sum", "mean"])
     ap.add_argument("--concurrent", type=int, default=None,
                     help="concurrent tournaments (default paths/16 per rank count, independent of the world size)")
     ap.add_argument("--backend", default="auto")
@@ -85,6 +89,10 @@ def main():
         cfg.a2c.gae_lambda = args.gae_lambda
     if args.rmsp_eps is not None:
         cfg.a2c.rmsp_epsilon = args.rmsp_eps
+    if args.grad_scale is not None:
+        cfg.a2c.grad_scale = args.grad_scale
+    if args.rank_reduction is not None:
+        cfg.a2c.rank_reduction = args.rank_reduction
     if args.N is not None:
         cfg.net.N = args.N
     if args.fitness is not None:
@@ -174,7 +182,8 @@ def main():
                           "concurrent_tournaments": cfg.ga.concurrent_tournaments, "backend": tr.backend,
                           "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
                           "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
-                          "rmsp_epsilon": cfg.a2c.rmsp_epsilon,
+                          "rmsp_epsilon": cfg.a2c.rmsp_epsilon, "grad_scale": cfg.a2c.grad_scale,
+                          "rank_reduction": cfg.a2c.rank_reduction,
                           "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
                           "ga": not args.no_ga, "same_path": args.same_path, "dtype": tr.compute_dtype}}
         out["config"]["seed"] = cfg.seed
