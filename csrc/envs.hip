@@ -365,18 +365,24 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OBS_H * OBS_W / 4);
   uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OBS_H * OBS_W / 4);
   uint32_t* outw = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(obs_out) + (long)env * out_stride);
-  // The old-stack load of the NEXT item is issued before this item's render work (one load in
-  // flight ahead).  Each item is owned by one thread, so obs_in == obs_out stays correct.
+  // The old-stack loads of the next TWO items are in flight during this item's render work: with one
+  // load ahead per thread the whole chip held ~8 MB of loads in flight, about half of what HBM's
+  // bandwidth x latency needs, and the packed-stack kernel ran at ~4.5 TB/s.  Each item is owned by
+  // one thread, so obs_in == obs_out stays correct.
   constexpr int NQ = OBS_H * OBS_W / 4, QR = OBS_W / 4;      // quads per frame / per row
   static_assert(256 % QR == 16 && 256 / QR == 8, "quad walk below assumes 30 quads per row");
-  uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
-  if (!RING && !done) nxt = in4[min((int)threadIdx.x, NQ - 1)];
+  uint4 nxt = make_uint4(0u, 0u, 0u, 0u), nxt2 = nxt;
+  if (!RING && !done) {
+    nxt = in4[min((int)threadIdx.x, NQ - 1)];
+    nxt2 = in4[min((int)threadIdx.x + 256, NQ - 1)];
+  }
   int y = (int)threadIdx.x / QR, xq = (int)threadIdx.x - y * QR;
   int ri_next = rowinfo[y];            // row word of the next quad, read one iteration ahead
   for (int q = threadIdx.x; q < NQ; q += 256) {
     PONG_LOOP_STAMP((q >> 8), rowinfo[y] >> 8);
     const uint4 cur = nxt;
-    if (!RING && !done && q + 256 < NQ) nxt = in4[q + 256];
+    nxt = nxt2;
+    if (!RING && !done) nxt2 = in4[min(q + 512, NQ - 1)];     // (clamped, unconditional: no loop-carried phi)
     const int ri = ri_next;
     {
       int yn = y + 8 + (xq + 16 >= QR ? 1 : 0);
