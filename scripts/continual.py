@@ -87,6 +87,9 @@ def train_task(tr, ti, args, label):
     solved = None
     budget = args.frames_per_task[name]
     while tr.global_step - tr.task_start_step < budget:
+        if solved is not None and args.stop_after_solve is not None and \
+                tr.global_step - tr.task_start_step >= solved["frames"] + args.stop_after_solve:
+            break
         st = tr.update()
         n += 1
         if not math.isnan(st.mean_return):
@@ -103,7 +106,8 @@ def train_task(tr, ti, args, label):
             curve.append(rec)
             print(json.dumps(rec), flush=True)
     tr.flush()
-    return {"task": name, "updates": n, "seconds": round(time.time() - ts, 1), "frames": budget,
+    return {"task": name, "updates": n, "seconds": round(time.time() - ts, 1),
+            "frames": tr.global_step - tr.task_start_step, "budget": budget,
             "threshold": thr, "best_winner": best if math.isfinite(best) else None, "final_mean_return": ema, "solved": solved is not None,
             "generations_to_solve": solved and solved["generation"], "frames_to_solve": solved and solved["frames"],
             "generations": tr.pop.generation - tr._task_gen0, "curve": curve}
@@ -127,6 +131,8 @@ def main():
     ap.add_argument("--eval-steps", type=int, default=6000)
     ap.add_argument("--report-every", type=float, default=20.0)
     ap.add_argument("--control", action="store_true", help="also train tasks >= 2 from scratch (transfer control)")
+    ap.add_argument("--stop-after-solve", type=float, default=None,
+                    help="end a task this many frames after its first solving tournament (default: run the budget)")
     ap.add_argument("--control-only", action="store_true",
                     help="only the from-scratch control runs of tasks >= 2 (e.g. in a separate job)")
     ap.add_argument("--out", default="gpurun_out/continual.json")
@@ -160,7 +166,8 @@ def main():
                "config": {"preset": args.preset, "use_lstm": cfg.net.use_lstm, "L": cfg.net.L, "paths": args.paths, "envs_per_path": args.envs, "t_max": args.tmax, "N": args.N,
                           "M": cfg.net.M, "B": cfg.ga.B, "trunk_scale": cfg.net.trunk_scale, "lr": cfg.a2c.lr,
                           "per_task_heads": True, "freeze_union": cfg.ga.freeze_union, "seed": args.seed,
-                          "env_reduction": cfg.a2c.env_reduction, "dtype": tr.compute_dtype if tr else None},
+                          "env_reduction": cfg.a2c.env_reduction, "dtype": tr.compute_dtype if tr else None,
+                          "stop_after_solve": args.stop_after_solve},
                "per_task": per_task, "scratch_control": controls, "seconds": round(time.time() - t0, 1)}
         os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
         with open(args.out, "w") as f:
