@@ -422,6 +422,176 @@ __global__ __launch_bounds__(256, LB) void conv1_fwd_x2(const uint8_t* __restric
 }
 
 // ===========================================================================
+// first layer forward with the input BAND in LDS: a stage = 8 output rows of one sample (232 positions), whose 36
+// input rows (17 KB of uint8) are copied into LDS with coalesced 16-byte loads while the previous band computes;
+// every pixel fragment is then one conflict-free ds_read_b64 (2 pixels x 4 channels) instead of conv1_fwd_x2's
+// 8-byte global loads (each input byte fetched 4 times through L2, the kernel waiting on them at 2 waves/SIMD).
+// Pixels enter as fp16(1024 + v) (v_perm) with the offset folded into the bias, weights (W * 2^8 hi/lo pair) as
+// the MFMA A operand, conv_epi_sw epilogue.  Passes of <= 2 column tiles (4 modules) keep LDS at 2 x 17.3 KB +
+// 33.8 KB so two workgroups share a CU.  grid = (chunks of bands, P).
+// ===========================================================================
+template <class G>
+struct BD1 {
+  static constexpr int OBR = 8;                                  // output rows per band
+  static constexpr int NB = (G::HO + OBR - 1) / OBR;             // bands per sample (5; the last has 7 rows)
+  static constexpr int IR = (OBR - 1) * G::S + G::KH;            // input rows per band (36)
+  static constexpr int RB = G::WIN * G::CIN;                     // bytes per input row (480)
+  static constexpr int BYTES = IR * RB;                          // 17 280
+  static constexpr int NCH = BYTES / 16;                         // 16-byte chunks (1 080)
+  static constexpr int CIT = (NCH + 255) / 256;
+  static constexpr int NPOS = OBR * G::WO;                       // 232
+  static constexpr int NRT = (NPOS + 15) / 16;                   // 15 position tiles
+  static_assert(BYTES % 16 == 0 && G::U8 && G::KW * G::CIN == 32 && G::K == G::KP, "uint8 first-layer geometry");
+};
+
+template <class G>
+__global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
+                                                           long ylo, uint8_t* __restrict__ bits,
+                                                           const uint16_t* __restrict__ Wh, long wlo,
+                                                           const float* __restrict__ flat, long bias_off, int chunk,
+                                                           const int* __restrict__ act_idx,
+                                                           const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                           int P, int E, int T, int t0, long bits_rows,
+                                                           int bands_per_wg, float in_scale, float out_scale) {
+  using B = BD1<G>;
+  constexpr int KPs = G::KP + 8;
+  constexpr int NK = G::KP / 32;
+  constexpr int NCXT = 2;
+  __shared__ __attribute__((aligned(16))) uint8_t Xb[2][B::BYTES];
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[2][NCXT * 16 * KPs];
+  __shared__ __attribute__((aligned(16))) float bias_s[NCXT * 16];
+  __shared__ float wsum_s[NCXT * 16];
+  __shared__ int mods[X3_MAXM];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int nct = (cnt + 1) >> 1;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15, q = grp;
+  const int PE = P * E;
+  const int nbands = T * E * B::NB;
+  const int b_beg = blockIdx.x * bands_per_wg;
+  const int b_end = min(nbands, b_beg + bands_per_wg);
+  if (b_beg >= b_end) return;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  const int npass = nct > NCXT ? (nct + NCXT - 1) / NCXT : 1;
+  static_assert(B::CIT == 5, "five named staging registers");
+  uint4 rg0, rg1, rg2, rg3, rg4;                       // (an indexed array captured by the lambdas went to scratch)
+  // band u -> (sample s = u / NB, first output row oh0 = (u % NB) * OBR); the last band's rows past HO read the
+  // sample's own last input rows (clamped) and are never stored.  Chunks past NCH reload chunk NCH - 1 (harmless).
+  auto band_src = [&](int u, int j) {
+    const int s = u / B::NB, oh0 = (u - s * B::NB) * B::OBR;
+    const int c = min(tid + 256 * j, B::NCH - 1);
+    const int r = c / (B::RB / 16), cc = c - r * (B::RB / 16);
+    const int ir = min(oh0 * G::S + r, G::HIN - 1);
+    return reinterpret_cast<const uint4*>(X + sample_global(p, s, E, PE, t0) * (long)G::IN_ELEMS + (long)ir * B::RB +
+                                          cc * 16);
+  };
+  auto load_band = [&](int u) {
+    rg0 = *band_src(u, 0);
+    rg1 = *band_src(u, 1);
+    rg2 = *band_src(u, 2);
+    rg3 = *band_src(u, 3);
+    rg4 = *band_src(u, 4);
+  };
+  auto store_band = [&](int buf) {
+    *reinterpret_cast<uint4*>(&Xb[buf][tid * 16]) = rg0;
+    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 256) * 16]) = rg1;
+    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 512) * 16]) = rg2;
+    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 768) * 16]) = rg3;
+    if (tid + 1024 < B::NCH) *reinterpret_cast<uint4*>(&Xb[buf][(tid + 1024) * 16]) = rg4;
+  };
+  for (int pass = 0; pass < npass; ++pass) {
+    const int ct0 = pass * NCXT;
+    const int ncg = nct == 0 ? 1 : min(NCXT, nct - ct0);
+    __syncthreads();                                   // mods visible; the previous pass's LDS reads done
+    static_assert(G::KC == 32, "weight-sum reduction: one column per 32 lanes");
+    for (int i = tid; i < ncg * 16 * G::KC; i += 256) {
+      const int col = i / G::KC, kc = i - col * G::KC;
+      const int slot = ct0 * 2 + (col >> 3);
+      s8v vh = {0, 0, 0, 0, 0, 0, 0, 0}, vl = vh;
+      if (slot < cnt) {
+        const long o = ((long)(mods[slot] * 8 + (col & 7))) * G::KP + kc * 8;
+        vh = *reinterpret_cast<const s8v*>(Wh + o);
+        vl = *reinterpret_cast<const s8v*>(Wh + wlo + o);
+      }
+      *reinterpret_cast<s8v*>(Ws[0] + col * KPs + kc * 8) = vh;
+      *reinterpret_cast<s8v*>(Ws[1] + col * KPs + kc * 8) = vl;
+      const h8v hh = __builtin_bit_cast(h8v, vh), ll = __builtin_bit_cast(h8v, vl);
+      float ws = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ws += (float)hh[j] + (float)ll[j];
+#pragma unroll
+      for (int m = 16; m >= 1; m >>= 1) ws += __shfl_xor(ws, m, 64);
+      if (kc == 0) wsum_s[col] = ws;
+    }
+    load_band(b_beg);
+    __syncthreads();
+    if (tid < ncg * 16) {
+      const int slot = ct0 * 2 + (tid >> 3);
+      const float b = slot < cnt ? flat[bias_off + (long)mods[slot] * chunk + (tid & 7)] : 0.f;
+      bias_s[tid] = b - in_scale * 1024.f * wsum_s[tid];
+    }
+    store_band(0);
+    auto run = [&](auto ncc) {
+      constexpr int NC = decltype(ncc)::value;
+      int buf = 0;
+      for (int u = b_beg; u < b_end; ++u, buf ^= 1) {
+        __syncthreads();                               // band u in LDS (and bias_s); buf ^ 1 free
+        if (u + 1 < b_end) load_band(u + 1);
+        const int s = u / B::NB, oh0 = (u - s * B::NB) * B::OBR;
+        const long growb = sample_global(p, s, E, PE, t0) * G::HOWO + (long)oh0 * G::WO;
+        const uint8_t* xb = Xb[buf];
+        // wave w: position tiles 4w .. 4w+3 (64 positions); every weight fragment read from LDS feeds 4 tiles x 2
+        // MFMAs (one tile per read made the kernel bound by LDS bandwidth: 124 vs 108 us)
+        static_assert(B::NRT <= 16, "4 waves x 4 position tiles");
+        int abase[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int pos = (4 * w + i) * 16 + c16;      // band-local position of this lane's column
+          const int po = pos < B::NPOS ? pos : 0;
+          const int orow = po / G::WO, ocol = po - orow * G::WO;
+          abase[i] = orow * G::S * B::RB + ocol * G::S * G::CIN + grp * 8;
+        }
+        f4v acc[4][NC];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) acc[i][ct] = (f4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {                // k-step kk = kernel row kh
+          s8v a[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            a[i] = u8x8_to_f16off(*reinterpret_cast<const uint2*>(xb + abase[i] + kk * B::RB));
+          const int kc = kk * 4 + grp;
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) {
+            const s8v bh = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
+            const s8v bl = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              acc[i][ct] = mfma16_f16(bl, a[i], acc[i][ct]);
+              acc[i][ct] = mfma16_f16(bh, a[i], acc[i][ct]);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);           // one k-step of LDS fragments live at a time
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int pos = (4 * w + i) * 16 + c16;
+          const bool valid = pos < B::NPOS && oh0 + pos / G::WO < G::HO;
+          conv_epi_sw<NC>(acc[i], bias_s, ct0, cnt, q, in_scale, out_scale, growb + pos, bits, bits_rows, Y, ylo,
+                          pass > 0, valid);
+        }
+        if (u + 1 < b_end) store_band(buf ^ 1);        // buf ^ 1 was read in band u - 1, before this band's barrier
+      }
+    };
+    if (ncg == 1) run(std::integral_constant<int, 1>{});
+    else run(std::integral_constant<int, 2>{});
+  }
+}
+
+// ===========================================================================
 // forward of the bf16-activation conv layers (39x29x8 4x4/s2, 18x13x8 3x3/s1): A hi/lo planes, B hi/lo in LDS,
 // three MFMAs per (row tile, column tile, k-step).  grid = (ceil(T*E*HOWO / (NT*128)), P).  The next 32-row
 // tile's A fragments (both planes) are loaded while this tile's MFMAs run.
@@ -2931,7 +3101,8 @@ static int X3_FC_KS = 1;
 // (pre-activation planes; bias, ReLU, bits and the slot sum in fc_slot_sum2_x3)
 static int X3_FC_MMV = 3;
 static int X3_WG3_TILE = 1;
-static int X3_FWD_TILE = 1;    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
+static int X3_FWD_TILE = 1;
+static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
 extern "C" {
@@ -2944,6 +3115,7 @@ void fast_conv_set_x3_wg3_tile(int t) { X3_WG3_TILE = t; }
 void fast_conv_set_x3_fc_mmv(int v) { X3_FC_MMV = v; }
 void fast_conv_set_x3_fc_dg_gemm(int v) { X3_FC_DG_GEMM = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
+void fast_conv_set_x3_c1_band(int v) { X3_C1_BAND = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
@@ -2960,6 +3132,16 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
     if ((E * C1::HOWO) % 16) return -2;
     const long rows = (long)T * E * C1::HOWO;
     const float isc = is / (float)(1 << X3_W0_SHIFT);
+    if (X3_C1_BAND) {
+      const long nbands = (long)T * E * BD1<C1>::NB;
+      long bpw = (nbands * P + 511) / 512;                 // ~2 workgroups per CU over the launch
+      if (bpw < 2) bpw = 2;
+      conv1_fwd_band_x2<C1><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+          (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac,
+          layer, L, M, P, E, T, t0, br, (int)bpw, isc, os);
+      const int rc = (int)hipGetLastError();
+      return rc ? -rc : 1;
+    }
 #define C1L(NT_, LB_)                                                                                           \
   if (X3_FWD_SW & 1) C1LS(NT_, LB_, true); else C1LS(NT_, LB_, false)
 #define C1LS(NT_, LB_, SW_)                                                                                     \

@@ -212,7 +212,7 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
         assert same > 0.999, (l, same)
 
 
-@pytest.mark.parametrize("arm", ["swapped", "tile"])
+@pytest.mark.parametrize("arm", ["swapped", "tile", "band"])
 @pytest.mark.parametrize("T", [1, 2])
 def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T, arm):
     """conv_epi_sw (weights as the MFMA A operand: one xor-32 module-pair sum, nibble ReLU bits, 8-byte stores; the
@@ -231,10 +231,16 @@ def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T, arm):
     lib = _lib.lib()
     outs = []
     for sw in (0, 3):
-        if arm == "tile":
+        if arm == "band":            # conv1: input band in LDS vs conv1_fwd_x2 (both swapped epilogue, folded offset)
+            lib.fast_conv_set_x3_fwd_sw(1)
+            lib.fast_conv_set_x3_fwd_tile(1)
+            lib.fast_conv_set_x3_c1_band(1 if sw else 0)
+        elif arm == "tile":
+            lib.fast_conv_set_x3_c1_band(0)
             lib.fast_conv_set_x3_fwd_sw(0)
             lib.fast_conv_set_x3_fwd_tile(1 if sw else 0)
         else:
+            lib.fast_conv_set_x3_c1_band(0)
             lib.fast_conv_set_x3_fwd_tile(0)
             lib.fast_conv_set_x3_fwd_sw(sw)
         acts, bits = [], []
@@ -251,6 +257,7 @@ def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T, arm):
         outs.append(([x2_value(a) for a in acts], [b.clone() for b in bits]))
     lib.fast_conv_set_x3_fwd_sw(1)
     lib.fast_conv_set_x3_fwd_tile(1)
+    lib.fast_conv_set_x3_c1_band(1)
     for l in range(3):
         a, b = outs[0][0][l], outs[1][0][l]
         e = rel(b, a)
