@@ -2239,7 +2239,9 @@ __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restri
   __shared__ __attribute__((aligned(16))) uint16_t As[2][2][BR * 32];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[2][2][BC * 32];
   const int R = T * E;
-  // unit -> (module j, row block, column half, k part); units of module j = ceil(inv_cnt[j] * R / 128) x NCS x KS
+  // unit -> (module j, row block, column half, k part); units of module j = ceil(inv_cnt[j] * R / 128) x NCS x KS.
+  // (An XCD-major walk -- a module's workgroups on one XCD -- measured slower: 46.3 vs 44.1 us, kwin_x3_v17.md;
+  // consecutive units go round-robin over the XCDs.)
   int u = (int)blockIdx.x, j = 0, ncnt = 0;
   for (; j < M; ++j) {
     ncnt = inv_cnt[layer * M + j];
@@ -2247,7 +2249,7 @@ __global__ __launch_bounds__(512, 2) void fc_fwd_mm2_x3(const uint16_t* __restri
     if (u < n) break;
     u -= n;
   }
-  if (j >= M) return;                                    // grid is an upper bound on the unit count
+  if (j >= M) return;
   const int kpart = u % KS;
   u /= KS;
   const int chalf = u % NCS, rb = u / NCS;
@@ -2684,7 +2686,11 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
   constexpr int BM = 128, BN = 256, CS = COUT / 32;                 // reduction steps per slot
   __shared__ __attribute__((aligned(16))) bf16_t As[2][2][BM * 32];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[2][2][BN * 32];
-  const int bid = (int)blockIdx.x;
+  // XCD-major: XCD x (= blockIdx % 8) takes the x-th contiguous eighth of the (path, row block, column block) list,
+  // so one path's weight set is fetched into one XCD's L2 rather than into all eight
+  const int ntot = P * nrb * ncb, per = (ntot + 7) >> 3, kx = (int)(blockIdx.x >> 3);
+  const int bid = (int)(blockIdx.x & 7) * per + kx;
+  if (kx >= per || bid >= ntot) return;
   const int p = bid / (nrb * ncb), rem = bid - p * (nrb * ncb);
   const int rbk = rem / ncb, cb = rem - rbk * ncb;
   const int R = T * E, PE = P * E;
@@ -3323,7 +3329,7 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
   const float isc = 1.f / (float)(1 << X3_W0_SHIFT);
   if (X3_FC_MMV >= 3) {
     // k split in two: partial planes Ys[2][M][P*R][256], then bias + ReLU + bits + slot sum in fc_slot_sum2_x3
-    const int umax = 2 * M * 2 * ((P * R + 127) / 128);
+    const int umax = (2 * M * 2 * ((P * R + 127) / 128) + 7) / 8 * 8;
     if (KP == 256)
       fc_fwd_mm2_x3<8, 3, 2><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,
                                                    (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path, inv_slot,
@@ -3344,7 +3350,7 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
     rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   } else if (X3_FC_MMV >= 2) {
-    const int umax = M * 2 * ((P * R + 127) / 128);    // every module on every path: an upper bound
+    const int umax = (M * 2 * ((P * R + 127) / 128) + 7) / 8 * 8;    // every module on every path: an upper bound
     if (KP == 256)
       fc_fwd_mm2_x3<8, 3, 1><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,
                                                    (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path, inv_slot,
@@ -3389,7 +3395,8 @@ int x3_fc_dgrad(const float* G, const void* bits, const void* WcT, long wlo, con
     int rc = (int)hipGetLastError();
     if (rc) return -rc;
     const int nrb = (R + 127) / 128, ncb = (K + 255) / 256;
-    fc_dgrad_gemm_x3<256><<<(unsigned)(P * nrb * ncb), 512, 0, st>>>((const bf16_t*)Gm, gmlo, (const bf16_t*)WcT, wlo,
+    fc_dgrad_gemm_x3<256><<<(unsigned)((P * nrb * ncb + 7) / 8 * 8), 512, 0, st>>>((const bf16_t*)Gm, gmlo,
+                                                                                  (const bf16_t*)WcT, wlo,
                                                                      ai, ac, layer, L, M, K, KP, P, E, T, br, dX, nrb,
                                                                      ncb);
     rc = (int)hipGetLastError();
