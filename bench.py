@@ -103,7 +103,9 @@ def build_trainer(args, ctx, dtype: str, stagger: bool):
     cfg.a2c.t_max = args.tmax
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
-    cfg.frame_ring = args.ring
+    # fp32x: the first layer reads the frame ring (env 70 -> 39 us per step; conv1 forward / weight gradient +6 % /
+    # +7 %; window 11.42 -> 11.15 ms, profiles/r3/kwin_x3_v19*.md); bf16 keeps packed stacks (a wash there, docs/PERF.md)
+    cfg.frame_ring = args.ring or (dtype == "fp32x" and not args.packed)
     cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
     cfg.ga.backend = args.ga_backend
     cfg.compute_dtype = dtype
@@ -187,6 +189,7 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--ring", action="store_true", help="frame ring (single-frame writes) instead of packed stacks")
+    ap.add_argument("--packed", action="store_true", help="fp32x: packed 4-frame stacks instead of the frame ring")
     ap.add_argument("--preset", default="pong")
     ap.add_argument("--env", default=None, help="train this task of the preset's suite instead of its first task")
     ap.add_argument("--kernel-opt", action="append", default=[],

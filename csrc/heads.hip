@@ -144,11 +144,86 @@ __global__ __launch_bounds__(256) void heads_fwd_lanes_kernel(
   actions[b] = best;
 }
 
+// 16 samples per workgroup (128 workgroups at the bench shape instead of 32): thread (slice fs = tid >> 4,
+// sample s = tid & 15) sums features [fs*F/16, (fs+1)*F/16) of its sample against LDS-staged weights; the 16
+// partials meet in LDS in slice order and threads 0..15 add biases and sample.  (The 64-sample kernel above left
+// 7/8 of the CUs idle and ran ~10.6 us per step on one GPU.)
+template <int AM, typename FT>
+__global__ __launch_bounds__(256) void heads_fwd_s16_kernel(
+    const FT* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
+    int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
+    const long long* __restrict__ ctr, int t, int T, int greedy, int b0) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  constexpr int AW = AM + 1;
+  float* Wl = hsm;                       // [F][AW]
+  float* red = hsm + F * AW;             // [16 slices][AW][16 samples]
+  const int fs = threadIdx.x >> 4, sl = threadIdx.x & 15;
+  for (int i = threadIdx.x; i < F * AW; i += 256) {
+    const int f = i / AW, j = i - f * AW;
+    Wl[i] = j == AM ? flat[vw + f] : (j < A ? flat[pw + (long)f * A + j] : 0.f);
+  }
+  __syncthreads();
+  const int b = b0 + blockIdx.x * 16 + sl;
+  const bool valid = b < B;
+  const int fq = F >> 4;
+  const int f0 = fs * fq;
+  float acc[AW];
+#pragma unroll
+  for (int j = 0; j < AW; ++j) acc[j] = 0.f;
+  const FT* fr = feat + (long)(valid ? b : 0) * F;
+  for (int f = f0; f < f0 + fq; f += 8) {
+    float x[8];
+    ldfeat8(fr + f, x);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const float* wr = Wl + (f + jj) * AW;
+#pragma unroll
+      for (int j = 0; j < AW; ++j) acc[j] += x[jj] * wr[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < AW; ++j) red[(fs * AW + j) * 16 + sl] = acc[j];
+  __syncthreads();
+  if (fs != 0 || !valid) return;
+#pragma unroll
+  for (int j = 0; j < AW; ++j) {
+    float v = 0.f;
+    for (int k = 0; k < 16; ++k) v += red[(k * AW + j) * 16 + sl];
+    acc[j] = v;
+  }
+  const uint32_t stepkey = (uint32_t)(ctr[0] * T + t);
+  int best = 0;
+  float bv = -3.0e38f;
+#pragma unroll
+  for (int j = 0; j < AM; ++j) {
+    if (j < A) {
+      const float lg = acc[j] + flat[pb + j];
+      logits[(long)b * A + j] = lg;
+      float sc = lg;
+      if (!greedy) sc += -__logf(-__logf(u01(seed, stepkey, (uint32_t)b, (uint32_t)j)));
+      if (sc > bv) { bv = sc; best = j; }
+    }
+  }
+  value[b] = acc[AM] + flat[vb];
+  actions[b] = best;
+}
+
+static int HEADS_S16 = 1;
+extern "C" void heads_set_s16(int v) { HEADS_S16 = v; }
+
 template <typename FT>
 static bool heads_fwd_lanes_launch(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
                                    int A, int B, float* logits, float* value, int* actions, unsigned seed,
                                    const long long* ctr, int t, int T, int greedy, int b0, hipStream_t stream) {
   if (F % 32 != 0 || A > 18) return false;
+  if (HEADS_S16 && F % 128 == 0 && A <= 8) {
+    const size_t sm = (size_t)(F * 9 + 16 * 9 * 16) * 4;
+    if (sm <= 64 * 1024) {
+      heads_fwd_s16_kernel<8, FT><<<(unsigned)((B - b0 + 15) / 16), 256, sm, stream>>>(
+          (const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T, greedy, b0);
+      return true;
+    }
+  }
   const unsigned g = (unsigned)((B - b0 + 63) / 64);
   if (A <= 8) {
     const size_t sm = (size_t)(F * 9 + 3 * 9 * 64) * 4;

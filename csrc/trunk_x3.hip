@@ -31,6 +31,7 @@ namespace x3 {
 #define X3_NCX 3          // column tiles (16 = 2 modules x 8 maps) of B / masked G in LDS per pass
 #define X3_MAXM 16
 #define X3_NCT 5          // column tiles of a full layer (M <= 10)
+#define X3_RING_FCS 1024  // frame-ring weight gradient: first-valid-channel bytes staged per workgroup
 #define X3_W0_SHIFT 8     // first-layer weights enter the fp16 MFMA as W * 2^8 (hi/lo pair)
 
 template <int HIN_, int WIN_, int CIN_, int KH_, int KW_, int S_, bool U8_>
@@ -444,7 +445,22 @@ struct BD1 {
   static_assert(BYTES % 16 == 0 && G::U8 && G::KW * G::CIN == 32 && G::K == G::KP, "uint8 first-layer geometry");
 };
 
-template <class G>
+// channel planes -> packed pixels: v.x .. v.w are 4 pixels of channel planes 0..3; returns the 4 pixels as
+// (c0, c1, c2, c3) byte words, the packed-stack layout (a 4x4 byte transpose, 8 v_perm_b32)
+DEVI uint4 planes_to_px4(uint4 v) {
+  const uint32_t t0 = __builtin_amdgcn_perm(v.y, v.x, 0x05010400u);   // A0 B0 A1 B1
+  const uint32_t t1 = __builtin_amdgcn_perm(v.y, v.x, 0x07030602u);   // A2 B2 A3 B3
+  const uint32_t t2 = __builtin_amdgcn_perm(v.w, v.z, 0x05010400u);   // C0 D0 C1 D1
+  const uint32_t t3 = __builtin_amdgcn_perm(v.w, v.z, 0x07030602u);   // C2 D2 C3 D3
+  return make_uint4(__builtin_amdgcn_perm(t2, t0, 0x05040100u), __builtin_amdgcn_perm(t2, t0, 0x07060302u),
+                    __builtin_amdgcn_perm(t3, t1, 0x05040100u), __builtin_amdgcn_perm(t3, t1, 0x07060302u));
+}
+
+// RING: X is the frame ring [P*E][nslots][HIN*WIN] uint8 (runtime/engine.py frame_ring); channel c of sample (t, b)
+// is frame slot t + max(c, fcv[t][b]) of env b.  A staging chunk is then 4 pixels of each of the 4 planes (four
+// coalesced 4-byte loads) transposed into the packed (pixel, channel) layout at LDS-write time, so the band in LDS
+// and every MFMA operand read are those of the packed-stack kernel.
+template <class G, bool RING = false>
 __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                            long ylo, uint8_t* __restrict__ bits,
                                                            const uint16_t* __restrict__ Wh, long wlo,
@@ -452,7 +468,8 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
                                                            const int* __restrict__ act_idx,
                                                            const int* __restrict__ act_cnt, int layer, int L, int M,
                                                            int P, int E, int T, int t0, long bits_rows,
-                                                           int bands_per_wg, float in_scale, float out_scale) {
+                                                           int bands_per_wg, float in_scale, float out_scale,
+                                                           const uint8_t* __restrict__ fcv = nullptr, int nslots = 0) {
   using B = BD1<G>;
   constexpr int KPs = G::KP + 8;
   constexpr int NK = G::KP / 32;
@@ -486,20 +503,51 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
     return reinterpret_cast<const uint4*>(X + sample_global(p, s, E, PE, t0) * (long)G::IN_ELEMS + (long)ir * B::RB +
                                           cc * 16);
   };
+  // RING: the 4 plane words of chunk j of band u (rg = {c0, c1, c2, c3} words of 4 pixels).  Measured: 8 pixels
+  // per plane and chunk (3 chunks per thread, two 16-byte LDS stores 32 bytes apart) ran 98.8-100.2 vs 97.4 us
+  auto ring_src = [&](int u, int j) {
+    const int s = u / B::NB, oh0 = (u - s * B::NB) * B::OBR;
+    const int st = s / E, e = s - st * E;
+    const int fc = (int)fcv[(long)(t0 + st) * PE + (long)p * E + e];
+    const long slot0 = (long)(p * E + e) * nslots + t0 + st;
+    const int c = min(tid + 256 * j, B::NCH - 1);
+    const int r = c / (G::WIN / 4), cc = c - r * (G::WIN / 4);
+    const int ir = min(oh0 * G::S + r, G::HIN - 1);
+    constexpr long HW = (long)G::HIN * G::WIN;
+    const uint8_t* src = X + slot0 * HW + (long)ir * G::WIN + cc * 4;
+    return make_uint4(*reinterpret_cast<const uint32_t*>(src + max(0, fc) * HW),
+                      *reinterpret_cast<const uint32_t*>(src + max(1, fc) * HW),
+                      *reinterpret_cast<const uint32_t*>(src + max(2, fc) * HW),
+                      *reinterpret_cast<const uint32_t*>(src + max(3, fc) * HW));
+  };
   auto load_band = [&](int u) {
-    rg0 = *band_src(u, 0);
-    rg1 = *band_src(u, 1);
-    rg2 = *band_src(u, 2);
-    rg3 = *band_src(u, 3);
-    rg4 = *band_src(u, 4);
+    if constexpr (RING) {
+      rg0 = ring_src(u, 0);
+      rg1 = ring_src(u, 1);
+      rg2 = ring_src(u, 2);
+      rg3 = ring_src(u, 3);
+      rg4 = ring_src(u, 4);
+    } else {
+      rg0 = *band_src(u, 0);
+      rg1 = *band_src(u, 1);
+      rg2 = *band_src(u, 2);
+      rg3 = *band_src(u, 3);
+      rg4 = *band_src(u, 4);
+    }
+  };
+  auto px = [&](const uint4& v) {
+    if constexpr (RING) return planes_to_px4(v);
+    else return v;
   };
   auto store_band = [&](int buf) {
-    *reinterpret_cast<uint4*>(&Xb[buf][tid * 16]) = rg0;
-    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 256) * 16]) = rg1;
-    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 512) * 16]) = rg2;
-    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 768) * 16]) = rg3;
-    if (tid + 1024 < B::NCH) *reinterpret_cast<uint4*>(&Xb[buf][(tid + 1024) * 16]) = rg4;
+    *reinterpret_cast<uint4*>(&Xb[buf][tid * 16]) = px(rg0);
+    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 256) * 16]) = px(rg1);
+    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 512) * 16]) = px(rg2);
+    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 768) * 16]) = px(rg3);
+    if (tid + 1024 < B::NCH) *reinterpret_cast<uint4*>(&Xb[buf][(tid + 1024) * 16]) = px(rg4);
   };
+
+
   for (int pass = 0; pass < npass; ++pass) {
     const int ct0 = pass * NCXT;
     const int ncg = nct == 0 ? 1 : min(NCXT, nct - ct0);
@@ -929,7 +977,11 @@ DEVI s8v tr8(const bf16_t* p0, const bf16_t* p1) {
   return (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 }
 
-template <class G, int OB, int PFM>
+// RING (uint8 first layer): X is the frame ring (conv1_fwd_band_x2); a stage loads 4 pixels of each of the 4 channel
+// planes per thread and transposes them into the packed slab at LDS-write time (planes_to_px4).  The first-valid
+// channels of the workgroup's samples are staged in LDS once (a per-stage global byte load would sit in front of
+// the stage's X loads).
+template <class G, int OB, int PFM, bool RING = false>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restrict__ X, long xlo,
                                                             const float* __restrict__ Gr,
                                                             const uint8_t* __restrict__ bits, float* __restrict__ grad,
@@ -937,8 +989,17 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
                                                             const int* __restrict__ act_idx,
                                                             const int* __restrict__ act_cnt, int layer, int L, int M,
                                                             int P, int E, int T, long bits_rows, int units_per_wg,
-                                                            float in_scale, float g_scale) {
+                                                            float in_scale, float g_scale,
+                                                            const uint8_t* __restrict__ fcv = nullptr,
+                                                            int nslots = 0) {
   using SB = Slab<G, OB>;
+  static_assert(!RING || (G::U8 && G::CIN == 4 && G::WIN % 4 == 0), "ring input: uint8 4-channel first layer");
+  // ring: 4-pixel groups per slab (one 16-byte LDS store each; 8-pixel groups, one round of loads but four stores
+  // 64 bytes apart, measured 2565 vs 2477 us)
+  constexpr int NG4 = SB::SR * G::WIN / 4;
+  constexpr int XIT4 = (NG4 + 255) / 256;
+  constexpr int FCS = RING ? X3_RING_FCS : 1;
+  __shared__ uint8_t fcs[FCS];
   constexpr bool XL = !G::U8;                       // bf16 input: lo plane too
   constexpr int NXP = XL ? 2 : 1;
   constexpr int GS = X3_NCX * 16 + 8;
@@ -963,6 +1024,11 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
   const int nunits = T * E * SB::NB;
   const int u_beg = blockIdx.x * units_per_wg;
   const int u_end = min(nunits, u_beg + units_per_wg);
+  const int s_first = u_beg / SB::NB;
+  if constexpr (RING) {
+    const int s_last = min(T * E, (u_end + SB::NB - 1) / SB::NB);
+    for (int i = tid; i < s_last - s_first && i < FCS; i += 256) fcs[i] = fcv[sample_global(p, s_first + i, E, PE, 0)];
+  }
   int aoff[SB::KS][2];
 #pragma unroll
   for (int ks = 0; ks < SB::KS; ++ks)
@@ -991,7 +1057,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
     // 3-tile accumulators would cap occupancy); stages load strictly in unit order
     constexpr int PF = (PFM >= 2 && NC <= 2) ? 2 : 1;
     struct Regs {
-      XRaw xr[SB::XIT];
+      XRaw xr[RING ? 1 : SB::XIT];
+      uint4 xq[RING ? XIT4 : 1];                     // ring: {c0, c1, c2, c3} words of 4 pixels
       s8v xl[XL ? SB::XIT : 1];
       float4 g0r[GIT], g1r[GIT];
       uint32_t gbr[GIT][2];
@@ -1016,9 +1083,26 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
       const int ih0 = band * OB * G::S;
       const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;
       Rg.navail = navail;
+      if constexpr (RING) {
+        constexpr long HW = (long)G::HIN * G::WIN;
+        const int fc = (int)fcs[ut * E + ue - s_first];
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(X) + ((long)(p * E + ue) * nslots + ut) * HW +
+                             (long)ih0 * G::WIN;
+        const int npx = min(SB::SR, G::HIN - ih0) * G::WIN;
+        Rg.navail = npx;
+#pragma unroll
+        for (int j = 0; j < XIT4; ++j) {
+          const int gi = tid + 256 * j;
+          const int e0 = (gi < NG4 && gi * 4 < npx) ? gi * 4 : 0;        // clamped, zeroed at write time
+          Rg.xq[j] = make_uint4(*reinterpret_cast<const uint32_t*>(src + max(0, fc) * HW + e0),
+                                *reinterpret_cast<const uint32_t*>(src + max(1, fc) * HW + e0),
+                                *reinterpret_cast<const uint32_t*>(src + max(2, fc) * HW + e0),
+                                *reinterpret_cast<const uint32_t*>(src + max(3, fc) * HW + e0));
+        }
+      }
       const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
 #pragma unroll
-      for (int j = 0; j < SB::XIT; ++j) {
+      for (int j = 0; j < (RING ? 0 : SB::XIT); ++j) {
         const int gi = tid + 256 * j;
         const int e0 = (gi < SB::NG8 && gi * 8 < navail) ? gi * 8 : 0;   // clamped, zeroed at write time
         if constexpr (G::U8) {
@@ -1048,8 +1132,24 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
       }
     };
     auto write_stage = [&](const Regs& Rg, int buf) {
+      if constexpr (RING) {
 #pragma unroll
-      for (int j = 0; j < SB::XIT; ++j) {
+        for (int j = 0; j < XIT4; ++j) {
+          const int gi = tid + 256 * j;
+          if (gi < NG4) {
+            s8v v0 = {0, 0, 0, 0, 0, 0, 0, 0}, v1 = v0;
+            if (gi * 4 < Rg.navail) {
+              const uint4 px = planes_to_px4(Rg.xq[j]);
+              v0 = u8x8_to_bf16(make_uint2(px.x, px.y));
+              v1 = u8x8_to_bf16(make_uint2(px.z, px.w));
+            }
+            *reinterpret_cast<s8v*>(&Xs[buf][0][gi * 16]) = v0;
+            *reinterpret_cast<s8v*>(&Xs[buf][0][gi * 16 + 8]) = v1;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < (RING ? 0 : SB::XIT); ++j) {
         const int gi = tid + 256 * j;
         if (gi < SB::NG8) {
           const bool ok = gi * 8 < Rg.navail;
@@ -3198,6 +3298,49 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
   return 0;
 }
 
+// first layer on the frame ring (frames [P*E][nslots][160*120] u8, fc [T+1][P*E] u8; runtime/engine.py frame_ring)
+int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, void* bits, const void* Wc, long wlo,
+                      const float* flat, long bias_off, int chunk, const int* ai, const int* ac, int L, int M, int P,
+                      int E, int T, int t0, int nslots, long br, float is, float os, hipStream_t st) {
+  if (!frames || !fc || chunk <= 0 || L <= 0 || M <= 0 || P <= 0 || E <= 0 || T <= 0 || t0 < 0 || br <= 0 ||
+      bias_off < 0 || ylo <= 0 || wlo <= 0 || nslots < t0 + T + 3) return -22;
+  if (M > 2 * X3_NCT) return 0;
+  if ((E * C1::HOWO) % 16) return -2;
+  const float isc = is / (float)(1 << X3_W0_SHIFT);
+  const long nbands = (long)T * E * BD1<C1>::NB;
+  long bpw = (nbands * P + 511) / 512;
+  if (bpw < 2) bpw = 2;
+  conv1_fwd_band_x2<C1, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+      (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
+      ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
+int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, const void* bits, float* grad, long w_off,
+                        long b_off, int chunk, const int* ai, const int* ac, int L, int M, int P, int E, int T,
+                        int nslots, long br, float is, float gs, hipStream_t st) {
+  if (!frames || !fc || chunk <= 0 || L <= 0 || M <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 || w_off < 0 ||
+      b_off < 0 || nslots < T + 3) return -22;
+  if (M > 2 * X3_NCT) return 0;
+  using SB = Slab<C1, 2>;
+  const long units = (long)T * E * SB::NB;
+  long upw = (units + 23) / 24;
+  if (upw < 8) upw = 8;
+  if (upw / SB::NB + 2 > X3_RING_FCS) return -22;       // the workgroup's first-valid bytes fit the LDS table
+  const dim3 grid((unsigned)((units + upw - 1) / upw), P);
+  if (X3_WGRAD_PF == 2)
+    conv_wgrad_slab_x3<C1, 2, 2, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
+                                                             chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
+                                                             (const uint8_t*)fc, nslots);
+  else
+    conv_wgrad_slab_x3<C1, 2, 1, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
+                                                             chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
+                                                             (const uint8_t*)fc, nslots);
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
 int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void* bits, float* grad, long w_off,
                   long b_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win,
                   int Cin, int KH, int KW, int S, int P, int E, int T, long br, float is, float gs, hipStream_t st) {
@@ -3328,26 +3471,33 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
   const int R = T * E, tpp = (R + 15) / 16;
   const float isc = 1.f / (float)(1 << X3_W0_SHIFT);
   if (X3_FC_MMV >= 3) {
-    // k split in two: partial planes Ys[2][M][P*R][256], then bias + ReLU + bits + slot sum in fc_slot_sum2_x3
-    const int umax = (2 * M * 2 * ((P * R + 127) / 128) + 7) / 8 * 8;
-    if (KP == 256)
-      fc_fwd_mm2_x3<8, 3, 2><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,
-                                                   (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path, inv_slot,
-                                                   inv_cnt, layer, M, KP, P, E, T, t0, br, isc);
-    else
-      fc_fwd_mm2_x3<0, 3, 2><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,
-                                                   (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path, inv_slot,
-                                                   inv_cnt, layer, M, KP, P, E, T, t0, br, isc);
-    int rc = (int)hipGetLastError();
-    if (rc) return -rc;
+    // k split in KS (2, or 4 for X3_FC_MMV >= 4): partial planes Ys[KS][M][P*R][256], then bias + ReLU + bits +
+    // slot sum in fc_slot_sum2_x3
+    const int ks = X3_FC_MMV >= 4 ? 4 : 2;
+    const int umax = (ks * M * 2 * ((P * R + 127) / 128) + 7) / 8 * 8;
     const unsigned g2 = (unsigned)(((long)P * R * 32 + 255) / 256);
-    if (ylo == 0)
-      fc_slot_sum2_x3<true, 2><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br, layer, L,
-                                                   M, P, E, T, t0, Y, 0, os);
-    else
-      fc_slot_sum2_x3<false, 2><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br, layer, L,
-                                                    M, P, E, T, t0, Y, ylo, os);
-    rc = (int)hipGetLastError();
+#define MM2KS(KS_)                                                                                                \
+    {                                                                                                             \
+      if (KP == 256)                                                                                              \
+        fc_fwd_mm2_x3<8, 3, KS_><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,          \
+                                                       (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path,  \
+                                                       inv_slot, inv_cnt, layer, M, KP, P, E, T, t0, br, isc);     \
+      else                                                                                                        \
+        fc_fwd_mm2_x3<0, 3, KS_><<<umax, 512, 0, st>>>((const uint16_t*)X, xlo, ldx, Ys, (uint16_t*)bits,          \
+                                                       (const uint16_t*)Wc, wlo, flat, bias_off, chunk, inv_path,  \
+                                                       inv_slot, inv_cnt, layer, M, KP, P, E, T, t0, br, isc);     \
+      int rc_ = (int)hipGetLastError();                                                                           \
+      if (rc_) return -rc_;                                                                                       \
+      if (ylo == 0)                                                                                               \
+        fc_slot_sum2_x3<true, KS_><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br,     \
+                                                       layer, L, M, P, E, T, t0, Y, 0, os);                        \
+      else                                                                                                        \
+        fc_slot_sum2_x3<false, KS_><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br,    \
+                                                        layer, L, M, P, E, T, t0, Y, ylo, os);                     \
+    }
+    if (ks == 4) MM2KS(4) else MM2KS(2)
+#undef MM2KS
+    const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   } else if (X3_FC_MMV >= 2) {
     const int umax = (M * 2 * ((P * R + 127) / 128) + 7) / 8 * 8;    // every module on every path: an upper bound

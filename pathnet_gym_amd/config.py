@@ -201,9 +201,9 @@ class TrainConfig:
     # fp32 kernels (slower: see docs/PERF.md)
     deterministic: bool = False
     use_graph: bool = True
-    frame_ring: bool = False            # HIP Pong: single-frame ring instead of packed stacks (runtime/engine.py;
-                                        # measured 13.06 vs 12.73 ms/update: the conv1 planar loads cost more than
-                                        # the env saves)
+    frame_ring: bool = False            # HIP Pong: single-frame ring instead of packed stacks (runtime/engine.py).
+                                        # bf16: 13.06 vs 12.73 ms/update (the conv1 planar loads cost more than the
+                                        # env saves); fp32x: 11.15 vs 11.42 ms (LDS-staged first layer, bench default)
     # HIP engine rollout: the population is stepped as this many path groups on their own HIP streams (one
     # branch each inside the rollout hipGraph) so one group's latency-bound fc / heads launches can overlap
     # the other group's env / conv1 launches (runtime/engine.py; packed-stack pixel envs without LSTM).

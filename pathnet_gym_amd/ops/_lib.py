@@ -120,6 +120,9 @@ _SIGS = {
                    + [c_long, c_float, c_float, P],
     "x3_conv_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 12
                      + [c_long, c_float, c_float, P],
+    "x3_conv1_ring_fwd": [P, P, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 7
+                         + [c_long, c_float, c_float, P],
+    "x3_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 6 + [c_long, c_float, c_float, P],
     "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P],
     "x3_fc_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 10
                  + [c_long, c_float, P],
@@ -139,6 +142,7 @@ _SIGS = {
     "fast_conv_set_x3_fc_dg_gemm": [c_int],
     "fast_conv_set_x3_fwd_tile": [c_int],
     "fast_conv_set_x3_c1_band": [c_int],
+    "heads_set_s16": [c_int],
     "fast_conv_set_x3_fc_d": [c_int],
     "fast_conv_set_x3_fc_ks": [c_int],
     "fast_conv_set_x3_wgrad_pf": [c_int],

@@ -197,9 +197,10 @@ class HipPathNet:
                 self.lstm = dict(F=F, H=H, k_off=ls["kernel"], b_off=ls["bias"],
                                  KpT=torch.zeros(4 * H, F + H, dtype=torch.bfloat16, device=dev),
                                  Kb=torch.zeros(F + H, 4 * H, dtype=torch.bfloat16, device=dev))
-        # frame-ring input for the first layer (runtime/engine.py): channel-major bf16 weights
+        # frame-ring input for the first layer (runtime/engine.py): channel-major bf16 weights; fp32x reads the ring
+        # into its packed LDS band / slab (csrc/trunk_x3.hip RING) and keeps its own weight pairs
         g0 = self.geoms[0]
-        self.ring_ok = (not self.deterministic and not self.x3 and g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
+        self.ring_ok = (not self.deterministic and not self.f32 and g0.kind == "conv" and g0.u8in and (g0.Hin, g0.Win, g0.Cin, g0.KH, g0.S) == (160, 120, 4, 8, 4)
                         and self.M <= 10 and g0.Cout == 8)
         self.Wc_ring = None
         # uint8 first conv layer: fp16 operand copy + per-column weight sums for the fp16-offset MFMA path
@@ -214,7 +215,7 @@ class HipPathNet:
         """Allocate the channel-major first-layer weight copy used with the frame ring."""
         if not self.ring_ok:
             raise NotImplementedError("frame ring needs the 160x120x4 / 8x8 s4 first conv layer and M <= 10")
-        if self.Wc_ring is None:
+        if self.Wc_ring is None and not self.x3:
             g = self.geoms[0]
             dev = self.model.device
             self.Wc_ring = torch.zeros(self.M, g.Cout, g.KP, dtype=torch.bfloat16, device=dev)
@@ -506,9 +507,9 @@ class HipPathNet:
                                "(fc layers take <= 32 rows per path and launch)")
 
     def _ys_buffer_x3(self, rows: int) -> torch.Tensor:
-        """fp32 module-slot planes [2][M][rows][256] of the module-major fc forward (two k-part planes of
+        """fp32 module-slot planes [4][M][rows][256] of the module-major fc forward (up to four k-part planes of
         pre-activations, or one plane of activations; grown before graph capture)."""
-        need = 2 * self.M * rows * 256
+        need = 4 * self.M * rows * 256
         if self._ys is None or self._ys.numel() < need:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("fp32x: fc slot buffer first needed inside a graph capture")
@@ -707,6 +708,15 @@ class HipPathNet:
         g = self.geoms[0]
         m = self.model
         out_scale = self.out_scale_last if self.L == 1 else 1.0
+        if self.x3:
+            _lib.check(Y, torch.float16, name="Y")
+            ok = _lib.call_fast("x3_conv1_ring_fwd", frames.data_ptr(), fc.data_ptr(), Y.data_ptr(), x2_lo(Y),
+                                bits.data_ptr(), self.Wc[0].data_ptr(), self.Wc[0][0].numel(), m.store.flat.data_ptr(),
+                                g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), self.L, self.M, P, E, T,
+                                t0, frames.shape[1], bits_rows, g.in_scale, out_scale, _lib.stream())
+            if not ok:
+                raise RuntimeError(f"fp32x: frame-ring forward has no kernel for P={P}, E={E}, M={self.M}")
+            return
         _lib.call("fast_conv1_ring_fwd", frames.data_ptr(), fc.data_ptr(), Y.data_ptr(), bits.data_ptr(),
                   self.Wh_ring.data_ptr(), m.store.flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
                   m.act_cnt.data_ptr(), 0, self.L, self.M, P, E, T, t0, frames.shape[1], bits_rows, g.in_scale,
@@ -717,6 +727,15 @@ class HipPathNet:
         g = self.geoms[0]
         m = self.model
         g_scale = self.out_scale_last if self.L == 1 else 1.0
+        if self.x3:
+            _lib.check(G, torch.float32, name="G")
+            ok = _lib.call_fast("x3_conv1_ring_wgrad", frames.data_ptr(), fc.data_ptr(), G.data_ptr(), bits.data_ptr(),
+                                grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
+                                m.act_cnt.data_ptr(), self.L, self.M, P, E, T, frames.shape[1], bits_rows, g.in_scale,
+                                g_scale, _lib.stream())
+            if not ok:
+                raise RuntimeError(f"fp32x: frame-ring weight gradient has no kernel for P={P}, E={E}, M={self.M}")
+            return
         _lib.call("fast_conv1_ring_wgrad", frames.data_ptr(), fc.data_ptr(), G.data_ptr(), bits.data_ptr(),
                   grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), 0,
                   self.L, self.M, P, E, T, frames.shape[1], bits_rows, g.in_scale, g_scale, _lib.stream())

@@ -301,9 +301,10 @@ def test_heads_and_a2c_grad(hip_lib):
         assert rel(gflat[s.offset:s.offset + s.numel], flat.grad[s.offset:s.offset + s.numel]) < 1e-4, name
 
 
-@pytest.mark.parametrize("A,F", [(18, 256), (6, 96), (3, 64)])
+@pytest.mark.parametrize("A,F", [(18, 256), (6, 96), (3, 64), (6, 256), (8, 128)])
 def test_heads_fwd_action_and_feature_widths(hip_lib, A, F):
-    """Lane-per-sample heads forward for A <= 8 and A <= 18, a partial last workgroup, several F."""
+    """Lane-per-sample heads forward for A <= 8 and A <= 18 (and the 16-samples-per-workgroup form for A <= 8,
+    F % 128 == 0), a partial last workgroup, several F."""
     cfg = PathNetConfig(L=2, M=4, N=2, input_shape=(4,), layers=[LayerSpec("fc", 64), LayerSpec("fc", F)],
                         trunk_scale="none", num_actions=A)
     P, E = 3, 16

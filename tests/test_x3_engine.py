@@ -168,6 +168,60 @@ def test_x3_gradient_check_detects_a_two_percent_module_error(x3_rollout):
         assert err > X3_LAYER_TOL, (l, err)
 
 
+@pytest.fixture(scope="module")
+def x3_ring_rollout(hip_lib):
+    """The x3_rollout update with the first layer on the frame ring (engine.frame_ring: T+4 single frames per env;
+    csrc/trunk_x3.hip conv1_fwd_band_x2 / conv_wgrad_slab_x3 RING), episode resets inside the rollout."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 4
+    cfg.use_graph = False
+    cfg.compute_dtype = "fp32x"
+    cfg.frame_ring = True
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng = tr.engine
+    assert tr.compute_dtype == "fp32x" and eng.ring
+    tr.env.max_episode_steps = 5
+    tr.update()
+    tr.model.set_paths(masks_with_edges(3, cfg.net.L, cfg.net.M, cfg.net.N, seed=2))
+    eng._rollout_backward_body()
+    torch.cuda.synchronize()
+    assert eng.dones.any()
+    return tr, eng, _oracle_grad(tr, eng), eng.grad_flat.clone()
+
+
+def test_x3_frame_ring_gradient_vs_plain_fp32_oracle(x3_ring_rollout):
+    tr, eng, g_ref, g_hip = x3_ring_rollout
+    err = layer_errors(tr, g_hip, g_ref)
+    print("fp32x frame-ring engine vs fp32 oracle, per layer:", {k: f"{v:.2e}" for k, v in err.items()})
+    for k, v in err.items():
+        assert v < X3_LAYER_TOL, (k, v)
+
+
+def test_x3_frame_ring_forward_bit_equal_to_packed(x3_ring_rollout):
+    """The ring forward stages the same packed band in LDS as the packed-stack kernel: its outputs and ReLU bits
+    must equal the packed kernel's on the reconstructed stacks bit for bit (resets included)."""
+    tr, eng, _, _ = x3_ring_rollout
+    hp = tr.model.hip
+    T, B = eng.T, eng.B
+    g = hp.geoms[0]
+    stacks = eng.obs_stacks(T + 1).contiguous()
+    Y = hp.alloc_act(0, (T + 1, B, g.out_feat))
+    bits, rows = hp.alloc_bits(0, T + 1, B)
+    hp.layer_fwd(0, stacks, Y, bits, eng.P, eng.E, T + 1, 0, rows)
+    torch.cuda.synchronize()
+    assert rows == eng.bits_rows[0]
+    assert torch.equal(x2_value(Y), x2_value(eng.acts[0]))
+    # ReLU bits: slots < the path's active-module count (slots past it keep whatever an earlier path set wrote)
+    cnt = tr.model.act_cnt.view(eng.P, -1)[:, 0].cpu()
+    hw = g.HWo
+    for p in range(eng.P):
+        for t in range(T + 1):
+            r0 = (t * B + p * eng.E) * hw
+            k = int(cnt[p])
+            assert torch.equal(bits[:k, r0:r0 + eng.E * hw], eng.bits[0][:k, r0:r0 + eng.E * hw]), (p, t)
+
+
 @pytest.mark.parametrize("E", [16, 32])
 @pytest.mark.parametrize("variant", ["split_k", "module_major", "module_major_ks1", "module_major_regs"])
 def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
