@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out/solve
 NAME=pong_bench_fp32x_seed3
-timeout -k 10 1050 python -u scripts/solve.py --preset pong --ga-backend device --seed 3 --dtype fp32x --report-every 30 \
+timeout -k 10 1050 python -u scripts/solve.py --preset pong --ga-backend device --seed 3 --dtype fp32x --ring --report-every 30 \
     --minutes 16 --curve gpurun_out/solve/$NAME.jsonl --out gpurun_out/solve/$NAME.json > gpurun_out/solve/$NAME.log 2>&1 \
     || { echo "SOLVE FAIL"; tail -5 gpurun_out/solve/$NAME.log; exit 1; }
 tail -1 gpurun_out/solve/$NAME.json | cut -c1-300

@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--same-path", action="store_true",
                     help="every path starts from the same random N-module genotype (ablation)")
     ap.add_argument("--out", default=None, help="also write the final JSON record to this file")
+    ap.add_argument("--ring", action="store_true", help="first layer on the frame ring (the fp32x bench default)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp32x"], help="HIP engine compute dtype")
     ap.add_argument("--deterministic", action="store_true", help="fixed-order gradient reductions")
     args = ap.parse_args()
@@ -106,6 +107,7 @@ def main():
         cfg.ga.fitness_window = args.fitness_window
     cfg.backend = args.backend
     cfg.use_graph = not args.no_graph
+    cfg.frame_ring = bool(args.ring)
     if args.dtype is not None:
         cfg.compute_dtype = args.dtype
     cfg.deterministic = bool(args.deterministic)
@@ -183,7 +185,7 @@ def main():
                           "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
                           "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
                           "rmsp_epsilon": cfg.a2c.rmsp_epsilon, "grad_scale": cfg.a2c.grad_scale,
-                          "rank_reduction": cfg.a2c.rank_reduction,
+                          "rank_reduction": cfg.a2c.rank_reduction, "frame_ring": bool(tr.engine.ring),
                           "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
                           "ga": not args.no_ga, "same_path": args.same_path, "dtype": tr.compute_dtype}}
         out["config"]["seed"] = cfg.seed
