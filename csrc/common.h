@@ -28,15 +28,19 @@ DEVI bf16_t f2bf(float f) {
 }
 
 // 8 x uint8 (0..255, exact in bf16) -> 8 x bf16: v_cvt_f32_ubyteN + v_cvt_pk_bf16_f32
+// float(v) of a byte has zero low 16 mantissa bits, so its upper half IS bf16(v): one v_cvt_f32_ubyte per value
+// and one v_perm_b32 per pair (the (__bf16) conversion compiled to a v_cvt_pk_bf16_f32 per value plus merges)
 DEVI s8v u8x8_to_bf16(uint2 v) {
-  __bf16 h[8];
+  uint32_t w[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    h[j] = (__bf16)(float)((v.x >> (8 * j)) & 0xFFu);
-    h[j + 4] = (__bf16)(float)((v.y >> (8 * j)) & 0xFFu);
+  for (int j = 0; j < 2; ++j) {
+    const float a = (float)(v.x >> (16 * j) & 0xFFu), b = (float)(v.x >> (16 * j + 8) & 0xFFu);
+    const float c = (float)(v.y >> (16 * j) & 0xFFu), d = (float)(v.y >> (16 * j + 8) & 0xFFu);
+    w[j] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x07060302u);
+    w[j + 2] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, d), __builtin_bit_cast(uint32_t, c), 0x07060302u);
   }
   s8v r;
-  __builtin_memcpy(&r, h, 16);
+  __builtin_memcpy(&r, w, 16);
   return r;
 }
 

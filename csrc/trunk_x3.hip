@@ -87,13 +87,22 @@ typedef float f2v_ __attribute__((ext_vector_type(2)));
 // hi = RNE bf16(v), lo = RNE bf16(v - hi): one v_cvt_pk_bf16_f32 per PAIR for hi (the scalar form converted each
 // value twice: once alone for the residual, once paired for the store), the residual's operand rebuilt from the
 // packed word by a shift / mask
+// bit C of v sign-extended (0 or ~0): one v_bfe_i32 (written out: the compiler turns the shift form back into a
+// compare + select per use)
+template <int C>
+DEVI uint32_t sbfe1(uint32_t v) {
+  uint32_t r;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(v), "n"(C));
+  return r;
+}
 DEVI void split8(const float (&v)[8], s8v& hi, s8v& lo) {
   uint32_t h[4], l[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    h[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v_){v[2 * j], v[2 * j + 1]}, b2v));
-    const float b0 = __builtin_bit_cast(float, h[j] << 16), b1 = __builtin_bit_cast(float, h[j] & 0xFFFF0000u);
-    l[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v_){v[2 * j] - b0, v[2 * j + 1] - b1}, b2v));
+    const f2v_ vv = {v[2 * j], v[2 * j + 1]};
+    h[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(vv, b2v));
+    const f2v_ bb = {__builtin_bit_cast(float, h[j] << 16), __builtin_bit_cast(float, h[j] & 0xFFFF0000u)};
+    l[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(vv - bb, b2v));      // one v_pk_add_f32
   }
   __builtin_memcpy(&hi, h, 16);
   __builtin_memcpy(&lo, l, 16);
@@ -1043,11 +1052,11 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
   using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
   auto run = [&](auto ncc, const int ct0) {
     constexpr int NC = decltype(ncc)::value;
-    float acc_b[2][8];
+    f2v_ acc_b[2][4];                                // channel pairs: v_pk_add_f32
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
-      for (int c = 0; c < 8; ++c) acc_b[k][c] = 0.f;
+      for (int c = 0; c < 4; ++c) acc_b[k][c] = (f2v_){0.f, 0.f};
     f4v acc[MPW][NC];
 #pragma unroll
     for (int a = 0; a < MPW; ++a)
@@ -1175,11 +1184,16 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
         for (int k = 0; k < 2; ++k) {
           const int rel = sub + 4 * k;
           if (rel < 2 * NC) {
+            // ReLU mask as a sign-extended bit field AND the value's bits (v_bfe_i32 + v_and instead of a compare,
+            // a select and a scalar mask merge per value)
+            const uint32_t bm = Rg.gvr[j] ? (uint32_t)Rg.gbr[j][k] : 0u;
+            const uint32_t mk[8] = {sbfe1<0>(bm), sbfe1<1>(bm), sbfe1<2>(bm), sbfe1<3>(bm),
+                                    sbfe1<4>(bm), sbfe1<5>(bm), sbfe1<6>(bm), sbfe1<7>(bm)};
             float m[8];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) m[c] = (Rg.gvr[j] && ((Rg.gbr[j][k] >> c) & 1u)) ? gg[c] : 0.f;
+            for (int c = 0; c < 8; ++c) m[c] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, gg[c]) & mk[c]);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) acc_b[k][c] += m[c];
+            for (int c = 0; c < 4; ++c) acc_b[k][c] += (f2v_){m[2 * c], m[2 * c + 1]};
             s8v hi, lo;
             split8(m, hi, lo);
             *reinterpret_cast<s8v*>(&Gs[buf][0][rho * GS + rel * 8]) = hi;
@@ -1290,7 +1304,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
       const int slot = 2 * ct0 + rel;
       if (rel < 2 * NC && slot < cnt) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) atomicAdd(&dbias[slot * 8 + c], acc_b[k][c] * g_scale);
+        for (int c = 0; c < 8; ++c) atomicAdd(&dbias[slot * 8 + c], acc_b[k][c >> 1][c & 1] * g_scale);
       }
     }
   };
