@@ -95,6 +95,13 @@ DEVI uint32_t sbfe1(uint32_t v) {
   asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(v), "n"(C));
   return r;
 }
+// m[c] = bit c of b ? g[c] : 0, as v_bfe_i32 + v_and per value
+DEVI void mask8(const float (&g)[8], uint32_t b, float (&m)[8]) {
+  const uint32_t mk[8] = {sbfe1<0>(b), sbfe1<1>(b), sbfe1<2>(b), sbfe1<3>(b),
+                          sbfe1<4>(b), sbfe1<5>(b), sbfe1<6>(b), sbfe1<7>(b)};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) m[c] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, g[c]) & mk[c]);
+}
 DEVI void split8(const float (&v)[8], s8v& hi, s8v& lo) {
   uint32_t h[4], l[4];
 #pragma unroll
@@ -1422,8 +1429,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
         float m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (gv) {
           const float gg[8] = {g0r.x, g0r.y, g0r.z, g0r.w, g1r.x, g1r.y, g1r.z, g1r.w};
-#pragma unroll
-          for (int c = 0; c < 8; ++c) m[c] = ((gbr >> c) & 1u) ? gg[c] : 0.f;
+          mask8(gg, (uint32_t)gbr, m);
         }
 #pragma unroll
         for (int c = 0; c < 8; ++c) bpart[c] += m[c];
@@ -1631,11 +1637,9 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
         if (it < W::NGI) {
           const float gg[8] = {g0r[j].x, g0r[j].y, g0r[j].z, g0r[j].w, g1r[j].x, g1r[j].y, g1r[j].z, g1r[j].w};
           float m[8];
+          mask8(gg, (uint32_t)gb[j], m);
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            m[c] = ((gb[j] >> c) & 1u) ? gg[c] : 0.f;
-            bpart[c] += m[c];
-          }
+          for (int c = 0; c < 8; ++c) bpart[c] += m[c];
           s8v hi, lo;
           split8(m, hi, lo);
           const int o = (it >> 2) * W::GS + a_my * 8;
@@ -1826,8 +1830,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
           for (int a4 = 0; a4 < 4; ++a4) {
             const int b = (int)gbr[j][(4 * g + a4) < 12 ? 4 * g + a4 : 0] * (4 * g + a4 < cnt ? 1 : 0);
             float m[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) m[c] = ((b >> c) & 1) ? gg[c] : 0.f;
+            mask8(gg, (uint32_t)b, m);
             s8v hi, lo;
             split8(m, hi, lo);
             const int o = pos * X3_DG_PSTR + (a4 ^ dg_swz(pos)) * 8;
