@@ -476,7 +476,9 @@ DEVI uint4 planes_to_px4(uint4 v) {
 // is frame slot t + max(c, fcv[t][b]) of env b.  A staging chunk is then 4 pixels of each of the 4 planes (four
 // coalesced 4-byte loads) transposed into the packed (pixel, channel) layout at LDS-write time, so the band in LDS
 // and every MFMA operand read are those of the packed-stack kernel.
-template <class G, bool RING = false>
+// PIPE: the next k-step's pixel and weight fragments are read from LDS while this k-step's MFMAs run (one k-step of
+// fragments ahead instead of a wait on every k-step's reads)
+template <class G, bool RING = false, bool PIPE = false>
 __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                            long ylo, uint8_t* __restrict__ bits,
                                                            const uint16_t* __restrict__ Wh, long wlo,
@@ -621,6 +623,46 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int ct = 0; ct < NC; ++ct) acc[i][ct] = (f4v){0.f, 0.f, 0.f, 0.f};
+        if constexpr (PIPE) {
+          uint2 ra[4];
+          s8v rbh[NC], rbl[NC];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ra[i] = *reinterpret_cast<const uint2*>(xb + abase[i]);
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) {
+            rbh[ct] = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + grp * 8);
+            rbl[ct] = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + grp * 8);
+          }
+#pragma unroll
+          for (int kk = 0; kk < NK; ++kk) {
+            s8v a[4], bh[NC], bl[NC];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = u8x8_to_f16off(ra[i]);
+#pragma unroll
+            for (int ct = 0; ct < NC; ++ct) {
+              bh[ct] = rbh[ct];
+              bl[ct] = rbl[ct];
+            }
+            if (kk + 1 < NK) {                           // (compile-time after unrolling)
+              const int kc = (kk + 1) * 4 + grp;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) ra[i] = *reinterpret_cast<const uint2*>(xb + abase[i] + (kk + 1) * B::RB);
+#pragma unroll
+              for (int ct = 0; ct < NC; ++ct) {
+                rbh[ct] = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
+                rbl[ct] = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
+              }
+            }
+#pragma unroll
+            for (int ct = 0; ct < NC; ++ct)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                acc[i][ct] = mfma16_f16(bl[ct], a[i], acc[i][ct]);
+                acc[i][ct] = mfma16_f16(bh[ct], a[i], acc[i][ct]);
+              }
+            __builtin_amdgcn_sched_barrier(0);         // this k-step's MFMAs + the next one's reads in flight
+          }
+        } else {
 #pragma unroll
         for (int kk = 0; kk < NK; ++kk) {                // k-step kk = kernel row kh
           s8v a[4];
@@ -639,6 +681,7 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
             }
           }
           __builtin_amdgcn_sched_barrier(0);           // one k-step of LDS fragments live at a time
+        }
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -3225,6 +3268,7 @@ static int X3_FC_KS = 1;
 static int X3_FC_MMV = 3;
 static int X3_WG3_TILE = 1;
 static int X3_FWD_TILE = 1;
+static int X3_C1_PIPE = 0;     // band forward: 1 = next k-step's LDS fragments read during this k-step's MFMAs
 static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
@@ -3239,6 +3283,7 @@ void fast_conv_set_x3_fc_mmv(int v) { X3_FC_MMV = v; }
 void fast_conv_set_x3_fc_dg_gemm(int v) { X3_FC_DG_GEMM = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
 void fast_conv_set_x3_c1_band(int v) { X3_C1_BAND = v; }
+void fast_conv_set_x3_c1_pipe(int v) { X3_C1_PIPE = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
@@ -3259,9 +3304,14 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
       const long nbands = (long)T * E * BD1<C1>::NB;
       long bpw = (nbands * P + 511) / 512;                 // ~2 workgroups per CU over the launch
       if (bpw < 2) bpw = 2;
-      conv1_fwd_band_x2<C1><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
-          (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac,
-          layer, L, M, P, E, T, t0, br, (int)bpw, isc, os);
+      if (X3_C1_PIPE)
+        conv1_fwd_band_x2<C1, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+            (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac,
+            layer, L, M, P, E, T, t0, br, (int)bpw, isc, os);
+      else
+        conv1_fwd_band_x2<C1><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+            (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac,
+            layer, L, M, P, E, T, t0, br, (int)bpw, isc, os);
       const int rc = (int)hipGetLastError();
       return rc ? -rc : 1;
     }
@@ -3327,9 +3377,14 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
   const long nbands = (long)T * E * BD1<C1>::NB;
   long bpw = (nbands * P + 511) / 512;
   if (bpw < 2) bpw = 2;
-  conv1_fwd_band_x2<C1, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
-      (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
-      ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+  if (X3_C1_PIPE)
+    conv1_fwd_band_x2<C1, true, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+        (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+  else
+    conv1_fwd_band_x2<C1, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+        (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
