@@ -560,8 +560,10 @@ class HipEngine:
         if self.ga_dev is not None:
             self._ga_body()
         if self.ring:
-            src = self.frames[:, self.T:self.T + 4]
-            self.frames[:, 0:4].copy_(src if self.T >= 4 else src.clone())   # T < 4: the slot ranges overlap
+            # through an int64 view: 8 bytes per element (the uint8 strided copy ran at ~3.4 TB/s, 92 us per update)
+            f64 = self.frames.view(torch.int64) if self.HW % 8 == 0 else self.frames
+            src = f64[:, self.T:self.T + 4]
+            f64[:, 0:4].copy_(src if self.T >= 4 else src.clone())   # T < 4: the slot ranges overlap
             self.fc[0].copy_(self.fc[self.T])
         self.ctr.add_(1)
 
