@@ -887,7 +887,9 @@ struct FT3 {
   static_assert(G::CIN == 8 && !G::U8 && G::IN_ELEMS % 8 == 0, "8-channel fp16-pair input");
 };
 
-template <class G>
+// PAIR: a wave computes two position tiles (rt, rt + 4) per weight-fragment read (one tile per read left the
+// kernel bound by LDS reads, as the first conv1 band kernel was)
+template <class G, bool PAIR = false>
 __global__ __launch_bounds__(256, 2) void conv_fwd_tile_x3(const uint16_t* __restrict__ X, long xlo,
                                                           uint16_t* __restrict__ Y, long ylo,
                                                           uint8_t* __restrict__ bits, const uint16_t* __restrict__ Wc,
@@ -970,6 +972,49 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tile_x3(const uint16_t* __res
         __syncthreads();
         if (s + 1 < s_end) load_sample(s + 1);
         const long growb = sample_global(p, s, E, PE, t0) * G::HOWO;
+        if constexpr (PAIR) {
+#pragma unroll 1
+          for (int rt = w; rt < F::NRT; rt += 8) {                  // tiles rt and rt + 4 (wave-uniform)
+            int poff[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int pos = (rt + 4 * h) * 16 + c16;
+              const int oh = pos / G::WO, ow = pos - (pos / G::WO) * G::WO;
+              poff[h] = pos < G::HOWO ? (oh * G::S * G::WIN + ow * G::S) * 8 : -1;
+            }
+            f4v acc[2][NC];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int ct = 0; ct < NC; ++ct) acc[h][ct] = (f4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < F::NK; ++kk) {
+              s8v ph[2], pl[2];
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const int a = (poff[h] < 0 || koffs[kk] < 0) ? G::IN_ELEMS : poff[h] + koffs[kk];
+                ph[h] = *reinterpret_cast<const s8v*>(&Xt[0][a]);
+                pl[h] = *reinterpret_cast<const s8v*>(&Xt[1][a]);
+              }
+              const int kc = kk * 4 + grp;
+#pragma unroll
+              for (int ct = 0; ct < NC; ++ct) {
+                const s8v bh = *reinterpret_cast<const s8v*>(Ws[0] + (ct * 16 + c16) * KPs + kc * 8);
+                const s8v bl = *reinterpret_cast<const s8v*>(Ws[1] + (ct * 16 + c16) * KPs + kc * 8);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) acc[h][ct] = mma3h_t(ph[h], pl[h], bh, bl, acc[h][ct]);
+              }
+              __builtin_amdgcn_sched_barrier(0);       // one k-step of fragments live at a time
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int pos = (rt + 4 * h) * 16 + c16;
+              conv_epi_sw<NC>(acc[h], bias_s, ct0, cnt, q, in_scale, out_scale, growb + pos, bits, bits_rows, Y, ylo,
+                              pass > 0, pos < G::HOWO);
+            }
+          }
+          continue;
+        }
 #pragma unroll 1
         for (int rt = w; rt < F::NRT; rt += 4) {                    // wave-uniform
           int poff;
@@ -3267,7 +3312,10 @@ static int X3_FC_KS = 1;
 // (pre-activation planes; bias, ReLU, bits and the slot sum in fc_slot_sum2_x3)
 static int X3_FC_MMV = 3;
 static int X3_WG3_TILE = 1;
-static int X3_FWD_TILE = 1;
+// conv2/3 forward: 1 = one position tile per weight read, 2 = two (PAIR), 3 = two for the 4x4/s2 layer only (234
+// output positions; the 3x3 layer's 176 leave paired waves idle).  Measured (kwin_x3_v24*.md, v25*.md): 4x4/s2
+// 25.3 us paired vs 26.0-26.2 single (32.5-32.7 in slow runs), 3x3 18.4-18.8 paired vs 15.9-16.2 single
+static int X3_FWD_TILE = 3;
 static int X3_C1_PIPE = 0;     // band forward: 1 = next k-step's LDS fragments read during this k-step's MFMAs
 static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
@@ -3341,9 +3389,14 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
       const long nsamp = (long)T * E;                                                                             \
       long spw = (nsamp * P + 511) / 512;                                                                         \
       if (spw < 2) spw = 2;                                                                                       \
-      conv_fwd_tile_x3<Gx><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), 256, 0, st>>>(                         \
-          (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \
-          chunk, ai, ac, layer, L, M, P, E, T, t0, br, (int)spw, isc, os);                                        \
+      if (X3_FWD_TILE == 2 || (X3_FWD_TILE == 3 && Gx::HOWO > 200))                                              \
+        conv_fwd_tile_x3<Gx, true><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), 256, 0, st>>>(                 \
+            (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,   \
+            chunk, ai, ac, layer, L, M, P, E, T, t0, br, (int)spw, isc, os);                                      \
+      else                                                                                                        \
+        conv_fwd_tile_x3<Gx><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), 256, 0, st>>>(                       \
+            (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,   \
+            chunk, ai, ac, layer, L, M, P, E, T, t0, br, (int)spw, isc, os);                                      \
     } else if (X3_FWD_DB)                                                                                         \
       conv_fwd_x3<Gx, 4, 2, true, false><<<grid, 256, 0, st>>>(                                                   \
           (const uint16_t*)X, xlo, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off,     \

@@ -266,7 +266,7 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
         assert same > 0.999, (l, same)
 
 
-@pytest.mark.parametrize("arm", ["swapped", "tile", "band", "band_pipe"])
+@pytest.mark.parametrize("arm", ["swapped", "tile", "tile_pair", "band", "band_pipe"])
 @pytest.mark.parametrize("T", [1, 2])
 def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T, arm):
     """conv_epi_sw (weights as the MFMA A operand: one xor-32 module-pair sum, nibble ReLU bits, 8-byte stores; the
@@ -285,7 +285,11 @@ def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T, arm):
     lib = _lib.lib()
     outs = []
     for sw in (0, 3):
-        if arm == "band_pipe":       # conv1 band: next k-step's LDS fragments in flight vs one k-step at a time
+        if arm == "tile_pair":       # conv2/3 tile: two position tiles per weight-fragment read vs one
+            lib.fast_conv_set_x3_fwd_sw(1)
+            lib.fast_conv_set_x3_c1_band(1)
+            lib.fast_conv_set_x3_fwd_tile(2 if sw else 1)
+        elif arm == "band_pipe":     # conv1 band: next k-step's LDS fragments in flight vs one k-step at a time
             lib.fast_conv_set_x3_fwd_sw(1)
             lib.fast_conv_set_x3_fwd_tile(1)
             lib.fast_conv_set_x3_c1_band(1)
@@ -315,12 +319,12 @@ def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T, arm):
         torch.cuda.synchronize()
         outs.append(([x2_value(a) for a in acts], [b.clone() for b in bits]))
     lib.fast_conv_set_x3_fwd_sw(1)
-    lib.fast_conv_set_x3_fwd_tile(1)
+    lib.fast_conv_set_x3_fwd_tile(3)         # the default: paired tiles for conv2, single for conv3
     lib.fast_conv_set_x3_c1_band(1)
     lib.fast_conv_set_x3_c1_pipe(0)
     for l in range(3):
         a, b = outs[0][0][l], outs[1][0][l]
-        if arm == "band_pipe":       # the same products in the same order
+        if arm in ("band_pipe", "tile_pair"):   # the same products in the same order
             assert torch.equal(a, b) and torch.equal(outs[0][1][l], outs[1][1][l]), l
         e = rel(b, a)
         same = (outs[0][1][l] == outs[1][1][l]).float().mean().item()
