@@ -332,18 +332,21 @@ __global__ __launch_bounds__(256) void a2c_grad_kernel(
 // part == nullptr: the row-chunk partials meet in grad with fp32 atomics.  Deterministic mode: chunk c writes
 // its partials to part[c][F*A + F + A + 1] (dWp, dWv, dbp, dbv) and heads_reduce_kernel sums the chunks in order.
 #define HB_ROWS 128
-template <int AM, typename FT>
+// atomic (non-deterministic) mode, heads_set_bwd_rows(32): 32-row chunks (1 280 workgroups at T*B = 40 960 instead of 320: each thread's
+// serial row loop of dependent loads is 4x shorter and ~5 workgroups share a CU)
+static int HB_ROWS_ATOMIC = HB_ROWS;     // 32 via heads_set_bwd_rows (not yet measured on the GPU)
+template <int AM, typename FT, int ROWS = HB_ROWS>
 __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const FT* __restrict__ feat, int F, const float* __restrict__ dlogits, const float* __restrict__ dvalue,
     int N, int A, const float* __restrict__ flat, long pw, long pb, long vw, long vb, float* __restrict__ grad,
     float* __restrict__ dfeat, float* __restrict__ part) {
   const long PS = (long)F * A + F + A + 1;
   float* pc = part ? part + blockIdx.x * PS : nullptr;
-  const long r0 = (long)blockIdx.x * HB_ROWS;
-  const long r1 = min((long)N, r0 + HB_ROWS);
+  const long r0 = (long)blockIdx.x * ROWS;
+  const long r1 = min((long)N, r0 + ROWS);
   // the chunk's dlogits / dvalue rows, staged once (coalesced) and read as LDS broadcasts: per-row uniform
   // global loads put one memory latency on every row of the serial row loop (138 us per update at T*B = 40960)
-  __shared__ float dzs[HB_ROWS][AM + 1];
+  __shared__ float dzs[ROWS][AM + 1];
   const int nr = (int)(r1 - r0);
   for (int i = threadIdx.x; i < nr * (AM + 1); i += 256) {
     const int rr = i / (AM + 1), j = i - rr * (AM + 1);
@@ -483,6 +486,16 @@ static int heads_bwd_launch(const void* feat, int F, const float* dlogits, const
                             const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
                             float* part, hipStream_t stream) {
   if (A > AMAX) return -1;
+  if (!part && HB_ROWS_ATOMIC == 32) {
+    const int nc = (N + 31) / 32;
+    if (A <= 8)
+      heads_bwd_kernel<8, FT, 32><<<nc, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw,
+                                                          vb, grad, dfeat, nullptr);
+    else
+      heads_bwd_kernel<AMAX, FT, 32><<<nc, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb,
+                                                             vw, vb, grad, dfeat, nullptr);
+    return (int)hipGetLastError();
+  }
   const int nchunk = (N + HB_ROWS - 1) / HB_ROWS;
   if (A <= 8)
     heads_bwd_kernel<8, FT><<<nchunk, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw,
@@ -513,6 +526,8 @@ int launch_heads_bwd_f32(const void* feat, int F, const float* dlogits, const fl
   return heads_bwd_launch<float>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, nullptr,
                                  stream);
 }
+
+extern "C" void heads_set_bwd_rows(int r) { HB_ROWS_ATOMIC = r == 32 ? 32 : HB_ROWS; }
 
 // deterministic heads backward (fixed-order chunk reduction); part: ceil(N/128) * (F*A + F + A + 1) floats
 long heads_bwd_part_numel(int N, int F, int A) {

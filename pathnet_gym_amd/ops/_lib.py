@@ -144,6 +144,7 @@ _SIGS = {
     "fast_conv_set_x3_c1_band": [c_int],
     "fast_conv_set_x3_c1_pipe": [c_int],
     "heads_set_s16": [c_int],
+    "heads_set_bwd_rows": [c_int],
     "fast_conv_set_x3_fc_d": [c_int],
     "fast_conv_set_x3_fc_ks": [c_int],
     "fast_conv_set_x3_wgrad_pf": [c_int],
