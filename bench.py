@@ -17,11 +17,25 @@ unit as the reference's 63 global steps/s (BASELINE.md, aliencentipede.txt);
 the synthetic Pong repeats each action for `frameskip`=4 emulator sub-frames
 that are NOT counted.  Weak scaling: P paths per GPU, fixed.
 
-Precision: the headline runs the fp32x engine (``--dtype fp32x``, reported as
-"dtype": "fp32"): the reference trains in fp32 (game_ac_network.py:89-110) and
-fp32x matches a plain fp32 oracle to <= 2e-5 per layer (fp16 / bf16 hi+lo
-operand pairs, three MFMAs per product, csrc/trunk_x3.hip).  The bf16 engine
-is timed on the same config as ``value_bf16``.
+Precision: the headline runs the fp32x engine (``--dtype fp32x``, reported as "dtype": "fp32x" with the
+bound "max_rel_err_per_layer": 2e-5): the reference trains in fp32 (game_ac_network.py:89-110) and fp32x
+matches a plain fp32 PyTorch oracle to <= 2e-5 per layer (fp16 / bf16 hi+lo operand pairs, three MFMAs per
+product, csrc/trunk_x3.hip; tests/test_x3_engine.py).  The bf16 engine is timed on the same config as
+``value_bf16``.
+
+Timing: after W warmup updates, ``--windows`` (default 3) back-to-back windows of EXACTLY K updates, each
+bracketed by barrier + synchronize; every window's time is the max over ranks; the reported time is the
+median window (``windows_ms_per_step`` lists all of them, ``spread_pct`` = (max - min) / median).
+
+Strong scaling (the half of the metric that frames/s cannot show): the default run is weak scaling, P paths
+per GPU.  ``strong_scaling`` additionally times the FIXED 64-path population split over the N ranks
+(TrainConfig.paths_total: 64 / N paths per GPU, the same GA over P_total and the same summed gradient, env and
+sampling RNG keyed by the global env index -- tests/test_distributed.py shows 4 ranks reproduce one process),
+i.e. the per-update latency that divides the wall time of a solve (solves take 20-34 K updates whatever the
+frame count, profiles/solve/README.md).  It reports the predicted seconds to solve (committed updates-to-solve
+x measured ms/update; labelled a prediction) and, on more than one GPU, one in-run strong-mode solve under a
+wall cap (the stop decision is collective, so ranks never disagree).  ``--scaling strong`` makes the strong
+config the headline instead.
 
 Steady state: every env's first episode starts at a random late score
 (PongVec.stagger_scores), so fitness windows fill and tournaments fire inside
@@ -39,6 +53,7 @@ import argparse
 import json
 import math
 import os
+import statistics
 import sys
 import time
 
@@ -91,7 +106,8 @@ def solve_records(key: dict, n_gpus: int):
             "solved_seeds": len(gens), "seeds": len(runs), "runs": runs, "config": key}
 
 
-def build_trainer(args, ctx, dtype: str, stagger: bool):
+def build_trainer(args, ctx, dtype: str, stagger: bool, paths_total: int = 0):
+    """The bench trainer; ``paths_total`` > 0: strong scaling (that population split over the ranks)."""
     from pathnet_gym_amd.config import preset
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     cfg = preset(args.preset)
@@ -99,6 +115,7 @@ def build_trainer(args, ctx, dtype: str, stagger: bool):
         cfg.env = args.env
         cfg.tasks = [args.env] + [t for t in cfg.tasks if t != args.env]
     cfg.paths = args.paths
+    cfg.paths_total = paths_total
     cfg.envs_per_path = args.envs
     cfg.a2c.t_max = args.tmax
     cfg.backend = args.backend
@@ -106,7 +123,10 @@ def build_trainer(args, ctx, dtype: str, stagger: bool):
     # fp32x: the first layer reads the frame ring (env 70 -> 39 us per step; conv1 forward / weight gradient +6 % /
     # +7 %; window 11.42 -> 11.15 ms, profiles/r3/kwin_x3_v19*.md); bf16 keeps packed stacks (a wash there, docs/PERF.md)
     cfg.frame_ring = args.ring or (dtype == "fp32x" and not args.packed)
-    cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
+    # concurrent tournaments: paths/16 of the population one GA sees per update -- per rank in weak scaling (the GA
+    # takes the same number of tournaments per update on 1, 2, 4 and 8 GPUs), of P_total in strong scaling (exactly
+    # the one-GPU GA)
+    cfg.ga.concurrent_tournaments = args.concurrent or max(1, (paths_total or cfg.paths) // 16)
     cfg.ga.backend = args.ga_backend
     cfg.compute_dtype = dtype
     cfg.deterministic = args.deterministic
@@ -117,8 +137,9 @@ def build_trainer(args, ctx, dtype: str, stagger: bool):
     return cfg, tr
 
 
-def timed_window(tr, ctx, steps: int, warmup: int, markers: bool = False):
-    """W untimed updates, then EXACTLY K updates between barrier + synchronize on both sides; max over ranks."""
+def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: bool = False):
+    """W untimed updates, then ``windows`` back-to-back windows of EXACTLY K updates, each between barrier +
+    synchronize on both sides; a window's time is the max over ranks.  Returns [(seconds, frames, generations)]."""
     import torch
 
     def sync():
@@ -131,51 +152,73 @@ def timed_window(tr, ctx, steps: int, warmup: int, markers: bool = False):
     for _ in range(warmup):
         tr.update()
     tr.flush()
-    sync()
-    gen0 = tr.pop.generation
-    step0 = tr.global_step
-    if markers:
-        from pathnet_gym_amd.ops import _lib as _plib
-        _plib.call("launch_prof_marker", 1, _plib.stream())
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        tr.update()
-    tr.flush()                               # drain the pipelined host bookkeeping of the last update
-    if markers:
-        _plib.call("launch_prof_marker", 2, _plib.stream())
-    sync()
-    dt = ctx.max_scalar(time.perf_counter() - t0)
-    return dt, tr.global_step - step0, tr.pop.generation - gen0   # whole-job agent steps (fused all-reduce)
+    out = []
+    for w in range(windows):
+        sync()
+        gen0 = tr.pop.generation
+        step0 = tr.global_step
+        if markers and w == 0:
+            from pathnet_gym_amd.ops import _lib as _plib
+            _plib.call("launch_prof_marker", 1, _plib.stream())
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tr.update()
+        tr.flush()                               # drain the pipelined host bookkeeping of the last update
+        if markers and w == 0:
+            _plib.call("launch_prof_marker", 2, _plib.stream())
+        sync()
+        dt = ctx.max_scalar(time.perf_counter() - t0)
+        out.append((dt, tr.global_step - step0, tr.pop.generation - gen0))   # whole-job agent steps
+    return out
 
 
-def in_run_solve(args, ctx, dtype: str, cap_s: float) -> dict:
+def window_summary(wins, steps: int) -> dict:
+    ms = [w[0] / steps * 1e3 for w in wins]
+    med = statistics.median(ms)
+    return {"ms": med, "all": [round(x, 3) for x in ms],
+            "spread_pct": round((max(ms) - min(ms)) / med * 100.0, 2) if med > 0 else 0.0,
+            "frames": wins[0][1], "generations": sum(w[2] for w in wins)}
+
+
+def in_run_solve(args, ctx, dtype: str, cap_s: float, paths_total: int = 0) -> dict:
     """One seed of generations-to-solve on a FRESH trainer of the bench config, observed inside this run (hard wall
     cap; scripts/solve.py is the multi-seed version): the first tournament whose winner fitness reaches the task's
-    reward threshold."""
+    reward threshold.  Every rank takes the same decisions: the GA state (hence "solved") is replicated, and the
+    wall cap is checked every 64 updates on the max over ranks of the elapsed time."""
     from pathnet_gym_amd.envs.registry import reward_threshold
-    cfg, tr = build_trainer(args, ctx, dtype, stagger=False)
+    cfg, tr = build_trainer(args, ctx, dtype, stagger=False, paths_total=paths_total)
     thr = reward_threshold(cfg.tasks[0])
     t0 = time.time()
     last = t0
     best = -math.inf
-    out = {"seed": cfg.seed, "threshold": thr, "cap_s": cap_s, "solved": False}
-    while time.time() - t0 < cap_s:
+    out = {"seed": cfg.seed, "threshold": thr, "cap_s": round(cap_s, 1), "solved": False,
+           "paths_per_gpu": cfg.paths, "paths_total": tr.P_total}
+    while True:
         st = tr.update()
         now = time.time()
         if now - last > 30 and ctx.is_main:      # progress on stderr (the JSON line stays the only stdout line)
             last = now
             print(f"[bench] solve t={now - t0:.0f}s generation={tr.pop.generation} frames={tr.global_step} "
-                  f"best_winner={best:.2f}", file=sys.stderr, flush=True)
+                  f"updates={tr.updates} best_winner={best:.2f}", file=sys.stderr, flush=True)
         if st.tournaments:
             best = max(best, st.best_winner)
             if st.best_winner >= thr:
-                out.update(solved=True, generations=tr.pop.generation, frames=tr.global_step,
+                out.update(solved=True, generations=tr.pop.generation, frames=tr.global_step, updates=tr.updates,
                            seconds=round(time.time() - t0, 1))
                 break
+        if tr.updates % 64 == 0 and ctx.max_scalar(time.time() - t0) >= cap_s:
+            break
     tr.flush()
     out.update(best_winner=best if best > -math.inf else None, generations_run=tr.pop.generation,
-               frames_run=tr.global_step, wall_s=round(time.time() - t0, 1))
+               frames_run=tr.global_step, updates_run=tr.updates, wall_s=round(time.time() - t0, 1))
     return out
+
+
+def committed_updates_to_solve(key: dict) -> list:
+    """Optimizer updates each committed solved seed of the one-GPU bench config needed (frames / frames per update)."""
+    rec = solve_records(key, 1)
+    per_update = key["paths_per_gpu"] * key["envs_per_path"] * key["t_max"]
+    return sorted(int(round(r["frames"] / per_update)) for r in rec.get("runs", []) if r["solved"] and r["frames"])
 
 
 def main():
@@ -183,7 +226,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--paths", type=int, default=64, help="paths per GPU")
+    ap.add_argument("--windows", type=int, default=3, help="timed windows of --steps updates (median reported)")
+    ap.add_argument("--paths", type=int, default=64, help="paths per GPU (weak scaling)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="headline: weak (--paths per GPU) or strong (--paths-total split over the GPUs)")
+    ap.add_argument("--paths-total", type=int, default=64,
+                    help="strong scaling: the fixed population split over the GPUs (the one-GPU bench population)")
     ap.add_argument("--envs", type=int, default=32, help="envs per path (multiple of 16)")
     ap.add_argument("--tmax", type=int, default=20)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
@@ -204,18 +252,19 @@ def main():
     ap.add_argument("--ga-backend", default="device", choices=["device", "host"],
                     help="device: GA kernels inside the update graph + pipelined host bookkeeping")
     ap.add_argument("--concurrent", type=int, default=None,
-                    help="concurrent tournaments (default paths/16 -- per rank count, NOT scaled by the world size, so "
-                         "the GA takes the same number of tournaments per update on 1, 2, 4 and 8 GPUs)")
+                    help="concurrent tournaments (default: paths/16 -- per rank in weak scaling, so the GA takes the "
+                         "same number of tournaments per update on 1, 2, 4 and 8 GPUs; of P_total in strong scaling)")
     ap.add_argument("--no-stagger", action="store_true",
                     help="start every env at 0-0 (default: random late scores, so tournaments fire inside the window)")
     ap.add_argument("--solve-seconds", type=float, default=None,
-                    help="after the timed window, run one generations-to-solve seed on a fresh trainer for at most "
-                         "this long (default: up to 420 s on one GPU, within a 540 s total; 0 = off; multi-GPU "
-                         "runs skip it)")
+                    help="after the timed windows, run one generations-to-solve seed on a fresh trainer for at most "
+                         "this long (default: what is left of a 540 s budget, at most 420 s; on one GPU the bench "
+                         "config, on several the strong-scaling config; 0 = off)")
     ap.add_argument("--compare-bf16", type=int, default=None,
                     help="also time the bf16 engine on the same config (default: on for one GPU)")
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling windows on several GPUs")
     ap.add_argument("--prof-window", action="store_true",
-                    help="launch marker kernels around the timed updates (scripts/prof_window.py summarises the "
+                    help="launch marker kernels around the first timed window (scripts/prof_window.py summarises the "
                          "rocprofv3 kernel trace between them)")
     args = ap.parse_args()
     t_start = time.time()
@@ -224,9 +273,10 @@ def main():
 
     from pathnet_gym_amd.parallel.dist import init_distributed
 
+    build_info = None
     if args.backend == "hip":
         from pathnet_gym_amd import _build
-        _build.build()
+        build_info = _build.build_info(_build.build())
 
     if args.kernel_opt:
         from pathnet_gym_amd.ops import _lib
@@ -235,32 +285,40 @@ def main():
             lib = _lib.lib()
             (getattr(lib, k) if hasattr(lib, k) and "_set_" in k else getattr(lib, "fast_conv_set_" + k))(int(v))
     ctx = init_distributed()
-    single = ctx.world == 1 and not args.prof_window
-    # the in-run solve may use what is left of a ~540 s budget (the driver allows 600 s for the whole bench; a fresh
-    # box can spend a minute or two importing torch), at most 420 s
-    solve_s = args.solve_seconds if args.solve_seconds is not None else (420.0 if single else 0.0)
+    world = ctx.world
+    single = world == 1 and not args.prof_window
+    if args.scaling == "strong" and args.paths_total % world:
+        raise SystemExit(f"--paths-total {args.paths_total} is not divisible by {world} GPUs")
+    head_total = args.paths_total if args.scaling == "strong" else 0
     compare = args.compare_bf16 if args.compare_bf16 is not None else int(single and args.dtype != "bf16")
     stagger = not args.no_stagger
-    cfg, tr = build_trainer(args, ctx, args.dtype, stagger)
-    dt, frames, gens = timed_window(tr, ctx, args.steps, args.warmup, markers=args.prof_window)
-    value = frames / dt
+    cfg, tr = build_trainer(args, ctx, args.dtype, stagger, paths_total=head_total)
+    wins = timed_windows(tr, ctx, args.steps, args.warmup, args.windows, markers=args.prof_window)
+    ws = window_summary(wins, args.steps)
+    dt = ws["ms"] * args.steps / 1e3
+    value = ws["frames"] / dt
+    x3 = tr.compute_dtype == "fp32x"
     rec = {
         "metric": "env_frames_per_sec_whole_node_pong_pathnet",
         "value": round(value, 1),
         "unit": "env frames/s (agent steps, all GPUs)",
-        "n_gpus": ctx.world,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "ms_per_step": round(ws["ms"], 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": round(value / BASELINE_STEPS_PER_SEC, 1),
-        "dtype": "fp32" if tr.compute_dtype == "fp32x" else tr.compute_dtype,
+        "dtype": tr.compute_dtype,
         "compute": {"fp32x": "fp32-accurate split operands: fp16 hi+lo pairs (forward), bf16 hi+lo pairs (gradients), "
                              "3 MFMAs per product, fp32 accumulation and master weights; <= 2e-5 relative per layer "
                              "vs a plain fp32 PyTorch oracle (tests/test_x3_engine.py)",
                     "fp32": "fp32 MFMA operands (v_mfma_f32_16x16x4_f32)",
                     "bf16": "bf16/fp16 MFMA operands, fp32 accumulation (reduced precision)"}[tr.compute_dtype],
+        "max_rel_err_per_layer": 2e-5 if x3 else (1e-5 if tr.compute_dtype == "fp32" else None),
+        "windows": args.windows,
+        "windows_ms_per_step": ws["all"],
+        "spread_pct": ws["spread_pct"],
         "data": (f"synthetic: on-device Atari-style {cfg.tasks[0]} simulator (210x160 RGB -> gray 160x120 x4 "
                  "stack), random-init weights") if len(cfg.net.input_shape) == 3 else
                 f"synthetic: on-device {cfg.tasks[0]}, random-init weights",
@@ -270,9 +328,10 @@ def main():
                                                              if sp.kind == "conv" else "")
                                   for sp in cfg.net.layers)
                      + f") x M={cfg.net.M} modules, N={cfg.net.N}, A2C T={cfg.a2c.t_max}, B={cfg.ga.B} tournament",
-            "global_batch": cfg.paths * cfg.envs_per_path * ctx.world * cfg.a2c.t_max,
+            "global_batch": cfg.paths * cfg.envs_per_path * world * cfg.a2c.t_max,
             "seq_len": cfg.a2c.t_max,
-            "parallelism": f"dp{ctx.world} (population split: {cfg.paths} paths x {cfg.envs_per_path} envs per GPU)",
+            "parallelism": f"dp{world} (population split: {cfg.paths} paths x {cfg.envs_per_path} envs per GPU"
+                           + (f", {tr.P_total} paths in total)" if head_total else ")"),
             "backend": args.backend,
             "hipgraph": cfg.use_graph,
             "frame_ring": bool(getattr(tr.engine, "ring", False)),
@@ -280,27 +339,64 @@ def main():
             "ga": f"{cfg.ga.backend} (B={cfg.ga.B}, {cfg.ga.concurrent_tournaments} concurrent tournaments, "
                   f"fitness {cfg.ga.fitness} over {cfg.ga.window_for(cfg.envs_per_path)} episodes)",
             "pipelined": bool(tr.pipelined),
+            "overlap_allreduce": bool(getattr(tr.engine, "split", False)),
             "deterministic": bool(getattr(tr.model.hip, "deterministic", False)),
             "episode_stagger": stagger,
         },
-        "generations_in_timed_window": int(gens),
+        "generations_in_timed_window": int(wins[0][2]),
+        "generations_in_timed_windows": int(ws["generations"]),
     }
+    if build_info is not None:
+        rec["build"] = build_info
     del tr
     if compare:
-        _, trb = build_trainer(args, ctx, "bf16", stagger)
-        dtb, fb, _ = timed_window(trb, ctx, args.steps, args.warmup)
-        rec["value_bf16"] = round(fb / dtb, 1)
-        rec["ms_per_step_bf16"] = round(dtb / args.steps * 1e3, 3)
+        _, trb = build_trainer(args, ctx, "bf16", stagger, paths_total=head_total)
+        wb = window_summary(timed_windows(trb, ctx, args.steps, args.warmup, args.windows), args.steps)
+        rec["value_bf16"] = round(wb["frames"] / (wb["ms"] * args.steps / 1e3), 1)
+        rec["ms_per_step_bf16"] = round(wb["ms"], 3)
+        rec["windows_ms_per_step_bf16"] = wb["all"]
         del trb
     torch.cuda.empty_cache() if torch.cuda.is_available() else None
-    # the metric's second half: one seed observed in this run, plus every committed multi-seed record of exactly
-    # this config (scripts/solve.py --out profiles/solve/*.json)
-    if solve_s > 0 and args.solve_seconds is None:
-        solve_s = max(0.0, min(solve_s, 540.0 - (time.time() - t_start)))
+    # strong scaling: the one-GPU population (64 paths) split over the ranks
+    key = solve_key(cfg, args.preset)
+    key1 = dict(key, paths_per_gpu=args.paths_total, concurrent_tournaments=max(1, args.paths_total // 16))
+    upd = committed_updates_to_solve(key1)
+    strong = None
+    if args.scaling == "strong" or (world == 1 and args.paths == args.paths_total):
+        strong = {"ms_per_update": round(ws["ms"], 3), "windows_ms": ws["all"], "same_as_headline": True}
+    elif not args.no_strong and args.paths_total % world == 0:
+        _, trs = build_trainer(args, ctx, args.dtype, stagger, paths_total=args.paths_total)
+        wst = window_summary(timed_windows(trs, ctx, args.steps, args.warmup, args.windows), args.steps)
+        strong = {"ms_per_update": round(wst["ms"], 3), "windows_ms": wst["all"], "spread_pct": wst["spread_pct"],
+                  "frames_per_sec": round(wst["frames"] / (wst["ms"] * args.steps / 1e3), 1)}
+        del trs
+        torch.cuda.empty_cache() if torch.cuda.is_available() else None
+    if strong is not None:
+        strong.update(paths_total=args.paths_total, paths_per_gpu=args.paths_total // world,
+                      envs_per_path=args.envs, n_gpus=world)
+        if upd:
+            med = upd[len(upd) // 2]
+            strong["committed_updates_to_solve_1gpu"] = upd
+            strong["predicted_seconds_to_solve"] = round(med * strong["ms_per_update"] / 1e3, 1)
+            strong["prediction"] = ("median committed one-GPU updates-to-solve of this config x the measured strong-"
+                                    "scaling ms/update (the strong run computes the one-GPU run's GA and summed "
+                                    "gradient, so it needs the same updates); a prediction, not a measured solve")
+        rec["strong_scaling"] = strong
+    # the metric's second half: one seed observed in this run (one GPU: the bench config; several GPUs: the strong
+    # config, whose updates are what more GPUs shorten), plus every committed multi-seed record of this config
+    solve_s = args.solve_seconds
+    if solve_s is None:
+        solve_s = 420.0 if (single or (world > 1 and strong is not None)) else 0.0
+        solve_s = max(0.0, min(solve_s, 540.0 - ctx.max_scalar(time.time() - t_start)))
     if solve_s > 0:
-        rec["generations_to_solve_in_run"] = in_run_solve(args, ctx, args.dtype, solve_s)
+        strong_solve = world > 1 and args.scaling == "weak"
+        r = in_run_solve(args, ctx, args.dtype, solve_s, paths_total=args.paths_total if strong_solve else head_total)
+        if strong_solve:
+            rec["strong_scaling"]["in_run_solve"] = r
+        else:
+            rec["generations_to_solve_in_run"] = r
     if ctx.is_main:
-        rec["generations_to_solve"] = solve_records(solve_key(cfg, args.preset), ctx.world)
+        rec["generations_to_solve"] = solve_records(key, world)
         print(json.dumps(rec), flush=True)
     ctx.destroy()
 

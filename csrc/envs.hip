@@ -199,7 +199,10 @@ DEVI void physics_wave0(int env, int* __restrict__ state, uint32_t* __restrict__
                         int n_actions, uint32_t seed, int frameskip, int max_steps, int no_op_max, int* phys,
                         float* __restrict__ reward_out, uint8_t* __restrict__ done_out,
                         float* __restrict__ epret_out, const uint8_t* __restrict__ fc_in,
-                        uint8_t* __restrict__ fc_out) {
+                        uint8_t* __restrict__ fc_out, uint32_t id_base) {
+  // RNG identity of the env: its GLOBAL index (id_base = first env of this rank), so a population sharded over
+  // any number of ranks draws the same random streams as on one GPU
+  const uint32_t rid = id_base + (uint32_t)env;
   St st;
 #pragma unroll
   for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
@@ -208,14 +211,14 @@ DEVI void physics_wave0(int env, int* __restrict__ state, uint32_t* __restrict__
   if (a >= n_actions || a < 0) a = 0;                    // game_state.py:38-39
   const int up = (a == 2 || a == 4), down = (a == 3 || a == 5);
   int reward = 0;
-  for (int f = 0; f < frameskip; ++f) reward += subframe(st, up, down, seed, (uint32_t)env, ctr);
+  for (int f = 0; f < frameskip; ++f) reward += subframe(st, up, down, seed, rid, ctr);
   ctr += 1;
   st.s[STEPS] += 1;
   st.s[EPRET] += reward;
   const bool done = st.s[PS] >= WIN_SCORE || st.s[CS] >= WIN_SCORE || st.s[STEPS] >= max_steps;
   const int epret = st.s[EPRET];
   if (done) {
-    reset_state(st, seed, (uint32_t)env, ctr, no_op_max, frameskip);
+    reset_state(st, seed, rid, ctr, no_op_max, frameskip);
     ctr += 1;
   }
   if (threadIdx.x == 0) {
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
                                                         int g_player, int g_ball,
                                                         const uint8_t* __restrict__ fc_in = nullptr,
                                                         uint8_t* __restrict__ fc_out = nullptr,
-                                                        long out_stride = 0, int b0 = 0) {
+                                                        long out_stride = 0, int b0 = 0, uint32_t id_base = 0) {
   using namespace pong;
   __shared__ __attribute__((aligned(16))) int tab[8 * 160];
   const int env = b0 + blockIdx.x;
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   __shared__ int phys[NSTATE + 4];
   if (threadIdx.x < 64)
     physics_wave0(env, state, counter, actions, n_actions, seed, frameskip, max_steps, no_op_max, phys, reward_out,
-                  done_out, epret_out, RING ? fc_in : nullptr, fc_out);
+                  done_out, epret_out, RING ? fc_in : nullptr, fc_out, id_base);
   PONG_STAMP(1);
   __syncthreads();    // tab[] staged and the new state published
   PONG_STAMP(2);
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
 // ---------------------------------------------------------------------------
 __global__ void cartpole_step_kernel(float* __restrict__ state, int* __restrict__ steps, float* __restrict__ epret,
                                      uint32_t* __restrict__ counter, const int* __restrict__ actions, int B,
-                                     uint32_t seed, int max_steps, float* __restrict__ obs_f32,
+                                     uint32_t seed, uint32_t id_base, int max_steps, float* __restrict__ obs_f32,
                                      bf16_t* __restrict__ obs_bf16, float* __restrict__ reward_out,
                                      uint8_t* __restrict__ done_out, float* __restrict__ epret_out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -443,7 +446,7 @@ __global__ void cartpole_step_kernel(float* __restrict__ state, int* __restrict_
   epret_out[b] = done ? er : 0.f;
   if (done) {
     float u[4];
-    for (int s = 0; s < 4; ++s) u[s] = (float)(env_rand_u32(seed, (uint32_t)b, ctr, (uint32_t)s) >> 8) * (1.0f / 16777216.0f);
+    for (int s = 0; s < 4; ++s) u[s] = (float)(env_rand_u32(seed, id_base + (uint32_t)b, ctr, (uint32_t)s) >> 8) * (1.0f / 16777216.0f);
     x = u[0] * 0.1f - 0.05f; xd = u[1] * 0.1f - 0.05f; th = u[2] * 0.1f - 0.05f; thd = u[3] * 0.1f - 0.05f;
     ctr += 1;
   }
@@ -468,7 +471,7 @@ extern "C" {
 int launch_pong_step(void* state, void* counter, const int* actions, int n_actions, const void* obs_in, void* obs_out,
                      const int* tables, float* reward, void* done, float* epret, int B, unsigned seed, int frameskip,
                      int max_steps, int no_op_max, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
-                     int b0, hipStream_t stream) {
+                     int b0, unsigned id_base, hipStream_t stream) {
   if (n_actions <= 0 || B <= 0 || frameskip < 0 || max_steps < 0 || no_op_max < 0 || g_bg < 0 || g_wall < 0 ||
       g_cpu < 0 || g_player < 0 || g_ball < 0 || b0 < 0) return -22;
   // envs [b0, B): one path group of the split rollout (runtime/engine.py); per-env state and RNG keys are global
@@ -476,7 +479,8 @@ int launch_pong_step(void* state, void* counter, const int* actions, int n_actio
   pong_step_kernel<false><<<B - b0, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions,
                                                       (const uint32_t*)obs_in, (uint32_t*)obs_out, tables, reward,
                                                       (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max,
-                                                      g_bg, g_wall, g_cpu, g_player, g_ball, nullptr, nullptr, 0, b0);
+                                                      g_bg, g_wall, g_cpu, g_player, g_ball, nullptr, nullptr, 0, b0,
+                                                      id_base);
   return (int)hipGetLastError();
 }
 
@@ -485,23 +489,25 @@ int launch_pong_step(void* state, void* counter, const int* actions, int n_actio
 int launch_pong_step_ring(void* state, void* counter, const int* actions, int n_actions, void* frame_out,
                           long out_stride, const void* fc_in, void* fc_out, const int* tables, float* reward,
                           void* done, float* epret, int B, unsigned seed, int frameskip, int max_steps, int no_op_max,
-                          int g_bg, int g_wall, int g_cpu, int g_player, int g_ball, hipStream_t stream) {
+                          int g_bg, int g_wall, int g_cpu, int g_player, int g_ball, unsigned id_base,
+                          hipStream_t stream) {
   if (n_actions <= 0 || out_stride <= 0 || B <= 0 || frameskip < 0 || max_steps < 0 || no_op_max < 0 || g_bg < 0 ||
       g_wall < 0 || g_cpu < 0 || g_player < 0 || g_ball < 0) return -22;
   if (out_stride < 160 * 120 || out_stride % 16) return -22;
   pong_step_kernel<true><<<B, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions, nullptr,
                                                 (uint32_t*)frame_out, tables, reward, (uint8_t*)done, epret, seed,
                                                 frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu, g_player,
-                                                g_ball, (const uint8_t*)fc_in, (uint8_t*)fc_out, out_stride);
+                                                g_ball, (const uint8_t*)fc_in, (uint8_t*)fc_out, out_stride, 0,
+                                                id_base);
   return (int)hipGetLastError();
 }
 
 int launch_cartpole_step(float* state, int* steps, float* epret, void* counter, const int* actions, int B,
-                         unsigned seed, int max_steps, float* obs_f32, void* obs_bf16, float* reward, void* done,
-                         float* epret_out, hipStream_t stream) {
+                         unsigned seed, unsigned id_base, int max_steps, float* obs_f32, void* obs_bf16,
+                         float* reward, void* done, float* epret_out, hipStream_t stream) {
   if (B <= 0 || max_steps < 0) return -22;
   cartpole_step_kernel<<<(B + 255) / 256, 256, 0, stream>>>(state, steps, epret, (uint32_t*)counter, actions, B, seed,
-                                                            max_steps, obs_f32, (bf16_t*)obs_bf16, reward,
+                                                            id_base, max_steps, obs_f32, (bf16_t*)obs_bf16, reward,
                                                             (uint8_t*)done, epret_out);
   return (int)hipGetLastError();
 }

@@ -415,7 +415,7 @@ struct Centipede {
 template <class G>
 __global__ __launch_bounds__(64) void game_step_kernel(int* __restrict__ state, const int* __restrict__ actions,
                                                        const uint8_t* __restrict__ mask, int mode, int n_actions, int N,
-                                                       uint32_t seed, int frameskip, int max_steps,
+                                                       uint32_t seed, uint32_t id_base, int frameskip, int max_steps,
                                                        float* __restrict__ reward, uint8_t* __restrict__ done,
                                                        float* __restrict__ epret, int16_t* __restrict__ rects) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(64) void game_step_kernel(int* __restrict__ state, 
   int s[G::NS];
   int* row = state + (long)e * G::NS;
   for (int i = 0; i < G::NS; ++i) s[i] = row[i];
-  Rng g{seed, (uint32_t)e, (uint32_t)s[G::COUNTER]};
+  Rng g{seed, id_base + (uint32_t)e, (uint32_t)s[G::COUNTER]};   // RNG identity: the global env index
   if (mode == 0) {
     int a = actions[e];
     if (a >= n_actions || a < 0) a = 0;
@@ -455,9 +455,9 @@ __global__ __launch_bounds__(64) void game_step_kernel(int* __restrict__ state, 
 
 template <class G>
 static int launch(void* state, const void* actions, const void* mask, int mode, int n_actions, int N, uint32_t seed,
-                  int frameskip, int max_steps, void* reward, void* done, void* epret, void* rects, hipStream_t st) {
+                  uint32_t id_base, int frameskip, int max_steps, void* reward, void* done, void* epret, void* rects, hipStream_t st) {
   game_step_kernel<G><<<(N + 63) / 64, 64, 0, st>>>((int*)state, (const int*)actions, (const uint8_t*)mask, mode,
-                                                    n_actions, N, seed, frameskip, max_steps, (float*)reward,
+                                                    n_actions, N, seed, id_base, frameskip, max_steps, (float*)reward,
                                                     (uint8_t*)done, (float*)epret, (int16_t*)rects);
   return (int)hipGetLastError();
 }
@@ -478,15 +478,15 @@ extern "C" int game_layout(int game, int* ns, int* nrects) {
 }
 
 extern "C" int launch_game_step(int game, void* state, const void* actions, const void* mask, int mode, int n_actions,
-                                int N, uint32_t seed, int frameskip, int max_steps, void* reward, void* done,
+                                int N, uint32_t seed, uint32_t id_base, int frameskip, int max_steps, void* reward, void* done,
                                 void* epret, void* rects, hipStream_t st) {
   using namespace games;
   switch (game) {
-    case 0: return launch<Breakout>(state, actions, mask, mode, n_actions, N, seed, frameskip, max_steps, reward, done, epret, rects, st);
-    case 1: return launch<SpaceInvaders>(state, actions, mask, mode, n_actions, N, seed, frameskip, max_steps, reward, done, epret, rects, st);
-    case 2: return launch<Alien>(state, actions, mask, mode, n_actions, N, seed, frameskip, max_steps, reward, done, epret, rects, st);
-    case 3: return launch<MsPacman>(state, actions, mask, mode, n_actions, N, seed, frameskip, max_steps, reward, done, epret, rects, st);
-    case 4: return launch<Centipede>(state, actions, mask, mode, n_actions, N, seed, frameskip, max_steps, reward, done, epret, rects, st);
+    case 0: return launch<Breakout>(state, actions, mask, mode, n_actions, N, seed, id_base, frameskip, max_steps, reward, done, epret, rects, st);
+    case 1: return launch<SpaceInvaders>(state, actions, mask, mode, n_actions, N, seed, id_base, frameskip, max_steps, reward, done, epret, rects, st);
+    case 2: return launch<Alien>(state, actions, mask, mode, n_actions, N, seed, id_base, frameskip, max_steps, reward, done, epret, rects, st);
+    case 3: return launch<MsPacman>(state, actions, mask, mode, n_actions, N, seed, id_base, frameskip, max_steps, reward, done, epret, rects, st);
+    case 4: return launch<Centipede>(state, actions, mask, mode, n_actions, N, seed, id_base, frameskip, max_steps, reward, done, epret, rects, st);
   }
   return -1;
 }

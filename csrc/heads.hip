@@ -29,7 +29,7 @@ template <typename FT>
 __global__ __launch_bounds__(256) void heads_fwd_sample_kernel(
     const FT* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
     int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
-    const long long* __restrict__ ctr, int t, int T, int greedy, int b0) {
+    const long long* __restrict__ ctr, int t, int T, int greedy, int b0, uint32_t rb) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int b = b0 + blockIdx.x * 4 + w;
   if (b >= B) return;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void heads_fwd_sample_kernel(
       if (j < A) {
         logits[(long)b * A + j] = lg[j];
         float s = lg[j];
-        if (!greedy) s += -__logf(-__logf(u01(seed, stepkey, (uint32_t)b, (uint32_t)j)));
+        if (!greedy) s += -__logf(-__logf(u01(seed, stepkey, rb + (uint32_t)b, (uint32_t)j)));
         if (s > bv) { bv = s; best = j; }
       }
     }
@@ -90,7 +90,7 @@ template <int AM, typename FT>
 __global__ __launch_bounds__(256) void heads_fwd_lanes_kernel(
     const FT* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
     int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
-    const long long* __restrict__ ctr, int t, int T, int greedy, int b0) {
+    const long long* __restrict__ ctr, int t, int T, int greedy, int b0, uint32_t rb) {
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   constexpr int AW = AM + 1;
   float* Wl = hsm;                       // [F][AW]: policy weights (zero padded to AM) + value weight
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void heads_fwd_lanes_kernel(
       const float lg = acc[j] + flat[pb + j];
       logits[(long)b * A + j] = lg;
       float sc = lg;
-      if (!greedy) sc += -__logf(-__logf(u01(seed, stepkey, (uint32_t)b, (uint32_t)j)));
+      if (!greedy) sc += -__logf(-__logf(u01(seed, stepkey, rb + (uint32_t)b, (uint32_t)j)));
       if (sc > bv) { bv = sc; best = j; }
     }
   }
@@ -152,7 +152,7 @@ template <int AM, typename FT>
 __global__ __launch_bounds__(256) void heads_fwd_s16_kernel(
     const FT* __restrict__ feat, int F, const float* __restrict__ flat, long pw, long pb, long vw, long vb, int A,
     int B, float* __restrict__ logits, float* __restrict__ value, int* __restrict__ actions, uint32_t seed,
-    const long long* __restrict__ ctr, int t, int T, int greedy, int b0) {
+    const long long* __restrict__ ctr, int t, int T, int greedy, int b0, uint32_t rb) {
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   constexpr int AW = AM + 1;
   float* Wl = hsm;                       // [F][AW]
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void heads_fwd_s16_kernel(
       const float lg = acc[j] + flat[pb + j];
       logits[(long)b * A + j] = lg;
       float sc = lg;
-      if (!greedy) sc += -__logf(-__logf(u01(seed, stepkey, (uint32_t)b, (uint32_t)j)));
+      if (!greedy) sc += -__logf(-__logf(u01(seed, stepkey, rb + (uint32_t)b, (uint32_t)j)));
       if (sc > bv) { bv = sc; best = j; }
     }
   }
@@ -214,13 +214,14 @@ extern "C" void heads_set_s16(int v) { HEADS_S16 = v; }
 template <typename FT>
 static bool heads_fwd_lanes_launch(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
                                    int A, int B, float* logits, float* value, int* actions, unsigned seed,
-                                   const long long* ctr, int t, int T, int greedy, int b0, hipStream_t stream) {
+                                   const long long* ctr, int t, int T, int greedy, int b0, unsigned rb,
+                                   hipStream_t stream) {
   if (F % 32 != 0 || A > 18) return false;
   if (HEADS_S16 && F % 128 == 0 && A <= 8) {
     const size_t sm = (size_t)(F * 9 + 16 * 9 * 16) * 4;
     if (sm <= 64 * 1024) {
       heads_fwd_s16_kernel<8, FT><<<(unsigned)((B - b0 + 15) / 16), 256, sm, stream>>>(
-          (const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T, greedy, b0);
+          (const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T, greedy, b0, rb);
       return true;
     }
   }
@@ -229,12 +230,12 @@ static bool heads_fwd_lanes_launch(const void* feat, int F, const float* flat, l
     const size_t sm = (size_t)(F * 9 + 3 * 9 * 64) * 4;
     if (sm > 64 * 1024) return false;
     heads_fwd_lanes_kernel<8, FT><<<g, 256, sm, stream>>>((const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits,
-                                                          value, actions, seed, ctr, t, T, greedy, b0);
+                                                          value, actions, seed, ctr, t, T, greedy, b0, rb);
   } else {
     const size_t sm = (size_t)(F * 19 + 3 * 19 * 64) * 4;
     if (sm > 64 * 1024) return false;
     heads_fwd_lanes_kernel<18, FT><<<g, 256, sm, stream>>>((const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits,
-                                                           value, actions, seed, ctr, t, T, greedy, b0);
+                                                           value, actions, seed, ctr, t, T, greedy, b0, rb);
   }
   return true;
 }
@@ -439,31 +440,33 @@ __global__ __launch_bounds__(256) void heads_reduce_kernel(const float* __restri
 extern "C" {
 
 // samples [b0, B) (a path group of the split rollout, runtime/engine.py); RNG keys use the global sample index
+// row_base + b (row_base = this rank's first sample: the same draws whatever the population's sharding)
 int launch_heads_fwd_sample(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb, int A,
                             int B, float* logits, float* value, int* actions, unsigned seed, const long long* ctr,
-                            int t, int T, int greedy, int b0, hipStream_t stream) {
+                            int t, int T, int greedy, int b0, unsigned row_base, hipStream_t stream) {
   if (F <= 0 || A <= 0 || B <= 0 || T <= 0 || pw < 0 || pb < 0 || vw < 0 || vb < 0 || t < 0 || greedy < 0 ||
       b0 < 0) return -22;
   if (A > AMAX || A < 1 || b0 < 0 || b0 >= B) return -1;
   if (!heads_fwd_lanes_launch<bf16_t>(feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T,
-                                      greedy, b0, stream))
+                                      greedy, b0, row_base, stream))
     heads_fwd_sample_kernel<bf16_t><<<(B - b0 + 3) / 4, 256, 0, stream>>>((const bf16_t*)feat, F, flat, pw, pb, vw,
                                                                            vb, A, B, logits, value, actions, seed, ctr,
-                                                                           t, T, greedy, b0);
+                                                                           t, T, greedy, b0, row_base);
   return (int)hipGetLastError();
 }
 
 int launch_heads_fwd_sample_f32(const void* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
                                 int A, int B, float* logits, float* value, int* actions, unsigned seed,
-                                const long long* ctr, int t, int T, int greedy, int b0, hipStream_t stream) {
+                                const long long* ctr, int t, int T, int greedy, int b0, unsigned row_base,
+                                hipStream_t stream) {
   if (F <= 0 || A <= 0 || B <= 0 || T <= 0 || pw < 0 || pb < 0 || vw < 0 || vb < 0 || t < 0 || greedy < 0 ||
       b0 < 0) return -22;
   if (A > AMAX || A < 1 || b0 < 0 || b0 >= B) return -1;
   if (!heads_fwd_lanes_launch<float>(feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T,
-                                     greedy, b0, stream))
+                                     greedy, b0, row_base, stream))
     heads_fwd_sample_kernel<float><<<(B - b0 + 3) / 4, 256, 0, stream>>>((const float*)feat, F, flat, pw, pb, vw, vb,
                                                                           A, B, logits, value, actions, seed, ctr, t,
-                                                                          T, greedy, b0);
+                                                                          T, greedy, b0, row_base);
   return (int)hipGetLastError();
 }
 

@@ -73,6 +73,23 @@ def _needs(obj, digest) -> bool:
     return d != digest or fsha != _file_sha(obj)
 
 
+LAST = {"compiled": [], "relinked": False}       # what the last build() call in this process did
+
+
+def source_digest() -> str:
+    """SHA-256 over every csrc/*.hip and csrc/*.h (names + contents), computed from the files on disk now."""
+    return _digest(sorted(glob.glob(os.path.join(CSRC, "*.hip"))) + sorted(glob.glob(os.path.join(CSRC, "*.h"))))
+
+
+def build_info(lib: str = LIB) -> dict:
+    """Provenance of the loaded library for result records: the digest of the sources on disk, the SHA-256 of the
+    library file, and which objects this process compiled (an object or library whose stamp does not match its
+    sources, flags or own bytes is rebuilt by build(), so the library always derives from these sources)."""
+    return {"sources_sha256": source_digest()[:16], "lib_sha256": _file_sha(lib)[:16],
+            "compiled_here": [os.path.basename(o) for o in LAST["compiled"]], "relinked_here": LAST["relinked"],
+            "arch": ARCH}
+
+
 def build(verbose: bool = False, jobs: int = 0) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
@@ -103,8 +120,11 @@ def build(verbose: bool = False, jobs: int = 0) -> str:
     n = min(n, 16)
     with cf.ThreadPoolExecutor(n) as ex:
         list(ex.map(comp, todo))
+    LAST["compiled"] = [o for _, o, _ in todo]
+    LAST["relinked"] = False
     lib_digest = hashlib.sha256("".join(digests).encode()).hexdigest()
     if todo or _needs(LIB, lib_digest):
+        LAST["relinked"] = True
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

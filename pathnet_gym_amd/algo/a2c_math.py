@@ -70,3 +70,28 @@ def sample_actions(logits: torch.Tensor, generator=None) -> torch.Tensor:
     """Categorical sampling (a3c_training_thread.py:89-90), on device."""
     probs = torch.softmax(logits.float(), -1)
     return torch.multinomial(probs, 1, generator=generator).squeeze(1)
+
+
+def sampling_u01(seed: int, stepkey: int, rows: torch.Tensor, A: int) -> torch.Tensor:
+    """The uniforms of the HIP heads kernel's Gumbel-max (csrc/heads.hip u01), bit for bit: hash(stepkey * 64 +
+    action) -> ^ global row -> ^ seed, 24 bits, centred.  rows: int64 [N] global sample indices.  [N, A] fp32."""
+    from ..envs.base import wang_hash
+    m = 0xFFFFFFFF
+    j = torch.arange(A, dtype=torch.int64, device=rows.device)
+    h = wang_hash(torch.full_like(j, (stepkey * 64) & m) + j)[None, :]        # [1, A]
+    h = wang_hash(h ^ (rows[:, None] & m))
+    h = wang_hash(h ^ (seed & m))
+    return ((h >> 8).to(torch.float32) + 0.5) * (1.0 / 16777216.0)
+
+
+def sample_actions_keyed(logits: torch.Tensor, seed: int, stepkey: int, row_base: int = 0,
+                         greedy: bool = False) -> torch.Tensor:
+    """Categorical sampling by Gumbel-max on the counter-based key (seed, stepkey, global row, action), the same
+    draws as the HIP heads kernel.  Row b of ``logits`` is global sample row_base + b, so a population sharded
+    over ranks samples exactly what one process sampling all rows would (strong scaling, TrainConfig.paths_total)."""
+    lg = logits.detach().float()
+    if greedy:
+        return lg.argmax(-1)
+    rows = torch.arange(lg.shape[0], dtype=torch.int64, device=lg.device) + int(row_base)
+    u = sampling_u01(int(seed), int(stepkey), rows, lg.shape[1])
+    return (lg - torch.log(-torch.log(u))).argmax(-1)

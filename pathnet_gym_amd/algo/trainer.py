@@ -36,7 +36,7 @@ from ..runtime.consistency import check_replicas
 from ..runtime.guard import NonFiniteGuard, Watchdog
 from ..utils.metrics import MetricsLogger
 from ..utils.tracing import PhaseTracer, performance_line
-from .a2c_math import a2c_loss, nstep_returns, sample_actions
+from .a2c_math import a2c_loss, nstep_returns, sample_actions_keyed
 from .ga import Population
 from .optim import RMSPropTF, anneal_lr
 
@@ -81,10 +81,20 @@ class PathNetTrainer:
         self.compute_dtype = cfg.compute_dtype if self.backend == "hip" else "fp32"
         self.logger = logger
         net = cfg.net
+        if cfg.paths_total:
+            # strong scaling: a fixed population split over the ranks (cfg.paths is resolved to the local count)
+            if cfg.paths_total % self.ctx.world:
+                raise ValueError(f"paths_total={cfg.paths_total} is not divisible by the world size {self.ctx.world}")
+            cfg.paths = cfg.paths_total // self.ctx.world
         self.P = cfg.paths
         self.E = cfg.envs_per_path
         self.P_total = self.P * self.ctx.world
         self.path_offset = self.ctx.rank * self.P
+        # global index of this rank's first env: every env's RNG (dynamics, resets, action sampling) is keyed by its
+        # global index and the seeds carry no rank term, so rank r computes exactly envs [env_base, env_base + P*E)
+        # of the one-GPU run of the same population (strong scaling reproduces one GPU; weak scaling = the first
+        # world * P paths of a bigger population)
+        self.env_base = self.path_offset * self.E
         self.device_ga = cfg.ga.backend == "device"
         pop_cls = Population
         if self.device_ga:
@@ -123,12 +133,14 @@ class PathNetTrainer:
     # ------------------------------------------------------------------
     def _make_env(self, task_idx: int):
         name = self.cfg.tasks[task_idx]
-        seed = self.cfg.seed * 7919 + self.ctx.rank * 104729 + task_idx * 113
+        seed = self.cfg.seed * 7919 + task_idx * 113
         kw = dict(gray=self.cfg.gray)
         if is_synthetic(name):
             kw["frameskip"] = self.cfg.frameskip
         env_backend = "hip" if self.backend == "hip" else "torch"
-        return make(name, num_envs=self.P * self.E, device=self.device, seed=seed, backend=env_backend, **kw)
+        env = make(name, num_envs=self.P * self.E, device=self.device, seed=seed, backend=env_backend, **kw)
+        env.set_id_base(self.env_base)
+        return env
 
     def _start_task(self, task_idx: int, fresh: bool = False):
         self.task_idx = task_idx
@@ -145,8 +157,8 @@ class PathNetTrainer:
         self.engine = None
         if self.backend == "hip":
             from ..runtime.engine import HipEngine
-            self.engine = HipEngine(self.model, self.env, self.cfg, self.opt,
-                                    seed=self.cfg.seed * 1000003 + self.ctx.rank * 7919 + task_idx)
+            self.engine = HipEngine(self.model, self.env, self.cfg, self.opt, seed=self._sample_seed(task_idx),
+                                    row_base=self.env_base)
             self.fitness_local = self.engine.fitness
             if self.device_ga:
                 self.engine.enable_device_ga(self.pop, self.comm, self.path_offset)
@@ -158,6 +170,10 @@ class PathNetTrainer:
         self.task_start_step = self.global_step
         self.solved_generation.setdefault(task_idx, None)
         self._task_gen0 = self.pop.generation
+
+    def _sample_seed(self, task_idx: int) -> int:
+        """Key of the action-sampling RNG (identical on every rank; rows are told apart by their global index)."""
+        return (self.cfg.seed * 1000003 + task_idx) & 0xFFFFFFFF
 
     def _enable_overlap(self):
         """TrainConfig.overlap_allreduce: split the HIP update at the first layer so the all-reduce of everything
@@ -223,7 +239,9 @@ class PathNetTrainer:
         ep_cnt = torch.zeros(P, device=self.device)
         for t in range(T):
             logits, value, state = model.forward(obs, E, state)
-            a = sample_actions(logits.detach())
+            # the HIP heads kernel's keyed Gumbel-max: sample b of this rank = global row env_base + b
+            a = sample_actions_keyed(logits, self._sample_seed(self.task_idx), self.updates * (T + 1) + t,
+                                     self.env_base)
             obs, r, d, info = env.step(a)
             finished = d.float()
             er = info["episode_return"].float()

@@ -186,7 +186,12 @@ class GAConfig:
 class TrainConfig:
     env: str = "Pong"
     tasks: List[str] = field(default_factory=lambda: ["Pong"])
-    paths: int = 64                     # paths per rank
+    paths: int = 64                     # paths per rank (weak scaling: the population grows with the ranks)
+    # strong scaling: a FIXED population of paths_total paths split over the ranks (paths = paths_total / world).
+    # Envs and action sampling are keyed by the global env index (VecEnv.set_id_base, heads row_base) and the
+    # GA and the summed gradient run over the same P_total, so any world size computes the one-GPU run of the
+    # same seed -- more GPUs shorten each update instead of growing it.  0 = weak scaling (``paths`` per rank)
+    paths_total: int = 0
     envs_per_path: int = 16
     net: PathNetConfig = field(default_factory=PathNetConfig)
     a2c: A2CConfig = field(default_factory=A2CConfig)

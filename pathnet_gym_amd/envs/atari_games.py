@@ -214,7 +214,7 @@ class PixelGameVec(VecEnv):
     def _hip_run(self, actions, mask, reward, done, epret):
         from ..ops import envs as henv
         henv.game_step(self.HIP_GAME, self._st32, actions, mask, self.num_actions, self.seed_int, self.frameskip,
-                       int(self.max_episode_steps), reward, done, epret, self._rects)
+                       int(self.max_episode_steps), reward, done, epret, self._rects, id_base=self.id_base)
 
     def _hip_push(self, obs_in, obs_out, reset_u8):
         from ..ops import envs as henv

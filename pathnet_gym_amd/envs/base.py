@@ -70,6 +70,7 @@ class VecEnv:
     reward_threshold: float = float("inf")
     max_episode_steps: int = 0
     id: str = ""
+    id_base: int = 0             # global index of instance 0 (RNG identity, see set_id_base)
 
     @property
     def action_space(self) -> Discrete:
@@ -77,6 +78,15 @@ class VecEnv:
 
     def seed(self, seed: int):
         raise NotImplementedError
+
+    def set_id_base(self, base: int):
+        """Instance b draws its random numbers as global instance ``base + b`` (counter-based RNG keyed by the
+        global index, torch and HIP alike).  A trainer rank that owns envs [base, base + num_envs) of a
+        population therefore sees exactly the streams those envs have in a one-GPU run of the same seed: the
+        trajectories do not depend on how the population is sharded.  Call before the first reset."""
+        self.id_base = int(base)
+        if isinstance(getattr(self, "env_id", None), torch.Tensor):
+            self.env_id = torch.arange(self.num_envs, dtype=torch.int64, device=self.env_id.device) + self.id_base
 
     def reset(self) -> torch.Tensor:
         raise NotImplementedError

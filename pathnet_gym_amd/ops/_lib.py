@@ -39,7 +39,7 @@ _SIGS = {
     "launch_fc_wgrad": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_long, c_float, P],
     "launch_heads_fwd_sample": [P, c_int, P, c_long, c_long, c_long, c_long, c_int, c_int, P, P, P, c_uint, P, c_int,
-                                c_int, c_int, c_int, P],
+                                c_int, c_int, c_int, c_uint, P],
     "launch_a2c_grad": [P, P, P, P, P, P, c_int, c_int, c_int, c_float, c_float, c_float, c_float, c_float, c_float,
                         P, P, P, P],
     "launch_heads_bwd": [P, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P],
@@ -47,18 +47,18 @@ _SIGS = {
     "launch_rmsprop": [P, P, P, P, P, P, P, c_int, P, P, P, P, P, c_float, c_float, c_float, c_float, P],
     "launch_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
     "launch_pong_step": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int, c_int, c_int,
-                         c_int, c_int, c_int, P],
+                         c_int, c_int, c_int, c_uint, P],
     "launch_refresh_weights_cmajor": [P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P],
     "fast_conv1_ring_fwd": [P, P, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_int, c_long, c_float, c_float, P, P, P],
     "fast_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_long, c_float, c_float, P],
     "launch_pong_step_ring": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int,
-                              c_int, c_int, c_int, c_int, P],
-    "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_int, P, P, P, P, P, P],
+                              c_int, c_int, c_int, c_int, c_uint, P],
+    "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_uint, c_int, P, P, P, P, P, P],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],
-    "launch_game_step": [c_int, P, P, P, c_int, c_int, c_int, c_uint, c_int, c_int, P, P, P, P, P],
+    "launch_game_step": [c_int, P, P, P, c_int, c_int, c_int, c_uint, c_uint, c_int, c_int, P, P, P, P, P],
     "game_layout": [c_int, P, P],
     "fast_conv_fwd": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_float, c_float, P, P, P],
@@ -93,7 +93,7 @@ _SIGS = {
     "launch_prof_marker": [c_int, P],
     "launch_pack_ranges": [P, P, P, c_int, c_long, c_int, P],
     "launch_heads_fwd_sample_f32": [P, c_int, P, c_long, c_long, c_long, c_long, c_int, c_int, P, P, P, c_uint, P,
-                                    c_int, c_int, c_int, c_int, P],
+                                    c_int, c_int, c_int, c_int, c_uint, P],
     "launch_heads_bwd_f32": [P, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P],
     "launch_conv_fwd_f32": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_long,

@@ -15,6 +15,12 @@ import torch
 from . import _lib
 
 
+def _id_base(env) -> int:
+    """Global index of the env's first instance: the RNG identity of instance b is id_base + b, so a population
+    sharded over ranks draws the same random streams as on one GPU (envs/base.py VecEnv.set_id_base)."""
+    return int(getattr(env, "id_base", 0)) & 0xFFFFFFFF
+
+
 # ------------------------------------------------------------------ Pong
 def pong_sync_to_device(env):
     """(Re)build the int32 kernel state from the torch (int64) state."""
@@ -57,7 +63,7 @@ def pong_step_into(env, actions, obs_in, obs_out, reward, done, epret, b0: int =
     _lib.call("launch_pong_step", env._st32.data_ptr(), env._ctr32.data_ptr(), actions.data_ptr(), env.num_actions,
               obs_in.data_ptr(), obs_out.data_ptr(), env._tab32.data_ptr(), reward.data_ptr(), done.data_ptr(),
               epret.data_ptr(), b1, env.seed_int, env.frameskip, env.max_episode_steps,
-              env.no_op_max, g[0], g[1], g[2], g[3], g[4], b0, _lib.stream())
+              env.no_op_max, g[0], g[1], g[2], g[3], g[4], b0, _id_base(env), _lib.stream())
 
 
 def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done, epret):
@@ -83,7 +89,7 @@ def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done,
               env.num_actions, frames[0, slot].data_ptr(), frames.stride(0), fc_in.data_ptr(), fc_out.data_ptr(),
               env._tab32.data_ptr(),
               reward.data_ptr(), done.data_ptr(), epret.data_ptr(), B, env.seed_int, env.frameskip,
-              env.max_episode_steps, env.no_op_max, g[0], g[1], g[2], g[3], g[4], _lib.stream())
+              env.max_episode_steps, env.no_op_max, g[0], g[1], g[2], g[3], g[4], _id_base(env), _lib.stream())
 
 
 def pong_step(env, actions, obs):
@@ -114,7 +120,7 @@ def cartpole_step_into(env, actions, obs_bf16_out, reward, done, epret, obs_f32_
     if obs_bf16_out is not None:
         _lib.check(obs_bf16_out, torch.bfloat16, numel=B * 8, name="obs_bf16")
     _lib.call("launch_cartpole_step", env.state.data_ptr(), env._steps32.data_ptr(), env.ep_ret.data_ptr(),
-              env._ctr32.data_ptr(), actions.data_ptr(), B, env.seed_int,
+              env._ctr32.data_ptr(), actions.data_ptr(), B, env.seed_int, _id_base(env),
               env.max_episode_steps, _lib.ptr(obs_f32_out), _lib.ptr(obs_bf16_out), reward.data_ptr(),
               done.data_ptr(), epret.data_ptr(), _lib.stream())
 
@@ -192,7 +198,8 @@ def game_layout(game: str):
 
 
 def game_step(game: str, state: torch.Tensor, actions, mask, n_actions: int, seed: int, frameskip: int,
-              max_steps: int, reward: torch.Tensor, done: torch.Tensor, epret: torch.Tensor, rects: torch.Tensor):
+              max_steps: int, reward: torch.Tensor, done: torch.Tensor, epret: torch.Tensor, rects: torch.Tensor,
+              id_base: int = 0):
     """One launch: agent step of every env (``actions`` int32 [N]) or, with ``mask`` (uint8 [N]) instead,
     ``reset_where``; writes reward/done/episode-return rows and the int16 scene [N, R, 4]."""
     N = state.shape[0]
@@ -207,7 +214,8 @@ def game_step(game: str, state: torch.Tensor, actions, mask, n_actions: int, see
     if mask is not None:
         _lib.check(mask, torch.uint8, (N,), name="mask")
     _lib.call("launch_game_step", GAME_IDS[game], state.data_ptr(), _lib.ptr(actions), _lib.ptr(mask),
-              0 if mask is None else 1, n_actions, N, seed & 0xFFFFFFFF, frameskip, max_steps, reward.data_ptr(),
+              0 if mask is None else 1, n_actions, N, seed & 0xFFFFFFFF, id_base & 0xFFFFFFFF, frameskip, max_steps,
+              reward.data_ptr(),
               done.data_ptr(), epret.data_ptr(), rects.data_ptr(), _lib.stream())
 
 

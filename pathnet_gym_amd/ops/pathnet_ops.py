@@ -750,9 +750,11 @@ class HipPathNet:
         rows = steps * B
         return torch.zeros(self.M, rows, g.Cout // 16, dtype=torch.int16, device=dev), rows
 
-    def heads_fwd(self, feat, logits, value, actions, seed, ctr, t, T, greedy=False, task=0, b0=0, b1=None):
+    def heads_fwd(self, feat, logits, value, actions, seed, ctr, t, T, greedy=False, task=0, b0=0, b1=None,
+                  row_base=0):
         """Heads + Gumbel-max sampling of samples [b0, b1) of feat [B, F] (default all; the split rollout
-        passes one path group's rows, runtime/engine.py)."""
+        passes one path group's rows, runtime/engine.py).  Sample b draws the RNG of global sample row_base + b
+        (row_base = the rank's first env of the population: sharding-invariant sampling)."""
         m = self.model
         h = m.store.layout.heads[task if m.cfg.per_task_heads else 0]
         B = feat.shape[0] if b1 is None else b1
@@ -765,7 +767,7 @@ class HipPathNet:
                   feat.data_ptr(), F,
                   m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"], A, B, logits.data_ptr(),
                   value.data_ptr(), actions.data_ptr(), seed & 0xFFFFFFFF, ctr.data_ptr(), t, T, int(greedy), b0,
-                  _lib.stream())
+                  int(row_base) & 0xFFFFFFFF, _lib.stream())
 
     def heads_bwd(self, feat, dlogits, dvalue, grad_flat, dfeat, task=0):
         m = self.model

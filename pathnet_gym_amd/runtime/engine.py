@@ -43,13 +43,16 @@ def loss_scale(cfg) -> float:
 
 
 class HipEngine:
-    def __init__(self, model, env, cfg, opt, seed: int = 1):
+    def __init__(self, model, env, cfg, opt, seed: int = 1, row_base: int = 0):
         self.model = model
         self.hip = model.hip
         self.env = env
         self.cfg = cfg
         self.opt = opt
         self.seed = seed & 0xFFFFFFFF
+        # global index of this rank's first env: action sampling draws the RNG of global sample row_base + b, so
+        # a population sharded over ranks samples exactly what one GPU would (trainer: rank * P * E)
+        self.row_base = int(row_base)
         a2c = cfg.a2c
         self.T = T = a2c.t_max
         self.P = P = model.P
@@ -313,7 +316,8 @@ class HipEngine:
         if grp is not None:
             p0, np_ = self._group_range(grp)
             hp.heads_fwd(feat, self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t, self.T + 1,
-                         greedy=greedy, task=self.model.task, b0=p0 * self.E, b1=(p0 + np_) * self.E)
+                         greedy=greedy, task=self.model.task, b0=p0 * self.E, b1=(p0 + np_) * self.E,
+                         row_base=self.row_base)
             return
         if self.lstm_hip:
             # state entering step t: slot t, reset where the previous step ended an episode
@@ -323,7 +327,7 @@ class HipEngine:
                         self.cst[t + 1], None if last else self.gates[t], None if last else self.xh[t])
             feat = self.hst[t + 1]
         hp.heads_fwd(feat, self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t,
-                     self.T + 1, greedy=greedy, task=self.model.task)
+                     self.T + 1, greedy=greedy, task=self.model.task, row_base=self.row_base)
 
     def _rollout_backward_hybrid(self):
         """LSTM nets: HIP trunk fwd/bwd, torch (autograd) LSTM + heads + loss in between."""

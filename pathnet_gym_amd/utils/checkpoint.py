@@ -32,7 +32,9 @@ import numpy as np
 import torch
 from safetensors.torch import load_file, save_file
 
-FORMAT_VERSION = 1
+# 1: rounds 1-3.  2: task ids name what they mean today (``Pong-v0`` = the real gym game, ``Pong`` / ``Synth*`` the
+# on-device ones) and env / sampling RNG streams are keyed by the global env index (VecEnv.set_id_base)
+FORMAT_VERSION = 2
 
 
 def _t(x) -> torch.Tensor:
@@ -203,12 +205,16 @@ def read_metadata(path: str) -> dict:
 
 
 def read_config(path: str):
-    """The TrainConfig stored in a checkpoint.  Task ids of the round-1 synthetic games (``Pong-v0`` ...: those ids
-    now mean the real gym games, envs/registry.py) are mapped to their ``Synth*`` equivalents with a warning."""
+    """The TrainConfig stored in a checkpoint.  In format-1 checkpoints (written before the rename) the ids of the
+    synthetic games (``Pong-v0`` ...: those ids now mean the real gym games, envs/registry.py) are mapped to their
+    ``Synth*`` equivalents with a warning; newer checkpoints keep their ids as written."""
     import warnings
     from ..config import TrainConfig
     from ..envs.registry import legacy_synth_id
-    cfg = TrainConfig.from_json(read_metadata(path)["config"])
+    meta = read_metadata(path)
+    cfg = TrainConfig.from_json(meta["config"])
+    if int(meta.get("format_version", "1")) >= 2:
+        return cfg
     new = [legacy_synth_id(t) or t for t in cfg.tasks]
     if new != list(cfg.tasks):
         warnings.warn(f"checkpoint tasks {cfg.tasks} use round-1 synthetic ids; mapped to {new}")

@@ -27,7 +27,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="pong")
     ap.add_argument("--minutes", type=float, default=10.0)
-    ap.add_argument("--paths", type=int, default=None)
+    ap.add_argument("--paths", type=int, default=None, help="paths per GPU (weak scaling)")
+    ap.add_argument("--paths-total", type=int, default=None,
+                    help="strong scaling: this population split over the GPUs (TrainConfig.paths_total)")
+    ap.add_argument("--checkpoint", default=None, help="save the trainer here at the end (and every --ckpt-minutes)")
+    ap.add_argument("--ckpt-minutes", type=float, default=0.0)
+    ap.add_argument("--resume", action="store_true",
+                    help="continue from --checkpoint (exact resume: weights, optimizer, GA, envs, RNG counters); the "
+                         "record's seconds / segments accumulate over the resumed runs (read back from --out)")
     ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--tmax", type=int, default=None)
     ap.add_argument("--lr", type=float, default=None)
@@ -111,7 +118,9 @@ def main():
     if args.dtype is not None:
         cfg.compute_dtype = args.dtype
     cfg.deterministic = bool(args.deterministic)
-    cfg.ga.concurrent_tournaments = args.concurrent or max(1, cfg.paths // 16)
+    if args.paths_total:
+        cfg.paths_total = args.paths_total
+    cfg.ga.concurrent_tournaments = args.concurrent or max(1, (cfg.paths_total or cfg.paths) // 16)
     if cfg.backend in ("hip", "auto") and ctx.device.type == "cuda":
         from pathnet_gym_amd import _build
         _build.build()
@@ -126,17 +135,32 @@ def main():
         tr._push_genotypes()
         if tr.engine is not None and tr.engine.ga_dev is not None:
             tr.engine.ga_upload(tr.pop)
+    prior = {"seconds": 0.0, "segments": []}
+    if args.resume and args.checkpoint and os.path.exists(args.checkpoint):
+        from pathnet_gym_amd.utils import checkpoint as ckpt
+        ckpt.load(tr, args.checkpoint)
+        if args.out and os.path.exists(args.out):
+            with open(args.out) as f:
+                old = json.loads(f.read().strip().splitlines()[-1])
+            prior = {"seconds": float(old.get("seconds", 0.0)), "segments": list(old.get("segments", []))
+                     or [{"updates": old.get("updates"), "seconds": old.get("seconds")}],
+                     "best": old.get("best_winner_fitness"), "ema": old.get("final_mean_return")}
+        if ctx.is_main:
+            print(json.dumps({"resumed": args.checkpoint, "updates": tr.updates, "generation": tr.pop.generation,
+                              "frames": tr.global_step, "prior_seconds": prior["seconds"]}), flush=True)
     thr = reward_threshold(cfg.tasks[0])
     curve = None
     if ctx.is_main and args.curve:
         os.makedirs(os.path.dirname(args.curve) or ".", exist_ok=True)
-        curve = open(args.curve, "w")
+        curve = open(args.curve, "a" if args.resume else "w")
 
     t0 = time.time()
     last = t0
-    best = -math.inf
+    last_ckpt = t0
+    u0 = tr.updates
+    best = prior.get("best") if prior.get("best") is not None else -math.inf
     solved = None
-    ret_ema = None
+    ret_ema = prior.get("ema")
     while True:
         st = tr.update()
         if not math.isnan(st.mean_return) and abs(st.mean_return) > 1000 and ctx.is_main:
@@ -155,12 +179,12 @@ def main():
         if st.tournaments:
             best = max(best, st.best_winner)
             if solved is None and st.best_winner >= thr:
-                solved = dict(generations=tr.pop.generation, frames=tr.global_step,
-                              seconds=round(time.time() - t0, 2), winner_fitness=st.best_winner)
+                solved = dict(generations=tr.pop.generation, frames=tr.global_step, updates=tr.updates,
+                              seconds=round(prior["seconds"] + time.time() - t0, 2), winner_fitness=st.best_winner)
         now = time.time()
         if now - last >= args.report_every or (solved and not args.keep_going):
             last = now
-            rec = dict(t=round(now - t0, 1), frames=tr.global_step, updates=tr.updates,
+            rec = dict(t=round(prior["seconds"] + now - t0, 1), frames=tr.global_step, updates=tr.updates,
                        generation=tr.pop.generation, mean_return=ret_ema, best_winner=best,
                        entropy=st.entropy, frames_per_sec=round(tr.global_step / (now - t0), 1))
             if ctx.is_main:
@@ -169,26 +193,41 @@ def main():
                     curve.write(json.dumps(rec) + "\n")
                     curve.flush()
         if solved and not args.keep_going:
+            break                                # replicated GA state: every rank breaks at the same update
+        # the wall limit is decided on the max over ranks at a fixed update cadence, so all ranks stop together
+        if tr.updates % 32 == 0 and ctx.max_scalar(now - t0) > args.minutes * 60:
             break
-        if now - t0 > args.minutes * 60:
-            break
-    el = time.time() - t0
+        if args.checkpoint and args.ckpt_minutes > 0 and tr.updates % 32 == 0 and \
+                ctx.max_scalar(now - last_ckpt) > args.ckpt_minutes * 60:
+            from pathnet_gym_amd.utils import checkpoint as ckpt
+            tr.flush()
+            ckpt.save(tr, args.checkpoint)
+            last_ckpt = time.time()
+    tr.flush()
+    if args.checkpoint:
+        from pathnet_gym_amd.utils import checkpoint as ckpt
+        ckpt.save(tr, args.checkpoint)
+    el = prior["seconds"] + time.time() - t0
     if ctx.is_main:
         out = {"metric": "generations_to_solve", "env": cfg.tasks[0], "threshold": thr,
                "solved": solved is not None, "generations_to_solve": solved and solved["generations"],
                "frames_to_solve": solved and solved["frames"], "seconds_to_solve": solved and solved["seconds"],
                "best_winner_fitness": best, "final_mean_return": ret_ema, "generations": tr.pop.generation,
-               "frames": tr.global_step, "seconds": round(el, 1), "n_gpus": ctx.world,
+               "frames": tr.global_step, "updates": tr.updates, "updates_to_solve": solved and solved["updates"],
+               "seconds": round(el, 1), "n_gpus": ctx.world,
+               "segments": prior["segments"] + [{"updates": tr.updates - u0, "seconds": round(time.time() - t0, 1)}],
                "config": {"preset": args.preset, "paths_per_gpu": cfg.paths, "envs_per_path": cfg.envs_per_path,
                           "t_max": cfg.a2c.t_max, "lr": cfg.a2c.lr, "B": cfg.ga.B,
                           "concurrent_tournaments": cfg.ga.concurrent_tournaments, "backend": tr.backend,
                           "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
                           "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
                           "rmsp_epsilon": cfg.a2c.rmsp_epsilon, "grad_scale": cfg.a2c.grad_scale,
-                          "rank_reduction": cfg.a2c.rank_reduction, "frame_ring": bool(tr.engine.ring),
+                          "rank_reduction": cfg.a2c.rank_reduction, "frame_ring": bool(getattr(tr.engine, "ring", False)),
                           "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
                           "ga": not args.no_ga, "same_path": args.same_path, "dtype": tr.compute_dtype}}
         out["config"]["seed"] = cfg.seed
+        if cfg.paths_total:
+            out["config"]["paths_total"] = cfg.paths_total
         print(json.dumps(out), flush=True)
         if args.out:
             os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)

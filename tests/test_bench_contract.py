@@ -13,7 +13,7 @@ def test_bench_two_rank_gloo_json_contract(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29653", os.path.join(ROOT, "bench.py"), "--gpus", "2",
            "--backend", "torch", "--preset", "cartpole-cpu", "--paths", "4", "--envs", "16", "--tmax", "5",
-           "--steps", "2", "--warmup", "1", "--ga-backend", "host"]
+           "--steps", "2", "--warmup", "1", "--ga-backend", "host", "--solve-seconds", "30"]
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -29,3 +29,10 @@ def test_bench_two_rank_gloo_json_contract(tmp_path):
     frames = 2 * 4 * 16 * 5 * 2
     assert abs(d["value"] - frames / (d["ms_per_step"] * 2 / 1e3)) / d["value"] < 0.01
     assert d["config"]["global_batch"] == 2 * 4 * 16 * 5 and d["config"]["parallelism"].startswith("dp2")
+    # median of 3 windows; the strong-scaling record times the fixed 64-path population split over the 2 ranks
+    assert d["windows"] == 3 and len(d["windows_ms_per_step"]) == 3
+    assert sorted(d["windows_ms_per_step"])[1] == d["ms_per_step"]
+    s = d["strong_scaling"]
+    assert s["paths_total"] == 64 and s["paths_per_gpu"] == 32 and s["n_gpus"] == 2 and s["ms_per_update"] > 0
+    r = s["in_run_solve"]
+    assert r["paths_total"] == 64 and r["paths_per_gpu"] == 32 and r["updates_run"] > 0

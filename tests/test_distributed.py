@@ -115,3 +115,73 @@ def test_replica_divergence_is_detected_on_every_rank():
     for r in range(2):
         assert "error" not in res[r], res[r].get("error")
         assert res[r]["raised"] is True
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# strong scaling (TrainConfig.paths_total): a fixed population split over the ranks computes the one-process run
+# ---------------------------------------------------------------------------------------------------------------
+def _strong_cfg():
+    from pathnet_gym_amd.config import preset
+    cfg = preset("cartpole-cpu")
+    cfg.paths_total, cfg.envs_per_path = 8, 4
+    cfg.ga.B = 2
+    cfg.ga.concurrent_tournaments = 2
+    return cfg
+
+
+def _strong_run(tr, updates=8):
+    hist = []
+    for _ in range(updates):
+        st = tr.update()
+        hist.append((st.episodes, st.tournaments, tr.pop.generation, tr.global_step))
+    return {"flat": tr.model.store.flat.detach().numpy().copy(), "ms": tr.opt.ms.numpy().copy(),
+            "geno": tr.pop.genotypes.copy(), "fit": tr.pop.fitness.copy(), "gen": tr.pop.generation,
+            "step": tr.global_step, "hist": hist, "P": tr.P}
+
+
+def _strong_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    try:
+        from pathnet_gym_amd.algo.trainer import PathNetTrainer
+        from pathnet_gym_amd.parallel.dist import init_distributed
+        ctx = init_distributed(device="cpu", backend="gloo")
+        tr = PathNetTrainer(_strong_cfg(), ctx=ctx)
+        out = _strong_run(tr)
+        q.put((rank, out))
+        ctx.destroy()
+    except Exception:   # pragma: no cover
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+def test_strong_scaling_four_ranks_reproduce_one_process():
+    """4 gloo ranks x 2 paths (paths_total = 8) vs one process with the 8 paths: same env streams, same sampled
+    actions, same episodes, the same GA decisions and genotypes; the weights differ only by the summation order of
+    the gradient (per-rank partial sums + all-reduce vs one backward)."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    torch.set_num_threads(1)
+    one = _strong_run(PathNetTrainer(_strong_cfg()))
+    assert one["P"] == 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_strong_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r in range(4):
+        assert "error" not in res[r], res[r].get("error")
+        assert res[r]["P"] == 2
+    four = res[0]
+    assert four["hist"] == one["hist"]                       # episodes, tournaments, generations, frames per update
+    assert four["gen"] == one["gen"] > 0 and four["step"] == one["step"]
+    assert np.array_equal(four["geno"], one["geno"])
+    assert np.array_equal(four["fit"], one["fit"])
+    np.testing.assert_allclose(four["flat"], one["flat"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(four["ms"], one["ms"], rtol=1e-4, atol=1e-6)
+    for r in range(1, 4):                                      # replicas stay bit-identical across ranks
+        assert np.array_equal(res[r]["flat"], four["flat"])
