@@ -126,16 +126,34 @@ DEVI void split8h(const float (&v)[8], s8v& hi, s8v& lo) {
 }
 DEVI uint16_t f2h(float v) { return __builtin_bit_cast(uint16_t, (_Float16)v); }
 DEVI float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+
+// fp16-pair range guard.  An activation stored as an fp16 pair must stay below fp16's largest finite value (65504):
+// beyond it the hi half is inf and the pair is garbage.  Every epilogue that writes a pair ORs X3_RANGE_ACT into
+// this flag when one of its values is out of range (a branch around one vector atomic, taken only on overflow); the
+// weight refresh of the next optimizer step folds it into the status word the host reads
+// (HipPathNet.check_x3_status raises X3RangeError).
+#define X3_RANGE_W 1u        // a weight * 2^X3_W0_SHIFT left the fp16 range (refresh_x3_kernel)
+#define X3_RANGE_ACT 2u      // an activation written as an fp16 pair left the fp16 range (forward epilogues)
+__device__ uint32_t g_x3_range;
+DEVI bool x3_oor(float v) { return !(fabsf(v) < 65504.f); }     // NaN counts as out of range
+DEVI void x3_flag_range(bool bad) {
+  if (bad) atomicOr(&g_x3_range, X3_RANGE_ACT);
+}
 // An activation between layers is stored as its fp16 pair in two 16-bit planes, ylo elements apart (22 significant
 // bits; the next layer's forward reads it as is).  The weight gradients meet it with the output gradient, which needs
 // bf16's exponent range, so they convert it to the bf16 pair while staging (x16pair_to_bf16pair).
 DEVI void st_x4(uint16_t* Y, long ylo, long i, float v) {
+  x3_flag_range(x3_oor(v));
   const uint16_t h = f2h(v);
   Y[i] = h;
   Y[i + ylo] = f2h(v - h2f(h));
 }
 DEVI float ld_x4(const uint16_t* Y, long ylo, long i) { return h2f(Y[i]) + h2f(Y[i + ylo]); }
 DEVI void st8_x4(uint16_t* Y, long ylo, const float (&o)[8]) {
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bad |= x3_oor(o[j]);
+  x3_flag_range(bad);
   s8v a, b;
   split8h(o, a, b);
   *reinterpret_cast<s8v*>(Y) = a;
@@ -225,6 +243,7 @@ DEVI void conv_epi_sw(const f4v (&acc)[NC], const float* bias_s, int ct0, int cn
 #pragma unroll
     for (int r = 0; r < 4; ++r) y[r] += h2f((uint16_t)hw[r]) + h2f((uint16_t)lw[r]);
   }
+  x3_flag_range(x3_oor(y[0]) || x3_oor(y[1]) || x3_oor(y[2]) || x3_oor(y[3]));
   const h2v h01 = __builtin_convertvector((f2v){y[0], y[1]}, h2v);
   const h2v h23 = __builtin_convertvector((f2v){y[2], y[3]}, h2v);
   uint2 out;
@@ -3241,8 +3260,9 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
 
 // hi/lo operand copies of one layer's weights: Wc [2][M][Cout][KP] (forward B operand, k contiguous, zero padded):
 // the fp16 pair of W * 2^X3_W0_SHIFT (f16 != 0) or the bf16 pair of W; optionally WcT [2][M][KP][Cout] (the fc input
-// gradient's B operand): always the bf16 pair, as the output gradients it meets.  *status = 1 when a scaled weight
-// leaves the fp16 range (the host checks it, HipPathNet.check_x3_status)
+// gradient's B operand): always the bf16 pair, as the output gradients it meets.  *status |= X3_RANGE_W when a scaled
+// weight leaves the fp16 range; x3_status_fold (end of the next rollout) moves it and the forward epilogues' flag
+// into the update's all-reduced counters, where every rank sees it (algo/trainer.py raises X3RangeError)
 __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict__ flat, long w_off, int chunk, int K,
                                                          int KP, int Cout, int M, uint16_t* __restrict__ Wc,
                                                          uint16_t* __restrict__ WcT, int f16,
@@ -3260,7 +3280,7 @@ __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict
       const float x = v * (float)(1 << X3_W0_SHIFT);
       hi = f2h(x);
       lo = f2h(x - h2f(hi));
-      if (!(fabsf(x) < 32768.f) && status) *status = 1u;
+      if (!(fabsf(x) < 32768.f) && status) atomicOr(status, X3_RANGE_W);
     }
     const long wi = ((long)j * Cout + c) * KP + k;
     Wc[wi] = hi;
@@ -3270,6 +3290,13 @@ __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict
       WcT[n + i] = bl;
     }
   }
+}
+
+// one thread: out[0] = (float)(activation flags since the last fold | weight flags of the last refresh), both reset
+__global__ void x3_status_fold_kernel(uint32_t* __restrict__ wstatus, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const uint32_t f = atomicExch(&g_x3_range, 0u) | atomicExch(wstatus, 0u);
+  out[0] = (float)f;
 }
 
 }  // namespace x3
@@ -3716,6 +3743,14 @@ int x3_fc_wgrad(const void* X, long xlo, int ldx, const float* G, const void* bi
       layer, M, Pmax, K, Cout, P, E, T, br, gs, nsplit);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
+}
+
+// fp16-pair range status of the last rollout (X3_RANGE_ACT) and weight refresh (X3_RANGE_W) -> *out (float, for the
+// all-reduced counters slot); both flags reset
+int x3_status_fold(void* wstatus, float* out, hipStream_t st) {
+  if (!wstatus || !out) return -22;
+  x3_status_fold_kernel<<<1, 64, 0, st>>>((uint32_t*)wstatus, out);
+  return (int)hipGetLastError();
 }
 
 int x3_refresh_weights(const float* flat, long w_off, int chunk, int K, int KP, int Cout, int M, void* Wc, void* WcT,

@@ -394,6 +394,10 @@ class PathNetTrainer:
     def _finish_update(self, fit_all, csum, losses, skip, step_at) -> UpdateStats:
         tr = self.tracer
         lp, lv, ent = losses
+        if self.engine is not None and self.model.hip.x3 and float(csum[3]) != 0.0:
+            # fp32x fp16-pair range flags, all-reduced: every rank raises at the same update
+            from ..runtime.guard import X3RangeError
+            raise X3RangeError(float(csum[3]), self.updates, self.ctx.world)
         eps = float(csum[1]) if np.isfinite(csum[1]) else 0.0
         st = UpdateStats(float(lp), float(lv), float(ent), int(round(eps)),
                          float(csum[2] / csum[1]) if eps >= 0.5 else float("nan"), steps=int(csum[0]),

@@ -271,6 +271,24 @@ class HipPathNet:
     def set_frozen(self, frozen):
         pass   # frozen segments are skipped by the optimizer; kernels compute their grads (cheap)
 
+    def fold_x3_status(self, out: torch.Tensor):
+        """fp32x: out[0] <- the fp16-pair range flags of the last rollout / weight refresh (csrc/trunk_x3.hip
+        x3_status_fold; 0.0 = in range); the flags reset.  Graph-capturable (one tiny kernel)."""
+        _lib.check(out, torch.float32, numel=1, name="status out")
+        _lib.call("x3_status_fold", self.x3_status.data_ptr(), out.data_ptr(), _lib.stream())
+
+    def check_x3_status(self, update: int = -1):
+        """Host check of the fp16-pair range flags (syncs); raises runtime.guard.X3RangeError when set."""
+        if not self.x3:
+            return 0
+        from ..runtime.guard import X3RangeError
+        out = torch.zeros(1, dtype=torch.float32, device=self.model.device)
+        self.fold_x3_status(out)
+        v = float(out.item())
+        if v != 0.0:
+            raise X3RangeError(v, update)
+        return 0
+
     def refresh_weights(self):
         flat = self.model.store.flat
         if self.x3:

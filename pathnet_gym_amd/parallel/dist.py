@@ -26,6 +26,10 @@ class DistContext:
     local_rank: int = 0
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    # a real process group even at world size 1 (init_distributed(force=True)): every collective and the
+    # multi-rank code paths (packed / overlapped all-reduce, RCCL barrier) run on a one-rank group -- how the
+    # RCCL branches are exercised on a one-GPU box (tests/test_rccl_world1.py)
+    forced: bool = False
 
     @property
     def is_main(self) -> bool:
@@ -33,7 +37,7 @@ class DistContext:
 
     @property
     def enabled(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.forced
 
     # -- collectives (no-ops at world 1) -----------------------------------
     def all_reduce_(self, t: torch.Tensor):
@@ -78,8 +82,10 @@ class DistContext:
             dist.destroy_process_group()
 
 
-def init_distributed(device: Optional[str] = None, backend: Optional[str] = None) -> DistContext:
-    """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+def init_distributed(device: Optional[str] = None, backend: Optional[str] = None, force: bool = False) -> DistContext:
+    """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*).  ``force`` (or PATHNET_DIST_FORCE=1):
+    create the process group even at world size 1."""
+    force = force or os.environ.get("PATHNET_DIST_FORCE") == "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -91,14 +97,16 @@ def init_distributed(device: Optional[str] = None, backend: Optional[str] = None
         dev = torch.device("cuda", dev_idx)
     else:
         dev = torch.device("cpu")
-    if world <= 1:
+    if world <= 1 and not force:
         return DistContext(0, 1, 0, "none", dev)
     # PATHNET_DIST_BACKEND=gloo lets several ranks share one GPU (test rehearsal); default RCCL ("nccl")
     be = backend or os.environ.get("PATHNET_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if world <= 1:
+        os.environ.setdefault("MASTER_PORT", "29531")
     if not dist.is_initialized():
         if be == "nccl":
             dist.init_process_group(be, rank=rank, world_size=world, device_id=dev)
         else:
             dist.init_process_group(be, rank=rank, world_size=world)
-    return DistContext(rank, world, dev.index if dev.type == "cuda" else local_rank, be, dev)
+    return DistContext(rank, world, dev.index if dev.type == "cuda" else local_rank, be, dev, forced=world <= 1)

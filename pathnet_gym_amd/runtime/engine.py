@@ -375,6 +375,8 @@ class HipEngine:
         self.grad_flat[tn:] += st.flat.grad[tn:]
         st.flat.grad = None
         self._fitness_update()
+        if self.hip.x3:
+            self.hip.fold_x3_status(self.counters[3:4])
         self.lstm_state = (h.detach(), c.detach())
 
     def _rollout_backward_body(self, part: Optional[str] = None):
@@ -396,6 +398,9 @@ class HipEngine:
                 self._env_step(t)
             self._forward_step(T, greedy=True)
         self._fitness_update()
+        if hp.x3:
+            # fp16-pair range flags of this rollout (+ the last weight refresh) -> the all-reduced counters slot 3
+            hp.fold_x3_status(self.counters[3:4])
         self.stats.zero_()
         _lib.call("launch_a2c_grad", self.logits.data_ptr(), self.values.data_ptr(), self.actions.data_ptr(),
                   self.rewards.data_ptr(), self.dones.data_ptr(), self.values[T].data_ptr(), T, B, self.A,

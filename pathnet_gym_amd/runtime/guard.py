@@ -32,6 +32,26 @@ class NonFiniteError(RuntimeError):
     pass
 
 
+class X3RangeError(FloatingPointError):
+    """fp32x (split fp16 pairs): a value left the fp16 range.  Bit 0 of the status: a first-layer weight scaled by
+    2^8 reached 32768 (its pair no longer represents it); bit 1: an activation written as an fp16 pair reached 65504.
+    The status travels in the update's all-reduced counters, so every rank raises together."""
+
+    def __init__(self, status: float, update: int, world: int = 1):
+        self.status = status
+        bits = int(status) if world == 1 else -1
+        what = []
+        if bits < 0:
+            what.append(f"status sum {status:g} over {world} ranks")
+        else:
+            if bits & 1:
+                what.append("a first-layer weight x 2^8 left the fp16 range (|W| >= 128)")
+            if bits & 2:
+                what.append("an activation stored as an fp16 pair reached 65504")
+        super().__init__(f"fp32x range overflow at update {update}: " + "; ".join(what)
+                         + " -- use compute_dtype='fp32' for this model / data scale")
+
+
 class NonFiniteGuard:
     def __init__(self, max_consecutive: int = 3):
         self.max_consecutive = max_consecutive

@@ -139,7 +139,7 @@ def test_two_gloo_ranks_on_one_gpu_hip_engine_device_ga_pipelined(hip_lib):
 # ---------------------------------------------------------------------------------------------------------------
 # overlapped all-reduce (TrainConfig.overlap_allreduce) and 4 ranks with tournaments firing
 # ---------------------------------------------------------------------------------------------------------------
-def _overlap_worker(rank, world, port, q, updates, trace_path):
+def _overlap_worker(rank, world, port, q, updates, trace_path, dtype="fp32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), PATHNET_DIST_BACKEND="gloo")
     torch.set_num_threads(2)
@@ -156,7 +156,10 @@ def _overlap_worker(rank, world, port, q, updates, trace_path):
             cfg.ga.concurrent_tournaments = 2
             cfg.ga.fitness_window = 2           # small window: tournaments fire during the run
             cfg.net.N = 2
-            cfg.compute_dtype = "fp32"          # fixed-order reductions: bit-reproducible, so the modes compare bitwise
+            # fp32: fixed-order reductions, bit-reproducible, so the modes compare bitwise; fp32x (the bench engine:
+            # frame ring, float atomics in the weight gradients) compares to its budget
+            cfg.compute_dtype = dtype
+            cfg.frame_ring = dtype == "fp32x"
             cfg.overlap_allreduce = mode == "overlap"
             tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
             tr.env.max_episode_steps = 6
@@ -197,11 +200,12 @@ def _overlap_worker(rank, world, port, q, updates, trace_path):
         q.put((rank, {"error": traceback.format_exc()}))
 
 
-def _run_ranks(world, updates, trace_path=None):
+def _run_ranks(world, updates, trace_path=None, dtype="fp32"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_overlap_worker, args=(r, world, port, q, updates, trace_path)) for r in range(world)]
+    ps = [ctx.Process(target=_overlap_worker, args=(r, world, port, q, updates, trace_path, dtype))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=300) for _ in ps)
@@ -228,6 +232,84 @@ def test_overlapped_allreduce_is_bit_equal_to_serial(hip_lib):
         assert all(x["b1_issue"] <= x["tail_enqueue"] <= x["b_all_done"] for x in log)
         assert sum(x["tail_enqueue"] < x["b1_done"] for x in log) >= 5      # tail issued before bucket 1 finished
     assert np.array_equal(res[0]["overlap"]["flat"], res[1]["overlap"]["flat"])
+
+
+def test_overlapped_allreduce_fp32x_matches_serial_and_replicas_agree(hip_lib):
+    """The bench engine (fp32x, frame ring) on 2 ranks: the overlapped split exchange vs the single bucket within the
+    fp32x budget (float atomics: not bitwise run to run), and within each mode the two replicas bit-identical (every
+    rank applies the same all-reduced gradient)."""
+    res = _run_ranks(2, 8, dtype="fp32x")
+    for r in range(2):
+        o, s = res[r]["overlap"], res[r]["serial"]
+        d = np.linalg.norm(o["flat"] - s["flat"]) / np.linalg.norm(s["flat"])
+        assert d < 1e-5, d
+        assert res[r]["split_n"][0] > 0 and res[r]["split_n"][1] > 0
+    for mode in ("overlap", "serial"):
+        assert np.array_equal(res[0][mode]["flat"], res[1][mode]["flat"]), mode
+        assert np.array_equal(res[0][mode]["geno"], res[1][mode]["geno"]), mode
+
+
+def _strong_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), PATHNET_DIST_BACKEND="gloo")
+    torch.set_num_threads(2)
+    try:
+        from pathnet_gym_amd.parallel.dist import init_distributed
+        ctx = init_distributed()
+        q.put((rank, _strong_run(ctx)))
+        ctx.destroy()
+    except Exception:   # pragma: no cover
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+def _strong_run(ctx, updates=8):
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.config import preset
+    cfg = preset("pong")
+    cfg.paths_total, cfg.envs_per_path, cfg.a2c.t_max = 8, 16, 4
+    cfg.ga.backend = "device"
+    cfg.ga.concurrent_tournaments = 2
+    cfg.ga.fitness_window = 2
+    cfg.net.N = 2
+    cfg.compute_dtype = "fp32"
+    tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
+    tr.env.max_episode_steps = 6
+    hist = []
+    for _ in range(updates):
+        st = tr.update()
+        hist.append((st.episodes, st.tournaments))
+    tr.flush()
+    torch.cuda.synchronize()
+    return {"flat": tr.model.store.flat.detach().cpu().numpy().copy(), "geno": tr.pop.genotypes.copy(),
+            "gen": tr.pop.generation, "step": tr.global_step, "P": tr.P, "hist": hist}
+
+
+def test_strong_scaling_two_ranks_reproduce_one_gpu_hip_engine(hip_lib):
+    """Strong scaling on the HIP engine (fp32, device GA, pipelined, overlapped exchange): 2 gloo ranks x 4 paths
+    (paths_total = 8) against one process with the 8 paths: same env streams and sampled actions (keyed by the global
+    env index), the same GA decisions; weights equal up to the gradient's summation order."""
+    from pathnet_gym_amd.parallel.dist import DistContext
+    one = _strong_run(DistContext(device=torch.device("cuda", 0)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_strong_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r in range(2):
+        assert "error" not in res[r], res[r].get("error")
+        assert res[r]["P"] == 4
+    two = res[0]
+    assert one["P"] == 8 and one["gen"] > 0
+    assert two["gen"] == one["gen"] and two["step"] == one["step"] and two["hist"] == one["hist"]
+    assert np.array_equal(two["geno"], one["geno"])
+    d = np.linalg.norm(two["flat"] - one["flat"]) / np.linalg.norm(one["flat"])
+    assert d < 1e-5, d
+    assert np.array_equal(res[0]["flat"], res[1]["flat"])
 
 
 def test_four_gloo_ranks_tournaments_fire_and_replicas_agree(hip_lib):

@@ -321,6 +321,65 @@ def test_heads_fwd_action_and_feature_widths(hip_lib, A, F):
     assert torch.equal(actions.long(), logits.argmax(-1))
 
 
+def test_heads_sampling_row_base_and_torch_keyed_sampler(hip_lib):
+    """Sampling is keyed by the GLOBAL sample index (row_base + b): a launch over rows [k, B) with row_base = k draws
+    what the full launch drew for those rows (strong scaling: a rank's envs sample like one GPU's), and the torch
+    sampler of the CPU backend (a2c_math.sample_actions_keyed) reproduces the kernel's draws."""
+    from pathnet_gym_amd.algo.a2c_math import sample_actions_keyed
+    cfg = PathNetConfig(L=2, M=4, N=2, input_shape=(4,), layers=[LayerSpec("fc", 64), LayerSpec("fc", 128)],
+                        trunk_scale="none", num_actions=6)
+    P, E = 4, 16
+    m = make_model(cfg, P, random_masks(P, cfg.L, cfg.M, cfg.N, with_edge=False))
+    B = P * E
+    feat = torch.randn(B, 128, device=DEV).to(torch.bfloat16)
+    ctr = torch.full((1,), 3, dtype=torch.int64, device=DEV)
+    outs = []
+    for k in (0, 16):
+        logits = torch.zeros(B - k, 6, device=DEV)
+        values = torch.zeros(B - k, device=DEV)
+        actions = torch.zeros(B - k, dtype=torch.int32, device=DEV)
+        m.hip.heads_fwd(feat[k:].contiguous(), logits, values, actions, 99, ctr, 2, 5, row_base=k)
+        outs.append((logits, actions))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[1][1], outs[0][1][16:])
+    ta = sample_actions_keyed(outs[0][0], 99, 3 * 5 + 2, 0)
+    agree = (ta.cpu() == outs[0][1].long().cpu()).float().mean().item()
+    assert agree > 0.98, agree            # __logf vs torch.log: only near-ties may differ
+
+
+@pytest.mark.parametrize("rows", [32, 128])
+def test_heads_bwd_row_chunks_match_oracle(hip_lib, rows):
+    """heads_set_bwd_rows(32) (1 280 workgroups at the bench shape) and the default 128-row chunks against the fp32
+    oracle at an N that is not a multiple of 32."""
+    from pathnet_gym_amd.models.pathnet import ParamStore
+    from pathnet_gym_amd.ops import _lib
+    cfg = small_pixel_cfg()
+    P = 2
+    m = make_model(cfg, P, random_masks(P, cfg.L, cfg.M, cfg.N, with_edge=False))
+    A = cfg.num_actions
+    N = 3 * 64 + 21
+    feat = (torch.randn(N, 256, device=DEV) * 0.5).to(torch.bfloat16)
+    dlog = torch.randn(N, A, device=DEV) * 0.1
+    dval = torch.randn(N, device=DEV) * 0.1
+    gflat = torch.zeros_like(m.store.flat, requires_grad=False)
+    dfeat = torch.zeros(N, 256, device=DEV)
+    _lib.lib().heads_set_bwd_rows(rows)
+    try:
+        m.hip.heads_bwd(feat, dlog, dval, gflat, dfeat)
+        torch.cuda.synchronize()
+    finally:
+        _lib.lib().heads_set_bwd_rows(128)
+    flat = m.store.flat.detach().clone().requires_grad_(True)
+    st = ParamStore(cfg, DEV, flat=flat)
+    fx = feat.float().requires_grad_(True)
+    l2, v2 = heads_ref(st, fx)
+    ((l2 * dlog).sum() + (v2 * dval).sum()).backward()
+    assert rel(dfeat, fx.grad) < 1e-4
+    for name in ("policy.weight", "policy.bias", "value.weight", "value.bias"):
+        s = m.store.layout.by_name[name]
+        assert rel(gflat[s.offset:s.offset + s.numel], flat.grad[s.offset:s.offset + s.numel]) < 1e-4, (rows, name)
+
+
 def test_rmsprop_kernel_matches_torch(hip_lib):
     from pathnet_gym_amd.algo.optim import RMSPropTF
     from pathnet_gym_amd.runtime.engine import HipEngine

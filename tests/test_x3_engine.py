@@ -387,3 +387,63 @@ def test_x3_fc_dgrad_gemm_matches_streaming_kernel(x3_rollout, l):
     print(f"fc layer {l} dgrad GEMM vs streaming: rel {e:.2e}, weight gradient rel {rel(gws[1], gws[0]):.2e}")
     assert e < 1e-6, e
     assert rel(gws[1], gws[0]) < 1e-6
+
+
+def _shipped_trainer(paths=3, envs=16, tmax=4, seed=1):
+    """The bench path at a small shape: fp32x, frame ring, hipGraph capture + replay, device GA, pipelined."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = paths, envs, tmax
+    cfg.compute_dtype = "fp32x"
+    cfg.frame_ring = True
+    cfg.use_graph = True
+    cfg.ga.backend = "device"
+    cfg.seed = seed
+    tr = PathNetTrainer(cfg, device=DEV)
+    assert tr.engine.ring and tr.engine.use_graph and tr.pipelined
+    return tr
+
+
+def test_x3_shipped_graph_path_gradient_vs_plain_fp32_oracle(hip_lib):
+    """What the bench runs: eager first update + capture, graph replays, then one more replay of the captured rollout
+    graph whose gradient is compared against the plain fp32 autograd oracle on the same stored rollout."""
+    tr = _shipped_trainer()
+    eng = tr.engine
+    tr.env.max_episode_steps = 5                 # episode resets inside the rollouts
+    for _ in range(4):
+        tr.update()
+    tr.flush()
+    assert eng.g_rollout is not None and eng.g_opt is not None
+    eng.rollout_backward()                       # a replay of the captured rollout + backward graph
+    torch.cuda.synchronize()
+    assert eng.dones.any()
+    g_ref = _oracle_grad(tr, eng)
+    err = layer_errors(tr, eng.grad_flat, g_ref)
+    print("fp32x shipped graph path vs fp32 oracle, per layer:", {k: f"{v:.2e}" for k, v in err.items()})
+    for k, v in err.items():
+        assert v < X3_LAYER_TOL, (k, v)
+
+
+@pytest.mark.parametrize("what", ["activation", "weight"])
+def test_x3_range_overflow_raises_named_error(hip_lib, what):
+    """fp16-pair range guard: an fc activation driven past 65504 (bias 1e5) or a first-layer weight past 128 (x 2^8
+    = 32768) must surface as X3RangeError naming the cause, through the all-reduced counters of the graph path."""
+    from pathnet_gym_amd.runtime.guard import X3RangeError
+    tr = _shipped_trainer()
+    tr.update()
+    tr.update()
+    tr.flush()                                   # in range so far
+    st = tr.model.store
+    with torch.no_grad():
+        for j in range(tr.cfg.net.M):
+            if what == "activation":
+                s = st.layout.by_name[f"layer3.module{j}.bias"]
+                st.flat[s.offset:s.offset + s.numel] = 1e5
+            else:
+                s = st.layout.by_name[f"layer0.module{j}.weight"]
+                st.flat[s.offset:s.offset + 4] = 1e3
+    tr.model.hip.refresh_weights()
+    with pytest.raises(X3RangeError, match="activation" if what == "activation" else "first-layer weight"):
+        for _ in range(3):
+            tr.update()
+        tr.flush()
