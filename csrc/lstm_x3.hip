@@ -1,0 +1,353 @@
+// Fused LSTM cell in the fp32-accurate split-operand mode (TrainConfig.compute_dtype = "fp32x"): the reference's
+// default network, BasicLSTMCell(256) unrolled over the rollout (game_ac_network.py:397-416, constants.py:30 USE_LSTM),
+// at the reference's precision.
+//
+// Same cell, batching and launch structure as csrc/lstm.hip (TF gate order i, j, f, o; forget_bias = 1; state reset
+// by the previous step's done flag); what changes is the operand precision, as in csrc/trunk_x3.hip:
+//   forward  z = [x | h] K + b : fp16 pairs, x = hi + lo (22 significant bits) against the fp16 pair of K * 2^8,
+//                                three MFMAs per product (hi*hi + hi*lo + lo*hi), fp32 accumulation; x (the fp32
+//                                trunk output) and h / c / the saved gates stay fp32
+//   backward dz K^T, dK = [x|h]^T dz : bf16 pairs (bf16's exponent range for the gradients), three MFMAs
+// Per-layer error against a plain fp32 oracle: tests/test_x3_engine.py (<= 2e-5, like the trunk).
+// Range: an input of the forward GEMM at or beyond fp16's 65504, or a kernel weight whose 2^8 multiple reaches
+// 32768, sets the engine's fp32x status word (bits 2 / 1, X3RangeError on the host).
+#include "common.h"
+
+namespace {
+
+#define LX3_SHIFT 8
+
+DEVI float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+DEVI float tanh_f(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  const float t = (1.f - e) / (1.f + e);
+  return copysignf(t, x);
+}
+DEVI uint16_t f2h(float v) { return __builtin_bit_cast(uint16_t, (_Float16)v); }
+DEVI float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+
+// 8 fp32 -> fp16 pair (hi = rnd(v), lo = rnd(v - hi))
+DEVI void split8h(const float (&v)[8], s8v& hi, s8v& lo) {
+  _Float16 h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = (_Float16)v[j];
+    l[j] = (_Float16)(v[j] - (float)h[j]);
+  }
+  __builtin_memcpy(&hi, h, 16);
+  __builtin_memcpy(&lo, l, 16);
+}
+// 8 fp32 -> bf16 pair
+DEVI void split8b(const float (&v)[8], s8v& hi, s8v& lo) {
+  bf16_t h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = f2bf(v[j]);
+    l[j] = f2bf(v[j] - bf2f(h[j]));
+  }
+  __builtin_memcpy(&hi, h, 16);
+  __builtin_memcpy(&lo, l, 16);
+}
+DEVI void ld8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+DEVI void st8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+// products from hi / lo pairs, the two small cross terms first (csrc/trunk_x3.hip mma3 / mma3h)
+DEVI f4v mma3h(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
+  c = mfma16_f16(al, bh, c);
+  c = mfma16_f16(ah, bl, c);
+  return mfma16_f16(ah, bh, c);
+}
+DEVI f4v mma3(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
+  c = mfma16(al, bh, c);
+  c = mfma16(ah, bl, c);
+  return mfma16(ah, bh, c);
+}
+
+// ---------------------------------------------------------------------------
+// forward: grid (ceil(B/64), H/16), 256 threads; wave w owns rows 16w..16w+15 of the 64-row tile and the 4 gate
+// blocks of 16 units (KpT2 columns permuted tile-major like csrc/lstm.hip: p = (u/16)*64 + g*16 + u%16).
+// X: fp32 [B][ldx] (features), hprev / cprev fp32 [B][H]; KpT2: fp16 [2][4H][KK] (hi, lo of K^T * 2^8).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
+    const float* __restrict__ X, int ldx, const float* __restrict__ hprev, const float* __restrict__ cprev,
+    const uint8_t* __restrict__ prev_done, const uint16_t* __restrict__ KpT2, const float* __restrict__ flat,
+    long b_off, float* __restrict__ hout, float* __restrict__ cout, float* __restrict__ gates,
+    float* __restrict__ xh, uint32_t* __restrict__ status, int F, int H, int B) {
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int row0 = blockIdx.x * 64 + w * 16;
+  if (row0 >= B) return;
+  const int ut = blockIdx.y;
+  const int KK = F + H;
+  const long plane = (long)4 * H * KK;
+  const int arow = row0 + c16;
+  const bool av = arow < B;
+  const bool keep = av && !(prev_done && prev_done[arow]);
+  const bool wr_xh = xh != nullptr && blockIdx.y == 0;
+  f4v acc[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) acc[g] = {0.f, 0.f, 0.f, 0.f};
+  bool bad = false;
+  const uint16_t* Bp = KpT2 + (long)(ut * 64 + c16) * KK + 8 * grp;
+  for (int k0 = 0; k0 < KK; k0 += 32) {
+    const int k = k0 + 8 * grp;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (av) {
+      if (k < F) ld8(X + (long)arow * ldx + k, v);
+      else if (keep) ld8(hprev + (long)arow * H + (k - F), v);
+    }
+    if (wr_xh && av) st8(xh + (long)arow * KK + k, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bad |= !(fabsf(v[j]) < 65504.f);
+    s8v ah, al;
+    split8h(v, ah, al);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const long o = (long)g * 16 * KK + k0;
+      const s8v bh = *reinterpret_cast<const s8v*>(Bp + o);
+      const s8v bl = *reinterpret_cast<const s8v*>(Bp + plane + o);
+      acc[g] = mma3h(ah, al, bh, bl, acc[g]);
+    }
+  }
+  if (bad && status) atomicOr(status, 2u);
+  const float sc = 1.0f / (float)(1 << LX3_SHIFT);
+  const int u = ut * 16 + c16;
+  const float bi = flat[b_off + u], bj = flat[b_off + H + u], bff = flat[b_off + 2 * H + u],
+              bo = flat[b_off + 3 * H + u];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = row0 + 4 * grp + r;
+    if (row >= B) continue;
+    const bool kp = !(prev_done && prev_done[row]);
+    const float c0 = kp ? cprev[(long)row * H + u] : 0.f;
+    const float si = sigm(acc[0][r] * sc + bi);
+    const float tj = tanh_f(acc[1][r] * sc + bj);
+    const float sf = sigm(acc[2][r] * sc + bff + 1.0f);
+    const float so = sigm(acc[3][r] * sc + bo);
+    const float c = c0 * sf + si * tj;
+    const float h = tanh_f(c) * so;
+    cout[(long)row * H + u] = c;
+    hout[(long)row * H + u] = h;
+    if (gates) {
+      float* gr = gates + (long)row * 4 * H;
+      gr[u] = si;
+      gr[H + u] = tj;
+      gr[2 * H + u] = sf;
+      gr[3 * H + u] = so;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward GEMM: out[b][n] = sum_p dz[b][p] K[n][p]; n < F -> dx, n >= F -> dh_prev.  Kb2: bf16 [2][KK][4H].
+// grid (ceil(B/64), KK/64); wave w: 16 rows x 64 columns (4 blocks of 16)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
+    const float* __restrict__ dz, const bf16_t* __restrict__ Kb2, float* __restrict__ dx, int lddx,
+    float* __restrict__ dh_prev, int F, int H, int B) {
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int row0 = blockIdx.x * 64 + w * 16;
+  if (row0 >= B) return;
+  const int n0 = blockIdx.y * 64;
+  const int G4 = 4 * H;
+  const long plane = (long)(F + H) * G4;
+  const int arow = row0 + c16;
+  const bool av = arow < B;
+  f4v acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
+  for (int p0 = 0; p0 < G4; p0 += 32) {
+    const int p = p0 + 8 * grp;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (av) ld8(dz + (long)arow * G4 + p, v);
+    s8v ah, al;
+    split8b(v, ah, al);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long o = (long)(n0 + j * 16 + c16) * G4 + p;
+      const s8v bh = *reinterpret_cast<const s8v*>(Kb2 + o);
+      const s8v bl = *reinterpret_cast<const s8v*>(Kb2 + plane + o);
+      acc[j] = mma3(ah, al, bh, bl, acc[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + j * 16 + c16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 4 * grp + r;
+      if (row >= B) continue;
+      if (n < F) dx[(long)row * lddx + n] = acc[j][r];
+      else dh_prev[(long)row * H + (n - F)] = acc[j][r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient: dK[n][p] += sum_r xh[r][n] dz[r][p] over a chunk of rows (xh, dz fp32, split into bf16 pairs
+// while staging in LDS); db[p] += sum_r dz[r][p] (blockIdx.x == 0 tiles).  grid (KK/64, 4H/64, nchunks)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
+    const float* __restrict__ xh, const float* __restrict__ dz, float* __restrict__ grad, long k_off, long b_off,
+    int F, int H, long R, int rows_per_chunk) {
+  constexpr int S = 64 + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][32 * S];
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][32 * S];
+  __shared__ float dbias[64];
+  const int KK = F + H, G4 = 4 * H;
+  const int n0b = blockIdx.x * 64, p0b = blockIdx.y * 64;
+  const long r_beg = (long)blockIdx.z * rows_per_chunk;
+  const long r_end = min(R, r_beg + rows_per_chunk);
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
+  const bool do_bias = blockIdx.x == 0;
+  if (tid < 64) dbias[tid] = 0.f;
+  f4v acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) { acc[a][0] = {0.f, 0.f, 0.f, 0.f}; acc[a][1] = {0.f, 0.f, 0.f, 0.f}; }
+  float bpart[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int srow = tid >> 3, sc = (tid & 7) * 8;
+  const int mt0 = 2 * (w >> 1), nt0 = 2 * (w & 1);
+  for (long rb = r_beg; rb < r_end; rb += 32) {
+    const long r = rb + srow;
+    float xv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (r < r_end) {
+      ld8(xh + r * KK + n0b + sc, xv);
+      ld8(dz + r * G4 + p0b + sc, gv);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) bpart[c] += gv[c];
+    }
+    s8v xhi, xlo, ghi, glo;
+    split8b(xv, xhi, xlo);
+    split8b(gv, ghi, glo);
+    *reinterpret_cast<s8v*>(Xs[0] + srow * S + sc) = xhi;
+    *reinterpret_cast<s8v*>(Xs[1] + srow * S + sc) = xlo;
+    *reinterpret_cast<s8v*>(Gs[0] + srow * S + sc) = ghi;
+    *reinterpret_cast<s8v*>(Gs[1] + srow * S + sc) = glo;
+    __syncthreads();
+    s8v af[2][2], bf[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const s4v v0 = lds_tr16(Xs[h] + (8 * grp + q) * S + (mt0 + i) * 16 + 4 * pp);
+        const s4v v1 = lds_tr16(Xs[h] + (8 * grp + 4 + q) * S + (mt0 + i) * 16 + 4 * pp);
+        af[h][i] = (s8v){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        const s4v u0 = lds_tr16(Gs[h] + (8 * grp + q) * S + (nt0 + i) * 16 + 4 * pp);
+        const s4v u1 = lds_tr16(Gs[h] + (8 * grp + 4 + q) * S + (nt0 + i) * 16 + 4 * pp);
+        bf[h][i] = (s8v){u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma3(af[0][i], af[1][i], bf[0][jj], bf[1][jj], acc[i][jj]);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0b + (mt0 + i) * 16 + 4 * grp + r;
+        const int p = p0b + (nt0 + jj) * 16 + i16;
+        atomicAdd(&grad[k_off + (long)n * G4 + p], acc[i][jj][r]);
+      }
+  if (do_bias) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) atomicAdd(&dbias[sc + c], bpart[c]);
+    __syncthreads();
+    if (tid < 64) atomicAdd(&grad[b_off + p0b + tid], dbias[tid]);
+  }
+}
+
+// operand copies of the fp32 master kernel: KpT2 = fp16 pair of K^T * 2^8 (permuted, forward), Kb2 = bf16 pair of K
+// (TF layout, backward); status |= 1 when a scaled weight leaves the fp16 range
+__global__ void lstm_refresh_x3_kernel(const float* __restrict__ flat, long k_off, int F, int H,
+                                       uint16_t* __restrict__ KpT2, bf16_t* __restrict__ Kb2,
+                                       uint32_t* __restrict__ status) {
+  const int KK = F + H, G4 = 4 * H;
+  const long n_el = (long)KK * G4;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n_el) return;
+  const int n = (int)(idx / G4), col = (int)(idx - (long)n * G4);   // TF [n][col], col = g*H + u
+  const float v = flat[k_off + idx];
+  const bf16_t bh = f2bf(v);
+  Kb2[idx] = bh;
+  Kb2[n_el + idx] = f2bf(v - bf2f(bh));
+  const float x = v * (float)(1 << LX3_SHIFT);
+  const uint16_t hh = f2h(x);
+  const int g = col / H, u = col - g * H;
+  const int p = (u >> 4) * 64 + g * 16 + (u & 15);
+  KpT2[(long)p * KK + n] = hh;
+  KpT2[n_el + (long)p * KK + n] = f2h(x - h2f(hh));
+  if (!(fabsf(x) < 32768.f) && status) atomicOr(status, 1u);
+}
+
+// fp32 state carried into the next rollout: slot0 = slotT * (1 - done_last)
+__global__ void lstm_carry_f32_kernel(const float* __restrict__ hT, const float* __restrict__ cT,
+                                      const uint8_t* __restrict__ done_last, float* __restrict__ h0,
+                                      float* __restrict__ c0, int H, int B) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)B * H) return;
+  const bool kp = !done_last[idx / H];
+  h0[idx] = kp ? hT[idx] : 0.f;
+  c0[idx] = kp ? cT[idx] : 0.f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int launch_lstm_fwd_x3(const float* X, int ldx, const float* hprev, const float* cprev, const uint8_t* prev_done,
+                       const void* KpT2, const float* flat, long b_off, float* hout, float* cout, float* gates,
+                       float* xh, void* status, int F, int H, int B, hipStream_t stream) {
+  if (ldx <= 0 || F <= 0 || H <= 0 || B <= 0 || b_off < 0) return -22;
+  if (F % 64 != 0 || H % 64 != 0 || ldx % 8 != 0 || ldx < F) return -1;
+  dim3 grid((B + 63) / 64, H / 16);
+  lstm_fwd_x3_kernel<<<grid, 256, 0, stream>>>(X, ldx, hprev, cprev, prev_done, (const uint16_t*)KpT2, flat, b_off,
+                                               hout, cout, gates, xh, (uint32_t*)status, F, H, B);
+  return (int)hipGetLastError();
+}
+
+int launch_lstm_bwd_gemm_x3(const float* dz, const void* Kb2, float* dx, int lddx, float* dh_prev, int F, int H,
+                            int B, hipStream_t stream) {
+  if (lddx <= 0 || F <= 0 || H <= 0 || B <= 0) return -22;
+  if (F % 64 != 0 || H % 64 != 0 || lddx < F) return -1;
+  dim3 grid((B + 63) / 64, (F + H) / 64);
+  lstm_bwd_gemm_x3_kernel<<<grid, 256, 0, stream>>>(dz, (const bf16_t*)Kb2, dx, lddx, dh_prev, F, H, B);
+  return (int)hipGetLastError();
+}
+
+int launch_lstm_wgrad_x3(const float* xh, const float* dz, float* grad, long k_off, long b_off, int F, int H, long R,
+                         int rows_per_chunk, hipStream_t stream) {
+  if (F <= 0 || H <= 0 || R <= 0 || rows_per_chunk <= 0 || k_off < 0 || b_off < 0) return -22;
+  if (F % 64 != 0 || H % 64 != 0 || rows_per_chunk % 32 != 0) return -1;
+  dim3 grid((F + H) / 64, (4 * H) / 64, (unsigned)((R + rows_per_chunk - 1) / rows_per_chunk));
+  lstm_wgrad_x3_kernel<<<grid, 256, 0, stream>>>(xh, dz, grad, k_off, b_off, F, H, R, rows_per_chunk);
+  return (int)hipGetLastError();
+}
+
+int launch_lstm_refresh_x3(const float* flat, long k_off, int F, int H, void* KpT2, void* Kb2, void* status,
+                           hipStream_t stream) {
+  if (F <= 0 || H <= 0 || k_off < 0) return -22;
+  const long n = (long)(F + H) * 4 * H;
+  lstm_refresh_x3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(flat, k_off, F, H, (uint16_t*)KpT2,
+                                                                          (bf16_t*)Kb2, (uint32_t*)status);
+  return (int)hipGetLastError();
+}
+
+int launch_lstm_carry_f32(const float* hT, const float* cT, const uint8_t* done_last, float* h0, float* c0, int H,
+                          int B, hipStream_t stream) {
+  if (H <= 0 || B <= 0) return -22;
+  const long n = (long)B * H;
+  lstm_carry_f32_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(hT, cT, done_last, h0, c0, H, B);
+  return (int)hipGetLastError();
+}
+}

@@ -73,6 +73,11 @@ _SIGS = {
     "launch_lstm_wgrad": [P, P, P, c_long, c_long, c_int, c_int, c_long, c_int, P],
     "launch_lstm_refresh": [P, c_long, c_int, c_int, P, P, P],
     "launch_lstm_carry": [P, P, P, P, P, c_int, c_int, P],
+    "launch_lstm_fwd_x3": [P, c_int, P, P, P, P, P, c_long, P, P, P, P, P, c_int, c_int, c_int, P],
+    "launch_lstm_bwd_gemm_x3": [P, P, P, c_int, P, c_int, c_int, c_int, P],
+    "launch_lstm_wgrad_x3": [P, P, P, c_long, c_long, c_int, c_int, c_long, c_int, P],
+    "launch_lstm_refresh_x3": [P, c_long, c_int, c_int, P, P, P, P],
+    "launch_lstm_carry_f32": [P, P, P, P, P, c_int, c_int, P],
     "fast_conv_set_slab": [c_int],
     "fast_conv_set_slab_fwd": [c_int],
     "fast_conv_set_dgrad_mfma": [c_int],

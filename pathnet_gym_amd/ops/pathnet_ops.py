@@ -188,15 +188,19 @@ class HipPathNet:
         self.inv_cnt = torch.zeros(self.L, self.M, dtype=torch.int32, device=dev)
         lay_h = lay.heads
         self.heads_off = lay_h
-        # fused LSTM cell (csrc/lstm.hip): bf16 copies of the fp32 master kernel
+        # fused LSTM cell: csrc/lstm.hip (bf16 copies of the fp32 master kernel) or, in fp32x, csrc/lstm_x3.hip (fp16 /
+        # bf16 hi+lo pairs, fp32 state: the reference's default network at its precision).  fp32 (deterministic) keeps
+        # the hybrid autograd LSTM.
         self.lstm = None
-        if cfg.use_lstm and not self.deterministic and not self.x3:   # fp32 / fp32x / deterministic: hybrid LSTM
+        if cfg.use_lstm and not self.deterministic:
             ls = lay.lstm
             F, H = ls["din"], ls["H"]
             if F % 64 == 0 and H % 64 == 0:
-                self.lstm = dict(F=F, H=H, k_off=ls["kernel"], b_off=ls["bias"],
-                                 KpT=torch.zeros(4 * H, F + H, dtype=torch.bfloat16, device=dev),
-                                 Kb=torch.zeros(F + H, 4 * H, dtype=torch.bfloat16, device=dev))
+                pl = (2,) if self.x3 else ()
+                self.lstm = dict(F=F, H=H, k_off=ls["kernel"], b_off=ls["bias"], x3=self.x3,
+                                 KpT=torch.zeros(pl + (4 * H, F + H), dtype=torch.float16 if self.x3 else torch.bfloat16,
+                                                 device=dev),
+                                 Kb=torch.zeros(pl + (F + H, 4 * H), dtype=torch.bfloat16, device=dev))
         # frame-ring input for the first layer (runtime/engine.py): channel-major bf16 weights; fp32x reads the ring
         # into its packed LDS band / slab (csrc/trunk_x3.hip RING) and keeps its own weight pairs
         g0 = self.geoms[0]
@@ -296,7 +300,9 @@ class HipPathNet:
                 _lib.call("x3_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
                           self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), 1, self.x3_status.data_ptr(), _lib.stream())
             if self.lstm is not None:
-                raise RuntimeError("fp32x runs the LSTM on the hybrid path")
+                ls = self.lstm
+                _lib.call("launch_lstm_refresh_x3", flat.data_ptr(), ls["k_off"], ls["F"], ls["H"], ls["KpT"].data_ptr(),
+                          ls["Kb"].data_ptr(), self.x3_status.data_ptr(), _lib.stream())
             return
         for l, g in enumerate(self.geoms):
             _lib.call("launch_refresh_weights_f32" if self.f32 else "launch_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
@@ -316,10 +322,28 @@ class HipPathNet:
                       ls["Kb"].data_ptr(), _lib.stream())
 
     # -- fused LSTM cell (csrc/lstm.hip) ------------------------------------------
+    @property
+    def lstm_dtype(self):
+        """dtype of the LSTM hidden state / saved [x | h] rows: fp32 in fp32x, bf16 otherwise."""
+        return torch.float32 if self.x3 else torch.bfloat16
+
     def lstm_fwd(self, x, hprev, cprev, prev_done, hout, cout, gates=None, xh=None):
-        """x [B,F] bf16, hprev [B,H] bf16, cprev [B,H] f32, prev_done [B] u8 or None -> hout/cout(/gates/xh)."""
+        """x [B,F], hprev [B,H] (bf16; fp32 in fp32x), cprev [B,H] f32, prev_done [B] u8 or None -> hout/cout
+        (/gates/xh)."""
         ls = self.lstm
         B = x.shape[0]
+        dt = self.lstm_dtype
+        _lib.check(x, self.feat_dtype, name="lstm x")
+        for t, nm in ((hprev, "hprev"), (hout, "hout")):
+            _lib.check(t, dt, numel=B * ls["H"], name=nm)
+        if xh is not None:
+            _lib.check(xh, dt, numel=B * (ls["F"] + ls["H"]), name="xh")
+        if ls["x3"]:
+            _lib.call("launch_lstm_fwd_x3", x.data_ptr(), x.shape[1], hprev.data_ptr(), cprev.data_ptr(),
+                      _lib.ptr(prev_done), ls["KpT"].data_ptr(), self.model.store.flat.data_ptr(), ls["b_off"],
+                      hout.data_ptr(), cout.data_ptr(), _lib.ptr(gates), _lib.ptr(xh), self.x3_status.data_ptr(),
+                      ls["F"], ls["H"], B, _lib.stream())
+            return
         _lib.call("launch_lstm_fwd", x.data_ptr(), x.shape[1], hprev.data_ptr(), cprev.data_ptr(),
                   _lib.ptr(prev_done), ls["KpT"].data_ptr(), self.model.store.flat.data_ptr(), ls["b_off"],
                   hout.data_ptr(), cout.data_ptr(), _lib.ptr(gates), _lib.ptr(xh), ls["F"], ls["H"], B,
@@ -333,18 +357,18 @@ class HipPathNet:
         _lib.call("launch_lstm_bwd_point", dh_heads.data_ptr(), _lib.ptr(dh_rec), _lib.ptr(dc_rec),
                   _lib.ptr(done_t), gates.data_ptr(), c_t.data_ptr(), c_prev.data_ptr(), _lib.ptr(prev_done),
                   dz.data_ptr(), dc_out.data_ptr(), ls["H"], B, st)
-        _lib.call("launch_lstm_bwd_gemm", dz.data_ptr(), ls["Kb"].data_ptr(), dx.data_ptr(), dx.shape[-1],
-                  dh_prev.data_ptr(), ls["F"], ls["H"], B, st)
+        _lib.call("launch_lstm_bwd_gemm_x3" if ls["x3"] else "launch_lstm_bwd_gemm", dz.data_ptr(), ls["Kb"].data_ptr(),
+                  dx.data_ptr(), dx.shape[-1], dh_prev.data_ptr(), ls["F"], ls["H"], B, st)
 
     def lstm_wgrad(self, xh, dz, grad_flat, rows_per_chunk: int = 2048):
         ls = self.lstm
         R = xh.numel() // (ls["F"] + ls["H"])
-        _lib.call("launch_lstm_wgrad", xh.data_ptr(), dz.data_ptr(), grad_flat.data_ptr(), ls["k_off"], ls["b_off"],
-                  ls["F"], ls["H"], R, rows_per_chunk, _lib.stream())
+        _lib.call("launch_lstm_wgrad_x3" if ls["x3"] else "launch_lstm_wgrad", xh.data_ptr(), dz.data_ptr(),
+                  grad_flat.data_ptr(), ls["k_off"], ls["b_off"], ls["F"], ls["H"], R, rows_per_chunk, _lib.stream())
 
     def lstm_carry(self, hT, cT, done_last, h0, c0):
-        _lib.call("launch_lstm_carry", hT.data_ptr(), cT.data_ptr(), done_last.data_ptr(), h0.data_ptr(),
-                  c0.data_ptr(), self.lstm["H"], h0.shape[0], _lib.stream())
+        _lib.call("launch_lstm_carry_f32" if self.lstm["x3"] else "launch_lstm_carry", hT.data_ptr(), cT.data_ptr(),
+                  done_last.data_ptr(), h0.data_ptr(), c0.data_ptr(), self.lstm["H"], h0.shape[0], _lib.stream())
 
     # ------------------------------------------------------------------
     def _fwd_ptrs(self, l: int, X, Y, bits, row0: int, p0: int, xrow0: int):

@@ -135,10 +135,11 @@ class HipEngine:
         self.lstm_state = model.init_state(B) if self.hybrid else None
         if self.lstm_hip:
             F, H = hp.lstm["F"], hp.lstm["H"]
-            self.hst = torch.zeros(T + 2, B, H, dtype=torch.bfloat16, device=dev)   # slot t = state entering step t
+            ldt = hp.lstm_dtype                  # bf16 (bf16 engine) or fp32 (fp32x: csrc/lstm_x3.hip)
+            self.hst = torch.zeros(T + 2, B, H, dtype=ldt, device=dev)   # slot t = state entering step t
             self.cst = torch.zeros(T + 2, B, H, device=dev)
             self.gates = torch.zeros(T, B, 4 * H, device=dev)
-            self.xh = torch.zeros(T, B, F + H, dtype=torch.bfloat16, device=dev)
+            self.xh = torch.zeros(T, B, F + H, dtype=ldt, device=dev)
             self.dz = torch.zeros(T, B, 4 * H, device=dev)
             self.dh_heads = torch.zeros(T, B, H, device=dev)
             self.dh_rec = torch.zeros(2, B, H, device=dev)

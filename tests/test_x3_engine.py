@@ -447,3 +447,88 @@ def test_x3_range_overflow_raises_named_error(hip_lib, what):
         for _ in range(3):
             tr.update()
         tr.flush()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# the reference's default network (BasicLSTMCell(256) after the L=4 trunk, constants.py:30) in fp32x:
+# csrc/lstm_x3.hip against a plain fp32 autograd oracle of the whole update
+# ---------------------------------------------------------------------------------------------------------------
+def _oracle_grad_lstm(tr, eng):
+    from pathnet_gym_amd.models.pathnet import lstm_cell_ref
+    cfg = tr.cfg
+    T, B = eng.T, eng.B
+    a2c = cfg.a2c
+    flat = tr.model.store.flat.detach().clone().requires_grad_(True)
+    st = ParamStore(cfg.net, DEV, flat=flat)
+    x = eng.obs_stacks().reshape((T + 1) * B, 160, 120, 4).float() / 255.0
+    mask = tr.model.mask.repeat_interleave(eng.E, 0).repeat(T + 1, 1, 1)
+    feat = trunk_forward_ref(st, x, mask).view(T + 1, B, -1)
+    k, bb = st.lstm()
+    h, c = eng.hst[0].float(), eng.cst[0].float()          # state entering step 0 (pre-masked by the carry)
+    hs = []
+    for t in range(T + 1):
+        if t > 0:
+            keep = (1.0 - eng.dones[t - 1].float())[:, None]
+            h, c = h * keep, c * keep
+        h, c = lstm_cell_ref(feat[t], h, c, k, bb)
+        hs.append(h)
+    hcat = torch.stack(hs).reshape((T + 1) * B, -1)
+    assert rel(hcat[:T * B], eng.hst[1:T + 1].reshape(T * B, -1)) < X3_LAYER_TOL
+    logits, values = heads_ref(st, hcat, tr.model.task)
+    assert rel(logits[:T * B], eng.logits[:T].reshape(-1, eng.A)) < 1e-5
+    assert rel(values, eng.values[:T + 1].reshape(-1)) < 1e-5
+    R, adv = nstep_returns(eng.rewards, eng.values[:T], eng.dones.bool(), eng.values[T], a2c.gamma,
+                           a2c.gae_lambda, a2c.reward_clip)
+    loss, _, _, _ = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(), R.reshape(-1),
+                             adv.reshape(-1), a2c.entropy_beta, a2c.value_coef,
+                             torch.full((T * B,), eng.weight, device=DEV))
+    loss.backward()
+    return flat.grad
+
+
+@pytest.fixture(scope="module", params=["eager", "graph"])
+def x3_lstm_rollout(hip_lib, request):
+    """The `reference` preset (L=4 trunk + LSTM 256, 18 actions) at a small shape in fp32x: the fused split-operand
+    LSTM (no autograd hybrid), frame ring, device GA; "graph": hipGraph capture + replays, the last replay compared."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("reference")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 4
+    cfg.compute_dtype = "fp32x"
+    cfg.frame_ring = True
+    cfg.use_graph = request.param == "graph"
+    cfg.ga.backend = "device"
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng = tr.engine
+    assert eng.lstm_hip and not eng.hybrid and eng.hst.dtype == torch.float32 and eng.ring
+    assert eng.use_graph == (request.param == "graph")
+    tr.env.max_episode_steps = 5
+    for _ in range(3 if cfg.use_graph else 1):
+        tr.update()
+    tr.flush()
+    if not cfg.use_graph:
+        tr.model.set_paths(masks_with_edges(3, cfg.net.L, cfg.net.M, cfg.net.N, seed=2))
+    else:
+        assert eng.g_rollout is not None
+    eng.rollout_backward()
+    torch.cuda.synchronize()
+    assert eng.dones.any()
+    return tr, eng, _oracle_grad_lstm(tr, eng), eng.grad_flat.clone()
+
+
+def test_x3_lstm_engine_gradient_vs_plain_fp32_oracle(x3_lstm_rollout):
+    tr, eng, g_ref, g_hip = x3_lstm_rollout
+    err = layer_errors(tr, g_hip, g_ref)
+    print("fp32x LSTM engine vs fp32 oracle, per layer:", {k: f"{v:.2e}" for k, v in err.items()})
+    assert "lstm" in err
+    for k, v in err.items():
+        assert v < X3_LAYER_TOL, (k, v)
+
+
+def test_x3_lstm_gradient_check_detects_a_two_percent_error(x3_lstm_rollout):
+    """Negative control: the LSTM kernel's (and bias') gradient scaled by 1.02 must fail the per-layer budget."""
+    tr, eng, g_ref, g_hip = x3_lstm_rollout
+    for name in ("lstm.kernel", "lstm.bias"):
+        s = tr.model.store.layout.by_name[name]
+        bad = g_hip.clone()
+        bad[s.offset:s.offset + s.numel] *= 1.02
+        assert layer_errors(tr, bad, g_ref)["lstm"] > X3_LAYER_TOL, name
