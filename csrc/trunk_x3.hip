@@ -1104,8 +1104,10 @@ DEVI s8v tr8(const bf16_t* p0, const bf16_t* p1) {
 // planes per thread and transposes them into the packed slab at LDS-write time (planes_to_px4).  The first-valid
 // channels of the workgroup's samples are staged in LDS once (a per-stage global byte load would sit in front of
 // the stage's X loads).
-template <class G, int OB, int PFM, bool RING = false>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restrict__ X, long xlo,
+// NCXP: column tiles per pass (X3_NCX = 3: paths of <= 6 active modules in one pass at 2 waves / SIMD; 2: <= 4
+// modules per pass -- the common N = 4 genotype -- with 16 fewer accumulator VGPRs, which fits 3 waves / SIMD)
+template <class G, int OB, int PFM, bool RING = false, int NCXP = X3_NCX>
+__global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(const void* __restrict__ X, long xlo,
                                                             const float* __restrict__ Gr,
                                                             const uint8_t* __restrict__ bits, float* __restrict__ grad,
                                                             long w_off, long b_off, int chunk,
@@ -1125,7 +1127,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
   __shared__ uint8_t fcs[FCS];
   constexpr bool XL = !G::U8;                       // bf16 input: lo plane too
   constexpr int NXP = XL ? 2 : 1;
-  constexpr int GS = X3_NCX * 16 + 8;
+  constexpr int GS = NCXP * 16 + 8;
   constexpr int NMT = G::KP / 16;
   constexpr int MPW = NMT / 4;
   constexpr int GROWS = SB::KS * 32;
@@ -1162,7 +1164,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
       const int ob = rho / G::WO, ow = rho - ob * G::WO;
       aoff[ks][hf] = ob * G::S * SB::RL + ow * SB::PS + 4 * pp;
     }
-  const int npass = (nct + X3_NCX - 1) / X3_NCX;
+  const int npass = (nct + NCXP - 1) / NCXP;
   using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
   auto run = [&](auto ncc, const int ct0) {
     constexpr int NC = decltype(ncc)::value;
@@ -1423,11 +1425,11 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_slab_x3(const void* __restr
     }
   };
   for (int pass = 0; pass < npass; ++pass) {
-    const int ct0 = pass * X3_NCX;
-    switch (min(X3_NCX, nct - ct0)) {
+    const int ct0 = pass * NCXP;
+    switch (min(NCXP, nct - ct0)) {
       case 1: run(std::integral_constant<int, 1>{}, ct0); break;
       case 2: run(std::integral_constant<int, 2>{}, ct0); break;
-      default: run(std::integral_constant<int, 3>{}, ct0); break;
+      default: run(std::integral_constant<int, (NCXP >= 3 ? 3 : 2)>{}, ct0); break;
     }
   }
   __syncthreads();
@@ -3326,6 +3328,9 @@ static int X3_FWD_DB = 0;      // bf16-activation conv forward: 1 = double-buffe
 // and 1 for the uint8 first layer (measured, steady-state window: conv1 2.63 (2) -> 2.32 ms (1), conv2 0.50 (2) vs
 // 0.52 ms (1); profiles/r3/kwin_x3_v4*.md)
 static int X3_WGRAD_PF = 3;
+// first-layer (frame ring) slab weight gradient: column tiles per pass (conv_wgrad_slab_x3 NCXP): 3 (2 waves / SIMD)
+// or 2 (3 waves / SIMD, a second pass for paths with > 4 active modules)
+static int X3_C1_WG_NCX = 3;
 // conv forward epilogue, bit 0: first layer, bit 1: the bf16-activation layers; set = swapped MFMA orientation
 // (conv_epi_sw; first layer also with the 1024-offset pixels folded into the bias), clear = rows-as-A
 static int X3_FWD_SW = 1;
@@ -3350,6 +3355,7 @@ static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEM
 extern "C" {
 
 void fast_conv_set_x3_fwd_nt(int nt) { X3_FWD_NT = nt; }
+void fast_conv_set_x3_c1_wg_ncx(int v) { X3_C1_WG_NCX = v == 2 ? 2 : 3; }
 void fast_conv_set_x3_fwd_lb(int lb) { X3_FWD_LB = lb; }
 void fast_conv_set_x3_fwd_db(int db) { X3_FWD_DB = db; }
 void fast_conv_set_x3_fwd_sw(int sw) { X3_FWD_SW = sw; }
@@ -3481,7 +3487,15 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (upw < 8) upw = 8;
   if (upw / SB::NB + 2 > X3_RING_FCS) return -22;       // the workgroup's first-valid bytes fit the LDS table
   const dim3 grid((unsigned)((units + upw - 1) / upw), P);
-  if (X3_WGRAD_PF == 2)
+  if (X3_C1_WG_NCX == 2 && X3_WGRAD_PF == 2)
+    conv_wgrad_slab_x3<C1, 2, 2, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
+                                                                b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
+                                                                is, gs, (const uint8_t*)fc, nslots);
+  else if (X3_C1_WG_NCX == 2)
+    conv_wgrad_slab_x3<C1, 2, 1, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
+                                                                b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
+                                                                is, gs, (const uint8_t*)fc, nslots);
+  else if (X3_WGRAD_PF == 2)
     conv_wgrad_slab_x3<C1, 2, 2, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
                                                              (const uint8_t*)fc, nslots);

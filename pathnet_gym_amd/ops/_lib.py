@@ -154,6 +154,7 @@ _SIGS = {
     "fast_conv_set_x3_fc_d": [c_int],
     "fast_conv_set_x3_fc_ks": [c_int],
     "fast_conv_set_x3_wgrad_pf": [c_int],
+    "fast_conv_set_x3_c1_wg_ncx": [c_int],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }

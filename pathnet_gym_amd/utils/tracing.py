@@ -7,7 +7,7 @@ GA) with ``torch.cuda.Event`` pairs on the compute stream (GPU time, no
 extra sync: events are resolved lazily, one update behind) and host wall
 clock, keeps running totals, and writes a Chrome/Perfetto trace
 (``chrome://tracing``) when given a path.  Kernel-level detail comes from
-``rocprofv3 --kernel-trace --stats`` (scripts/gpu_prof.sh).
+``rocprofv3 --kernel-trace --stats`` (``scripts/gpu.sh "kwin TAG"``).
 """
 from __future__ import annotations
 

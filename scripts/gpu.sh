@@ -4,7 +4,7 @@
 # the chain stops at the first failure (no GPU work after a fault, an abort or a time limit).
 #
 #   scripts/gpu.sh "tests" "smoke" "bench --steps 20"
-#   scripts/gpu.sh "tests -k x3_engine"                      pytest -m gpu (extra pytest args)
+#   scripts/gpu.sh "tests x3_lstm,two_tile"                  pytest -m gpu [-k "x3_lstm or two_tile"]
 #   scripts/gpu.sh "smoke"                                   __graft_entry__.smoke()
 #   scripts/gpu.sh "bench <bench.py args>"                   -> gpurun_out/r4/bench_<n>.json
 #   scripts/gpu.sh "kwin TAG <bench.py args>"                rocprofv3 kernel trace, steady-state window summary
@@ -29,7 +29,9 @@ nb=0
 fail() { echo "STEP FAIL ($1) rc=$2"; [ -n "$3" ] && tail -25 "$3"; exit 1; }
 
 step_tests() {
-  $T 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "$@" \
+  local k=()
+  [ -n "$1" ] && k=(-k "${1//,/ or }")
+  $T 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${k[@]}" \
       > "$OUT/pytest_gpu.log" 2>&1 || fail tests $? "$OUT/pytest_gpu.log"
   tail -2 "$OUT/pytest_gpu.log"
 }

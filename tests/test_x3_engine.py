@@ -489,7 +489,7 @@ def _oracle_grad_lstm(tr, eng):
 @pytest.fixture(scope="module", params=["eager", "graph"])
 def x3_lstm_rollout(hip_lib, request):
     """The `reference` preset (L=4 trunk + LSTM 256, 18 actions) at a small shape in fp32x: the fused split-operand
-    LSTM (no autograd hybrid), frame ring, device GA; "graph": hipGraph capture + replays, the last replay compared."""
+    LSTM (no autograd hybrid), device GA (Alien: packed stacks); "graph": hipGraph capture + replays, the last replay compared."""
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     cfg = preset("reference")
     cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 4
@@ -499,7 +499,7 @@ def x3_lstm_rollout(hip_lib, request):
     cfg.ga.backend = "device"
     tr = PathNetTrainer(cfg, device=DEV)
     eng = tr.engine
-    assert eng.lstm_hip and not eng.hybrid and eng.hst.dtype == torch.float32 and eng.ring
+    assert eng.lstm_hip and not eng.hybrid and eng.hst.dtype == torch.float32
     assert eng.use_graph == (request.param == "graph")
     tr.env.max_episode_steps = 5
     for _ in range(3 if cfg.use_graph else 1):
@@ -532,3 +532,31 @@ def test_x3_lstm_gradient_check_detects_a_two_percent_error(x3_lstm_rollout):
         bad = g_hip.clone()
         bad[s.offset:s.offset + s.numel] *= 1.02
         assert layer_errors(tr, bad, g_ref)["lstm"] > X3_LAYER_TOL, name
+
+
+@pytest.mark.parametrize("ncx,pf", [(2, 1), (2, 2)])
+def test_x3_conv1_ring_wgrad_two_tile_passes_match_default(x3_ring_rollout, ncx, pf):
+    """conv_wgrad_slab_x3 with 2 column tiles per pass (3 waves / SIMD; the all-modules path of masks_with_edges takes
+    3 passes) == the default 3-tile form, weights and biases, up to float-atomic order."""
+    from pathnet_gym_amd.ops import _lib
+    tr, eng, g_ref, g_hip = x3_ring_rollout
+    hp = tr.model.hip
+    lib = _lib.lib()
+    g = hp.geoms[0]
+    seg = slice(g.w_off, g.w_off + hp.M * g.chunk)
+    outs = []
+    for arm in ("default", "variant"):
+        lib.fast_conv_set_x3_c1_wg_ncx(ncx if arm == "variant" else 3)
+        lib.fast_conv_set_x3_wgrad_pf(pf if arm == "variant" else 3)
+        eng.grad_flat.zero_()
+        hp.ring_wgrad(eng.frames, eng.fc, eng.grads[0], eng.bits[0], eng.grad_flat, eng.P, eng.E, eng.T,
+                      eng.bits_rows[0])
+        torch.cuda.synchronize()
+        outs.append(eng.grad_flat[seg].clone())
+    lib.fast_conv_set_x3_c1_wg_ncx(3)
+    lib.fast_conv_set_x3_wgrad_pf(3)
+    assert outs[0].norm() > 0
+    e = rel(outs[1], outs[0])
+    print(f"conv1 ring wgrad ncx={ncx} pf={pf} vs default: rel {e:.2e}")
+    assert e < 1e-6, e
+    assert rel(outs[0], g_hip[seg]) < 1e-6
