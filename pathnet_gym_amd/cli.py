@@ -48,7 +48,11 @@ def build_parser():
         p.add_argument("--fc", default=None, help='linear PathNet layer widths, e.g. "256,256"')
         p.add_argument("--B", type=int, default=None, help="tournament size")
         # framework flags
-        p.add_argument("--paths", type=int, default=None, help="paths per rank")
+        p.add_argument("--paths", type=int, default=None, help="paths per rank (weak scaling)")
+        p.add_argument("--paths_total", type=int, default=None,
+                       help="strong scaling: this fixed population split over the ranks (paths = paths_total / world)")
+        p.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                       help="strong: --paths_total (default: --paths) is the whole population, split over the ranks")
         p.add_argument("--envs_per_path", type=int, default=None)
         p.add_argument("--tasks", default=None, help='comma list, e.g. "Pong,Breakout"')
         p.add_argument("--backend", default=None, choices=["auto", "hip", "torch"])
@@ -57,8 +61,10 @@ def build_parser():
         p.add_argument("--trunk_scale", default=None, choices=["M", "none"],
                        help="divide the trunk output by M (reference FF net) or not (reference LSTM net)")
         p.add_argument("--no_graph", action="store_true")
-        p.add_argument("--compute_dtype", default=None, choices=["bf16", "fp32"],
-                       help="HIP engine operand precision (fp32 = the reference's precision, csrc/trunk_f32.hip)")
+        p.add_argument("--compute_dtype", default=None, choices=["bf16", "fp32", "fp32x"],
+                       help="HIP engine operand precision: fp32 (fp32 MFMA operands, csrc/trunk_f32.hip, bit-"
+                            "reproducible), fp32x (fp32-accurate fp16/bf16 hi+lo pairs, csrc/trunk_x3.hip + lstm_x3.hip, "
+                            "<= 2e-5 per layer vs fp32), bf16")
         p.add_argument("--deterministic", type=int, default=None,
                        help="1: fixed-order gradient reductions (bit-reproducible updates)")
         # RL constants (constants.py)
@@ -177,6 +183,10 @@ def config_from_args(a):
     pop = a.paths if a.paths is not None else a.worker_hosts_num
     if pop is not None:
         cfg.paths = pop
+    if getattr(a, "paths_total", None):
+        cfg.paths_total = a.paths_total
+    elif getattr(a, "scaling", None) == "strong":
+        cfg.paths_total = cfg.paths
     for k in ("envs_per_path", "backend", "seed", "log_dir", "gray", "frameskip"):
         v = getattr(a, k, None)
         if v is not None:

@@ -187,3 +187,20 @@ def test_compute_dtype_and_deterministic_flags():
     ok = preset("cartpole-cpu")
     ok.compute_dtype = "bf16"
     assert PathNetTrainer(ok, device="cpu").compute_dtype == "fp32"
+
+
+def test_checkpoint_format_version_gates_legacy_task_id_mapping(tmp_path):
+    """Format-1 checkpoints (rounds 1-3) named the synthetic games Pong-v0 ...; read_config maps those ids to Synth*.
+    Format-2 checkpoints keep their ids: Pong-v0 now means the real gym game."""
+    import torch
+    from safetensors.torch import save_file
+    from pathnet_gym_amd.config import preset
+    from pathnet_gym_amd.utils import checkpoint as ckpt
+    cfg = preset("cartpole-cpu")
+    cfg.tasks = ["Pong-v0", "Breakout-v0"]
+    cfg.env = "Pong-v0"
+    for ver, want in (("1", ["SynthPong-v0", "SynthBreakout-v0"]), ("2", ["Pong-v0", "Breakout-v0"])):
+        p = str(tmp_path / f"v{ver}.safetensors")
+        save_file({"x": torch.zeros(1)}, p, metadata={"format_version": ver, "config": cfg.to_json()})
+        assert ckpt.read_config(p).tasks == want, ver
+    assert ckpt.FORMAT_VERSION == 2
