@@ -348,6 +348,8 @@ def main():
     }
     if build_info is not None:
         rec["build"] = build_info
+    if getattr(tr, "precision_note", None):
+        rec["precision_note"] = tr.precision_note
     del tr
     if compare:
         _, trb = build_trainer(args, ctx, "bf16", stagger, paths_total=head_total)

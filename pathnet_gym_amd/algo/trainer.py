@@ -79,6 +79,16 @@ class PathNetTrainer:
         if cfg.compute_dtype not in ("bf16", "fp32", "fp32x"):
             raise ValueError(f"compute_dtype {cfg.compute_dtype!r}: expected 'bf16', 'fp32' or 'fp32x'")
         self.compute_dtype = cfg.compute_dtype if self.backend == "hip" else "fp32"
+        self.precision_note = None
+        if self.compute_dtype == "fp32x":
+            from ..ops.pathnet_ops import x3_unsupported_reason
+            why = x3_unsupported_reason(cfg.net)
+            if why is not None:
+                # no split-operand kernels for this geometry: the fp32 engine keeps (and exceeds) fp32x's accuracy
+                import warnings
+                self.precision_note = f"fp32x -> fp32: {why}"
+                warnings.warn(f"compute_dtype fp32x: {why}; running the fp32 engine (csrc/trunk_f32.hip) instead")
+                self.compute_dtype = "fp32"
         self.logger = logger
         net = cfg.net
         if cfg.paths_total:

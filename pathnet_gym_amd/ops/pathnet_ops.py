@@ -93,6 +93,26 @@ class LayerGeom:
         return self.w_off + self.K * self.Cout
 
 
+# conv geometries with fp32x kernels (csrc/trunk_x3.hip): (Hin, Win, Cin, kernel, stride, uint8 input)
+X3_CONV_GEOMS = ((160, 120, 4, 8, 4, True), (39, 29, 8, 4, 2, False), (18, 13, 8, 3, 1, False))
+
+
+def x3_unsupported_reason(net) -> Optional[str]:
+    """Why the fp32x kernels cannot run PathNetConfig ``net`` (None: they can).  The trainer then runs the fp32 engine
+    (csrc/trunk_f32.hip: fp32 operands, at least the accuracy fp32x promises, bit-reproducible, slower) instead of
+    failing -- e.g. for the reference's --kernel_num / --stride_size flags beyond the default 8,4,3 / 4,2,1 trunk."""
+    if net.M > 10:
+        return f"M={net.M} > 10 modules per layer"
+    for l, (spec, (ins, outs, K, cin)) in enumerate(zip(net.layers, net.layer_shapes())):
+        if spec.kind == "conv":
+            g = (ins[0], ins[1], ins[2], spec.kernel, spec.stride, l == 0)
+            if g not in X3_CONV_GEOMS:
+                return f"conv layer {l} geometry {g[:5]} has no fp32x kernel"
+        elif l == 0 or spec.out % 64 != 0 or K % 8 != 0:
+            return f"fc layer {l} needs a conv input and width % 64 == 0"
+    return None
+
+
 class HipPathNet:
     """Kernel-side view of an ``ACPathNet`` (created by it when backend='hip')."""
 
@@ -226,7 +246,7 @@ class HipPathNet:
             self.Wh_ring = torch.zeros(self.M, g.Cout, g.KP, dtype=torch.float16, device=dev)     # fp16-offset path
             self.refresh_weights()
 
-    _X3_CONV = ((160, 120, 4, 8, 4, True), (39, 29, 8, 4, 2, False), (18, 13, 8, 3, 1, False))
+    _X3_CONV = X3_CONV_GEOMS
 
     def _check_x3(self):
         """fp32x kernels exist for the reference pixel trunk geometries (csrc/trunk_x3.hip): uint8 160x120x4 8x8/s4,

@@ -43,13 +43,16 @@ def _t(x) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
 
 
-def state_tensors(trainer) -> Dict[str, torch.Tensor]:
+def state_tensors(trainer, light: bool = False) -> Dict[str, torch.Tensor]:
+    """``light``: leave out the momentum slots when they are all zero (momentum 0.0, the reference's setting)."""
     st = trainer.model.store
     out: Dict[str, torch.Tensor] = {}
+    skip_mom = light and not bool(trainer.opt.mom.any())
     for s in st.layout.segments:
         out[s.name] = _t(st.flat[s.offset:s.offset + s.numel].view(s.shape))
         out[s.name + "/RMSProp"] = _t(trainer.opt.ms[s.offset:s.offset + s.numel].view(s.shape))
-        out[s.name + "/RMSProp_1"] = _t(trainer.opt.mom[s.offset:s.offset + s.numel].view(s.shape))
+        if not skip_mom:
+            out[s.name + "/RMSProp_1"] = _t(trainer.opt.mom[s.offset:s.offset + s.numel].view(s.shape))
     out["optim.seg_trainable"] = _t(trainer.opt.seg_trainable.to(torch.uint8))
     out["init_flat"] = _t(trainer.init_flat)
     for k, v in trainer.pop.state_dict().items():
@@ -78,7 +81,9 @@ def state_tensors(trainer) -> Dict[str, torch.Tensor]:
     return out
 
 
-def rank_tensors(trainer) -> Dict[str, torch.Tensor]:
+def rank_tensors(trainer, light: bool = False) -> Dict[str, torch.Tensor]:
+    """``light``: leave out the frame stacks entering the next rollout (1.3 GB at 512 paths x 32 envs); a load then
+    rebuilds every env's stack from its current frame, as at an episode start (resume no longer bit-exact)."""
     env = trainer.env
     out: Dict[str, torch.Tensor] = {}
     if hasattr(env, "_st32"):          # HIP pong: kernel-side state is authoritative
@@ -87,14 +92,15 @@ def rank_tensors(trainer) -> Dict[str, torch.Tensor]:
     if hasattr(env, "_steps32"):
         env.steps = env._steps32.long()
         env.counter = env._ctr32.long() & 0xFFFFFFFF
-    for name in ("state", "counter", "steps", "ep_ret", "obs"):
+    for name in ("state", "counter", "steps", "ep_ret") + (() if light else ("obs",)):
         if hasattr(env, name) and isinstance(getattr(env, name), torch.Tensor):
             out["env." + name] = _t(getattr(env, name))
     out["env.seed"] = torch.tensor([env.seed_int], dtype=torch.int64)
     if trainer.engine is not None:
         eng = trainer.engine
         out["engine.ctr"] = _t(eng.ctr)
-        out["engine.obs0"] = _t(eng.obs_stack(0))
+        if not light:
+            out["engine.obs0"] = _t(eng.obs_stack(0))
         out["engine.fitness"] = _t(eng.fitness)
         out["engine.fit_cnt"] = _t(eng.fit_cnt)
         out["engine.fit_sum"] = _t(eng.fit_sum)
@@ -110,15 +116,33 @@ def rank_tensors(trainer) -> Dict[str, torch.Tensor]:
     return out
 
 
-def save(trainer, path: str) -> str:
-    """Write ``path`` (rank-0 global state) and ``path.rank<r>.safetensors`` (every rank)."""
+def save(trainer, path: str, light: bool = False) -> str:
+    """Write ``path`` (rank-0 global state) and ``path.rank<r>.safetensors`` (every rank).  ``light``: a continuation
+    checkpoint without the frame stacks and the all-zero momentum slots (state_tensors / rank_tensors)."""
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
-    meta = {"format_version": str(FORMAT_VERSION), "config": trainer.cfg.to_json(),
+    meta = {"format_version": str(FORMAT_VERSION), "config": trainer.cfg.to_json(), "light": str(int(light)),
             "world": str(trainer.ctx.world), "segments": json.dumps([s.name for s in trainer.model.store.layout.segments])}
     if trainer.ctx.is_main:
-        save_file(state_tensors(trainer), path, metadata=meta)
-    save_file(rank_tensors(trainer), f"{path}.rank{trainer.ctx.rank}.safetensors", metadata=meta)
+        save_file(state_tensors(trainer, light), path, metadata=meta)
+    save_file(rank_tensors(trainer, light), f"{path}.rank{trainer.ctx.rank}.safetensors", metadata=meta)
     return path
+
+
+def _restack_current_frame(trainer):
+    """Light checkpoints: every env's stack entering the next rollout = its current frame x 4 (episode-start rule)."""
+    env = trainer.env
+    if not hasattr(env, "frame"):
+        return
+    if hasattr(env, "_st32"):
+        from ..ops import envs as henv
+        henv.pong_sync_from_device(env)
+    f = env.frame()                                   # [N, H, W] uint8
+    stack = f[..., None].expand(-1, -1, -1, 4).contiguous()
+    env.obs = stack
+    if trainer.engine is not None:
+        trainer.engine.set_obs_stack0(stack.reshape(stack.shape[0], -1))
+    else:
+        trainer.obs = stack.clone()
 
 
 def load(trainer, path: str, strict: bool = True):
@@ -134,7 +158,10 @@ def load(trainer, path: str, strict: bool = True):
                 continue
             st.flat[s.offset:s.offset + s.numel].copy_(d[s.name].reshape(-1).to(dev))
             trainer.opt.ms[s.offset:s.offset + s.numel].copy_(d[s.name + "/RMSProp"].reshape(-1).to(dev))
-            trainer.opt.mom[s.offset:s.offset + s.numel].copy_(d[s.name + "/RMSProp_1"].reshape(-1).to(dev))
+            if s.name + "/RMSProp_1" in d:
+                trainer.opt.mom[s.offset:s.offset + s.numel].copy_(d[s.name + "/RMSProp_1"].reshape(-1).to(dev))
+            else:                                     # light checkpoint: the momentum slots were all zero
+                trainer.opt.mom[s.offset:s.offset + s.numel].zero_()
         trainer.opt.seg_trainable.copy_(d["optim.seg_trainable"].bool().to(dev))
         trainer.init_flat.copy_(d["init_flat"].to(dev))
     ga = {k[3:]: v.numpy() for k, v in d.items() if k.startswith("ga.")}
@@ -174,13 +201,14 @@ def load(trainer, path: str, strict: bool = True):
         if trainer.engine is not None:
             eng = trainer.engine
             eng.ctr.copy_(r["engine.ctr"].to(dev))
-            eng.set_obs_stack0(r["engine.obs0"].to(dev))
+            if "engine.obs0" in r:
+                eng.set_obs_stack0(r["engine.obs0"].to(dev))
             eng.fitness.copy_(r["engine.fitness"].to(dev))
             if "engine.fit_cnt" in r:
                 eng.fit_cnt.copy_(r["engine.fit_cnt"].to(dev))
                 eng.fit_sum.copy_(r["engine.fit_sum"].to(dev))
             eng.refresh_trainable()
-        else:
+        elif "train.obs" in r:
             trainer.obs = r["train.obs"].to(dev)
             trainer.fitness_local = r["train.fitness_local"].to(dev)
             if "train.fit_cnt" in r:
@@ -191,6 +219,8 @@ def load(trainer, path: str, strict: bool = True):
                 trainer.engine.load_lstm_state(r["lstm.h"].to(dev), r["lstm.c"].to(dev))
             else:
                 trainer.lstm_state = (r["lstm.h"].to(dev), r["lstm.c"].to(dev))
+    if os.path.exists(rp) and "engine.obs0" not in r and "train.obs" not in r:
+        _restack_current_frame(trainer)
     if trainer.backend == "hip":
         trainer.model.hip.refresh_weights()
         if trainer.engine is not None and trainer.engine.ga_dev is not None:

@@ -201,12 +201,14 @@ def main():
                 ctx.max_scalar(now - last_ckpt) > args.ckpt_minutes * 60:
             from pathnet_gym_amd.utils import checkpoint as ckpt
             tr.flush()
-            ckpt.save(tr, args.checkpoint)
+            ckpt.save(tr, args.checkpoint, light=True)
             last_ckpt = time.time()
     tr.flush()
     if args.checkpoint:
+        # a continuation checkpoint (no frame stacks, no all-zero momentum: ~45 MB at the bench network instead of
+        # 1.3 GB at 512 x 32 envs); the resumed run restarts every env's stack from its current frame
         from pathnet_gym_amd.utils import checkpoint as ckpt
-        ckpt.save(tr, args.checkpoint)
+        ckpt.save(tr, args.checkpoint, light=True)
     el = prior["seconds"] + time.time() - t0
     if ctx.is_main:
         out = {"metric": "generations_to_solve", "env": cfg.tasks[0], "threshold": thr,

@@ -113,3 +113,15 @@ def test_init_ranges_muupan():
     assert float(w.abs().max()) <= d + 1e-6
     pw, pb, vw, vb = st.head()
     assert float(pw.abs().max()) <= 1 / np.sqrt(256) + 1e-6
+
+
+def test_x3_geometry_support_and_fp32_fallback_reason():
+    """fp32x kernels exist for the reference pixel trunk (8,4,3 / 4,2,1 on 160x120x4) and fc widths % 64; any other
+    --kernel_num / --stride_size runs the fp32 engine (trainer.precision_note says why) instead of raising."""
+    from pathnet_gym_amd.config import PathNetConfig, preset, reference_pixel_layers
+    from pathnet_gym_amd.ops.pathnet_ops import x3_unsupported_reason
+    assert x3_unsupported_reason(preset("pong").net) is None
+    assert x3_unsupported_reason(preset("reference").net) is None
+    odd = PathNetConfig(L=4, M=10, N=4, layers=reference_pixel_layers(4, (8, 4, 3), (4, 2, 2)))
+    assert "conv layer 2" in x3_unsupported_reason(odd)
+    assert "M=12" in x3_unsupported_reason(PathNetConfig(L=4, M=12, N=4))

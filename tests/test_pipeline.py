@@ -83,3 +83,42 @@ def test_frozen_modules_bit_identical_across_task2_updates_hip(hip_lib):
     geno = tr.engine.ga_dev["geno"].cpu().numpy() | tr.engine.ga_dev["frozen"].cpu().numpy()[None]
     assert (geno[:, frozen > 0.5] == 1).all()
     assert (tr.model.mask.cpu().numpy()[:, frozen > 0.5] == 1).all()
+
+
+@pytest.mark.gpu
+def test_light_checkpoint_resume_restacks_current_frame(hip_lib, tmp_path):
+    """Continuation checkpoints (scripts/solve.py): no frame stacks, no zero momentum slots; the resumed trainer has
+    the same weights, RMSProp slots, GA state and counters, and every env's stack is its current frame x 4."""
+    import numpy as np
+    import torch
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.config import preset
+    from pathnet_gym_amd.utils import checkpoint as ckpt
+
+    def make():
+        cfg = preset("pong")
+        cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 4
+        cfg.ga.backend = "device"
+        cfg.compute_dtype = "fp32x"
+        cfg.frame_ring = True
+        return PathNetTrainer(cfg, device="cuda")
+    a = make()
+    for _ in range(3):
+        a.update()
+    a.flush()
+    p = str(tmp_path / "ck.safetensors")
+    ckpt.save(a, p, light=True)
+    from safetensors import safe_open
+    with safe_open(p + ".rank0.safetensors", framework="pt") as f:
+        assert "engine.obs0" not in f.keys()
+    with safe_open(p, framework="pt") as f:
+        assert not any(k.endswith("/RMSProp_1") for k in f.keys())
+    b = make()
+    ckpt.load(b, p)
+    assert torch.equal(a.model.store.flat, b.model.store.flat) and torch.equal(a.opt.ms, b.opt.ms)
+    assert np.array_equal(a.pop.genotypes, b.pop.genotypes) and a.updates == b.updates
+    st = b.engine.obs_stack(0).view(b.P * b.E, -1, 4)
+    assert torch.equal(st[..., 0], st[..., 3]) and st.float().mean() > 0
+    b.update()
+    b.flush()
+    assert torch.isfinite(b.model.store.flat).all()
