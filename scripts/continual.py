@@ -49,6 +49,9 @@ def build_cfg(args, tasks):
     cfg.a2c.max_time_step = 2 * args.frames
     cfg.a2c.lr_anneal = "none"
     cfg.seed = cfg.ga.seed = args.seed
+    if args.dtype:
+        cfg.compute_dtype = args.dtype
+    cfg.frame_ring = bool(args.ring)
     return cfg
 
 
@@ -136,6 +139,14 @@ def main():
     ap.add_argument("--control-only", action="store_true",
                     help="only the from-scratch control runs of tasks >= 2 (e.g. in a separate job)")
     ap.add_argument("--out", default="gpurun_out/continual.json")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp32x"], help="HIP engine compute dtype")
+    ap.add_argument("--ring", action="store_true", help="first layer on the frame ring (the fp32x bench default)")
+    ap.add_argument("--checkpoint", default=None,
+                    help="continuation checkpoint written after every task (light: no frame stacks)")
+    ap.add_argument("--resume", action="store_true",
+                    help="continue a sequence from --checkpoint and the per-task records already in --out")
+    ap.add_argument("--max-tasks", type=int, default=None,
+                    help="train at most this many tasks of the sequence in this process (then --resume)")
     args = ap.parse_args()
     if args.preset == "atari4":
         args.paths = args.paths or 16
@@ -159,6 +170,26 @@ def main():
     per_task = []
     frozen_snap = []
     controls = []
+    prior_s = 0.0
+    if args.resume and tr is not None and args.checkpoint and os.path.exists(args.checkpoint):
+        from pathnet_gym_amd.utils import checkpoint as ckpt
+        ckpt.load(tr, args.checkpoint)
+        with open(args.out) as f:
+            old = json.load(f)
+        per_task = old["per_task"]
+        controls = old.get("scratch_control", [])
+        prior_s = float(old.get("seconds", 0.0))
+        # frozen parameters of the finished tasks as the checkpoint holds them (taken right after their freeze)
+        lay = tr.model.store.layout
+        flat0 = tr.model.store.flat.detach().cpu().numpy()
+        for ti in range(len(per_task)):
+            keep = np.zeros(lay.numel, bool)
+            for s_ in lay.segments:
+                if (s_.layer >= 0 and tr.task_paths[ti][s_.layer, s_.module] > 0.5) or s_.task == ti:
+                    keep[s_.offset:s_.offset + s_.numel] = True
+            frozen_snap.append((keep, flat0[keep].copy()))
+        print(json.dumps({"resumed": args.checkpoint, "tasks_done": len(per_task), "task_idx": tr.task_idx}), flush=True)
+    n_done0 = len(per_task)
 
     def write_out(stage):
         out = {"experiment": "continual", "reference": "doom_pathnet.py:274-293, aliencentipede.txt:55-93",
@@ -169,12 +200,18 @@ def main():
                           "env_reduction": cfg.a2c.env_reduction, "dtype": tr.compute_dtype if tr else None,
                           "stop_after_solve": args.stop_after_solve},
                "per_task": per_task, "scratch_control": controls, "seconds": round(time.time() - t0, 1)}
+        out["seconds"] = round(prior_s + time.time() - t0, 1)
         os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
         with open(args.out, "w") as f:
             json.dump(out, f, indent=1)
         return out
 
     for ti, name in enumerate([] if args.control_only else tasks):
+        if ti < n_done0:
+            continue
+        if args.max_tasks is not None and ti - n_done0 >= args.max_tasks:
+            print(json.dumps({"paused": True, "tasks_done": ti, "resume_with": "--resume"}), flush=True)
+            return
         rec = train_task(tr, ti, args, "sequence")
         # the parameters as the task left them: end_task re-initialises everything outside the frozen paths and
         # heads, which includes the shared LSTM cell of the reference's default network (its modules are frozen,
@@ -196,6 +233,9 @@ def main():
         per_task.append(rec)
         print(json.dumps({k: v for k, v in rec.items() if k != "curve"}), flush=True)
         write_out("sequence")
+        if args.checkpoint:
+            from pathnet_gym_amd.utils import checkpoint as ckpt
+            ckpt.save(tr, args.checkpoint, light=True)
     flat_end = None if tr is None else tr.model.store.flat.detach().cpu().numpy()
     for ti, name in enumerate([] if args.control_only else tasks):
         keep, vals = frozen_snap[ti]
