@@ -44,10 +44,11 @@ def _t(x) -> torch.Tensor:
 
 
 def state_tensors(trainer, light: bool = False) -> Dict[str, torch.Tensor]:
-    """``light``: leave out the momentum slots when they are all zero (momentum 0.0, the reference's setting)."""
+    """``light``: leave out the momentum slots when the momentum coefficient is 0.0 (the reference's setting: TF's
+    ApplyRMSProp then only stores the last step in them and never reads them back)."""
     st = trainer.model.store
     out: Dict[str, torch.Tensor] = {}
-    skip_mom = light and not bool(trainer.opt.mom.any())
+    skip_mom = light and float(trainer.opt.momentum) == 0.0
     for s in st.layout.segments:
         out[s.name] = _t(st.flat[s.offset:s.offset + s.numel].view(s.shape))
         out[s.name + "/RMSProp"] = _t(trainer.opt.ms[s.offset:s.offset + s.numel].view(s.shape))
@@ -118,7 +119,7 @@ def rank_tensors(trainer, light: bool = False) -> Dict[str, torch.Tensor]:
 
 def save(trainer, path: str, light: bool = False) -> str:
     """Write ``path`` (rank-0 global state) and ``path.rank<r>.safetensors`` (every rank).  ``light``: a continuation
-    checkpoint without the frame stacks and the all-zero momentum slots (state_tensors / rank_tensors)."""
+    checkpoint without the frame stacks and, at momentum 0, the momentum slots (state_tensors / rank_tensors)."""
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
     meta = {"format_version": str(FORMAT_VERSION), "config": trainer.cfg.to_json(), "light": str(int(light)),
             "world": str(trainer.ctx.world), "segments": json.dumps([s.name for s in trainer.model.store.layout.segments])}
@@ -160,7 +161,7 @@ def load(trainer, path: str, strict: bool = True):
             trainer.opt.ms[s.offset:s.offset + s.numel].copy_(d[s.name + "/RMSProp"].reshape(-1).to(dev))
             if s.name + "/RMSProp_1" in d:
                 trainer.opt.mom[s.offset:s.offset + s.numel].copy_(d[s.name + "/RMSProp_1"].reshape(-1).to(dev))
-            else:                                     # light checkpoint: the momentum slots were all zero
+            else:                                     # light checkpoint, momentum 0: the slots are never read
                 trainer.opt.mom[s.offset:s.offset + s.numel].zero_()
         trainer.opt.seg_trainable.copy_(d["optim.seg_trainable"].bool().to(dev))
         trainer.init_flat.copy_(d["init_flat"].to(dev))

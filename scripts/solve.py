@@ -205,7 +205,7 @@ def main():
             last_ckpt = time.time()
     tr.flush()
     if args.checkpoint:
-        # a continuation checkpoint (no frame stacks, no all-zero momentum: ~45 MB at the bench network instead of
+        # a continuation checkpoint (no frame stacks, no momentum slots at momentum 0: ~45 MB at the bench network, not
         # 1.3 GB at 512 x 32 envs); the resumed run restarts every env's stack from its current frame
         from pathnet_gym_amd.utils import checkpoint as ckpt
         ckpt.save(tr, args.checkpoint, light=True)

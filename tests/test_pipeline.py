@@ -87,7 +87,7 @@ def test_frozen_modules_bit_identical_across_task2_updates_hip(hip_lib):
 
 @pytest.mark.gpu
 def test_light_checkpoint_resume_restacks_current_frame(hip_lib, tmp_path):
-    """Continuation checkpoints (scripts/solve.py): no frame stacks, no zero momentum slots; the resumed trainer has
+    """Continuation checkpoints (scripts/solve.py): no frame stacks, no momentum slots (momentum 0); the resumed trainer has
     the same weights, RMSProp slots, GA state and counters, and every env's stack is its current frame x 4."""
     import numpy as np
     import torch
