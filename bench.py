@@ -258,8 +258,8 @@ def main():
                     help="start every env at 0-0 (default: random late scores, so tournaments fire inside the window)")
     ap.add_argument("--solve-seconds", type=float, default=None,
                     help="after the timed windows, run one generations-to-solve seed on a fresh trainer for at most "
-                         "this long (default: what is left of a 540 s budget, at most 420 s; on one GPU the bench "
-                         "config, on several the strong-scaling config; 0 = off)")
+                         "this long (default: one GPU, the bench config, what is left of a 540 s run, at most 420 s; "
+                         "several GPUs, the strong-scaling config, what is left of 480 s, at most 300 s; 0 = off)")
     ap.add_argument("--compare-bf16", type=int, default=None,
                     help="also time the bf16 engine on the same config (default: on for one GPU)")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling windows on several GPUs")
@@ -388,8 +388,11 @@ def main():
     # config, whose updates are what more GPUs shorten), plus every committed multi-seed record of this config
     solve_s = args.solve_seconds
     if solve_s is None:
-        solve_s = 420.0 if (single or (world > 1 and strong is not None)) else 0.0
-        solve_s = max(0.0, min(solve_s, 540.0 - ctx.max_scalar(time.time() - t_start)))
+        # one GPU: up to 420 s within a 540 s run; several: the strong config solves in ~20-34 K updates of a few ms,
+        # so up to 300 s within a 480 s run
+        cap, budget = (420.0, 540.0) if world == 1 else (300.0, 480.0)
+        solve_s = cap if (single or (world > 1 and strong is not None)) else 0.0
+        solve_s = max(0.0, min(solve_s, budget - ctx.max_scalar(time.time() - t_start)))
     if solve_s > 0:
         strong_solve = world > 1 and args.scaling == "weak"
         r = in_run_solve(args, ctx, args.dtype, solve_s, paths_total=args.paths_total if strong_solve else head_total)

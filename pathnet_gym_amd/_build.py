@@ -91,7 +91,19 @@ def build_info(lib: str = LIB) -> dict:
 
 
 def build(verbose: bool = False, jobs: int = 0) -> str:
+    """Compile what is stale and relink.  Ranks of one job that call this together (bench.py under torchrun) are
+    serialised by an exclusive lock on the output directory: the first compiles, the others then find it current."""
     os.makedirs(OUT_DIR, exist_ok=True)
+    import fcntl
+    with open(os.path.join(OUT_DIR, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            return _build_locked(verbose, jobs)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(verbose: bool, jobs: int) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = sorted(glob.glob(os.path.join(CSRC, "*.h")))
     objs = []
