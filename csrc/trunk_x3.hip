@@ -3330,7 +3330,9 @@ static int X3_FWD_DB = 0;      // bf16-activation conv forward: 1 = double-buffe
 static int X3_WGRAD_PF = 3;
 // first-layer (frame ring) slab weight gradient: column tiles per pass (conv_wgrad_slab_x3 NCXP): 3 (2 waves / SIMD)
 // or 2 (3 waves / SIMD, a second pass for paths with > 4 active modules)
-static int X3_C1_WG_NCX = 3;
+// measured (profiles/r4/kwin_c1ncx*.md): 2.28 ms (3 tiles, PF 1) -> 2.02 (2, PF 1) -> 1.94 (2, PF 2; the default: PF 2
+// unless X3_WGRAD_PF == 1)
+static int X3_C1_WG_NCX = 2;
 // conv forward epilogue, bit 0: first layer, bit 1: the bf16-activation layers; set = swapped MFMA orientation
 // (conv_epi_sw; first layer also with the 1024-offset pixels folded into the bias), clear = rows-as-A
 static int X3_FWD_SW = 1;
@@ -3487,7 +3489,7 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (upw < 8) upw = 8;
   if (upw / SB::NB + 2 > X3_RING_FCS) return -22;       // the workgroup's first-valid bytes fit the LDS table
   const dim3 grid((unsigned)((units + upw - 1) / upw), P);
-  if (X3_C1_WG_NCX == 2 && X3_WGRAD_PF == 2)
+  if (X3_C1_WG_NCX == 2 && X3_WGRAD_PF != 1)       // 2 tiles per pass: two stages in flight fit (162 VGPRs)
     conv_wgrad_slab_x3<C1, 2, 2, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
                                                                 is, gs, (const uint8_t*)fc, nslots);

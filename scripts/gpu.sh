@@ -31,8 +31,13 @@ fail() { echo "STEP FAIL ($1) rc=$2"; [ -n "$3" ] && tail -25 "$3"; exit 1; }
 step_tests() {
   local k=()
   [ -n "$1" ] && k=(-k "${1//,/ or }")
+  local rc=0
   $T 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${k[@]}" \
-      > "$OUT/pytest_gpu.log" 2>&1 || fail tests $? "$OUT/pytest_gpu.log"
+      > "$OUT/pytest_gpu.log" 2>&1 || rc=$?
+  # a failed assertion (rc 1) is a result, not a fault: report it and go on with the next steps; a time limit, an
+  # abort or a crash (rc 124 / 137 / 134 / 139 / >128) ends the call
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then fail tests $rc "$OUT/pytest_gpu.log"; fi
+  [ $rc -ne 0 ] && grep -E "^E |^FAILED|per layer" "$OUT/pytest_gpu.log" | head -12
   tail -2 "$OUT/pytest_gpu.log"
 }
 

@@ -548,8 +548,8 @@ def test_x3_lstm_gradient_check_detects_a_two_percent_error(x3_lstm_rollout):
 
 @pytest.mark.parametrize("ncx,pf", [(2, 1), (2, 2)])
 def test_x3_conv1_ring_wgrad_two_tile_passes_match_default(x3_ring_rollout, ncx, pf):
-    """conv_wgrad_slab_x3 with 2 column tiles per pass (3 waves / SIMD; the all-modules path of masks_with_edges takes
-    3 passes) == the default 3-tile form, weights and biases, up to float-atomic order."""
+    """conv_wgrad_slab_x3 with 2 column tiles per pass (3 waves / SIMD, the default; the all-modules path of
+    masks_with_edges takes 3 passes) == the 3-tile form, weights and biases, up to float-atomic order."""
     from pathnet_gym_amd.ops import _lib
     tr, eng, g_ref, g_hip = x3_ring_rollout
     hp = tr.model.hip
@@ -565,7 +565,7 @@ def test_x3_conv1_ring_wgrad_two_tile_passes_match_default(x3_ring_rollout, ncx,
                       eng.bits_rows[0])
         torch.cuda.synchronize()
         outs.append(eng.grad_flat[seg].clone())
-    lib.fast_conv_set_x3_c1_wg_ncx(3)
+    lib.fast_conv_set_x3_c1_wg_ncx(2)            # the defaults
     lib.fast_conv_set_x3_wgrad_pf(3)
     assert outs[0].norm() > 0
     e = rel(outs[1], outs[0])
