@@ -7,7 +7,9 @@
 //   forward  z = [x | h] K + b : fp16 pairs, x = hi + lo (22 significant bits) against the fp16 pair of K * 2^8,
 //                                three MFMAs per product (hi*hi + hi*lo + lo*hi), fp32 accumulation; x (the fp32
 //                                trunk output) and h / c / the saved gates stay fp32
-//   backward dz K^T, dK = [x|h]^T dz : bf16 pairs (bf16's exponent range for the gradients), three MFMAs
+//   backward dz K^T, dK = [x|h]^T dz : scaled fp16 pairs (csrc/trunk_x3.hip G16): dz_t * 2^e_t (e_t from the amax of
+//                                      step t's dz, written by the pointwise kernel), [x|h] * 2^e_x (amax written by the
+//                                      forward), K * 2^8; three f16 MFMAs, so 22 significant bits on both operands
 // Per-layer error against a plain fp32 oracle: tests/test_x3_engine.py (<= 2e-5, like the trunk).
 // Range: an input of the forward GEMM at or beyond fp16's 65504, or a kernel weight whose 2^8 multiple reaches
 // 32768, sets the engine's fp32x status word (bits 2 / 1, X3RangeError on the host).
@@ -56,6 +58,26 @@ DEVI void st8(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
+// G16 (csrc/trunk_x3.hip): power-of-two scale putting amax into [2^13, 2^14); one atomicMax per wave
+DEVI float g16_scale_of(float m) {
+  const uint32_t b = __float_as_uint(m);
+  const int e = (int)((b >> 23) & 0xFFu) - 127;
+  if ((b & 0x7FFFFFFFu) == 0u || e < -110 || e >= 128) return 1.0f;
+  const int se = min(13 - e, 126);
+  return __uint_as_float((uint32_t)(se + 127) << 23);
+}
+DEVI void g16_flush_amax(float m, float* __restrict__ amax) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m > 0.f && amax) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+}
+DEVI void split8hs(const float (&v)[8], float s, s8v& hi, s8v& lo) {
+  float t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = v[j] * s;
+  split8h(t, hi, lo);
+}
+
 // products from hi / lo pairs, the two small cross terms first (csrc/trunk_x3.hip mma3 / mma3h)
 DEVI f4v mma3h(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
   c = mfma16_f16(al, bh, c);
@@ -77,7 +99,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
     const float* __restrict__ X, int ldx, const float* __restrict__ hprev, const float* __restrict__ cprev,
     const uint8_t* __restrict__ prev_done, const uint16_t* __restrict__ KpT2, const float* __restrict__ flat,
     long b_off, float* __restrict__ hout, float* __restrict__ cout, float* __restrict__ gates,
-    float* __restrict__ xh, uint32_t* __restrict__ status, int F, int H, int B) {
+    float* __restrict__ xh, uint32_t* __restrict__ status, float* __restrict__ amax_xh, int F, int H, int B) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
   const int row0 = blockIdx.x * 64 + w * 16;
@@ -93,6 +115,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
 #pragma unroll
   for (int g = 0; g < 4; ++g) acc[g] = {0.f, 0.f, 0.f, 0.f};
   bool bad = false;
+  float am = 0.f;                                 // amax of the saved [x | h] rows (G16 scale of the weight gradient)
   const uint16_t* Bp = KpT2 + (long)(ut * 64 + c16) * KK + 8 * grp;
   for (int k0 = 0; k0 < KK; k0 += 32) {
     const int k = k0 + 8 * grp;
@@ -103,7 +126,10 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
     }
     if (wr_xh && av) st8(xh + (long)arow * KK + k, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bad |= !(fabsf(v[j]) < 65504.f);
+    for (int j = 0; j < 8; ++j) {
+      bad |= !(fabsf(v[j]) < 65504.f);
+      am = fmaxf(am, fabsf(v[j]));
+    }
     s8v ah, al;
     split8h(v, ah, al);
 #pragma unroll
@@ -115,6 +141,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
     }
   }
   if (bad && status) atomicOr(status, 2u);
+  if (wr_xh) g16_flush_amax(am, amax_xh);
   const float sc = 1.0f / (float)(1 << LX3_SHIFT);
   const int u = ut * 16 + c16;
   const float bi = flat[b_off + u], bj = flat[b_off + H + u], bff = flat[b_off + 2 * H + u],
@@ -147,9 +174,43 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
 // backward GEMM: out[b][n] = sum_p dz[b][p] K[n][p]; n < F -> dx, n >= F -> dh_prev.  Kb2: bf16 [2][KK][4H].
 // grid (ceil(B/64), KK/64); wave w: 16 rows x 64 columns (4 blocks of 16)
 // ---------------------------------------------------------------------------
+// pointwise backward of one step (csrc/lstm.hip lstm_bwd_point_kernel) + the amax of the step's dz (G16)
+__global__ __launch_bounds__(256) void lstm_bwd_point_x3_kernel(
+    const float* __restrict__ dh_heads, const float* __restrict__ dh_rec, const float* __restrict__ dc_rec,
+    const uint8_t* __restrict__ done_t, const float* __restrict__ gates, const float* __restrict__ c_t,
+    const float* __restrict__ c_prev, const uint8_t* __restrict__ prev_done, float* __restrict__ dz,
+    float* __restrict__ dc_out, float* __restrict__ amax_dz, int H, int B) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  float am = 0.f;
+  if (idx < (long)B * H) {
+    const int row = (int)(idx / H), u = (int)(idx - (long)row * H);
+    const float kt = (done_t && done_t[row]) ? 0.f : 1.f;
+    float dh = dh_heads[idx];
+    float dc = 0.f;
+    if (dh_rec) dh += kt * dh_rec[idx];
+    if (dc_rec) dc = kt * dc_rec[idx];
+    const float* gr = gates + (long)row * 4 * H;
+    const float si = gr[u], tj = gr[H + u], sf = gr[2 * H + u], so = gr[3 * H + u];
+    const float c = c_t[idx];
+    const float tc = tanh_f(c);
+    const float c0 = (prev_done && prev_done[row]) ? 0.f : c_prev[idx];
+    dc += dh * so * (1.f - tc * tc);
+    float* dzr = dz + (long)row * 4 * H;
+    const float z0 = dc * tj * si * (1.f - si), z1 = dc * si * (1.f - tj * tj), z2 = dc * c0 * sf * (1.f - sf),
+                z3 = dh * tc * so * (1.f - so);
+    dzr[u] = z0;
+    dzr[H + u] = z1;
+    dzr[2 * H + u] = z2;
+    dzr[3 * H + u] = z3;
+    dc_out[idx] = dc * sf;
+    am = fmaxf(fmaxf(fabsf(z0), fabsf(z1)), fmaxf(fabsf(z2), fabsf(z3)));
+  }
+  g16_flush_amax(am, amax_dz);
+}
+
 __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
-    const float* __restrict__ dz, const bf16_t* __restrict__ Kb2, float* __restrict__ dx, int lddx,
-    float* __restrict__ dh_prev, int F, int H, int B) {
+    const float* __restrict__ dz, const uint16_t* __restrict__ Kb2, float* __restrict__ dx, int lddx,
+    float* __restrict__ dh_prev, const float* __restrict__ amax_dz, int F, int H, int B) {
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
   const int row0 = blockIdx.x * 64 + w * 16;
@@ -162,20 +223,22 @@ __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
   f4v acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
+  const float gs = g16_scale_of(*amax_dz);
   for (int p0 = 0; p0 < G4; p0 += 32) {
     const int p = p0 + 8 * grp;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (av) ld8(dz + (long)arow * G4 + p, v);
     s8v ah, al;
-    split8b(v, ah, al);
+    split8hs(v, gs, ah, al);                      // fp16 pair of dz * 2^e against the fp16 pair of K * 2^8
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long o = (long)(n0 + j * 16 + c16) * G4 + p;
       const s8v bh = *reinterpret_cast<const s8v*>(Kb2 + o);
       const s8v bl = *reinterpret_cast<const s8v*>(Kb2 + plane + o);
-      acc[j] = mma3(ah, al, bh, bl, acc[j]);
+      acc[j] = mma3h(ah, al, bh, bl, acc[j]);
     }
   }
+  const float inv = 1.0f / (gs * (float)(1 << LX3_SHIFT));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + j * 16 + c16;
@@ -183,8 +246,8 @@ __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
     for (int r = 0; r < 4; ++r) {
       const int row = row0 + 4 * grp + r;
       if (row >= B) continue;
-      if (n < F) dx[(long)row * lddx + n] = acc[j][r];
-      else dh_prev[(long)row * H + (n - F)] = acc[j][r];
+      if (n < F) dx[(long)row * lddx + n] = acc[j][r] * inv;
+      else dh_prev[(long)row * H + (n - F)] = acc[j][r] * inv;
     }
   }
 }
@@ -195,7 +258,8 @@ __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
     const float* __restrict__ xh, const float* __restrict__ dz, float* __restrict__ grad, long k_off, long b_off,
-    int F, int H, long R, int rows_per_chunk) {
+    int F, int H, long R, int rows_per_chunk, const float* __restrict__ amax_dz, int T,
+    const float* __restrict__ amax_xh) {
   constexpr int S = 64 + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][32 * S];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][32 * S];
@@ -214,6 +278,9 @@ __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
   float bpart[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int srow = tid >> 3, sc = (tid & 7) * 8;
   const int mt0 = 2 * (w >> 1), nt0 = 2 * (w & 1);
+  float mdz = 0.f;                                 // dz amax over the T steps (one slot per step)
+  for (int t = 0; t < T; ++t) mdz = fmaxf(mdz, amax_dz[t]);
+  const float sg = g16_scale_of(mdz), sx = g16_scale_of(*amax_xh);
   for (long rb = r_beg; rb < r_end; rb += 32) {
     const long r = rb + srow;
     float xv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, gv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -224,8 +291,8 @@ __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
       for (int c = 0; c < 8; ++c) bpart[c] += gv[c];
     }
     s8v xhi, xlo, ghi, glo;
-    split8b(xv, xhi, xlo);
-    split8b(gv, ghi, glo);
+    split8hs(xv, sx, xhi, xlo);
+    split8hs(gv, sg, ghi, glo);
     *reinterpret_cast<s8v*>(Xs[0] + srow * S + sc) = xhi;
     *reinterpret_cast<s8v*>(Xs[1] + srow * S + sc) = xlo;
     *reinterpret_cast<s8v*>(Gs[0] + srow * S + sc) = ghi;
@@ -246,7 +313,7 @@ __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma3(af[0][i], af[1][i], bf[0][jj], bf[1][jj], acc[i][jj]);
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma3h(af[0][i], af[1][i], bf[0][jj], bf[1][jj], acc[i][jj]);
     __syncthreads();
   }
 #pragma unroll
@@ -257,7 +324,7 @@ __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
       for (int r = 0; r < 4; ++r) {
         const int n = n0b + (mt0 + i) * 16 + 4 * grp + r;
         const int p = p0b + (nt0 + jj) * 16 + i16;
-        atomicAdd(&grad[k_off + (long)n * G4 + p], acc[i][jj][r]);
+        atomicAdd(&grad[k_off + (long)n * G4 + p], acc[i][jj][r] * (1.0f / (sx * sg)));
       }
   if (do_bias) {
 #pragma unroll
@@ -267,10 +334,10 @@ __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
   }
 }
 
-// operand copies of the fp32 master kernel: KpT2 = fp16 pair of K^T * 2^8 (permuted, forward), Kb2 = bf16 pair of K
-// (TF layout, backward); status |= 1 when a scaled weight leaves the fp16 range
+// operand copies of the fp32 master kernel: KpT2 = fp16 pair of K^T * 2^8 (permuted, forward), Kb2 = fp16 pair of
+// K * 2^8 (TF layout, backward); status |= 1 when a scaled weight leaves the fp16 range
 __global__ void lstm_refresh_x3_kernel(const float* __restrict__ flat, long k_off, int F, int H,
-                                       uint16_t* __restrict__ KpT2, bf16_t* __restrict__ Kb2,
+                                       uint16_t* __restrict__ KpT2, uint16_t* __restrict__ Kb2,
                                        uint32_t* __restrict__ status) {
   const int KK = F + H, G4 = 4 * H;
   const long n_el = (long)KK * G4;
@@ -278,11 +345,10 @@ __global__ void lstm_refresh_x3_kernel(const float* __restrict__ flat, long k_of
   if (idx >= n_el) return;
   const int n = (int)(idx / G4), col = (int)(idx - (long)n * G4);   // TF [n][col], col = g*H + u
   const float v = flat[k_off + idx];
-  const bf16_t bh = f2bf(v);
-  Kb2[idx] = bh;
-  Kb2[n_el + idx] = f2bf(v - bf2f(bh));
   const float x = v * (float)(1 << LX3_SHIFT);
   const uint16_t hh = f2h(x);
+  Kb2[idx] = hh;                                   // backward copy: the same fp16 pair of K * 2^8, TF layout
+  Kb2[n_el + idx] = f2h(x - h2f(hh));
   const int g = col / H, u = col - g * H;
   const int p = (u >> 4) * 64 + g * 16 + (u & 15);
   KpT2[(long)p * KK + n] = hh;
@@ -307,30 +373,43 @@ extern "C" {
 
 int launch_lstm_fwd_x3(const float* X, int ldx, const float* hprev, const float* cprev, const uint8_t* prev_done,
                        const void* KpT2, const float* flat, long b_off, float* hout, float* cout, float* gates,
-                       float* xh, void* status, int F, int H, int B, hipStream_t stream) {
+                       float* xh, void* status, float* amax_xh, int F, int H, int B, hipStream_t stream) {
   if (ldx <= 0 || F <= 0 || H <= 0 || B <= 0 || b_off < 0) return -22;
   if (F % 64 != 0 || H % 64 != 0 || ldx % 8 != 0 || ldx < F) return -1;
   dim3 grid((B + 63) / 64, H / 16);
   lstm_fwd_x3_kernel<<<grid, 256, 0, stream>>>(X, ldx, hprev, cprev, prev_done, (const uint16_t*)KpT2, flat, b_off,
-                                               hout, cout, gates, xh, (uint32_t*)status, F, H, B);
+                                               hout, cout, gates, xh, (uint32_t*)status, amax_xh, F, H, B);
   return (int)hipGetLastError();
 }
 
-int launch_lstm_bwd_gemm_x3(const float* dz, const void* Kb2, float* dx, int lddx, float* dh_prev, int F, int H,
-                            int B, hipStream_t stream) {
-  if (lddx <= 0 || F <= 0 || H <= 0 || B <= 0) return -22;
+int launch_lstm_bwd_point_x3(const float* dh_heads, const float* dh_rec, const float* dc_rec, const uint8_t* done_t,
+                             const float* gates, const float* c_t, const float* c_prev, const uint8_t* prev_done,
+                             float* dz, float* dc_out, float* amax_dz, int H, int B, hipStream_t stream) {
+  if (H <= 0 || B <= 0 || !amax_dz) return -22;
+  const long n = (long)B * H;
+  lstm_bwd_point_x3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(dh_heads, dh_rec, dc_rec, done_t, gates,
+                                                                            c_t, c_prev, prev_done, dz, dc_out,
+                                                                            amax_dz, H, B);
+  return (int)hipGetLastError();
+}
+
+int launch_lstm_bwd_gemm_x3(const float* dz, const void* Kb2, float* dx, int lddx, float* dh_prev,
+                            const float* amax_dz, int F, int H, int B, hipStream_t stream) {
+  if (lddx <= 0 || F <= 0 || H <= 0 || B <= 0 || !amax_dz) return -22;
   if (F % 64 != 0 || H % 64 != 0 || lddx < F) return -1;
   dim3 grid((B + 63) / 64, (F + H) / 64);
-  lstm_bwd_gemm_x3_kernel<<<grid, 256, 0, stream>>>(dz, (const bf16_t*)Kb2, dx, lddx, dh_prev, F, H, B);
+  lstm_bwd_gemm_x3_kernel<<<grid, 256, 0, stream>>>(dz, (const uint16_t*)Kb2, dx, lddx, dh_prev, amax_dz, F, H, B);
   return (int)hipGetLastError();
 }
 
 int launch_lstm_wgrad_x3(const float* xh, const float* dz, float* grad, long k_off, long b_off, int F, int H, long R,
-                         int rows_per_chunk, hipStream_t stream) {
-  if (F <= 0 || H <= 0 || R <= 0 || rows_per_chunk <= 0 || k_off < 0 || b_off < 0) return -22;
+                         int rows_per_chunk, const float* amax_dz, int T, const float* amax_xh, hipStream_t stream) {
+  if (F <= 0 || H <= 0 || R <= 0 || rows_per_chunk <= 0 || k_off < 0 || b_off < 0 || T <= 0 || !amax_dz || !amax_xh)
+    return -22;
   if (F % 64 != 0 || H % 64 != 0 || rows_per_chunk % 32 != 0) return -1;
   dim3 grid((F + H) / 64, (4 * H) / 64, (unsigned)((R + rows_per_chunk - 1) / rows_per_chunk));
-  lstm_wgrad_x3_kernel<<<grid, 256, 0, stream>>>(xh, dz, grad, k_off, b_off, F, H, R, rows_per_chunk);
+  lstm_wgrad_x3_kernel<<<grid, 256, 0, stream>>>(xh, dz, grad, k_off, b_off, F, H, R, rows_per_chunk, amax_dz, T,
+                                                 amax_xh);
   return (int)hipGetLastError();
 }
 
@@ -339,7 +418,7 @@ int launch_lstm_refresh_x3(const float* flat, long k_off, int F, int H, void* Kp
   if (F <= 0 || H <= 0 || k_off < 0) return -22;
   const long n = (long)(F + H) * 4 * H;
   lstm_refresh_x3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(flat, k_off, F, H, (uint16_t*)KpT2,
-                                                                          (bf16_t*)Kb2, (uint32_t*)status);
+                                                                          (uint16_t*)Kb2, (uint32_t*)status);
   return (int)hipGetLastError();
 }
 

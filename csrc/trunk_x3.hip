@@ -190,6 +190,40 @@ DEVI f4v mma2(const s8v& a, const s8v& bh, const s8v& bl, f4v c) {
   c = mfma16(a, bl, c);
   return mfma16(a, bh, c);
 }
+// exact operand a (uint8 pixels in fp16) against an fp16 pair b
+DEVI f4v mma2h(const s8v& a, const s8v& bh, const s8v& bl, f4v c) {
+  c = mfma16_f16(a, bl, c);
+  return mfma16_f16(a, bh, c);
+}
+
+// ---- scaled fp16-pair gradients ("G16") ----
+// Every output gradient G of a trunk layer enters the backward GEMMs as the fp16 pair of G * 2^e, one power of two per
+// layer and update chosen from the tensor's largest magnitude (amax) so that amax * 2^e lies in [2^13, 2^14): 22
+// significant bits down to amax * 2^-27 (the bf16 pair kept 16), on the f16 MFMA at the bf16 rate, and the
+// activation operands (already fp16 pairs) need no conversion.  The producer of G writes its amax: x3_amax for the
+// last layer's input gradient (heads / LSTM), the input-gradient epilogues (conv_dgrad_x3, fc_dgrad_gemm_x3,
+// fc_dgrad_x3) for the layer below; float bits of non-negative values order like unsigned ints, so one
+// atomicMax per wave.  scripts/x3_numerics.py: per-layer weight-gradient error 1.1-1.8e-5 (bf16 pairs) -> 2-3e-7.
+DEVI float g16_scale(const float* amax) {
+  const uint32_t b = __float_as_uint(*amax);
+  const int e = (int)((b >> 23) & 0xFFu) - 127;           // floor(log2 amax) (normal amax)
+  if ((b & 0x7FFFFFFFu) == 0u || e < -110 || e >= 128) return 1.0f;   // zero / tiny / non-finite: unscaled
+  const int se = min(13 - e, 126);
+  return __uint_as_float((uint32_t)(se + 127) << 23);
+}
+DEVI void g16_flush_amax(float m, float* __restrict__ amax) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m > 0.f && amax) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+}
+// 8 values * s -> fp16 pair
+DEVI void split8hs(const float (&v)[8], float s, s8v& hi, s8v& lo) {
+  float t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = v[j] * s;
+  split8h(t, hi, lo);
+}
+
 // 8 x uint8 -> 8 x fp16 holding the exact pixel value: fp16(1024 + v) built by v_perm, minus 1024 (exact)
 DEVI s8v u8x8_to_f16(uint2 v) {
   h8v x = __builtin_bit_cast(h8v, u8x8_to_f16off(v));
@@ -1115,8 +1149,8 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
                                                             const int* __restrict__ act_cnt, int layer, int L, int M,
                                                             int P, int E, int T, long bits_rows, int units_per_wg,
                                                             float in_scale, float g_scale,
-                                                            const uint8_t* __restrict__ fcv = nullptr,
-                                                            int nslots = 0) {
+                                                            const uint8_t* __restrict__ fcv, int nslots,
+                                                            const float* __restrict__ gamax) {
   using SB = Slab<G, OB>;
   static_assert(!RING || (G::U8 && G::CIN == 4 && G::WIN % 4 == 0), "ring input: uint8 4-channel first layer");
   // ring: 4-pixel groups per slab (one 16-byte LDS store each; 8-pixel groups, one round of loads but four stores
@@ -1165,6 +1199,7 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
       aoff[ks][hf] = ob * G::S * SB::RL + ow * SB::PS + 4 * pp;
     }
   const int npass = (nct + NCXP - 1) / NCXP;
+  const float gs = g16_scale(gamax), ginv = 1.0f / gs;   // G16: the staged gradient is the fp16 pair of G * 2^e
   using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
   auto run = [&](auto ncc, const int ct0) {
     constexpr int NC = decltype(ncc)::value;
@@ -1265,8 +1300,8 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
             s8v v0 = {0, 0, 0, 0, 0, 0, 0, 0}, v1 = v0;
             if (gi * 4 < Rg.navail) {
               const uint4 px = planes_to_px4(Rg.xq[j]);
-              v0 = u8x8_to_bf16(make_uint2(px.x, px.y));
-              v1 = u8x8_to_bf16(make_uint2(px.z, px.w));
+              v0 = u8x8_to_f16(make_uint2(px.x, px.y));      // pixels exact in fp16
+              v1 = u8x8_to_f16(make_uint2(px.z, px.w));
             }
             *reinterpret_cast<s8v*>(&Xs[buf][0][gi * 16]) = v0;
             *reinterpret_cast<s8v*>(&Xs[buf][0][gi * 16 + 8]) = v1;
@@ -1280,10 +1315,13 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
           const bool ok = gi * 8 < Rg.navail;
           s8v v = {0, 0, 0, 0, 0, 0, 0, 0};
           if constexpr (G::U8) {
-            if (ok) v = u8x8_to_bf16(Rg.xr[j]);
+            if (ok) v = u8x8_to_f16(Rg.xr[j]);                            // pixels exact in fp16
           } else {
             s8v vl = v;
-            if (ok) x16pair_to_bf16pair(Rg.xr[j], Rg.xl[j], v, vl);      // fp16 pair -> bf16 pair
+            if (ok) {                                                     // the activation's fp16 pair as is
+              v = Rg.xr[j];
+              vl = Rg.xl[j];
+            }
             *reinterpret_cast<s8v*>(&Xs[buf][XL ? 1 : 0][gi * 8]) = vl;
           }
           *reinterpret_cast<s8v*>(&Xs[buf][0][gi * 8]) = v;
@@ -1311,7 +1349,7 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
 #pragma unroll
             for (int c = 0; c < 4; ++c) acc_b[k][c] += (f2v_){m[2 * c], m[2 * c + 1]};
             s8v hi, lo;
-            split8(m, hi, lo);
+            split8hs(m, gs, hi, lo);
             *reinterpret_cast<s8v*>(&Gs[buf][0][rho * GS + rel * 8]) = hi;
             *reinterpret_cast<s8v*>(&Gs[buf][1][rho * GS + rel * 8]) = lo;
           }
@@ -1339,10 +1377,10 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
           if constexpr (XL) {
             const s8v al = tr8(xlp + kb + aoff[ks][0], xlp + kb + aoff[ks][1]);
 #pragma unroll
-            for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma3(ah, al, bh[nt], bl[nt], acc[mi][nt]);
+            for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma3h(ah, al, bh[nt], bl[nt], acc[mi][nt]);
           } else {
 #pragma unroll
-            for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma2(ah, bh[nt], bl[nt], acc[mi][nt]);
+            for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma2h(ah, bh[nt], bl[nt], acc[mi][nt]);
           }
         }
       }
@@ -1409,7 +1447,7 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int k = mt * 16 + 4 * grp + r;
-            if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale));
+            if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale * ginv));
           }
         }
       }
@@ -1449,7 +1487,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
                                                        const int* __restrict__ act_idx,
                                                        const int* __restrict__ act_cnt, int layer, int L, int M, int P,
                                                        int E, int T, long bits_rows, int rows_per_chunk,
-                                                       float in_scale, float g_scale) {
+                                                       float in_scale, float g_scale, const float* __restrict__ gamax) {
   static_assert(!G::U8 && G::HOWO > X3_WG_RB, "bf16 input; one row wrap per stage");
   constexpr int XS = G::KP + 8;
   constexpr int GS = X3_NCX * 16 + 8;
@@ -1476,6 +1514,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
   const int grow = tid >> 3, gsl = tid & 7;       // G staging role (threads < 256): row, slot of the pass
   const int npass = (nct + X3_NCX - 1) / X3_NCX;
+  const float gs = g16_scale(gamax), ginv = 1.0f / gs;   // G16
   int xkoff[XIT];
 #pragma unroll
   for (int j = 0; j < XIT; ++j) {
@@ -1529,7 +1568,10 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
         if (it < X3_WG_RB * G::KC) {
           const int row = it / G::KC, kc = it - row * G::KC;
           s8v bh = {0, 0, 0, 0, 0, 0, 0, 0}, bl = bh;
-          if (xv[j]) x16pair_to_bf16pair(xh[j], xlr[j], bh, bl);     // fp16 pair -> bf16 pair
+          if (xv[j]) {                                                // the activation's fp16 pair as is
+            bh = xh[j];
+            bl = xlr[j];
+          }
           *reinterpret_cast<s8v*>(&Xs[buf][0][row * XS + kc * 8]) = bh;
           *reinterpret_cast<s8v*>(&Xs[buf][1][row * XS + kc * 8]) = bl;
         }
@@ -1543,7 +1585,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
 #pragma unroll
         for (int c = 0; c < 8; ++c) bpart[c] += m[c];
         s8v hi, lo;
-        split8(m, hi, lo);
+        split8hs(m, gs, hi, lo);
         *reinterpret_cast<s8v*>(&Gs[buf][0][grow * GS + gsl * 8]) = hi;
         *reinterpret_cast<s8v*>(&Gs[buf][1][grow * GS + gsl * 8]) = lo;
       }
@@ -1564,7 +1606,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
           const s8v ah = tr8(Xs[buf][0] + o0, Xs[buf][0] + o1);
           const s8v al = tr8(Xs[buf][1] + o0, Xs[buf][1] + o1);
 #pragma unroll
-          for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma3(ah, al, bh[nt], bl[nt], acc[mi][nt]);
+          for (int nt = 0; nt < NC; ++nt) acc[mi][nt] = mma3h(ah, al, bh[nt], bl[nt], acc[mi][nt]);
         }
       }
     };
@@ -1595,7 +1637,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int k = mt * 16 + 4 * grp + r;
-              if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale));
+              if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale * ginv));
             }
           }
         }
@@ -1653,7 +1695,8 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
                                                                    int chunk, const int* __restrict__ act_idx,
                                                                    const int* __restrict__ act_cnt, int layer, int L,
                                                                    int M, int P, int E, int T, long bits_rows,
-                                                                   int samples_per_wg, float in_scale, float g_scale) {
+                                                                   int samples_per_wg, float in_scale, float g_scale,
+                                                                   const float* __restrict__ gamax) {
   using W = WT3<G>;
   __shared__ __attribute__((aligned(16))) bf16_t Xt[2][2][W::TILEP];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][2][W::NPP * W::GS];
@@ -1704,6 +1747,7 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
   const int nct = (cnt + 1) >> 1;
   const int npass = (nct + 1) / 2;
   const int a_my = tid & 3;                       // the slot (within the pass) of every staging item of this thread
+  const float gs = g16_scale(gamax), ginv = 1.0f / gs;   // G16
   for (int pass = 0; pass < npass; ++pass) {
     const int ct0 = pass * 2;
     const int nc = min(2, nct - ct0);
@@ -1734,11 +1778,9 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
       }
     };
     auto write_sample = [&](int buf) {
-      if (tid < W::NXC) {
-        s8v bh, bl;
-        x16pair_to_bf16pair(xh, xl, bh, bl);
-        *reinterpret_cast<s8v*>(&Xt[buf][0][tid * 8]) = bh;
-        *reinterpret_cast<s8v*>(&Xt[buf][1][tid * 8]) = bl;
+      if (tid < W::NXC) {                          // the activation's fp16 pair as is
+        *reinterpret_cast<s8v*>(&Xt[buf][0][tid * 8]) = xh;
+        *reinterpret_cast<s8v*>(&Xt[buf][1][tid * 8]) = xl;
       }
 #pragma unroll
       for (int j = 0; j < W::GIT; ++j) {
@@ -1750,7 +1792,7 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
 #pragma unroll
           for (int c = 0; c < 8; ++c) bpart[c] += m[c];
           s8v hi, lo;
-          split8(m, hi, lo);
+          split8hs(m, gs, hi, lo);
           const int o = (it >> 2) * W::GS + a_my * 8;
           *reinterpret_cast<s8v*>(&Gs[buf][0][o]) = hi;
           *reinterpret_cast<s8v*>(&Gs[buf][1][o]) = lo;
@@ -1769,7 +1811,7 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
           const int o1 = (ks * 32 + 8 * grp + 4 + q) * W::GS + nt * 16 + 4 * pp;
           const s8v bh = tr8(Gs[buf][0] + o0, Gs[buf][0] + o1);
           const s8v bl = tr8(Gs[buf][1] + o0, Gs[buf][1] + o1);
-          acc[nt] = mma3(ah, al, bh, bl, acc[nt]);
+          acc[nt] = mma3h(ah, al, bh, bl, acc[nt]);
         }
       }
     };
@@ -1792,7 +1834,7 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int k = w * 16 + 4 * grp + r;
-          if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[nt][r] * (in_scale * g_scale));
+          if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[nt][r] * (in_scale * g_scale * ginv));
         }
       }
     }
@@ -1832,7 +1874,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
                                                        const int* __restrict__ act_idx,
                                                        const int* __restrict__ act_cnt, int layer, int L, int M, int P,
                                                        int E, int T, long bits_rows, float g_scale,
-                                                       float* __restrict__ dX, int samples_per_wg) {
+                                                       float* __restrict__ dX, int samples_per_wg,
+                                                       const float* __restrict__ gamax, float* __restrict__ gamax_out) {
   using D = DGM<G>;
   constexpr int S = D::S;
   constexpr int NTAPP = (D::NTAP + 3) & ~3;
@@ -1871,7 +1914,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
         for (int c = 0; c < 8; ++c) v[c] = wp[c];
       }
       s8v hi, lo;
-      split8(v, hi, lo);
+      split8hs(v, (float)(1 << X3_W0_SHIFT), hi, lo);       // fp16 pair of W * 2^8 (G16)
       const int o = (tap * D::NT * 16 + n) * 32 + (a4 ^ dg_swz(n)) * 8;
       *reinterpret_cast<s8v*>(Bs[0] + o) = hi;
       *reinterpret_cast<s8v*>(Bs[1] + o) = lo;
@@ -1922,6 +1965,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
     nofs[nt] = ((cls / S) * G::WIN + npw[nt]) * 8 + ci;
   }
   if (ngroup == 1) stage_b(0);
+  const float gs = g16_scale(gamax), inv = 1.0f / (gs * (float)(1 << X3_W0_SHIFT));
+  float am = 0.f;
   load_sample(s_beg);
   for (int s = s_beg; s < s_end; ++s) {
     const long sg = sample_global(p, s, E, PE, 0);
@@ -1941,7 +1986,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
             float m[8];
             mask8(gg, (uint32_t)b, m);
             s8v hi, lo;
-            split8(m, hi, lo);
+            split8hs(m, gs, hi, lo);
             const int o = pos * X3_DG_PSTR + (a4 ^ dg_swz(pos)) * 8;
             *reinterpret_cast<s8v*>(Gs[0] + o) = hi;
             *reinterpret_cast<s8v*>(Gs[1] + o) = lo;
@@ -1965,7 +2010,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
           for (int nt = 0; nt < D::NT; ++nt) {
             const s8v bh = *reinterpret_cast<const s8v*>(Bs[0] + bo + nt * 16 * 32);
             const s8v bl = *reinterpret_cast<const s8v*>(Bs[1] + bo + nt * 16 * 32);
-            acc[nt] = mma3(ah, al, bh, bl, acc[nt]);
+            acc[nt] = mma3h(ah, al, bh, bl, acc[nt]);
           }
         }
         const uint2 e4 = *reinterpret_cast<const uint2*>(etab + rt * 16 + 4 * grp);
@@ -1979,13 +2024,16 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
             const bool okw = npw[nt] == 0 || ((v >> 15) & 1u);
             if (v != 0xFFFFu && okh && okw) {
               float* o = dXs + (int)(v & 0x3FFFu) + nofs[nt];
-              *o = g == 0 ? acc[nt][r] : *o + acc[nt][r];
+              const float y = g == 0 ? acc[nt][r] * inv : *o + acc[nt][r] * inv;
+              *o = y;
+              if (g == ngroup - 1) am = fmaxf(am, fabsf(y));
             }
           }
         }
       }
     }
   }
+  g16_flush_amax(am, gamax_out);
 }
 
 // ===========================================================================
@@ -2726,7 +2774,8 @@ __global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, 
                                                    int layer, int L, int M, int K, int KP, int P, int E, int T,
                                                    long bits_rows, float g_scale, float* __restrict__ dX,
                                                    int chunks_per_split, int nrowb, int nsplit,
-                                                   bf16_t* __restrict__ Gm, long gmlo) {
+                                                   bf16_t* __restrict__ Gm, long gmlo,
+                                                   const float* __restrict__ gamax, float* __restrict__ gamax_out) {
   constexpr int CS = COUT + 8;
   constexpr int NW = COUT / 16;
   constexpr int NSL = 2;                               // slots per group
@@ -2754,6 +2803,8 @@ __global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, 
       sg_out[rb][r] = row < R ? sample_global(p, (int)row, E, PE, 0) : -1;
     }
   const int ngroups = cnt > 0 ? (cnt + NSL - 1) / NSL : 1;
+  const float gs = g16_scale(gamax), inv = 1.0f / (gs * (float)(1 << X3_W0_SHIFT));
+  float am = 0.f;
   for (int gi = 0; gi < ngroups; ++gi) {
     const int g0 = gi * NSL;
     const int ng = min(NSL, cnt - g0);
@@ -2780,7 +2831,7 @@ __global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, 
 #pragma unroll
           for (int j = 0; j < 8; ++j) m[j] = ((bw >> j) & 1u) ? gv[j] : 0.f;
           s8v hi, lo;
-          split8(m, hi, lo);
+          split8hs(m, gs, hi, lo);
           *reinterpret_cast<s8v*>(Gs[0] + (a * 64 + sr) * CS + c) = hi;
           *reinterpret_cast<s8v*>(Gs[1] + (a * 64 + sr) * CS + c) = lo;
           if (Gm != nullptr && v && (tid & 7) % nsplit == bz) {
@@ -2829,7 +2880,7 @@ __global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, 
         for (int rb = 0; rb < 4; ++rb) {
           const s8v fh = *reinterpret_cast<const s8v*>(Gs[0] + ao + rb * 16 * CS + 32 * c);
           const s8v fl = *reinterpret_cast<const s8v*>(Gs[1] + ao + rb * 16 * CS + 32 * c);
-          acc[rb] = mma3(fh, fl, bh[c], bl[c], acc[rb]);
+          acc[rb] = mma3h(fh, fl, bh[c], bl[c], acc[rb]);
         }
       const int kcol = ch * 128 + w * 16 + c16;
       if (a == ng - 1 && kcol < K) {
@@ -2840,7 +2891,9 @@ __global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, 
             const long sg = sg_out[rb][r];
             if (sg >= 0) {
               float* o = dX + sg * K + kcol;
-              *o = gi == 0 ? acc[rb][r] : *o + acc[rb][r];
+              const float v = gi == 0 ? acc[rb][r] * inv : *o + acc[rb][r] * inv;
+              *o = v;
+              if (gi == ngroups - 1) am = fmaxf(am, fabsf(v));
             }
           }
       }
@@ -2861,6 +2914,7 @@ __global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, 
       body(b0h, b0l, it);
     }
   }
+  g16_flush_amax(am, gamax_out);
 }
 
 // ===========================================================================
@@ -2875,7 +2929,8 @@ __global__ __launch_bounds__(512) void fc_dgrad_x3(const float* __restrict__ G, 
 template <int COUT>
 __global__ __launch_bounds__(256) void fc_gm_x3(const float* __restrict__ G, const uint16_t* __restrict__ bits,
                                                 const int* __restrict__ act_cnt, int layer, int L, int P, int E, int T,
-                                                long bits_rows, float g_scale, bf16_t* __restrict__ Gm, long gmlo) {
+                                                long bits_rows, float g_scale, bf16_t* __restrict__ Gm, long gmlo,
+                                                const float* __restrict__ gamax) {
   constexpr int NW = COUT / 16, C8 = COUT / 8;
   const int R = T * E;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
@@ -2889,13 +2944,14 @@ __global__ __launch_bounds__(256) void fc_gm_x3(const float* __restrict__ G, con
   const float4 a1 = *reinterpret_cast<const float4*>(G + sg * COUT + c + 4);
   const float gv[8] = {a0.x * g_scale, a0.y * g_scale, a0.z * g_scale, a0.w * g_scale,
                        a1.x * g_scale, a1.y * g_scale, a1.z * g_scale, a1.w * g_scale};
+  const float gs = g16_scale(gamax);
   for (int a = 0; a < cnt; ++a) {
     const uint32_t bw = (uint32_t)bits[((long)a * bits_rows + sg) * NW + (c >> 4)] >> (c & 15);
     float m[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) m[j] = ((bw >> j) & 1u) ? gv[j] : 0.f;
     s8v hi, lo;
-    split8(m, hi, lo);
+    split8hs(m, gs, hi, lo);                   // Gm: the fp16 pair of the masked gradient * 2^e (G16)
     bf16_t* gp = Gm + ((long)a * bits_rows + sg) * COUT + c;
     *reinterpret_cast<s8v*>(gp) = hi;
     *reinterpret_cast<s8v*>(gp + gmlo) = lo;
@@ -2908,7 +2964,8 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
                                                         const int* __restrict__ act_idx,
                                                         const int* __restrict__ act_cnt, int layer, int L, int M, int K,
                                                         int KP, int P, int E, int T, long bits_rows,
-                                                        float* __restrict__ dX, int nrb, int ncb) {
+                                                        float* __restrict__ dX, int nrb, int ncb,
+                                                        const float* __restrict__ gamax, float* __restrict__ gamax_out) {
   constexpr int BM = 128, BN = 256, CS = COUT / 32;                 // reduction steps per slot
   __shared__ __attribute__((aligned(16))) bf16_t As[2][2][BM * 32];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[2][2][BN * 32];
@@ -2975,7 +3032,7 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
         const s8v ah = *reinterpret_cast<const s8v*>(&As[buf][0][o]);
         const s8v al = *reinterpret_cast<const s8v*>(&As[buf][1][o]);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mma3(ah, al, bh[jj], bl[jj], acc[i][jj]);
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mma3h(ah, al, bh[jj], bl[jj], acc[i][jj]);
       }
     };
     // set 0 holds the even steps' loads, set 1 the odd ones; step s stores step s + 1's set, then reloads it with
@@ -3000,7 +3057,10 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
 #undef DG_LOAD
 #undef DG_STORE
   }
-  // epilogue: rows-as-A D layout, fp32 dX (zeros for a path with no active slot)
+  // epilogue: rows-as-A D layout, fp32 dX (zeros for a path with no active slot); Gm * 2^e against W * 2^8, so
+  // scaled back by 2^-(e + 8); the amax of dX for the layer below (G16)
+  const float inv = 1.0f / (g16_scale(gamax) * (float)(1 << X3_W0_SHIFT));
+  float am = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -3011,10 +3071,15 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int k = col0 + wn * 64 + jj * 16 + c16;
-        if (k < K) o[k] = acc[i][jj][r];
+        if (k < K) {
+          const float v = acc[i][jj][r] * inv;
+          o[k] = v;
+          am = fmaxf(am, fabsf(v));
+        }
       }
     }
   }
+  g16_flush_amax(am, gamax_out);
 }
 
 // ===========================================================================
@@ -3028,7 +3093,8 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
                                                       const int* __restrict__ inv_path,
                                                       const int* __restrict__ inv_slot,
                                                       const int* __restrict__ inv_cnt, int layer, int M, int Pmax,
-                                                      int K, int P, int E, int T, long bits_rows, int nsplit) {
+                                                      int K, int P, int E, int T, long bits_rows, int nsplit,
+                                                      const float* __restrict__ gamax) {
   constexpr int XS = 128 + 8;
   constexpr int GS = COUT + 8;
   constexpr int NT = COUT / 32;
@@ -3087,12 +3153,8 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
   gload(0);
   for (int it = 0; it < n_it; ++it) {
     const int buf = it & 1;
-    {
-      s8v bh, bl;
-      x16pair_to_bf16pair(xrh, xrl, bh, bl);          // fp16 pair -> bf16 pair (zeros stay zeros)
-      *reinterpret_cast<s8v*>(Xs[buf][0] + lr * XS + lxs) = bh;
-      *reinterpret_cast<s8v*>(Xs[buf][1] + lr * XS + lxs) = bl;
-    }
+    *reinterpret_cast<s8v*>(Xs[buf][0] + lr * XS + lxs) = xrh;     // the activation's fp16 pair as is (G16)
+    *reinterpret_cast<s8v*>(Xs[buf][1] + lr * XS + lxs) = xrl;
 #pragma unroll
     for (int h = 0; h < GSEG / 8; ++h) {
       *reinterpret_cast<s8v*>(Gsh[buf][0] + lr * GS + lgs + 8 * h) = grh[h];
@@ -3114,15 +3176,16 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
       const int o0 = (8 * grp + q) * GS + nb + 4 * pp, o1 = (8 * grp + 4 + q) * GS + nb + 4 * pp;
       const s8v bh = tr8(Gsh[buf][0] + o0, Gsh[buf][0] + o1);
       const s8v bl = tr8(Gsh[buf][1] + o0, Gsh[buf][1] + o1);
-      acc[0][jj] = mma3(afh[0], afl[0], bh, bl, acc[0][jj]);
-      acc[1][jj] = mma3(afh[1], afl[1], bh, bl, acc[1][jj]);
+      acc[0][jj] = mma3h(afh[0], afl[0], bh, bl, acc[0][jj]);
+      acc[1][jj] = mma3h(afh[1], afl[1], bh, bl, acc[1][jj]);
       if (do_bias) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) bsum[jj] += bf2f((uint16_t)bh[e]) + bf2f((uint16_t)bl[e]);
+        for (int e = 0; e < 8; ++e) bsum[jj] += h2f((uint16_t)bh[e]) + h2f((uint16_t)bl[e]);
       }
     }
   }
   const long base = w_off + (long)j * chunk;
+  const float ginv = 1.0f / g16_scale(gamax);          // Gm holds the gradient * 2^e
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -3132,14 +3195,14 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
         const int k = k0 + 32 * wk + 16 * i + 4 * grp + r;
         const int n = (COUT / 2) * wn + 16 * jj + i16;
         if (k < K) {
-          if (nsplit == 1) grad[base + (long)k * COUT + n] = acc[i][jj][r];
-          else atomicAdd(&grad[base + (long)k * COUT + n], acc[i][jj][r]);
+          if (nsplit == 1) grad[base + (long)k * COUT + n] = acc[i][jj][r] * ginv;
+          else atomicAdd(&grad[base + (long)k * COUT + n], acc[i][jj][r] * ginv);
         }
       }
   if (do_bias) {
 #pragma unroll
     for (int jj = 0; jj < NT; ++jj) {
-      float v = bsum[jj];
+      float v = bsum[jj] * ginv;
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
       if (grp == 0) {
@@ -3161,7 +3224,7 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
                                                    const int* __restrict__ inv_path, const int* __restrict__ inv_slot,
                                                    const int* __restrict__ inv_cnt, int layer, int M, int Pmax, int K,
                                                    int Cout, int P, int E, int T, long bits_rows, float g_scale,
-                                                   int nsplit) {
+                                                   int nsplit, const float* __restrict__ gamax) {
   constexpr int S = 64 + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][32 * S];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][32 * S];
@@ -3184,6 +3247,7 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
   float bpart[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int srow = tid >> 3, sc = (tid & 7) * 8;
   const int mt0 = 2 * (w >> 1), nt0 = 2 * (w & 1);
+  const float gs = g16_scale(gamax), ginv = 1.0f / gs;
   for (int u = u_beg; u < u_end; ++u) {
     const int p = inv_path[(layer * M + j) * Pmax + u];
     const int a = inv_slot[(layer * M + j) * Pmax + u];
@@ -3210,11 +3274,10 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
           }
         }
       }
-      s8v gh, gl, bh, bl;
-      split8(m, gh, gl);
-      x16pair_to_bf16pair(xh, xl, bh, bl);            // fp16 pair -> bf16 pair
-      *reinterpret_cast<s8v*>(Xs[0] + srow * S + sc) = bh;
-      *reinterpret_cast<s8v*>(Xs[1] + srow * S + sc) = bl;
+      s8v gh, gl;
+      split8hs(m, gs, gh, gl);                         // G16: fp16 pair of the masked gradient * 2^e
+      *reinterpret_cast<s8v*>(Xs[0] + srow * S + sc) = xh;     // the activation's fp16 pair as is
+      *reinterpret_cast<s8v*>(Xs[1] + srow * S + sc) = xl;
       *reinterpret_cast<s8v*>(Gs[0] + srow * S + sc) = gh;
       *reinterpret_cast<s8v*>(Gs[1] + srow * S + sc) = gl;
       __syncthreads();
@@ -3231,7 +3294,7 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma3(afh[i], afl[i], bfh[jj], bfl[jj], acc[i][jj]);
+        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = mma3h(afh[i], afl[i], bfh[jj], bfl[jj], acc[i][jj]);
       __syncthreads();
     }
   }
@@ -3245,8 +3308,8 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
         const int k = k0b + (mt0 + i) * 16 + 4 * grp + r;
         const int n = n0b + (nt0 + jj) * 16 + i16;
         if (k < K && n < Cout) {
-          if (nsplit == 1) grad[base + (long)k * Cout + n] = acc[i][jj][r];
-          else atomicAdd(&grad[base + (long)k * Cout + n], acc[i][jj][r]);
+          if (nsplit == 1) grad[base + (long)k * Cout + n] = acc[i][jj][r] * ginv;
+          else atomicAdd(&grad[base + (long)k * Cout + n], acc[i][jj][r] * ginv);
         }
       }
   if (do_bias) {
@@ -3262,7 +3325,7 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
 
 // hi/lo operand copies of one layer's weights: Wc [2][M][Cout][KP] (forward B operand, k contiguous, zero padded):
 // the fp16 pair of W * 2^X3_W0_SHIFT (f16 != 0) or the bf16 pair of W; optionally WcT [2][M][KP][Cout] (the fc input
-// gradient's B operand): always the bf16 pair, as the output gradients it meets.  *status |= X3_RANGE_W when a scaled
+// gradient's B operand): the fp16 pair of W * 2^X3_W0_SHIFT, as the scaled fp16-pair gradients it meets (G16).  *status |= X3_RANGE_W when a scaled
 // weight leaves the fp16 range; x3_status_fold (end of the next rollout) moves it and the forward epilogues' flag
 // into the update's all-reduced counters, where every rank sees it (algo/trainer.py raises X3RangeError)
 __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict__ flat, long w_off, int chunk, int K,
@@ -3287,9 +3350,11 @@ __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict
     const long wi = ((long)j * Cout + c) * KP + k;
     Wc[wi] = hi;
     Wc[n + wi] = lo;
-    if (WcT) {
-      WcT[i] = bh;
-      WcT[n + i] = bl;
+    if (WcT) {                       // the fc input gradient's B operand: fp16 pair of W * 2^8 (meets G16 gradients)
+      const float x = v * (float)(1 << X3_W0_SHIFT);
+      const uint16_t th = f2h(x);
+      WcT[i] = th;
+      WcT[n + i] = f2h(x - h2f(th));
     }
   }
 }
@@ -3479,9 +3544,9 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
 
 int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, const void* bits, float* grad, long w_off,
                         long b_off, int chunk, const int* ai, const int* ac, int L, int M, int P, int E, int T,
-                        int nslots, long br, float is, float gs, hipStream_t st) {
+                        int nslots, long br, float is, float gs, const float* gamax, hipStream_t st) {
   if (!frames || !fc || chunk <= 0 || L <= 0 || M <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 || w_off < 0 ||
-      b_off < 0 || nslots < T + 3) return -22;
+      b_off < 0 || nslots < T + 3 || !gamax) return -22;
   if (M > 2 * X3_NCT) return 0;
   using SB = Slab<C1, 2>;
   const long units = (long)T * E * SB::NB;
@@ -3492,28 +3557,29 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (X3_C1_WG_NCX == 2 && X3_WGRAD_PF != 1)       // 2 tiles per pass: two stages in flight fit (162 VGPRs)
     conv_wgrad_slab_x3<C1, 2, 2, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax);
   else if (X3_C1_WG_NCX == 2)
     conv_wgrad_slab_x3<C1, 2, 1, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax);
   else if (X3_WGRAD_PF == 2)
     conv_wgrad_slab_x3<C1, 2, 2, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots);
+                                                             (const uint8_t*)fc, nslots, gamax);
   else
     conv_wgrad_slab_x3<C1, 2, 1, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots);
+                                                             (const uint8_t*)fc, nslots, gamax);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
 
 int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void* bits, float* grad, long w_off,
                   long b_off, int chunk, const int* ai, const int* ac, int layer, int L, int M, int Hin, int Win,
-                  int Cin, int KH, int KW, int S, int P, int E, int T, long br, float is, float gs, hipStream_t st) {
+                  int Cin, int KH, int KW, int S, int P, int E, int T, long br, float is, float gs,
+                  const float* gamax, hipStream_t st) {
   if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 || P <= 0 ||
-      E <= 0 || T <= 0 || br <= 0 || u8in < 0 || w_off < 0 || b_off < 0 || layer < 0 || xlo < 0) return -22;
+      E <= 0 || T <= 0 || br <= 0 || u8in < 0 || w_off < 0 || b_off < 0 || layer < 0 || xlo < 0 || !gamax) return -22;
   if (M > 2 * X3_NCT) return 0;
   auto slab = [&](auto gc, auto obc) {
     using Gx = typename decltype(gc)::type;
@@ -3526,10 +3592,12 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     const int pf = Gx::U8 ? (X3_WGRAD_PF == 2 ? 2 : 1) : (X3_WGRAD_PF >= 2 ? 2 : 1);
     if (pf == 2)
       conv_wgrad_slab_x3<Gx, OB, 2><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
-                                                          ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs);
+                                                          ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs, nullptr,
+                                                          0, gamax);
     else
       conv_wgrad_slab_x3<Gx, OB, 1><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
-                                                          ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs);
+                                                          ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs, nullptr,
+                                                          0, gamax);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   };
@@ -3545,7 +3613,7 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     if (spw < 4) spw = 4;
     conv_wgrad_tile_x3<C3><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), WT3<C3>::NT, 0, st>>>(
         (const uint16_t*)X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br,
-        (int)spw, is, gs);
+        (int)spw, is, gs, gamax);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   }
@@ -3557,7 +3625,7 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     if (rpc < X3_WG_RB * 4) rpc = X3_WG_RB * 4;
     conv_wgrad_x3<C3><<<dim3((unsigned)((rows + rpc - 1) / rpc), P), 512, 0, st>>>(
         (const bf16_t*)X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br,
-        (int)rpc, is, gs);
+        (int)rpc, is, gs, gamax);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   }
@@ -3566,9 +3634,9 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
 
 int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_off, int chunk, const int* ai,
                   const int* ac, int layer, int L, int M, int Hin, int Win, int Cin, int KH, int KW, int S, int P,
-                  int E, int T, long br, float gs, float* dX, hipStream_t st) {
+                  int E, int T, long br, float gs, float* dX, const float* gamax, float* gamax_out, hipStream_t st) {
   if (chunk <= 0 || L <= 0 || M <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || KH <= 0 || KW <= 0 || S <= 0 || P <= 0 ||
-      E <= 0 || T <= 0 || br <= 0 || w_off < 0 || layer < 0) return -22;
+      E <= 0 || T <= 0 || br <= 0 || w_off < 0 || layer < 0 || !gamax) return -22;
   if (M > 2 * X3_NCT) return 0;
   const int nsamp = T * E;
   int spw = (nsamp + 31) / 32;
@@ -3577,7 +3645,7 @@ int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_o
 #define DGX(Gx)                                                                                                    \
   if (x3_is<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                                    \
     conv_dgrad_x3<Gx><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, \
-                                            T, br, gs, dX, spw);                                                   \
+                                            T, br, gs, dX, spw, gamax, gamax_out);                                 \
     const int rc = (int)hipGetLastError();                                                                         \
     return rc ? -rc : 1;                                                                                           \
   }
@@ -3701,22 +3769,22 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
 
 int x3_fc_dgrad(const float* G, const void* bits, const void* WcT, long wlo, const int* ai, const int* ac, int layer,
                 int L, int M, int K, int KP, int Cout, int P, int E, int T, long br, float gs, float* dX, void* Gm,
-                long gmlo, hipStream_t st) {
+                long gmlo, const float* gamax, float* gamax_out, hipStream_t st) {
   if (L <= 0 || M <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 || layer < 0 ||
-      wlo <= 0 || gmlo < 0 || (Gm && gmlo <= 0)) return -22;
+      wlo <= 0 || gmlo < 0 || (Gm && gmlo <= 0) || !gamax) return -22;
   if (M > X3_MAXM || Cout != 256) return 0;
   if (X3_FC_DG_GEMM && Gm != nullptr) {
     const int R = T * E;
     const long thr = (long)P * R * (256 / 8);
     fc_gm_x3<256><<<(unsigned)((thr + 255) / 256), 256, 0, st>>>(G, (const uint16_t*)bits, ac, layer, L, P, E, T, br,
-                                                                  gs, (bf16_t*)Gm, gmlo);
+                                                                  gs, (bf16_t*)Gm, gmlo, gamax);
     int rc = (int)hipGetLastError();
     if (rc) return -rc;
     const int nrb = (R + 127) / 128, ncb = (K + 255) / 256;
     fc_dgrad_gemm_x3<256><<<(unsigned)((P * nrb * ncb + 7) / 8 * 8), 512, 0, st>>>((const bf16_t*)Gm, gmlo,
                                                                                   (const bf16_t*)WcT, wlo,
                                                                      ai, ac, layer, L, M, K, KP, P, E, T, br, dX, nrb,
-                                                                     ncb);
+                                                                     ncb, gamax, gamax_out);
     rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   }
@@ -3726,39 +3794,70 @@ int x3_fc_dgrad(const float* G, const void* bits, const void* WcT, long wlo, con
   const int nrowb = (int)(((long)T * E + 63) / 64);
   const int nwg = (nrowb * P * split + 7) / 8 * 8;
   fc_dgrad_x3<256><<<nwg, 512, 0, st>>>(G, (const uint16_t*)bits, (const bf16_t*)WcT, wlo, ai, ac, layer, L, M, K, KP,
-                                        P, E, T, br, gs, dX, per, nrowb, split, (bf16_t*)Gm, gmlo);
+                                        P, E, T, br, gs, dX, per, nrowb, split, (bf16_t*)Gm, gmlo, gamax, gamax_out);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
 
 int x3_fc_wgrad_gm(const void* X, long xlo, int ldx, const void* Gm, long gmlo, float* grad, long w_off, long b_off,
                    int chunk, const int* inv_path, const int* inv_slot, const int* inv_cnt, int layer, int M, int Pmax,
-                   int K, int Cout, int P, int E, int T, long br, int nsplit, hipStream_t st) {
+                   int K, int Cout, int P, int E, int T, long br, int nsplit, const float* gamax, hipStream_t st) {
   if (ldx <= 0 || chunk <= 0 || M <= 0 || Pmax <= 0 || K <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 ||
-      nsplit <= 0 || w_off < 0 || b_off < 0 || layer < 0 || xlo <= 0 || gmlo <= 0) return -22;
+      nsplit <= 0 || w_off < 0 || b_off < 0 || layer < 0 || xlo <= 0 || gmlo <= 0 || !gamax) return -22;
   if (Cout != 256 || ldx % 8 != 0 || K % 8 != 0) return 0;
   const int kt = (K + 127) / 128;
   fc_wgrad_gm_x3<256><<<kt * M * nsplit, 512, 0, st>>>((const bf16_t*)X, xlo, ldx, (const bf16_t*)Gm, gmlo, grad,
                                                        w_off, b_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, Pmax,
-                                                       K, P, E, T, br, nsplit);
+                                                       K, P, E, T, br, nsplit, gamax);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
 
 int x3_fc_wgrad(const void* X, long xlo, int ldx, const float* G, const void* bits, float* grad, long w_off,
                 long b_off, int chunk, const int* inv_path, const int* inv_slot, const int* inv_cnt, int layer, int M,
-                int Pmax, int K, int Cout, int P, int E, int T, long br, float gs, hipStream_t st) {
+                int Pmax, int K, int Cout, int P, int E, int T, long br, float gs, const float* gamax, hipStream_t st) {
   if (ldx <= 0 || chunk <= 0 || M <= 0 || Pmax <= 0 || K <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 ||
-      w_off < 0 || b_off < 0 || layer < 0 || xlo <= 0) return -22;
+      w_off < 0 || b_off < 0 || layer < 0 || xlo <= 0 || !gamax) return -22;
   if (Cout % 16 != 0 || ldx % 8 != 0) return 0;
   const int tiles = ((K + 63) / 64) * ((Cout + 63) / 64) * M;
   int nsplit = (2048 + tiles - 1) / tiles;
   nsplit = nsplit < 1 ? 1 : (nsplit > Pmax ? Pmax : nsplit);
   fc_wgrad_x3<<<dim3((K + 63) / 64, (Cout + 63) / 64, M * nsplit), 256, 0, st>>>(
       (const bf16_t*)X, xlo, ldx, G, (const uint16_t*)bits, grad, w_off, b_off, chunk, inv_path, inv_slot, inv_cnt,
-      layer, M, Pmax, K, Cout, P, E, T, br, gs, nsplit);
+      layer, M, Pmax, K, Cout, P, E, T, br, gs, nsplit, gamax);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
+}
+
+// G16 amax of an fp32 gradient tensor: *amax = max(*amax, max |g|) (grid-stride; the caller zeroes it when a new
+// backward starts: x3_amax_reset)
+__global__ __launch_bounds__(256) void x3_amax_kernel(const float* __restrict__ g, long n, float* __restrict__ amax) {
+  float m = 0.f;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (long)gridDim.x * 256 * 4) {
+    if (i + 3 < n) {
+      const float4 v = *reinterpret_cast<const float4*>(g + i);
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    } else {
+      for (long j = i; j < n; ++j) m = fmaxf(m, fabsf(g[j]));
+    }
+  }
+  g16_flush_amax(m, amax);
+}
+__global__ void x3_amax_reset_kernel(float* __restrict__ amax, int n) {
+  if ((int)threadIdx.x < n) amax[threadIdx.x] = 0.f;
+}
+int x3_amax(const float* g, long n, float* amax, hipStream_t st) {
+  if (!g || !amax || n <= 0) return -22;
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  x3_amax_kernel<<<(unsigned)blocks, 256, 0, st>>>(g, n, amax);
+  return (int)hipGetLastError();
+}
+int x3_amax_reset(float* amax, int n, hipStream_t st) {
+  if (!amax || n <= 0 || n > 64) return -22;
+  x3_amax_reset_kernel<<<1, 64, 0, st>>>(amax, n);
+  return (int)hipGetLastError();
 }
 
 // fp16-pair range status of the last rollout (X3_RANGE_ACT) and weight refresh (X3_RANGE_W) -> *out (float, for the

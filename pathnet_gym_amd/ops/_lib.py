@@ -73,9 +73,10 @@ _SIGS = {
     "launch_lstm_wgrad": [P, P, P, c_long, c_long, c_int, c_int, c_long, c_int, P],
     "launch_lstm_refresh": [P, c_long, c_int, c_int, P, P, P],
     "launch_lstm_carry": [P, P, P, P, P, c_int, c_int, P],
-    "launch_lstm_fwd_x3": [P, c_int, P, P, P, P, P, c_long, P, P, P, P, P, c_int, c_int, c_int, P],
-    "launch_lstm_bwd_gemm_x3": [P, P, P, c_int, P, c_int, c_int, c_int, P],
-    "launch_lstm_wgrad_x3": [P, P, P, c_long, c_long, c_int, c_int, c_long, c_int, P],
+    "launch_lstm_fwd_x3": [P, c_int, P, P, P, P, P, c_long, P, P, P, P, P, P, c_int, c_int, c_int, P],
+    "launch_lstm_bwd_point_x3": [P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P],
+    "launch_lstm_bwd_gemm_x3": [P, P, P, c_int, P, P, c_int, c_int, c_int, P],
+    "launch_lstm_wgrad_x3": [P, P, P, c_long, c_long, c_int, c_int, c_long, c_int, P, c_int, P, P],
     "launch_lstm_refresh_x3": [P, c_long, c_int, c_int, P, P, P, P],
     "launch_lstm_carry_f32": [P, P, P, P, P, c_int, c_int, P],
     "fast_conv_set_slab": [c_int],
@@ -124,19 +125,22 @@ _SIGS = {
     "x3_conv_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 13
                    + [c_long, c_float, c_float, P],
     "x3_conv_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 12
-                     + [c_long, c_float, c_float, P],
+                     + [c_long, c_float, c_float, P, P],
     "x3_conv1_ring_fwd": [P, P, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 7
                          + [c_long, c_float, c_float, P],
-    "x3_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 6 + [c_long, c_float, c_float, P],
-    "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P],
+    "x3_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 6 + [c_long, c_float, c_float, P,
+                                                                                         P],
+    "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P, P, P],
     "x3_fc_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 10
                  + [c_long, c_float, P],
     "x3_fc_fwd_mm": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P, P, P, P, P] + [c_int] * 10
                     + [c_long, c_float, P],
-    "x3_fc_dgrad": [P, P, P, c_long, P, P] + [c_int] * 9 + [c_long, c_float, P, P, c_long, P],
+    "x3_fc_dgrad": [P, P, P, c_long, P, P] + [c_int] * 9 + [c_long, c_float, P, P, c_long, P, P, P],
+    "x3_amax": [P, c_long, P, P],
+    "x3_amax_reset": [P, c_int, P],
     "x3_fc_wgrad_gm": [P, c_long, c_int, P, c_long, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8
-                      + [c_long, c_int, P],
-    "x3_fc_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8 + [c_long, c_float, P],
+                      + [c_long, c_int, P, P],
+    "x3_fc_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8 + [c_long, c_float, P, P],
     "x3_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
     "x3_status_fold": [P, P, P],
     "fast_conv_set_x3_fwd_nt": [c_int],

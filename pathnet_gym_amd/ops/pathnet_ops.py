@@ -189,9 +189,13 @@ class HipPathNet:
             wdt = torch.float16 if self.x3 else self.act_dtype
             self.Wc.append(torch.zeros(npl + (self.M, g.Cout, g.KP), dtype=wdt, device=dev))
             need_t = g.kind == "fc" and l > 0
-            self.WcT.append(torch.zeros(npl + (self.M, g.KP, g.Cout), dtype=self.act_dtype, device=dev)
-                            if need_t else None)
+            # fp32x: fp16 pair of W^T * 2^8 (the fc input gradient's B operand against scaled fp16-pair gradients)
+            self.WcT.append(torch.zeros(npl + (self.M, g.KP, g.Cout), dtype=torch.float16 if self.x3 else self.act_dtype,
+                                        device=dev) if need_t else None)
         self.x3_status = torch.zeros(1, dtype=torch.int32, device=dev)   # fp16 range overflow of the scaled conv1 pair
+        # fp32x backward: amax of every layer's output gradient (G16 scales, csrc/trunk_x3.hip g16_scale); layer L-1's
+        # is measured when a backward starts, the others written by the input-gradient kernels of the layer above
+        self.gamax = torch.zeros(max(1, len(cfg.layers)), dtype=torch.float32, device=dev)
         self._part = None            # fp32 conv wgrad partial slabs (allocated on first use, before capture)
         self._ys = None              # fp32x module-major fc forward: per-slot fp32 output planes
         # fp32x fc forward: module-major (csrc/trunk_x3.hip fc_fwd_mm2_x3: one workgroup per module x 128 rows of
@@ -220,7 +224,10 @@ class HipPathNet:
                 self.lstm = dict(F=F, H=H, k_off=ls["kernel"], b_off=ls["bias"], x3=self.x3,
                                  KpT=torch.zeros(pl + (4 * H, F + H), dtype=torch.float16 if self.x3 else torch.bfloat16,
                                                  device=dev),
-                                 Kb=torch.zeros(pl + (F + H, 4 * H), dtype=torch.bfloat16, device=dev))
+                                 Kb=torch.zeros(pl + (F + H, 4 * H), dtype=torch.float16 if self.x3 else torch.bfloat16,
+                                                device=dev),
+                                 # fp32x G16 scales: [0] amax of the saved [x | h] rows, [1 + t] amax of step t's dz
+                                 amax=torch.zeros(2, dtype=torch.float32, device=dev) if self.x3 else None)
         # frame-ring input for the first layer (runtime/engine.py): channel-major bf16 weights; fp32x reads the ring
         # into its packed LDS band / slab (csrc/trunk_x3.hip RING) and keeps its own weight pairs
         g0 = self.geoms[0]
@@ -347,6 +354,17 @@ class HipPathNet:
         """dtype of the LSTM hidden state / saved [x | h] rows: fp32 in fp32x, bf16 otherwise."""
         return torch.float32 if self.x3 else torch.bfloat16
 
+    def lstm_prepare(self, T: int):
+        """fp32x: size the G16 amax slots for a T-step rollout (before any graph capture)."""
+        ls = self.lstm
+        if ls is not None and ls["x3"] and ls["amax"].numel() < T + 1:
+            ls["amax"] = torch.zeros(T + 1, dtype=torch.float32, device=ls["amax"].device)
+
+    def lstm_amax_reset(self):
+        """fp32x: zero the G16 amaxes at the start of a rollout (the forward's xh rows, then the backward's dz)."""
+        if self.lstm is not None and self.lstm["x3"]:
+            self.lstm["amax"].zero_()
+
     def lstm_fwd(self, x, hprev, cprev, prev_done, hout, cout, gates=None, xh=None):
         """x [B,F], hprev [B,H] (bf16; fp32 in fp32x), cprev [B,H] f32, prev_done [B] u8 or None -> hout/cout
         (/gates/xh)."""
@@ -362,7 +380,7 @@ class HipPathNet:
             _lib.call("launch_lstm_fwd_x3", x.data_ptr(), x.shape[1], hprev.data_ptr(), cprev.data_ptr(),
                       _lib.ptr(prev_done), ls["KpT"].data_ptr(), self.model.store.flat.data_ptr(), ls["b_off"],
                       hout.data_ptr(), cout.data_ptr(), _lib.ptr(gates), _lib.ptr(xh), self.x3_status.data_ptr(),
-                      ls["F"], ls["H"], B, _lib.stream())
+                      ls["amax"].data_ptr(), ls["F"], ls["H"], B, _lib.stream())
             return
         _lib.call("launch_lstm_fwd", x.data_ptr(), x.shape[1], hprev.data_ptr(), cprev.data_ptr(),
                   _lib.ptr(prev_done), ls["KpT"].data_ptr(), self.model.store.flat.data_ptr(), ls["b_off"],
@@ -370,21 +388,38 @@ class HipPathNet:
                   _lib.stream())
 
     def lstm_bwd_step(self, dh_heads, dh_rec, dc_rec, done_t, gates, c_t, c_prev, prev_done, dz, dc_out, dx,
-                      dh_prev):
+                      dh_prev, t: int = 0):
+        """One reverse step; t = the rollout step (fp32x: its dz amax slot, csrc/lstm_x3.hip G16)."""
         ls = self.lstm
         B = dh_heads.shape[0]
         st = _lib.stream()
+        if ls["x3"]:
+            if not 0 <= t < ls["amax"].numel() - 1:
+                raise ValueError(f"lstm_bwd_step: step {t} has no amax slot (lstm_prepare({t + 1}) first)")
+            am = ls["amax"].data_ptr() + 4 * (1 + t)
+            _lib.call("launch_lstm_bwd_point_x3", dh_heads.data_ptr(), _lib.ptr(dh_rec), _lib.ptr(dc_rec),
+                      _lib.ptr(done_t), gates.data_ptr(), c_t.data_ptr(), c_prev.data_ptr(), _lib.ptr(prev_done),
+                      dz.data_ptr(), dc_out.data_ptr(), am, ls["H"], B, st)
+            _lib.call("launch_lstm_bwd_gemm_x3", dz.data_ptr(), ls["Kb"].data_ptr(), dx.data_ptr(), dx.shape[-1],
+                      dh_prev.data_ptr(), am, ls["F"], ls["H"], B, st)
+            return
         _lib.call("launch_lstm_bwd_point", dh_heads.data_ptr(), _lib.ptr(dh_rec), _lib.ptr(dc_rec),
                   _lib.ptr(done_t), gates.data_ptr(), c_t.data_ptr(), c_prev.data_ptr(), _lib.ptr(prev_done),
                   dz.data_ptr(), dc_out.data_ptr(), ls["H"], B, st)
-        _lib.call("launch_lstm_bwd_gemm_x3" if ls["x3"] else "launch_lstm_bwd_gemm", dz.data_ptr(), ls["Kb"].data_ptr(),
-                  dx.data_ptr(), dx.shape[-1], dh_prev.data_ptr(), ls["F"], ls["H"], B, st)
+        _lib.call("launch_lstm_bwd_gemm", dz.data_ptr(), ls["Kb"].data_ptr(), dx.data_ptr(), dx.shape[-1],
+                  dh_prev.data_ptr(), ls["F"], ls["H"], B, st)
 
     def lstm_wgrad(self, xh, dz, grad_flat, rows_per_chunk: int = 2048):
         ls = self.lstm
         R = xh.numel() // (ls["F"] + ls["H"])
-        _lib.call("launch_lstm_wgrad_x3" if ls["x3"] else "launch_lstm_wgrad", xh.data_ptr(), dz.data_ptr(),
-                  grad_flat.data_ptr(), ls["k_off"], ls["b_off"], ls["F"], ls["H"], R, rows_per_chunk, _lib.stream())
+        if ls["x3"]:
+            am = ls["amax"]
+            _lib.call("launch_lstm_wgrad_x3", xh.data_ptr(), dz.data_ptr(), grad_flat.data_ptr(), ls["k_off"],
+                      ls["b_off"], ls["F"], ls["H"], R, rows_per_chunk, am.data_ptr() + 4, am.numel() - 1,
+                      am.data_ptr(), _lib.stream())
+            return
+        _lib.call("launch_lstm_wgrad", xh.data_ptr(), dz.data_ptr(), grad_flat.data_ptr(), ls["k_off"], ls["b_off"],
+                  ls["F"], ls["H"], R, rows_per_chunk, _lib.stream())
 
     def lstm_carry(self, hT, cT, done_last, h0, c0):
         _lib.call("launch_lstm_carry_f32" if self.lstm["x3"] else "launch_lstm_carry", hT.data_ptr(), cT.data_ptr(),
@@ -578,6 +613,10 @@ class HipPathNet:
             self._ys = torch.empty(need, dtype=torch.float32, device=self.model.device)
         return self._ys
 
+    def _gamax(self, l: int):
+        """Device address of layer l's gradient amax (G16), or None below layer 0."""
+        return None if l < 0 else self.gamax.data_ptr() + 4 * l
+
     def _layer_bwd_x3(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st):
         g = self.geoms[l]
         m = self.model
@@ -585,16 +624,21 @@ class HipPathNet:
         _lib.check(G, torch.float32, name="G")
         if dX is not None:
             _lib.check(dX, torch.float32, name="dX")
+        if l == self.L - 1:
+            # a backward starts at the last layer: fresh amaxes, the incoming gradient's measured here
+            _lib.call("x3_amax_reset", self.gamax.data_ptr(), self.L, st)
+            _lib.call("x3_amax", G.data_ptr(), G.numel(), self._gamax(l), st)
+        ga, ga_out = self._gamax(l), self._gamax(l - 1)
         xb, xblo = self._x3_bf16(X)
         if g.kind == "conv":
             ok = _lib.call_fast("x3_conv_wgrad", xb, xblo, int(g.u8in), G.data_ptr(),
                                 bits.data_ptr(), grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
                                 m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T,
-                                bits_rows, g.in_scale, g_scale, st)
+                                bits_rows, g.in_scale, g_scale, ga, st)
             if ok and dX is not None:
                 ok = _lib.call_fast("x3_conv_dgrad", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
                                     m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin,
-                                    g.KH, g.KW, g.S, P, E, T, bits_rows, g_scale, dX.data_ptr(), st)
+                                    g.KH, g.KW, g.S, P, E, T, bits_rows, g_scale, dX.data_ptr(), ga, ga_out, st)
             if not ok:
                 raise RuntimeError(f"fp32x: conv layer {l} backward has no split-bf16 kernel")
             return
@@ -607,7 +651,8 @@ class HipPathNet:
         if dX is not None:
             ok = _lib.call_fast("x3_fc_dgrad", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
                                 self.WcT[l][0].numel(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M,
-                                g.K, g.KP, g.Cout, P, E, T, bits_rows, g_scale, dX.data_ptr(), _lib.ptr(gm), gmlo, st)
+                                g.K, g.KP, g.Cout, P, E, T, bits_rows, g_scale, dX.data_ptr(), _lib.ptr(gm), gmlo, ga,
+                                ga_out, st)
         if ok and use_gm_wgrad:
             tiles = ((g.K + 127) // 128) * self.M
             # workgroups ~ a whole number of rounds of one per CU (fc_wgrad_gm_x3 holds 102 KB of LDS): 110 tiles x 7
@@ -616,12 +661,12 @@ class HipPathNet:
             ok = _lib.call_fast("x3_fc_wgrad_gm", xb, xblo, g.ldx, gm.data_ptr(), gmlo,
                                 grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
                                 self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T,
-                                bits_rows, nsplit, st)
+                                bits_rows, nsplit, ga, st)
         elif ok:
             ok = _lib.call_fast("x3_fc_wgrad", xb, xblo, g.ldx, G.data_ptr(), bits.data_ptr(),
                                 grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
                                 self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T,
-                                bits_rows, g_scale, st)
+                                bits_rows, g_scale, ga, st)
         if not ok:
             raise RuntimeError(f"fp32x: fc layer {l} backward has no split-bf16 kernel")
 
@@ -794,7 +839,7 @@ class HipPathNet:
             ok = _lib.call_fast("x3_conv1_ring_wgrad", frames.data_ptr(), fc.data_ptr(), G.data_ptr(), bits.data_ptr(),
                                 grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
                                 m.act_cnt.data_ptr(), self.L, self.M, P, E, T, frames.shape[1], bits_rows, g.in_scale,
-                                g_scale, _lib.stream())
+                                g_scale, self._gamax(0), _lib.stream())
             if not ok:
                 raise RuntimeError(f"fp32x: frame-ring weight gradient has no kernel for P={P}, E={E}, M={self.M}")
             return

@@ -136,6 +136,7 @@ class HipEngine:
         if self.lstm_hip:
             F, H = hp.lstm["F"], hp.lstm["H"]
             ldt = hp.lstm_dtype                  # bf16 (bf16 engine) or fp32 (fp32x: csrc/lstm_x3.hip)
+            hp.lstm_prepare(T)
             self.hst = torch.zeros(T + 2, B, H, dtype=ldt, device=dev)   # slot t = state entering step t
             self.cst = torch.zeros(T + 2, B, H, device=dev)
             self.gates = torch.zeros(T, B, 4 * H, device=dev)
@@ -391,6 +392,8 @@ class HipEngine:
         T, P, E, B = self.T, self.P, self.E, self.B
         a2c = self.cfg.a2c
         hp = self.hip
+        if self.lstm_hip:
+            hp.lstm_amax_reset()
         if self.groups > 1:
             self._rollout_split()
         else:
@@ -538,7 +541,7 @@ class HipEngine:
             hp.lstm_bwd_step(self.dh_heads[t], None if first else self.dh_rec[nxt], None if first else self.dc_rec[nxt],
                              self.dones[t], self.gates[t], self.cst[t + 1], self.cst[t],
                              self.dones[t - 1] if t > 0 else None, self.dz[t], self.dc_rec[cur], dfeat[t],
-                             self.dh_rec[cur])
+                             self.dh_rec[cur], t=t)
         hp.lstm_wgrad(self.xh, self.dz, self.grad_flat)
 
     def lstm_state_tensors(self):
