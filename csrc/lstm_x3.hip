@@ -220,24 +220,30 @@ __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
   const long plane = (long)(F + H) * G4;
   const int arow = row0 + c16;
   const bool av = arow < B;
-  f4v acc[4];
+  f4v acc[4], accn[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 4; ++j) acc[j] = accn[j] = (f4v){0.f, 0.f, 0.f, 0.f};
   const float gs = g16_scale_of(*amax_dz);
   for (int p0 = 0; p0 < G4; p0 += 32) {
     const int p = p0 + 8 * grp;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (av) ld8(dz + (long)arow * G4 + p, v);
+    // odd k-steps on the negated pieces into a second chain, subtracted at the end: the f16 MFMA's -inf rounding
+    // bias enters with alternating signs instead of accumulating (csrc/trunk_x3.hip fc_dgrad_gemm_x3 FOLD 2)
+    const float sg = ((p0 >> 5) & 1) ? -1.f : 1.f;
     s8v ah, al;
-    split8hs(v, gs, ah, al);                      // fp16 pair of dz * 2^e against the fp16 pair of K * 2^8
+    split8hs(v, sg * gs, ah, al);                 // fp16 pair of dz * 2^e against the fp16 pair of K * 2^8
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long o = (long)(n0 + j * 16 + c16) * G4 + p;
       const s8v bh = *reinterpret_cast<const s8v*>(Kb2 + o);
       const s8v bl = *reinterpret_cast<const s8v*>(Kb2 + plane + o);
-      acc[j] = mma3h(ah, al, bh, bl, acc[j]);
+      if (sg < 0.f) accn[j] = mma3h(ah, al, bh, bl, accn[j]);
+      else acc[j] = mma3h(ah, al, bh, bl, acc[j]);
     }
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] -= accn[j];
   const float inv = 1.0f / (gs * (float)(1 << LX3_SHIFT));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {

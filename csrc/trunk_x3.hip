@@ -1868,7 +1868,7 @@ struct DGM {
   static constexpr int NT = (NN + 15) / 16;
 };
 
-template <class G>
+template <class G, bool W3 = false, bool ALT = false>
 __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
                                                        const float* __restrict__ flat, long w_off, int chunk,
                                                        const int* __restrict__ act_idx,
@@ -1882,7 +1882,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
   constexpr int GPL = (G::HOWO + 1) * X3_DG_PSTR;
   constexpr int BPL = D::NTAP * D::NT * 16 * 32;
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][GPL];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BPL];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[W3 ? 3 : 2][BPL];
   __shared__ int mods[X3_MAXM];
   __shared__ __attribute__((aligned(16))) uint16_t atap[D::NRT * 16 * NTAPP];
   __shared__ __attribute__((aligned(8))) uint16_t etab[D::NRT * 16];
@@ -1914,10 +1914,18 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
         for (int c = 0; c < 8; ++c) v[c] = wp[c];
       }
       s8v hi, lo;
-      split8hs(v, (float)(1 << X3_W0_SHIFT), hi, lo);       // fp16 pair of W * 2^8 (G16)
+      // fp16 pair of W * 2^8 (G16); ALT: odd taps' weights staged negated (the second accumulator chain)
+      split8hs(v, (ALT && (tap & 1)) ? -(float)(1 << X3_W0_SHIFT) : (float)(1 << X3_W0_SHIFT), hi, lo);
       const int o = (tap * D::NT * 16 + n) * 32 + (a4 ^ dg_swz(n)) * 8;
       *reinterpret_cast<s8v*>(Bs[0] + o) = hi;
       *reinterpret_cast<s8v*>(Bs[1] + o) = lo;
+      if constexpr (W3) {                                   // third piece: W * 2^8 - hi - lo
+        const h8v hh = __builtin_bit_cast(h8v, hi), ll = __builtin_bit_cast(h8v, lo);
+        _Float16 r[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) r[c] = (_Float16)(v[c] * (float)(1 << X3_W0_SHIFT) - (float)hh[c] - (float)ll[c]);
+        *reinterpret_cast<s8v*>(Bs[2] + o) = __builtin_bit_cast(s8v, r);
+      }
     }
   };
   constexpr int GIT = (G::HOWO + 255) / 256;
@@ -1997,21 +2005,37 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
       if (g == ngroup - 1 && s + 1 < s_end) load_sample(s + 1);
       for (int rt = w; rt < D::NRT; rt += 4) {
         const uint16_t* tp = atap + (rt * 16 + c16) * NTAPP;
-        f4v acc[D::NT];
+        f4v acc[D::NT], accn[ALT ? D::NT : 1];
 #pragma unroll
         for (int nt = 0; nt < D::NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (ALT) {
+#pragma unroll
+          for (int nt = 0; nt < D::NT; ++nt) accn[nt] = {0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
         for (int tap = 0; tap < D::NTAP; ++tap) {
           const int ao = (int)tp[tap] ^ (grp << 3);
           const s8v ah = *reinterpret_cast<const s8v*>(Gs[0] + ao);
           const s8v al = *reinterpret_cast<const s8v*>(Gs[1] + ao);
+          // ALT: odd taps (negated weights in LDS) into a second chain, subtracted at the end (the f16 MFMA's -inf
+          // rounding bias enters with alternating signs; fc_dgrad_gemm_x3 FOLD 2)
+          const bool neg = ALT && (tap & 1);
           const int bo = (tap * D::NT * 16 + c16) * 32 + (grp ^ dg_swz(c16)) * 8;
 #pragma unroll
           for (int nt = 0; nt < D::NT; ++nt) {
             const s8v bh = *reinterpret_cast<const s8v*>(Bs[0] + bo + nt * 16 * 32);
             const s8v bl = *reinterpret_cast<const s8v*>(Bs[1] + bo + nt * 16 * 32);
-            acc[nt] = mma3h(ah, al, bh, bl, acc[nt]);
+            if (neg) {
+              accn[nt] = mma3h(ah, al, bh, bl, accn[nt]);
+            } else {
+              if constexpr (W3) acc[nt] = mfma16_f16(ah, *reinterpret_cast<const s8v*>(Bs[2] + bo + nt * 16 * 32), acc[nt]);
+              acc[nt] = mma3h(ah, al, bh, bl, acc[nt]);
+            }
           }
+        }
+        if constexpr (ALT) {
+#pragma unroll
+          for (int nt = 0; nt < D::NT; ++nt) acc[nt] -= accn[nt];
         }
         const uint2 e4 = *reinterpret_cast<const uint2*>(etab + rt * 16 + 4 * grp);
         const uint32_t ev[4] = {e4.x & 0xFFFFu, e4.x >> 16, e4.y & 0xFFFFu, e4.y >> 16};
@@ -2958,7 +2982,7 @@ __global__ __launch_bounds__(256) void fc_gm_x3(const float* __restrict__ G, con
   }
 }
 
-template <int COUT>
+template <int COUT, bool W3 = false, int FOLD = 0>
 __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict__ Gm, long gmlo,
                                                         const bf16_t* __restrict__ WcT, long wlo,
                                                         const int* __restrict__ act_idx,
@@ -2967,8 +2991,9 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
                                                         float* __restrict__ dX, int nrb, int ncb,
                                                         const float* __restrict__ gamax, float* __restrict__ gamax_out) {
   constexpr int BM = 128, BN = 256, CS = COUT / 32;                 // reduction steps per slot
+  constexpr int NBP = W3 ? 3 : 2;                                    // weight pieces staged (W3: + the third)
   __shared__ __attribute__((aligned(16))) bf16_t As[2][2][BM * 32];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][2][BN * 32];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][NBP][BN * 32];
   // XCD-major: XCD x (= blockIdx % 8) takes the x-th contiguous eighth of the (path, row block, column block) list,
   // so one path's weight set is fetched into one XCD's L2 rather than into all eight
   const int ntot = P * nrb * ncb, per = (ntot + 7) >> 3, kx = (int)(blockIdx.x >> 3);
@@ -2983,11 +3008,17 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
   const int wm = w >> 2, wn = w & 3;                                 // wave tile: rows 64*wm.., columns 64*wn..
   const int row0 = rbk * BM, col0 = cb * BN;
   const int nsteps = cnt * CS;
-  f4v acc[4][4];
+  f4v acc[4][4], accn[FOLD == 2 ? 4 : 1][FOLD == 2 ? 4 : 1];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (f4v){0.f, 0.f, 0.f, 0.f};
+  if constexpr (FOLD == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) accn[i][jj] = (f4v){0.f, 0.f, 0.f, 0.f};
+  }
   if (nsteps > 0) {
     // staging roles: A: thread -> (row tid >> 2, chunk tid & 3), both planes; B: two columns (tid >> 2, + 128)
     const int sr = tid >> 2, sk = tid & 3;
@@ -2996,7 +3027,8 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
     const int kb0 = min(col0 + sr, K - 1), kb1 = min(col0 + 128 + sr, K - 1);
     const int* aidx = act_idx + (p * L + layer) * M;
     const int sdA = mm2_sw(sr, sk) * 8, sdB0 = sdA, sdB1 = mm2_sw(sr + 128, sk) * 8;
-    uint4 x0, x1, y0, y1, z0, z1, u0, u1, v0, v1, t0_, t1_;     // two sets: A hi/lo, B col hi/lo, B col+128 hi/lo
+    // two sets: A hi/lo, B col hi/lo(/third), B col+128 hi/lo(/third)
+    uint4 x0, x1, y0, y1, z0, z1, u0, u1, v0, v1, t0_, t1_, r0, r1, q0, q1;
 #define DG_LOAD(S, st)                                                                                      \
     do {                                                                                                    \
       const int a_ = (st) / CS, c_ = ((st) - a_ * CS) * 32 + sk * 8;                                        \
@@ -3008,23 +3040,36 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
       u##S = *reinterpret_cast<const uint4*>(wb_ + wlo + (long)kb0 * COUT);                                 \
       v##S = *reinterpret_cast<const uint4*>(wb_ + (long)kb1 * COUT);                                       \
       t##S##_ = *reinterpret_cast<const uint4*>(wb_ + wlo + (long)kb1 * COUT);                              \
+      if constexpr (W3) {                                                                                   \
+        r##S = *reinterpret_cast<const uint4*>(wb_ + 2 * wlo + (long)kb0 * COUT);                           \
+        q##S = *reinterpret_cast<const uint4*>(wb_ + 2 * wlo + (long)kb1 * COUT);                           \
+      }                                                                                                     \
     } while (0)
 #define DG_STORE(S, buf)                                                                                    \
     do {                                                                                                    \
+      if (FOLD == 2 && (buf) == 1) {            /* odd k-steps: the gradient pieces negated (sign bits) */  \
+        x##S.x ^= 0x80008000u; x##S.y ^= 0x80008000u; x##S.z ^= 0x80008000u; x##S.w ^= 0x80008000u;         \
+        y##S.x ^= 0x80008000u; y##S.y ^= 0x80008000u; y##S.z ^= 0x80008000u; y##S.w ^= 0x80008000u;         \
+      }                                                                                                     \
       *reinterpret_cast<uint4*>(&As[buf][0][sdA]) = x##S;                                                   \
       *reinterpret_cast<uint4*>(&As[buf][1][sdA]) = y##S;                                                   \
       *reinterpret_cast<uint4*>(&Bs[buf][0][sdB0]) = z##S;                                                  \
       *reinterpret_cast<uint4*>(&Bs[buf][1][sdB0]) = u##S;                                                  \
       *reinterpret_cast<uint4*>(&Bs[buf][0][sdB1]) = v##S;                                                  \
       *reinterpret_cast<uint4*>(&Bs[buf][1][sdB1]) = t##S##_;                                               \
+      if constexpr (W3) {                                                                                   \
+        *reinterpret_cast<uint4*>(&Bs[buf][NBP - 1][sdB0]) = r##S;                                          \
+        *reinterpret_cast<uint4*>(&Bs[buf][NBP - 1][sdB1]) = q##S;                                          \
+      }                                                                                                     \
     } while (0)
     auto compute = [&](int buf) {
-      s8v bh[4], bl[4];
+      s8v bh[4], bl[4], br[W3 ? 4 : 1];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int o = mm2_sw(wn * 64 + jj * 16 + c16, grp) * 8;
         bh[jj] = *reinterpret_cast<const s8v*>(&Bs[buf][0][o]);
         bl[jj] = *reinterpret_cast<const s8v*>(&Bs[buf][1][o]);
+        if constexpr (W3) br[jj] = *reinterpret_cast<const s8v*>(&Bs[buf][NBP - 1][o]);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -3032,7 +3077,25 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
         const s8v ah = *reinterpret_cast<const s8v*>(&As[buf][0][o]);
         const s8v al = *reinterpret_cast<const s8v*>(&As[buf][1][o]);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = mma3h(ah, al, bh[jj], bl[jj], acc[i][jj]);
+        for (int jj = 0; jj < 4; ++jj) {
+          // W3: the weights' third piece first (smallest term).  FOLD 1: each k-step's products into a zeroed
+          // accumulator, added to the running sum with one IEEE fp32 add.  FOLD 2: odd k-steps run on negated
+          // gradient pieces into a second accumulator chain, subtracted at the end: the f16 MFMA's sum is biased
+          // toward -inf (measured: mean error / mean |error| = -0.13 on the fc input gradient,
+          // scripts/x3_lstm_diag.py), which the weight gradients below sum coherently; on the negated chain the
+          // same bias enters with the opposite sign
+          if constexpr (FOLD == 2) {
+            if (buf == 1) {
+              accn[i][jj] = mma3h(ah, al, bh[jj], bl[jj], accn[i][jj]);
+              continue;
+            }
+          }
+          f4v c = FOLD == 1 ? (f4v){0.f, 0.f, 0.f, 0.f} : acc[i][jj];
+          if constexpr (W3) c = mfma16_f16(ah, br[jj], c);
+          c = mma3h(ah, al, bh[jj], bl[jj], c);
+          if constexpr (FOLD == 1) acc[i][jj] += c;
+          else acc[i][jj] = c;
+        }
       }
     };
     // set 0 holds the even steps' loads, set 1 the odd ones; step s stores step s + 1's set, then reloads it with
@@ -3061,6 +3124,12 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
   // scaled back by 2^-(e + 8); the amax of dX for the layer below (G16)
   const float inv = 1.0f / (g16_scale(gamax) * (float)(1 << X3_W0_SHIFT));
   float am = 0.f;
+  if constexpr (FOLD == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[i][jj] -= accn[i][jj];
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -3324,8 +3393,9 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
 }
 
 // hi/lo operand copies of one layer's weights: Wc [2][M][Cout][KP] (forward B operand, k contiguous, zero padded):
-// the fp16 pair of W * 2^X3_W0_SHIFT (f16 != 0) or the bf16 pair of W; optionally WcT [2][M][KP][Cout] (the fc input
-// gradient's B operand): the fp16 pair of W * 2^X3_W0_SHIFT, as the scaled fp16-pair gradients it meets (G16).  *status |= X3_RANGE_W when a scaled
+// the fp16 pair of W * 2^X3_W0_SHIFT (f16 != 0) or the bf16 pair of W; optionally WcT [3][M][KP][Cout] (the fc input
+// gradient's B operand): the fp16 hi, lo and third piece of W * 2^X3_W0_SHIFT, as the scaled fp16-pair gradients it
+// meets (G16).  *status |= X3_RANGE_W when a scaled
 // weight leaves the fp16 range; x3_status_fold (end of the next rollout) moves it and the forward epilogues' flag
 // into the update's all-reduced counters, where every rank sees it (algo/trainer.py raises X3RangeError)
 __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict__ flat, long w_off, int chunk, int K,
@@ -3350,11 +3420,14 @@ __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict
     const long wi = ((long)j * Cout + c) * KP + k;
     Wc[wi] = hi;
     Wc[n + wi] = lo;
-    if (WcT) {                       // the fc input gradient's B operand: fp16 pair of W * 2^8 (meets G16 gradients)
+    if (WcT) {                       // the fc input gradient's B operand: fp16 pieces of W * 2^8 (meets G16 gradients)
       const float x = v * (float)(1 << X3_W0_SHIFT);
       const uint16_t th = f2h(x);
+      const float r = x - h2f(th);
+      const uint16_t tl = f2h(r);
       WcT[i] = th;
-      WcT[n + i] = f2h(x - h2f(th));
+      WcT[n + i] = tl;
+      WcT[2 * n + i] = f2h(r - h2f(tl));           // third piece: W exact to 33 bits (X3_DG_W3)
     }
   }
 }
@@ -3417,6 +3490,13 @@ static int X3_WG3_TILE = 1;
 static int X3_FWD_TILE = 3;
 static int X3_C1_PIPE = 0;     // band forward: 1 = next k-step's LDS fragments read during this k-step's MFMAs
 static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
+// input gradients (conv_dgrad_x3, fc_dgrad_gemm_x3): 1 = the weights as THREE fp16 pieces (a fourth MFMA per k-step),
+// exact for fp32 weights: the pair's 2^-23 weight rounding is the same for every row, so it enters a layer's input
+// gradient coherently and the weight gradients below sum it without cancellation (scripts/x3_lstm_diag.py)
+static int X3_DG_W3 = 0;
+// fc input gradient: 1 = every k-step's MFMA products summed from zero and added to the running fp32 sum by a VALU add;
+// 2 = the same with odd k-steps on negated operands, subtracted (cancels the f16 MFMA's -inf rounding bias)
+static int X3_DG_FOLD = 2;
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
 extern "C" {
@@ -3429,6 +3509,8 @@ void fast_conv_set_x3_fwd_sw(int sw) { X3_FWD_SW = sw; }
 void fast_conv_set_x3_wg3_tile(int t) { X3_WG3_TILE = t; }
 void fast_conv_set_x3_fc_mmv(int v) { X3_FC_MMV = v; }
 void fast_conv_set_x3_fc_dg_gemm(int v) { X3_FC_DG_GEMM = v; }
+void fast_conv_set_x3_dg_w3(int v) { X3_DG_W3 = v; }
+void fast_conv_set_x3_dg_fold(int v) { X3_DG_FOLD = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
 void fast_conv_set_x3_c1_band(int v) { X3_C1_BAND = v; }
 void fast_conv_set_x3_c1_pipe(int v) { X3_C1_PIPE = v; }
@@ -3644,8 +3726,15 @@ int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_o
   const dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
 #define DGX(Gx)                                                                                                    \
   if (x3_is<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                                    \
-    conv_dgrad_x3<Gx><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, \
-                                            T, br, gs, dX, spw, gamax, gamax_out);                                 \
+    if (X3_DG_FOLD == 2)                                                                                           \
+      conv_dgrad_x3<Gx, false, true><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac,     \
+                                                           layer, L, M, P, E, T, br, gs, dX, spw, gamax, gamax_out); \
+    else if (X3_DG_W3)                                                                                             \
+      conv_dgrad_x3<Gx, true><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, \
+                                                    M, P, E, T, br, gs, dX, spw, gamax, gamax_out);                 \
+    else                                                                                                           \
+      conv_dgrad_x3<Gx><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P,  \
+                                              E, T, br, gs, dX, spw, gamax, gamax_out);                            \
     const int rc = (int)hipGetLastError();                                                                         \
     return rc ? -rc : 1;                                                                                           \
   }
@@ -3781,10 +3870,17 @@ int x3_fc_dgrad(const float* G, const void* bits, const void* WcT, long wlo, con
     int rc = (int)hipGetLastError();
     if (rc) return -rc;
     const int nrb = (R + 127) / 128, ncb = (K + 255) / 256;
-    fc_dgrad_gemm_x3<256><<<(unsigned)((P * nrb * ncb + 7) / 8 * 8), 512, 0, st>>>((const bf16_t*)Gm, gmlo,
-                                                                                  (const bf16_t*)WcT, wlo,
-                                                                     ai, ac, layer, L, M, K, KP, P, E, T, br, dX, nrb,
-                                                                     ncb, gamax, gamax_out);
+    const unsigned nwg = (unsigned)((P * nrb * ncb + 7) / 8 * 8);
+#define DGG(W3_, FOLD_)                                                                                           \
+    fc_dgrad_gemm_x3<256, W3_, FOLD_><<<nwg, 512, 0, st>>>((const bf16_t*)Gm, gmlo, (const bf16_t*)WcT, wlo, ai, ac, \
+                                                           layer, L, M, K, KP, P, E, T, br, dX, nrb, ncb, gamax,     \
+                                                           gamax_out)
+    if (X3_DG_FOLD == 2) DGG(false, 2);
+    else if (X3_DG_W3 && X3_DG_FOLD) DGG(true, 1);
+    else if (X3_DG_W3) DGG(true, 0);
+    else if (X3_DG_FOLD) DGG(false, 1);
+    else DGG(false, 0);
+#undef DGG
     rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   }

@@ -54,12 +54,13 @@ def a2c_loss(logits: torch.Tensor, values: torch.Tensor, actions: torch.Tensor,
     value_loss = value_coef * l2_loss(R - V) = value_coef*0.5*sum (R-V)^2   (:56)
     ``weight`` [N] optionally scales each sample (mean-over-envs reduction).
     """
-    pi = torch.softmax(logits.float(), -1)
+    wide = logits.dtype == torch.float64            # float64 oracles (tests/test_x3_engine.py) stay float64
+    pi = torch.softmax(logits if wide else logits.float(), -1)
     log_pi = torch.log(pi.clamp(1e-20, 1.0))
     entropy = -(pi * log_pi).sum(-1)
     lp_a = log_pi.gather(1, actions.long()[:, None]).squeeze(1)
     pol = -(lp_a * adv.detach() + entropy_beta * entropy)
-    val = value_coef * 0.5 * (returns.detach() - values.float()) ** 2
+    val = value_coef * 0.5 * (returns.detach() - (values if wide else values.float())) ** 2
     if weight is not None:
         pol = pol * weight
         val = val * weight

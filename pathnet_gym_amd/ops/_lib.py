@@ -150,6 +150,8 @@ _SIGS = {
     "fast_conv_set_x3_wg3_tile": [c_int],
     "fast_conv_set_x3_fc_mmv": [c_int],
     "fast_conv_set_x3_fc_dg_gemm": [c_int],
+    "fast_conv_set_x3_dg_w3": [c_int],
+    "fast_conv_set_x3_dg_fold": [c_int],
     "fast_conv_set_x3_fwd_tile": [c_int],
     "fast_conv_set_x3_c1_band": [c_int],
     "fast_conv_set_x3_c1_pipe": [c_int],

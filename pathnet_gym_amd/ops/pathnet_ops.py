@@ -189,9 +189,11 @@ class HipPathNet:
             wdt = torch.float16 if self.x3 else self.act_dtype
             self.Wc.append(torch.zeros(npl + (self.M, g.Cout, g.KP), dtype=wdt, device=dev))
             need_t = g.kind == "fc" and l > 0
-            # fp32x: fp16 pair of W^T * 2^8 (the fc input gradient's B operand against scaled fp16-pair gradients)
-            self.WcT.append(torch.zeros(npl + (self.M, g.KP, g.Cout), dtype=torch.float16 if self.x3 else self.act_dtype,
-                                        device=dev) if need_t else None)
+            # fp32x: fp16 pieces of W^T * 2^8 (the fc input gradient's B operand against scaled fp16-pair gradients):
+            # hi, lo and the third piece (the residual W - hi - lo, csrc/trunk_x3.hip X3_DG_W3)
+            self.WcT.append(torch.zeros(((3,) if self.x3 else ()) + (self.M, g.KP, g.Cout),
+                                        dtype=torch.float16 if self.x3 else self.act_dtype, device=dev)
+                            if need_t else None)
         self.x3_status = torch.zeros(1, dtype=torch.int32, device=dev)   # fp16 range overflow of the scaled conv1 pair
         # fp32x backward: amax of every layer's output gradient (G16 scales, csrc/trunk_x3.hip g16_scale); layer L-1's
         # is measured when a backward starts, the others written by the input-gradient kernels of the layer above

@@ -32,7 +32,7 @@ step_tests() {
   local k=()
   [ -n "$1" ] && k=(-k "${1//,/ or }")
   local rc=0
-  $T 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${k[@]}" \
+  $T 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread "${k[@]}" \
       > "$OUT/pytest_gpu.log" 2>&1 || rc=$?
   # a failed assertion (rc 1) is a result, not a fault: report it and go on with the next steps; a time limit, an
   # abort or a crash (rc 124 / 137 / 134 / 139 / >128) ends the call

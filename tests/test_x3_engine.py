@@ -22,8 +22,8 @@ X3_LAYER_TOL = 2e-5
 
 
 def rel(a, b):
-    a = a.float().flatten()
-    b = b.float().flatten()
+    a = a.double().flatten()
+    b = b.double().flatten()
     return float((a - b).norm() / (b.norm() + 1e-12))
 
 
@@ -74,6 +74,10 @@ def test_x3_weight_pairs_reconstruct_fp32(hip_lib):
             pt = hp.WcT[l].float()
             assert hp.WcT[l].dtype == torch.float16
             assert rel((pt[0] + pt[1])[:, :g.K] / 256.0, W) < 1e-7
+            # the third piece (X3_DG_W3 input gradients): hi + lo + third == W to fp32 accuracy (exact but for
+            # weights below ~2^-13, whose third piece is an fp16 subnormal)
+            p3 = hp.WcT[l].double()
+            assert rel((p3[0] + p3[1] + p3[2])[:, :g.K] / 256.0, W.double()) < 3e-9
     assert int(hp.x3_status.item()) == 0
 
 
@@ -99,26 +103,48 @@ def test_x3_trunk_forward_matches_plain_fp32_oracle(hip_lib):
     assert max(errs) < X3_LAYER_TOL, errs
 
 
-def _oracle_grad(tr, eng):
-    """Autograd of the A2C loss over the engine's stored rollout, plain fp32."""
+def _oracle_grad(tr, eng, dtype=torch.float32):
+    """Autograd of the A2C loss over the engine's stored rollout: plain fp32, or float64 (the truth the fp32x engine
+    and the plain fp32 oracle are both measured against)."""
     cfg = tr.cfg
     T, B = eng.T, eng.B
     a2c = cfg.a2c
-    flat = tr.model.store.flat.detach().clone().requires_grad_(True)
+    flat = tr.model.store.flat.detach().clone().to(dtype).requires_grad_(True)
     st = ParamStore(cfg.net, DEV, flat=flat)
-    x = eng.obs_stacks().reshape((T + 1) * B, 160, 120, 4).float() / 255.0
-    mask = tr.model.mask.repeat_interleave(eng.E, 0).repeat(T + 1, 1, 1)
+    x = eng.obs_stacks().reshape((T + 1) * B, 160, 120, 4).to(dtype) / 255.0
+    mask = tr.model.mask.repeat_interleave(eng.E, 0).repeat(T + 1, 1, 1).to(dtype)
     feat = trunk_forward_ref(st, x, mask)
     logits, values = heads_ref(st, feat)
     assert rel(logits[:T * B], eng.logits[:T].reshape(-1, eng.A)) < 1e-5
     assert rel(values, eng.values[:T + 1].reshape(-1)) < 1e-5
     R, adv = nstep_returns(eng.rewards, eng.values[:T], eng.dones.bool(), eng.values[T], a2c.gamma,
                            a2c.gae_lambda, a2c.reward_clip)
-    loss, _, _, _ = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(), R.reshape(-1),
-                             adv.reshape(-1), a2c.entropy_beta, a2c.value_coef,
-                             torch.full((T * B,), eng.weight, device=DEV))
+    loss, _, _, _ = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(),
+                             R.reshape(-1).to(dtype), adv.reshape(-1).to(dtype), a2c.entropy_beta, a2c.value_coef,
+                             torch.full((T * B,), eng.weight, device=DEV, dtype=dtype))
     loss.backward()
     return flat.grad
+
+
+def _oracles(fn, tr, eng):
+    """(float64 truth, plain fp32 oracle) of one stored rollout."""
+    return fn(tr, eng, torch.float64), fn(tr, eng, torch.float32)
+
+
+def check_layers(label, tr, g_hip, g64, g32, tol=lambda k: X3_LAYER_TOL):
+    """Per-layer budget against the float64 truth: < 2e-5, or -- on a layer whose gradient is ill-conditioned in the
+    forward values (the policy head: the A2C policy gradient cancels across samples, so the 1e-7 differences between
+    any fp32 forward and the float64 forward come back amplified) -- no worse than 1.25x the plain fp32 oracle's own
+    error against that truth.  Every number is printed."""
+    e64 = layer_errors(tr, g_hip, g64)
+    o32 = layer_errors(tr, g32, g64)
+    e32 = layer_errors(tr, g_hip, g32)
+    print(f"{label} per layer: vs float64", {k: f"{v:.2e}" for k, v in e64.items()},
+          "| plain fp32 oracle vs float64", {k: f"{v:.2e}" for k, v in o32.items()},
+          "| fp32x vs plain fp32", {k: f"{v:.2e}" for k, v in e32.items()})
+    for k, v in e64.items():
+        assert v < max(tol(k), 1.25 * o32[k]), (k, v, o32[k])
+    return e64
 
 
 def layer_errors(tr, g_hip, g_ref):
@@ -144,20 +170,17 @@ def x3_rollout(hip_lib):
     tr.model.set_paths(masks_with_edges(3, cfg.net.L, cfg.net.M, cfg.net.N, seed=2))
     eng._rollout_backward_body()
     torch.cuda.synchronize()
-    return tr, eng, _oracle_grad(tr, eng), eng.grad_flat.clone()
+    return (tr, eng, *_oracles(_oracle_grad, tr, eng), eng.grad_flat.clone())
 
 
 def test_x3_engine_gradient_vs_plain_fp32_oracle(x3_rollout):
-    tr, eng, g_ref, g_hip = x3_rollout
-    err = layer_errors(tr, g_hip, g_ref)
-    print("fp32x engine vs fp32 oracle, per layer:", {k: f"{v:.2e}" for k, v in err.items()})
-    for k, v in err.items():
-        assert v < X3_LAYER_TOL, (k, v)
+    tr, eng, g_ref, g32, g_hip = x3_rollout
+    check_layers("fp32x engine", tr, g_hip, g_ref, g32)
 
 
 def test_x3_gradient_check_detects_a_two_percent_module_error(x3_rollout):
     """Negative control: one active module's weight gradient scaled by 1.02 must fail the per-layer budget."""
-    tr, eng, g_ref, g_hip = x3_rollout
+    tr, eng, g_ref, _, g_hip = x3_rollout
     hp = tr.model.hip
     for l, g in enumerate(hp.geoms):
         act = np.nonzero(tr.model.mask[0, l].cpu().numpy() > 0.5)[0]
@@ -188,21 +211,18 @@ def x3_ring_rollout(hip_lib):
     eng._rollout_backward_body()
     torch.cuda.synchronize()
     assert eng.dones.any()
-    return tr, eng, _oracle_grad(tr, eng), eng.grad_flat.clone()
+    return (tr, eng, *_oracles(_oracle_grad, tr, eng), eng.grad_flat.clone())
 
 
 def test_x3_frame_ring_gradient_vs_plain_fp32_oracle(x3_ring_rollout):
-    tr, eng, g_ref, g_hip = x3_ring_rollout
-    err = layer_errors(tr, g_hip, g_ref)
-    print("fp32x frame-ring engine vs fp32 oracle, per layer:", {k: f"{v:.2e}" for k, v in err.items()})
-    for k, v in err.items():
-        assert v < X3_LAYER_TOL, (k, v)
+    tr, eng, g_ref, g32, g_hip = x3_ring_rollout
+    check_layers("fp32x frame-ring engine", tr, g_hip, g_ref, g32)
 
 
 def test_x3_frame_ring_forward_bit_equal_to_packed(x3_ring_rollout):
     """The ring forward stages the same packed band in LDS as the packed-stack kernel: its outputs and ReLU bits
     must equal the packed kernel's on the reconstructed stacks bit for bit (resets included)."""
-    tr, eng, _, _ = x3_ring_rollout
+    tr, eng, _, _, _ = x3_ring_rollout
     hp = tr.model.hip
     T, B = eng.T, eng.B
     g = hp.geoms[0]
@@ -338,7 +358,7 @@ def test_x3_conv3_wgrad_tile_matches_im2col_rows(x3_rollout):
     """conv_wgrad_tile_x3 (one sample per stage: the input tile converted once, im2col^T read straight from it with
     transposed LDS reads) == conv_wgrad_x3 (32-row im2col stages) up to fp32 summation order, weights and biases."""
     from pathnet_gym_amd.ops import _lib
-    tr, eng, g_ref, g_hip = x3_rollout
+    tr, eng, _, _, g_hip = x3_rollout
     hp = tr.model.hip
     lib = _lib.lib()
     l = 2
@@ -360,13 +380,47 @@ def test_x3_conv3_wgrad_tile_matches_im2col_rows(x3_rollout):
     assert rel(outs[1], g_hip[seg]) < 1e-6
 
 
+@pytest.mark.parametrize("l", [1, 2, 3, 4])
+def test_x3_dgrad_accumulation_variants_match_plain_chain(x3_rollout, l):
+    """Input gradients (conv_dgrad_x3 / fc_dgrad_gemm_x3) in the shipped sign-alternating accumulation (FOLD 2: odd
+    k-steps on negated operands, summed from zero and subtracted) and with the weights as three fp16 pieces (W3) ==
+    the plain MFMA chain up to fp32 rounding; the weight gradient is untouched."""
+    from pathnet_gym_amd.ops import _lib
+    tr, eng, _, _, g_hip = x3_rollout
+    hp = tr.model.hip
+    lib = _lib.lib()
+    g = hp.geoms[l]
+    seg = slice(g.w_off, g.w_off + hp.M * g.chunk)
+    dxs, gws = [], []
+    for fold, w3 in ((0, 0), (2, 0), (0, 1)):
+        lib.fast_conv_set_x3_dg_fold(fold)
+        lib.fast_conv_set_x3_dg_w3(w3)
+        eng.grad_flat.zero_()
+        dX = eng.grads[l - 1]
+        dX.fill_(float("nan"))
+        hp.layer_bwd(l, eng.acts[l - 1], eng.grads[l], eng.bits[l], eng.grad_flat, dX, eng.P, eng.E, eng.T,
+                     eng.bits_rows[l])
+        torch.cuda.synchronize()
+        dxs.append(dX[:eng.T * eng.B].clone())
+        gws.append(eng.grad_flat[seg].clone())
+    lib.fast_conv_set_x3_dg_fold(2)              # the defaults
+    lib.fast_conv_set_x3_dg_w3(0)
+    assert dxs[0].norm() > 0
+    for name, d, gw in (("fold 2", dxs[1], gws[1]), ("three weight pieces", dxs[2], gws[2])):
+        assert torch.isfinite(d).all()
+        e = rel(d, dxs[0])
+        print(f"layer {l} input gradient, {name} vs plain chain: rel {e:.2e}")
+        assert 0 < e < 1e-6, (name, e)
+        assert rel(gw, gws[0]) < 1e-6
+
+
 @pytest.mark.parametrize("l", [3, 4])
 def test_x3_fc_dgrad_gemm_matches_streaming_kernel(x3_rollout, l):
     """fc_gm_x3 + fc_dgrad_gemm_x3 (per-path GEMM over (slot, column) with LDS-staged 128 x 256 tiles) == fc_dgrad_x3
     (64-row workgroups streaming the weights): input gradient to fp32 summation order, weight gradient (which reads
     the same Gm) equal up to its own float atomics."""
     from pathnet_gym_amd.ops import _lib
-    tr, eng, g_ref, g_hip = x3_rollout
+    tr, eng, _, _, g_hip = x3_rollout
     hp = tr.model.hip
     lib = _lib.lib()
     g = hp.geoms[l]
@@ -418,11 +472,7 @@ def test_x3_shipped_graph_path_gradient_vs_plain_fp32_oracle(hip_lib):
     eng.rollout_backward()                       # a replay of the captured rollout + backward graph
     torch.cuda.synchronize()
     assert eng.dones.any()
-    g_ref = _oracle_grad(tr, eng)
-    err = layer_errors(tr, eng.grad_flat, g_ref)
-    print("fp32x shipped graph path vs fp32 oracle, per layer:", {k: f"{v:.2e}" for k, v in err.items()})
-    for k, v in err.items():
-        assert v < X3_LAYER_TOL, (k, v)
+    check_layers("fp32x shipped graph path", tr, eng.grad_flat, *_oracles(_oracle_grad, tr, eng))
 
 
 @pytest.mark.parametrize("what", ["activation", "weight"])
@@ -454,22 +504,22 @@ def test_x3_range_overflow_raises_named_error(hip_lib, what):
 # the reference's default network (BasicLSTMCell(256) after the L=4 trunk, constants.py:30) in fp32x:
 # csrc/lstm_x3.hip against a plain fp32 autograd oracle of the whole update
 # ---------------------------------------------------------------------------------------------------------------
-def _oracle_grad_lstm(tr, eng):
+def _oracle_grad_lstm(tr, eng, dtype=torch.float32):
     from pathnet_gym_amd.models.pathnet import lstm_cell_ref
     cfg = tr.cfg
     T, B = eng.T, eng.B
     a2c = cfg.a2c
-    flat = tr.model.store.flat.detach().clone().requires_grad_(True)
+    flat = tr.model.store.flat.detach().clone().to(dtype).requires_grad_(True)
     st = ParamStore(cfg.net, DEV, flat=flat)
-    x = eng.obs_stacks().reshape((T + 1) * B, 160, 120, 4).float() / 255.0
-    mask = tr.model.mask.repeat_interleave(eng.E, 0).repeat(T + 1, 1, 1)
+    x = eng.obs_stacks().reshape((T + 1) * B, 160, 120, 4).to(dtype) / 255.0
+    mask = tr.model.mask.repeat_interleave(eng.E, 0).repeat(T + 1, 1, 1).to(dtype)
     feat = trunk_forward_ref(st, x, mask).view(T + 1, B, -1)
     k, bb = st.lstm()
-    h, c = eng.hst[0].float(), eng.cst[0].float()          # state entering step 0 (pre-masked by the carry)
+    h, c = eng.hst[0].to(dtype), eng.cst[0].to(dtype)      # state entering step 0 (pre-masked by the carry)
     hs = []
     for t in range(T + 1):
         if t > 0:
-            keep = (1.0 - eng.dones[t - 1].float())[:, None]
+            keep = (1.0 - eng.dones[t - 1].to(dtype))[:, None]
             h, c = h * keep, c * keep
         h, c = lstm_cell_ref(feat[t], h, c, k, bb)
         hs.append(h)
@@ -480,17 +530,11 @@ def _oracle_grad_lstm(tr, eng):
     assert rel(values, eng.values[:T + 1].reshape(-1)) < 1e-5
     R, adv = nstep_returns(eng.rewards, eng.values[:T], eng.dones.bool(), eng.values[T], a2c.gamma,
                            a2c.gae_lambda, a2c.reward_clip)
-    loss, _, _, _ = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(), R.reshape(-1),
-                             adv.reshape(-1), a2c.entropy_beta, a2c.value_coef,
-                             torch.full((T * B,), eng.weight, device=DEV))
+    loss, _, _, _ = a2c_loss(logits[:T * B], values[:T * B], eng.actions[:T].reshape(-1).long(),
+                             R.reshape(-1).to(dtype), adv.reshape(-1).to(dtype), a2c.entropy_beta, a2c.value_coef,
+                             torch.full((T * B,), eng.weight, device=DEV, dtype=dtype))
     loss.backward()
     return flat.grad
-
-
-# the conv layers' gradients on Alien's frames: the trunk's bf16-pair gradient chain (conv2 dgrad -> conv1 wgrad)
-# measured 2.55e-5 (conv1) / 1.88e-5 (conv2) there vs <= 7e-6 on Pong frames (gpurun_out r4): the budget of the conv
-# layers for that data only; the LSTM, heads and fc layers keep X3_LAYER_TOL on both
-X3_CONV_TOL_ALIEN = 3e-5
 
 
 @pytest.fixture(scope="module", params=[("eager", "Alien"), ("graph", "Alien"), ("eager", "Pong")],
@@ -523,23 +567,18 @@ def x3_lstm_rollout(hip_lib, request):
     eng.rollout_backward()
     torch.cuda.synchronize()
     assert eng.dones.any()
-    return tr, eng, _oracle_grad_lstm(tr, eng), eng.grad_flat.clone(), task
+    return (tr, eng, *_oracles(_oracle_grad_lstm, tr, eng), eng.grad_flat.clone(), task)
 
 
 def test_x3_lstm_engine_gradient_vs_plain_fp32_oracle(x3_lstm_rollout):
-    tr, eng, g_ref, g_hip, task = x3_lstm_rollout
-    err = layer_errors(tr, g_hip, g_ref)
-    print(f"fp32x LSTM engine ({task}) vs fp32 oracle, per layer:", {k: f"{v:.2e}" for k, v in err.items()})
+    tr, eng, g_ref, g32, g_hip, task = x3_lstm_rollout
+    err = check_layers(f"fp32x LSTM engine ({task})", tr, g_hip, g_ref, g32)
     assert "lstm" in err
-    conv = {l for l, g in enumerate(tr.model.hip.geoms) if g.kind == "conv"}
-    for k, v in err.items():
-        tol = X3_CONV_TOL_ALIEN if (task == "Alien" and k in conv) else X3_LAYER_TOL
-        assert v < tol, (k, v)
 
 
 def test_x3_lstm_gradient_check_detects_a_two_percent_error(x3_lstm_rollout):
     """Negative control: the LSTM kernel's (and bias') gradient scaled by 1.02 must fail the per-layer budget."""
-    tr, eng, g_ref, g_hip, _ = x3_lstm_rollout
+    tr, eng, g_ref, _, g_hip, _ = x3_lstm_rollout
     for name in ("lstm.kernel", "lstm.bias"):
         s = tr.model.store.layout.by_name[name]
         bad = g_hip.clone()
@@ -552,7 +591,7 @@ def test_x3_conv1_ring_wgrad_two_tile_passes_match_default(x3_ring_rollout, ncx,
     """conv_wgrad_slab_x3 with 2 column tiles per pass (3 waves / SIMD, the default; the all-modules path of
     masks_with_edges takes 3 passes) == the 3-tile form, weights and biases, up to float-atomic order."""
     from pathnet_gym_amd.ops import _lib
-    tr, eng, g_ref, g_hip = x3_ring_rollout
+    tr, eng, _, _, g_hip = x3_ring_rollout
     hp = tr.model.hip
     lib = _lib.lib()
     g = hp.geoms[0]
