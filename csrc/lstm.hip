@@ -17,7 +17,7 @@
 // transposed reads, fp32 atomics into the flat gradient), bias gradient fused.
 #include "common.h"
 
-namespace {
+namespace lstmk {
 
 DEVI float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 DEVI float tanh_f(float x) {
@@ -266,7 +266,8 @@ __global__ void lstm_carry_kernel(const bf16_t* __restrict__ hT, const float* __
   c0[idx] = kp ? cT[idx] : 0.f;
 }
 
-}  // namespace
+}  // namespace lstmk
+using namespace lstmk;
 
 extern "C" {
 

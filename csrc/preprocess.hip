@@ -80,42 +80,64 @@ extern "C" int launch_rgb_stack_push(const void* rgb, const void* obs_in, void* 
 // Rectangle-list renderer + preprocessing + stack push for the pixel games whose logic runs in
 // torch (envs/atari_games.py): each game emits its scene as [N][R][4] int16 rectangles
 // (y0, x0, h, w; h*w == 0 = hidden) painted in order with one gray level per rectangle slot.
-// One workgroup per env rasterises the scene into an LDS gray image (cooperative fill, one
-// barrier per visible rectangle keeps the painter's order), then resizes + pushes as above.
+// One workgroup per env rasterises the scene into an LDS gray image (below), then resizes + pushes
+// as above.
 // Replaces N x R full-frame boolean mask ops of the torch renderer.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rects_stack_push_kernel(const int16_t* __restrict__ rects,
-                                                               const uint8_t* __restrict__ rect_gray, int R, int bg,
-                                                               const uint32_t* __restrict__ obs_in,
-                                                               uint32_t* __restrict__ obs_out,
-                                                               const uint8_t* __restrict__ reset,
-                                                               const int* __restrict__ tables) {
+// Painter's order without a barrier per rectangle: thread t owns source row t (SH = 210 <= 256 threads) and walks
+// the whole rectangle list (staged once in LDS) painting only its own row, so every pixel is written by one thread
+// in list order.  (One barrier per visible rectangle cost 224 barriers per env for Alien: 260 us per step at 2048
+// envs.)  RING: the resized frame goes to frames + env * frame_stride (one 19.2 KB plane of the engine's frame ring)
+// with the next stack's first valid channel fc_out = reset ? 3 : max(fc_in - 1, 0); otherwise it is pushed into the
+// packed uint32-per-pixel stack.
+#define RECT_MAX 512
+template <bool RING>
+__global__ __launch_bounds__(256) void rects_push_kernel(const int16_t* __restrict__ rects,
+                                                         const uint8_t* __restrict__ rect_gray, int R, int bg,
+                                                         const uint32_t* __restrict__ obs_in,
+                                                         uint32_t* __restrict__ obs_out,
+                                                         const uint8_t* __restrict__ reset,
+                                                         const int* __restrict__ tables, uint8_t* __restrict__ frames,
+                                                         long frame_stride, const uint8_t* __restrict__ fc_in,
+                                                         uint8_t* __restrict__ fc_out) {
   using namespace pre;
   __shared__ int tab[8 * 160];
   __shared__ uint32_t gray[SH * SW / 4];
+  __shared__ uint2 rs_[RECT_MAX];                  // (y0 | y1 << 16, x0 | x1 << 16), clamped; empty -> y1 = y0
+  __shared__ uint8_t rg_[RECT_MAX];
   const int env = blockIdx.x;
   for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
-  const uint32_t bg4 = (uint32_t)bg * 0x01010101u;
-  for (int i = threadIdx.x; i < SH * SW / 4; i += 256) gray[i] = bg4;
-  __syncthreads();
-  uint8_t* g8 = reinterpret_cast<uint8_t*>(gray);
   const int16_t* rr = rects + (long)env * R * 4;
-  for (int r = 0; r < R; ++r) {
+  for (int r = threadIdx.x; r < R; r += 256) {
     int y0 = rr[r * 4 + 0], x0 = rr[r * 4 + 1];
     int y1 = y0 + rr[r * 4 + 2], x1 = x0 + rr[r * 4 + 3];
     y0 = max(y0, 0); x0 = max(x0, 0); y1 = min(y1, SH); x1 = min(x1, SW);
-    if (y1 <= y0 || x1 <= x0) continue;            // uniform across the workgroup
-    const int w = x1 - x0, area = (y1 - y0) * w;
-    const uint8_t g = rect_gray[r];
-    for (int i = threadIdx.x; i < area; i += 256) {
-      const int y = y0 + i / w, x = x0 + (i - (i / w) * w);
-      g8[y * SW + x] = g;
-    }
-    __syncthreads();
+    if (y1 <= y0 || x1 <= x0) y1 = y0 = 0;
+    rs_[r] = make_uint2((uint32_t)y0 | ((uint32_t)y1 << 16), (uint32_t)x0 | ((uint32_t)x1 << 16));
+    rg_[r] = rect_gray[r];
   }
+  __syncthreads();
+  uint8_t* g8 = reinterpret_cast<uint8_t*>(gray);
+  const int row = threadIdx.x;
+  if (row < SH) {
+    uint32_t* rw = gray + row * (SW / 4);
+    const uint32_t bg4 = (uint32_t)bg * 0x01010101u;
+    for (int i = 0; i < SW / 4; ++i) rw[i] = bg4;
+    uint8_t* r8 = g8 + row * SW;
+    for (int r = 0; r < R; ++r) {
+      const uint2 b = rs_[r];                      // one broadcast LDS read per rectangle
+      if (row < (int)(b.x & 0xFFFFu) || row >= (int)(b.x >> 16)) continue;
+      const int x0 = (int)(b.y & 0xFFFFu), x1 = (int)(b.y >> 16);
+      const uint8_t g = rg_[r];
+      for (int x = x0; x < x1; ++x) r8[x] = g;
+    }
+  }
+  __syncthreads();
   const bool rs = reset != nullptr && reset[env];
+  if (RING && threadIdx.x == 0) fc_out[env] = rs ? 3 : (uint8_t)max((int)fc_in[env] - 1, 0);
   const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OH * OW / 4);
   uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OH * OW / 4);
+  uint32_t* fo = RING ? reinterpret_cast<uint32_t*>(frames + (long)env * frame_stride) : nullptr;
   for (int q = threadIdx.x; q < OH * OW / 4; q += 256) {
     const int y = q / (OW / 4), x0 = (q - y * (OW / 4)) * 4;
     const int ys0 = tab[0 * 160 + y], ys1 = tab[1 * 160 + y], cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
@@ -130,6 +152,11 @@ __global__ __launch_bounds__(256) void rects_stack_push_kernel(const int16_t* __
       v = v < 0 ? 0 : (v > 255 ? 255 : v);
       f4[e] = (uint32_t)v;
     }
+    if constexpr (RING) {
+      // the 4 new pixels as one word (a v_perm: the shift / or form of this packing came out with a wrong byte 2
+      // from this kernel's build, tests/test_games_hip.py test_hip_game_frame_ring_matches_packed_stacks)
+      fo[q] = __builtin_amdgcn_perm(f4[3] << 16 | f4[2], f4[1] << 16 | f4[0], 0x06040200u);
+    } else {
     uint4 o;
     if (rs) {
       o = make_uint4(f4[0] * 0x01010101u, f4[1] * 0x01010101u, f4[2] * 0x01010101u, f4[3] * 0x01010101u);
@@ -139,14 +166,30 @@ __global__ __launch_bounds__(256) void rects_stack_push_kernel(const int16_t* __
                      (i.w >> 8) | (f4[3] << 24));
     }
     out4[q] = o;
+    }
   }
 }
 
 extern "C" int launch_rects_stack_push(const void* rects, const void* rect_gray, int R, int bg, const void* obs_in,
                                        void* obs_out, const void* reset, const int* tables, int N,
                                        hipStream_t stream) {
-  rects_stack_push_kernel<<<N, 256, 0, stream>>>((const int16_t*)rects, (const uint8_t*)rect_gray, R, bg,
-                                                 (const uint32_t*)obs_in, (uint32_t*)obs_out, (const uint8_t*)reset,
-                                                 tables);
+  if (R < 0 || R > RECT_MAX || N <= 0) return -22;
+  rects_push_kernel<false><<<N, 256, 0, stream>>>((const int16_t*)rects, (const uint8_t*)rect_gray, R, bg,
+                                                  (const uint32_t*)obs_in, (uint32_t*)obs_out, (const uint8_t*)reset,
+                                                  tables, nullptr, 0, nullptr, nullptr);
+  return (int)hipGetLastError();
+}
+
+// frame-ring form: frames = the engine ring's plane of this step for env 0 ([B][slots][160*120], frame_stride bytes
+// between envs); fc_in / fc_out [B] uint8
+extern "C" int launch_rects_ring_push(const void* rects, const void* rect_gray, int R, int bg, void* frames,
+                                      long frame_stride, const void* fc_in, void* fc_out, const void* reset,
+                                      const int* tables, int N, hipStream_t stream) {
+  if (R < 0 || R > RECT_MAX || N <= 0 || frame_stride < 160 * 120 || frame_stride % 4 || !fc_in || !fc_out ||
+      !frames)
+    return -22;
+  rects_push_kernel<true><<<N, 256, 0, stream>>>((const int16_t*)rects, (const uint8_t*)rect_gray, R, bg, nullptr,
+                                                 nullptr, (const uint8_t*)reset, tables, (uint8_t*)frames,
+                                                 frame_stride, (const uint8_t*)fc_in, (uint8_t*)fc_out);
   return (int)hipGetLastError();
 }

@@ -348,6 +348,30 @@ class PixelGameVec(VecEnv):
         self.obs = self._push(self.obs, done)
         return self.obs.clone(), reward.float(), done, {"episode_return": ep_return}
 
+    @property
+    def supports_ring(self) -> bool:
+        """The engine's frame ring (runtime/engine.py) needs the HIP game logic + renderer."""
+        return bool(getattr(self, "_hip", False))
+
+    def step_ring_into(self, actions, frames, slot, fc_in, fc_out, reward, done, epret):
+        """Engine frame-ring step (HIP only): game logic, then the scene rasterised straight into the ring plane
+        frames[:, slot] with the next stack's first valid channel (csrc/preprocess.hip rects_push_kernel<true>)."""
+        if not self.supports_ring:
+            raise RuntimeError(f"{self.id}: the frame ring needs the HIP game backend")
+        from ..ops import envs as henv
+        a = actions if actions.dtype == torch.int32 and actions.is_contiguous() else \
+            actions.to(torch.int32).contiguous()
+        direct = (reward.dtype == torch.float32 and done.dtype == torch.uint8 and epret.dtype == torch.float32
+                  and reward.is_contiguous() and done.is_contiguous() and epret.is_contiguous())
+        rw, dn, ep = (reward, done, epret) if direct else (self._rw, self._dn, self._ep)
+        self._hip_run(a, None, rw, dn, ep)
+        henv.rects16_ring_push(self._rects, self._gray_tab, self._bg_gray, frames, slot, fc_in, fc_out,
+                               dn.reshape(-1), self._tab32)
+        if not direct:
+            reward.copy_(rw.view(reward.shape))
+            done.copy_(dn.view(done.shape).to(done.dtype))
+            epret.copy_(ep.view(epret.shape))
+
     def step_into(self, actions, obs_in, obs_out, reward, done, epret):
         """Engine hook: torch physics + render, then (backend 'hip') ONE fused kernel that preprocesses the
         frame and pushes it from the engine's obs slot t straight into slot t+1.  With the HIP game logic

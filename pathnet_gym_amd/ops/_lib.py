@@ -58,6 +58,7 @@ _SIGS = {
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_uint, c_int, P, P, P, P, P, P],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],
+    "launch_rects_ring_push": [P, P, c_int, c_int, P, c_long, P, P, P, P, c_int, P],
     "launch_game_step": [c_int, P, P, P, c_int, c_int, c_int, c_uint, c_uint, c_int, c_int, P, P, P, P, P],
     "game_layout": [c_int, P, P],
     "fast_conv_fwd": [P, c_int, P, P, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

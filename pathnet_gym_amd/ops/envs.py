@@ -233,3 +233,24 @@ def rects16_stack_push(rects: torch.Tensor, gray_tab: torch.Tensor, bg_gray: int
         _lib.check(reset, torch.uint8, numel=N, name="reset")
     _lib.call("launch_rects_stack_push", rects.data_ptr(), gray_tab.data_ptr(), R, int(bg_gray), obs_in.data_ptr(),
               obs_out.data_ptr(), _lib.ptr(reset), tables32.data_ptr(), N, _lib.stream())
+
+
+def rects16_ring_push(rects: torch.Tensor, gray_tab: torch.Tensor, bg_gray: int, frames: torch.Tensor, slot: int,
+                      fc_in: torch.Tensor, fc_out: torch.Tensor, reset, tables32: torch.Tensor):
+    """Frame-ring form of ``rects16_stack_push`` (csrc/preprocess.hip rects_push_kernel<true>): write only the new
+    plane frames[:, slot] of the engine's ring [N][slots][160*120] and the next stack's first valid channel
+    fc_out = reset ? 3 : max(fc_in - 1, 0) (runtime/engine.py frame ring)."""
+    N, R = rects.shape[0], rects.shape[1]
+    _lib.check(rects, torch.int16, (N, R, 4), name="rects")
+    _lib.check(gray_tab, torch.uint8, (R,), name="gray_tab")
+    _lib.check(frames, torch.uint8, name="frames")
+    if frames.dim() != 3 or frames.shape[0] != N or frames.shape[2] != 160 * 120 or not 0 <= slot < frames.shape[1]:
+        raise ValueError(f"frames {tuple(frames.shape)} / slot {slot} do not match [{N}, slots, 19200]")
+    _lib.check(fc_in, torch.uint8, numel=N, name="fc_in")
+    _lib.check(fc_out, torch.uint8, numel=N, name="fc_out")
+    _lib.check(tables32, torch.int32, name="tables")
+    if reset is not None:
+        _lib.check(reset, torch.uint8, numel=N, name="reset")
+    _lib.call("launch_rects_ring_push", rects.data_ptr(), gray_tab.data_ptr(), R, int(bg_gray),
+              frames[0, slot].data_ptr(), frames.stride(0), fc_in.data_ptr(), fc_out.data_ptr(), _lib.ptr(reset),
+              tables32.data_ptr(), N, _lib.stream())

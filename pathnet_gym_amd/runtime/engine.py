@@ -68,7 +68,7 @@ class HipEngine:
         # channels before fc[t] replaced by the first valid frame after an episode reset.  The env
         # step writes 19.2 KB per env instead of reading + writing a 77 KB stack.
         self.ring = bool(self.pixels and getattr(cfg, "frame_ring", True) and hp.ring_ok and _lib.USE_FAST
-                         and hasattr(env, "step_ring_into"))
+                         and hasattr(env, "step_ring_into") and getattr(env, "supports_ring", True))
         # observation double buffer (non-ring): the rollout of parity q reads bufs[q][0..T-1] and its last
         # env step writes the NEXT rollout's step-0 input straight into bufs[1-q][0] (the bootstrap forward
         # reads it there), so no obs[0] <- obs[T] copy of the whole stack batch (157 MB at the bench shape)

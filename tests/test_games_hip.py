@@ -84,3 +84,41 @@ def test_hip_game_step_into_engine_buffers(hip_lib):
     assert torch.equal(obs[0][1], obs[1][1])
     for x, y in zip(*rows):
         assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", GAME_NAMES)
+def test_hip_game_frame_ring_matches_packed_stacks(hip_lib, name):
+    """step_ring_into (csrc/preprocess.hip rects_push_kernel<true>: one new plane per env and step + the first valid
+    channel) reconstructs, through the engine's stack rule (runtime/engine.py obs_stack), exactly the packed 4-frame
+    stacks of step(), episode resets included."""
+    N, T = 64, 60
+    ep = GAMES[name](N, device="cuda", seed=7, backend="hip")
+    er = GAMES[name](N, device="cuda", seed=7, backend="hip")
+    assert er.supports_ring
+    for e in (ep, er):
+        e.max_episode_steps = 25
+    o0 = ep.reset()
+    assert torch.equal(o0, er.reset())
+    frames = torch.zeros(N, T + 4, 160 * 120, dtype=torch.uint8, device="cuda")
+    st = o0.reshape(N, 160 * 120, 4)
+    for c in range(4):
+        frames[:, c].copy_(st[:, :, c])
+    fc = torch.zeros(T + 1, N, dtype=torch.uint8, device="cuda")
+    rw, dn, eret = (torch.zeros(N, device="cuda"), torch.zeros(N, dtype=torch.uint8, device="cuda"),
+                    torch.zeros(N, device="cuda"))
+    g = torch.Generator().manual_seed(5)
+    ndone = 0
+    ar = torch.arange(N, device="cuda")[:, None]
+    c4 = torch.arange(4, device="cuda")[None, :]
+    for t in range(T):
+        a = torch.randint(0, ep.num_actions, (N,), generator=g).cuda()
+        obs, r, d, _ = ep.step(a)
+        er.step_ring_into(a.to(torch.int32), frames, t + 4, fc[t], fc[t + 1], rw, dn, eret)
+        assert torch.equal(rw, r.float()), t
+        assert torch.equal(dn.bool(), d.bool()), t
+        idx = (t + 1) + torch.maximum(c4, fc[t + 1].long()[:, None])
+        stack = frames[ar, idx].permute(0, 2, 1).reshape(N, 160, 120, 4)
+        assert torch.equal(stack, obs), t
+        ndone += int(d.sum())
+    assert ndone > 0
