@@ -104,8 +104,10 @@ DEVI f4v mma3(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c)
 }
 
 // ---------------------------------------------------------------------------
-// forward: grid (ceil(B/64), H/16), 256 threads; wave w owns rows 16w..16w+15 of the 64-row tile and the 4 gate
-// blocks of 16 units (KpT2 columns permuted tile-major like csrc/lstm.hip: p = (u/16)*64 + g*16 + u%16).
+// forward: grid (ceil(B/16), H/16), 256 threads.  The workgroup owns 16 rows and the 4 gate blocks of 16 units
+// (KpT2 columns permuted tile-major like csrc/lstm.hip: p = (u/16)*64 + g*16 + u%16); its 4 waves split the
+// reduction (wave w takes k-steps w, w + 4, ...) and sum through LDS, so 8x as many waves are in flight as with one
+// 16-row tile per wave over the whole K (a 16-step chain of dependent global loads per wave: 50 us per step).
 // X: fp32 [B][ldx] (features), hprev / cprev fp32 [B][H]; KpT2: fp16 [2][4H][KK] (hi, lo of K^T * 2^8).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
@@ -113,10 +115,10 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
     const uint8_t* __restrict__ prev_done, const uint16_t* __restrict__ KpT2, const float* __restrict__ flat,
     long b_off, float* __restrict__ hout, float* __restrict__ cout, float* __restrict__ gates,
     float* __restrict__ xh, uint32_t* __restrict__ status, float* __restrict__ amax_xh, int F, int H, int B) {
+  __shared__ f4v red[3][4][64];                   // waves 1..3's partial sums [wave][gate][lane]
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
-  const int row0 = blockIdx.x * 64 + w * 16;
-  if (row0 >= B) return;
+  const int row0 = blockIdx.x * 16;
   const int ut = blockIdx.y;
   const int KK = F + H;
   const long plane = (long)4 * H * KK;
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
   bool bad = false;
   float am = 0.f;                                 // amax of the saved [x | h] rows (G16 scale of the weight gradient)
   const uint16_t* Bp = KpT2 + (long)(ut * 64 + c16) * KK + 8 * grp;
-  for (int k0 = 0; k0 < KK; k0 += 32) {
+  for (int k0 = 32 * w; k0 < KK; k0 += 128) {
     const int k = k0 + 8 * grp;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (av) {
@@ -154,7 +156,15 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
     }
   }
   if (bad && status) atomicOr(status, 2u);
-  if (wr_xh) g16_flush_amax(am, amax_xh);
+  if (wr_xh) g16_flush_amax(am, amax_xh);        // (blockIdx.y uniform: whole workgroups flush or skip)
+  if (w > 0) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) red[w - 1][g][l] = acc[g];
+  }
+  __syncthreads();
+  if (w > 0) return;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) acc[g] += red[0][g][l] + red[1][g][l] + red[2][g][l];
   const float sc = 1.0f / (float)(1 << LX3_SHIFT);
   const int u = ut * 16 + c16;
   const float bi = flat[b_off + u], bj = flat[b_off + H + u], bff = flat[b_off + 2 * H + u],
@@ -184,8 +194,9 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// backward GEMM: out[b][n] = sum_p dz[b][p] K[n][p]; n < F -> dx, n >= F -> dh_prev.  Kb2: bf16 [2][KK][4H].
-// grid (ceil(B/64), KK/64); wave w: 16 rows x 64 columns (4 blocks of 16)
+// backward GEMM: out[b][n] = sum_p dz[b][p] K[n][p]; n < F -> dx, n >= F -> dh_prev.  Kb2: fp16 [2][KK][4H]
+// (hi, lo of K * 2^8).  grid (ceil(B/16), KK/64): a workgroup owns 16 rows x 64 columns (4 blocks of 16), its 4
+// waves split the reduction (below)
 // ---------------------------------------------------------------------------
 // pointwise backward of one step (csrc/lstm.hip lstm_bwd_point_kernel) + the amax of the step's dz (G16)
 __global__ __launch_bounds__(256) void lstm_bwd_point_x3_kernel(
@@ -223,26 +234,27 @@ __global__ __launch_bounds__(256) void lstm_bwd_point_x3_kernel(
 __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
     const float* __restrict__ dz, const uint16_t* __restrict__ Kb2, float* __restrict__ dx, int lddx,
     float* __restrict__ dh_prev, const float* __restrict__ amax_dz, int F, int H, int B) {
+  __shared__ f4v red[3][4][64];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
-  const int row0 = blockIdx.x * 64 + w * 16;
-  if (row0 >= B) return;
+  const int row0 = blockIdx.x * 16;               // the workgroup's 16 rows; its 4 waves split the reduction
   const int n0 = blockIdx.y * 64;
   const int G4 = 4 * H;
   const long plane = (long)(F + H) * G4;
   const int arow = row0 + c16;
   const bool av = arow < B;
-  f4v acc[4], accn[4];
+  f4v acc[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = accn[j] = (f4v){0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 4; ++j) acc[j] = (f4v){0.f, 0.f, 0.f, 0.f};
   const float gs = g16_scale_of(*amax_dz);
-  for (int p0 = 0; p0 < G4; p0 += 32) {
+  // wave w takes k-steps w, w + 4, ...: odd waves hold the odd steps on the negated pieces and are subtracted in the
+  // reduction, so the f16 MFMA's -inf rounding bias enters with alternating signs instead of accumulating
+  // (csrc/trunk_x3.hip fc_dgrad_gemm_x3 FOLD 2)
+  const float sg = (w & 1) ? -1.f : 1.f;
+  for (int p0 = 32 * w; p0 < G4; p0 += 128) {
     const int p = p0 + 8 * grp;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (av) ld8(dz + (long)arow * G4 + p, v);
-    // odd k-steps on the negated pieces into a second chain, subtracted at the end: the f16 MFMA's -inf rounding
-    // bias enters with alternating signs instead of accumulating (csrc/trunk_x3.hip fc_dgrad_gemm_x3 FOLD 2)
-    const float sg = ((p0 >> 5) & 1) ? -1.f : 1.f;
     s8v ah, al;
     split8hs(v, sg * gs, ah, al);                 // fp16 pair of dz * 2^e against the fp16 pair of K * 2^8
 #pragma unroll
@@ -250,12 +262,17 @@ __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
       const long o = (long)(n0 + j * 16 + c16) * G4 + p;
       const s8v bh = *reinterpret_cast<const s8v*>(Kb2 + o);
       const s8v bl = *reinterpret_cast<const s8v*>(Kb2 + plane + o);
-      if (sg < 0.f) accn[j] = mma3h(ah, al, bh, bl, accn[j]);
-      else acc[j] = mma3h(ah, al, bh, bl, acc[j]);
+      acc[j] = mma3h(ah, al, bh, bl, acc[j]);
     }
   }
+  if (w > 0) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] -= accn[j];
+    for (int j = 0; j < 4; ++j) red[w - 1][j][l] = acc[j];
+  }
+  __syncthreads();
+  if (w > 0) return;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = (acc[j] + red[1][j][l]) - (red[0][j][l] + red[2][j][l]);
   const float inv = 1.0f / (gs * (float)(1 << LX3_SHIFT));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -395,7 +412,7 @@ int launch_lstm_fwd_x3(const float* X, int ldx, const float* hprev, const float*
                        float* xh, void* status, float* amax_xh, int F, int H, int B, hipStream_t stream) {
   if (ldx <= 0 || F <= 0 || H <= 0 || B <= 0 || b_off < 0) return -22;
   if (F % 64 != 0 || H % 64 != 0 || ldx % 8 != 0 || ldx < F) return -1;
-  dim3 grid((B + 63) / 64, H / 16);
+  dim3 grid((B + 15) / 16, H / 16);
   lstm_fwd_x3_kernel<<<grid, 256, 0, stream>>>(X, ldx, hprev, cprev, prev_done, (const uint16_t*)KpT2, flat, b_off,
                                                hout, cout, gates, xh, (uint32_t*)status, amax_xh, F, H, B);
   return (int)hipGetLastError();
@@ -416,7 +433,7 @@ int launch_lstm_bwd_gemm_x3(const float* dz, const void* Kb2, float* dx, int ldd
                             const float* amax_dz, int F, int H, int B, hipStream_t stream) {
   if (lddx <= 0 || F <= 0 || H <= 0 || B <= 0 || !amax_dz) return -22;
   if (F % 64 != 0 || H % 64 != 0 || lddx < F) return -1;
-  dim3 grid((B + 63) / 64, (F + H) / 64);
+  dim3 grid((B + 15) / 16, (F + H) / 64);
   lstm_bwd_gemm_x3_kernel<<<grid, 256, 0, stream>>>(dz, (const uint16_t*)Kb2, dx, lddx, dh_prev, amax_dz, F, H, B);
   return (int)hipGetLastError();
 }

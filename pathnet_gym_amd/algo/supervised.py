@@ -236,6 +236,10 @@ def run_supervised_transfer(a) -> Dict:
                       "steps_per_gen": a.steps_per_gen, "batch": a.batch, "lr": a.lr, "seed": a.seed,
                       "backend": sp.backend, "frozen_mode": frozen_mode}}
     t0 = time.time()
+    gsz = [int(v) for v in str(getattr(a, "task_generations", "") or "").split(",") if v.strip()]
+    gens_of = lambda ti: gsz[min(ti, len(gsz) - 1)] if gsz else a.generations      # noqa: E731
+    eval_every = int(getattr(a, "eval_every", 0) or 0)
+    out["config"].update(task_generations=[gens_of(i) for i in range(len(tasks))], eval_every=eval_every)
 
     clip = getattr(a, "clip", 0.0)
     standardize = getattr(a, "standardize", False)
@@ -260,17 +264,22 @@ def run_supervised_transfer(a) -> Dict:
         if ti > 0:
             sp.pop.rng = np.random.RandomState(a.seed * 7919 + ti)     # the paired control replays this draw
             sp.pop.init_genotypes()
-        best_hist = []
-        for gen in range(a.generations):
+        best_hist, test_curve = [], []
+        for gen in range(gens_of(ti)):
             acc = sp.train_generation(data, ti, a.steps_per_gen, a.batch, a.lr, gen, clip)
             sp.pop.step(acc.astype(np.float32), gen)
             best_hist.append(float(acc.max()))
+            if eval_every and ti == len(tasks) - 1 and (gen + 1) % eval_every == 0:
+                # held-out accuracy of the generation's best path: the learning-speed curve of the PathNet paper's
+                # transfer comparison (the paired control records the same curve)
+                test_curve.append([gen + 1, sp.test_accuracy(sp.paths()[int(np.argmax(acc))], test, ti)])
             _progress(name, gen, best_hist[-1], t0)
         winner = int(np.argmax(acc))
         test_acc = sp.test_accuracy(sp.paths()[winner], test, ti)
         sp.end_task(winner)
         out["per_task"].append({"task": name, "best_accuracy": best_hist[-1], "test_accuracy": test_acc,
-                                "curve": best_hist, "frozen": sp.frozen.astype(int).tolist()})
+                                "curve": best_hist, "test_curve": test_curve,
+                                "frozen": sp.frozen.astype(int).tolist()})
     if getattr(a, "control", False) and len(tasks) > 1:
         # transfer check: the last task learned from scratch (no frozen source path), same budget.  paired (default):
         # common random numbers -- the same initial parameters and task head, the same minibatch and GA random
@@ -288,14 +297,21 @@ def run_supervised_transfer(a) -> Dict:
             task_c = 0
         data, test = prep(make_digits(tasks[-1], n_of(last), a.seed * 31 + last, device),
                           make_digits(tasks[-1], 2048, a.seed * 31 + last + 7919, device))
-        hist = []
-        for gen in range(a.generations):
+        hist, ctl_curve = [], []
+        for gen in range(gens_of(last)):
             acc = ctl.train_generation(data, task_c, a.steps_per_gen, a.batch, a.lr, gen, clip)
             ctl.pop.step(acc.astype(np.float32), gen)
             hist.append(float(acc.max()))
+            if eval_every and (gen + 1) % eval_every == 0:
+                ctl_curve.append([gen + 1, ctl.test_accuracy(ctl.paths()[int(np.argmax(acc))], test, task_c)])
             _progress(tasks[-1] + " (scratch)", gen, hist[-1], t0)
         out["control"] = {"task": tasks[-1], "best_accuracy": hist[-1], "curve": hist, "paired": paired,
+                          "test_curve": ctl_curve,
                           "test_accuracy": ctl.test_accuracy(ctl.paths()[int(np.argmax(acc))], test, task_c)}
+        if ctl_curve:
+            tr_c = out["per_task"][-1]["test_curve"]
+            out["transfer_auc"] = {"transfer": float(np.mean([v for _, v in tr_c])),
+                                   "from_scratch": float(np.mean([v for _, v in ctl_curve]))}
         thr = getattr(a, "target_accuracy", 0.9)
         first = lambda c: next((i for i, v in enumerate(c) if v >= thr), None)     # noqa: E731
         out["generations_to_accuracy"] = {"threshold": thr, "transfer": first(out["per_task"][-1]["curve"]),

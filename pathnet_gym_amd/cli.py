@@ -134,6 +134,10 @@ def build_parser():
                    help="or: frozen modules always expressed (reference RL semantics); available: selectable by later paths")
     s.add_argument("--clip", type=float, default=5.0, help="global gradient-norm clip per SGD step (0: off)")
     s.add_argument("--standardize", type=int, default=1, help="per-task per-channel input standardisation")
+    s.add_argument("--task_generations", default="",
+                   help="per-task generation budgets, e.g. 50,10 (overrides --generations)")
+    s.add_argument("--eval_every", type=int, default=0,
+                   help="held-out accuracy of the best path every K generations of the last task and the control")
     s.add_argument("--steps_per_gen", type=int, default=50)
     s.add_argument("--batch", type=int, default=16)
     s.add_argument("--lr", type=float, default=0.05)
