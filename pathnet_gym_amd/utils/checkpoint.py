@@ -82,20 +82,29 @@ def state_tensors(trainer, light: bool = False) -> Dict[str, torch.Tensor]:
     return out
 
 
+def _sync_env_from_device(env):
+    """Kernel-side env state is authoritative: HIP Pong (csrc/envs.hip) or a HIP synthetic game (csrc/games.hip)."""
+    if hasattr(env, "_st32") and hasattr(env, "_ctr32"):
+        from ..ops import envs as henv
+        henv.pong_sync_from_device(env)
+    elif getattr(env, "_hip", False) and hasattr(env, "sync_from_device"):
+        env.sync_from_device()
+
+
 def rank_tensors(trainer, light: bool = False) -> Dict[str, torch.Tensor]:
     """``light``: leave out the frame stacks entering the next rollout (1.3 GB at 512 paths x 32 envs); a load then
     rebuilds every env's stack from its current frame, as at an episode start (resume no longer bit-exact)."""
     env = trainer.env
     out: Dict[str, torch.Tensor] = {}
-    if hasattr(env, "_st32"):          # HIP pong: kernel-side state is authoritative
-        from ..ops import envs as henv
-        henv.pong_sync_from_device(env)
+    _sync_env_from_device(env)
     if hasattr(env, "_steps32"):
         env.steps = env._steps32.long()
         env.counter = env._ctr32.long() & 0xFFFFFFFF
     for name in ("state", "counter", "steps", "ep_ret") + (() if light else ("obs",)):
         if hasattr(env, name) and isinstance(getattr(env, name), torch.Tensor):
             out["env." + name] = _t(getattr(env, name))
+    if getattr(env, "_hip", False) and hasattr(env, "_hip_pack"):
+        out["env.game_state32"] = _t(env._st32)     # HIP synthetic game: the packed kernel state (csrc/games.hip)
     out["env.seed"] = torch.tensor([env.seed_int], dtype=torch.int64)
     if trainer.engine is not None:
         eng = trainer.engine
@@ -134,9 +143,7 @@ def _restack_current_frame(trainer):
     env = trainer.env
     if not hasattr(env, "frame"):
         return
-    if hasattr(env, "_st32"):
-        from ..ops import envs as henv
-        henv.pong_sync_from_device(env)
+    _sync_env_from_device(env)
     f = env.frame()                                   # [N, H, W] uint8
     stack = f[..., None].expand(-1, -1, -1, 4).contiguous()
     env.obs = stack
@@ -193,7 +200,10 @@ def load(trainer, path: str, strict: bool = True):
         for name in ("state", "counter", "steps", "ep_ret", "obs"):
             if "env." + name in r and hasattr(env, name):
                 setattr(env, name, r["env." + name].to(getattr(env, name).device))
-        if hasattr(env, "_st32"):
+        if "env.game_state32" in r and getattr(env, "_hip", False):
+            env._st32.copy_(r["env.game_state32"].to(env._st32.device))
+            env.sync_from_device()
+        elif hasattr(env, "_st32") and hasattr(env, "_ctr32"):
             from ..ops import envs as henv
             henv.pong_sync_to_device(env)
         if hasattr(env, "_steps32"):

@@ -122,3 +122,38 @@ def test_light_checkpoint_resume_restacks_current_frame(hip_lib, tmp_path):
     b.update()
     b.flush()
     assert torch.isfinite(b.model.store.flat).all()
+
+
+@pytest.mark.gpu
+def test_light_checkpoint_of_a_hip_game_on_the_frame_ring(hip_lib, tmp_path):
+    """The same continuation checkpoint with a HIP synthetic game (csrc/games.hip) on the frame ring: the game's
+    kernel-side state is synced through its own unpacker (not Pong's), and the resumed trainer steps on."""
+    import torch
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.config import preset
+    from pathnet_gym_amd.utils import checkpoint as ckpt
+
+    def make():
+        cfg = preset("atari4")
+        cfg.tasks = ["Breakout"]
+        cfg.env = "Breakout"
+        cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 4
+        cfg.ga.backend = "device"
+        cfg.compute_dtype = "fp32x"
+        cfg.frame_ring = True
+        return PathNetTrainer(cfg, device="cuda")
+    a = make()
+    assert a.engine.ring and a.env.supports_ring
+    for _ in range(3):
+        a.update()
+    a.flush()
+    p = str(tmp_path / "ck.safetensors")
+    ckpt.save(a, p, light=True)
+    b = make()
+    ckpt.load(b, p)
+    assert torch.equal(a.model.store.flat, b.model.store.flat)
+    st = b.engine.obs_stack(0).view(b.P * b.E, -1, 4)
+    assert torch.equal(st[..., 0], st[..., 3]) and st.float().mean() > 0
+    b.update()
+    b.flush()
+    assert torch.isfinite(b.model.store.flat).all()
