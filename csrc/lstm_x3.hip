@@ -104,21 +104,23 @@ DEVI f4v mma3(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c)
 }
 
 // ---------------------------------------------------------------------------
-// forward: grid (ceil(B/16), H/16), 256 threads.  The workgroup owns 16 rows and the 4 gate blocks of 16 units
-// (KpT2 columns permuted tile-major like csrc/lstm.hip: p = (u/16)*64 + g*16 + u%16); its 4 waves split the
-// reduction (wave w takes k-steps w, w + 4, ...) and sum through LDS, so 8x as many waves are in flight as with one
-// 16-row tile per wave over the whole K (a 16-step chain of dependent global loads per wave: 50 us per step).
+// forward: grid (ceil(B/64), H/16), 256 threads.  The workgroup owns 64 rows (wave w: rows 16w..16w+15) and the 4
+// gate blocks of 16 units (KpT2 columns permuted tile-major like csrc/lstm.hip: p = (u/16)*64 + g*16 + u%16).  The
+// 64 weight columns of each 32-wide k-step are staged once per workgroup in LDS (double-buffered, the next step's
+// loads in flight during this step's MFMAs): every 16-row block reading the whole weight copy from L2 made the
+// kernel L2-bandwidth-bound (256 MB per call at B = 2048: 50 us).
 // X: fp32 [B][ldx] (features), hprev / cprev fp32 [B][H]; KpT2: fp16 [2][4H][KK] (hi, lo of K^T * 2^8).
 // ---------------------------------------------------------------------------
+#define LX3_BSTR 40                               // LDS halves per staged column (32 + 8 pad)
 __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
     const float* __restrict__ X, int ldx, const float* __restrict__ hprev, const float* __restrict__ cprev,
     const uint8_t* __restrict__ prev_done, const uint16_t* __restrict__ KpT2, const float* __restrict__ flat,
     long b_off, float* __restrict__ hout, float* __restrict__ cout, float* __restrict__ gates,
     float* __restrict__ xh, uint32_t* __restrict__ status, float* __restrict__ amax_xh, int F, int H, int B) {
-  __shared__ f4v red[3][4][64];                   // waves 1..3's partial sums [wave][gate][lane]
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][2][64 * LX3_BSTR];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
-  const int row0 = blockIdx.x * 16;
+  const int row0 = blockIdx.x * 64 + w * 16;
   const int ut = blockIdx.y;
   const int KK = F + H;
   const long plane = (long)4 * H * KK;
@@ -126,13 +128,25 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
   const bool av = arow < B;
   const bool keep = av && !(prev_done && prev_done[arow]);
   const bool wr_xh = xh != nullptr && blockIdx.y == 0;
+  // staging role: column sc (0..63) of the tile, 8 halves at k-offset 8 * sp, both planes
+  const int sc = tid >> 2, sp = tid & 3;
+  const uint16_t* Bg = KpT2 + (long)(ut * 64 + sc) * KK + 8 * sp;
+  uint4 rh = *reinterpret_cast<const uint4*>(Bg), rl = *reinterpret_cast<const uint4*>(Bg + plane);
   f4v acc[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) acc[g] = {0.f, 0.f, 0.f, 0.f};
   bool bad = false;
   float am = 0.f;                                 // amax of the saved [x | h] rows (G16 scale of the weight gradient)
-  const uint16_t* Bp = KpT2 + (long)(ut * 64 + c16) * KK + 8 * grp;
-  for (int k0 = 32 * w; k0 < KK; k0 += 128) {
+  const int nsteps = KK / 32;
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1, k0 = st * 32;
+    *reinterpret_cast<uint4*>(&Bs[buf][0][sc * LX3_BSTR + 8 * sp]) = rh;
+    *reinterpret_cast<uint4*>(&Bs[buf][1][sc * LX3_BSTR + 8 * sp]) = rl;
+    __syncthreads();                              // this step's tile in LDS; the step before last is read out
+    if (st + 1 < nsteps) {
+      rh = *reinterpret_cast<const uint4*>(Bg + k0 + 32);
+      rl = *reinterpret_cast<const uint4*>(Bg + plane + k0 + 32);
+    }
     const int k = k0 + 8 * grp;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (av) {
@@ -149,23 +163,16 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
     split8h(v, ah, al);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const long o = (long)g * 16 * KK + k0;
-      const s8v bh = *reinterpret_cast<const s8v*>(Bp + o);
-      const s8v bl = *reinterpret_cast<const s8v*>(Bp + plane + o);
+      const int o = (g * 16 + c16) * LX3_BSTR + 8 * grp;
+      const s8v bh = *reinterpret_cast<const s8v*>(&Bs[buf][0][o]);
+      const s8v bl = *reinterpret_cast<const s8v*>(&Bs[buf][1][o]);
       acc[g] = mma3h(ah, al, bh, bl, acc[g]);
     }
   }
   if (bad && status) atomicOr(status, 2u);
-  if (wr_xh) g16_flush_amax(am, amax_xh);        // (blockIdx.y uniform: whole workgroups flush or skip)
-  if (w > 0) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) red[w - 1][g][l] = acc[g];
-  }
-  __syncthreads();
-  if (w > 0) return;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) acc[g] += red[0][g][l] + red[1][g][l] + red[2][g][l];
-  const float sc = 1.0f / (float)(1 << LX3_SHIFT);
+  if (wr_xh) g16_flush_amax(am, amax_xh);        // (whole waves: blockIdx.y is uniform)
+  if (row0 >= B) return;
+  const float sc_ = 1.0f / (float)(1 << LX3_SHIFT);
   const int u = ut * 16 + c16;
   const float bi = flat[b_off + u], bj = flat[b_off + H + u], bff = flat[b_off + 2 * H + u],
               bo = flat[b_off + 3 * H + u];
@@ -175,10 +182,10 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
     if (row >= B) continue;
     const bool kp = !(prev_done && prev_done[row]);
     const float c0 = kp ? cprev[(long)row * H + u] : 0.f;
-    const float si = sigm(acc[0][r] * sc + bi);
-    const float tj = tanh_f(acc[1][r] * sc + bj);
-    const float sf = sigm(acc[2][r] * sc + bff + 1.0f);
-    const float so = sigm(acc[3][r] * sc + bo);
+    const float si = sigm(acc[0][r] * sc_ + bi);
+    const float tj = tanh_f(acc[1][r] * sc_ + bj);
+    const float sf = sigm(acc[2][r] * sc_ + bff + 1.0f);
+    const float so = sigm(acc[3][r] * sc_ + bo);
     const float c = c0 * sf + si * tj;
     const float h = tanh_f(c) * so;
     cout[(long)row * H + u] = c;
@@ -195,8 +202,8 @@ __global__ __launch_bounds__(256) void lstm_fwd_x3_kernel(
 
 // ---------------------------------------------------------------------------
 // backward GEMM: out[b][n] = sum_p dz[b][p] K[n][p]; n < F -> dx, n >= F -> dh_prev.  Kb2: fp16 [2][KK][4H]
-// (hi, lo of K * 2^8).  grid (ceil(B/16), KK/64): a workgroup owns 16 rows x 64 columns (4 blocks of 16), its 4
-// waves split the reduction (below)
+// (hi, lo of K * 2^8).  grid (ceil(B/64), KK/64): a workgroup owns 64 rows (16 per wave) x 64 columns (4 blocks
+// of 16); each 32-wide k-step's weight tile is staged once per workgroup in LDS, as in the forward
 // ---------------------------------------------------------------------------
 // pointwise backward of one step (csrc/lstm.hip lstm_bwd_point_kernel) + the amax of the step's dz (G16)
 __global__ __launch_bounds__(256) void lstm_bwd_point_x3_kernel(
@@ -234,45 +241,52 @@ __global__ __launch_bounds__(256) void lstm_bwd_point_x3_kernel(
 __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
     const float* __restrict__ dz, const uint16_t* __restrict__ Kb2, float* __restrict__ dx, int lddx,
     float* __restrict__ dh_prev, const float* __restrict__ amax_dz, int F, int H, int B) {
-  __shared__ f4v red[3][4][64];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][2][64 * LX3_BSTR];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
-  const int row0 = blockIdx.x * 16;               // the workgroup's 16 rows; its 4 waves split the reduction
+  const int row0 = blockIdx.x * 64 + w * 16;     // the workgroup's 64 rows share each staged weight tile
   const int n0 = blockIdx.y * 64;
   const int G4 = 4 * H;
   const long plane = (long)(F + H) * G4;
   const int arow = row0 + c16;
   const bool av = arow < B;
-  f4v acc[4];
+  const int sc = tid >> 2, sp = tid & 3;
+  const uint16_t* Bg = Kb2 + (long)(n0 + sc) * G4 + 8 * sp;
+  uint4 rh = *reinterpret_cast<const uint4*>(Bg), rl = *reinterpret_cast<const uint4*>(Bg + plane);
+  f4v acc[4], accn[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = (f4v){0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 4; ++j) acc[j] = accn[j] = (f4v){0.f, 0.f, 0.f, 0.f};
   const float gs = g16_scale_of(*amax_dz);
-  // wave w takes k-steps w, w + 4, ...: odd waves hold the odd steps on the negated pieces and are subtracted in the
-  // reduction, so the f16 MFMA's -inf rounding bias enters with alternating signs instead of accumulating
-  // (csrc/trunk_x3.hip fc_dgrad_gemm_x3 FOLD 2)
-  const float sg = (w & 1) ? -1.f : 1.f;
-  for (int p0 = 32 * w; p0 < G4; p0 += 128) {
+  const int nsteps = G4 / 32;
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1, p0 = st * 32;
+    *reinterpret_cast<uint4*>(&Bs[buf][0][sc * LX3_BSTR + 8 * sp]) = rh;
+    *reinterpret_cast<uint4*>(&Bs[buf][1][sc * LX3_BSTR + 8 * sp]) = rl;
+    __syncthreads();
+    if (st + 1 < nsteps) {
+      rh = *reinterpret_cast<const uint4*>(Bg + p0 + 32);
+      rl = *reinterpret_cast<const uint4*>(Bg + plane + p0 + 32);
+    }
     const int p = p0 + 8 * grp;
     float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (av) ld8(dz + (long)arow * G4 + p, v);
+    // odd k-steps on the negated pieces into a second chain, subtracted at the end: the f16 MFMA's -inf rounding
+    // bias enters with alternating signs instead of accumulating (csrc/trunk_x3.hip fc_dgrad_gemm_x3 FOLD 2)
+    const bool odd = st & 1;
     s8v ah, al;
-    split8hs(v, sg * gs, ah, al);                 // fp16 pair of dz * 2^e against the fp16 pair of K * 2^8
+    split8hs(v, odd ? -gs : gs, ah, al);          // fp16 pair of dz * 2^e against the fp16 pair of K * 2^8
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const long o = (long)(n0 + j * 16 + c16) * G4 + p;
-      const s8v bh = *reinterpret_cast<const s8v*>(Kb2 + o);
-      const s8v bl = *reinterpret_cast<const s8v*>(Kb2 + plane + o);
-      acc[j] = mma3h(ah, al, bh, bl, acc[j]);
+      const int o = (j * 16 + c16) * LX3_BSTR + 8 * grp;
+      const s8v bh = *reinterpret_cast<const s8v*>(&Bs[buf][0][o]);
+      const s8v bl = *reinterpret_cast<const s8v*>(&Bs[buf][1][o]);
+      if (odd) accn[j] = mma3h(ah, al, bh, bl, accn[j]);
+      else acc[j] = mma3h(ah, al, bh, bl, acc[j]);
     }
   }
-  if (w > 0) {
+  if (row0 >= B) return;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) red[w - 1][j][l] = acc[j];
-  }
-  __syncthreads();
-  if (w > 0) return;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = (acc[j] + red[1][j][l]) - (red[0][j][l] + red[2][j][l]);
+  for (int j = 0; j < 4; ++j) acc[j] -= accn[j];
   const float inv = 1.0f / (gs * (float)(1 << LX3_SHIFT));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -412,7 +426,7 @@ int launch_lstm_fwd_x3(const float* X, int ldx, const float* hprev, const float*
                        float* xh, void* status, float* amax_xh, int F, int H, int B, hipStream_t stream) {
   if (ldx <= 0 || F <= 0 || H <= 0 || B <= 0 || b_off < 0) return -22;
   if (F % 64 != 0 || H % 64 != 0 || ldx % 8 != 0 || ldx < F) return -1;
-  dim3 grid((B + 15) / 16, H / 16);
+  dim3 grid((B + 63) / 64, H / 16);
   lstm_fwd_x3_kernel<<<grid, 256, 0, stream>>>(X, ldx, hprev, cprev, prev_done, (const uint16_t*)KpT2, flat, b_off,
                                                hout, cout, gates, xh, (uint32_t*)status, amax_xh, F, H, B);
   return (int)hipGetLastError();
@@ -433,7 +447,7 @@ int launch_lstm_bwd_gemm_x3(const float* dz, const void* Kb2, float* dx, int ldd
                             const float* amax_dz, int F, int H, int B, hipStream_t stream) {
   if (lddx <= 0 || F <= 0 || H <= 0 || B <= 0 || !amax_dz) return -22;
   if (F % 64 != 0 || H % 64 != 0 || lddx < F) return -1;
-  dim3 grid((B + 15) / 16, (F + H) / 64);
+  dim3 grid((B + 63) / 64, (F + H) / 64);
   lstm_bwd_gemm_x3_kernel<<<grid, 256, 0, stream>>>(dz, (const uint16_t*)Kb2, dx, lddx, dh_prev, amax_dz, F, H, B);
   return (int)hipGetLastError();
 }
