@@ -544,7 +544,10 @@ DEVI uint4 planes_to_px4(uint4 v) {
 // and every MFMA operand read are those of the packed-stack kernel.
 // PIPE: the next k-step's pixel and weight fragments are read from LDS while this k-step's MFMAs run (one k-step of
 // fragments ahead instead of a wait on every k-step's reads)
-template <class G, bool RING = false, bool PIPE = false>
+// F16B: the band is converted to fp16 (1024 + v) ONCE while it is staged (single LDS buffer of 2 x 17.3 KB, one more
+// barrier per band) instead of per MFMA operand read: every pixel of an 8x8/s4 band feeds 4 positions x 2 kernel
+// rows, so the per-read conversion (v_perm per 2 pixels) ran ~4x per pixel
+template <class G, bool RING = false, bool PIPE = false, bool F16B = false>
 __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                            long ylo, uint8_t* __restrict__ bits,
                                                            const uint16_t* __restrict__ Wh, long wlo,
@@ -558,7 +561,8 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
   constexpr int KPs = G::KP + 8;
   constexpr int NK = G::KP / 32;
   constexpr int NCXT = 2;
-  __shared__ __attribute__((aligned(16))) uint8_t Xb[2][B::BYTES];
+  static_assert(!(F16B && PIPE), "F16B: plain k loop");
+  __shared__ __attribute__((aligned(16))) uint8_t Xb[F16B ? 1 : 2][F16B ? 2 * B::BYTES : B::BYTES];
   __shared__ __attribute__((aligned(16))) uint16_t Ws[2][NCXT * 16 * KPs];
   __shared__ __attribute__((aligned(16))) float bias_s[NCXT * 16];
   __shared__ float wsum_s[NCXT * 16];
@@ -623,12 +627,21 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
     if constexpr (RING) return planes_to_px4(v);
     else return v;
   };
+  auto put = [&](int buf, int c, const uint4& v) {
+    if constexpr (F16B) {                           // 16 pixel bytes -> 16 fp16 (1024 + v), 32 bytes
+      const uint4 q = px(v);
+      *reinterpret_cast<s8v*>(&Xb[0][c * 32]) = u8x8_to_f16off(make_uint2(q.x, q.y));
+      *reinterpret_cast<s8v*>(&Xb[0][c * 32 + 16]) = u8x8_to_f16off(make_uint2(q.z, q.w));
+    } else {
+      *reinterpret_cast<uint4*>(&Xb[buf][c * 16]) = px(v);
+    }
+  };
   auto store_band = [&](int buf) {
-    *reinterpret_cast<uint4*>(&Xb[buf][tid * 16]) = px(rg0);
-    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 256) * 16]) = px(rg1);
-    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 512) * 16]) = px(rg2);
-    *reinterpret_cast<uint4*>(&Xb[buf][(tid + 768) * 16]) = px(rg3);
-    if (tid + 1024 < B::NCH) *reinterpret_cast<uint4*>(&Xb[buf][(tid + 1024) * 16]) = px(rg4);
+    put(buf, tid, rg0);
+    put(buf, tid + 256, rg1);
+    put(buf, tid + 512, rg2);
+    put(buf, tid + 768, rg3);
+    if (tid + 1024 < B::NCH) put(buf, tid + 1024, rg4);
   };
 
 
@@ -667,7 +680,7 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
     auto run = [&](auto ncc) {
       constexpr int NC = decltype(ncc)::value;
       int buf = 0;
-      for (int u = b_beg; u < b_end; ++u, buf ^= 1) {
+      for (int u = b_beg; u < b_end; ++u, buf ^= (F16B ? 0 : 1)) {
         __syncthreads();                               // band u in LDS (and bias_s); buf ^ 1 free
         if (u + 1 < b_end) load_band(u + 1);
         const int s = u / B::NB, oh0 = (u - s * B::NB) * B::OBR;
@@ -733,8 +746,10 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
         for (int kk = 0; kk < NK; ++kk) {                // k-step kk = kernel row kh
           s8v a[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            a[i] = u8x8_to_f16off(*reinterpret_cast<const uint2*>(xb + abase[i] + kk * B::RB));
+          for (int i = 0; i < 4; ++i) {
+            if constexpr (F16B) a[i] = *reinterpret_cast<const s8v*>(xb + 2 * (abase[i] + kk * B::RB));
+            else a[i] = u8x8_to_f16off(*reinterpret_cast<const uint2*>(xb + abase[i] + kk * B::RB));
+          }
           const int kc = kk * 4 + grp;
 #pragma unroll
           for (int ct = 0; ct < NC; ++ct) {
@@ -756,7 +771,14 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
           conv_epi_sw<NC>(acc[i], bias_s, ct0, cnt, q, in_scale, out_scale, growb + pos, bits, bits_rows, Y, ylo,
                           pass > 0, valid);
         }
-        if (u + 1 < b_end) store_band(buf ^ 1);        // buf ^ 1 was read in band u - 1, before this band's barrier
+        if constexpr (F16B) {
+          if (u + 1 < b_end) {
+            __syncthreads();                           // every wave done with band u (one buffer)
+            store_band(0);
+          }
+        } else {
+          if (u + 1 < b_end) store_band(buf ^ 1);      // buf ^ 1 was read in band u - 1, before this band's barrier
+        }
       }
     };
     if (ncg == 1) run(std::integral_constant<int, 1>{});
@@ -3501,6 +3523,7 @@ static int X3_WG3_TILE = 1;
 // output positions; the 3x3 layer's 176 leave paired waves idle).  Measured (kwin_x3_v24*.md, v25*.md): 4x4/s2
 // 25.3 us paired vs 26.0-26.2 single (32.5-32.7 in slow runs), 3x3 18.4-18.8 paired vs 15.9-16.2 single
 static int X3_FWD_TILE = 3;
+static int X3_C1_F16B = 0;     // band forward: 1 = the band converted to fp16 once at staging (conv1_fwd_band_x2 F16B)
 static int X3_C1_PIPE = 0;     // band forward: 1 = next k-step's LDS fragments read during this k-step's MFMAs
 static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
 // input gradients (conv_dgrad_x3, fc_dgrad_gemm_x3): 1 = the weights as THREE fp16 pieces (a fourth MFMA per k-step),
@@ -3527,6 +3550,7 @@ void fast_conv_set_x3_dg_fold(int v) { X3_DG_FOLD = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
 void fast_conv_set_x3_c1_band(int v) { X3_C1_BAND = v; }
 void fast_conv_set_x3_c1_pipe(int v) { X3_C1_PIPE = v; }
+void fast_conv_set_x3_c1_f16b(int v) { X3_C1_F16B = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
@@ -3547,7 +3571,11 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
       const long nbands = (long)T * E * BD1<C1>::NB;
       long bpw = (nbands * P + 511) / 512;                 // ~2 workgroups per CU over the launch
       if (bpw < 2) bpw = 2;
-      if (X3_C1_PIPE)
+      if (X3_C1_F16B)
+        conv1_fwd_band_x2<C1, false, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+            (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac,
+            layer, L, M, P, E, T, t0, br, (int)bpw, isc, os);
+      else if (X3_C1_PIPE)
         conv1_fwd_band_x2<C1, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
             (const uint8_t*)X, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac,
             layer, L, M, P, E, T, t0, br, (int)bpw, isc, os);
@@ -3625,7 +3653,11 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
   const long nbands = (long)T * E * BD1<C1>::NB;
   long bpw = (nbands * P + 511) / 512;
   if (bpw < 2) bpw = 2;
-  if (X3_C1_PIPE)
+  if (X3_C1_F16B)
+    conv1_fwd_band_x2<C1, true, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+        (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+  else if (X3_C1_PIPE)
     conv1_fwd_band_x2<C1, true, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
         (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
         ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);

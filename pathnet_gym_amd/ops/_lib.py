@@ -152,6 +152,7 @@ _SIGS = {
     "fast_conv_set_x3_fc_mmv": [c_int],
     "fast_conv_set_x3_fc_dg_gemm": [c_int],
     "fast_conv_set_x3_dg_w3": [c_int],
+    "fast_conv_set_x3_c1_f16b": [c_int],
     "fast_conv_set_x3_dg_fold": [c_int],
     "fast_conv_set_x3_fwd_tile": [c_int],
     "fast_conv_set_x3_c1_band": [c_int],
