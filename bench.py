@@ -310,9 +310,11 @@ def main():
         "scaling": args.scaling,
         "vs_baseline": round(value / BASELINE_STEPS_PER_SEC, 1),
         "dtype": tr.compute_dtype,
-        "compute": {"fp32x": "fp32-accurate split operands: fp16 hi+lo pairs (forward), bf16 hi+lo pairs (gradients), "
-                             "3 MFMAs per product, fp32 accumulation and master weights; <= 2e-5 relative per layer "
-                             "vs a plain fp32 PyTorch oracle (tests/test_x3_engine.py)",
+        "compute": {"fp32x": "fp32-accurate split operands: fp16 hi+lo pairs (forward), fp16 hi+lo pairs of G * 2^e "
+                             "(gradients, one power of two per layer from the amax), 3 MFMAs per product, "
+                             "sign-alternating accumulation in the input gradients, fp32 accumulation and master "
+                             "weights; < 2e-5 relative per layer vs a float64 autograd truth, at most plain fp32's own "
+                             "error on ill-conditioned layers (tests/test_x3_engine.py)",
                     "fp32": "fp32 MFMA operands (v_mfma_f32_16x16x4_f32)",
                     "bf16": "bf16/fp16 MFMA operands, fp32 accumulation (reduced precision)"}[tr.compute_dtype],
         "max_rel_err_per_layer": 2e-5 if x3 else (1e-5 if tr.compute_dtype == "fp32" else None),
