@@ -19,8 +19,8 @@ that are NOT counted.  Weak scaling: P paths per GPU, fixed.
 
 Precision: the headline runs the fp32x engine (``--dtype fp32x``, reported as "dtype": "fp32x" with the
 bound "max_rel_err_per_layer": 2e-5): the reference trains in fp32 (game_ac_network.py:89-110) and fp32x
-matches a plain fp32 PyTorch oracle to <= 2e-5 per layer (fp16 / bf16 hi+lo operand pairs, three MFMAs per
-product, csrc/trunk_x3.hip; tests/test_x3_engine.py).  The bf16 engine is timed on the same config as
+matches a float64 autograd truth to < 2e-5 per layer (fp16 hi+lo operand pairs, gradients as scaled fp16 pairs,
+three MFMAs per product, csrc/trunk_x3.hip; tests/test_x3_engine.py).  The bf16 engine is timed on the same config as
 ``value_bf16``.
 
 Timing: after W warmup updates, ``--windows`` (default 3) back-to-back windows of EXACTLY K updates, each

@@ -302,8 +302,8 @@ __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// weight gradient: dK[n][p] += sum_r xh[r][n] dz[r][p] over a chunk of rows (xh, dz fp32, split into bf16 pairs
-// while staging in LDS); db[p] += sum_r dz[r][p] (blockIdx.x == 0 tiles).  grid (KK/64, 4H/64, nchunks)
+// weight gradient: dK[n][p] += sum_r xh[r][n] dz[r][p] over a chunk of rows (xh, dz fp32, split into scaled fp16
+// pairs while staging in LDS: xh * 2^ex, dz * 2^ez from their amaxes); db[p] += sum_r dz[r][p] (blockIdx.x == 0 tiles).  grid (KK/64, 4H/64, nchunks)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
     const float* __restrict__ xh, const float* __restrict__ dz, float* __restrict__ grad, long k_off, long b_off,

@@ -1,15 +1,17 @@
-// PathNet trunk in the fp32-accurate split-bf16 mode (TrainConfig.compute_dtype = "fp32x").
+// PathNet trunk in the fp32-accurate split-operand mode (TrainConfig.compute_dtype = "fp32x").
 //
 // The reference computes in fp32 (TF default dtype, game_ac_network.py:89-110).  gfx950 has no xf32 MFMA and its
 // fp32-input MFMA runs at 1/16 of the bf16 rate, so this mode keeps every value the bf16 engine keeps in 16 bits as
-// a PAIR: x = hi + lo, hi = rnd(x), lo = rnd(x - hi).  The forward uses fp16 pairs (22 significant bits; activations
-// are ReLU sums, weights enter as W * 2^8, both far inside fp16's range); the gradient side uses bf16 pairs (16 bits,
-// bf16's exponent range for the output gradients).  A product is three MFMAs into one fp32 accumulator,
-//     a*b ~ a_hi*b_hi + a_hi*b_lo + a_lo*b_hi          (the dropped a_lo*b_lo term is <= 2^-16 |a*b| in bf16)
+// a PAIR: x = hi + lo, hi = rnd(x), lo = rnd(x - hi), fp16 halves (22 significant bits).  Activations are ReLU sums
+// and weights enter as W * 2^8, both far inside fp16's range; output gradients enter as G * 2^e, one power of two per
+// layer from the gradient's amax (G16, below).  A product is three MFMAs into one fp32 accumulator,
+//     a*b ~ a_hi*b_hi + a_hi*b_lo + a_lo*b_hi          (the dropped a_lo*b_lo term is <= 2^-22 |a*b|)
 // so each MFMA k-step costs 3x the bf16 engine's, against 16x for v_mfma_f32_16x16x4_f32 (csrc/trunk_f32.hip).
 // Inputs that are exact in 16 bits need two: the uint8 frame stack (exact in fp16) against the fp16 hi/lo pair of
-// the first layer's weights (scaled by 2^X3_W0_SHIFT so the lo half stays out of the fp16 subnormal range), and the
-// same uint8 stack (exact in bf16) against the hi/lo output gradient in that layer's weight gradient.
+// the first layer's weights, and the same stack against the output gradient's pair in that layer's weight gradient.
+// The input gradients accumulate odd k-steps on negated operands in a second chain (X3_DG_FOLD = 2): the f16 MFMA's
+// sum is biased toward -inf, which the weight gradients below would otherwise sum coherently
+// (profiles/r4/x3_precision.md).
 //
 // Storage (pathnet_gym_amd/ops/pathnet_ops.py allocates it):
 //   activations between layers : the fp16 pair (hi | lo planes of the bf16 engine's layout; kernels take the hi
@@ -203,7 +205,8 @@ DEVI f4v mma2h(const s8v& a, const s8v& bh, const s8v& bl, f4v c) {
 // activation operands (already fp16 pairs) need no conversion.  The producer of G writes its amax: x3_amax for the
 // last layer's input gradient (heads / LSTM), the input-gradient epilogues (conv_dgrad_x3, fc_dgrad_gemm_x3,
 // fc_dgrad_x3) for the layer below; float bits of non-negative values order like unsigned ints, so one
-// atomicMax per wave.  scripts/x3_numerics.py: per-layer weight-gradient error 1.1-1.8e-5 (bf16 pairs) -> 2-3e-7.
+// atomicMax per wave (per workgroup for elementwise producers).  scripts/x3_numerics.py: per-layer weight-gradient
+// error 1.1-1.8e-5 with bf16 pairs -> 2-3e-7 in float64 emulation.
 DEVI float g16_scale(const float* amax) {
   const uint32_t b = __float_as_uint(*amax);
   const int e = (int)((b >> 23) & 0xFFu) - 127;           // floor(log2 amax) (normal amax)

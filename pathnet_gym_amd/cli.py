@@ -63,8 +63,8 @@ def build_parser():
         p.add_argument("--no_graph", action="store_true")
         p.add_argument("--compute_dtype", default=None, choices=["bf16", "fp32", "fp32x"],
                        help="HIP engine operand precision: fp32 (fp32 MFMA operands, csrc/trunk_f32.hip, bit-"
-                            "reproducible), fp32x (fp32-accurate fp16/bf16 hi+lo pairs, csrc/trunk_x3.hip + lstm_x3.hip, "
-                            "<= 2e-5 per layer vs fp32), bf16")
+                            "reproducible), fp32x (fp32-accurate fp16 hi+lo pairs, csrc/trunk_x3.hip + lstm_x3.hip, "
+                            "< 2e-5 per layer vs a float64 truth), bf16")
         p.add_argument("--deterministic", type=int, default=None,
                        help="1: fixed-order gradient reductions (bit-reproducible updates)")
         # RL constants (constants.py)

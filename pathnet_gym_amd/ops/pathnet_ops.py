@@ -214,8 +214,8 @@ class HipPathNet:
         self.inv_cnt = torch.zeros(self.L, self.M, dtype=torch.int32, device=dev)
         lay_h = lay.heads
         self.heads_off = lay_h
-        # fused LSTM cell: csrc/lstm.hip (bf16 copies of the fp32 master kernel) or, in fp32x, csrc/lstm_x3.hip (fp16 /
-        # bf16 hi+lo pairs, fp32 state: the reference's default network at its precision).  fp32 (deterministic) keeps
+        # fused LSTM cell: csrc/lstm.hip (bf16 copies of the fp32 master kernel) or, in fp32x, csrc/lstm_x3.hip (fp16
+        # hi+lo pairs, fp32 state: the reference's default network at its precision).  fp32 (deterministic) keeps
         # the hybrid autograd LSTM.
         self.lstm = None
         if cfg.use_lstm and not self.deterministic:
@@ -673,7 +673,8 @@ class HipPathNet:
             raise RuntimeError(f"fp32x: fc layer {l} backward has no split-bf16 kernel")
 
     def _gm_buffer_x3(self, bits_rows: int) -> torch.Tensor:
-        """[2][M][bits_rows][256] bf16 hi/lo scratch for the masked fc gradient (allocated before graph capture)."""
+        """[2][M][bits_rows][256] 16-bit hi/lo scratch for the masked fc gradient: fp16 pair of G * 2^e (G16; a bf16
+        tensor only as storage), allocated before graph capture."""
         n = 2 * self.M * bits_rows * 256
         buf = getattr(self, "_gm", None)
         if buf is None or buf.numel() != n:
