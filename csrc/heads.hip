@@ -333,9 +333,12 @@ __global__ __launch_bounds__(256) void a2c_grad_kernel(
 // part == nullptr: the row-chunk partials meet in grad with fp32 atomics.  Deterministic mode: chunk c writes
 // its partials to part[c][F*A + F + A + 1] (dWp, dWv, dbp, dbv) and heads_reduce_kernel sums the chunks in order.
 #define HB_ROWS 128
-// atomic (non-deterministic) mode, heads_set_bwd_rows(32): 32-row chunks (1 280 workgroups at T*B = 40 960 instead of 320: each thread's
-// serial row loop of dependent loads is 4x shorter and ~5 workgroups share a CU)
-static int HB_ROWS_ATOMIC = HB_ROWS;     // 32 via heads_set_bwd_rows (not yet measured on the GPU)
+// non-deterministic mode (launch_heads_bwd_split, default heads_set_bwd_rows(32)): 32-row chunks (1 280 workgroups at
+// T*B = 40 960 instead of 320: each thread's serial row loop of dependent loads is 4x shorter and ~5 workgroups share
+// a CU) writing partials that heads_reduce_wide_kernel sums: 32 + 20 vs 113 us for the 128-row kernel with fp32
+// atomics (heads_set_bwd_rows(128)).  32-row chunks with atomics instead of partials ran 257 us (2.3 M atomics on the
+// 1 799 weight / bias gradient addresses).
+static int HB_ROWS_ATOMIC = 32;
 template <int AM, typename FT, int ROWS = HB_ROWS>
 __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const FT* __restrict__ feat, int F, const float* __restrict__ dlogits, const float* __restrict__ dvalue,
@@ -484,21 +487,59 @@ int launch_a2c_grad(const float* logits, const float* values, const int* actions
 
 }  // extern "C"
 
+// the split path's chunk reduction: 64 elements per workgroup, the 4 waves each sum a quarter of the chunks (8
+// independent partial sums per lane), combined in LDS; one writer per element.  (heads_reduce_kernel's one thread
+// per element over all 1 280 chunks was a 1 280-long dependent load chain: 307 us.)
+__global__ __launch_bounds__(256) void heads_reduce_wide_kernel(const float* __restrict__ part, int nchunk, int F,
+                                                                int A, long pw, long pb, long vw, long vb,
+                                                                float* __restrict__ grad) {
+  __shared__ float red[4][64];
+  const long PS = (long)F * A + F + A + 1;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const long e = (long)blockIdx.x * 64 + l;
+  const int c0 = (int)((long)nchunk * w / 4), c1 = (int)((long)nchunk * (w + 1) / 4);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (e < PS) {
+    int c = c0;
+    for (; c + 8 <= c1; c += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += part[(long)(c + j) * PS + e];
+    }
+    for (; c < c1; ++c) a[0] += part[(long)c * PS + e];
+  }
+  red[w][l] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (w > 0 || e >= PS) return;
+  const float s = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  long dst;
+  if (e < (long)F * A) dst = pw + e;
+  else if (e < (long)F * A + F) dst = vw + (e - (long)F * A);
+  else if (e < PS - 1) dst = pb + (e - (long)F * A - F);
+  else dst = vb;
+  grad[dst] += s;
+}
+
+template <typename FT>
+static int heads_bwd_split32(const void* feat, int F, const float* dlogits, const float* dvalue, int N, int A,
+                             const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
+                             float* part, hipStream_t stream) {
+  const int nc = (N + 31) / 32;
+  if (A <= 8)
+    heads_bwd_kernel<8, FT, 32><<<nc, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw,
+                                                        vb, grad, dfeat, part);
+  else
+    heads_bwd_kernel<AMAX, FT, 32><<<nc, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb,
+                                                           vw, vb, grad, dfeat, part);
+  const long PS = (long)F * A + F + A + 1;
+  heads_reduce_wide_kernel<<<(unsigned)((PS + 63) / 64), 256, 0, stream>>>(part, nc, F, A, pw, pb, vw, vb, grad);
+  return (int)hipGetLastError();
+}
+
 template <typename FT>
 static int heads_bwd_launch(const void* feat, int F, const float* dlogits, const float* dvalue, int N, int A,
                             const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
                             float* part, hipStream_t stream) {
   if (A > AMAX) return -1;
-  if (!part && HB_ROWS_ATOMIC == 32) {
-    const int nc = (N + 31) / 32;
-    if (A <= 8)
-      heads_bwd_kernel<8, FT, 32><<<nc, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw,
-                                                          vb, grad, dfeat, nullptr);
-    else
-      heads_bwd_kernel<AMAX, FT, 32><<<nc, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb,
-                                                             vw, vb, grad, dfeat, nullptr);
-    return (int)hipGetLastError();
-  }
   const int nchunk = (N + HB_ROWS - 1) / HB_ROWS;
   if (A <= 8)
     heads_bwd_kernel<8, FT><<<nchunk, 256, 0, stream>>>((const FT*)feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw,
@@ -531,6 +572,28 @@ int launch_heads_bwd_f32(const void* feat, int F, const float* dlogits, const fl
 }
 
 extern "C" void heads_set_bwd_rows(int r) { HB_ROWS_ATOMIC = r == 32 ? 32 : HB_ROWS; }
+
+// non-deterministic heads backward with a partials buffer of heads_bwd_split_numel floats: 32-row chunks + ordered
+// chunk reduction when heads_set_bwd_rows(32), else the 128-row atomic kernel (part unused)
+long heads_bwd_split_numel(int N, int F, int A) {
+  if (N <= 0 || F <= 0 || A <= 0) return -1;
+  return (long)((N + 31) / 32) * ((long)F * A + F + A + 1);
+}
+
+int launch_heads_bwd_split(const void* feat, int f32, int F, const float* dlogits, const float* dvalue, int N, int A,
+                           const float* flat, long pw, long pb, long vw, long vb, float* grad, float* dfeat,
+                           float* part, hipStream_t stream) {
+  if (F <= 0 || N <= 0 || A <= 0 || f32 < 0 || pw < 0 || pb < 0 || vw < 0 || vb < 0 || !part) return -22;
+  if (A > AMAX) return -1;
+  if (HB_ROWS_ATOMIC != 32)
+    return f32 ? heads_bwd_launch<float>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, nullptr,
+                                         stream)
+               : heads_bwd_launch<bf16_t>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, nullptr,
+                                          stream);
+  return f32 ? heads_bwd_split32<float>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, part, stream)
+             : heads_bwd_split32<bf16_t>(feat, F, dlogits, dvalue, N, A, flat, pw, pb, vw, vb, grad, dfeat, part,
+                                         stream);
+}
 
 // deterministic heads backward (fixed-order chunk reduction); part: ceil(N/128) * (F*A + F + A + 1) floats
 long heads_bwd_part_numel(int N, int F, int A) {

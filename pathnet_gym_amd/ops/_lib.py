@@ -119,6 +119,8 @@ _SIGS = {
     "launch_refresh_weights_f32": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, P],
     "launch_heads_bwd_det": [P, c_int, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P, P],
     "heads_bwd_part_numel": [c_int, c_int, c_int],
+    "heads_bwd_split_numel": [c_int, c_int, c_int],
+    "launch_heads_bwd_split": [P, c_int, c_int, P, P, c_int, c_int, P, c_long, c_long, c_long, c_long, P, P, P, P],
     "fast_conv_dgrad_bf16": [P, c_int, P, P, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_int, c_int, c_int, c_int, c_long, c_float, P, c_int, P],
     "fast_conv_wgrad_bf16g": [P, c_int, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -143,6 +143,7 @@ class HipPathNet:
         # so one seed reproduces the update bit for bit
         self.deterministic = self.f32 or bool(getattr(model, "deterministic", False))
         self._hpart = None
+        self._hsplit = None
         self.L, self.M = cfg.L, cfg.M
         lay = model.store.layout
         dev = model.device
@@ -893,10 +894,16 @@ class HipPathNet:
                       dvalue.data_ptr(), N, A, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"],
                       grad_flat.data_ptr(), dfeat.data_ptr(), self._hpart.data_ptr(), _lib.stream())
             return
-        _lib.call("launch_heads_bwd_f32" if self.feat_dtype == torch.float32 else "launch_heads_bwd", feat.data_ptr(), F,
-                  dlogits.data_ptr(),
-                  dvalue.data_ptr(), N, A, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"], h["vb"],
-                  grad_flat.data_ptr(), dfeat.data_ptr(), _lib.stream())
+        # partials buffer of the 32-row split (csrc/heads.hip launch_heads_bwd_split; the 128-row atomic kernel
+        # unless heads_set_bwd_rows(32)); grown outside graph capture like _hpart
+        n = _lib.lib().heads_bwd_split_numel(N, F, A)
+        if self._hsplit is None or self._hsplit.numel() < n:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("heads backward partials first needed inside a graph capture")
+            self._hsplit = torch.empty(n, dtype=torch.float32, device=feat.device)
+        _lib.call("launch_heads_bwd_split", feat.data_ptr(), int(self.feat_dtype == torch.float32), F,
+                  dlogits.data_ptr(), dvalue.data_ptr(), N, A, m.store.flat.data_ptr(), h["pw"], h["pb"], h["vw"],
+                  h["vb"], grad_flat.data_ptr(), dfeat.data_ptr(), self._hsplit.data_ptr(), _lib.stream())
 
     # -- standalone forward (tests / acting): obs [B, ...] -> feat [B, F] --------
     def trunk(self, obs: torch.Tensor, samples_per_path: int):

@@ -349,8 +349,8 @@ def test_heads_sampling_row_base_and_torch_keyed_sampler(hip_lib):
 
 @pytest.mark.parametrize("rows", [32, 128])
 def test_heads_bwd_row_chunks_match_oracle(hip_lib, rows):
-    """heads_set_bwd_rows(32) (1 280 workgroups at the bench shape) and the default 128-row chunks against the fp32
-    oracle at an N that is not a multiple of 32."""
+    """The default 32-row chunks with partials + wide chunk reduction (1 280 workgroups at the bench shape) and the
+    128-row atomic kernel (heads_set_bwd_rows(128)) against the fp32 oracle at an N that is not a multiple of 32."""
     from pathnet_gym_amd.models.pathnet import ParamStore
     from pathnet_gym_amd.ops import _lib
     cfg = small_pixel_cfg()
@@ -368,7 +368,7 @@ def test_heads_bwd_row_chunks_match_oracle(hip_lib, rows):
         m.hip.heads_bwd(feat, dlog, dval, gflat, dfeat)
         torch.cuda.synchronize()
     finally:
-        _lib.lib().heads_set_bwd_rows(128)
+        _lib.lib().heads_set_bwd_rows(32)            # the default
     flat = m.store.flat.detach().clone().requires_grad_(True)
     st = ParamStore(cfg, DEV, flat=flat)
     fx = feat.float().requires_grad_(True)
