@@ -46,6 +46,22 @@ committed multi-seed record of exactly this config (scripts/solve.py).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+``--gpus N`` > 1 without torchrun's WORLD_SIZE in the environment launches its own N ranks (like the reference's
+auto_run.sh:6-14, which starts every process of its cluster itself): ``torch.distributed.run`` on 127.0.0.1 as a
+CHILD process, started before this process imports torch or touches the GPU; rank 0's JSON line goes straight to
+this process's stdout and the exit code is the launcher's.  Under torchrun, a WORLD_SIZE different from ``--gpus``
+is an error (exit 2), so an N-GPU record can never come from a different number of ranks.
+
+Per-rank strong-scaling shapes (one GPU): the 1-GPU run also times the per-rank shapes of the strong-scaling
+split, P_total / N paths x E envs for N = 2, 4, 8 (3 windows each), and reports ``strong_scaling.per_rank`` with a
+predicted seconds-to-solve per N: committed one-GPU updates-to-solve x (measured per-rank ms + a modelled ring
+all-reduce of the gradient over xGMI).  A prediction, labelled as one.
+
+Build provenance: on one GPU, a cold build of every csrc/*.hip into a scratch directory runs in a niced background
+process during the run (``python -m pathnet_gym_amd._build --verify``); ``build.verified`` reports whether the cold
+objects and library are byte-identical to the loaded ones (the build is reproducible: explicit compilation-unit
+ids, relative paths).
 """
 from __future__ import annotations
 
@@ -221,6 +237,97 @@ def committed_updates_to_solve(key: dict) -> list:
     return sorted(int(round(r["frames"] / per_update)) for r in rec.get("runs", []) if r["solved"] and r["frames"])
 
 
+def self_launch(n: int) -> int:
+    """``--gpus N`` > 1 outside torchrun: run ``torch.distributed.run --nproc-per-node N`` on 127.0.0.1 over this same
+    command line as a child process (this process never imports torch or touches the GPU) and return its exit code.
+    The ranks inherit stdout, so rank 0's JSON line is this process's only stdout line."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC only on this host driver (RCCL peer access)
+    print(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def start_build_verify():
+    """Cold-build every source in a niced background process (build provenance; collected by finish_build_verify)."""
+    import subprocess
+    import tempfile
+    out = tempfile.NamedTemporaryFile("w+", suffix=".json", delete=False)
+    cmd = ["nice", "-n", "19", sys.executable, "-m", "pathnet_gym_amd._build", "--verify", "--jobs", "8"]
+    p = subprocess.Popen(cmd, stdout=out, stderr=subprocess.STDOUT, cwd=os.path.dirname(os.path.abspath(__file__)))
+    return p, out, time.time()
+
+
+def finish_build_verify(h, wait_s: float = 240.0) -> dict:
+    p, out, t0 = h
+    try:
+        p.wait(timeout=wait_s)
+    except Exception:
+        p.kill()
+        p.wait()
+        return {"status": f"not finished {wait_s:.0f} s after the run (killed)"}
+    out.seek(0)
+    lines = [l for l in out.read().splitlines() if l.startswith("{")]
+    os.unlink(out.name)
+    if p.returncode != 0 or not lines:
+        return {"status": f"failed (rc {p.returncode})"}
+    d = json.loads(lines[-1])
+    d["status"] = "ok"
+    return d
+
+
+# modelled ring all-reduce of the fp32 gradient over xGMI (per-rank strong-scaling prediction on one GPU): RCCL ring,
+# 2 (N - 1) steps of ALLREDUCE_STEP_US latency plus 2 (N - 1) / N x bytes at ALLREDUCE_BUS_GBS bus bandwidth.  A
+# model, not a measurement (no multi-GPU node here); the overlapped exchange hides part of it behind the first
+# layer's weight gradient, which the model ignores (conservative).
+ALLREDUCE_STEP_US = 10.0
+ALLREDUCE_BUS_GBS = 150.0
+
+
+def allreduce_model_ms(n: int, nbytes: int) -> float:
+    if n <= 1:
+        return 0.0
+    return (2 * (n - 1) * ALLREDUCE_STEP_US * 1e-6 + 2.0 * (n - 1) / n * nbytes / (ALLREDUCE_BUS_GBS * 1e9)) * 1e3
+
+
+def per_rank_shapes(args, ctx, numel: int, upd: list, headline_ms: float) -> dict:
+    """One GPU: time the per-rank shape of the strong-scaling split for each N in --per-rank-shapes --
+    paths_total / N paths x E envs, with the GA taking the whole population's paths_total / 16 concurrent
+    tournaments -- in ``--windows`` windows, and predict seconds-to-solve on N GPUs from it."""
+    import torch
+    out = {}
+    med = upd[len(upd) // 2] if upd else None
+    for n in [int(x) for x in str(args.per_rank_shapes).split(",") if x.strip()]:
+        if n <= 1 or args.paths_total % n:
+            continue
+        a = argparse.Namespace(**vars(args))
+        a.paths = args.paths_total // n
+        a.concurrent = args.concurrent or max(1, args.paths_total // 16)
+        _, trn = build_trainer(a, ctx, args.dtype, not args.no_stagger)
+        w = window_summary(timed_windows(trn, ctx, args.steps, args.warmup, args.windows), args.steps)
+        del trn
+        torch.cuda.empty_cache() if torch.cuda.is_available() else None
+        ar = allreduce_model_ms(n, 4 * numel)
+        r = {"paths_per_gpu": a.paths, "envs_per_path": args.envs, "ms_per_update": round(w["ms"], 3),
+             "windows_ms": w["all"], "spread_pct": w["spread_pct"], "allreduce_model_ms": round(ar, 3),
+             "predicted_speedup_vs_1gpu": round(headline_ms / (w["ms"] + ar), 2)}
+        if med:
+            r["predicted_seconds_to_solve"] = round(med * (w["ms"] + ar) / 1e3, 1)
+        out[str(n)] = r
+    return {"measured_on": "1 GPU, each per-rank shape run alone", "by_n_gpus": out,
+            "allreduce_model": f"ring: 2(N-1) x {ALLREDUCE_STEP_US:g} us + 2(N-1)/N x {4 * numel} B at "
+                               f"{ALLREDUCE_BUS_GBS:g} GB/s bus bandwidth (modelled, not measured)",
+            "prediction": "median committed one-GPU updates-to-solve x (measured per-rank ms/update + modelled "
+                          "all-reduce); strong mode computes the one-GPU GA and summed gradient, so it needs the same "
+                          "updates.  A prediction, not a measured multi-GPU solve"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -266,8 +373,22 @@ def main():
     ap.add_argument("--prof-window", action="store_true",
                     help="launch marker kernels around the first timed window (scripts/prof_window.py summarises the "
                          "rocprofv3 kernel trace between them)")
+    ap.add_argument("--per-rank-shapes", default="2,4,8",
+                    help="one GPU: also time the strong-scaling per-rank shapes paths_total/N for these N ('' = off)")
+    ap.add_argument("--no-verify-build", action="store_true",
+                    help="skip the background cold build that checks the loaded library against the sources")
     args = ap.parse_args()
     t_start = time.time()
+    ws_env = os.environ.get("WORLD_SIZE")
+    if ws_env is None and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
+    if ws_env is not None and int(ws_env) != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={ws_env}: refusing to report an {args.gpus}-GPU record from "
+              f"{ws_env} ranks", file=sys.stderr, flush=True)
+        sys.exit(2)
+    verify_h = None
+    if args.backend == "hip" and int(ws_env or 1) == 1 and not args.no_verify_build and not args.prof_window:
+        verify_h = start_build_verify()
 
     import torch
 
@@ -352,6 +473,7 @@ def main():
         rec["build"] = build_info
     if getattr(tr, "precision_note", None):
         rec["precision_note"] = tr.precision_note
+    tr_numel = int(tr.model.store.layout.numel)
     del tr
     if compare:
         _, trb = build_trainer(args, ctx, "bf16", stagger, paths_total=head_total)
@@ -383,8 +505,11 @@ def main():
             strong["committed_updates_to_solve_1gpu"] = upd
             strong["predicted_seconds_to_solve"] = round(med * strong["ms_per_update"] / 1e3, 1)
             strong["prediction"] = ("median committed one-GPU updates-to-solve of this config x the measured strong-"
-                                    "scaling ms/update (the strong run computes the one-GPU run's GA and summed "
-                                    "gradient, so it needs the same updates); a prediction, not a measured solve")
+                                    "scaling ms/update on these n_gpus (the strong run computes the one-GPU run's GA "
+                                    "and summed gradient, so it needs the same updates); a prediction, not a measured "
+                                    "solve")
+        if world == 1 and args.scaling == "weak" and args.per_rank_shapes and args.paths == args.paths_total:
+            strong["per_rank"] = per_rank_shapes(args, ctx, tr_numel, upd, ws["ms"])
         rec["strong_scaling"] = strong
     # the metric's second half: one seed observed in this run (one GPU: the bench config; several GPUs: the strong
     # config, whose updates are what more GPUs shorten), plus every committed multi-seed record of this config
@@ -402,6 +527,8 @@ def main():
             rec["strong_scaling"]["in_run_solve"] = r
         else:
             rec["generations_to_solve_in_run"] = r
+    if verify_h is not None:
+        rec.setdefault("build", {})["verified"] = finish_build_verify(verify_h)
     if ctx.is_main:
         rec["generations_to_solve"] = solve_records(key, world)
         print(json.dumps(rec), flush=True)

@@ -12,7 +12,8 @@
 //                                      forward), K * 2^8; three f16 MFMAs, so 22 significant bits on both operands
 // Per-layer error against a plain fp32 oracle: tests/test_x3_engine.py (<= 2e-5, like the trunk).
 // Range: an input of the forward GEMM at or beyond fp16's 65504, or a kernel weight whose 2^8 multiple reaches
-// 32768, sets the engine's fp32x status word (bits 2 / 1, X3RangeError on the host).
+// 32768, sets the engine's fp32x status word (value 2: an fp16-pair state overflow; value 1: a scaled LSTM kernel weight
+// overflow -- the same bit as a trunk weight; X3RangeError on the host).
 #include "common.h"
 
 namespace lstmx3 {

@@ -171,5 +171,5 @@ class CounterPopulation(Population):
         super().load_state_dict(d)
         if "slots" in d:
             self.slots = np.asarray(d["slots"]).astype(np.int64)
-            self.draw_round = int(np.asarray(d["draw_round"]))
+            self.draw_round = int(np.asarray(d["draw_round"]).reshape(-1)[0])
             self.candidates = [list(map(int, r)) for r in self.slots if r[0] >= 0]

@@ -392,6 +392,7 @@ class PathNetTrainer:
         optimizer step (the last one) is read here, so it reaches the guard too."""
         pending = getattr(self, "_pending", None)
         self._pending = None
+        self._check_x3_refresh()
         if pending is None:
             return None
         st = self._collect(pending)
@@ -400,6 +401,20 @@ class PathNetTrainer:
             if self._guard_opt(float(self.engine.opt_status), u):
                 st.skipped, st.skipped_update = True, u
         return st
+
+    def _check_x3_refresh(self):
+        """fp32x: fold the range flags raised since the last rollout (the weight refresh of the last optimizer
+        step) and raise X3RangeError now -- all-reduced, so every rank raises together -- instead of one update
+        late (flush runs at task end and before every checkpoint: no checkpoint holds out-of-range weights)."""
+        if self.engine is None or not self.model.hip.x3:
+            return
+        out = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.model.hip.fold_x3_status(out)
+        self.ctx.all_reduce_(out)
+        v = float(out.item())
+        if v != 0.0:
+            from ..runtime.guard import X3RangeError
+            raise X3RangeError(v, self.updates, self.ctx.world)
 
     def _finish_update(self, fit_all, csum, losses, skip, step_at) -> UpdateStats:
         tr = self.tracer

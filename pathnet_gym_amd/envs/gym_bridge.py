@@ -103,8 +103,13 @@ class GymVecEnv(VecEnv):
         self.gray = gray
         self.id = env_id
         self.seed_int = int(seed) & 0xFFFFFFFF
-        self.rng = np.random.RandomState(self.seed_int)
-        first = np.asarray(_reset(self.envs[0], self.seed_int))
+        # global index of envs[0] (trainer: rank * P * E, VecEnv.set_id_base): env i is seeded with
+        # seed + id_base + i and draws its no-op starts from its own RNG keyed by (seed, id_base + i), so the
+        # ranks of a sharded population never replay each other's emulator seeds or no-op counts (the
+        # reference gives every worker its own rand_seed, a3c_training_thread.py:81)
+        self.id_base = 0
+        self._make_rngs()
+        first = np.asarray(_reset(self.envs[0], self._env_seed(0)))
         self.pixels = first.ndim == 3 and first.shape[-1] == 3 and first.dtype == np.uint8
         # the reference plays randint(0, no_op_max) no-ops after every reset, no_op_max = action count
         self.no_op_max = (self.num_actions if self.pixels else 0) if no_op_max is None else int(no_op_max)
@@ -133,6 +138,20 @@ class GymVecEnv(VecEnv):
         self.reset()
 
     # -- host side ------------------------------------------------------------
+    def _env_seed(self, i: int) -> int:
+        return (self.seed_int + self.id_base + i) & 0xFFFFFFFF
+
+    def _make_rngs(self):
+        self.rngs = [np.random.RandomState([self.seed_int, (self.id_base + i) & 0xFFFFFFFF])
+                     for i in range(self.num_envs)]
+
+    def set_id_base(self, base: int):
+        """Shard this bridge as global envs [base, base + N): re-key the seeds and no-op RNGs; the next reset()
+        re-seeds every env (the constructor's reset of env 0 used the unsharded seed)."""
+        self.id_base = int(base)
+        self._make_rngs()
+        self._first = None
+
     def _write(self, i: int, obs):
         o = np.asarray(obs)
         if self.pixels:
@@ -145,7 +164,7 @@ class GymVecEnv(VecEnv):
         if i == 0:
             self._first = None
         if self.no_op_max > 0:
-            for _ in range(self.rng.randint(0, self.no_op_max + 1)):      # game_state.py:57-60
+            for _ in range(self.rngs[i].randint(0, self.no_op_max + 1)):      # game_state.py:57-60
                 obs, _, done, _ = _step(self.envs[i], 0)
                 if done:
                     obs = _reset(self.envs[i], None)
@@ -182,12 +201,12 @@ class GymVecEnv(VecEnv):
     # -- VecEnv API -----------------------------------------------------------
     def seed(self, seed: int):
         self.seed_int = int(seed) & 0xFFFFFFFF
-        self.rng = np.random.RandomState(self.seed_int)
+        self._make_rngs()
 
     def reset(self):
         self._host_ready()
         for i in range(self.num_envs):
-            self._write(i, self._reset_env(i, self.seed_int + i))
+            self._write(i, self._reset_env(i, self._env_seed(i)))
         self._upload()
         if self.pixels:
             allm = torch.ones(self.num_envs, dtype=torch.uint8, device=self.device)

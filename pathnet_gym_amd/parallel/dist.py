@@ -102,8 +102,12 @@ def init_distributed(device: Optional[str] = None, backend: Optional[str] = None
     # PATHNET_DIST_BACKEND=gloo lets several ranks share one GPU (test rehearsal); default RCCL ("nccl")
     be = backend or os.environ.get("PATHNET_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if world <= 1:
-        os.environ.setdefault("MASTER_PORT", "29531")
+    if world <= 1 and "MASTER_PORT" not in os.environ:
+        # a forced one-rank group: bind port 0 for a free port, so concurrent forced jobs on one box do not collide
+        import socket
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            s.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(s.getsockname()[1])
     if not dist.is_initialized():
         if be == "nccl":
             dist.init_process_group(be, rank=rank, world_size=world, device_id=dev)

@@ -33,9 +33,15 @@ class NonFiniteError(RuntimeError):
 
 
 class X3RangeError(FloatingPointError):
-    """fp32x (split fp16 pairs): a value left the fp16 range.  Bit 0 of the status: a first-layer weight scaled by
-    2^8 reached 32768 (its pair no longer represents it); bit 1: an activation written as an fp16 pair reached 65504.
-    The status travels in the update's all-reduced counters, so every rank raises together."""
+    """fp32x (split fp16 pairs): a value left the fp16 range.  Bit 0 (value 1) of the status: a weight scaled by
+    2^8 -- of any trunk layer (x3_refresh_weights) or the LSTM kernel (lstm_refresh_x3) -- reached 32768 (its pair
+    no longer represents it); bit 1 (value 2): an activation written as an fp16 pair (trunk or LSTM state) reached
+    65504.  The status travels in the update's all-reduced counters, so every rank raises together.
+
+    Lag: the flags are folded into the counters after each rollout, so an overflow raised by the weight refresh at
+    the end of update u surfaces with update u + 1.  ``PathNetTrainer.flush()`` (called at task end and before every
+    checkpoint) folds and checks the flags of the last refresh too, so no checkpoint is written over out-of-range
+    weights."""
 
     def __init__(self, status: float, update: int, world: int = 1):
         self.status = status
@@ -45,7 +51,7 @@ class X3RangeError(FloatingPointError):
             what.append(f"status sum {status:g} over {world} ranks")
         else:
             if bits & 1:
-                what.append("a first-layer weight x 2^8 left the fp16 range (|W| >= 128)")
+                what.append("a weight x 2^8 (a trunk layer or the LSTM kernel) left the fp16 range (|W| >= 128)")
             if bits & 2:
                 what.append("an activation stored as an fp16 pair reached 65504")
         super().__init__(f"fp32x range overflow at update {update}: " + "; ".join(what)

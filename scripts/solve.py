@@ -33,7 +33,9 @@ def main():
     ap.add_argument("--checkpoint", default=None, help="save the trainer here at the end (and every --ckpt-minutes)")
     ap.add_argument("--ckpt-minutes", type=float, default=0.0)
     ap.add_argument("--resume", action="store_true",
-                    help="continue from --checkpoint (exact resume: weights, optimizer, GA, envs, RNG counters); the "
+                    help="continue from --checkpoint (continuation resume, not bit-exact: weights, optimizer, GA and RNG "
+                         "counters restored; light checkpoints rebuild each env's frame stack from its current frame "
+                         "and, at momentum 0, hold no momentum slots); the "
                          "record's seconds / segments accumulate over the resumed runs (read back from --out)")
     ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--tmax", type=int, default=None)

@@ -36,3 +36,31 @@ def test_bench_two_rank_gloo_json_contract(tmp_path):
     assert s["paths_total"] == 64 and s["paths_per_gpu"] == 32 and s["n_gpus"] == 2 and s["ms_per_update"] > 0
     r = s["in_run_solve"]
     assert r["paths_total"] == 64 and r["paths_per_gpu"] == 32 and r["updates_run"] > 0
+
+
+def test_bench_gpus_flag_self_launches_its_ranks(tmp_path):
+    """``bench.py --gpus 2`` outside torchrun starts its own 2 ranks (torch.distributed.run as a child, 127.0.0.1) and
+    relays rank 0's single JSON line: n_gpus 2, with the strong-scaling windows and in-run solve of a multi-GPU run."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "torch", "--preset",
+           "cartpole-cpu", "--paths", "4", "--envs", "16", "--tmax", "5", "--steps", "2", "--warmup", "1",
+           "--windows", "1", "--ga-backend", "host", "--solve-seconds", "20"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"].startswith("dp2")
+    s = d["strong_scaling"]
+    assert s["n_gpus"] == 2 and s["paths_per_gpu"] == 32 and s["ms_per_update"] > 0
+    assert s["in_run_solve"]["updates_run"] > 0
+
+
+def test_bench_refuses_a_world_size_that_differs_from_gpus(tmp_path):
+    """Under torchrun (WORLD_SIZE set), --gpus must equal the world size: exit 2 before any torch import."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--backend", "torch"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr and not r.stdout.strip()

@@ -95,6 +95,33 @@ def test_pixel_bridge_matches_reference_preprocessing():
         assert np.allclose(obs.numpy().astype(np.float32) / 255.0, np.stack(stacks), atol=1e-6)
 
 
+def test_sharded_bridge_reproduces_the_unsharded_envs():
+    """Two ranks owning envs [0, 2) and [2, 4) (set_id_base, as the trainer does with rank * P * E) see exactly the
+    seeds, no-op starts and trajectories of one 4-env bridge, and the two ranks' envs differ from each other."""
+    def catch_env(n, base):
+        e = GymVecEnv([PyCatch(balls=3, speed=30) for _ in range(n)], seed=11, no_op_max=4)
+        e.set_id_base(base)
+        return e, e.reset().clone()
+    whole, o_whole = catch_env(4, 0)
+    r0, o0 = catch_env(2, 0)
+    r1, o1 = catch_env(2, 2)
+    assert torch.equal(torch.cat([o0, o1]), o_whole)
+    assert not torch.equal(o0, o1)
+    for t in range(15):
+        a = torch.tensor([t % 3, 1, 2, (t + 2) % 3])
+        ow, rw, dw, iw = whole.step(a)
+        oa, ra, da, ia = r0.step(a[:2])
+        ob, rb, db, ib = r1.step(a[2:])
+        assert torch.equal(torch.cat([oa, ob]), ow) and torch.equal(torch.cat([da, db]), dw)
+        assert torch.equal(torch.cat([ia["episode_return"], ib["episode_return"]]), iw["episode_return"])
+    # vector obs: rank 1's first env is seeded as global env 2
+    v = GymVecEnv([PyCartPole() for _ in range(2)], seed=7)
+    v.set_id_base(2)
+    ref = PyCartPole()
+    ref.seed(7 + 2)
+    assert np.allclose(v.reset()[0].numpy(), ref.reset())
+
+
 def test_trainer_learns_cartpole_through_the_bridge():
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     from pathnet_gym_amd.config import preset
