@@ -254,13 +254,21 @@ def self_launch(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def under_profiler() -> bool:
+    """rocprofv3 (or another tool) preloads a library that initialises the GPU in every process it enters, so a
+    child started from here would count as an exec after GPU initialisation: no background build then."""
+    return "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def start_build_verify():
-    """Cold-build every source in a niced background process (build provenance; collected by finish_build_verify)."""
+    """Cold-build every source in a background child process at the lowest CPU priority (build provenance; collected
+    by finish_build_verify).  The child is this interpreter itself (no `nice` / shell hop in between)."""
     import subprocess
     import tempfile
     out = tempfile.NamedTemporaryFile("w+", suffix=".json", delete=False)
-    cmd = ["nice", "-n", "19", sys.executable, "-m", "pathnet_gym_amd._build", "--verify", "--jobs", "8"]
-    p = subprocess.Popen(cmd, stdout=out, stderr=subprocess.STDOUT, cwd=os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "pathnet_gym_amd._build", "--verify", "--jobs", "8"]
+    p = subprocess.Popen(cmd, stdout=out, stderr=subprocess.STDOUT, cwd=os.path.dirname(os.path.abspath(__file__)),
+                         preexec_fn=lambda: os.nice(19))
     return p, out, time.time()
 
 
@@ -365,7 +373,7 @@ def main():
                     help="start every env at 0-0 (default: random late scores, so tournaments fire inside the window)")
     ap.add_argument("--solve-seconds", type=float, default=None,
                     help="after the timed windows, run one generations-to-solve seed on a fresh trainer for at most "
-                         "this long (default: one GPU, the bench config, what is left of a 540 s run, at most 420 s; "
+                         "this long (default: one GPU, the bench config, what is left of a 560 s run, at most 480 s; "
                          "several GPUs, the strong-scaling config, what is left of 480 s, at most 300 s; 0 = off)")
     ap.add_argument("--compare-bf16", type=int, default=None,
                     help="also time the bf16 engine on the same config (default: on for one GPU)")
@@ -387,7 +395,8 @@ def main():
               f"{ws_env} ranks", file=sys.stderr, flush=True)
         sys.exit(2)
     verify_h = None
-    if args.backend == "hip" and int(ws_env or 1) == 1 and not args.no_verify_build and not args.prof_window:
+    if args.backend == "hip" and int(ws_env or 1) == 1 and not args.no_verify_build and not args.prof_window \
+            and not under_profiler():
         verify_h = start_build_verify()
 
     import torch
@@ -515,9 +524,10 @@ def main():
     # config, whose updates are what more GPUs shorten), plus every committed multi-seed record of this config
     solve_s = args.solve_seconds
     if solve_s is None:
-        # one GPU: up to 420 s within a 540 s run; several: the strong config solves in ~20-34 K updates of a few ms,
+        # one GPU: up to 480 s within a 560 s run (seed 1 needs 34-40 K updates of ~10.6 ms); several: the strong config
+        # solves in ~20-40 K updates of a few ms,
         # so up to 300 s within a 480 s run
-        cap, budget = (420.0, 540.0) if world == 1 else (300.0, 480.0)
+        cap, budget = (480.0, 560.0) if world == 1 else (300.0, 480.0)
         solve_s = cap if (single or (world > 1 and strong is not None)) else 0.0
         solve_s = max(0.0, min(solve_s, budget - ctx.max_scalar(time.time() - t_start)))
     if solve_s > 0:

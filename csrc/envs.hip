@@ -413,6 +413,58 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   PONG_STAMP(4);
 }
 
+// Frame ring, small populations: the env step as two launches -- physics (one wave per env) and the render split
+// over `split` workgroups per env (each builds the scene tables and renders 1/split of the quads).  The fused kernel
+// is one workgroup per env, so at B = 256 envs (8 paths x 32) its ~20 us per-workgroup critical path (physics,
+// scene tables, 19 quads per thread) is the whole step; the split shortens the render walk and takes the physics
+// off the render's path.  Same physics, same pixels (bit-identical to pong_step_kernel<true>).
+__global__ __launch_bounds__(64) void pong_physics_kernel(int* __restrict__ state, uint32_t* __restrict__ counter,
+                                                         const int* __restrict__ actions, int n_actions,
+                                                         float* __restrict__ reward_out, uint8_t* __restrict__ done_out,
+                                                         float* __restrict__ epret_out, uint32_t seed, int frameskip,
+                                                         int max_steps, int no_op_max, const uint8_t* __restrict__ fc_in,
+                                                         uint8_t* __restrict__ fc_out, uint32_t id_base) {
+  __shared__ int phys[pong::NSTATE + 4];
+  pong::physics_wave0((int)blockIdx.x, state, counter, actions, n_actions, seed, frameskip, max_steps, no_op_max, phys,
+                      reward_out, done_out, epret_out, fc_in, fc_out, id_base);
+}
+
+__global__ __launch_bounds__(256, 8) void pong_render_ring_kernel(const int* __restrict__ state,
+                                                                 const int* __restrict__ tables,
+                                                                 uint8_t* __restrict__ frame_out, long out_stride,
+                                                                 int split, int g_bg, int g_wall, int g_cpu,
+                                                                 int g_player, int g_ball) {
+  using namespace pong;
+  __shared__ __attribute__((aligned(16))) int tab[8 * 160];
+  __shared__ int rowinfo[OBS_H];
+  __shared__ __attribute__((aligned(16))) int colmask[OBS_W];
+  __shared__ int quadmask[OBS_W / 4];
+  __shared__ uint8_t band[BAND_R * BAND_C];
+  __shared__ __attribute__((aligned(4))) uint8_t dlut[DL_R * 48];
+  const int env = (int)blockIdx.y;
+  for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
+  St st;
+#pragma unroll
+  for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
+  __syncthreads();                                   // tab[] staged
+  Scene S;
+  scene_tables<256>(st, S, tab, rowinfo, colmask, quadmask, band, dlut, g_bg, g_wall, g_cpu, g_player, g_ball);
+  constexpr int NQ = OBS_H * OBS_W / 4, QR = OBS_W / 4;
+  const int per = (NQ + split - 1) / split;
+  const int q0 = (int)blockIdx.x * per, q1 = min(NQ, q0 + per);
+  uint32_t* outw = reinterpret_cast<uint32_t*>(frame_out + (long)env * out_stride);
+  int q = q0 + (int)threadIdx.x;
+  int y = q / QR, xq = q - (q / QR) * QR;
+  for (; q < q1; q += 256) {
+    uint32_t f4[4];
+    quad_gray(S, y, xq, rowinfo[y], tab, colmask, quadmask, dlut, f4);
+    outw[q] = f4[0] | (f4[1] << 8) | (f4[2] << 16) | (f4[3] << 24);
+    xq += 16;
+    y += 8;
+    if (xq >= QR) { xq -= QR; ++y; }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // CartPole-v1: thread per env. state [B][4] f32, steps [B] i32, epret [B] f32,
 // counter [B] u32; writes obs bf16 [B][8] (zero padded) for the trunk.
@@ -499,6 +551,30 @@ int launch_pong_step_ring(void* state, void* counter, const int* actions, int n_
                                                 frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu, g_player,
                                                 g_ball, (const uint8_t*)fc_in, (uint8_t*)fc_out, out_stride, 0,
                                                 id_base);
+  return (int)hipGetLastError();
+}
+
+// the same step as launch_pong_step_ring in two launches (physics, then the render over `split` workgroups per env);
+// split <= 1: the fused kernel
+int launch_pong_step_ring_split(void* state, void* counter, const int* actions, int n_actions, void* frame_out,
+                                long out_stride, const void* fc_in, void* fc_out, const int* tables, float* reward,
+                                void* done, float* epret, int B, unsigned seed, int frameskip, int max_steps,
+                                int no_op_max, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
+                                unsigned id_base, int split, hipStream_t stream) {
+  if (split <= 1)
+    return launch_pong_step_ring(state, counter, actions, n_actions, frame_out, out_stride, fc_in, fc_out, tables,
+                                 reward, done, epret, B, seed, frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu,
+                                 g_player, g_ball, id_base, stream);
+  if (n_actions <= 0 || out_stride <= 0 || B <= 0 || frameskip < 0 || max_steps < 0 || no_op_max < 0 || g_bg < 0 ||
+      g_wall < 0 || g_cpu < 0 || g_player < 0 || g_ball < 0 || split > 64 || !fc_in || !fc_out) return -22;
+  if (out_stride < 160 * 120 || out_stride % 16) return -22;
+  pong_physics_kernel<<<B, 64, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions, reward,
+                                            (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max,
+                                            (const uint8_t*)fc_in, (uint8_t*)fc_out, id_base);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  pong_render_ring_kernel<<<dim3((unsigned)split, (unsigned)B), 256, 0, stream>>>(
+      (const int*)state, tables, (uint8_t*)frame_out, out_stride, split, g_bg, g_wall, g_cpu, g_player, g_ball);
   return (int)hipGetLastError();
 }
 

@@ -980,21 +980,28 @@ struct FT3 {
 
 // PAIR: a wave computes two position tiles (rt, rt + 4) per weight-fragment read (one tile per read left the
 // kernel bound by LDS reads, as the first conv1 band kernel was)
-template <class G, bool PAIR = false>
-__global__ __launch_bounds__(256, 2) void conv_fwd_tile_x3(const uint16_t* __restrict__ X, long xlo,
-                                                          uint16_t* __restrict__ Y, long ylo,
-                                                          uint8_t* __restrict__ bits, const uint16_t* __restrict__ Wc,
-                                                          long wlo, const float* __restrict__ flat, long bias_off,
-                                                          int chunk, const int* __restrict__ act_idx,
-                                                          const int* __restrict__ act_cnt, int layer, int L, int M,
-                                                          int P, int E, int T, int t0, long bits_rows,
-                                                          int samples_per_wg, float in_scale, float out_scale) {
+// LDS of one layer's tile forward: the sample's input planes and the staged weight pairs (conv_fwd_tile_body)
+template <class G>
+struct TileLds {
+  static constexpr int KPs = G::KP + 8;
+  static constexpr int XT = FT3<G>::TILEP;           // u16 per input plane
+  static constexpr int WS = 2 * 16 * KPs;            // u16 per weight plane
+  static constexpr int BYTES = (2 * XT + 2 * WS) * 2;
+};
+
+template <class G, bool PAIR>
+DEVI void conv_fwd_tile_body(const uint16_t* __restrict__ X, long xlo, uint16_t* __restrict__ Y, long ylo,
+                             uint8_t* __restrict__ bits, const uint16_t* __restrict__ Wc, long wlo,
+                             const float* __restrict__ flat, long bias_off, int chunk,
+                             const int* __restrict__ act_idx, const int* __restrict__ act_cnt, int layer, int L, int M,
+                             int P, int E, int T, int t0, long bits_rows, int samples_per_wg, float in_scale,
+                             float out_scale, uint16_t* __restrict__ lds, float* __restrict__ bias_s,
+                             int* __restrict__ mods) {
   using F = FT3<G>;
+  using TL = TileLds<G>;
   constexpr int KPs = G::KP + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t Xt[2][F::TILEP];
-  __shared__ __attribute__((aligned(16))) uint16_t Ws[2][2 * 16 * KPs];
-  __shared__ __attribute__((aligned(16))) float bias_s[2 * 16];
-  __shared__ int mods[X3_MAXM];
+  uint16_t* const Xt[2] = {lds, lds + TL::XT};
+  uint16_t* const Ws[2] = {lds + 2 * TL::XT, lds + 2 * TL::XT + TL::WS};
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
   const int nct = (cnt + 1) >> 1;
@@ -1139,6 +1146,54 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tile_x3(const uint16_t* __res
     if (ncg == 1) run(std::integral_constant<int, 1>{});
     else run(std::integral_constant<int, 2>{});
   }
+}
+
+template <class G, bool PAIR = false>
+__global__ __launch_bounds__(256, 2) void conv_fwd_tile_x3(const uint16_t* __restrict__ X, long xlo,
+                                                          uint16_t* __restrict__ Y, long ylo,
+                                                          uint8_t* __restrict__ bits, const uint16_t* __restrict__ Wc,
+                                                          long wlo, const float* __restrict__ flat, long bias_off,
+                                                          int chunk, const int* __restrict__ act_idx,
+                                                          const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                          int P, int E, int T, int t0, long bits_rows,
+                                                          int samples_per_wg, float in_scale, float out_scale) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[TileLds<G>::BYTES / 2];
+  __shared__ __attribute__((aligned(16))) float bias_s[2 * 16];
+  __shared__ int mods[X3_MAXM];
+  conv_fwd_tile_body<G, PAIR>(X, xlo, Y, ylo, bits, Wc, wlo, flat, bias_off, chunk, act_idx, act_cnt, layer, L, M, P,
+                              E, T, t0, bits_rows, samples_per_wg, in_scale, out_scale, lds, bias_s, mods);
+}
+
+// The 4x4/s2 and 3x3/s1 layers' forwards in ONE launch: a workgroup runs conv_fwd_tile_body for layer `layer` over
+// its samples (writing Y1 and its ReLU bits as the conv2 kernel does), then -- the same samples, so no other workgroup
+// is involved -- layer + 1 reading those Y1 rows back (L2-hot), into Y2.  A device-scope fence between the phases
+// makes this workgroup's Y1 stores visible to its own loads (it also invalidates the CU's L1).  Saves a launch and the
+// second kernel's ramp per rollout step; same arithmetic as the two launches (bit-identical).
+template <class G1, class G2, bool PAIR1>
+__global__ __launch_bounds__(256, 2) void conv23_fwd_tile_x3(const uint16_t* __restrict__ X, long xlo,
+                                                            uint16_t* __restrict__ Y1, long y1lo,
+                                                            uint8_t* __restrict__ bits1, long bits_rows1,
+                                                            const uint16_t* __restrict__ Wc1, long w1lo,
+                                                            long bias1_off, int chunk1,
+                                                            uint16_t* __restrict__ Y2, long y2lo,
+                                                            uint8_t* __restrict__ bits2, long bits_rows2,
+                                                            const uint16_t* __restrict__ Wc2, long w2lo,
+                                                            long bias2_off, int chunk2, const float* __restrict__ flat,
+                                                            const int* __restrict__ act_idx,
+                                                            const int* __restrict__ act_cnt, int layer, int L, int M,
+                                                            int P, int E, int T, int t0, int samples_per_wg,
+                                                            float in_scale, float out_scale1, float out_scale2) {
+  constexpr int B1 = TileLds<G1>::BYTES, B2 = TileLds<G2>::BYTES;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[(B1 > B2 ? B1 : B2) / 2];
+  __shared__ __attribute__((aligned(16))) float bias_s[2 * 16];
+  __shared__ int mods[X3_MAXM];
+  conv_fwd_tile_body<G1, PAIR1>(X, xlo, Y1, y1lo, bits1, Wc1, w1lo, flat, bias1_off, chunk1, act_idx, act_cnt, layer, L,
+                                M, P, E, T, t0, bits_rows1, samples_per_wg, in_scale, out_scale1, lds, bias_s, mods);
+  __threadfence();
+  __syncthreads();
+  conv_fwd_tile_body<G2, false>(Y1, y1lo, Y2, y2lo, bits2, Wc2, w2lo, flat, bias2_off, chunk2, act_idx, act_cnt,
+                                layer + 1, L, M, P, E, T, t0, bits_rows2, samples_per_wg, in_scale, out_scale2, lds,
+                                bias_s, mods);
 }
 
 // ===========================================================================
@@ -3440,25 +3495,24 @@ __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict
                                                          int KP, int Cout, int M, uint16_t* __restrict__ Wc,
                                                          uint16_t* __restrict__ WcT, int f16,
                                                          uint32_t* __restrict__ status) {
+  // one 32 (k) x 64 (column) tile of one module per workgroup, transposed through LDS: the master weights are read
+  // and WcT ([M][KP][Cout], the flat order) written along the columns, Wc ([M][Cout][KP]) written along k -- both
+  // coalesced (the flat-order loop wrote Wc with a KP stride: 5 launches x ~16 us per update)
+  __shared__ float tile[32][65];
+  const int tk = (KP + 31) / 32, tc = (Cout + 63) / 64;
+  const int b = (int)blockIdx.x;
+  const int j = b / (tk * tc), rem = b - j * tk * tc;
+  const int kt = rem / tc, ct = rem - kt * tc;
+  if (j >= M) return;
   const long n = (long)M * KP * Cout;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const int j = (int)(i / ((long)KP * Cout));
-    const int rem = (int)(i - (long)j * KP * Cout);
-    const int k = rem / Cout, c = rem - k * Cout;
-    const float v = k < K ? flat[w_off + (long)j * chunk + (long)k * Cout + c] : 0.f;
-    const bf16_t bh = f2bf(v);
-    const bf16_t bl = f2bf(v - bf2f(bh));
-    uint16_t hi = bh, lo = bl;
-    if (f16) {
-      const float x = v * (float)(1 << X3_W0_SHIFT);
-      hi = f2h(x);
-      lo = f2h(x - h2f(hi));
-      if (!(fabsf(x) < 32768.f) && status) atomicOr(status, X3_RANGE_W);
-    }
-    const long wi = ((long)j * Cout + c) * KP + k;
-    Wc[wi] = hi;
-    Wc[n + wi] = lo;
-    if (WcT) {                       // the fc input gradient's B operand: fp16 pieces of W * 2^8 (meets G16 gradients)
+  const int t = (int)threadIdx.x;
+  bool bad = false;
+  for (int kk = t >> 6; kk < 32; kk += 4) {
+    const int k = kt * 32 + kk, c = ct * 64 + (t & 63);
+    const float v = (k < K && c < Cout) ? flat[w_off + (long)j * chunk + (long)k * Cout + c] : 0.f;
+    tile[kk][t & 63] = v;
+    if (WcT && k < KP && c < Cout) {  // the fc input gradient's B operand: fp16 pieces of W * 2^8 (meets G16 gradients)
+      const long i = ((long)j * KP + k) * Cout + c;
       const float x = v * (float)(1 << X3_W0_SHIFT);
       const uint16_t th = f2h(x);
       const float r = x - h2f(th);
@@ -3468,6 +3522,27 @@ __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict
       WcT[2 * n + i] = f2h(r - h2f(tl));           // third piece: W exact to 33 bits (X3_DG_W3)
     }
   }
+  __syncthreads();
+  for (int cc = t >> 5; cc < 64; cc += 8) {
+    const int k = kt * 32 + (t & 31), c = ct * 64 + cc;
+    if (k >= KP || c >= Cout) continue;
+    const float v = tile[t & 31][cc];
+    uint16_t hi, lo;
+    if (f16) {
+      const float x = v * (float)(1 << X3_W0_SHIFT);
+      hi = f2h(x);
+      lo = f2h(x - h2f(hi));
+      bad |= !(fabsf(x) < 32768.f);
+    } else {
+      const bf16_t bh = f2bf(v);
+      hi = bh;
+      lo = f2bf(v - bf2f(bh));
+    }
+    const long wi = ((long)j * Cout + c) * KP + k;
+    Wc[wi] = hi;
+    Wc[n + wi] = lo;
+  }
+  if (bad && status) atomicOr(status, X3_RANGE_W);
 }
 
 // one thread: out[0] = (float)(activation flags since the last fold | weight flags of the last refresh), both reset
@@ -3536,6 +3611,15 @@ static int X3_DG_W3 = 0;
 // fc input gradient: 1 = every k-step's MFMA products summed from zero and added to the running fp32 sum by a VALU add;
 // 2 = the same with odd k-steps on negated operands, subtracted (cancels the f16 MFMA's -inf rounding bias)
 static int X3_DG_FOLD = 2;
+// small populations: grid sizes follow P so a launch keeps ~2 rounds of workgroups when P shrinks (at the bench's
+// P = 64 these give the fixed sizes measured before).  Slab weight gradients: ~X3_WG_TARGET workgroups in total
+// (units per workgroup = units * P / target, >= 8); conv input gradients: ~X3_DG_TARGET (samples per workgroup >= 2);
+// 0 = the fixed per-path sizes (24 / 32 chunks per path).
+static int X3_WG_TARGET = 1536;
+static int X3_DG_TARGET = 2048;
+// module-major fc forward k split: 0 = auto by rows (P*T*E <= 256: 8 parts, else 2), else the fixed part count (2 / 4 /
+// 8), capped so every part keeps >= 2 k-steps
+static int X3_FC_KS_PARTS = 0;
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
 extern "C" {
@@ -3557,6 +3641,9 @@ void fast_conv_set_x3_c1_f16b(int v) { X3_C1_F16B = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
+void fast_conv_set_x3_wg_target(int v) { X3_WG_TARGET = v < 0 ? 0 : v; }
+void fast_conv_set_x3_dg_target(int v) { X3_DG_TARGET = v < 0 ? 0 : v; }
+void fast_conv_set_x3_fc_ks_parts(int v) { X3_FC_KS_PARTS = (v == 2 || v == 4 || v == 8) ? v : 0; }
 
 int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits, const void* Wc, long wlo,
                 const float* flat, long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M,
@@ -3672,6 +3759,37 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
   return rc ? -rc : 1;
 }
 
+// the 4x4/s2 and 3x3/s1 layers' forwards in one launch (conv23_fwd_tile_x3): layer `layer` (C2 geometry) reads X and
+// writes Y1 / bits1, layer + 1 (C3) reads Y1 and writes Y2 / bits2, over the same sample partition as the two
+// conv_fwd_tile_x3 launches
+int x3_conv23_fwd(const void* X, long xlo, void* Y1, long y1lo, void* bits1, long br1, const void* Wc1, long w1lo,
+                  long bias1_off, int chunk1, void* Y2, long y2lo, void* bits2, long br2, const void* Wc2, long w2lo,
+                  long bias2_off, int chunk2, const float* flat, const int* ai, const int* ac, int layer, int L, int M,
+                  int P, int E, int T, int t0, float os1, float os2, hipStream_t st) {
+  if (!X || !Y1 || !Y2 || !bits1 || !bits2 || !Wc1 || !Wc2 || !flat || !ai || !ac || xlo <= 0 || y1lo <= 0 ||
+      y2lo <= 0 || w1lo <= 0 || w2lo <= 0 || br1 <= 0 || br2 <= 0 || chunk1 <= 0 || chunk2 <= 0 || bias1_off < 0 ||
+      bias2_off < 0 || layer < 0 || layer + 1 >= L || M <= 0 || P <= 0 || E <= 0 || T <= 0 || t0 < 0) return -22;
+  if (M > 2 * X3_NCT || !X3_FWD_TILE) return 0;
+  if ((E * C2::HOWO) % 16 || (E * C3::HOWO) % 16) return -2;
+  const long nsamp = (long)T * E;
+  long spw = (nsamp * P + 511) / 512;
+  if (spw < 2) spw = 2;
+  const float isc = 1.f / (float)(1 << X3_W0_SHIFT);
+  const dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
+  if (X3_FWD_TILE == 2 || X3_FWD_TILE == 3)
+    conv23_fwd_tile_x3<C2, C3, true><<<grid, 256, 0, st>>>(
+        (const uint16_t*)X, xlo, (uint16_t*)Y1, y1lo, (uint8_t*)bits1, br1, (const uint16_t*)Wc1, w1lo, bias1_off, chunk1,
+        (uint16_t*)Y2, y2lo, (uint8_t*)bits2, br2, (const uint16_t*)Wc2, w2lo, bias2_off, chunk2, flat, ai, ac, layer, L,
+        M, P, E, T, t0, (int)spw, isc, os1, os2);
+  else
+    conv23_fwd_tile_x3<C2, C3, false><<<grid, 256, 0, st>>>(
+        (const uint16_t*)X, xlo, (uint16_t*)Y1, y1lo, (uint8_t*)bits1, br1, (const uint16_t*)Wc1, w1lo, bias1_off, chunk1,
+        (uint16_t*)Y2, y2lo, (uint8_t*)bits2, br2, (const uint16_t*)Wc2, w2lo, bias2_off, chunk2, flat, ai, ac, layer, L,
+        M, P, E, T, t0, (int)spw, isc, os1, os2);
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
 int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, const void* bits, float* grad, long w_off,
                         long b_off, int chunk, const int* ai, const int* ac, int L, int M, int P, int E, int T,
                         int nslots, long br, float is, float gs, const float* gamax, hipStream_t st) {
@@ -3680,7 +3798,7 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (M > 2 * X3_NCT) return 0;
   using SB = Slab<C1, 2>;
   const long units = (long)T * E * SB::NB;
-  long upw = (units + 23) / 24;
+  long upw = X3_WG_TARGET > 0 ? (units * P + X3_WG_TARGET - 1) / X3_WG_TARGET : (units + 23) / 24;
   if (upw < 8) upw = 8;
   if (upw / SB::NB + 2 > X3_RING_FCS) return -22;       // the workgroup's first-valid bytes fit the LDS table
   const dim3 grid((unsigned)((units + upw - 1) / upw), P);
@@ -3716,7 +3834,9 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     constexpr int OB = decltype(obc)::value;
     using SB = Slab<Gx, OB>;
     const long units = (long)T * E * SB::NB;
-    long upw = (units + 23) / 24;
+    // the P-scaled grid pays for the uint8 first layer (P = 8: 567 -> 305 us) but not for the 4x4/s2 layer
+    // (105 -> 126 us: its per-workgroup setup is a larger share of a shorter unit walk)
+    long upw = (X3_WG_TARGET > 0 && Gx::U8) ? (units * P + X3_WG_TARGET - 1) / X3_WG_TARGET : (units + 23) / 24;
     if (upw < 8) upw = 8;
     const dim3 grid((unsigned)((units + upw - 1) / upw), P);
     const int pf = Gx::U8 ? (X3_WGRAD_PF == 2 ? 2 : 1) : (X3_WGRAD_PF >= 2 ? 2 : 1);
@@ -3769,7 +3889,10 @@ int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_o
       E <= 0 || T <= 0 || br <= 0 || w_off < 0 || layer < 0 || !gamax) return -22;
   if (M > 2 * X3_NCT) return 0;
   const int nsamp = T * E;
-  int spw = (nsamp + 31) / 32;
+  // P-scaled grid for the 4x4/s2 layer's input gradient (P = 8: 127 -> 119 us); the 3x3 layer keeps 32 chunks per
+  // path (100 -> 110 us when scaled)
+  int spw = (X3_DG_TARGET > 0 && x3_is<C2>(Hin, Win, Cin, KH, KW, S, 0))
+                ? (int)(((long)nsamp * P + X3_DG_TARGET - 1) / X3_DG_TARGET) : (nsamp + 31) / 32;
   if (spw < 2) spw = 2;
   const dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
 #define DGX(Gx)                                                                                                    \
@@ -3846,7 +3969,10 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
   if (X3_FC_MMV >= 3) {
     // k split in KS (2, or 4 for X3_FC_MMV >= 4): partial planes Ys[KS][M][P*R][256], then bias + ReLU + bits +
     // slot sum in fc_slot_sum2_x3
-    const int ks = X3_FC_MMV >= 4 ? 4 : 2;
+    int ks = X3_FC_MMV >= 4 ? 4 : 2;
+    if (X3_FC_KS_PARTS > 0) ks = X3_FC_KS_PARTS;
+    else if (X3_FC_MMV == 3) ks = (long)P * R <= 256 ? 8 : 2;   // 8 paths: 21.4 + 5.8 -> 13.3 + 8.4 us; 16: none
+    while (ks > 2 && (KP / 32) / ks < 2) ks >>= 1;           // every part keeps >= 2 k-steps
     const int umax = (ks * M * 2 * ((P * R + 127) / 128) + 7) / 8 * 8;
     const unsigned g2 = (unsigned)(((long)P * R * 32 + 255) / 256);
 #define MM2KS(KS_)                                                                                                \
@@ -3868,7 +3994,7 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
         fc_slot_sum2_x3<false, KS_><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br,    \
                                                         layer, L, M, P, E, T, t0, Y, ylo, os);                     \
     }
-    if (ks == 4) MM2KS(4) else MM2KS(2)
+    if (ks == 8) MM2KS(8) else if (ks == 4) MM2KS(4) else MM2KS(2)
 #undef MM2KS
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
@@ -4015,11 +4141,10 @@ int x3_status_fold(void* wstatus, float* out, hipStream_t st) {
 int x3_refresh_weights(const float* flat, long w_off, int chunk, int K, int KP, int Cout, int M, void* Wc, void* WcT,
                        int f16, void* status, hipStream_t st) {
   if (chunk <= 0 || K <= 0 || KP <= 0 || Cout <= 0 || M <= 0 || w_off < 0 || f16 < 0 || KP < K) return -22;
-  const long n = (long)M * KP * Cout;
-  int blocks = (int)((n + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  refresh_x3_kernel<<<blocks, 256, 0, st>>>(flat, w_off, chunk, K, KP, Cout, M, (uint16_t*)Wc, (uint16_t*)WcT, f16,
-                                            (uint32_t*)status);
+  const long blocks = (long)M * ((KP + 31) / 32) * ((Cout + 63) / 64);
+  if (blocks > 0x7FFFFFFFL) return -22;
+  refresh_x3_kernel<<<(unsigned)blocks, 256, 0, st>>>(flat, w_off, chunk, K, KP, Cout, M, (uint16_t*)Wc,
+                                                      (uint16_t*)WcT, f16, (uint32_t*)status);
   return (int)hipGetLastError();
 }
 }

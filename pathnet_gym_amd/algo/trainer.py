@@ -30,7 +30,7 @@ import torch
 from ..config import FITNESS_PENDING, PERFORMANCE_LOG_INTERVAL, TrainConfig
 from ..envs.registry import is_synthetic, make, reward_threshold
 from ..models.acnet import ACPathNet
-from ..parallel.comm import FusedUpdateComm, GatherBroadcastComm
+from ..parallel.comm import FusedUpdateComm, GatherBroadcastComm, active_union
 from ..parallel.dist import DistContext
 from ..runtime.consistency import check_replicas
 from ..runtime.guard import NonFiniteGuard, Watchdog
@@ -191,7 +191,7 @@ class PathNetTrainer:
         eng = self.engine
         if not (getattr(self.cfg, "overlap_allreduce", True) and self.ctx.enabled and self.pipelined
                 and isinstance(self.comm, FusedUpdateComm) and type(self.comm) is FusedUpdateComm
-                and not eng.hybrid and not eng.lstm_hip and self.device.type == "cuda"):
+                and not eng.hybrid and self.device.type == "cuda"):
             return
         segs = self.model.store.layout.segments
         split_off = max(s.offset + s.numel for s in segs if s.layer == 0)
@@ -345,11 +345,7 @@ class PathNetTrainer:
             eng.rollout_backward("head" if eng.split else None)
         with tr.phase("allreduce"):
             if self.ctx.enabled:
-                # modules the running rollout uses, from the device GA of the previous optimizer step (the GPU is
-                # busy with this rollout while the host waits for that small read-back and builds the plan)
-                union = eng.active_union()
-                if union is not None:
-                    self.comm.plan_union(union)
+                self._plan_exchange(eng)
             if eng.split:
                 # bucket 1 (layers >= 1, heads, fitness, counters) is reduced while the first layer's weight
                 # gradient runs; bucket 2 (the first layer) after it
@@ -368,6 +364,34 @@ class PathNetTrainer:
             return UpdateStats(float("nan"), float("nan"), float("nan"), 0, float("nan"),
                                steps=self.cfg.a2c.t_max * self.P * self.E * self.ctx.world)
         return self._collect(prev)
+
+    # the host mirror's module union covers at least this share of the trainable (non-frozen) modules: all-reduce
+    # every trainable module (static plan, no per-update read-back); below it, the exact device union
+    static_plan_min_density = 0.9
+
+    def _plan_exchange(self, eng):
+        """Plan the gradient all-reduce of the update just enqueued, identically on every rank.
+
+        * Static plan (steady state of a large population): every non-frozen module + heads/LSTM -- the reference's
+          own apply set (get_vars_idx, a3c_training_thread.py:190-216; a module no path uses carries a zero
+          gradient).  Its ranges change only with the frozen mask, so the update needs no device read-back and no
+          Python replanning (``plan_union`` returns on an unchanged key).
+        * Exact plan: when the population's union is sparse, only the modules the running rollout expresses, read
+          back from the device GA of the previous optimizer step (one small D2H + event wait per update).
+        The choice uses the host GA mirror (identical on every rank, one update behind), never a timing-dependent
+        read, so ranks always issue the same collective sizes; both plans contain every module the rollout uses."""
+        pop = self.pop
+        trainable = ~(np.asarray(pop.frozen) > 0.5)
+        n_tr = int(trainable.sum())
+        mirror = active_union(pop.expressed(), pop.frozen)
+        if n_tr == 0 or mirror.sum() >= self.static_plan_min_density * n_tr:
+            self.comm.plan_union(trainable)
+            self.plan_mode = "static"
+            return
+        union = eng.active_union()
+        if union is not None:
+            self.comm.plan_union(union)
+            self.plan_mode = "exact"
 
     def _guard_opt(self, flag: float, update: int) -> bool:
         """Feed the device optimizer status of ``update`` to the guard once (pipelined: it arrives late)."""

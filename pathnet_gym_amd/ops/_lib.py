@@ -55,6 +55,8 @@ _SIGS = {
                               c_int, c_long, c_float, c_float, P],
     "launch_pong_step_ring": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_int, c_int, c_uint, P],
+    "launch_pong_step_ring_split": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int,
+                                    c_int, c_int, c_int, c_int, c_int, c_uint, c_int, P],
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_uint, c_int, P, P, P, P, P, P],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],
@@ -131,6 +133,8 @@ _SIGS = {
                      + [c_long, c_float, c_float, P, P],
     "x3_conv1_ring_fwd": [P, P, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 7
                          + [c_long, c_float, c_float, P],
+    "x3_conv23_fwd": [P, c_long, P, c_long, P, c_long, P, c_long, c_long, c_int, P, c_long, P, c_long, P, c_long,
+                      c_long, c_int, P, P, P] + [c_int] * 7 + [c_float, c_float, P],
     "x3_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 6 + [c_long, c_float, c_float, P,
                                                                                          P],
     "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P, P, P],
@@ -165,6 +169,9 @@ _SIGS = {
     "fast_conv_set_x3_fc_ks": [c_int],
     "fast_conv_set_x3_wgrad_pf": [c_int],
     "fast_conv_set_x3_c1_wg_ncx": [c_int],
+    "fast_conv_set_x3_wg_target": [c_int],
+    "fast_conv_set_x3_dg_target": [c_int],
+    "fast_conv_set_x3_fc_ks_parts": [c_int],
     "conv_fwd_smem": [c_int, c_int],
     "conv_wgrad_smem": [c_int],
 }

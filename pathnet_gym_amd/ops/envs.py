@@ -8,6 +8,8 @@ Two entry points per env:
 """
 from __future__ import annotations
 
+import os
+
 import ctypes
 
 import torch
@@ -85,11 +87,21 @@ def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done,
     if not hasattr(env, "_gray"):
         env._gray = _gray_consts(env)
     g = env._gray
-    _lib.call("launch_pong_step_ring", env._st32.data_ptr(), env._ctr32.data_ptr(), actions.data_ptr(),
+    _lib.call("launch_pong_step_ring_split", env._st32.data_ptr(), env._ctr32.data_ptr(), actions.data_ptr(),
               env.num_actions, frames[0, slot].data_ptr(), frames.stride(0), fc_in.data_ptr(), fc_out.data_ptr(),
               env._tab32.data_ptr(),
               reward.data_ptr(), done.data_ptr(), epret.data_ptr(), B, env.seed_int, env.frameskip,
-              env.max_episode_steps, env.no_op_max, g[0], g[1], g[2], g[3], g[4], _id_base(env), _lib.stream())
+              env.max_episode_steps, env.no_op_max, g[0], g[1], g[2], g[3], g[4], _id_base(env), ring_split(B),
+              _lib.stream())
+
+
+def ring_split(B: int) -> int:
+    """Render workgroups per env of the frame-ring Pong step (csrc/envs.hip launch_pong_step_ring_split).  Default 1:
+    the fused one-workgroup-per-env kernel.  Measured at 8 paths x 32 envs (profiles/r5/): physics 5.4 + split-4
+    render 18.5 us vs 20.5 us fused -- a render workgroup's latency is its scene tables, not its quad walk -- so the
+    split is kept for A/B runs only (PATHNET_PONG_SPLIT=N)."""
+    v = os.environ.get("PATHNET_PONG_SPLIT")
+    return max(1, int(v)) if v is not None else 1
 
 
 def pong_step(env, actions, obs):

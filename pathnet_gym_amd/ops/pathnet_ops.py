@@ -208,6 +208,11 @@ class HipPathNet:
         # profiles/r3/kwin_x3_v6*.md).  PATHNET_X3_FC_MM=0 selects path-major.
         self.fc_fwd_mm = os.environ.get("PATHNET_X3_FC_MM", "1") == "1"
         self.fc_fwd_mm_min_k = int(os.environ.get("PATHNET_X3_FC_MM_MIN_K", "1024"))   # fc2 (K = 256): path-major
+        # ... unless the launch is small (P*T*E rows <= this; measured at 8 paths: module-major k-split 4 + slot sum
+        # 10.1 + 6.2 us vs path-major 16.2 us -- a wash, so off by default)
+        self.fc_fwd_mm_small_rows = int(os.environ.get("PATHNET_X3_FC_MM_SMALL_ROWS", "0"))
+        # conv2 + conv3 forward in one launch per rollout step (conv23_fwd)
+        self.fuse23 = os.environ.get("PATHNET_X3_FUSE23", "1") != "0"
         self.fc_wgrad_gm_wgs = int(os.environ.get("PATHNET_X3_FC_WGRAD_WGS", "768"))    # target workgroup count
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
@@ -590,8 +595,8 @@ class HipPathNet:
             ok = _lib.call_fast("x3_conv_fwd", xp, self._x3_lo(X), int(g.u8in), yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
                                 flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L, self.M, g.Hin, g.Win, g.Cin,
                                 g.KH, g.KW, g.S, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
-        elif self.fc_fwd_mm and g.Cout == 256 and g.K >= self.fc_fwd_mm_min_k and P == self.model.P \
-                and aip == self.model.act_idx.data_ptr():
+        elif self.fc_fwd_mm and g.Cout == 256 and (g.K >= self.fc_fwd_mm_min_k or P * T * E <= self.fc_fwd_mm_small_rows) \
+                and P == self.model.P and aip == self.model.act_idx.data_ptr():
             # module-major: each module's weight slice read once per 64 rows of the paths using it
             ys = self._ys_buffer_x3(P * T * E)
             ok = _lib.call_fast("x3_fc_fwd_mm", xp, x2_lo(X), g.ldx, yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
@@ -606,10 +611,30 @@ class HipPathNet:
             raise RuntimeError(f"fp32x: layer {l} forward shape (P={P}, E={E}, T={T}) has no split-bf16 kernel "
                                "(fc layers take <= 32 rows per path and launch)")
 
+    def conv23_fwd(self, l: int, X, Y1, bits1, rows1: int, Y2, bits2, rows2: int, P: int, E: int, T: int,
+                   t0: int) -> bool:
+        """fp32x: the forwards of conv layers l (39x29x8 4x4/s2) and l + 1 (18x13x8 3x3/s1) in ONE launch
+        (csrc/trunk_x3.hip conv23_fwd_tile_x3, bit-identical to two layer_fwd calls).  False when the pair does not
+        have those geometries (the caller then runs layer_fwd twice).  PATHNET_X3_FUSE23=0 disables it."""
+        if not self.x3 or not self.fuse23 or l + 1 >= self.L:
+            return False
+        g1, g2 = self.geoms[l], self.geoms[l + 1]
+        if g1.kind != "conv" or g2.kind != "conv" or (g1.Hin, g1.Win, g1.Cin, g1.KH, g1.S, g1.u8in) != self._X3_CONV[1] \
+                or (g2.Hin, g2.Win, g2.Cin, g2.KH, g2.S, g2.u8in) != self._X3_CONV[2] or l + 1 == self.L - 1:
+            return False
+        m = self.model
+        for t, nm in ((Y1, "Y1"), (Y2, "Y2")):
+            _lib.check(t, torch.float16, name=nm)
+        return _lib.call_fast("x3_conv23_fwd", X.data_ptr(), x2_lo(X), Y1.data_ptr(), x2_lo(Y1), bits1.data_ptr(), rows1,
+                              self.Wc[l].data_ptr(), self.Wc[l][0].numel(), g1.b_off, g1.chunk, Y2.data_ptr(), x2_lo(Y2),
+                              bits2.data_ptr(), rows2, self.Wc[l + 1].data_ptr(), self.Wc[l + 1][0].numel(), g2.b_off,
+                              g2.chunk, m.store.flat.data_ptr(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L,
+                              self.M, P, E, T, t0, 1.0, 1.0, _lib.stream())
+
     def _ys_buffer_x3(self, rows: int) -> torch.Tensor:
-        """fp32 module-slot planes [4][M][rows][256] of the module-major fc forward (up to four k-part planes of
+        """fp32 module-slot planes [8][M][rows][256] of the module-major fc forward (up to eight k-part planes of
         pre-activations, or one plane of activations; grown before graph capture)."""
-        need = 4 * self.M * rows * 256
+        need = 8 * self.M * rows * 256
         if self._ys is None or self._ys.numel() < need:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("fp32x: fc slot buffer first needed inside a graph capture")

@@ -286,8 +286,14 @@ class HipEngine:
         hp = self.hip
         if self.ring:
             hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0])
-            for l in range(1, len(hp.geoms)):
+            l = 1
+            while l < len(hp.geoms):
+                if l + 1 < len(hp.geoms) and hp.conv23_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l], self.bits_rows[l], self.acts[l + 1],
+                                 self.bits[l + 1], self.bits_rows[l + 1], self.P, self.E, 1, t):
+                    l += 2
+                    continue
                 hp.layer_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l], self.P, self.E, 1, t, self.bits_rows[l])
+                l += 1
             return
         p0, np_ = self._group_range(grp)
         x, xrow0 = self._obs_x(t)

@@ -7,7 +7,7 @@ relative error of the engine's stored forward values (trunk outputs, LSTM h) and
 (engine.grads[l], written by layer l+1's dgrad / the LSTM backward) against the float64 truth, beside the plain fp32
 oracle's error on the same quantity:
 
-    python scripts/x3_lstm_diag.py --task Pong
+    python scripts/diag/x3_lstm_diag.py --task Pong
 """
 from __future__ import annotations
 
@@ -18,7 +18,7 @@ import sys
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 DEV = "cuda"
 
@@ -127,7 +127,7 @@ def main():
     ap.add_argument("--task", default="Pong")
     ap.add_argument("--ring", type=int, default=1)
     a = ap.parse_args()
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tests"))
     from test_x3_engine import layer_errors, masks_with_edges
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     from pathnet_gym_amd.config import preset

@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """CPU emulation: how does the fp16-pair representation of a FIXED operand (the weights) propagate into the weight
 gradients of the reference network (L=4 trunk + LSTM 256, A2C loss), compared with the rounding of per-sample
-operands?  (Companion of scripts/x3_lstm_diag.py, which measures the HIP engine itself on the GPU.)
+operands?  (Companion of scripts/diag/x3_lstm_diag.py, which measures the HIP engine itself on the GPU.)
 
 Builds one synthetic update on CPU in float64 -- real synthetic-game frames (torch backend), the reference preset's
 parameters, random paths, an A2C loss over T steps -- and recomputes the gradient with single stages rounded the way
 csrc/trunk_x3.hip rounds them:
 
-    python scripts/x3_lstm_emul.py --game Pong
+    python scripts/diag/x3_lstm_emul.py --game Pong
 """
 from __future__ import annotations
 
@@ -19,7 +19,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 D = torch.float64
 

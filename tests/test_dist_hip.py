@@ -139,7 +139,7 @@ def test_two_gloo_ranks_on_one_gpu_hip_engine_device_ga_pipelined(hip_lib):
 # ---------------------------------------------------------------------------------------------------------------
 # overlapped all-reduce (TrainConfig.overlap_allreduce) and 4 ranks with tournaments firing
 # ---------------------------------------------------------------------------------------------------------------
-def _overlap_worker(rank, world, port, q, updates, trace_path, dtype="fp32"):
+def _overlap_worker(rank, world, port, q, updates, trace_path, dtype="fp32", preset_name="pong", density=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), PATHNET_DIST_BACKEND="gloo")
     torch.set_num_threads(2)
@@ -150,7 +150,7 @@ def _overlap_worker(rank, world, port, q, updates, trace_path, dtype="fp32"):
         ctx = init_distributed()
         out = {}
         for mode in ("overlap", "serial"):
-            cfg = preset("pong")
+            cfg = preset(preset_name)
             cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 4
             cfg.ga.backend = "device"
             cfg.ga.concurrent_tournaments = 2
@@ -162,6 +162,8 @@ def _overlap_worker(rank, world, port, q, updates, trace_path, dtype="fp32"):
             cfg.frame_ring = dtype == "fp32x"
             cfg.overlap_allreduce = mode == "overlap"
             tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
+            if density is not None:
+                tr.static_plan_min_density = density      # 0: always the static plan; > 1: always the exact union
             tr.env.max_episode_steps = 6
             assert tr.engine.split == (mode == "overlap")
             if mode == "overlap":
@@ -171,7 +173,8 @@ def _overlap_worker(rank, world, port, q, updates, trace_path, dtype="fp32"):
             tr.flush()
             torch.cuda.synchronize()
             out[mode] = dict(flat=tr.model.store.flat.detach().cpu().numpy().copy(), gen=tr.pop.generation,
-                             geno=tr.pop.genotypes.copy(), ms=tr.opt.ms.detach().cpu().numpy().copy())
+                             geno=tr.pop.genotypes.copy(), ms=tr.opt.ms.detach().cpu().numpy().copy(),
+                             plan_mode=getattr(tr, "plan_mode", None), lstm=bool(tr.engine.lstm_hip))
             if mode == "overlap":
                 log = tr.comm.overlap_log
                 out["log"] = log
@@ -200,11 +203,11 @@ def _overlap_worker(rank, world, port, q, updates, trace_path, dtype="fp32"):
         q.put((rank, {"error": traceback.format_exc()}))
 
 
-def _run_ranks(world, updates, trace_path=None, dtype="fp32"):
+def _run_ranks(world, updates, trace_path=None, dtype="fp32", preset_name="pong", density=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_overlap_worker, args=(r, world, port, q, updates, trace_path, dtype))
+    ps = [ctx.Process(target=_overlap_worker, args=(r, world, port, q, updates, trace_path, dtype, preset_name, density))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -247,6 +250,36 @@ def test_overlapped_allreduce_fp32x_matches_serial_and_replicas_agree(hip_lib):
     for mode in ("overlap", "serial"):
         assert np.array_equal(res[0][mode]["flat"], res[1][mode]["flat"]), mode
         assert np.array_equal(res[0][mode]["geno"], res[1][mode]["geno"]), mode
+
+
+def test_static_and_exact_exchange_plans_agree_bitwise(hip_lib):
+    """The two all-reduce plans of the pipelined exchange (trainer._plan_exchange): every trainable module (static,
+    no device read-back) vs the exact module union read back from the device GA.  fp32 (fixed-order reductions):
+    the same weights, RMSProp slots and genotypes bit for bit, with tournaments firing."""
+    st = _run_ranks(2, 8, density=0.0)
+    ex = _run_ranks(2, 8, density=2.0)
+    for r in range(2):
+        assert st[r]["overlap"]["plan_mode"] == "static" and ex[r]["overlap"]["plan_mode"] == "exact"
+        for mode in ("overlap", "serial"):
+            assert np.array_equal(st[r][mode]["flat"], ex[r][mode]["flat"]), mode
+            assert np.array_equal(st[r][mode]["ms"], ex[r][mode]["ms"]), mode
+            assert np.array_equal(st[r][mode]["geno"], ex[r][mode]["geno"]), mode
+        assert st[r]["overlap"]["gen"] > 0
+
+
+def test_reference_lstm_preset_overlapped_exchange_two_ranks(hip_lib):
+    """The reference network (L=4 trunk + fused fp32x LSTM, synthetic Alien on the frame ring) on 2 gloo ranks with
+    the overlapped split exchange (bucket 1 = layers >= 1 + LSTM + heads + fitness + counters, reduced while the first
+    layer's weight gradient runs): within the fp32x budget of the single-bucket exchange, replicas bit-identical."""
+    res = _run_ranks(2, 6, dtype="fp32x", preset_name="reference")
+    for r in range(2):
+        o, s = res[r]["overlap"], res[r]["serial"]
+        assert o["lstm"], "the reference preset must run the fused HIP LSTM"
+        d = np.linalg.norm(o["flat"] - s["flat"]) / np.linalg.norm(s["flat"])
+        assert d < 1e-5, d
+        assert res[r]["split_n"][0] > 0 and res[r]["split_n"][1] > 0
+    for mode in ("overlap", "serial"):
+        assert np.array_equal(res[0][mode]["flat"], res[1][mode]["flat"]), mode
 
 
 def _strong_worker(rank, world, port, q):

@@ -736,9 +736,12 @@ def test_bf16_conv_gradients_match_fp32(hip_lib):
     budget.check("bf16_conv_act_grads_wgrad", errs, 2e-2)
 
 
-def test_frame_ring_stacks_match_packed_env(hip_lib):
+@pytest.mark.parametrize("split", ["1", "2", "4"])
+def test_frame_ring_stacks_match_packed_env(hip_lib, monkeypatch, split):
     """Frame-ring rollout (single-frame writes + first-valid-channel bytes) reproduces, bit for bit,
-    the packed 4-frame stacks the packed Pong kernel produces for the same actions, resets included."""
+    the packed 4-frame stacks the packed Pong kernel produces for the same actions, resets included -- with the fused
+    ring kernel (split 1) and the physics + split-render launches (csrc/envs.hip launch_pong_step_ring_split)."""
+    monkeypatch.setenv("PATHNET_PONG_SPLIT", split)
     from pathnet_gym_amd.algo.trainer import PathNetTrainer
     from pathnet_gym_amd.ops import envs as henv
     cfg = preset("pong")

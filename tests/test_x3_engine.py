@@ -244,7 +244,8 @@ def test_x3_frame_ring_forward_bit_equal_to_packed(x3_ring_rollout):
 
 
 @pytest.mark.parametrize("E", [16, 32])
-@pytest.mark.parametrize("variant", ["split_k", "module_major", "module_major_ks1", "module_major_regs"])
+@pytest.mark.parametrize("variant", ["split_k", "module_major", "module_major_ks1", "module_major_regs",
+                                     "module_major_ks2", "module_major_ks4", "module_major_ks8"])
 def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     """fc_fwd_ks_x3 (two waves per module, partial sums meet in LDS), fc_fwd_mm2_x3 (module-major LDS tiles, one or
     two k parts; the two-part form leaves bias / ReLU / bits to fc_slot_sum2_x3) and fc_fwd_mm_x3 (one workgroup per module
@@ -261,6 +262,8 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     outs = []
     lib = _lib.lib()
     lib.fast_conv_set_x3_fc_mmv({"module_major_regs": 1, "module_major_ks1": 2}.get(variant, 3))
+    # k parts of the two-part module-major form: fixed 2 / 4 / 8, or 0 = auto (8 at these small row counts)
+    lib.fast_conv_set_x3_fc_ks_parts(int(variant[-1]) if variant[-3:-1] == "ks" and variant[-1] in "248" else 0)
     hp.fc_fwd_mm_min_k = 0
     for ref in (False, True):
         hp.fc_fwd_mm = variant.startswith("module_major") and not ref
@@ -280,11 +283,51 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     hp.fc_fwd_mm_min_k = 1024
     lib.fast_conv_set_x3_fc_mmv(3)
     lib.fast_conv_set_x3_fc_ks(1)
+    lib.fast_conv_set_x3_fc_ks_parts(0)
     for l in (3, 4):
         a, b = outs[0][0][l], outs[1][0][l]
         assert rel(a, b) < 1e-6, (l, rel(a, b))
         same = (outs[0][1][l] == outs[1][1][l]).float().mean().item()
         assert same > 0.999, (l, same)
+
+
+@pytest.mark.parametrize("T", [1, 3])
+def test_x3_fused_conv23_forward_bit_equal(hip_lib, T):
+    """conv23_fwd_tile_x3 (conv2 + conv3 forward in one launch, csrc/trunk_x3.hip) == two conv_fwd_tile_x3 launches,
+    bit for bit: activations (both fp16 planes) and ReLU bits, including a path with every module active (multi-pass
+    accumulation through global memory) and a path with an empty layer."""
+    cfg = pixel_cfg()
+    P, E = 4, 16
+    m = ACPathNet(cfg, P, DEV, "hip", seed=11, compute_dtype="fp32x")
+    m.set_paths(masks_with_edges(P, cfg.L, cfg.M, cfg.N, seed=6))   # path 1: all 10 modules (multi-pass), path 0: none
+    hp = m.hip
+    g = torch.Generator(device="cpu").manual_seed(5)
+    obs = torch.randint(0, 256, (T * P * E, 160, 120, 4), generator=g, dtype=torch.uint8).to(DEV)
+    X0 = hp.alloc_act(0, (T, P * E, hp.geoms[0].out_feat))
+    b0, r0 = hp.alloc_bits(0, T, P * E)
+    hp.layer_fwd(0, obs, X0, b0, P, E, T, 0, r0)
+    outs = []
+    for fused in (False, True):
+        Y1 = hp.alloc_act(1, (T, P * E, hp.geoms[1].out_feat))
+        Y2 = hp.alloc_act(2, (T, P * E, hp.geoms[2].out_feat))
+        b1, r1 = hp.alloc_bits(1, T, P * E)
+        b2, r2 = hp.alloc_bits(2, T, P * E)
+        if fused:
+            assert hp.conv23_fwd(1, X0, Y1, b1, r1, Y2, b2, r2, P, E, T, 0)
+        else:
+            hp.layer_fwd(1, X0, Y1, b1, P, E, T, 0, r1)
+            hp.layer_fwd(2, Y1, Y2, b2, P, E, T, 0, r2)
+        torch.cuda.synchronize()
+        outs.append([x2_value(Y1), x2_value(Y2), b1.clone(), b2.clone(), Y1.clone(), Y2.clone()])
+    cnt = m.act_cnt.view(P, -1).cpu()
+    for i in (0, 1, 4, 5):
+        assert torch.equal(outs[0][i], outs[1][i]), i
+    for bi, l, hw in ((2, 1, hp.geoms[1].HWo), (3, 2, hp.geoms[2].HWo)):
+        for p in range(P):
+            k = int(cnt[p, l])
+            for t in range(T):
+                r = (t * P * E + p * E) * hw
+                assert torch.equal(outs[0][bi][:k, r:r + E * hw], outs[1][bi][:k, r:r + E * hw]), (l, p, t)
 
 
 @pytest.mark.parametrize("arm", ["swapped", "tile", "tile_pair", "band", "band_pipe"])
