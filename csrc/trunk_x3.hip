@@ -275,12 +275,20 @@ DEVI void conv_epi_sw(const f4v (&acc)[NC], const float* bias_s, int ct0, int cn
       sum[r] += pos ? v : 0.f;
       nib |= pos ? (1u << r) : 0u;
     }
-    const uint32_t hi4 = (uint32_t)__shfl_xor((int)nib, 16, 64);      // channels 4..7 of the same slot and row
+    // channels 4..7 of the same slot and row: lane l ^ 16.  v_permlane16_swap (x, x) leaves row 2k+1's values in the
+    // SECOND result's row 2k, which is what the lanes that store the byte (rows 0 and 2: q even) need -- one VALU op
+    // instead of a ds_bpermute round trip
+    const uint32_t hi4 = __builtin_amdgcn_permlane16_swap(nib, nib, false, false)[1];
     const int slot = (ct0 + ct) * 2 + (q >> 1);
     if ((q & 1) == 0 && slot < cnt && valid) bits[(long)slot * bits_rows + grow] = (uint8_t)(nib | (hi4 << 4));
   }
+  // + the other slot of each pair (lane l ^ 32): v_permlane32_swap (x, x) gives {lanes 0-31's half, lanes 32-63's
+  // half} on every lane; their sum is the same float addition as the shuffle's in either order (bit-identical)
 #pragma unroll
-  for (int r = 0; r < 4; ++r) sum[r] += __shfl_xor(sum[r], 32, 64);   // + the other slot of each pair
+  for (int r = 0; r < 4; ++r) {
+    const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(sum[r]), __float_as_uint(sum[r]), false, false);
+    sum[r] = __uint_as_float(pr[0]) + __uint_as_float(pr[1]);
+  }
   float y[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) y[r] = sum[r] * out_scale;
@@ -1166,9 +1174,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tile_x3(const uint16_t* __res
 
 // The 4x4/s2 and 3x3/s1 layers' forwards in ONE launch: a workgroup runs conv_fwd_tile_body for layer `layer` over
 // its samples (writing Y1 and its ReLU bits as the conv2 kernel does), then -- the same samples, so no other workgroup
-// is involved -- layer + 1 reading those Y1 rows back (L2-hot), into Y2.  A device-scope fence between the phases
-// makes this workgroup's Y1 stores visible to its own loads (it also invalidates the CU's L1).  Saves a launch and the
-// second kernel's ramp per rollout step; same arithmetic as the two launches (bit-identical).
+// is involved -- layer + 1 reading those Y1 rows back (L2-hot), into Y2; the barrier between the phases orders the
+// workgroup's own global stores and loads.  Same arithmetic as the two launches (bit-identical).
 template <class G1, class G2, bool PAIR1>
 __global__ __launch_bounds__(256, 2) void conv23_fwd_tile_x3(const uint16_t* __restrict__ X, long xlo,
                                                             uint16_t* __restrict__ Y1, long y1lo,
@@ -1189,8 +1196,8 @@ __global__ __launch_bounds__(256, 2) void conv23_fwd_tile_x3(const uint16_t* __r
   __shared__ int mods[X3_MAXM];
   conv_fwd_tile_body<G1, PAIR1>(X, xlo, Y1, y1lo, bits1, Wc1, w1lo, flat, bias1_off, chunk1, act_idx, act_cnt, layer, L,
                                 M, P, E, T, t0, bits_rows1, samples_per_wg, in_scale, out_scale1, lds, bias_s, mods);
-  __threadfence();
-  __syncthreads();
+  __syncthreads();     // the workgroup's Y1 stores are visible to its own waves (workgroup-scope fences; a device-scope
+                       // __threadfence here wrote back L2 per workgroup: 85 vs 43 us per step at 64 paths)
   conv_fwd_tile_body<G2, false>(Y1, y1lo, Y2, y2lo, bits2, Wc2, w2lo, flat, bias2_off, chunk2, act_idx, act_cnt,
                                 layer + 1, L, M, P, E, T, t0, bits_rows2, samples_per_wg, in_scale, out_scale2, lds,
                                 bias_s, mods);

@@ -32,6 +32,13 @@ from ..ops import _lib
 from ..ops import envs as henv
 
 
+# hipGraph capture mode: thread-local, so other threads' HIP calls stay legal during a capture.  The RCCL process
+# group's watchdog thread polls the completion events of earlier collectives; under the default global mode a poll
+# that lands inside a capture fails with hipErrorStreamCaptureUnsupported and aborts the process (seen when a second
+# trainer captured its graphs after the first one's all-reduces: bench.py strong / per-rank windows, in-run solve).
+CAPTURE_MODE = "thread_local"
+
+
 def loss_scale(cfg) -> float:
     """grad_scale x (1 / world size when rank_reduction == "mean"): the factor on every sample's loss weight."""
     a2c = cfg.a2c
@@ -598,18 +605,18 @@ class HipEngine:
         for q in ((0, 1) if self._obs_bufs is not None else (par,)):      # one rollout graph per obs parity
             self._par = q
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 self._rollout_backward_body("head" if self.split else None)
             self.g_rollouts.append(g)
             if self.split:
                 gt = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gt):
+                with torch.cuda.graph(gt, capture_error_mode=CAPTURE_MODE):
                     self._rollout_backward_body("tail")
                 self.g_tails.append(gt)
         self._par = par
         self.g_rollout = self.g_rollouts[0]
         self.g_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_opt):
+        with torch.cuda.graph(self.g_opt, capture_error_mode=CAPTURE_MODE):
             self._optimizer_body()
         torch.cuda.synchronize()
 

@@ -119,3 +119,34 @@ def test_forced_one_rank_rccl_group_reproduces_no_group(hip_lib):
         else:
             d = np.linalg.norm(a["flat"] - ref["flat"]) / np.linalg.norm(ref["flat"])
             assert d < 1e-5, d
+
+
+@pytest.mark.gpu
+def test_forced_rccl_bench_builds_several_trainers(hip_lib, tmp_path):
+    """bench.py on a forced one-rank RCCL group: the headline trainer's all-reduces, then a per-rank-shape trainer and
+    an in-run-solve trainer that capture their hipGraphs while the process group's watchdog thread still polls the
+    earlier collectives' events.  With the default global capture mode such a poll aborted the process
+    (hipErrorStreamCaptureUnsupported); the engine captures in thread-local mode (runtime/engine.py CAPTURE_MODE)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PATHNET_DIST_FORCE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--paths", "16", "--paths-total", "16", "--envs", "16",
+           "--tmax", "5", "--steps", "3", "--warmup", "2", "--windows", "2", "--per-rank-shapes", "2",
+           "--solve-seconds", "8", "--compare-bf16", "0", "--no-verify-build"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["strong_scaling"]["per_rank"]["by_n_gpus"]["2"]["paths_per_gpu"] == 8
+    assert d["generations_to_solve_in_run"]["updates_run"] > 0
+
+
+def test_engine_captures_graphs_thread_local():
+    """CPU guard for the capture mode the RCCL watchdog needs (see the GPU test above)."""
+    from pathnet_gym_amd.runtime import engine
+    assert engine.CAPTURE_MODE == "thread_local"
+    src = open(engine.__file__).read()
+    assert src.count("capture_error_mode=CAPTURE_MODE") == 3 and src.count("torch.cuda.graph(") == 3
