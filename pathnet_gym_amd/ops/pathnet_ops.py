@@ -493,16 +493,22 @@ class HipPathNet:
                       self.M, g.K, g.KP, g.Cout, P, E, T, t0, bits_rows, out_scale, st)
 
     def layer_bwd(self, l: int, X: torch.Tensor, G: torch.Tensor, bits: torch.Tensor, grad_flat: torch.Tensor,
-                  dX: Optional[torch.Tensor], P: int, E: int, T: int, bits_rows: int, rows_per_chunk: int = 0):
+                  dX: Optional[torch.Tensor], P: int, E: int, T: int, bits_rows: int, rows_per_chunk: int = 0,
+                  part: Optional[str] = None):
+        """Backward of layer l.  part (fp32x only): None = both gradients; "d" = the input gradient (plus, on the last
+        layer, the G16 amax of the incoming gradient; on fc layers, the masked gradient Gm the weight gradient reads);
+        "w" = the weight gradient only, issued after "d" (runtime/engine.py runs it on a side stream)."""
         g = self.geoms[l]
         m = self.model
         flat = m.store.flat
         g_scale = self.out_scale_last if l == self.L - 1 else 1.0
         st = _lib.stream()
+        if part is not None and not self.x3:
+            raise ValueError("layer_bwd(part=...) is implemented for the fp32x engine")
         if self.f32:
             return self._layer_bwd_f32(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
         if self.x3:
-            return self._layer_bwd_x3(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
+            return self._layer_bwd_x3(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st, part)
         if self.deterministic:
             return self._layer_bwd_det(l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st)
         if (G.dtype == torch.bfloat16) or (dX is not None and dX.dtype == torch.bfloat16):
@@ -645,25 +651,28 @@ class HipPathNet:
         """Device address of layer l's gradient amax (G16), or None below layer 0."""
         return None if l < 0 else self.gamax.data_ptr() + 4 * l
 
-    def _layer_bwd_x3(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st):
+    def _layer_bwd_x3(self, l, X, G, bits, grad_flat, dX, P, E, T, bits_rows, g_scale, st, part=None):
         g = self.geoms[l]
         m = self.model
         flat = m.store.flat
+        do_w, do_d = part in (None, "w"), part in (None, "d")
         _lib.check(G, torch.float32, name="G")
         if dX is not None:
             _lib.check(dX, torch.float32, name="dX")
-        if l == self.L - 1:
+        if l == self.L - 1 and do_d:
             # a backward starts at the last layer: fresh amaxes, the incoming gradient's measured here
             _lib.call("x3_amax_reset", self.gamax.data_ptr(), self.L, st)
             _lib.call("x3_amax", G.data_ptr(), G.numel(), self._gamax(l), st)
         ga, ga_out = self._gamax(l), self._gamax(l - 1)
         xb, xblo = self._x3_bf16(X)
         if g.kind == "conv":
-            ok = _lib.call_fast("x3_conv_wgrad", xb, xblo, int(g.u8in), G.data_ptr(),
-                                bits.data_ptr(), grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
-                                m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin, g.KH, g.KW, g.S, P, E, T,
-                                bits_rows, g.in_scale, g_scale, ga, st)
-            if ok and dX is not None:
+            ok = True
+            if do_w:
+                ok = _lib.call_fast("x3_conv_wgrad", xb, xblo, int(g.u8in), G.data_ptr(),
+                                    bits.data_ptr(), grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk,
+                                    m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin,
+                                    g.KH, g.KW, g.S, P, E, T, bits_rows, g.in_scale, g_scale, ga, st)
+            if ok and dX is not None and do_d:
                 ok = _lib.call_fast("x3_conv_dgrad", G.data_ptr(), bits.data_ptr(), flat.data_ptr(), g.w_off, g.chunk,
                                     m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.Hin, g.Win, g.Cin,
                                     g.KH, g.KW, g.S, P, E, T, bits_rows, g_scale, dX.data_ptr(), ga, ga_out, st)
@@ -676,12 +685,14 @@ class HipPathNet:
         gm = self._gm_buffer_x3(bits_rows) if (dX is not None and g.Cout == 256) else None
         gmlo = gm.numel() // 2 if gm is not None else 0
         ok = True
-        if dX is not None:
+        if dX is not None and do_d:
             ok = _lib.call_fast("x3_fc_dgrad", G.data_ptr(), bits.data_ptr(), self.WcT[l].data_ptr(),
                                 self.WcT[l][0].numel(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M,
                                 g.K, g.KP, g.Cout, P, E, T, bits_rows, g_scale, dX.data_ptr(), _lib.ptr(gm), gmlo, ga,
                                 ga_out, st)
-        if ok and use_gm_wgrad:
+        if not do_w:
+            pass
+        elif ok and use_gm_wgrad:
             tiles = ((g.K + 127) // 128) * self.M
             # workgroups ~ a whole number of rounds of one per CU (fc_wgrad_gm_x3 holds 102 KB of LDS): 110 tiles x 7
             # = 770 = 3.0 rounds on 256 CUs, where 110 x 5 = 550 left the third round 15 % full

@@ -310,11 +310,30 @@ class HipEngine:
                          xrow0=xrow0 + p0 * self.E if l == 0 else None)
             x = self.acts[l]
 
+    def _bwd_side_stream(self):
+        """Side stream of the backward (fp32x, small populations): layer l's weight gradient runs there while the
+        main stream computes its input gradient and the layers below -- the input-gradient chain is the critical
+        path.  Measured (profiles/r5/kwin_p*_bwd_side.md): the concurrent kernels contend instead of overlapping at
+        every population size (8 paths 3.59 -> 3.70 ms, 16 paths 4.63 -> 5.24 ms; the fc1 weight gradient 106 ->
+        228 us), as two streams did at 64 paths in round 1, so it is off; PATHNET_BWD_STREAMS=2 turns it on."""
+        import os
+        on = os.environ.get("PATHNET_BWD_STREAMS") == "2"
+        if not (on and self.hip.x3 and not self.hybrid):
+            return None
+        if getattr(self, "_bwd_side", None) is None:
+            self._bwd_side = torch.cuda.Stream(device=self.device)
+        return self._bwd_side
+
     def _layer_bwd_all(self, T, lo: int = 0, hi: Optional[int] = None):
-        """Backward of layers hi-1 .. lo (default: all)."""
+        """Backward of layers hi-1 .. lo (default: all).  With a side stream (fp32x, small P) every layer's weight
+        gradient is forked off after the main stream has issued that layer's input gradient (fc layers: which also
+        writes the masked gradient the weight gradient reads; the last layer: the G16 amax) and joined at the end."""
         hp = self.hip
         P, E = self.P, self.E
         hi = len(hp.geoms) if hi is None else hi
+        side = self._bwd_side_stream()
+        main = torch.cuda.current_stream() if side is not None else None
+        forked = False
         for l in range(hi - 1, lo - 1, -1):
             if l == 0 and self.ring:
                 hp.ring_wgrad(self.frames, self.fc, self.grads[0], self.bits[0], self.grad_flat, P, E, T,
@@ -322,7 +341,17 @@ class HipEngine:
                 continue
             X = self.obs if l == 0 else self.acts[l - 1]
             dX = self.grads[l - 1] if l > 0 else None
-            hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
+            if side is None or dX is None:
+                hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l])
+                continue
+            hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l], part="d")
+            side.wait_stream(main)
+            forked = True
+            with torch.cuda.stream(side):
+                hp.layer_bwd(l, X, self.grads[l], self.bits[l], self.grad_flat, dX, P, E, T, self.bits_rows[l],
+                             part="w")
+        if forked:
+            main.wait_stream(side)
 
     def _forward_step(self, t, greedy=False, grp=None):
         hp = self.hip

@@ -291,6 +291,34 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
         assert same > 0.999, (l, same)
 
 
+def test_x3_backward_side_stream_matches_one_stream(hip_lib, monkeypatch):
+    """Small populations run every layer's weight gradient on a side stream (runtime/engine.py _layer_bwd_all): the
+    first update's gradient equals the one-stream backward's to fp32 rounding (float atomics in both); the captured
+    graphs replay.  (Off by default: measured slower; PATHNET_BWD_STREAMS=2.)"""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    grads = {}
+    for mode in ("1", "2"):
+        monkeypatch.setenv("PATHNET_BWD_STREAMS", mode)
+        cfg = preset("pong")
+        cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 4
+        cfg.compute_dtype = "fp32x"
+        cfg.frame_ring = True
+        cfg.ga.backend = "device"
+        tr = PathNetTrainer(cfg, device=DEV)
+        tr.env.max_episode_steps = 5
+        eng = tr.engine
+        assert (eng._bwd_side_stream() is not None) == (mode == "2")
+        tr.update()                           # eager; the graphs are captured at its end
+        torch.cuda.synchronize()
+        grads[mode] = eng.grad_flat.clone()
+        for _ in range(2):
+            tr.update()                       # graph replays
+        tr.flush()
+        torch.cuda.synchronize()
+        assert eng.g_opt is not None and torch.isfinite(tr.model.store.flat).all()
+    assert rel(grads["2"], grads["1"]) < 1e-6, rel(grads["2"], grads["1"])
+
+
 @pytest.mark.parametrize("T", [1, 3])
 def test_x3_fused_conv23_forward_bit_equal(hip_lib, T):
     """conv23_fwd_tile_x3 (conv2 + conv3 forward in one launch, csrc/trunk_x3.hip) == two conv_fwd_tile_x3 launches,
