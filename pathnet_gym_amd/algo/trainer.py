@@ -387,11 +387,14 @@ class PathNetTrainer:
         if n_tr == 0 or mirror.sum() >= self.static_plan_min_density * n_tr:
             self.comm.plan_union(trainable)
             self.plan_mode = "static"
+            eng.want_union = False
             return
+        # exact plan: the union of the previous optimizer step's device GA; read back only while the exact plan is
+        # in use, so the first update after a switch takes the static superset instead
+        eng.want_union = True
         union = eng.active_union()
-        if union is not None:
-            self.comm.plan_union(union)
-            self.plan_mode = "exact"
+        self.comm.plan_union(union if union is not None else trainable)
+        self.plan_mode = "exact" if union is not None else "static"
 
     def _guard_opt(self, flag: float, update: int) -> bool:
         """Feed the device optimizer status of ``update`` to the guard once (pipelined: it arrives late)."""

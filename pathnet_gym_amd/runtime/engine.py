@@ -546,8 +546,10 @@ class HipEngine:
             self.fit_sum.masked_fill_(fired, 0.0)
 
     def _read_union(self):
-        """After an optimizer step: start the D2H of the device GA's next module union (outside any graph)."""
-        if self.ga_dev is None:
+        """After an optimizer step: start the D2H of the device GA's next module union (outside any graph) -- only
+        when the trainer's next exchange plan needs it (``want_union``: a multi-rank run on the exact plan)."""
+        if self.ga_dev is None or not getattr(self, "want_union", False):
+            self._union_ev = None
             return
         self.ga_dev["union_host"].copy_(self.ga_dev["union"], non_blocking=True)
         self._union_ev = torch.cuda.Event()
