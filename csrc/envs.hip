@@ -423,9 +423,9 @@ __global__ __launch_bounds__(64) void pong_physics_kernel(int* __restrict__ stat
                                                          float* __restrict__ reward_out, uint8_t* __restrict__ done_out,
                                                          float* __restrict__ epret_out, uint32_t seed, int frameskip,
                                                          int max_steps, int no_op_max, const uint8_t* __restrict__ fc_in,
-                                                         uint8_t* __restrict__ fc_out, uint32_t id_base) {
+                                                         uint8_t* __restrict__ fc_out, uint32_t id_base, int b0) {
   __shared__ int phys[pong::NSTATE + 4];
-  pong::physics_wave0((int)blockIdx.x, state, counter, actions, n_actions, seed, frameskip, max_steps, no_op_max, phys,
+  pong::physics_wave0(b0 + (int)blockIdx.x, state, counter, actions, n_actions, seed, frameskip, max_steps, no_op_max, phys,
                       reward_out, done_out, epret_out, fc_in, fc_out, id_base);
 }
 
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256, 8) void pong_render_ring_kernel(const int* __r
                                                                  const int* __restrict__ tables,
                                                                  uint8_t* __restrict__ frame_out, long out_stride,
                                                                  int split, int g_bg, int g_wall, int g_cpu,
-                                                                 int g_player, int g_ball) {
+                                                                 int g_player, int g_ball, int b0) {
   using namespace pong;
   __shared__ __attribute__((aligned(16))) int tab[8 * 160];
   __shared__ int rowinfo[OBS_H];
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256, 8) void pong_render_ring_kernel(const int* __r
   __shared__ int quadmask[OBS_W / 4];
   __shared__ uint8_t band[BAND_R * BAND_C];
   __shared__ __attribute__((aligned(4))) uint8_t dlut[DL_R * 48];
-  const int env = (int)blockIdx.y;
+  const int env = b0 + (int)blockIdx.y;
   for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
   St st;
 #pragma unroll
@@ -537,45 +537,55 @@ int launch_pong_step(void* state, void* counter, const int* actions, int n_actio
 }
 
 // frame-ring variant: frame_out = env 0's new frame (160*120 uint8), env b's at + b*out_stride bytes;
-// fc_in/fc_out [B] uint8
+// fc_in/fc_out [B] uint8.  Envs [b0, B) only (one path group of the split rollout, runtime/engine.py): every index
+// (state, RNG key, frame, fc) stays global.
+static int pong_ring_launch(void* state, void* counter, const int* actions, int n_actions, void* frame_out,
+                            long out_stride, const void* fc_in, void* fc_out, const int* tables, float* reward,
+                            void* done, float* epret, int B, unsigned seed, int frameskip, int max_steps,
+                            int no_op_max, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball, unsigned id_base,
+                            int b0, int split, hipStream_t stream) {
+  if (n_actions <= 0 || out_stride <= 0 || B <= 0 || frameskip < 0 || max_steps < 0 || no_op_max < 0 || g_bg < 0 ||
+      g_wall < 0 || g_cpu < 0 || g_player < 0 || g_ball < 0 || b0 < 0 || b0 >= B || split > 64) return -22;
+  if (out_stride < 160 * 120 || out_stride % 16) return -22;
+  if (split <= 1) {
+    pong_step_kernel<true><<<B - b0, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions, nullptr,
+                                                       (uint32_t*)frame_out, tables, reward, (uint8_t*)done, epret,
+                                                       seed, frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu,
+                                                       g_player, g_ball, (const uint8_t*)fc_in, (uint8_t*)fc_out,
+                                                       out_stride, b0, id_base);
+    return (int)hipGetLastError();
+  }
+  if (!fc_in || !fc_out) return -22;
+  // the same step in two launches (physics, then the render over `split` workgroups per env)
+  pong_physics_kernel<<<B - b0, 64, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions, reward,
+                                                 (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max,
+                                                 (const uint8_t*)fc_in, (uint8_t*)fc_out, id_base, b0);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  pong_render_ring_kernel<<<dim3((unsigned)split, (unsigned)(B - b0)), 256, 0, stream>>>(
+      (const int*)state, tables, (uint8_t*)frame_out, out_stride, split, g_bg, g_wall, g_cpu, g_player, g_ball, b0);
+  return (int)hipGetLastError();
+}
+
 int launch_pong_step_ring(void* state, void* counter, const int* actions, int n_actions, void* frame_out,
                           long out_stride, const void* fc_in, void* fc_out, const int* tables, float* reward,
                           void* done, float* epret, int B, unsigned seed, int frameskip, int max_steps, int no_op_max,
                           int g_bg, int g_wall, int g_cpu, int g_player, int g_ball, unsigned id_base,
                           hipStream_t stream) {
-  if (n_actions <= 0 || out_stride <= 0 || B <= 0 || frameskip < 0 || max_steps < 0 || no_op_max < 0 || g_bg < 0 ||
-      g_wall < 0 || g_cpu < 0 || g_player < 0 || g_ball < 0) return -22;
-  if (out_stride < 160 * 120 || out_stride % 16) return -22;
-  pong_step_kernel<true><<<B, 256, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions, nullptr,
-                                                (uint32_t*)frame_out, tables, reward, (uint8_t*)done, epret, seed,
-                                                frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu, g_player,
-                                                g_ball, (const uint8_t*)fc_in, (uint8_t*)fc_out, out_stride, 0,
-                                                id_base);
-  return (int)hipGetLastError();
+  return pong_ring_launch(state, counter, actions, n_actions, frame_out, out_stride, fc_in, fc_out, tables, reward,
+                          done, epret, B, seed, frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu, g_player, g_ball,
+                          id_base, 0, 1, stream);
 }
 
-// the same step as launch_pong_step_ring in two launches (physics, then the render over `split` workgroups per env);
-// split <= 1: the fused kernel
+// envs [b0, b1) of the ring step; split <= 1: the fused kernel, else physics + a render over `split` workgroups/env
 int launch_pong_step_ring_split(void* state, void* counter, const int* actions, int n_actions, void* frame_out,
                                 long out_stride, const void* fc_in, void* fc_out, const int* tables, float* reward,
-                                void* done, float* epret, int B, unsigned seed, int frameskip, int max_steps,
+                                void* done, float* epret, int b1, unsigned seed, int frameskip, int max_steps,
                                 int no_op_max, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
-                                unsigned id_base, int split, hipStream_t stream) {
-  if (split <= 1)
-    return launch_pong_step_ring(state, counter, actions, n_actions, frame_out, out_stride, fc_in, fc_out, tables,
-                                 reward, done, epret, B, seed, frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu,
-                                 g_player, g_ball, id_base, stream);
-  if (n_actions <= 0 || out_stride <= 0 || B <= 0 || frameskip < 0 || max_steps < 0 || no_op_max < 0 || g_bg < 0 ||
-      g_wall < 0 || g_cpu < 0 || g_player < 0 || g_ball < 0 || split > 64 || !fc_in || !fc_out) return -22;
-  if (out_stride < 160 * 120 || out_stride % 16) return -22;
-  pong_physics_kernel<<<B, 64, 0, stream>>>((int*)state, (uint32_t*)counter, actions, n_actions, reward,
-                                            (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max,
-                                            (const uint8_t*)fc_in, (uint8_t*)fc_out, id_base);
-  int rc = (int)hipGetLastError();
-  if (rc) return rc;
-  pong_render_ring_kernel<<<dim3((unsigned)split, (unsigned)B), 256, 0, stream>>>(
-      (const int*)state, tables, (uint8_t*)frame_out, out_stride, split, g_bg, g_wall, g_cpu, g_player, g_ball);
-  return (int)hipGetLastError();
+                                unsigned id_base, int b0, int split, hipStream_t stream) {
+  return pong_ring_launch(state, counter, actions, n_actions, frame_out, out_stride, fc_in, fc_out, tables, reward,
+                          done, epret, b1, seed, frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu, g_player, g_ball,
+                          id_base, b0, split, stream);
 }
 
 int launch_cartpole_step(float* state, int* steps, float* epret, void* counter, const int* actions, int B,

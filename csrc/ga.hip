@@ -181,7 +181,47 @@ __global__ __launch_bounds__(64) void ga_compact_inverse_kernel(const float* __r
   if (lane == 0) inv_cnt[l * M + j] = n;
 }
 
+// inverse lists of one path group [p0, p0 + np) of the split rollout (runtime/engine.py): every module's path-ordered
+// list is cut to the group's paths and re-based to group-local path indices, so the module-major fc forward of the
+// group sees a population of np paths (its X / Y / bits / act tables passed at the group's base).  One wave per
+// (layer, module).  Layout [L][M][np].
+__global__ __launch_bounds__(64) void inv_group_kernel(const int* __restrict__ inv_path, const int* __restrict__ inv_slot,
+                                                       const int* __restrict__ inv_cnt, int P, int L, int M, int p0,
+                                                       int np, int* __restrict__ gpath, int* __restrict__ gslot,
+                                                       int* __restrict__ gcnt) {
+  const int item = blockIdx.x;
+  if (item >= L * M) return;
+  const int lane = threadIdx.x;
+  const long base = (long)item * P, gbase = (long)item * np;
+  const int n = inv_cnt[item];
+  int k = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const int p = i < n ? inv_path[base + i] : -1;
+    const bool in = p >= p0 && p < p0 + np;
+    const uint64_t bal = __ballot(in);
+    const int rank = k + __popcll(bal & ((1ull << lane) - 1ull));
+    if (in) {
+      gpath[gbase + rank] = p - p0;
+      gslot[gbase + rank] = inv_slot[base + i];
+    }
+    k += __popcll(bal);
+  }
+  for (int kk = k + lane; kk < np; kk += 64) {
+    gpath[gbase + kk] = 0;
+    gslot[gbase + kk] = 0;
+  }
+  if (lane == 0) gcnt[item] = k;
+}
+
 extern "C" {
+int launch_inv_group(const int* inv_path, const int* inv_slot, const int* inv_cnt, int P, int L, int M, int p0, int np,
+                     int* gpath, int* gslot, int* gcnt, hipStream_t stream) {
+  if (P <= 0 || L <= 0 || M <= 0 || p0 < 0 || np <= 0 || p0 + np > P || !gpath || !gslot || !gcnt) return -22;
+  inv_group_kernel<<<L * M, 64, 0, stream>>>(inv_path, inv_slot, inv_cnt, P, L, M, p0, np, gpath, gslot, gcnt);
+  return (int)hipGetLastError();
+}
+
 int launch_ga_step(void* geno, float* fitness, int* slots, long long* gen_ctr, int* events, int P, int L, int M,
                    int N, int B, int C, unsigned seed, void* reset, hipStream_t stream) {
   if (P <= 0 || L <= 0 || M <= 0 || N <= 0 || B <= 0 || C <= 0) return -22;

@@ -335,10 +335,13 @@ class PongVec(VecEnv):
         if hip_state:
             henv.pong_sync_to_device(self)
 
-    def step_ring_into(self, actions, frames, slot, fc_in, fc_out, reward, done, epret):
-        """Engine frame-ring step (HIP only): write frames[:, slot] + the next first valid channel."""
+    # the ring step takes an env range (the split rollout steps one path group per launch, runtime/engine.py)
+    ring_ranges = True
+
+    def step_ring_into(self, actions, frames, slot, fc_in, fc_out, reward, done, epret, b0: int = 0, b1=None):
+        """Engine frame-ring step (HIP only): write frames[:, slot] + the next first valid channel, envs [b0, b1)."""
         from ..ops import envs as henv
-        henv.pong_step_ring_into(self, actions, frames, slot, fc_in, fc_out, reward, done, epret)
+        henv.pong_step_ring_into(self, actions, frames, slot, fc_in, fc_out, reward, done, epret, b0=b0, b1=b1)
 
     def step(self, actions: torch.Tensor):
         if self.backend == "hip":

@@ -53,10 +53,11 @@ _SIGS = {
                             c_int, c_long, c_float, c_float, P, P, P],
     "fast_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_long, c_float, c_float, P],
+    "launch_inv_group": [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P],
     "launch_pong_step_ring": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_int, c_int, c_uint, P],
     "launch_pong_step_ring_split": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int,
-                                    c_int, c_int, c_int, c_int, c_int, c_uint, c_int, P],
+                                    c_int, c_int, c_int, c_int, c_int, c_uint, c_int, c_int, P],
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_uint, c_int, P, P, P, P, P, P],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],

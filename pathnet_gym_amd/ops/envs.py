@@ -68,11 +68,14 @@ def pong_step_into(env, actions, obs_in, obs_out, reward, done, epret, b0: int =
               env.no_op_max, g[0], g[1], g[2], g[3], g[4], b0, _id_base(env), _lib.stream())
 
 
-def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done, epret):
+def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done, epret, b0: int = 0, b1=None):
     """Frame-ring engine path: write only the new newest frame plane frames[:, slot] of the ring
     [B][slots][160*120] and the next stack's first valid channel (csrc/envs.hip RING;
-    runtime/engine.py frame ring)."""
+    runtime/engine.py frame ring).  Envs [b0, b1) only (default all): one path group of the split rollout."""
     B = env.num_envs
+    b1 = B if b1 is None else b1
+    if not 0 <= b0 < b1 <= B:
+        raise ValueError(f"pong_step_ring_into: env range [{b0}, {b1}) outside [0, {B})")
     if not hasattr(env, "_st32"):
         pong_sync_to_device(env)
     _lib.check(actions, torch.int32, (B,), name="actions")
@@ -90,9 +93,9 @@ def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done,
     _lib.call("launch_pong_step_ring_split", env._st32.data_ptr(), env._ctr32.data_ptr(), actions.data_ptr(),
               env.num_actions, frames[0, slot].data_ptr(), frames.stride(0), fc_in.data_ptr(), fc_out.data_ptr(),
               env._tab32.data_ptr(),
-              reward.data_ptr(), done.data_ptr(), epret.data_ptr(), B, env.seed_int, env.frameskip,
-              env.max_episode_steps, env.no_op_max, g[0], g[1], g[2], g[3], g[4], _id_base(env), ring_split(B),
-              _lib.stream())
+              reward.data_ptr(), done.data_ptr(), epret.data_ptr(), b1, env.seed_int, env.frameskip,
+              env.max_episode_steps, env.no_op_max, g[0], g[1], g[2], g[3], g[4], _id_base(env), b0,
+              ring_split(b1 - b0), _lib.stream())
 
 
 def ring_split(B: int) -> int:

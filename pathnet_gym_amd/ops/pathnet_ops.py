@@ -218,6 +218,9 @@ class HipPathNet:
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
         self.inv_slot = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
         self.inv_cnt = torch.zeros(self.L, self.M, dtype=torch.int32, device=dev)
+        # split rollout (runtime/engine.py rollout groups): per path group (p0, np), the group's own inverse lists
+        # (group-local path indices, rebuilt on device at the start of every rollout) and fc slot planes
+        self._groups = {}
         lay_h = lay.heads
         self.heads_off = lay_h
         # fused LSTM cell: csrc/lstm.hip (bf16 copies of the fp32 master kernel) or, in fp32x, csrc/lstm_x3.hip (fp16
@@ -450,6 +453,42 @@ class HipPathNet:
         return (X.data_ptr() + xrow0 * xrow, Y.data_ptr() + row0 * yrow, bits.data_ptr() + row0 * brow,
                 m.act_idx.data_ptr() + p0 * self.L * self.M * i4, m.act_cnt.data_ptr() + p0 * self.L * i4)
 
+    @staticmethod
+    def _row_ptr(t: torch.Tensor, row: int) -> int:
+        """Address of row ``row`` of a [rows, features] buffer (the hi plane of an fp16 pair: lo stays x2_lo away)."""
+        return t.data_ptr() + row * t.shape[-1] * t.element_size()
+
+    def _bits_ptr(self, l: int, bits: torch.Tensor, row: int) -> int:
+        g = self.geoms[l]
+        per_row = g.HWo * bits.element_size() if g.kind == "conv" else bits.shape[-1] * bits.element_size()
+        return bits.data_ptr() + row * per_row
+
+    def _tab_ptrs(self, p0: int):
+        m = self.model
+        i4 = m.act_idx.element_size()
+        return m.act_idx.data_ptr() + p0 * self.L * self.M * i4, m.act_cnt.data_ptr() + p0 * self.L * i4
+
+    def prepare_group(self, p0: int, np_: int, rows: int):
+        """Allocate path group (p0, np_)'s inverse lists and fc slot planes (outside graph capture)."""
+        key = (p0, np_)
+        if key not in self._groups:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("path-group buffers first needed inside a graph capture")
+            dev = self.model.device
+            self._groups[key] = dict(
+                inv_path=torch.zeros(self.L, self.M, np_, dtype=torch.int32, device=dev),
+                inv_slot=torch.zeros(self.L, self.M, np_, dtype=torch.int32, device=dev),
+                inv_cnt=torch.zeros(self.L, self.M, dtype=torch.int32, device=dev),
+                ys=torch.empty(8 * self.M * rows * 256, dtype=torch.float32, device=dev))
+        return self._groups[key]
+
+    def group_inverse(self, p0: int, np_: int):
+        """Rebuild group (p0, np_)'s inverse lists from the population's (csrc/ga.hip inv_group_kernel)."""
+        g = self._groups[(p0, np_)]
+        _lib.call("launch_inv_group", self.inv_path.data_ptr(), self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(),
+                  self.model.P, self.L, self.M, p0, np_, g["inv_path"].data_ptr(), g["inv_slot"].data_ptr(),
+                  g["inv_cnt"].data_ptr(), _lib.stream())
+
     def layer_fwd(self, l: int, X: torch.Tensor, Y: torch.Tensor, bits: torch.Tensor, P: int, E: int, T: int,
                   t0: int, bits_rows: int, row0: int = 0, p0: int = 0, xrow0: Optional[int] = None):
         """Forward of layer l for P paths x E envs x T steps from step t0.  row0/p0/xrow0: a one-step window of
@@ -471,7 +510,7 @@ class HipPathNet:
             _lib.check(Y, torch.float32, name="Y")
             return self._layer_fwd_f32(l, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st)
         if self.x3:
-            return self._layer_fwd_x3(l, X, Y, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st)
+            return self._layer_fwd_x3(l, X, Y, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st, p0)
         if g.kind == "conv":
             if (E * g.HWo) % 16 != 0:
                 raise ValueError(f"layer {l}: envs_per_path*Ho*Wo must be a multiple of 16")
@@ -588,7 +627,7 @@ class HipPathNet:
             return t.data_ptr(), 0
         return t.data_ptr(), x2_lo(t)
 
-    def _layer_fwd_x3(self, l, X, Y, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st):
+    def _layer_fwd_x3(self, l, X, Y, xp, yp, bp, aip, acp, P, E, T, t0, bits_rows, out_scale, st, p0=0):
         g = self.geoms[l]
         flat = self.model.store.flat
         last = l == self.L - 1
@@ -602,12 +641,21 @@ class HipPathNet:
                                 flat.data_ptr(), g.b_off, g.chunk, aip, acp, l, self.L, self.M, g.Hin, g.Win, g.Cin,
                                 g.KH, g.KW, g.S, P, E, T, t0, bits_rows, g.in_scale, out_scale, st)
         elif self.fc_fwd_mm and g.Cout == 256 and (g.K >= self.fc_fwd_mm_min_k or P * T * E <= self.fc_fwd_mm_small_rows) \
-                and P == self.model.P and aip == self.model.act_idx.data_ptr():
-            # module-major: each module's weight slice read once per 64 rows of the paths using it
-            ys = self._ys_buffer_x3(P * T * E)
+                and ((P == self.model.P and aip == self.model.act_idx.data_ptr()) or (p0, P) in self._groups):
+            # module-major: each module's weight slice read once per 64 rows of the paths using it (a path group:
+            # its own inverse lists and slot planes, so two groups' launches never share scratch)
+            if P == self.model.P and p0 == 0:
+                inv = (self.inv_path, self.inv_slot, self.inv_cnt)
+                ys = self._ys_buffer_x3(P * T * E)
+            else:
+                grp = self._groups[(p0, P)]
+                inv = (grp["inv_path"], grp["inv_slot"], grp["inv_cnt"])
+                ys = grp["ys"]
+                if ys.numel() < 8 * self.M * P * T * E * 256:
+                    raise RuntimeError(f"path group ({p0}, {P}): fc slot planes too small for {T * E} rows per path")
             ok = _lib.call_fast("x3_fc_fwd_mm", xp, x2_lo(X), g.ldx, yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
-                                flat.data_ptr(), g.b_off, g.chunk, acp, aip, self.inv_path.data_ptr(),
-                                self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), ys.data_ptr(), l, self.L, self.M,
+                                flat.data_ptr(), g.b_off, g.chunk, acp, aip, inv[0].data_ptr(),
+                                inv[1].data_ptr(), inv[2].data_ptr(), ys.data_ptr(), l, self.L, self.M,
                                 g.K, g.KP, g.Cout, P, E, T, t0, bits_rows, out_scale, st)
         else:
             ok = _lib.call_fast("x3_fc_fwd", xp, x2_lo(X), g.ldx, yp, ylo, bp, self.Wc[l].data_ptr(), wlo,
@@ -618,7 +666,7 @@ class HipPathNet:
                                "(fc layers take <= 32 rows per path and launch)")
 
     def conv23_fwd(self, l: int, X, Y1, bits1, rows1: int, Y2, bits2, rows2: int, P: int, E: int, T: int,
-                   t0: int) -> bool:
+                   t0: int, row0: int = 0, p0: int = 0) -> bool:
         """fp32x: the forwards of conv layers l (39x29x8 4x4/s2) and l + 1 (18x13x8 3x3/s1) in ONE launch
         (csrc/trunk_x3.hip conv23_fwd_tile_x3, bit-identical to two layer_fwd calls).  False when the pair does not
         have those geometries (the caller then runs layer_fwd twice).  PATHNET_X3_FUSE23=0 disables it."""
@@ -631,11 +679,18 @@ class HipPathNet:
         m = self.model
         for t, nm in ((Y1, "Y1"), (Y2, "Y2")):
             _lib.check(t, torch.float16, name=nm)
-        return _lib.call_fast("x3_conv23_fwd", X.data_ptr(), x2_lo(X), Y1.data_ptr(), x2_lo(Y1), bits1.data_ptr(), rows1,
-                              self.Wc[l].data_ptr(), self.Wc[l][0].numel(), g1.b_off, g1.chunk, Y2.data_ptr(), x2_lo(Y2),
-                              bits2.data_ptr(), rows2, self.Wc[l + 1].data_ptr(), self.Wc[l + 1][0].numel(), g2.b_off,
-                              g2.chunk, m.store.flat.data_ptr(), m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L,
-                              self.M, P, E, T, t0, 1.0, 1.0, _lib.stream())
+        if row0 or p0:
+            # one step of path group p0..p0+P-1 (runtime/engine.py split rollout): every operand at the group's
+            # first sample row row0, the active-module tables at path p0; the kernel sees P paths at t0 = 0
+            if t0 != 0 or T != 1 or p0 + P > m.P or row0 + P * E > min(X.shape[0] * X.shape[1], Y2.shape[0] * Y2.shape[1]):
+                raise ValueError(f"conv23_fwd: path-group window (row0={row0}, p0={p0}, P={P}) out of range")
+        aip, acp = self._tab_ptrs(p0)
+        return _lib.call_fast("x3_conv23_fwd", self._row_ptr(X, row0), x2_lo(X), self._row_ptr(Y1, row0), x2_lo(Y1),
+                              self._bits_ptr(l, bits1, row0), rows1, self.Wc[l].data_ptr(), self.Wc[l][0].numel(),
+                              g1.b_off, g1.chunk, self._row_ptr(Y2, row0), x2_lo(Y2), self._bits_ptr(l + 1, bits2, row0),
+                              rows2, self.Wc[l + 1].data_ptr(), self.Wc[l + 1][0].numel(), g2.b_off, g2.chunk,
+                              m.store.flat.data_ptr(), aip, acp, l, self.L, self.M, P, E, T, t0, 1.0, 1.0,
+                              _lib.stream())
 
     def _ys_buffer_x3(self, rows: int) -> torch.Tensor:
         """fp32 module-slot planes [8][M][rows][256] of the module-major fc forward (up to eight k-part planes of
@@ -850,17 +905,35 @@ class HipPathNet:
         if frames.shape[1] < steps + 3 or fc.numel() < steps * P * E:
             raise ValueError("frame ring too short for the requested steps")
 
-    def ring_fwd(self, frames, fc, Y, bits, P: int, E: int, T: int, t0: int, bits_rows: int):
+    def ring_fwd(self, frames, fc, Y, bits, P: int, E: int, T: int, t0: int, bits_rows: int, p0: int = 0,
+                 np_: Optional[int] = None):
+        """First layer on the frame ring, P paths x E envs x T steps from t0.  p0/np_ (fp32x): paths p0..p0+np_-1 of
+        step t0 only (one group of the split rollout): frames, fc, Y, bits and the module tables are passed at the
+        group's base (frames at env p0*E, slot t0; fc and the output rows at row t0*P*E + p0*E), so the kernel
+        sees np_ paths at t0 = 0."""
         self._check_ring(frames, fc, P, E, t0 + T)
         g = self.geoms[0]
         m = self.model
         out_scale = self.out_scale_last if self.L == 1 else 1.0
+        grouped = np_ is not None and (p0, np_) != (0, P)
+        if grouped and (not self.x3 or T != 1 or p0 < 0 or np_ <= 0 or p0 + np_ > P):
+            raise ValueError(f"ring_fwd: path group (p0={p0}, np={np_}) needs fp32x, T = 1 and paths within {P}")
         if self.x3:
             _lib.check(Y, torch.float16, name="Y")
-            ok = _lib.call_fast("x3_conv1_ring_fwd", frames.data_ptr(), fc.data_ptr(), Y.data_ptr(), x2_lo(Y),
-                                bits.data_ptr(), self.Wc[0].data_ptr(), self.Wc[0][0].numel(), m.store.flat.data_ptr(),
-                                g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), self.L, self.M, P, E, T,
-                                t0, frames.shape[1], bits_rows, g.in_scale, out_scale, _lib.stream())
+            if grouped:
+                B = P * E
+                row0 = t0 * B + p0 * E
+                fp = frames.data_ptr() + (p0 * E * frames.shape[1] + t0) * frames.shape[2]
+                aip, acp = self._tab_ptrs(p0)
+                args = (fp, fc.data_ptr() + row0, self._row_ptr(Y, row0), x2_lo(Y), self._bits_ptr(0, bits, row0),
+                        aip, acp, np_, 0)
+            else:
+                args = (frames.data_ptr(), fc.data_ptr(), Y.data_ptr(), x2_lo(Y), bits.data_ptr(),
+                        m.act_idx.data_ptr(), m.act_cnt.data_ptr(), P, t0)
+            fp, fcp, yp, ylo, bp, aip, acp, Pk, t0k = args
+            ok = _lib.call_fast("x3_conv1_ring_fwd", fp, fcp, yp, ylo, bp, self.Wc[0].data_ptr(), self.Wc[0][0].numel(),
+                                m.store.flat.data_ptr(), g.b_off, g.chunk, aip, acp, self.L, self.M, Pk, E, T, t0k,
+                                frames.shape[1], bits_rows, g.in_scale, out_scale, _lib.stream())
             if not ok:
                 raise RuntimeError(f"fp32x: frame-ring forward has no kernel for P={P}, E={E}, M={self.M}")
             return

@@ -23,6 +23,7 @@ the MI355X replacement for the reference's per-step ``sess.run`` over gRPC
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -155,21 +156,33 @@ class HipEngine:
         # torch-implemented games (envs/atari_games.py) are stepped eagerly, outside hipGraphs
         self.env_graph_safe = getattr(env, "graph_safe", True)
         self.use_graph = bool(cfg.use_graph) and not self.hybrid and self.env_graph_safe
+        self.auto_group_max_paths = int(os.environ.get("PATHNET_AUTO_GROUP_MAX_PATHS", "0"))
         self.groups = self._rollout_groups(getattr(cfg, "rollout_groups", 0))
         self.side_streams = [torch.cuda.Stream(device=dev) for _ in range(self.groups - 1)]
+        if self.groups > 1 and self.ring:
+            for g in range(self.groups):
+                p0, np_ = self._group_range(g)
+                hp.prepare_group(p0, np_, rows=np_ * E)
         self.load_obs(env)
 
     def _rollout_groups(self, want: int) -> int:
         """Path groups of the split rollout (TrainConfig.rollout_groups): each group's forward + env step chain
-        runs on its own stream.  Needs per-range launches: the packed-stack Pong kernel (pong_step_into b0/b1),
-        the trunk forward (HipPathNet.layer_fwd row0/p0) and the heads (heads_fwd b0/b1)."""
-        ok = (self.pixels and not self.ring and not self.lstm_hip and not self.hybrid
-              and not hasattr(self.env, "step_into") and self.env_graph_safe)
+        runs on its own stream (a branch of the rollout hipGraph).  Needs per-range launches: the Pong kernels
+        (pong_step_into / pong_step_ring_into b0/b1), the trunk forward (HipPathNet.layer_fwd row0/p0; on the frame
+        ring, fp32x: ring_fwd / conv23_fwd at the group's base and the module-major fc forward on the group's own
+        inverse lists) and the heads (heads_fwd b0/b1).  0 = auto = one group: two were 3 % slower at 64 paths in
+        bf16 (round 1), and on the fp32x frame ring (profiles/r5/groups_sweep.md) 3.43 (1) / 3.45 (2) / 3.81 (4) ms
+        at 8 paths, 4.31 / 4.37 / 4.76 at 16, 6.13 / 6.33 at 32: a 4-path group's kernels take as long as the
+        8-path ones (their latency is one workgroup's chain) and two concurrent chains run ~1.55x, not 2x, the
+        work of one.  PATHNET_AUTO_GROUP_MAX_PATHS=N makes auto pick two groups at <= N paths."""
+        packed = (self.pixels and not self.ring and not hasattr(self.env, "step_into"))
+        ring = self.ring and self.hip.x3 and getattr(self.env, "ring_ranges", False)
+        ok = (packed or ring) and not self.lstm_hip and not self.hybrid and self.env_graph_safe
         if want == 0:
-            want = 1       # measured: two groups 3 % slower at the bench shape (TrainConfig.rollout_groups)
+            want = 2 if (ring and ok and self.P <= self.auto_group_max_paths and self.P % 2 == 0) else 1
         if want > 1 and (not ok or self.P % want != 0):
-            raise ValueError(f"rollout_groups={want} needs a packed-stack pixel env without LSTM and paths "
-                             f"({self.P}) divisible by it")
+            raise ValueError(f"rollout_groups={want} needs a packed-stack pixel env (or the fp32x frame ring with a "
+                             f"ranged env step) without LSTM and paths ({self.P}) divisible by it")
         return max(1, want)
 
     # -- observation double buffer -------------------------------------------
@@ -270,6 +283,10 @@ class HipEngine:
         env = self.env
         if grp is not None:
             p0, np_ = self._group_range(grp)
+            if self.ring:
+                env.step_ring_into(self.actions[t], self.frames, t + 4, self.fc[t], self.fc[t + 1], self.rewards[t],
+                                   self.dones[t], self.epret[t], b0=p0 * self.E, b1=(p0 + np_) * self.E)
+                return
             henv.pong_step_into(env, self.actions[t], self._obs_at(t), self._obs_at(t + 1), self.rewards[t],
                                 self.dones[t], self.epret[t], b0=p0 * self.E, b1=(p0 + np_) * self.E)
             return
@@ -292,14 +309,24 @@ class HipEngine:
     def _trunk_step(self, t, grp=None):
         hp = self.hip
         if self.ring:
-            hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0])
+            if grp is None:
+                p0, np_, t0, row0 = 0, self.P, t, 0
+                hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0])
+            else:
+                # one path group: every launch at the group's first row of step t, the kernels at t0 = 0
+                p0, np_ = self._group_range(grp)
+                t0, row0 = 0, t * self.B + p0 * self.E
+                hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0],
+                            p0=p0, np_=np_)
             l = 1
             while l < len(hp.geoms):
-                if l + 1 < len(hp.geoms) and hp.conv23_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l], self.bits_rows[l], self.acts[l + 1],
-                                 self.bits[l + 1], self.bits_rows[l + 1], self.P, self.E, 1, t):
+                if l + 1 < len(hp.geoms) and hp.conv23_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l],
+                                                           self.bits_rows[l], self.acts[l + 1], self.bits[l + 1],
+                                                           self.bits_rows[l + 1], np_, self.E, 1, t0, row0=row0, p0=p0):
                     l += 2
                     continue
-                hp.layer_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l], self.P, self.E, 1, t, self.bits_rows[l])
+                hp.layer_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l], np_, self.E, 1, t0, self.bits_rows[l],
+                             row0=row0, p0=p0)
                 l += 1
             return
         p0, np_ = self._group_range(grp)
@@ -473,6 +500,12 @@ class HipEngine:
         streams = [cur] + self.side_streams
         for s in self.side_streams:
             s.wait_stream(cur)
+        if self.ring:
+            # the groups' module-major fc forwards read inverse lists of their own paths, cut from the population's
+            # (which the last optimizer step's device GA, or the host GA, rewrote)
+            for g, s in enumerate(streams):
+                with torch.cuda.stream(s):
+                    self.hip.group_inverse(*self._group_range(g))
         for t in range(T + 1):
             for g, s in enumerate(streams):
                 with torch.cuda.stream(s):

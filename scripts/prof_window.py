@@ -35,6 +35,20 @@ def main(path, updates, title):
             tot[name] += int(r[t1k]) - t
             calls[name] += 1
     total = sum(tot.values())
+    # busy time = union of the window's dispatch intervals: below the summed kernel time when launches of
+    # different streams (the split rollout's path groups) overlap
+    iv = sorted((int(r[t0k]), int(r[t1k])) for r in rows
+                if lo < int(r[t0k]) < hi and "prof_window_marker" not in r[key])
+    busy, cur0, cur1 = 0, None, None
+    for a, b in iv:
+        if cur1 is None or a > cur1:
+            if cur1 is not None:
+                busy += cur1 - cur0
+            cur0, cur1 = a, b
+        else:
+            cur1 = max(cur1, b)
+    if cur1 is not None:
+        busy += cur1 - cur0
     out = [f"# {title}", "", f"source: `{path}` (rocprofv3 --kernel-trace); {updates} timed updates between the "
            f"bench.py --prof-window markers; wall between markers {(hi - lo) / 1e6 / updates:.3f} ms per update", "",
            "| kernel | calls/update | avg us | ms/update | % |", "|---|---:|---:|---:|---:|"]
@@ -42,6 +56,8 @@ def main(path, updates, title):
         out.append(f"| `{name[:70] if not by_grid else name[:50] + name[name.rfind(' ['):]}` | {calls[name] / updates:.1f} | {tot[name] / calls[name] / 1e3:.1f} | "
                    f"{tot[name] / 1e6 / updates:.3f} | {100 * tot[name] / total:.1f} |")
     out.append(f"| **total GPU kernel time** | | | **{total / 1e6 / updates:.2f}** | 100 |")
+    out.append(f"| **GPU busy (union of dispatch intervals)** | | | **{busy / 1e6 / updates:.2f}** | "
+               f"{100 * busy / max(total, 1):.0f} |")
     return "\n".join(out) + "\n"
 
 

@@ -109,3 +109,65 @@ def test_rollout_groups_rejects_unsupported():
     cfg.rollout_groups = 2
     with pytest.raises(ValueError):
         PathNetTrainer(cfg, device=DEV)
+
+
+def _run_x3_ring(groups, graph, updates=4, paths=8):
+    """fp32x on the frame ring with a zero learning rate: the weights never move, so every rollout is a pure function
+    of the (deterministic) env and GA state and the float-atomic gradient order cannot leak into later updates."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = paths, 16, 5
+    cfg.compute_dtype = "fp32x"
+    cfg.frame_ring = True
+    cfg.use_graph = graph
+    cfg.ga.backend = "device"
+    cfg.ga.concurrent_tournaments = 2
+    cfg.a2c.lr = 0.0
+    cfg.rollout_groups = groups
+    tr = PathNetTrainer(cfg, device=DEV)
+    e = tr.engine
+    assert e.ring and e.groups == (groups or e.groups)
+    tr.env.max_episode_steps = 7          # episode ends + auto-resets inside the compared rollouts
+    snaps = []
+    for _ in range(updates):              # eager, capture, replays (the device GA fires tournaments in between)
+        tr.update()
+        torch.cuda.synchronize()
+        snaps.append({"obs": e.obs_stacks().clone(), "actions": e.actions.clone(), "logits": e.logits.clone(),
+                      "values": e.values.clone(), "rewards": e.rewards.clone(), "dones": e.dones.clone(),
+                      "acts": [a.clone() for a in e.acts], "bits": [b.clone() for b in e.bits],
+                      "act_idx": tr.model.act_idx.clone()})
+    tr.flush()
+    return tr, snaps
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_x3_ring_split_rollout_is_bit_identical(hip_lib, graph):
+    """fp32x frame ring, two path groups (ranged ring env step, ring_fwd / conv23_fwd at the group's base, the
+    module-major fc forward on group inverse lists): every update's observations, actions, logits, activations and
+    ReLU bits equal the one-stream rollout's, through the eager update, the capture and replays, and across the
+    genotype changes of device-GA tournaments."""
+    _, ref = _run_x3_ring(1, graph)
+    tr, got = _run_x3_ring(2, graph)
+    assert tr.engine.groups == 2
+    assert not torch.equal(ref[0]["act_idx"], ref[-1]["act_idx"]) or tr.pop.generation > 0
+    for u, (a, b) in enumerate(zip(ref, got)):
+        for k in a:
+            if isinstance(a[k], list):
+                for i, (x, y) in enumerate(zip(a[k], b[k])):
+                    assert torch.equal(x, y), (u, k, i)
+            else:
+                assert torch.equal(a[k], b[k]), (u, k)
+
+
+def test_x3_ring_auto_groups(hip_lib, monkeypatch):
+    """rollout_groups = 0 (auto): one group (measured: two never paid, runtime/engine.py _rollout_groups);
+    PATHNET_AUTO_GROUP_MAX_PATHS=16 picks two at <= 16 paths on the fp32x frame ring, one at 32."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    for limit, paths, want in (("0", 8, 1), ("16", 8, 2), ("16", 16, 2), ("16", 32, 1)):
+        monkeypatch.setenv("PATHNET_AUTO_GROUP_MAX_PATHS", limit)
+        cfg = preset("pong")
+        cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = paths, 16, 2
+        cfg.compute_dtype = "fp32x"
+        cfg.frame_ring = True
+        cfg.rollout_groups = 0
+        assert PathNetTrainer(cfg, device=DEV).engine.groups == want, (limit, paths)
