@@ -34,6 +34,7 @@ namespace x3 {
 #define X3_MAXM 16
 #define X3_NCT 5          // column tiles of a full layer (M <= 10)
 #define X3_RING_FCS 1024  // frame-ring weight gradient: first-valid-channel bytes staged per workgroup
+#define X3_C1_FWD_FCS 128  // frame-ring band forward: first-valid-channel bytes staged per workgroup
 #define X3_W0_SHIFT 8     // first-layer weights enter the fp16 MFMA as W * 2^8 (hi/lo pair)
 
 template <int HIN_, int WIN_, int CIN_, int KH_, int KW_, int S_, bool U8_>
@@ -578,6 +579,9 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
   __shared__ __attribute__((aligned(16))) float bias_s[NCXT * 16];
   __shared__ float wsum_s[NCXT * 16];
   __shared__ int mods[X3_MAXM];
+  // RING: the first-valid channel of every sample of the workgroup's bands, staged once.  Read per band from global
+  // memory it put a dependent byte load (and a full vmcnt wait) in front of every band's frame loads.
+  __shared__ uint8_t fcs[RING ? X3_C1_FWD_FCS : 1];
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
   const int nct = (cnt + 1) >> 1;
@@ -589,6 +593,14 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
   const int b_end = min(nbands, b_beg + bands_per_wg);
   if (b_beg >= b_end) return;
   if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  const int s_first = b_beg / B::NB;
+  if constexpr (RING) {
+    const int ns = (b_end - 1) / B::NB - s_first + 1;     // <= X3_C1_FWD_FCS (launcher caps bands_per_wg)
+    for (int i = tid; i < ns; i += 256) {
+      const int s = s_first + i, st = s / E, e = s - st * E;
+      fcs[i] = fcv[(long)(t0 + st) * PE + (long)p * E + e];
+    }
+  }
   const int npass = nct > NCXT ? (nct + NCXT - 1) / NCXT : 1;
   static_assert(B::CIT == 5, "five named staging registers");
   uint4 rg0, rg1, rg2, rg3, rg4;                       // (an indexed array captured by the lambdas went to scratch)
@@ -607,7 +619,7 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
   auto ring_src = [&](int u, int j) {
     const int s = u / B::NB, oh0 = (u - s * B::NB) * B::OBR;
     const int st = s / E, e = s - st * E;
-    const int fc = (int)fcv[(long)(t0 + st) * PE + (long)p * E + e];
+    const int fc = (int)fcs[s - s_first];
     const long slot0 = (long)(p * E + e) * nslots + t0 + st;
     const int c = min(tid + 256 * j, B::NCH - 1);
     const int r = c / (G::WIN / 4), cc = c - r * (G::WIN / 4);
@@ -3750,6 +3762,7 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
   const long nbands = (long)T * E * BD1<C1>::NB;
   long bpw = (nbands * P + 511) / 512;
   if (bpw < 2) bpw = 2;
+  if (bpw > (X3_C1_FWD_FCS - 2) * BD1<C1>::NB) bpw = (X3_C1_FWD_FCS - 2) * BD1<C1>::NB;   // staged fc bytes
   if (X3_C1_F16B)
     conv1_fwd_band_x2<C1, true, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
         (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
