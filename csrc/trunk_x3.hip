@@ -1262,7 +1262,7 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
                                                             int P, int E, int T, long bits_rows, int units_per_wg,
                                                             float in_scale, float g_scale,
                                                             const uint8_t* __restrict__ fcv, int nslots,
-                                                            const float* __restrict__ gamax) {
+                                                            const float* __restrict__ gamax, int pmap) {
   using SB = Slab<G, OB>;
   static_assert(!RING || (G::U8 && G::CIN == 4 && G::WIN % 4 == 0), "ring input: uint8 4-channel first layer");
   // ring: 4-pixel groups per slab (one 16-byte LDS store each; 8-pixel groups, one round of loads but four stores
@@ -1273,7 +1273,10 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
   __shared__ uint8_t fcs[FCS];
   constexpr bool XL = !G::U8;                       // bf16 input: lo plane too
   constexpr int NXP = XL ? 2 : 1;
-  constexpr int GS = NCXP * 16 + 8;
+  // G rows: 48 elements (24 dwords) apart, so the 8 rows one lane group of a transposed B read touches land on 8
+  // disjoint 8-bank windows (40 put rows q and q + 3 on shared banks)
+  constexpr int GS = 48;
+  static_assert(NCXP * 16 <= GS, "column tiles of a pass fit a G row");
   constexpr int NMT = G::KP / 16;
   constexpr int MPW = NMT / 4;
   constexpr int GROWS = SB::KS * 32;
@@ -1305,11 +1308,16 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
   for (int ks = 0; ks < SB::KS; ++ks)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      int rho = ks * 32 + 8 * grp + 4 * hf + q;
+      // position of k-slot (grp, hf, q) of k-step ks.  pmap 1: lanes 0-31 of one transposed read take 8 consecutive
+      // positions (64 consecutive dwords of the slab: every bank once); pmap 0 (round 4): positions p and p + 8,
+      // 64 dwords apart, two lanes per bank on every read.  The B reads below use the same map, so the MFMA sums
+      // the same 32 products per k-step in another slot order.
+      int rho = ks * 32 + (pmap ? 16 * hf + 4 * grp : 8 * grp + 4 * hf) + q;
       if (rho >= SB::NPOS) rho = 0;                     // padded position: its G row is zero
       const int ob = rho / G::WO, ow = rho - ob * G::WO;
       aoff[ks][hf] = ob * G::S * SB::RL + ow * SB::PS + 4 * pp;
     }
+  const int r0 = pmap ? 4 * grp : 8 * grp, r1 = pmap ? 16 + 4 * grp : 8 * grp + 4;   // B rows of k-slots hf = 0, 1
   const int npass = (nct + NCXP - 1) / NCXP;
   const float gs = g16_scale(gamax), ginv = 1.0f / gs;   // G16: the staged gradient is the fp16 pair of G * 2^e
   using XRaw = typename std::conditional<G::U8, uint2, s8v>::type;
@@ -1476,8 +1484,8 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
         s8v bh[NC], bl[NC];
 #pragma unroll
         for (int nt = 0; nt < NC; ++nt) {
-          const int o0 = (ks * 32 + 8 * grp + q) * GS + nt * 16 + 4 * pp;
-          const int o1 = (ks * 32 + 8 * grp + 4 + q) * GS + nt * 16 + 4 * pp;
+          const int o0 = (ks * 32 + r0 + q) * GS + nt * 16 + 4 * pp;
+          const int o1 = (ks * 32 + r1 + q) * GS + nt * 16 + 4 * pp;
           bh[nt] = tr8(Gs[buf][0] + o0, Gs[buf][0] + o1);
           bl[nt] = tr8(Gs[buf][1] + o0, Gs[buf][1] + o1);
         }
@@ -3635,6 +3643,8 @@ static int X3_DG_FOLD = 2;
 // (units per workgroup = units * P / target, >= 8); conv input gradients: ~X3_DG_TARGET (samples per workgroup >= 2);
 // 0 = the fixed per-path sizes (24 / 32 chunks per path).
 static int X3_WG_TARGET = 1536;
+// slab weight gradient: k-slot -> position map of the transposed operand reads (conv_wgrad_slab_x3 pmap)
+static int X3_SLAB_PMAP = 1;
 static int X3_DG_TARGET = 2048;
 // module-major fc forward k split: 0 = auto by rows (P*T*E <= 256: 8 parts, else 2), else the fixed part count (2 / 4 /
 // 8), capped so every part keeps >= 2 k-steps
@@ -3660,6 +3670,7 @@ void fast_conv_set_x3_c1_f16b(int v) { X3_C1_F16B = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
+void fast_conv_set_x3_slab_pmap(int v) { X3_SLAB_PMAP = v ? 1 : 0; }
 void fast_conv_set_x3_wg_target(int v) { X3_WG_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_dg_target(int v) { X3_DG_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_fc_ks_parts(int v) { X3_FC_KS_PARTS = (v == 2 || v == 4 || v == 8) ? v : 0; }
@@ -3825,19 +3836,19 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (X3_C1_WG_NCX == 2 && X3_WGRAD_PF != 1)       // 2 tiles per pass: two stages in flight fit (162 VGPRs)
     conv_wgrad_slab_x3<C1, 2, 2, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots, gamax);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP);
   else if (X3_C1_WG_NCX == 2)
     conv_wgrad_slab_x3<C1, 2, 1, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots, gamax);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP);
   else if (X3_WGRAD_PF == 2)
     conv_wgrad_slab_x3<C1, 2, 2, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots, gamax);
+                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP);
   else
     conv_wgrad_slab_x3<C1, 2, 1, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots, gamax);
+                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
@@ -3863,11 +3874,11 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     if (pf == 2)
       conv_wgrad_slab_x3<Gx, OB, 2><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
                                                           ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs, nullptr,
-                                                          0, gamax);
+                                                          0, gamax, X3_SLAB_PMAP);
     else
       conv_wgrad_slab_x3<Gx, OB, 1><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
                                                           ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs, nullptr,
-                                                          0, gamax);
+                                                          0, gamax, X3_SLAB_PMAP);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   };

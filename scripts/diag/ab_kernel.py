@@ -1,0 +1,82 @@
+"""Interleaved A/B timing of one engine kernel under two (or more) kernel-option settings, in ONE process on the
+same data: a bench window per setting drifts by +-10 % between runs on one box (clock / thermal state), which
+swamps a 5 % kernel change.  Example:
+
+    python scripts/diag/ab_kernel.py --kernel ring_wgrad --opt x3_slab_pmap=0 --opt x3_slab_pmap=1
+"""
+import argparse
+import json
+import statistics
+import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+from pathnet_gym_amd.algo.trainer import PathNetTrainer  # noqa: E402
+from pathnet_gym_amd.config import preset  # noqa: E402
+from pathnet_gym_amd.ops import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="ring_wgrad", choices=["ring_wgrad", "ring_fwd", "conv23_fwd", "layer_bwd"])
+    ap.add_argument("--layer", type=int, default=1)
+    ap.add_argument("--opt", action="append", default=[], help="name=value (fast_conv_set_<name>); one per arm")
+    ap.add_argument("--paths", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=6)
+    a = ap.parse_args()
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = a.paths, 32, 20
+    cfg.compute_dtype = "fp32x"
+    cfg.frame_ring = True
+    cfg.ga.backend = "device"
+    tr = PathNetTrainer(cfg, device="cuda")
+    for _ in range(2):
+        tr.update()
+    tr.flush()
+    torch.cuda.synchronize()
+    e, hp = tr.engine, tr.engine.hip
+    P, E, T = e.P, e.E, e.T
+    scratch = torch.zeros_like(e.grad_flat)
+
+    def run():
+        if a.kernel == "ring_wgrad":
+            hp.ring_wgrad(e.frames, e.fc, e.grads[0], e.bits[0], scratch, P, E, T, e.bits_rows[0])
+        elif a.kernel == "ring_fwd":
+            hp.ring_fwd(e.frames, e.fc, e.acts[0], e.bits[0], P, E, 1, 3, e.bits_rows[0])
+        elif a.kernel == "conv23_fwd":
+            hp.conv23_fwd(1, e.acts[0], e.acts[1], e.bits[1], e.bits_rows[1], e.acts[2], e.bits[2], e.bits_rows[2],
+                          P, E, 1, 3)
+        else:
+            l = a.layer
+            hp.layer_bwd(l, e.acts[l - 1], e.grads[l], e.bits[l], scratch, e.grads[l - 1], P, E, T, e.bits_rows[l])
+
+    arms = a.opt or ["none=0"]
+    lib = _lib.lib()
+
+    def setopt(kv):
+        k, v = kv.split("=")
+        if k != "none":
+            getattr(lib, "fast_conv_set_" + k)(int(v))
+
+    times = {kv: [] for kv in arms}
+    for r in range(a.rounds):
+        for kv in (arms if r % 2 == 0 else arms[::-1]):
+            setopt(kv)
+            run()
+            torch.cuda.synchronize()
+            s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.reps):
+                run()
+            t.record()
+            torch.cuda.synchronize()
+            times[kv].append(s.elapsed_time(t) / a.reps * 1e3)
+    out = {kv: {"median_us": round(statistics.median(v), 1), "all_us": [round(x, 1) for x in v]} for kv, v in times.items()}
+    print(json.dumps({"kernel": a.kernel, "paths": a.paths, "arms": out}))
+
+
+if __name__ == "__main__":
+    main()
