@@ -3829,7 +3829,11 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (M > 2 * X3_NCT) return 0;
   using SB = Slab<C1, 2>;
   const long units = (long)T * E * SB::NB;
-  long upw = X3_WG_TARGET > 0 ? (units * P + X3_WG_TARGET - 1) / X3_WG_TARGET : (units + 23) / 24;
+  // X3_WG_TARGET workgroups, up to twice that while every workgroup keeps >= 256 stages (interleaved A/B,
+  // scripts/diag/ab_kernel.py: 64 paths 1766 (1536) -> 1722 us (3072); 32 paths 888 vs 898; 8 paths 299 vs 375)
+  long wgs = X3_WG_TARGET;
+  if (wgs > 0) wgs = std::max(wgs, std::min(2 * wgs, units * P / 256));
+  long upw = wgs > 0 ? (units * P + wgs - 1) / wgs : (units + 23) / 24;
   if (upw < 8) upw = 8;
   if (upw / SB::NB + 2 > X3_RING_FCS) return -22;       // the workgroup's first-valid bytes fit the LDS table
   const dim3 grid((unsigned)((units + upw - 1) / upw), P);

@@ -22,7 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="ring_wgrad", choices=["ring_wgrad", "ring_fwd", "conv23_fwd", "layer_bwd"])
     ap.add_argument("--layer", type=int, default=1)
-    ap.add_argument("--opt", action="append", default=[], help="name=value (fast_conv_set_<name>); one per arm")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="one arm: name=value[,name=value...] (fast_conv_set_<name>); give every varied name in every arm")
     ap.add_argument("--paths", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=6)
@@ -56,12 +57,16 @@ def main():
     arms = a.opt or ["none=0"]
     lib = _lib.lib()
 
-    def setopt(kv):
-        k, v = kv.split("=")
-        if k != "none":
-            getattr(lib, "fast_conv_set_" + k)(int(v))
+    def setopt(arm):
+        for kv in arm.split(","):
+            k, v = kv.split("=")
+            if k != "none":
+                getattr(lib, "fast_conv_set_" + k)(int(v))
 
     times = {kv: [] for kv in arms}
+    for kv in arms:                       # one untimed pass per arm (first-touch / clock ramp)
+        setopt(kv)
+        run()
     for r in range(a.rounds):
         for kv in (arms if r % 2 == 0 else arms[::-1]):
             setopt(kv)
