@@ -559,8 +559,10 @@ DEVI uint4 planes_to_px4(uint4 v) {
 // F16B: the band is converted to fp16 (1024 + v) ONCE while it is staged (single LDS buffer of 2 x 17.3 KB, one more
 // barrier per band) instead of per MFMA operand read: every pixel of an 8x8/s4 band feeds 4 positions x 2 kernel
 // rows, so the per-read conversion (v_perm per 2 pixels) ran ~4x per pixel
-template <class G, bool RING = false, bool PIPE = false, bool F16B = false>
-__global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
+// SB1: ONE uint8 band buffer (17.3 KB; one more barrier per band, like F16B) so that the workgroup's 51 KB of LDS
+// lets three workgroups share a CU (3 waves / SIMD, <= 168 VGPRs) instead of two
+template <class G, bool RING = false, bool PIPE = false, bool F16B = false, bool SB1 = false>
+__global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                            long ylo, uint8_t* __restrict__ bits,
                                                            const uint16_t* __restrict__ Wh, long wlo,
                                                            const float* __restrict__ flat, long bias_off, int chunk,
@@ -573,8 +575,9 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
   constexpr int KPs = G::KP + 8;
   constexpr int NK = G::KP / 32;
   constexpr int NCXT = 2;
-  static_assert(!(F16B && PIPE), "F16B: plain k loop");
-  __shared__ __attribute__((aligned(16))) uint8_t Xb[F16B ? 1 : 2][F16B ? 2 * B::BYTES : B::BYTES];
+  static_assert(!(F16B && PIPE) && !(SB1 && (F16B || PIPE)), "F16B / SB1: plain k loop, one band buffer");
+  constexpr bool ONEBUF = F16B || SB1;
+  __shared__ __attribute__((aligned(16))) uint8_t Xb[ONEBUF ? 1 : 2][F16B ? 2 * B::BYTES : B::BYTES];
   __shared__ __attribute__((aligned(16))) uint16_t Ws[2][NCXT * 16 * KPs];
   __shared__ __attribute__((aligned(16))) float bias_s[NCXT * 16];
   __shared__ float wsum_s[NCXT * 16];
@@ -703,7 +706,7 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
     auto run = [&](auto ncc) {
       constexpr int NC = decltype(ncc)::value;
       int buf = 0;
-      for (int u = b_beg; u < b_end; ++u, buf ^= (F16B ? 0 : 1)) {
+      for (int u = b_beg; u < b_end; ++u, buf ^= (ONEBUF ? 0 : 1)) {
         __syncthreads();                               // band u in LDS (and bias_s); buf ^ 1 free
         if (u + 1 < b_end) load_band(u + 1);
         const int s = u / B::NB, oh0 = (u - s * B::NB) * B::OBR;
@@ -794,7 +797,7 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_band_x2(const uint8_t* __res
           conv_epi_sw<NC>(acc[i], bias_s, ct0, cnt, q, in_scale, out_scale, growb + pos, bits, bits_rows, Y, ylo,
                           pass > 0, valid);
         }
-        if constexpr (F16B) {
+        if constexpr (ONEBUF) {
           if (u + 1 < b_end) {
             __syncthreads();                           // every wave done with band u (one buffer)
             store_band(0);
@@ -3629,6 +3632,7 @@ static int X3_WG3_TILE = 1;
 // 25.3 us paired vs 26.0-26.2 single (32.5-32.7 in slow runs), 3x3 18.4-18.8 paired vs 15.9-16.2 single
 static int X3_FWD_TILE = 3;
 static int X3_C1_F16B = 0;     // band forward: 1 = the band converted to fp16 once at staging (conv1_fwd_band_x2 F16B)
+static int X3_C1_SB1 = 0;      // band forward (ring): 1 = one band buffer, three workgroups per CU (conv1_fwd_band_x2 SB1)
 static int X3_C1_PIPE = 0;     // band forward: 1 = next k-step's LDS fragments read during this k-step's MFMAs
 static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
 // input gradients (conv_dgrad_x3, fc_dgrad_gemm_x3): 1 = the weights as THREE fp16 pieces (a fourth MFMA per k-step),
@@ -3665,6 +3669,7 @@ void fast_conv_set_x3_dg_w3(int v) { X3_DG_W3 = v; }
 void fast_conv_set_x3_dg_fold(int v) { X3_DG_FOLD = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
 void fast_conv_set_x3_c1_band(int v) { X3_C1_BAND = v; }
+void fast_conv_set_x3_c1_sb1(int v) { X3_C1_SB1 = v; }
 void fast_conv_set_x3_c1_pipe(int v) { X3_C1_PIPE = v; }
 void fast_conv_set_x3_c1_f16b(int v) { X3_C1_F16B = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
@@ -3774,7 +3779,11 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
   long bpw = (nbands * P + 511) / 512;
   if (bpw < 2) bpw = 2;
   if (bpw > (X3_C1_FWD_FCS - 2) * BD1<C1>::NB) bpw = (X3_C1_FWD_FCS - 2) * BD1<C1>::NB;   // staged fc bytes
-  if (X3_C1_F16B)
+  if (X3_C1_SB1)
+    conv1_fwd_band_x2<C1, true, false, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
+        (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+  else if (X3_C1_F16B)
     conv1_fwd_band_x2<C1, true, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
         (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
         ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);

@@ -20,7 +20,7 @@ from pathnet_gym_amd.ops import _lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="ring_wgrad", choices=["ring_wgrad", "ring_fwd", "conv23_fwd", "layer_bwd"])
+    ap.add_argument("--kernel", default="ring_wgrad", choices=["ring_wgrad", "ring_fwd", "conv23_fwd", "layer_bwd", "layer_fwd"])
     ap.add_argument("--layer", type=int, default=1)
     ap.add_argument("--opt", action="append", default=[],
                     help="one arm: name=value[,name=value...] (fast_conv_set_<name>); give every varied name in every arm")
@@ -50,6 +50,9 @@ def main():
         elif a.kernel == "conv23_fwd":
             hp.conv23_fwd(1, e.acts[0], e.acts[1], e.bits[1], e.bits_rows[1], e.acts[2], e.bits[2], e.bits_rows[2],
                           P, E, 1, 3)
+        elif a.kernel == "layer_fwd":
+            l = a.layer
+            hp.layer_fwd(l, e.acts[l - 1], e.acts[l], e.bits[l], P, E, 1, 3, e.bits_rows[l])
         else:
             l = a.layer
             hp.layer_bwd(l, e.acts[l - 1], e.grads[l], e.bits[l], scratch, e.grads[l - 1], P, E, T, e.bits_rows[l])
