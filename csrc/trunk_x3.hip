@@ -105,6 +105,24 @@ DEVI void mask8(const float (&g)[8], uint32_t b, float (&m)[8]) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) m[c] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, g[c]) & mk[c]);
 }
+// an fp16 pair (hi, lo) of 8 values masked by the ReLU bits b (bit c: channel c): the pair of the masked values, since
+// the split of 0 is (0, 0).  Per dword j (channels 2j, 2j+1): the two sign-extended bits joined by one v_perm.
+DEVI void mask_pair8(const s8v& hi, const s8v& lo, uint32_t b, s8v& mh, s8v& ml) {
+  const uint32_t m[4] = {__builtin_amdgcn_perm(sbfe1<1>(b), sbfe1<0>(b), 0x07060100u),
+                         __builtin_amdgcn_perm(sbfe1<3>(b), sbfe1<2>(b), 0x07060100u),
+                         __builtin_amdgcn_perm(sbfe1<5>(b), sbfe1<4>(b), 0x07060100u),
+                         __builtin_amdgcn_perm(sbfe1<7>(b), sbfe1<6>(b), 0x07060100u)};
+  uint32_t h[4], l[4];
+  __builtin_memcpy(h, &hi, 16);
+  __builtin_memcpy(l, &lo, 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    h[j] &= m[j];
+    l[j] &= m[j];
+  }
+  __builtin_memcpy(&mh, h, 16);
+  __builtin_memcpy(&ml, l, 16);
+}
 DEVI void split8(const float (&v)[8], s8v& hi, s8v& lo) {
   uint32_t h[4], l[4];
 #pragma unroll
@@ -1998,7 +2016,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
                                                        const int* __restrict__ act_cnt, int layer, int L, int M, int P,
                                                        int E, int T, long bits_rows, float g_scale,
                                                        float* __restrict__ dX, int samples_per_wg,
-                                                       const float* __restrict__ gamax, float* __restrict__ gamax_out) {
+                                                       const float* __restrict__ gamax, float* __restrict__ gamax_out,
+                                                       int presplit) {
   using D = DGM<G>;
   constexpr int S = D::S;
   constexpr int NTAPP = (D::NTAP + 3) & ~3;
@@ -2111,13 +2130,21 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
         if (pos < G::HOWO) {
           const float gg[8] = {g0r[j].x * g_scale, g0r[j].y * g_scale, g0r[j].z * g_scale, g0r[j].w * g_scale,
                                g1r[j].x * g_scale, g1r[j].y * g_scale, g1r[j].z * g_scale, g1r[j].w * g_scale};
+          // presplit: the fp16 pair of G * 2^e once per position, masked per slot (bit-identical to masking the fp32
+          // values and splitting per slot, at a quarter of the conversions)
+          s8v ph, pl;
+          if (presplit) split8hs(gg, gs, ph, pl);
 #pragma unroll
           for (int a4 = 0; a4 < 4; ++a4) {
             const int b = (int)gbr[j][(4 * g + a4) < 12 ? 4 * g + a4 : 0] * (4 * g + a4 < cnt ? 1 : 0);
-            float m[8];
-            mask8(gg, (uint32_t)b, m);
             s8v hi, lo;
-            split8hs(m, gs, hi, lo);
+            if (presplit) {
+              mask_pair8(ph, pl, (uint32_t)b, hi, lo);
+            } else {
+              float m[8];
+              mask8(gg, (uint32_t)b, m);
+              split8hs(m, gs, hi, lo);
+            }
             const int o = pos * X3_DG_PSTR + (a4 ^ dg_swz(pos)) * 8;
             *reinterpret_cast<s8v*>(Gs[0] + o) = hi;
             *reinterpret_cast<s8v*>(Gs[1] + o) = lo;
@@ -3649,6 +3676,8 @@ static int X3_DG_FOLD = 2;
 static int X3_WG_TARGET = 1536;
 // slab weight gradient: k-slot -> position map of the transposed operand reads (conv_wgrad_slab_x3 pmap)
 static int X3_SLAB_PMAP = 1;
+// staged output gradients: 1 = one fp16-pair split per value, masked per slot (mask_pair8); 0 = mask, then split per slot
+static int X3_PRESPLIT = 1;
 static int X3_DG_TARGET = 2048;
 // module-major fc forward k split: 0 = auto by rows (P*T*E <= 256: 8 parts, else 2), else the fixed part count (2 / 4 /
 // 8), capped so every part keeps >= 2 k-steps
@@ -3675,6 +3704,7 @@ void fast_conv_set_x3_c1_f16b(int v) { X3_C1_F16B = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
+void fast_conv_set_x3_presplit(int v) { X3_PRESPLIT = v ? 1 : 0; }
 void fast_conv_set_x3_slab_pmap(int v) { X3_SLAB_PMAP = v ? 1 : 0; }
 void fast_conv_set_x3_wg_target(int v) { X3_WG_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_dg_target(int v) { X3_DG_TARGET = v < 0 ? 0 : v; }
@@ -3943,13 +3973,13 @@ int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_o
   if (x3_is<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                                    \
     if (X3_DG_FOLD == 2)                                                                                           \
       conv_dgrad_x3<Gx, false, true><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac,     \
-                                                           layer, L, M, P, E, T, br, gs, dX, spw, gamax, gamax_out); \
+                                                           layer, L, M, P, E, T, br, gs, dX, spw, gamax, gamax_out, X3_PRESPLIT); \
     else if (X3_DG_W3)                                                                                             \
       conv_dgrad_x3<Gx, true><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, \
-                                                    M, P, E, T, br, gs, dX, spw, gamax, gamax_out);                 \
+                                                    M, P, E, T, br, gs, dX, spw, gamax, gamax_out, X3_PRESPLIT);    \
     else                                                                                                           \
       conv_dgrad_x3<Gx><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P,  \
-                                              E, T, br, gs, dX, spw, gamax, gamax_out);                            \
+                                              E, T, br, gs, dX, spw, gamax, gamax_out, X3_PRESPLIT);               \
     const int rc = (int)hipGetLastError();                                                                         \
     return rc ? -rc : 1;                                                                                           \
   }

@@ -173,6 +173,7 @@ _SIGS = {
     "fast_conv_set_x3_wg_target": [c_int],
     "fast_conv_set_x3_slab_pmap": [c_int],
     "fast_conv_set_x3_c1_sb1": [c_int],
+    "fast_conv_set_x3_presplit": [c_int],
     "fast_conv_set_x3_dg_target": [c_int],
     "fast_conv_set_x3_fc_ks_parts": [c_int],
     "conv_fwd_smem": [c_int, c_int],

@@ -485,6 +485,29 @@ def test_x3_dgrad_accumulation_variants_match_plain_chain(x3_rollout, l):
         assert rel(gw, gws[0]) < 1e-6
 
 
+@pytest.mark.parametrize("l", [1, 2])
+def test_x3_dgrad_presplit_staging_bit_equal(x3_rollout, l):
+    """conv_dgrad_x3 staging the output gradient's fp16 pair once per position and masking it per slot (X3_PRESPLIT,
+    csrc/trunk_x3.hip mask_pair8) == masking the fp32 values and splitting per slot: the split of 0 is (0, 0), so the
+    input gradient is bit-identical."""
+    from pathnet_gym_amd.ops import _lib
+    tr, eng, _, _, _ = x3_rollout
+    hp = tr.model.hip
+    lib = _lib.lib()
+    dxs = []
+    for on in (0, 1):
+        lib.fast_conv_set_x3_presplit(on)
+        dX = eng.grads[l - 1]
+        dX.fill_(float("nan"))
+        hp.layer_bwd(l, eng.acts[l - 1], eng.grads[l], eng.bits[l], torch.zeros_like(eng.grad_flat), dX, eng.P,
+                     eng.E, eng.T, eng.bits_rows[l], part="d")
+        torch.cuda.synchronize()
+        dxs.append(dX[:eng.T * eng.B].clone())
+    lib.fast_conv_set_x3_presplit(1)
+    assert torch.isfinite(dxs[0]).all() and dxs[0].norm() > 0
+    assert torch.equal(dxs[0], dxs[1])
+
+
 @pytest.mark.parametrize("l", [3, 4])
 def test_x3_fc_dgrad_gemm_matches_streaming_kernel(x3_rollout, l):
     """fc_gm_x3 + fc_dgrad_gemm_x3 (per-path GEMM over (slot, column) with LDS-staged 128 x 256 tiles) == fc_dgrad_x3
