@@ -121,6 +121,15 @@ DEVI uint32_t wang_hash(uint32_t x) {
   return x;
 }
 
+// action-sampling RNG (heads.hip Gumbel-max, trunk_x3.hip fused heads): a uniform in (0, 1) keyed by
+// (seed, update counter x step, sample, action)
+DEVI float sample_u01(uint32_t seed, uint32_t stepkey, uint32_t b, uint32_t j) {
+  uint32_t h = wang_hash(stepkey * 64u + j);
+  h = wang_hash(h ^ b);
+  h = wang_hash(h ^ seed);
+  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
 DEVI uint32_t env_rand_u32(uint32_t seed, uint32_t env_id, uint32_t counter, uint32_t stream) {
   uint32_t h = wang_hash(counter * 4u + stream);
   h = wang_hash(h ^ env_id);

@@ -13,13 +13,8 @@
 
 #define AMAX 32
 
-// key for the sampling RNG: depends on (seed, update counter, step, sample, action)
-DEVI float u01(uint32_t seed, uint32_t stepkey, uint32_t b, uint32_t j) {
-  uint32_t h = wang_hash(stepkey * 64u + j);
-  h = wang_hash(h ^ b);
-  h = wang_hash(h ^ seed);
-  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
-}
+// key for the sampling RNG: depends on (seed, update counter, step, sample, action) (common.h sample_u01)
+DEVI float u01(uint32_t seed, uint32_t stepkey, uint32_t b, uint32_t j) { return sample_u01(seed, stepkey, b, j); }
 
 // trunk features are bf16 (bf16 engine) or fp32 (compute_dtype = "fp32", csrc/trunk_f32.hip)
 DEVI float ldfeat(const bf16_t* p) { return bf2f(*p); }
@@ -177,8 +172,10 @@ __global__ __launch_bounds__(256) void heads_fwd_s16_kernel(
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const float* wr = Wl + (f + jj) * AW;
+      // explicit fused multiply-adds: the contraction is then the same in every kernel that repeats this sum
+      // (trunk_x3.hip fc_heads_fwd_x3 is bit-identical to this kernel)
 #pragma unroll
-      for (int j = 0; j < AW; ++j) acc[j] += x[jj] * wr[j];
+      for (int j = 0; j < AW; ++j) acc[j] = __builtin_fmaf(x[jj], wr[j], acc[j]);
     }
   }
 #pragma unroll

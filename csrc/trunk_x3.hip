@@ -2358,6 +2358,175 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const uint16_t* __restrict__ X,
 }
 
 // ===========================================================================
+// the last trunk fc layer (fp32 output) + the actor-critic heads + action sampling in ONE launch, for the rollout's
+// one-step forwards: a workgroup = one path x 16 sample rows, wave w = output columns [64w, 64w + 64) of EVERY active
+// module in slot order.  Per module the 16 x 64 tile is fc_fwd_x3's (same fragments, same k order, same epilogue and
+// ReLU bits) and the wave keeps fc_fwd_x3's four per-wave slot partials (slots k, k + 4, ...) in registers and sums
+// them in the same order; the 16 x 256 feature rows go to Y and to LDS, and the heads run heads_fwd_s16_kernel<8, float>'s
+// arithmetic on them (16 feature slices x 16 samples, slices summed in order).  Bit-identical to the two launches;
+// one launch and no feature round trip instead of two chains of ~8-16 us each.
+// grid = (ceil(E / 16), P), T = 1.
+// ===========================================================================
+template <int NKS, int D>
+__global__ __launch_bounds__(256) void fc_heads_fwd_x3(const uint16_t* __restrict__ X, long xlo, int ldx,
+                                                       float* __restrict__ Y, uint16_t* __restrict__ bits,
+                                                       const uint16_t* __restrict__ Wc, long wlo,
+                                                       const float* __restrict__ flat, long bias_off, int chunk,
+                                                       const int* __restrict__ act_idx, const int* __restrict__ act_cnt,
+                                                       int layer, int L, int M, int P, int E, int t0, long bits_rows,
+                                                       float in_scale, float out_scale, long pw, long pb, long vw,
+                                                       long vb, int A, float* __restrict__ logits,
+                                                       float* __restrict__ value, int* __restrict__ actions,
+                                                       uint32_t seed, const long long* __restrict__ ctr, int t,
+                                                       int Tsteps, int greedy, uint32_t rb) {
+  constexpr int COUT = 256, KP = NKS * 32, F = COUT, AM = 8, AW = AM + 1, NWORDS = COUT / 16;
+  __shared__ __attribute__((aligned(16))) float feat_s[16][F + 4];
+  __shared__ float Wl[F * AW];
+  __shared__ float red[16 * AW * 16];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int PE = P * E;
+  const int row0 = (int)blockIdx.x * 16;
+  const int col0 = w * 64;
+  // heads weights [F][AW] (policy columns zero-padded to AM, then the value weight): independent of the fc work
+  for (int i = tid; i < F * AW; i += 256) {
+    const int f = i / AW, j = i - f * AW;
+    Wl[i] = j == AM ? flat[vw + f] : (j < A ? flat[pw + (long)f * A + j] : 0.f);
+  }
+  const long xrow = sample_global(p, row0 + c16 < E ? row0 + c16 : row0, E, PE, t0) * ldx;
+  long sgb[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = row0 + 4 * grp + r;
+    sgb[r] = sample_global(p, row < E ? row : row0, E, PE, t0);
+  }
+  // slot partials as fc_fwd_x3's waves keep them (partial k = slots k, k + 4, ... in order), summed in order below
+  float tot[4][4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tot[k][j][r] = 0.f;
+  for (int a = 0; a < cnt; ++a) {
+    const int ka = a & 3;                 // the partial this slot joins (adding 0.f to the others is exact)
+    const int mod = act_idx[(p * L + layer) * M + a];
+    const uint16_t* Wm = Wc + (long)mod * COUT * KP + (long)(col0 + c16) * KP + 8 * grp;
+    f4v acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
+    s8v ah[D], al[D], bh[D][4], bl[D][4];
+    auto load = [&](int d, int kk) {
+      ah[d] = *reinterpret_cast<const s8v*>(X + xrow + kk + 8 * grp);
+      al[d] = *reinterpret_cast<const s8v*>(X + xlo + xrow + kk + 8 * grp);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bh[d][j] = *reinterpret_cast<const s8v*>(Wm + (long)j * 16 * KP + kk);
+        bl[d][j] = *reinterpret_cast<const s8v*>(Wm + wlo + (long)j * 16 * KP + kk);
+      }
+    };
+    auto mma = [&](int d) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = mma3h(ah[d], al[d], bh[d][j], bl[d][j], acc[j]);
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (d < NKS) load(d, d * 32);
+    int s = 0;
+#pragma unroll
+    for (; s + 2 * D <= NKS; s += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        mma(d);
+        load(d, (s + d + D) * 32);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (s + d < NKS) {
+        mma(d);
+        if (s + d + D < NKS) load(d, (s + d + D) * 32);
+      }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (s + D + d < NKS) mma(d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float bb = flat[bias_off + (long)mod * chunk + col0 + j * 16 + c16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[j][r] * in_scale + bb;
+        const bool pos = v > 0.f;
+        const float pv = pos ? v : 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tot[k][j][r] += ka == k ? pv : 0.f;
+        const uint64_t bal = __ballot(pos);
+        if (c16 == 0 && row0 + 4 * grp + r < E)
+          bits[((long)a * bits_rows + sgb[r]) * NWORDS + (col0 + j * 16) / 16] =
+              (uint16_t)((bal >> (16 * grp)) & 0xFFFFull);
+      }
+    }
+  }
+  // features: Y (the heads backward and the next update's inputs read it) and the LDS rows of the heads
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int lr = 4 * grp + r;
+      const float y = (((tot[0][j][r] + tot[1][j][r]) + tot[2][j][r]) + tot[3][j][r]) * out_scale;
+      feat_s[lr][col0 + j * 16 + c16] = row0 + lr < E ? y : 0.f;
+      if (row0 + lr < E) Y[sgb[r] * COUT + col0 + j * 16 + c16] = y;
+    }
+  __syncthreads();
+  // heads_fwd_s16_kernel: thread (feature slice fs, sample sl)
+  const int fs = tid >> 4, sl = tid & 15;
+  const bool valid = row0 + sl < E;
+  float hacc[AW];
+#pragma unroll
+  for (int j = 0; j < AW; ++j) hacc[j] = 0.f;
+  constexpr int FQ = F / 16;
+  for (int f = fs * FQ; f < fs * FQ + FQ; f += 8) {
+    float x[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) x[jj] = feat_s[sl][f + jj];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const float* wr = Wl + (f + jj) * AW;
+#pragma unroll
+      for (int j = 0; j < AW; ++j) hacc[j] = __builtin_fmaf(x[jj], wr[j], hacc[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < AW; ++j) red[(fs * AW + j) * 16 + sl] = hacc[j];
+  __syncthreads();
+  if (fs != 0 || !valid) return;
+#pragma unroll
+  for (int j = 0; j < AW; ++j) {
+    float v = 0.f;
+    for (int k = 0; k < 16; ++k) v += red[(k * AW + j) * 16 + sl];
+    hacc[j] = v;
+  }
+  const int b = p * E + row0 + sl;                     // the sample's row of this step's [B] buffers
+  const uint32_t stepkey = (uint32_t)(ctr[0] * Tsteps + t);
+  int best = 0;
+  float bv = -3.0e38f;
+#pragma unroll
+  for (int j = 0; j < AM; ++j) {
+    if (j < A) {
+      const float lg = hacc[j] + flat[pb + j];
+      logits[(long)b * A + j] = lg;
+      float sc = lg;
+      if (!greedy) sc += -__logf(-__logf(sample_u01(seed, stepkey, rb + (uint32_t)b, (uint32_t)j)));
+      if (sc > bv) { bv = sc; best = j; }
+    }
+  }
+  value[b] = hacc[AM] + flat[vb];
+  actions[b] = best;
+}
+
+// ===========================================================================
 // fc forward, split-K: fc_fwd_x3 with KS waves per module (KS x 256 threads), each summing 1/KS of the k-steps;
 // the partial accumulators of a module meet in LDS before its bias + ReLU.  The rollout's fc launches have one
 // workgroup per (path, 64 columns) -- 256 workgroups at the bench shape -- so the module-per-wave kernel runs one
@@ -3678,6 +3847,7 @@ static int X3_WG_TARGET = 1536;
 static int X3_SLAB_PMAP = 1;
 // staged output gradients: 1 = one fp16-pair split per value, masked per slot (mask_pair8); 0 = mask, then split per slot
 static int X3_PRESPLIT = 1;
+static int X3_FH_D = 3;        // fused last fc + heads: k-steps of fragments in flight (fc_heads_fwd_x3 D)
 static int X3_DG_TARGET = 2048;
 // module-major fc forward k split: 0 = auto by rows (P*T*E <= 256: 8 parts, else 2), else the fixed part count (2 / 4 /
 // 8), capped so every part keeps >= 2 k-steps
@@ -3704,6 +3874,7 @@ void fast_conv_set_x3_c1_f16b(int v) { X3_C1_F16B = v; }
 void fast_conv_set_x3_fc_d(int d) { X3_FC_D = d; }
 void fast_conv_set_x3_fc_ks(int ks) { X3_FC_KS = ks; }
 void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
+void fast_conv_set_x3_fh_d(int v) { X3_FH_D = v; }
 void fast_conv_set_x3_presplit(int v) { X3_PRESPLIT = v ? 1 : 0; }
 void fast_conv_set_x3_slab_pmap(int v) { X3_SLAB_PMAP = v ? 1 : 0; }
 void fast_conv_set_x3_wg_target(int v) { X3_WG_TARGET = v < 0 ? 0 : v; }
@@ -4024,6 +4195,28 @@ int x3_fc_fwd(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, c
     if (of) FCX(2, 4, 0, true); else FCX(2, 4, 0, false);
   }
 #undef FCX
+  const int rc = (int)hipGetLastError();
+  return rc ? -rc : 1;
+}
+
+// the last fc layer + heads of one rollout step (fc_heads_fwd_x3); 0 = shape not covered (the caller runs the two
+// launches).  logits / value / actions: step t's [B] rows.
+int x3_fc_heads_fwd(const void* X, long xlo, int ldx, float* Y, void* bits, const void* Wc, long wlo,
+                    const float* flat, long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M,
+                    int K, int KP, int Cout, int P, int E, int t0, long br, float os, long pw, long pb, long vw,
+                    long vb, int A, float* logits, float* value, int* actions, unsigned seed, const long long* ctr,
+                    int t, int Tsteps, int greedy, unsigned rb, hipStream_t st) {
+  if (!X || !Y || !bits || !Wc || !flat || !ai || !ac || !logits || !value || !actions || !ctr || ldx <= 0 ||
+      chunk <= 0 || L <= 0 || M <= 0 || P <= 0 || E <= 0 || t0 < 0 || br <= 0 || bias_off < 0 || xlo <= 0 ||
+      wlo <= 0 || A <= 0) return -22;
+  if (M > X3_MAXM || Cout != 256 || K != 256 || KP != 256 || ldx % 8 != 0 || ldx < KP || E > 32 || A > 8) return 0;
+#define FHX(D_)                                                                                                    \
+  fc_heads_fwd_x3<8, D_><<<dim3((unsigned)((E + 15) / 16), (unsigned)P), 256, 0, st>>>(                             \
+      (const uint16_t*)X, xlo, ldx, Y, (uint16_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, layer, \
+      L, M, P, E, t0, br, 1.f / (float)(1 << X3_W0_SHIFT), os, pw, pb, vw, vb, A, logits, value, actions, seed, ctr, t,  \
+      Tsteps, greedy, rb)
+  if (X3_FH_D >= 3) FHX(3); else FHX(2);
+#undef FHX
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }

@@ -141,6 +141,9 @@ _SIGS = {
     "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P, P, P],
     "x3_fc_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 10
                  + [c_long, c_float, P],
+    "x3_fc_heads_fwd": [P, c_long, c_int, P, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 9
+                       + [c_long, c_float, c_long, c_long, c_long, c_long, c_int, P, P, P, c_uint, P, c_int, c_int,
+                          c_int, c_uint, P],
     "x3_fc_fwd_mm": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P, P, P, P, P] + [c_int] * 10
                     + [c_long, c_float, P],
     "x3_fc_dgrad": [P, P, P, c_long, P, P] + [c_int] * 9 + [c_long, c_float, P, P, c_long, P, P, P],
@@ -174,6 +177,7 @@ _SIGS = {
     "fast_conv_set_x3_slab_pmap": [c_int],
     "fast_conv_set_x3_c1_sb1": [c_int],
     "fast_conv_set_x3_presplit": [c_int],
+    "fast_conv_set_x3_fh_d": [c_int],
     "fast_conv_set_x3_dg_target": [c_int],
     "fast_conv_set_x3_fc_ks_parts": [c_int],
     "conv_fwd_smem": [c_int, c_int],

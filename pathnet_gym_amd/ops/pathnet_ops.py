@@ -213,6 +213,11 @@ class HipPathNet:
         self.fc_fwd_mm_small_rows = int(os.environ.get("PATHNET_X3_FC_MM_SMALL_ROWS", "0"))
         # conv2 + conv3 forward in one launch per rollout step (conv23_fwd)
         self.fuse23 = os.environ.get("PATHNET_X3_FUSE23", "1") != "0"
+        # the last fc layer + heads + sampling of a rollout step in one launch (fc_heads_fwd): bit-identical but
+        # measured slower (42 us vs 25 us for fc_fwd_x3 + heads at 64 and at 8 paths, scripts/diag/ab_kernel.py: one
+        # wave walks every module of its 64 columns in turn, where fc_fwd_x3 gives each module its own wave and each
+        # column tile its own workgroup), so off; PATHNET_X3_FUSE_HEADS=1 turns it on
+        self.fuse_heads = os.environ.get("PATHNET_X3_FUSE_HEADS", "0") == "1"
         self.fc_wgrad_gm_wgs = int(os.environ.get("PATHNET_X3_FC_WGRAD_WGS", "768"))    # target workgroup count
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
@@ -969,6 +974,32 @@ class HipPathNet:
             return torch.zeros(self.M, rows, dtype=torch.uint8, device=dev), rows
         rows = steps * B
         return torch.zeros(self.M, rows, g.Cout // 16, dtype=torch.int16, device=dev), rows
+
+    def fc_heads_fwd(self, X, Y, bits, bits_rows: int, logits, value, actions, seed, ctr, t: int, T: int, P: int,
+                     E: int, t0: int, greedy=False, task=0, row_base=0) -> bool:
+        """fp32x: the last trunk layer (an fc layer of 256 outputs over 256 inputs) AND the heads + sampling of one
+        rollout step in one launch (csrc/trunk_x3.hip fc_heads_fwd_x3: bit-identical to layer_fwd + heads_fwd).
+        X / Y / bits: the layer's full [steps, B, ...] buffers (step t0's rows are used); logits / value / actions:
+        step t's [B] rows.  False when the shape is not covered (the caller then runs the two launches);
+        PATHNET_X3_FUSE_HEADS=0 disables it."""
+        l = self.L - 1
+        g = self.geoms[l]
+        m = self.model
+        if not (self.x3 and self.fuse_heads and g.kind == "fc" and self.lstm is None and l > 0):
+            return False
+        h = m.store.layout.heads[task if m.cfg.per_task_heads else 0]
+        _lib.check(Y, torch.float32, name="Y")
+        B = P * E
+        if X.shape[-2] != B or Y.shape[-2] != B or logits.numel() < B * m.cfg.num_actions or value.numel() < B \
+                or actions.numel() < B:
+            raise ValueError("fc_heads_fwd: buffers do not hold one step of P*E samples")
+        return _lib.call_fast("x3_fc_heads_fwd", X.data_ptr(), x2_lo(X), g.ldx, Y.data_ptr(), bits.data_ptr(),
+                              self.Wc[l].data_ptr(), self.Wc[l][0].numel(), m.store.flat.data_ptr(), g.b_off, g.chunk,
+                              m.act_idx.data_ptr(), m.act_cnt.data_ptr(), l, self.L, self.M, g.K, g.KP, g.Cout, P, E,
+                              t0, bits_rows, self.out_scale_last, h["pw"], h["pb"], h["vw"], h["vb"],
+                              m.cfg.num_actions, logits.data_ptr(), value.data_ptr(), actions.data_ptr(),
+                              seed & 0xFFFFFFFF, ctr.data_ptr(), t, T, int(greedy), int(row_base) & 0xFFFFFFFF,
+                              _lib.stream())
 
     def heads_fwd(self, feat, logits, value, actions, seed, ctr, t, T, greedy=False, task=0, b0=0, b1=None,
                   row_base=0):

@@ -306,8 +306,11 @@ class HipEngine:
             henv.cartpole_step_into(env, self.actions[t], self._obs_at(t + 1), self.rewards[t], self.dones[t],
                                     self.epret[t])
 
-    def _trunk_step(self, t, grp=None):
+    def _trunk_step(self, t, grp=None, skip_last=False):
+        """Trunk forward of step t (one path group, or all); ``skip_last``: every layer but the last (the caller runs
+        the last layer fused with the heads)."""
         hp = self.hip
+        nl = len(hp.geoms) - (1 if skip_last else 0)
         if self.ring:
             if grp is None:
                 p0, np_, t0, row0 = 0, self.P, t, 0
@@ -319,8 +322,8 @@ class HipEngine:
                 hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0],
                             p0=p0, np_=np_)
             l = 1
-            while l < len(hp.geoms):
-                if l + 1 < len(hp.geoms) and hp.conv23_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l],
+            while l < nl:
+                if l + 1 < nl and hp.conv23_fwd(l, self.acts[l - 1], self.acts[l], self.bits[l],
                                                            self.bits_rows[l], self.acts[l + 1], self.bits[l + 1],
                                                            self.bits_rows[l + 1], np_, self.E, 1, t0, row0=row0, p0=p0):
                     l += 2
@@ -332,7 +335,7 @@ class HipEngine:
         p0, np_ = self._group_range(grp)
         x, xrow0 = self._obs_x(t)
         row0 = t * self.B + p0 * self.E
-        for l in range(len(hp.geoms)):
+        for l in range(nl):
             hp.layer_fwd(l, x, self.acts[l], self.bits[l], np_, self.E, 1, 0, self.bits_rows[l], row0=row0, p0=p0,
                          xrow0=xrow0 + p0 * self.E if l == 0 else None)
             x = self.acts[l]
@@ -380,8 +383,28 @@ class HipEngine:
         if forked:
             main.wait_stream(side)
 
+    def _fused_heads(self) -> bool:
+        """fp32x rollout steps: the last fc layer, the heads and the sampling in one launch (HipPathNet.fc_heads_fwd)."""
+        hp = self.hip
+        L = len(hp.geoms)
+        return (hp.x3 and hp.fuse_heads and not self.lstm_hip and not self.hybrid and L > 1
+                and hp.geoms[-1].kind == "fc" and hp.geoms[-1].Cout == 256 and hp.geoms[-1].K == 256
+                and self.E <= 32 and self.A <= 8)
+
     def _forward_step(self, t, greedy=False, grp=None):
         hp = self.hip
+        if grp is None and self._fused_heads():
+            self._trunk_step(t, None, skip_last=True)
+            L = len(hp.geoms)
+            if hp.fc_heads_fwd(self.acts[L - 2], self.acts[L - 1], self.bits[L - 1], self.bits_rows[L - 1],
+                               self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t, self.T + 1,
+                               self.P, self.E, t, greedy=greedy, task=self.model.task, row_base=self.row_base):
+                return
+            hp.layer_fwd(L - 1, self.acts[L - 2], self.acts[L - 1], self.bits[L - 1], self.P, self.E, 1, t,
+                         self.bits_rows[L - 1])
+            hp.heads_fwd(self.acts[L - 1][t], self.logits[t], self.values[t], self.actions[t], self.seed, self.ctr, t,
+                         self.T + 1, greedy=greedy, task=self.model.task, row_base=self.row_base)
+            return
         self._trunk_step(t, grp)
         feat = self.acts[-1][t]
         if grp is not None:

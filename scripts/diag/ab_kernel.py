@@ -20,7 +20,7 @@ from pathnet_gym_amd.ops import _lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="ring_wgrad", choices=["ring_wgrad", "ring_fwd", "conv23_fwd", "layer_bwd", "layer_fwd"])
+    ap.add_argument("--kernel", default="ring_wgrad", choices=["ring_wgrad", "ring_fwd", "conv23_fwd", "layer_bwd", "layer_fwd", "fc_heads", "fc_then_heads"])
     ap.add_argument("--layer", type=int, default=1)
     ap.add_argument("--opt", action="append", default=[],
                     help="one arm: name=value[,name=value...] (fast_conv_set_<name>); give every varied name in every arm")
@@ -50,6 +50,14 @@ def main():
         elif a.kernel == "conv23_fwd":
             hp.conv23_fwd(1, e.acts[0], e.acts[1], e.bits[1], e.bits_rows[1], e.acts[2], e.bits[2], e.bits_rows[2],
                           P, E, 1, 3)
+        elif a.kernel == "fc_heads":
+            L = len(hp.geoms)
+            hp.fc_heads_fwd(e.acts[L - 2], e.acts[L - 1], e.bits[L - 1], e.bits_rows[L - 1], e.logits[3], e.values[3],
+                            e.actions[3], e.seed, e.ctr, 3, T + 1, P, E, 3)
+        elif a.kernel == "fc_then_heads":
+            L = len(hp.geoms)
+            hp.layer_fwd(L - 1, e.acts[L - 2], e.acts[L - 1], e.bits[L - 1], P, E, 1, 3, e.bits_rows[L - 1])
+            hp.heads_fwd(e.acts[L - 1][3], e.logits[3], e.values[3], e.actions[3], e.seed, e.ctr, 3, T + 1)
         elif a.kernel == "layer_fwd":
             l = a.layer
             hp.layer_fwd(l, e.acts[l - 1], e.acts[l], e.bits[l], P, E, 1, 3, e.bits_rows[l])

@@ -735,3 +735,38 @@ def test_x3_conv1_band_f16_staging_bit_equal(x3_ring_rollout, opt):
     setter(0)
     assert outs[0][0].float().abs().sum() > 0
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_x3_fused_fc_heads_bit_equal(hip_lib, monkeypatch, graph):
+    """fc_heads_fwd_x3 (the last fc layer + heads + Gumbel-max sampling of a rollout step in one launch,
+    csrc/trunk_x3.hip) == fc_fwd_x3 + heads_fwd_s16_kernel: features, ReLU bits, logits, values and sampled actions
+    bit for bit, over several updates (zero learning rate, so the float-atomic gradient order cannot leak into the
+    compared rollouts) through the eager update, the capture and replays."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    runs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("PATHNET_X3_FUSE_HEADS", fuse)
+        cfg = preset("pong")
+        cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 32, 5
+        cfg.compute_dtype = "fp32x"
+        cfg.frame_ring = True
+        cfg.use_graph = graph
+        cfg.ga.backend = "device"
+        cfg.a2c.lr = 0.0
+        tr = PathNetTrainer(cfg, device=DEV)
+        e = tr.engine
+        assert e._fused_heads() == (fuse == "1")
+        tr.env.max_episode_steps = 7
+        snaps = []
+        for _ in range(3):
+            tr.update()
+            torch.cuda.synchronize()
+            snaps.append((e.acts[-1].clone(), e.bits[-1].clone(), e.logits.clone(), e.values.clone(),
+                          e.actions.clone()))
+        tr.flush()
+        runs.append(snaps)
+    assert runs[0][0][2].abs().sum() > 0
+    for u, (a, b) in enumerate(zip(*runs)):
+        for k, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), (u, ("feat", "bits", "logits", "values", "actions")[k])
