@@ -121,6 +121,20 @@ DEVI uint32_t wang_hash(uint32_t x) {
   return x;
 }
 
+// heads accumulation acc[j] += x * w[j] (j < AW) as fused multiply-adds, pairs of j on v_pk_fma_f32, the odd one on
+// v_fma_f32: the same instructions in every kernel that repeats the heads sum (heads.hip, trunk_x3.hip fused heads)
+template <int AW>
+DEVI void heads_fma(float (&acc)[AW], float x, const float* w) {
+  typedef float hf2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int j = 0; j + 1 < AW; j += 2) {
+    const hf2 r = __builtin_elementwise_fma((hf2){x, x}, (hf2){w[j], w[j + 1]}, (hf2){acc[j], acc[j + 1]});
+    acc[j] = r[0];
+    acc[j + 1] = r[1];
+  }
+  if constexpr (AW % 2) acc[AW - 1] = __builtin_fmaf(x, w[AW - 1], acc[AW - 1]);
+}
+
 // action-sampling RNG (heads.hip Gumbel-max, trunk_x3.hip fused heads): a uniform in (0, 1) keyed by
 // (seed, update counter x step, sample, action)
 DEVI float sample_u01(uint32_t seed, uint32_t stepkey, uint32_t b, uint32_t j) {

@@ -171,11 +171,8 @@ __global__ __launch_bounds__(256) void heads_fwd_s16_kernel(
     ldfeat8(fr + f, x);
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      const float* wr = Wl + (f + jj) * AW;
-      // explicit fused multiply-adds: the contraction is then the same in every kernel that repeats this sum
-      // (trunk_x3.hip fc_heads_fwd_x3 is bit-identical to this kernel)
-#pragma unroll
-      for (int j = 0; j < AW; ++j) acc[j] = __builtin_fmaf(x[jj], wr[j], acc[j]);
+      // explicit fused multiply-adds (common.h heads_fma): trunk_x3.hip fc_heads_fwd_x3 repeats this sum bit for bit
+      heads_fma<AW>(acc, x[jj], Wl + (f + jj) * AW);
     }
   }
 #pragma unroll

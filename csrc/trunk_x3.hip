@@ -2254,8 +2254,11 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const uint16_t* __restrict__ X,
       const long row = row0 + i * 16 + 4 * grp + r;
       sgb[i][r] = sample_global(p, (int)(row < Rtot ? row : row0), E, PE, t0);
     }
+  // this wave's first module index goes out beside the count (the list is padded with -1 past it), so the first
+  // weight loads wait for one load level instead of two
+  const int mod_w = w < M ? act_idx[(p * L + layer) * M + w] : -1;
   for (int a = w; a < cnt; a += 4) {
-    const int mod = act_idx[(p * L + layer) * M + a];
+    const int mod = a == w ? mod_w : act_idx[(p * L + layer) * M + a];
     const uint16_t* Wm = Wc + (long)mod * Cout * KP + (long)(col0 + c16) * KP + 8 * grp;
     f4v acc[RT][4];
 #pragma unroll
@@ -2492,11 +2495,7 @@ __global__ __launch_bounds__(256) void fc_heads_fwd_x3(const uint16_t* __restric
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) x[jj] = feat_s[sl][f + jj];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const float* wr = Wl + (f + jj) * AW;
-#pragma unroll
-      for (int j = 0; j < AW; ++j) hacc[j] = __builtin_fmaf(x[jj], wr[j], hacc[j]);
-    }
+    for (int jj = 0; jj < 8; ++jj) heads_fma<AW>(hacc, x[jj], Wl + (f + jj) * AW);
   }
 #pragma unroll
   for (int j = 0; j < AW; ++j) red[(fs * AW + j) * 16 + sl] = hacc[j];
@@ -3029,7 +3028,18 @@ __global__ __launch_bounds__(256) void fc_slot_sum2_x3(const float* __restrict__
   const bool live = row < PR;
   const long rowc = live ? row : 0;
   const int p = (int)(rowc / R), r = (int)(rowc - (long)p * R);
+  // act_cnt and the slot's module index are loaded side by side (the index list is padded with -1 past the count,
+  // so it does not wait for it), and the first slot's partial planes go out with them: one dependent load level
+  // (the bias) instead of three in front of the first sum
   const int cnt = live ? act_cnt[p * L + layer] : 0;
+  const int mod0 = act_idx[(p * L + layer) * M];
+  float4 x0[KS], y0[KS];
+#pragma unroll
+  for (int kp = 0; kp < KS; ++kp) {
+    const float* src = Ys + (((long)kp * M) * PR + rowc) * COUT + c0;
+    x0[kp] = *reinterpret_cast<const float4*>(src);
+    y0[kp] = *reinterpret_cast<const float4*>(src + 4);
+  }
   const long sg = sample_global(p, r, E, P * E, t0);
   float o[8];
 #pragma unroll
@@ -3037,14 +3047,21 @@ __global__ __launch_bounds__(256) void fc_slot_sum2_x3(const float* __restrict__
   // the xor-1 partner is in the same row (32 lanes per row), so it runs the same slot count
   for (int a = 0; a < cnt; ++a) {
     float v[8];
-    const int mod = act_idx[(p * L + layer) * M + a];
+    const int mod = a == 0 ? mod0 : act_idx[(p * L + layer) * M + a];
     const float* bsrc = flat + bias_off + (long)mod * chunk + c0;      // (no alignment assumed)
 #pragma unroll
     for (int c = 0; c < 8; ++c) v[c] = bsrc[c];
 #pragma unroll
     for (int kp = 0; kp < KS; ++kp) {
-      const float* src = Ys + (((long)kp * M + a) * PR + row) * COUT + c0;
-      const float4 x = *reinterpret_cast<const float4*>(src), y = *reinterpret_cast<const float4*>(src + 4);
+      float4 x, y;
+      if (a == 0) {
+        x = x0[kp];
+        y = y0[kp];
+      } else {
+        const float* src = Ys + (((long)kp * M + a) * PR + row) * COUT + c0;
+        x = *reinterpret_cast<const float4*>(src);
+        y = *reinterpret_cast<const float4*>(src + 4);
+      }
       v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
       v[4] += y.x; v[5] += y.y; v[6] += y.z; v[7] += y.w;
     }
