@@ -3844,7 +3844,8 @@ static int X3_WG3_TILE = 1;
 // output positions; the 3x3 layer's 176 leave paired waves idle).  Measured (kwin_x3_v24*.md, v25*.md): 4x4/s2
 // 25.3 us paired vs 26.0-26.2 single (32.5-32.7 in slow runs), 3x3 18.4-18.8 paired vs 15.9-16.2 single
 static int X3_FWD_TILE = 3;
-static int X3_C1_F16B = 0;     // band forward: 1 = the band converted to fp16 once at staging (conv1_fwd_band_x2 F16B)
+static int X3_C1_F16B = 1;     // band forward: 1 = the band converted to fp16 once at staging (conv1_fwd_band_x2 F16B;
+                               // interleaved A/B: 64 paths 97.1 -> 95.8 us, 8 paths 20.9 -> 20.4)
 static int X3_C1_SB1 = 0;      // band forward (ring): 1 = one band buffer, three workgroups per CU (conv1_fwd_band_x2 SB1)
 static int X3_C1_PIPE = 0;     // band forward: 1 = next k-step's LDS fragments read during this k-step's MFMAs
 static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows

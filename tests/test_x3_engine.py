@@ -715,9 +715,9 @@ def test_x3_conv1_ring_wgrad_two_tile_passes_match_default(x3_ring_rollout, ncx,
 
 @pytest.mark.parametrize("opt", ["f16b", "sb1"])
 def test_x3_conv1_band_f16_staging_bit_equal(x3_ring_rollout, opt):
-    """conv1_fwd_band_x2 F16B (the band converted to fp16 once while staged, X3_C1_F16B) and SB1 (one band buffer,
-    three workgroups per CU, X3_C1_SB1) == the default double-buffered per-read conversion: the same MFMA operands,
-    so outputs and ReLU bits agree bit for bit."""
+    """conv1_fwd_band_x2 F16B (the band converted to fp16 once while staged, X3_C1_F16B, the default) == the
+    double-buffered per-read conversion, and SB1 (one band buffer, three workgroups per CU, X3_C1_SB1) == the
+    default: the same MFMA operands, so outputs and ReLU bits agree bit for bit."""
     from pathnet_gym_amd.ops import _lib
     tr, eng, _, _, _ = x3_ring_rollout
     hp = tr.model.hip
@@ -732,7 +732,7 @@ def test_x3_conv1_band_f16_staging_bit_equal(x3_ring_rollout, opt):
             hp.ring_fwd(eng.frames, eng.fc, eng.acts[0], eng.bits[0], eng.P, eng.E, 1, t, eng.bits_rows[0])
         torch.cuda.synchronize()
         outs.append((eng.acts[0].clone(), eng.bits[0].clone()))
-    setter(0)
+    setter(1 if opt == "f16b" else 0)           # the defaults
     assert outs[0][0].float().abs().sum() > 0
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
