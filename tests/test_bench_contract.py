@@ -4,6 +4,7 @@ import json
 import os
 import subprocess
 import sys
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -64,3 +65,13 @@ def test_bench_refuses_a_world_size_that_differs_from_gpus(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--backend", "torch"],
                        cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr and not r.stdout.strip()
+
+
+@pytest.mark.gpu
+def test_bench_mismatch_guard_on_the_gpu_box(tmp_path):
+    """The same guard with the HIP backend on an MI355X box: a torchrun-style environment whose WORLD_SIZE differs
+    from --gpus exits 2 before anything touches the GPU (no JSON line, nothing launched)."""
+    env = dict(os.environ, WORLD_SIZE="4", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29671")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "0"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=4" in r.stderr and not r.stdout.strip(), (r.returncode, r.stderr[-400:])
