@@ -199,7 +199,7 @@ DEVI void physics_wave0(int env, int* __restrict__ state, uint32_t* __restrict__
                         int n_actions, uint32_t seed, int frameskip, int max_steps, int no_op_max, int* phys,
                         float* __restrict__ reward_out, uint8_t* __restrict__ done_out,
                         float* __restrict__ epret_out, const uint8_t* __restrict__ fc_in,
-                        uint8_t* __restrict__ fc_out, uint32_t id_base) {
+                        uint8_t* __restrict__ fc_out, uint32_t id_base, int act_in = -1) {
   // RNG identity of the env: its GLOBAL index (id_base = first env of this rank), so a population sharded over
   // any number of ranks draws the same random streams as on one GPU
   const uint32_t rid = id_base + (uint32_t)env;
@@ -207,7 +207,8 @@ DEVI void physics_wave0(int env, int* __restrict__ state, uint32_t* __restrict__
 #pragma unroll
   for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
   uint32_t ctr = (uint32_t)__builtin_amdgcn_readfirstlane((int)counter[env]);
-  int a = __builtin_amdgcn_readfirstlane(actions[env]);
+  // act_in >= 0: the action sampled in this workgroup (pong_step_kernel HEADS), else the engine's action buffer
+  int a = act_in >= 0 ? act_in : __builtin_amdgcn_readfirstlane(actions[env]);
   if (a >= n_actions || a < 0) a = 0;                    // game_state.py:38-39
   const int up = (a == 2 || a == 4), down = (a == 3 || a == 5);
   int reward = 0;
@@ -309,6 +310,76 @@ DEVI void scene_tables(const St& st, Scene& S, const int* tab, int* rowinfo, int
 }
 }  // namespace pong
 
+// The actor-critic heads + Gumbel-max sampling of ONE sample, folded into the env step of that sample
+// (pong_step_kernel HEADS): the arithmetic of heads.hip heads_fwd_s16_kernel<8, float> -- 16 feature slices of 16
+// features each summed in order with packed FMAs (common.h heads_fma), the slices summed in order -- so logits,
+// value and the sampled action are bit-identical to the separate heads launch.  F = 256, A <= 8, fp32 features.
+struct HeadsArgs {
+  const float* feat;            // [B][256] step t's features
+  const float* flat;            // parameter store
+  long pw, pb, vw, vb;          // heads offsets in flat
+  int A;
+  float* logits;                // step t's [B][A]
+  float* value;                 // [B]
+  int* actions;                 // [B]
+  uint32_t seed, rb;
+  const long long* ctr;
+  int t, T;
+};
+DEVI int heads_sample_one(const HeadsArgs& h, int b, float* red) {
+  constexpr int F = 256, AM = 8, AW = AM + 1, FQ = F / 16;
+  // thread (slice fs, output j), 144 of them: the slice's 16 features in order, one fused multiply-add each -- the
+  // lane arithmetic of heads_fwd_s16_kernel's packed FMAs -- with every load of the chain issued up front
+  if (threadIdx.x < 16 * AW) {
+    const int fs = threadIdx.x / AW, j = threadIdx.x - fs * AW;
+    const float* fr = h.feat + (long)b * F + fs * FQ;
+    float x[FQ], wv[FQ];
+#pragma unroll
+    for (int k = 0; k < FQ; ++k) {
+      const int f = fs * FQ + k;
+      x[k] = fr[k];
+      wv[k] = j == AM ? h.flat[h.vw + f] : (j < h.A ? h.flat[h.pw + (long)f * h.A + j] : 0.f);
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < FQ; ++k) acc = __builtin_fmaf(x[k], wv[k], acc);
+    red[fs * AW + j] = acc;
+  }
+  __syncthreads();
+  // lanes j < 9 of wave 0: output j's slice sum in slice order, bias, Gumbel key; the first maximum wins (the
+  // sequential strict-greater scan of heads_fwd_s16_kernel)
+  __shared__ int act_s;
+  if (threadIdx.x < 64) {
+    const int j = threadIdx.x;
+    float v = 0.f;
+    if (j < AW)
+      for (int k = 0; k < 16; ++k) v += red[k * AW + j];
+    float sc = -3.0e38f;
+    if (j < h.A) {
+      const uint32_t stepkey = (uint32_t)(h.ctr[0] * h.T + h.t);
+      const float lg = v + h.flat[h.pb + j];
+      h.logits[(long)b * h.A + j] = lg;
+      const float g = lg - __logf(-__logf(sample_u01(h.seed, stepkey, h.rb + (uint32_t)b, (uint32_t)j)));
+      if (g > sc) sc = g;                                     // (a NaN key never wins, as in the scan)
+    }
+    if (j == AM) h.value[b] = v + h.flat[h.vb];
+    int bj = j < h.A ? j : 64;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const float osc = __shfl_xor(sc, o, 64);
+      const int oj = __shfl_xor(bj, o, 64);
+      if (osc > sc || (osc == sc && oj < bj)) { sc = osc; bj = oj; }
+    }
+    if (j == 0) {
+      const int best = bj < h.A ? bj : 0;
+      h.actions[b] = best;
+      act_s = best;
+    }
+  }
+  __syncthreads();
+  return act_s;
+}
+
 // state [B][12] int32, counter [B] uint32, actions [B] int32 (any int; >= n_actions remapped to 0)
 // obs_in/obs_out [B][160*120] uint32 (4 stacked uint8 frames), tables [8][160] int32
 //
@@ -316,7 +387,7 @@ DEVI void scene_tables(const St& st, Scene& S, const int* tab, int* rowinfo, int
 // (frame_out [B][160*120] uint8, 19.2 KB per env instead of a 77 KB stack read + 77 KB
 // stack write) and the next stack's first valid channel: fc_out = done ? 3 : max(fc_in-1, 0)
 // (a reset stack repeats the fresh frame in all 4 channels; see conv_fwd_fast RING).
-template <bool RING>
+template <bool RING, bool HEADS = false>
 __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ state, uint32_t* __restrict__ counter,
                                                         const int* __restrict__ actions, int n_actions,
                                                         const uint32_t* __restrict__ obs_in,
@@ -327,19 +398,25 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
                                                         int g_player, int g_ball,
                                                         const uint8_t* __restrict__ fc_in = nullptr,
                                                         uint8_t* __restrict__ fc_out = nullptr,
-                                                        long out_stride = 0, int b0 = 0, uint32_t id_base = 0) {
+                                                        long out_stride = 0, int b0 = 0, uint32_t id_base = 0,
+                                                        HeadsArgs ha = HeadsArgs{}) {
   using namespace pong;
   __shared__ __attribute__((aligned(16))) int tab[8 * 160];
   const int env = b0 + blockIdx.x;
   PONG_STAMP(0);
   for (int i = threadIdx.x; i < 8 * 160; i += 256) tab[i] = tables[i];
+  int act_in = -1;
+  if constexpr (HEADS) {
+    __shared__ float hred[16 * 9];
+    act_in = heads_sample_one(ha, env, hred);              // (its barriers also publish tab[])
+  }
   // --- physics: wave 0 only (scalar code; the 4 waves of a workgroup share ONE scalar unit per
   // CU with the other workgroups there, so running it redundantly in every wave made the SALU the
   // kernel's bottleneck), published through LDS ---
   __shared__ int phys[NSTATE + 4];
   if (threadIdx.x < 64)
     physics_wave0(env, state, counter, actions, n_actions, seed, frameskip, max_steps, no_op_max, phys, reward_out,
-                  done_out, epret_out, RING ? fc_in : nullptr, fc_out, id_base);
+                  done_out, epret_out, RING ? fc_in : nullptr, fc_out, id_base, act_in);
   PONG_STAMP(1);
   __syncthreads();    // tab[] staged and the new state published
   PONG_STAMP(2);
@@ -564,6 +641,27 @@ static int pong_ring_launch(void* state, void* counter, const int* actions, int 
   if (rc) return rc;
   pong_render_ring_kernel<<<dim3((unsigned)split, (unsigned)(B - b0)), 256, 0, stream>>>(
       (const int*)state, tables, (uint8_t*)frame_out, out_stride, split, g_bg, g_wall, g_cpu, g_player, g_ball, b0);
+  return (int)hipGetLastError();
+}
+
+// the ring step of envs [b0, b1) with the heads + sampling of each env's sample in the same workgroup
+// (pong_step_kernel<true, true>); feat: step t's [B][256] fp32 features
+int launch_pong_heads_step_ring(void* state, void* counter, int n_actions, void* frame_out, long out_stride,
+                                const void* fc_in, void* fc_out, const int* tables, float* reward, void* done,
+                                float* epret, int b1, unsigned seed, int frameskip, int max_steps, int no_op_max,
+                                int g_bg, int g_wall, int g_cpu, int g_player, int g_ball, unsigned id_base, int b0,
+                                const float* feat, int F, const float* flat, long pw, long pb, long vw, long vb,
+                                float* logits, float* value, int* actions, unsigned hseed, const long long* ctr, int t,
+                                int T, unsigned rb, hipStream_t stream) {
+  if (n_actions <= 0 || n_actions > 8 || F != 256 || out_stride < 160 * 120 || out_stride % 16 || b1 <= 0 || b0 < 0 ||
+      b0 >= b1 || !feat || !flat || !logits || !value || !actions || !ctr || !fc_in || !fc_out || frameskip < 0 ||
+      max_steps < 0 || no_op_max < 0 || g_bg < 0 || g_wall < 0 || g_cpu < 0 || g_player < 0 || g_ball < 0)
+    return -22;
+  HeadsArgs ha{feat, flat, pw, pb, vw, vb, n_actions, logits, value, actions, hseed, rb, ctr, t, T};
+  pong_step_kernel<true, true><<<b1 - b0, 256, 0, stream>>>(
+      (int*)state, (uint32_t*)counter, actions, n_actions, nullptr, (uint32_t*)frame_out, tables, reward,
+      (uint8_t*)done, epret, seed, frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu, g_player, g_ball,
+      (const uint8_t*)fc_in, (uint8_t*)fc_out, out_stride, b0, id_base, ha);
   return (int)hipGetLastError();
 }
 

@@ -338,6 +338,16 @@ class PongVec(VecEnv):
     # the ring step takes an env range (the split rollout steps one path group per launch, runtime/engine.py)
     ring_ranges = True
 
+    # ... and the heads + sampling of each env's sample folded into its step (runtime/engine.py fused env heads)
+    ring_heads = True
+
+    def step_ring_heads_into(self, feat, flat, heads, logits, value, actions, seed, ctr, t, T, row_base, frames, slot,
+                             fc_in, fc_out, reward, done, epret):
+        """Engine frame-ring step with the actor-critic heads of step t folded in (ops/envs.py)."""
+        from ..ops import envs as henv
+        henv.pong_heads_step_ring_into(self, feat, flat, heads, logits, value, actions, seed, ctr, t, T, row_base,
+                                       frames, slot, fc_in, fc_out, reward, done, epret)
+
     def step_ring_into(self, actions, frames, slot, fc_in, fc_out, reward, done, epret, b0: int = 0, b1=None):
         """Engine frame-ring step (HIP only): write frames[:, slot] + the next first valid channel, envs [b0, b1)."""
         from ..ops import envs as henv

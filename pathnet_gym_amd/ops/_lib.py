@@ -56,6 +56,9 @@ _SIGS = {
     "launch_inv_group": [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P],
     "launch_pong_step_ring": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int, c_int,
                               c_int, c_int, c_int, c_int, c_uint, P],
+    "launch_pong_heads_step_ring": [P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int,
+                                    c_int, c_int, c_int, c_int, c_int, c_uint, c_int, P, c_int, P, c_long, c_long,
+                                    c_long, c_long, P, P, P, c_uint, P, c_int, c_int, c_uint, P],
     "launch_pong_step_ring_split": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, c_uint, c_int, c_int, P],
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_uint, c_int, P, P, P, P, P, P],

@@ -98,6 +98,38 @@ def pong_step_ring_into(env, actions, frames, slot, fc_in, fc_out, reward, done,
               ring_split(b1 - b0), _lib.stream())
 
 
+def pong_heads_step_ring_into(env, feat, flat, heads, logits, value, actions, seed, ctr, t, T, row_base, frames, slot,
+                              fc_in, fc_out, reward, done, epret):
+    """The frame-ring step of every env with the actor-critic heads + Gumbel-max sampling of its sample folded into
+    the same workgroup (csrc/envs.hip pong_step_kernel<true, true>): feat [B, 256] fp32 = step t's trunk features,
+    heads = the parameter offsets {pw, pb, vw, vb}; writes logits [B, A], value [B] and actions [B] exactly as
+    HipPathNet.heads_fwd would, then steps the env with those actions."""
+    B = env.num_envs
+    if not hasattr(env, "_st32"):
+        pong_sync_to_device(env)
+    _lib.check(feat, torch.float32, (B, 256), name="feat")
+    _lib.check(logits, torch.float32, numel=B * env.num_actions, name="logits")
+    _lib.check(value, torch.float32, numel=B, name="value")
+    _lib.check(actions, torch.int32, (B,), name="actions")
+    _lib.check(frames, torch.uint8, name="frames")
+    if frames.dim() != 3 or frames.shape[0] != B or frames.shape[2] != 160 * 120 or not 0 <= slot < frames.shape[1]:
+        raise ValueError(f"frames {tuple(frames.shape)} / slot {slot} do not match [{B}, slots, 19200]")
+    for tns, nm in ((fc_in, "fc_in"), (fc_out, "fc_out"), (done, "done")):
+        _lib.check(tns, torch.uint8, numel=B, name=nm)
+    for tns, nm in ((reward, "reward"), (epret, "epret")):
+        _lib.check(tns, torch.float32, numel=B, name=nm)
+    if not hasattr(env, "_gray"):
+        env._gray = _gray_consts(env)
+    g = env._gray
+    _lib.call("launch_pong_heads_step_ring", env._st32.data_ptr(), env._ctr32.data_ptr(), env.num_actions,
+              frames[0, slot].data_ptr(), frames.stride(0), fc_in.data_ptr(), fc_out.data_ptr(), env._tab32.data_ptr(),
+              reward.data_ptr(), done.data_ptr(), epret.data_ptr(), B, env.seed_int, env.frameskip,
+              env.max_episode_steps, env.no_op_max, g[0], g[1], g[2], g[3], g[4], _id_base(env), 0,
+              feat.data_ptr(), 256, flat.data_ptr(), heads["pw"], heads["pb"], heads["vw"], heads["vb"],
+              logits.data_ptr(), value.data_ptr(), actions.data_ptr(), seed & 0xFFFFFFFF, ctr.data_ptr(), t, T,
+              int(row_base) & 0xFFFFFFFF, _lib.stream())
+
+
 def ring_split(B: int) -> int:
     """Render workgroups per env of the frame-ring Pong step (csrc/envs.hip launch_pong_step_ring_split).  Default 1:
     the fused one-workgroup-per-env kernel.  Measured at 8 paths x 32 envs (profiles/r5/): physics 5.4 + split-4

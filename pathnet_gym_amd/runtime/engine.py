@@ -156,6 +156,12 @@ class HipEngine:
         # torch-implemented games (envs/atari_games.py) are stepped eagerly, outside hipGraphs
         self.env_graph_safe = getattr(env, "graph_safe", True)
         self.use_graph = bool(cfg.use_graph) and not self.hybrid and self.env_graph_safe
+        # the heads + sampling of rollout steps 0..T-1 folded into the env step (frame-ring Pong, fp32 features):
+        # one launch per step less (csrc/envs.hip pong_step_kernel HEADS)
+        self.fuse_env_heads = (self.ring and getattr(env, "ring_heads", False) and hp.feat_dtype == torch.float32
+                               and not self.lstm_hip and not self.hybrid and self.env_graph_safe
+                               and model.cfg.num_actions <= 8 and hp.geoms[-1].out_feat == 256
+                               and os.environ.get("PATHNET_FUSE_ENV_HEADS", "1") != "0")
         self.auto_group_max_paths = int(os.environ.get("PATHNET_AUTO_GROUP_MAX_PATHS", "0"))
         self.groups = self._rollout_groups(getattr(cfg, "rollout_groups", 0))
         self.side_streams = [torch.cuda.Stream(device=dev) for _ in range(self.groups - 1)]
@@ -279,8 +285,16 @@ class HipEngine:
         pg = self.P // self.groups
         return grp * pg, pg
 
-    def _env_step(self, t, grp=None):
+    def _env_step(self, t, grp=None, heads=False):
+        """Env step t (``heads``: with step t's heads + sampling folded in, fuse_env_heads)."""
         env = self.env
+        if heads:
+            m = self.model
+            h = m.store.layout.heads[m.task if m.cfg.per_task_heads else 0]
+            env.step_ring_heads_into(self.acts[-1][t], m.store.flat, h, self.logits[t], self.values[t],
+                                     self.actions[t], self.seed, self.ctr, t, self.T + 1, self.row_base, self.frames,
+                                     t + 4, self.fc[t], self.fc[t + 1], self.rewards[t], self.dones[t], self.epret[t])
+            return
         if grp is not None:
             p0, np_ = self._group_range(grp)
             if self.ring:
@@ -391,8 +405,12 @@ class HipEngine:
                 and hp.geoms[-1].kind == "fc" and hp.geoms[-1].Cout == 256 and hp.geoms[-1].K == 256
                 and self.E <= 32 and self.A <= 8)
 
-    def _forward_step(self, t, greedy=False, grp=None):
+    def _forward_step(self, t, greedy=False, grp=None, heads=True):
+        """Forward of step t; ``heads`` False: the trunk only (the env step runs the heads, fuse_env_heads)."""
         hp = self.hip
+        if not heads:
+            self._trunk_step(t, grp)
+            return
         if grp is None and self._fused_heads():
             self._trunk_step(t, None, skip_last=True)
             L = len(hp.geoms)
@@ -489,9 +507,10 @@ class HipEngine:
         if self.groups > 1:
             self._rollout_split()
         else:
+            fh = self.fuse_env_heads
             for t in range(T):
-                self._forward_step(t)
-                self._env_step(t)
+                self._forward_step(t, heads=not fh)
+                self._env_step(t, heads=fh)
             self._forward_step(T, greedy=True)
         self._fitness_update()
         if hp.x3:

@@ -770,3 +770,39 @@ def test_x3_fused_fc_heads_bit_equal(hip_lib, monkeypatch, graph):
     for u, (a, b) in enumerate(zip(*runs)):
         for k, (x, y) in enumerate(zip(a, b)):
             assert torch.equal(x, y), (u, ("feat", "bits", "logits", "values", "actions")[k])
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_x3_env_step_with_folded_heads_bit_equal(hip_lib, monkeypatch, graph):
+    """The frame-ring Pong step with the heads + Gumbel-max sampling of each env's sample folded into its workgroup
+    (csrc/envs.hip pong_step_kernel<true, true>, engine fuse_env_heads) == heads_fwd_s16_kernel + the ring step:
+    logits, values, actions, frames, rewards and dones bit for bit over several updates (zero learning rate),
+    through the eager update, the capture and replays, across episode resets."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    runs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("PATHNET_FUSE_ENV_HEADS", fuse)
+        cfg = preset("pong")
+        cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 4, 16, 5
+        cfg.compute_dtype = "fp32x"
+        cfg.frame_ring = True
+        cfg.use_graph = graph
+        cfg.ga.backend = "device"
+        cfg.a2c.lr = 0.0
+        tr = PathNetTrainer(cfg, device=DEV)
+        e = tr.engine
+        assert e.fuse_env_heads == (fuse == "1")
+        tr.env.max_episode_steps = 7
+        snaps = []
+        for _ in range(3):
+            tr.update()
+            torch.cuda.synchronize()
+            snaps.append((e.logits.clone(), e.values.clone(), e.actions.clone(), e.frames.clone(), e.rewards.clone(),
+                          e.dones.clone(), e.fc.clone()))
+        tr.flush()
+        runs.append(snaps)
+    assert runs[0][0][0].abs().sum() > 0 and runs[0][-1][5].any()
+    names = ("logits", "values", "actions", "frames", "rewards", "dones", "fc")
+    for u, (a, b) in enumerate(zip(*runs)):
+        for k, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), (u, names[k])
