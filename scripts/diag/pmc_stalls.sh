@@ -12,5 +12,5 @@ for C in "$A" "$B"; do
   rm -rf /tmp/pmc_$i
   timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d /tmp/pmc_$i -o p -- python3 $R/bench.py --paths $P --paths-total $P --steps 2 --warmup 1 --windows 1 --no-graph --no-strong --per-rank-shapes "" --solve-seconds 0 --no-verify-build > $R/gpurun_out/pmc_stalls_$i.log 2>&1 || exit 1
   f=$(find /tmp/pmc_$i -name "*counter_collection.csv" | head -1)
-  python3 $R/scripts/pmc_dump.py $f --top 14 > $R/gpurun_out/pmc_stalls_p${P}_$i.txt || exit 1
+  python3 $R/scripts/pmc_dump.py $f --top 40 > $R/gpurun_out/pmc_stalls_p${P}_$i.txt || exit 1
 done
