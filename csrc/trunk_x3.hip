@@ -3861,6 +3861,7 @@ static int X3_DG_FOLD = 2;
 // (units per workgroup = units * P / target, >= 8); conv input gradients: ~X3_DG_TARGET (samples per workgroup >= 2);
 // 0 = the fixed per-path sizes (24 / 32 chunks per path).
 static int X3_WG_TARGET = 1536;
+static int X3_WG_AUTO = 1;     // conv1 ring weight gradient: whole rounds of resident workgroups (x3_conv1_ring_wgrad)
 // slab weight gradient: k-slot -> position map of the transposed operand reads (conv_wgrad_slab_x3 pmap)
 static int X3_SLAB_PMAP = 1;
 // staged output gradients: 1 = one fp16-pair split per value, masked per slot (mask_pair8); 0 = mask, then split per slot
@@ -3895,6 +3896,7 @@ void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
 void fast_conv_set_x3_fh_d(int v) { X3_FH_D = v; }
 void fast_conv_set_x3_presplit(int v) { X3_PRESPLIT = v ? 1 : 0; }
 void fast_conv_set_x3_slab_pmap(int v) { X3_SLAB_PMAP = v ? 1 : 0; }
+void fast_conv_set_x3_wg_auto(int v) { X3_WG_AUTO = v; }
 void fast_conv_set_x3_wg_target(int v) { X3_WG_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_dg_target(int v) { X3_DG_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_fc_ks_parts(int v) { X3_FC_KS_PARTS = (v == 2 || v == 4 || v == 8) ? v : 0; }
@@ -4057,10 +4059,23 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (M > 2 * X3_NCT) return 0;
   using SB = Slab<C1, 2>;
   const long units = (long)T * E * SB::NB;
-  // X3_WG_TARGET workgroups, up to twice that while every workgroup keeps >= 256 stages (interleaved A/B,
-  // scripts/diag/ab_kernel.py: 64 paths 1766 (1536) -> 1722 us (3072); 32 paths 888 vs 898; 8 paths 299 vs 375)
+  // whole rounds of resident workgroups (3 per CU at 2 column tiles per pass): a partial last round is a tail in
+  // which most CUs idle.  Rounds: 1, 2 or 4 by the work in ~133-stage rounds (<= 1.5, <= 5, more; interleaved A/B,
+  // scripts/diag/ab_kernel.py: 8 paths 293 (1536) -> 261 us (768); 16 paths 487 (1536) vs 517 (1024) / 636 (800);
+  // 32 paths 888 (1536) vs 898 (3072); 64 paths 1766 (1536) -> 1722 (3072)).  X3_WG_AUTO = 0: X3_WG_TARGET as is.
   long wgs = X3_WG_TARGET;
-  if (wgs > 0) wgs = std::max(wgs, std::min(2 * wgs, units * P / 256));
+  if (X3_WG_AUTO && wgs > 0) {
+    static int ncu = 0;
+    if (ncu == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    }
+    const long cap = 3L * ncu;
+    const long r10 = units * P * 10 / (cap * 133);       // work in tenths of a 133-stage round
+    wgs = cap * (r10 <= 15 ? 1 : (r10 <= 50 ? 2 : 4));
+  }
   long upw = wgs > 0 ? (units * P + wgs - 1) / wgs : (units + 23) / 24;
   if (upw < 8) upw = 8;
   if (upw / SB::NB + 2 > X3_RING_FCS) return -22;       // the workgroup's first-valid bytes fit the LDS table
