@@ -3867,7 +3867,7 @@ static int X3_SLAB_PMAP = 1;
 // staged output gradients: 1 = one fp16-pair split per value, masked per slot (mask_pair8); 0 = mask, then split per slot
 static int X3_PRESPLIT = 1;
 static int X3_FH_D = 3;        // fused last fc + heads: k-steps of fragments in flight (fc_heads_fwd_x3 D)
-static int X3_DG_TARGET = 2048;
+static int X3_DG_TARGET = 1536;  // conv2 input gradient: workgroups (8 paths 224 -> 214 us, 16 and 64 paths equal; 2048 before)
 // module-major fc forward k split: 0 = auto by rows (P*T*E <= 256: 8 parts, else 2), else the fixed part count (2 / 4 /
 // 8), capped so every part keeps >= 2 k-steps
 static int X3_FC_KS_PARTS = 0;
