@@ -3856,18 +3856,23 @@ static int X3_DG_W3 = 0;
 // fc input gradient: 1 = every k-step's MFMA products summed from zero and added to the running fp32 sum by a VALU add;
 // 2 = the same with odd k-steps on negated operands, subtracted (cancels the f16 MFMA's -inf rounding bias)
 static int X3_DG_FOLD = 2;
-// small populations: grid sizes follow P so a launch keeps ~2 rounds of workgroups when P shrinks (at the bench's
-// P = 64 these give the fixed sizes measured before).  Slab weight gradients: ~X3_WG_TARGET workgroups in total
-// (units per workgroup = units * P / target, >= 8); conv input gradients: ~X3_DG_TARGET (samples per workgroup >= 2);
-// 0 = the fixed per-path sizes (24 / 32 chunks per path).
+// grid sizes of the backward kernels.  Measured with interleaved A/Bs (scripts/diag/ab_kernel.py): a grid that is
+// ONE whole round of resident workgroups (2 per CU: 512) beats the fixed per-path sizes and the ~2-round targets of
+// round 5's first half at every population for the conv2 / conv3 input gradients and the conv2 weight gradient
+// (8 paths: conv2 backward 214 -> 167 us, conv3 backward 153 -> 128 us; 64 paths -1.5 to -2 %).  The conv1 ring
+// weight gradient (3 per CU) takes 1, 2 or 4 whole rounds by its work (x3_conv1_ring_wgrad, X3_WG_AUTO); with
+// X3_WG_AUTO = 0 it takes ~X3_WG_TARGET workgroups.  0 = the fixed per-path sizes (24 / 32 chunks per path).
 static int X3_WG_TARGET = 1536;
-static int X3_WG_AUTO = 1;     // conv1 ring weight gradient: whole rounds of resident workgroups (x3_conv1_ring_wgrad)
+static int X3_WG_AUTO = 1;
+static int X3_WG2_TARGET = 512;    // 4x4/s2 slab weight gradient (units per workgroup = units * P / target, >= 8)
+static int X3_DG3_TARGET = 512;    // 3x3 input gradient (samples per workgroup >= 2)
 // slab weight gradient: k-slot -> position map of the transposed operand reads (conv_wgrad_slab_x3 pmap)
 static int X3_SLAB_PMAP = 1;
 // staged output gradients: 1 = one fp16-pair split per value, masked per slot (mask_pair8); 0 = mask, then split per slot
 static int X3_PRESPLIT = 1;
 static int X3_FH_D = 3;        // fused last fc + heads: k-steps of fragments in flight (fc_heads_fwd_x3 D)
-static int X3_DG_TARGET = 1536;  // conv2 input gradient: workgroups (8 paths 224 -> 214 us, 16 and 64 paths equal; 2048 before)
+static int X3_DG_TARGET = 512;     // 4x4/s2 input gradient (2048 -> 1536 -> 512: 8 paths 224 -> 214 -> 191 -> 167 us with
+                                   // the conv2 weight gradient)
 // module-major fc forward k split: 0 = auto by rows (P*T*E <= 256: 8 parts, else 2), else the fixed part count (2 / 4 /
 // 8), capped so every part keeps >= 2 k-steps
 static int X3_FC_KS_PARTS = 0;
@@ -3896,6 +3901,8 @@ void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
 void fast_conv_set_x3_fh_d(int v) { X3_FH_D = v; }
 void fast_conv_set_x3_presplit(int v) { X3_PRESPLIT = v ? 1 : 0; }
 void fast_conv_set_x3_slab_pmap(int v) { X3_SLAB_PMAP = v ? 1 : 0; }
+void fast_conv_set_x3_wg2_target(int v) { X3_WG2_TARGET = v < 0 ? 0 : v; }
+void fast_conv_set_x3_dg3_target(int v) { X3_DG3_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_wg_auto(int v) { X3_WG_AUTO = v; }
 void fast_conv_set_x3_wg_target(int v) { X3_WG_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_dg_target(int v) { X3_DG_TARGET = v < 0 ? 0 : v; }
@@ -4114,7 +4121,8 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     const long units = (long)T * E * SB::NB;
     // the P-scaled grid pays for the uint8 first layer (P = 8: 567 -> 305 us) but not for the 4x4/s2 layer
     // (105 -> 126 us: its per-workgroup setup is a larger share of a shorter unit walk)
-    long upw = (X3_WG_TARGET > 0 && Gx::U8) ? (units * P + X3_WG_TARGET - 1) / X3_WG_TARGET : (units + 23) / 24;
+    const long tgt = Gx::U8 ? X3_WG_TARGET : X3_WG2_TARGET;
+    long upw = tgt > 0 ? (units * P + tgt - 1) / tgt : (units + 23) / 24;
     if (upw < 8) upw = 8;
     const dim3 grid((unsigned)((units + upw - 1) / upw), P);
     const int pf = Gx::U8 ? (X3_WGRAD_PF == 2 ? 2 : 1) : (X3_WGRAD_PF >= 2 ? 2 : 1);
@@ -4169,8 +4177,8 @@ int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_o
   const int nsamp = T * E;
   // P-scaled grid for the 4x4/s2 layer's input gradient (P = 8: 127 -> 119 us); the 3x3 layer keeps 32 chunks per
   // path (100 -> 110 us when scaled)
-  int spw = (X3_DG_TARGET > 0 && x3_is<C2>(Hin, Win, Cin, KH, KW, S, 0))
-                ? (int)(((long)nsamp * P + X3_DG_TARGET - 1) / X3_DG_TARGET) : (nsamp + 31) / 32;
+  const long dgt = x3_is<C2>(Hin, Win, Cin, KH, KW, S, 0) ? X3_DG_TARGET : X3_DG3_TARGET;
+  int spw = dgt > 0 ? (int)(((long)nsamp * P + dgt - 1) / dgt) : (nsamp + 31) / 32;
   if (spw < 2) spw = 2;
   const dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
 #define DGX(Gx)                                                                                                    \
