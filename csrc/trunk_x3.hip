@@ -3866,6 +3866,10 @@ static int X3_WG_TARGET = 1536;
 static int X3_WG_AUTO = 1;
 static int X3_WG2_TARGET = 512;    // 4x4/s2 slab weight gradient (units per workgroup = units * P / target, >= 8)
 static int X3_DG3_TARGET = 512;    // 3x3 input gradient (samples per workgroup >= 2)
+static int X3_WG3_TARGET = 256;    // 3x3 tile weight gradient, one round at 1 per CU (samples per workgroup >= 4;
+                                   // 512 before: conv3 backward 8 paths 128 -> 117 us, 64 paths 682 -> 676)
+static int X3_FCW_TARGET = 1024;   // narrow fc weight gradient (fc_wgrad_x3): workgroups, via the path split
+                                   // (2048 before: fc2 backward 8 paths 114 -> 109 us, 64 paths 330 -> 323)
 // slab weight gradient: k-slot -> position map of the transposed operand reads (conv_wgrad_slab_x3 pmap)
 static int X3_SLAB_PMAP = 1;
 // staged output gradients: 1 = one fp16-pair split per value, masked per slot (mask_pair8); 0 = mask, then split per slot
@@ -3901,6 +3905,8 @@ void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
 void fast_conv_set_x3_fh_d(int v) { X3_FH_D = v; }
 void fast_conv_set_x3_presplit(int v) { X3_PRESPLIT = v ? 1 : 0; }
 void fast_conv_set_x3_slab_pmap(int v) { X3_SLAB_PMAP = v ? 1 : 0; }
+void fast_conv_set_x3_wg3_target(int v) { X3_WG3_TARGET = v < 1 ? 1 : v; }
+void fast_conv_set_x3_fcw_target(int v) { X3_FCW_TARGET = v < 1 ? 1 : v; }
 void fast_conv_set_x3_wg2_target(int v) { X3_WG2_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_dg3_target(int v) { X3_DG3_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_wg_auto(int v) { X3_WG_AUTO = v; }
@@ -4145,7 +4151,7 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
   if (x3_is<C3>(Hin, Win, Cin, KH, KW, S, u8in) && X3_WG3_TILE) {
     if (xlo <= 0) return -22;
     const long nsamp = (long)T * E;
-    long spw = (nsamp * P + 511) / 512;            // ~2 workgroups per CU over the whole launch
+    long spw = (nsamp * P + X3_WG3_TARGET - 1) / X3_WG3_TARGET;   // ~X3_WG3_TARGET workgroups over the launch
     if (spw < 4) spw = 4;
     conv_wgrad_tile_x3<C3><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), WT3<C3>::NT, 0, st>>>(
         (const uint16_t*)X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br,
@@ -4398,7 +4404,7 @@ int x3_fc_wgrad(const void* X, long xlo, int ldx, const float* G, const void* bi
       w_off < 0 || b_off < 0 || layer < 0 || xlo <= 0 || !gamax) return -22;
   if (Cout % 16 != 0 || ldx % 8 != 0) return 0;
   const int tiles = ((K + 63) / 64) * ((Cout + 63) / 64) * M;
-  int nsplit = (2048 + tiles - 1) / tiles;
+  int nsplit = (X3_FCW_TARGET + tiles - 1) / tiles;
   nsplit = nsplit < 1 ? 1 : (nsplit > Pmax ? Pmax : nsplit);
   fc_wgrad_x3<<<dim3((K + 63) / 64, (Cout + 63) / 64, M * nsplit), 256, 0, st>>>(
       (const bf16_t*)X, xlo, ldx, G, (const uint16_t*)bits, grad, w_off, b_off, chunk, inv_path, inv_slot, inv_cnt,

@@ -179,6 +179,8 @@ _SIGS = {
     "fast_conv_set_x3_wg_target": [c_int],
     "fast_conv_set_x3_wg_auto": [c_int],
     "fast_conv_set_x3_wg2_target": [c_int],
+    "fast_conv_set_x3_wg3_target": [c_int],
+    "fast_conv_set_x3_fcw_target": [c_int],
     "fast_conv_set_x3_dg3_target": [c_int],
     "fast_conv_set_x3_slab_pmap": [c_int],
     "fast_conv_set_x3_c1_sb1": [c_int],

@@ -218,7 +218,10 @@ class HipPathNet:
         # wave walks every module of its 64 columns in turn, where fc_fwd_x3 gives each module its own wave and each
         # column tile its own workgroup), so off; PATHNET_X3_FUSE_HEADS=1 turns it on
         self.fuse_heads = os.environ.get("PATHNET_X3_FUSE_HEADS", "0") == "1"
-        self.fc_wgrad_gm_wgs = int(os.environ.get("PATHNET_X3_FC_WGRAD_WGS", "768"))    # target workgroup count
+        # target workgroup count of the fc1 weight gradient (paths split over ~wgs / tiles groups); at <= 16 paths a
+        # split holds too few paths and 256 wins (8 paths: 173 -> 163 us), at 64 paths 768 (933 vs 1023 us at 256)
+        self.fc_wgrad_gm_wgs = int(os.environ.get("PATHNET_X3_FC_WGRAD_WGS", "768"))
+        self.fc_wgrad_gm_wgs_small = int(os.environ.get("PATHNET_X3_FC_WGRAD_WGS_SMALL", "256"))
         P = model.P
         self.inv_path = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
         self.inv_slot = torch.zeros(self.L, self.M, P, dtype=torch.int32, device=dev)
@@ -756,7 +759,8 @@ class HipPathNet:
             tiles = ((g.K + 127) // 128) * self.M
             # workgroups ~ a whole number of rounds of one per CU (fc_wgrad_gm_x3 holds 102 KB of LDS): 110 tiles x 7
             # = 770 = 3.0 rounds on 256 CUs, where 110 x 5 = 550 left the third round 15 % full
-            nsplit = max(1, min(m.P, -(-self.fc_wgrad_gm_wgs // tiles)))
+            wgs = self.fc_wgrad_gm_wgs if m.P > 16 else self.fc_wgrad_gm_wgs_small
+            nsplit = max(1, min(m.P, -(-wgs // tiles)))
             ok = _lib.call_fast("x3_fc_wgrad_gm", xb, xblo, g.ldx, gm.data_ptr(), gmlo,
                                 grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, self.inv_path.data_ptr(),
                                 self.inv_slot.data_ptr(), self.inv_cnt.data_ptr(), l, self.M, m.P, g.K, g.Cout, P, E, T,

@@ -71,7 +71,9 @@ def main():
     def setopt(arm):
         for kv in arm.split(","):
             k, v = kv.split("=")
-            if k != "none":
+            if k.startswith("py."):              # a HipPathNet attribute (e.g. py.fc_wgrad_gm_wgs=512)
+                setattr(hp, k[3:], int(v))
+            elif k != "none":
                 getattr(lib, "fast_conv_set_" + k)(int(v))
 
     times = {kv: [] for kv in arms}
