@@ -3866,6 +3866,10 @@ static int X3_WG_TARGET = 1536;
 static int X3_WG_AUTO = 1;
 static int X3_WG2_TARGET = 512;    // 4x4/s2 slab weight gradient (units per workgroup = units * P / target, >= 8)
 static int X3_DG3_TARGET = 512;    // 3x3 input gradient (samples per workgroup >= 2)
+static int X3_C1F_TARGET = 512;    // ring band forward: workgroups (bands per workgroup >= X3_C1F_MINB)
+static int X3_C1F_MINB = 2;
+static int X3_C23_TARGET = 512;    // fused conv2 + conv3 forward: workgroups (samples per workgroup >= X3_C23_MINS)
+static int X3_C23_MINS = 1;        // (2 before: 16 paths 17.5 -> 16.2 us, 8 paths 16.1 -> 15.9, 64 paths equal)
 static int X3_WG3_TARGET = 256;    // 3x3 tile weight gradient, one round at 1 per CU (samples per workgroup >= 4;
                                    // 512 before: conv3 backward 8 paths 128 -> 117 us, 64 paths 682 -> 676)
 static int X3_FCW_TARGET = 1024;   // narrow fc weight gradient (fc_wgrad_x3): workgroups, via the path split
@@ -3905,6 +3909,10 @@ void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
 void fast_conv_set_x3_fh_d(int v) { X3_FH_D = v; }
 void fast_conv_set_x3_presplit(int v) { X3_PRESPLIT = v ? 1 : 0; }
 void fast_conv_set_x3_slab_pmap(int v) { X3_SLAB_PMAP = v ? 1 : 0; }
+void fast_conv_set_x3_c1f_target(int v) { X3_C1F_TARGET = v < 1 ? 1 : v; }
+void fast_conv_set_x3_c1f_minb(int v) { X3_C1F_MINB = v < 1 ? 1 : v; }
+void fast_conv_set_x3_c23_target(int v) { X3_C23_TARGET = v < 1 ? 1 : v; }
+void fast_conv_set_x3_c23_mins(int v) { X3_C23_MINS = v < 1 ? 1 : v; }
 void fast_conv_set_x3_wg3_target(int v) { X3_WG3_TARGET = v < 1 ? 1 : v; }
 void fast_conv_set_x3_fcw_target(int v) { X3_FCW_TARGET = v < 1 ? 1 : v; }
 void fast_conv_set_x3_wg2_target(int v) { X3_WG2_TARGET = v < 0 ? 0 : v; }
@@ -4010,8 +4018,8 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
   if ((E * C1::HOWO) % 16) return -2;
   const float isc = is / (float)(1 << X3_W0_SHIFT);
   const long nbands = (long)T * E * BD1<C1>::NB;
-  long bpw = (nbands * P + 511) / 512;
-  if (bpw < 2) bpw = 2;
+  long bpw = (nbands * P + X3_C1F_TARGET - 1) / X3_C1F_TARGET;
+  if (bpw < X3_C1F_MINB) bpw = X3_C1F_MINB;
   if (bpw > (X3_C1_FWD_FCS - 2) * BD1<C1>::NB) bpw = (X3_C1_FWD_FCS - 2) * BD1<C1>::NB;   // staged fc bytes
   if (X3_C1_SB1)
     conv1_fwd_band_x2<C1, true, false, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
@@ -4046,8 +4054,8 @@ int x3_conv23_fwd(const void* X, long xlo, void* Y1, long y1lo, void* bits1, lon
   if (M > 2 * X3_NCT || !X3_FWD_TILE) return 0;
   if ((E * C2::HOWO) % 16 || (E * C3::HOWO) % 16) return -2;
   const long nsamp = (long)T * E;
-  long spw = (nsamp * P + 511) / 512;
-  if (spw < 2) spw = 2;
+  long spw = (nsamp * P + X3_C23_TARGET - 1) / X3_C23_TARGET;
+  if (spw < X3_C23_MINS) spw = X3_C23_MINS;
   const float isc = 1.f / (float)(1 << X3_W0_SHIFT);
   const dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
   if (X3_FWD_TILE == 2 || X3_FWD_TILE == 3)

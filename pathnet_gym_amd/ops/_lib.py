@@ -180,6 +180,10 @@ _SIGS = {
     "fast_conv_set_x3_wg_auto": [c_int],
     "fast_conv_set_x3_wg2_target": [c_int],
     "fast_conv_set_x3_wg3_target": [c_int],
+    "fast_conv_set_x3_c1f_target": [c_int],
+    "fast_conv_set_x3_c1f_minb": [c_int],
+    "fast_conv_set_x3_c23_target": [c_int],
+    "fast_conv_set_x3_c23_mins": [c_int],
     "fast_conv_set_x3_fcw_target": [c_int],
     "fast_conv_set_x3_dg3_target": [c_int],
     "fast_conv_set_x3_slab_pmap": [c_int],
