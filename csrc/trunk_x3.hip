@@ -2230,7 +2230,7 @@ __global__ __launch_bounds__(256) void fc_fwd_x3(const uint16_t* __restrict__ X,
   const int grp = l >> 4, c16 = l & 15;
   const long Rtot = (long)T * E;
   const int PE = P * E;
-  const long row0 = (long)blockIdx.x * 32;
+  const long row0 = (long)blockIdx.x * (16 * RT);
   const int col0 = blockIdx.y * 64;
   long xrow[RT];
 #pragma unroll
@@ -3866,6 +3866,7 @@ static int X3_WG_TARGET = 1536;
 static int X3_WG_AUTO = 1;
 static int X3_WG2_TARGET = 512;    // 4x4/s2 slab weight gradient (units per workgroup = units * P / target, >= 8)
 static int X3_DG3_TARGET = 512;    // 3x3 input gradient (samples per workgroup >= 2)
+static int X3_FC_RT1 = 2;          // path-major fc forward, 17..32 rows per path: 16-row workgroups (0 off, 1 on, 2 auto)
 static int X3_C1F_TARGET = 512;    // ring band forward: workgroups (bands per workgroup >= X3_C1F_MINB)
 static int X3_C1F_MINB = 2;
 static int X3_C23_TARGET = 512;    // fused conv2 + conv3 forward: workgroups (samples per workgroup >= X3_C23_MINS)
@@ -3909,6 +3910,7 @@ void fast_conv_set_x3_wgrad_pf(int pf) { X3_WGRAD_PF = pf; }
 void fast_conv_set_x3_fh_d(int v) { X3_FH_D = v; }
 void fast_conv_set_x3_presplit(int v) { X3_PRESPLIT = v ? 1 : 0; }
 void fast_conv_set_x3_slab_pmap(int v) { X3_SLAB_PMAP = v ? 1 : 0; }
+void fast_conv_set_x3_fc_rt1(int v) { X3_FC_RT1 = v; }
 void fast_conv_set_x3_c1f_target(int v) { X3_C1F_TARGET = v < 1 ? 1 : v; }
 void fast_conv_set_x3_c1f_minb(int v) { X3_C1F_MINB = v < 1 ? 1 : v; }
 void fast_conv_set_x3_c23_target(int v) { X3_C23_TARGET = v < 1 ? 1 : v; }
@@ -4222,6 +4224,21 @@ int x3_fc_fwd(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits, c
       br <= 0 || bias_off < 0 || layer < 0 || t0 < 0 || xlo <= 0 || ylo < 0 || wlo <= 0) return -22;
   if (M > X3_MAXM || KP % 32 != 0 || Cout % 64 != 0 || ldx % 8 != 0 || ldx < K || (long)T * E > 32) return 0;
   const dim3 grid(1, Cout / 64, P);
+  if ((X3_FC_RT1 == 1 || (X3_FC_RT1 == 2 && (long)P * (Cout / 64) <= 64)) && (long)T * E > 16 && KP == 256) {
+    // 16-row workgroups: twice the grid for small populations (8 paths: fc2 16.1 -> 12.8 us; at 64 paths 16.9 ->
+    // 22.5, so auto only while the 32-row grid has <= 64 workgroups)
+    const dim3 g1((unsigned)((T * E + 15) / 16), Cout / 64, P);
+    if (ylo == 0)
+      fc_fwd_x3<1, 4, 8, true><<<g1, 256, 0, st>>>((const uint16_t*)X, xlo, ldx, Y, ylo, (uint16_t*)bits,
+                                                  (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, layer, L, M, K,
+                                                  KP, Cout, P, E, T, t0, br, 1.f / (float)(1 << X3_W0_SHIFT), os);
+    else
+      fc_fwd_x3<1, 4, 8, false><<<g1, 256, 0, st>>>((const uint16_t*)X, xlo, ldx, Y, ylo, (uint16_t*)bits,
+                                                   (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, layer, L, M,
+                                                   K, KP, Cout, P, E, T, t0, br, 1.f / (float)(1 << X3_W0_SHIFT), os);
+    const int rc = (int)hipGetLastError();
+    return rc ? -rc : 1;
+  }
 #define FCX(RT_, D_, NKS_, OF_)                                                                                      \
   fc_fwd_x3<RT_, D_, NKS_, OF_><<<grid, 256, 0, st>>>((const uint16_t*)X, xlo, ldx, Y, ylo, (uint16_t*)bits,        \
                                                       (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai, ac, layer, \

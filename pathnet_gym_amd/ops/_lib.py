@@ -181,6 +181,7 @@ _SIGS = {
     "fast_conv_set_x3_wg2_target": [c_int],
     "fast_conv_set_x3_wg3_target": [c_int],
     "fast_conv_set_x3_c1f_target": [c_int],
+    "fast_conv_set_x3_fc_rt1": [c_int],
     "fast_conv_set_x3_c1f_minb": [c_int],
     "fast_conv_set_x3_c23_target": [c_int],
     "fast_conv_set_x3_c23_mins": [c_int],

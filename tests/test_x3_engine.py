@@ -245,12 +245,12 @@ def test_x3_frame_ring_forward_bit_equal_to_packed(x3_ring_rollout):
 
 @pytest.mark.parametrize("E", [16, 32])
 @pytest.mark.parametrize("variant", ["split_k", "module_major", "module_major_ks1", "module_major_regs",
-                                     "module_major_ks2", "module_major_ks4", "module_major_ks8"])
+                                     "module_major_ks2", "module_major_ks4", "module_major_ks8", "rows16"])
 def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     """fc_fwd_ks_x3 (two waves per module, partial sums meet in LDS), fc_fwd_mm2_x3 (module-major LDS tiles, one or
     two k parts; the two-part form leaves bias / ReLU / bits to fc_slot_sum2_x3) and fc_fwd_mm_x3 (one workgroup per module
-    x 64 rows, slot planes summed in slot order) == the path-major fc_fwd_x3 up to summation order: outputs to
-    fp32 rounding, relu bits equal but for exact ties."""
+    x 64 rows, slot planes summed in slot order) and fc_fwd_x3 in 16-row workgroups (rows16) == the path-major
+    fc_fwd_x3 up to summation order: outputs to fp32 rounding, relu bits equal but for exact ties."""
     from pathnet_gym_amd.ops import _lib
     cfg = pixel_cfg()
     P = 5
@@ -267,7 +267,9 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     hp.fc_fwd_mm_min_k = 0
     for ref in (False, True):
         hp.fc_fwd_mm = variant.startswith("module_major") and not ref
-        lib.fast_conv_set_x3_fc_ks(1 if ref or variant.startswith("module_major") else 2)
+        lib.fast_conv_set_x3_fc_ks(1 if ref or variant.startswith("module_major") or variant == "rows16" else 2)
+        # rows16: the path-major kernel in 16-row workgroups (forced) vs 32-row ones
+        lib.fast_conv_set_x3_fc_rt1(1 if variant == "rows16" and not ref else 0)
         acts, bits = [], []
         x = obs
         for l, geo in enumerate(hp.geoms):
@@ -284,6 +286,7 @@ def test_x3_fc_forward_variants_match_path_major(hip_lib, E, variant):
     lib.fast_conv_set_x3_fc_mmv(3)
     lib.fast_conv_set_x3_fc_ks(1)
     lib.fast_conv_set_x3_fc_ks_parts(0)
+    lib.fast_conv_set_x3_fc_rt1(2)
     for l in (3, 4):
         a, b = outs[0][0][l], outs[1][0][l]
         assert rel(a, b) < 1e-6, (l, rel(a, b))
