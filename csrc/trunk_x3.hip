@@ -3882,7 +3882,7 @@ static int X3_PRESPLIT = 1;
 static int X3_FH_D = 3;        // fused last fc + heads: k-steps of fragments in flight (fc_heads_fwd_x3 D)
 static int X3_DG_TARGET = 512;     // 4x4/s2 input gradient (2048 -> 1536 -> 512: 8 paths 224 -> 214 -> 191 -> 167 us with
                                    // the conv2 weight gradient)
-// module-major fc forward k split: 0 = auto by rows (P*T*E <= 256: 8 parts, else 2), else the fixed part count (2 / 4 /
+// module-major fc forward k split: 0 = auto by rows (P*T*E <= 512: 4 parts, else 2), else the fixed part count (2 / 4 /
 // 8), capped so every part keeps >= 2 k-steps
 static int X3_FC_KS_PARTS = 0;
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
@@ -4310,7 +4310,9 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
     // slot sum in fc_slot_sum2_x3
     int ks = X3_FC_MMV >= 4 ? 4 : 2;
     if (X3_FC_KS_PARTS > 0) ks = X3_FC_KS_PARTS;
-    else if (X3_FC_MMV == 3) ks = (long)P * R <= 256 ? 8 : 2;   // 8 paths: 21.4 + 5.8 -> 13.3 + 8.4 us; 16: none
+    // 4 parts up to 512 rows (layer A/B, profiles/r5/ab_ks*.json: 8 paths 22.0 (8 parts) -> 21.6, 16 paths 27.9 (2)
+    // -> 23.9, 24 paths 28.3 -> 24.4 us; 32 paths 29.2 (2) vs 33.8 (4))
+    else if (X3_FC_MMV == 3) ks = (long)P * R <= 512 ? 4 : 2;
     while (ks > 2 && (KP / 32) / ks < 2) ks >>= 1;           // every part keeps >= 2 k-steps
     const int umax = (ks * M * 2 * ((P * R + 127) / 128) + 7) / 8 * 8;
     const unsigned g2 = (unsigned)(((long)P * R * 32 + 255) / 256);

@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="ring_wgrad", choices=["ring_wgrad", "ring_fwd", "conv23_fwd", "layer_bwd", "layer_fwd", "fc_heads", "fc_then_heads"])
     ap.add_argument("--layer", type=int, default=1)
+    ap.add_argument("--part", default=None, choices=["d", "w"], help="layer_bwd: input (d) or weight (w) gradient only")
     ap.add_argument("--opt", action="append", default=[],
                     help="one arm: name=value[,name=value...] (fast_conv_set_<name>); give every varied name in every arm")
     ap.add_argument("--paths", type=int, default=64)
@@ -63,7 +64,8 @@ def main():
             hp.layer_fwd(l, e.acts[l - 1], e.acts[l], e.bits[l], P, E, 1, 3, e.bits_rows[l])
         else:
             l = a.layer
-            hp.layer_bwd(l, e.acts[l - 1], e.grads[l], e.bits[l], scratch, e.grads[l - 1], P, E, T, e.bits_rows[l])
+            hp.layer_bwd(l, e.acts[l - 1], e.grads[l], e.bits[l], scratch, e.grads[l - 1], P, E, T, e.bits_rows[l],
+                         part=a.part)
 
     arms = a.opt or ["none=0"]
     lib = _lib.lib()
