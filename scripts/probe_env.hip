@@ -34,10 +34,10 @@ int main(int argc, char** argv) {
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
   for (int it = 0; it < 20; ++it)
     launch_pong_step_ring(dst, dctr, dact, 6, dframes, HW, dfc, dfc + B, dtab, drew, ddone, dep, B, 7, 4, 100000, 6,
-                          87, 142, 130, 150, 200, 0);
+                          87, 142, 130, 150, 200, 0, nullptr);
   hipEventRecord(a, 0);
   launch_pong_step_ring(dst, dctr, dact, 6, dframes, HW, dfc, dfc + B, dtab, drew, ddone, dep, B, 7, 4, 100000, 6, 87,
-                        142, 130, 150, 200, 0);
+                        142, 130, 150, 200, 0, nullptr);
   hipEventRecord(b, 0);
   hipEventSynchronize(b);
   float ms; hipEventElapsedTime(&ms, a, b);
