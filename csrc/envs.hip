@@ -131,6 +131,12 @@ DEVI int static_gray(const Scene& S, int r) {
 // per-source-pixel gray levels, built once per workgroup in LDS
 constexpr int BAND_R = 5 * DIGIT_SCALE, BAND_C = 56;
 constexpr int DL_R = 18;    // output rows of the per-workgroup score-digit box (rows 0..16 reach a digit)
+// The score-digit boxes depend on one score each (the cpu box, output x 16..39, only reaches the cpu digits; the
+// player box, x 76..99, only the player's) and on the env's constant colours and resize tables, so they are built
+// once per env object (launch_pong_digit_tables) into the tail of the tables buffer: [side][score][DL_R][6 words].
+// Per step the kernel copies its two 18 x 24 boxes instead of evaluating 864 pixels x 4 taps per workgroup.
+constexpr int TAB_INTS = 8 * 160, DL_SCORES = WIN_SCORE + 1, DL_WORDS = DL_R * 6;
+constexpr int TABLES_INTS = TAB_INTS + 2 * DL_SCORES * DL_WORDS;
 
 DEVI int band_col(int c) { return (c >= 24 && c < 52) ? c - 24 : ((c >= 104 && c < 132) ? c - 104 + 28 : -1); }
 
@@ -143,6 +149,23 @@ DEVI int scene_gray_pf(const Scene& S, int r, int c) {
   g = (play && c >= PLAYER_X && c < PLAYER_X + PADDLE_W && r >= S.py && r < S.py + PADDLE_H) ? S.g_player : g;
   g = (play && S.vis && c >= S.bx && c < S.bx + BALL_W && r >= S.by && r < S.by + BALL_H) ? S.g_ball : g;
   return g;
+}
+
+// scene_gray_pf factored by axis: bit k of tap_rows(r) / tap_cols(c) = source row r / column c lies in rectangle k
+// (0 cpu paddle, 1 player paddle, 2 ball; rows outside the playfield in none), so scene_gray_pf(S, r, c) ==
+// tap_gray(S, tap_rows(r) & tap_cols(c), static colour of row r) (the same priority: ball > player > cpu)
+DEVI int tap_rows(const Scene& S, int r) {
+  const bool play = r >= TOP && r < BOTTOM;
+  return play ? ((r >= S.cy && r < S.cy + PADDLE_H ? 1 : 0) | (r >= S.py && r < S.py + PADDLE_H ? 2 : 0) |
+                 (S.vis && r >= S.by && r < S.by + BALL_H ? 4 : 0))
+              : 0;
+}
+DEVI int tap_cols(const Scene& S, int c) {
+  return (c >= CPU_X && c < CPU_X + PADDLE_W ? 1 : 0) | (c >= PLAYER_X && c < PLAYER_X + PADDLE_W ? 2 : 0) |
+         (c >= S.bx && c < S.bx + BALL_W ? 4 : 0);
+}
+DEVI int tap_gray(const Scene& S, int m, int stat) {
+  return (m & 4) ? S.g_ball : ((m & 2) ? S.g_player : ((m & 1) ? S.g_cpu : stat));
 }
 
 DEVI int scene_gray(const Scene& S, const uint8_t* band, int r, int c) {
@@ -159,6 +182,11 @@ DEVI int scene_gray(const Scene& S, const uint8_t* band, int r, int c) {
 }  // namespace pong
 
 namespace pong {
+// byte offset of output quad xq in a dlut row (the score-digit boxes: quads 4..9 and 19..24), -1 outside them
+DEVI int digit_quad(int xq) {
+  return xq >= 4 && xq < 10 ? (xq - 4) * 4 : (xq >= 19 && xq < 25 ? 24 + (xq - 19) * 4 : -1);
+}
+
 // The 4 new-frame pixels of output quad (y, xq) (row word ri = rowinfo[y]): the row's static value, the
 // score-digit box from dlut, or -- on paddle / ball rows whose columns touch the same rectangle -- the 4 taps
 // evaluated analytically (all 4 pixels' taps and weights in 4 vector LDS reads, branch-free).
@@ -167,7 +195,7 @@ DEVI void quad_gray(const Scene& S, int y, int xq, int ri, const int* tab, const
   const uint32_t vr = (uint32_t)(ri & 0xFF);
   f4[0] = f4[1] = f4[2] = f4[3] = vr;
   const int rm = ri >> 8;
-  const int dq = xq >= 4 && xq < 10 ? (xq - 4) * 4 : (xq >= 19 && xq < 25 ? 24 + (xq - 19) * 4 : -1);
+  const int dq = digit_quad(xq);
   if (y < DL_R && dq >= 0) {
     const uint32_t w = *reinterpret_cast<const uint32_t*>(&dlut[y * 48 + dq]);
     f4[0] = w & 0xFFu; f4[1] = (w >> 8) & 0xFFu; f4[2] = (w >> 16) & 0xFFu; f4[3] = w >> 24;
@@ -189,6 +217,32 @@ DEVI void quad_gray(const Scene& S, int y, int xq, int ri, const int* tab, const
       v = v < 0 ? 0 : (v > 255 ? 255 : v);
       f4[e] = (rm & cma[e]) ? (uint32_t)v : f4[e];
     }
+  }
+}
+
+// quad_gray's analytic branch from the per-tap row / column rectangle bits (scene_tables rowtap / coltap): the same
+// taps, weights and rounding, ~4 logic ops per tap instead of scene_gray_pf's three rectangle tests
+DEVI void quad_gray_taps(const Scene& S, int y, int xq, int ri, const int* tab, const int* colmask,
+                         const int* rowtap, const int* coltap, uint32_t* f4) {
+  const int rm = ri >> 8;
+  const int rt = rowtap[y];
+  const int rb0 = rt & 7, rb1 = (rt >> 3) & 7, st0 = (rt >> 8) & 0xFF, st1 = (rt >> 16) & 0xFF;
+  const int cy0 = tab[2 * 160 + y], cy1 = tab[3 * 160 + y];
+  const int4 ctv = *reinterpret_cast<const int4*>(&coltap[xq * 4]);
+  const int4 cx0v = *reinterpret_cast<const int4*>(&tab[6 * 160 + xq * 4]);
+  const int4 cx1v = *reinterpret_cast<const int4*>(&tab[7 * 160 + xq * 4]);
+  const int4 cmv = *reinterpret_cast<const int4*>(&colmask[xq * 4]);
+  const int cta[4] = {ctv.x, ctv.y, ctv.z, ctv.w};
+  const int cx0a[4] = {cx0v.x, cx0v.y, cx0v.z, cx0v.w}, cx1a[4] = {cx1v.x, cx1v.y, cx1v.z, cx1v.w};
+  const int cma[4] = {cmv.x, cmv.y, cmv.z, cmv.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c0 = cta[e] & 7, c1 = cta[e] >> 3;
+    const int ra = tap_gray(S, rb0 & c0, st0) * cx0a[e] + tap_gray(S, rb0 & c1, st0) * cx1a[e];
+    const int rb = tap_gray(S, rb1 & c0, st1) * cx0a[e] + tap_gray(S, rb1 & c1, st1) * cx1a[e];
+    int v = (ra * cy0 + rb * cy1 + (1 << 21)) >> 22;
+    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+    f4[e] = (rm & cma[e]) ? (uint32_t)v : f4[e];
   }
 }
 
@@ -239,9 +293,11 @@ DEVI void physics_wave0(int env, int* __restrict__ state, uint32_t* __restrict__
 
 // Per-workgroup scene tables of the fused render (pong_step_kernel): the row / column
 // rectangle masks, per-row static colour, score band and score-digit box.  Contains two barriers.
+// dl: the precomputed digit boxes (tables tail), or nullptr to evaluate them here (launch_pong_digit_tables)
 template <int NTH>
 DEVI void scene_tables(const St& st, Scene& S, const int* tab, int* rowinfo, int* colmask, int* quadmask,
-                       uint8_t* band, uint8_t* dlut, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball) {
+                       uint8_t* band, uint8_t* dlut, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
+                       const uint32_t* __restrict__ dl = nullptr, int* rowtap = nullptr, int* coltap = nullptr) {
   S.cy = st.s[CY] >> 4;   // floor division by U=16 (values are non-negative)
   S.py = st.s[PY] >> 4;
   S.bx = st.s[BX] >= 0 ? st.s[BX] / U : -((-st.s[BX] + U - 1) / U);   // floor
@@ -263,7 +319,16 @@ DEVI void scene_tables(const St& st, Scene& S, const int* tab, int* rowinfo, int
   const int C0[5] = {24, 104, S.bx, PLAYER_X, CPU_X};
   const int C1[5] = {40 + 3 * DIGIT_SCALE, 120 + 3 * DIGIT_SCALE, S.bx + BALL_W, PLAYER_X + PADDLE_W,
                      CPU_X + PADDLE_W};
-  for (int i = threadIdx.x; i < BAND_R * BAND_C; i += NTH) {
+  const bool pre = dl != nullptr && st.s[CS] >= 0 && st.s[CS] < DL_SCORES && st.s[PS] >= 0 && st.s[PS] < DL_SCORES;
+  if (pre) {
+    // the two boxes of this step's scores: row yy = 6 cpu-box words then 6 player-box words (dlut[yy][48] bytes)
+    for (int i = threadIdx.x; i < DL_R * 12; i += NTH) {
+      const int yy = i / 12, wd = i - yy * 12, side = wd >= 6 ? 1 : 0;
+      const int sc = side ? st.s[PS] : st.s[CS];
+      *reinterpret_cast<uint32_t*>(&dlut[yy * 48 + wd * 4]) = dl[((side * DL_SCORES + sc) * DL_R + yy) * 6 + wd - side * 6];
+    }
+  }
+  for (int i = threadIdx.x; !pre && i < BAND_R * BAND_C; i += NTH) {
     const int r = SCORE_ROW0 + i / BAND_C, bc = i - (i / BAND_C) * BAND_C;
     const int c = bc < 28 ? 24 + bc : 104 + (bc - 28);
     int g = S.g_bg;
@@ -280,6 +345,8 @@ DEVI void scene_tables(const St& st, Scene& S, const int* tab, int* rowinfo, int
       int v = (static_gray(S, ys0) * cy0 + static_gray(S, ys1) * cy1 + 1024) >> 11;
       v = v < 0 ? 0 : (v > 255 ? 255 : v);
       rowinfo[i] = v | (m << 8);
+      if (rowtap) rowtap[i] = tap_rows(S, ys0) | (tap_rows(S, ys1) << 3) | (static_gray(S, ys0) << 8) |
+                              (static_gray(S, ys1) << 16);
     } else {
       const int x = i - OBS_H;
       const int xs0 = tab[4 * 160 + x], xs1 = tab[5 * 160 + x];
@@ -287,6 +354,7 @@ DEVI void scene_tables(const St& st, Scene& S, const int* tab, int* rowinfo, int
 #pragma unroll
       for (int k = 0; k < 5; ++k) m |= (xs1 >= C0[k] && xs0 < C1[k]) ? (1 << k) : 0;
       colmask[x] = m;
+      if (coltap) coltap[x] = tap_cols(S, xs0) | (tap_cols(S, xs1) << 3);
     }
   }
   __syncthreads();
@@ -296,7 +364,7 @@ DEVI void scene_tables(const St& st, Scene& S, const int* tab, int* rowinfo, int
   // score-digit output box (rows < DL_R, quads 4..9 and 19..24 = x 16..39 and 76..99: every output
   // pixel whose taps can reach a digit), each pixel evaluated once per workgroup from the LDS band
   // map instead of inside the (divergent) quad loop
-  for (int i = threadIdx.x; i < DL_R * 48; i += NTH) {
+  for (int i = threadIdx.x; !pre && i < DL_R * 48; i += NTH) {
     const int yy = i / 48, lx = i - yy * 48;
     const int x = lx < 24 ? 16 + lx : 76 + (lx - 24);
     const int ys0 = tab[0 * 160 + yy], ys1 = tab[1 * 160 + yy], cy0 = tab[2 * 160 + yy], cy1 = tab[3 * 160 + yy];
@@ -439,9 +507,56 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   __shared__ int quadmask[OBS_W / 4];    // OR of the 4 columns' masks per quad
   __shared__ uint8_t band[BAND_R * BAND_C];
   __shared__ __attribute__((aligned(4))) uint8_t dlut[DL_R * 48];
+  __shared__ int rowtap[RING ? OBS_H : 1];
+  __shared__ __attribute__((aligned(16))) int coltap[RING ? OBS_W : 4];
   Scene S;
-  scene_tables<256>(st, S, tab, rowinfo, colmask, quadmask, band, dlut, g_bg, g_wall, g_cpu, g_player, g_ball);
+  scene_tables<256>(st, S, tab, rowinfo, colmask, quadmask, band, dlut, g_bg, g_wall, g_cpu, g_player, g_ball,
+                    reinterpret_cast<const uint32_t*>(tables + TAB_INTS), RING ? rowtap : nullptr,
+                    RING ? coltap : nullptr);
   PONG_STAMP(3);
+  constexpr int NQ = OBS_H * OBS_W / 4, QR = OBS_W / 4;      // quads per frame / per row
+  if constexpr (RING) {
+    // Four quads per thread at a time, their row words, quad masks and digit-box words read from LDS up front: at
+    // one workgroup per CU (8 paths x 32 envs) the walk of one quad at a time -- dependent LDS round trips and a
+    // branch per quad -- took ~850 cycles per quad and was the kernel's critical path
+    // (scripts/probe_env.hip).  Same pixels: a quad is its row's static value, its digit-box word, or quad_gray's
+    // analytic taps when its row and columns touch the same rectangle.
+    uint32_t* outw = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(obs_out) + (long)env * out_stride);
+    for (int q0 = threadIdx.x; q0 < NQ; q0 += 4 * 256) {
+      PONG_LOOP_STAMP((q0 >> 10), 0);
+      int yk[4], xk[4], rik[4], qmk[4];
+      uint32_t dwk[4];
+      bool dk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = min(q0 + 256 * k, NQ - 1);
+        yk[k] = q / QR;
+        xk[k] = q - yk[k] * QR;
+        rik[k] = rowinfo[yk[k]];
+        qmk[k] = quadmask[xk[k]];
+        const int dq = digit_quad(xk[k]);
+        dk[k] = yk[k] < DL_R && dq >= 0;
+        dwk[k] = *reinterpret_cast<const uint32_t*>(&dlut[min(yk[k], DL_R - 1) * 48 + max(dq, 0)]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = q0 + 256 * k;
+        if (q < NQ) {
+          uint32_t wv = (uint32_t)(rik[k] & 0xFF) * 0x01010101u;
+          if (dk[k]) {
+            wv = dwk[k];
+          } else if ((rik[k] >> 8) & qmk[k]) {
+            uint32_t f4[4] = {wv & 0xFFu, wv & 0xFFu, wv & 0xFFu, wv & 0xFFu};
+            quad_gray_taps(S, yk[k], xk[k], rik[k], tab, colmask, rowtap, coltap, f4);
+            wv = f4[0] | (f4[1] << 8) | (f4[2] << 16) | (f4[3] << 24);
+          }
+          outw[q] = wv;
+        }
+      }
+    }
+    PONG_STAMP(4);
+    return;
+  }
   const uint4* in4 = reinterpret_cast<const uint4*>(obs_in) + (long)env * (OBS_H * OBS_W / 4);
   uint4* out4 = reinterpret_cast<uint4*>(obs_out) + (long)env * (OBS_H * OBS_W / 4);
   uint32_t* outw = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(obs_out) + (long)env * out_stride);
@@ -449,7 +564,6 @@ __global__ __launch_bounds__(256, 8) void pong_step_kernel(int* __restrict__ sta
   // load ahead per thread the whole chip held ~8 MB of loads in flight, about half of what HBM's
   // bandwidth x latency needs, and the packed-stack kernel ran at ~4.5 TB/s.  Each item is owned by
   // one thread, so obs_in == obs_out stays correct.
-  constexpr int NQ = OBS_H * OBS_W / 4, QR = OBS_W / 4;      // quads per frame / per row
   static_assert(256 % QR == 16 && 256 / QR == 8, "quad walk below assumes 30 quads per row");
   uint4 nxt = make_uint4(0u, 0u, 0u, 0u), nxt2 = nxt;
   if (!RING && !done) {
@@ -525,7 +639,8 @@ __global__ __launch_bounds__(256, 8) void pong_render_ring_kernel(const int* __r
   for (int i = 0; i < NSTATE; ++i) st.s[i] = __builtin_amdgcn_readfirstlane(state[env * NSTATE + i]);
   __syncthreads();                                   // tab[] staged
   Scene S;
-  scene_tables<256>(st, S, tab, rowinfo, colmask, quadmask, band, dlut, g_bg, g_wall, g_cpu, g_player, g_ball);
+  scene_tables<256>(st, S, tab, rowinfo, colmask, quadmask, band, dlut, g_bg, g_wall, g_cpu, g_player, g_ball,
+                    reinterpret_cast<const uint32_t*>(tables + TAB_INTS));
   constexpr int NQ = OBS_H * OBS_W / 4, QR = OBS_W / 4;
   const int per = (NQ + split - 1) / split;
   const int q0 = (int)blockIdx.x * per, q1 = min(NQ, q0 + per);
@@ -539,6 +654,35 @@ __global__ __launch_bounds__(256, 8) void pong_render_ring_kernel(const int* __r
     xq += 16;
     y += 8;
     if (xq >= QR) { xq -= QR; ++y; }
+  }
+}
+
+// The score-digit boxes of every score (launch_pong_digit_tables): workgroup sc evaluates the scene of a state with
+// both scores = sc (the ball hidden; the boxes never reach the playfield) with the per-step code path, then stores
+// its cpu box as side 0 / score sc and its player box as side 1 / score sc in the tables tail.
+__global__ __launch_bounds__(256) void pong_digit_tables_kernel(int* __restrict__ tables, int g_bg, int g_wall,
+                                                                int g_cpu, int g_player, int g_ball) {
+  using namespace pong;
+  __shared__ __attribute__((aligned(16))) int tab[TAB_INTS];
+  __shared__ int rowinfo[OBS_H];
+  __shared__ __attribute__((aligned(16))) int colmask[OBS_W];
+  __shared__ int quadmask[OBS_W / 4];
+  __shared__ uint8_t band[BAND_R * BAND_C];
+  __shared__ __attribute__((aligned(4))) uint8_t dlut[DL_R * 48];
+  for (int i = threadIdx.x; i < TAB_INTS; i += 256) tab[i] = tables[i];
+  St st;
+#pragma unroll
+  for (int i = 0; i < NSTATE; ++i) st.s[i] = 0;
+  st.s[CS] = st.s[PS] = (int)blockIdx.x;
+  st.s[SERVE] = 1;
+  __syncthreads();                                   // tab[] staged
+  Scene S;
+  scene_tables<256>(st, S, tab, rowinfo, colmask, quadmask, band, dlut, g_bg, g_wall, g_cpu, g_player, g_ball);
+  uint32_t* out = reinterpret_cast<uint32_t*>(tables + TAB_INTS);
+  for (int i = threadIdx.x; i < DL_R * 12; i += 256) {
+    const int yy = i / 12, wd = i - yy * 12, side = wd >= 6 ? 1 : 0;
+    out[((side * DL_SCORES + (int)blockIdx.x) * DL_R + yy) * 6 + wd - side * 6] =
+        *reinterpret_cast<const uint32_t*>(&dlut[yy * 48 + wd * 4]);
   }
 }
 
@@ -684,6 +828,16 @@ int launch_pong_step_ring_split(void* state, void* counter, const int* actions, 
   return pong_ring_launch(state, counter, actions, n_actions, frame_out, out_stride, fc_in, fc_out, tables, reward,
                           done, epret, b1, seed, frameskip, max_steps, no_op_max, g_bg, g_wall, g_cpu, g_player, g_ball,
                           id_base, b0, split, stream);
+}
+
+// tables: [TAB_INTS resize tables | digit boxes]; fills the digit boxes from the resize tables (every Pong step
+// launcher reads a tables buffer of pong_tables_ints() ints filled by this)
+int pong_tables_ints() { return pong::TABLES_INTS; }
+int launch_pong_digit_tables(int* tables, int g_bg, int g_wall, int g_cpu, int g_player, int g_ball,
+                             hipStream_t stream) {
+  if (!tables || g_bg < 0 || g_wall < 0 || g_cpu < 0 || g_player < 0 || g_ball < 0) return -22;
+  pong_digit_tables_kernel<<<pong::DL_SCORES, 256, 0, stream>>>(tables, g_bg, g_wall, g_cpu, g_player, g_ball);
+  return (int)hipGetLastError();
 }
 
 int launch_cartpole_step(float* state, int* steps, float* epret, void* counter, const int* actions, int B,

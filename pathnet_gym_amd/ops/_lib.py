@@ -62,6 +62,8 @@ _SIGS = {
     "launch_pong_step_ring_split": [P, P, P, c_int, P, c_long, P, P, P, P, P, P, c_int, c_uint, c_int, c_int, c_int,
                                     c_int, c_int, c_int, c_int, c_int, c_uint, c_int, c_int, P],
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_uint, c_int, P, P, P, P, P, P],
+    "launch_pong_digit_tables": [P, c_int, c_int, c_int, c_int, c_int, P],
+    "pong_tables_ints": [],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],
     "launch_rects_ring_push": [P, P, c_int, c_int, P, c_long, P, P, P, P, c_int, P],

@@ -28,7 +28,20 @@ def pong_sync_to_device(env):
     """(Re)build the int32 kernel state from the torch (int64) state."""
     env._st32 = env.state.to(torch.int32).contiguous()
     env._ctr32 = env.counter.to(torch.int32).contiguous()
-    env._tab32 = env.tables.to(torch.int32).contiguous()
+    env._tab32 = pong_tables(env)
+
+
+def pong_tables(env) -> torch.Tensor:
+    """The Pong step kernels' tables buffer: the [8][160] resize tables followed by the score-digit boxes of every
+    score (csrc/envs.hip launch_pong_digit_tables, built here once per env object)."""
+    if not hasattr(env, "_gray"):
+        env._gray = _gray_consts(env)
+    g = env._gray
+    lib = _lib.lib()
+    tab = torch.zeros(int(lib.pong_tables_ints()), dtype=torch.int32, device=env.tables.device)
+    tab[: 8 * 160] = env.tables.to(torch.int32).reshape(-1)
+    _lib.call("launch_pong_digit_tables", tab.data_ptr(), g[0], g[1], g[2], g[3], g[4], _lib.stream())
+    return tab
 
 
 def pong_sync_from_device(env):

@@ -25,11 +25,12 @@ int main(int argc, char** argv) {
   for (int y = 0; y < 160; ++y) { tab[y] = (y * 210) / 160; tab[160 + y] = std::min(209, tab[y] + 1); tab[320 + y] = 1024; tab[480 + y] = 1024; }
   for (int x = 0; x < 120; ++x) { tab[640 + x] = (x * 160) / 120; tab[800 + x] = std::min(159, tab[640 + x] + 1); tab[960 + x] = 1024; tab[1120 + x] = 1024; }
   int *dst, *dtab, *dact; unsigned *dctr; float *drew, *dep; unsigned char *ddone, *dfc, *dframes;
-  hipMalloc(&dst, B * NST * 4); hipMalloc(&dtab, 8 * 160 * 4); hipMalloc(&dact, B * 4); hipMalloc(&dctr, B * 4);
+  hipMalloc(&dst, B * NST * 4); hipMalloc(&dtab, pong_tables_ints() * 4); hipMalloc(&dact, B * 4); hipMalloc(&dctr, B * 4);
   hipMalloc(&drew, B * 4); hipMalloc(&dep, B * 4); hipMalloc(&ddone, B); hipMalloc(&dfc, 2 * B);
   hipMalloc(&dframes, (size_t)B * HW);
   hipMemcpy(dst, st.data(), B * NST * 4, hipMemcpyHostToDevice);
   hipMemcpy(dtab, tab.data(), 8 * 160 * 4, hipMemcpyHostToDevice);
+  launch_pong_digit_tables(dtab, 87, 142, 130, 150, 200, nullptr);
   hipMemset(dact, 0, B * 4); hipMemset(dctr, 0, B * 4); hipMemset(dfc, 0, 2 * B);
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
   for (int it = 0; it < 20; ++it)

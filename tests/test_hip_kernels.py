@@ -468,6 +468,42 @@ def test_pong_env_hip_bit_exact_vs_torch(hip_lib):
     assert ndone > 0     # at least one auto-reset exercised
 
 
+def test_pong_score_digits_every_score_bit_exact(hip_lib):
+    """The score boxes come from per-score tables built once per env (csrc/envs.hip launch_pong_digit_tables): every
+    score 0..20 on both sides renders as the torch game does, and the frame-ring kernel's batched quad walk writes
+    the packed kernel's newest frame."""
+    from pathnet_gym_amd.envs.pong import CS, PS, PongVec
+    from pathnet_gym_amd.ops import envs as henv
+    N = 42
+    et = PongVec(N, device=DEV, seed=5, backend="torch")
+    eh = PongVec(N, device=DEV, seed=5, backend="hip")
+    er = PongVec(N, device=DEV, seed=5, backend="hip")
+    idx = torch.arange(N, device=DEV)
+    for e in (et, eh, er):
+        e.reset()
+        e.state[:, CS] = idx % 21
+        e.state[:, PS] = (idx * 8 + 3) % 21
+    for e in (eh, er):
+        henv.pong_sync_to_device(e)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    frames = torch.zeros(N, 2, 160 * 120, dtype=torch.uint8, device=DEV)
+    fc_in = torch.zeros(N, dtype=torch.uint8, device=DEV)
+    fc_out = torch.zeros_like(fc_in)
+    for i in range(6):
+        a = torch.randint(0, 6, (N,), generator=g).to(DEV)
+        ot, rt, dt, _ = et.step(a)
+        oh, rh, dh, _ = eh.step(a)
+        r = torch.empty(N, device=DEV)
+        d = torch.empty(N, dtype=torch.uint8, device=DEV)
+        ep = torch.empty(N, device=DEV)
+        er.step_ring_into(a.to(torch.int32).contiguous(), frames, 1, fc_in, fc_out, r, d, ep)
+        torch.cuda.synchronize()
+        assert torch.equal(ot, oh), i
+        assert torch.equal(frames[:, 1], oh[..., 3].reshape(N, -1)), i
+        assert torch.equal(r, rh) and torch.equal(d, dh.to(torch.uint8)), i
+    assert len(set(er._st32[:, CS].tolist())) >= 20 and len(set(er._st32[:, PS].tolist())) >= 20
+
+
 def test_cartpole_env_hip_vs_torch(hip_lib):
     from pathnet_gym_amd.envs.cartpole import CartPoleVec
     N = 64
