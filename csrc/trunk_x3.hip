@@ -579,6 +579,9 @@ DEVI uint4 planes_to_px4(uint4 v) {
 // rows, so the per-read conversion (v_perm per 2 pixels) ran ~4x per pixel
 // SB1: ONE uint8 band buffer (17.3 KB; one more barrier per band, like F16B) so that the workgroup's 51 KB of LDS
 // lets three workgroups share a CU (3 waves / SIMD, <= 168 VGPRs) instead of two
+#ifndef X3_C1_EARLY_BAND
+#define X3_C1_EARLY_BAND 1
+#endif
 template <class G, bool RING = false, bool PIPE = false, bool F16B = false, bool SB1 = false>
 __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                            long ylo, uint8_t* __restrict__ bits,
@@ -692,7 +695,10 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
   for (int pass = 0; pass < npass; ++pass) {
     const int ct0 = pass * NCXT;
     const int ncg = nct == 0 ? 1 : min(NCXT, nct - ct0);
-    __syncthreads();                                   // mods visible; the previous pass's LDS reads done
+    __syncthreads();                                   // mods (and fcs) visible; the previous pass's LDS reads done
+    // the first band's loads go out before the weight staging's, so the two global latencies overlap (the staging
+    // loop's waits then cover both)
+    if (X3_C1_EARLY_BAND) load_band(b_beg);
     static_assert(G::KC == 32, "weight-sum reduction: one column per 32 lanes");
     for (int i = tid; i < ncg * 16 * G::KC; i += 256) {
       const int col = i / G::KC, kc = i - col * G::KC;
@@ -713,7 +719,7 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
       for (int m = 16; m >= 1; m >>= 1) ws += __shfl_xor(ws, m, 64);
       if (kc == 0) wsum_s[col] = ws;
     }
-    load_band(b_beg);
+    if (!X3_C1_EARLY_BAND) load_band(b_beg);
     __syncthreads();
     if (tid < ncg * 16) {
       const int slot = ct0 * 2 + (tid >> 3);
