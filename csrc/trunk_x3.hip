@@ -3740,16 +3740,14 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
 // meets (G16).  *status |= X3_RANGE_W when a scaled
 // weight leaves the fp16 range; x3_status_fold (end of the next rollout) moves it and the forward epilogues' flag
 // into the update's all-reduced counters, where every rank sees it (algo/trainer.py raises X3RangeError)
-__global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict__ flat, long w_off, int chunk, int K,
-                                                         int KP, int Cout, int M, uint16_t* __restrict__ Wc,
-                                                         uint16_t* __restrict__ WcT, int f16,
-                                                         uint32_t* __restrict__ status) {
+DEVI void refresh_x3_tile(const float* __restrict__ flat, long w_off, int chunk, int K, int KP, int Cout, int M,
+                          uint16_t* __restrict__ Wc, uint16_t* __restrict__ WcT, int f16, uint32_t* __restrict__ status,
+                          int b) {
   // one 32 (k) x 64 (column) tile of one module per workgroup, transposed through LDS: the master weights are read
   // and WcT ([M][KP][Cout], the flat order) written along the columns, Wc ([M][Cout][KP]) written along k -- both
   // coalesced (the flat-order loop wrote Wc with a KP stride: 5 launches x ~16 us per update)
   __shared__ float tile[32][65];
   const int tk = (KP + 31) / 32, tc = (Cout + 63) / 64;
-  const int b = (int)blockIdx.x;
   const int j = b / (tk * tc), rem = b - j * tk * tc;
   const int kt = rem / tc, ct = rem - kt * tc;
   if (j >= M) return;
@@ -3792,6 +3790,32 @@ __global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict
     Wc[n + wi] = lo;
   }
   if (bad && status) atomicOr(status, X3_RANGE_W);
+}
+
+__global__ __launch_bounds__(256) void refresh_x3_kernel(const float* __restrict__ flat, long w_off, int chunk, int K,
+                                                         int KP, int Cout, int M, uint16_t* __restrict__ Wc,
+                                                         uint16_t* __restrict__ WcT, int f16,
+                                                         uint32_t* __restrict__ status) {
+  refresh_x3_tile(flat, w_off, chunk, K, KP, Cout, M, Wc, WcT, f16, status, (int)blockIdx.x);
+}
+
+// every layer's refresh in ONE launch (x3_refresh_weights_all): layer i owns blocks [b0[i], b0[i + 1])
+constexpr int X3_REFRESH_MAXL = 8;
+struct RefreshSet {
+  long w_off[X3_REFRESH_MAXL];
+  uint16_t* Wc[X3_REFRESH_MAXL];
+  uint16_t* WcT[X3_REFRESH_MAXL];
+  int chunk[X3_REFRESH_MAXL], K[X3_REFRESH_MAXL], KP[X3_REFRESH_MAXL], Cout[X3_REFRESH_MAXL];
+  int b0[X3_REFRESH_MAXL + 1];
+  int n, M, f16;
+};
+__global__ __launch_bounds__(256) void refresh_x3_all_kernel(const float* __restrict__ flat, RefreshSet rs,
+                                                             uint32_t* __restrict__ status) {
+  const int b = (int)blockIdx.x;
+  int i = 0;
+  while (i + 1 < rs.n && b >= rs.b0[i + 1]) ++i;
+  refresh_x3_tile(flat, rs.w_off[i], rs.chunk[i], rs.K[i], rs.KP[i], rs.Cout[i], rs.M, rs.Wc[i], rs.WcT[i], rs.f16,
+                  status, b - rs.b0[i]);
 }
 
 // one thread: out[0] = (float)(activation flags since the last fold | weight flags of the last refresh), both reset
@@ -4482,6 +4506,29 @@ int x3_amax_reset(float* amax, int n, hipStream_t st) {
 int x3_status_fold(void* wstatus, float* out, hipStream_t st) {
   if (!wstatus || !out) return -22;
   x3_status_fold_kernel<<<1, 64, 0, st>>>((uint32_t*)wstatus, out);
+  return (int)hipGetLastError();
+}
+
+// n layers, meta[i] = {w_off, chunk, K, KP, Cout}, Wc[i] / WcT[i] (WcT[i] may be null); one launch
+int x3_refresh_weights_all(const float* flat, int n, const long* meta, void* const* Wc, void* const* WcT, int M,
+                           int f16, void* status, hipStream_t st) {
+  if (n <= 0 || n > X3_REFRESH_MAXL || !meta || !Wc || !WcT || M <= 0 || f16 < 0) return -22;
+  RefreshSet rs{};
+  long blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const long* m = meta + 5 * i;
+    if (m[1] <= 0 || m[2] <= 0 || m[3] <= 0 || m[4] <= 0 || m[0] < 0 || m[3] < m[2] || !Wc[i]) return -22;
+    rs.w_off[i] = m[0];
+    rs.chunk[i] = (int)m[1]; rs.K[i] = (int)m[2]; rs.KP[i] = (int)m[3]; rs.Cout[i] = (int)m[4];
+    rs.Wc[i] = (uint16_t*)Wc[i];
+    rs.WcT[i] = (uint16_t*)WcT[i];
+    rs.b0[i] = (int)blocks;
+    blocks += (long)M * ((m[3] + 31) / 32) * ((m[4] + 63) / 64);
+    if (blocks > 0x7FFFFFFFL) return -22;
+  }
+  rs.b0[n] = (int)blocks;
+  rs.n = n; rs.M = M; rs.f16 = f16;
+  refresh_x3_all_kernel<<<(unsigned)blocks, 256, 0, st>>>(flat, rs, (uint32_t*)status);
   return (int)hipGetLastError();
 }
 

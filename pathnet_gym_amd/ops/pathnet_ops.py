@@ -24,6 +24,7 @@ forward of step t and the whole-rollout backward agree.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 from typing import List, Optional
@@ -342,9 +343,17 @@ class HipPathNet:
     def refresh_weights(self):
         flat = self.model.store.flat
         if self.x3:
-            for l, g in enumerate(self.geoms):
-                _lib.call("x3_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, self.M,
-                          self.Wc[l].data_ptr(), _lib.ptr(self.WcT[l]), 1, self.x3_status.data_ptr(), _lib.stream())
+            # every layer's fp16-pair copies in one launch (csrc/trunk_x3.hip x3_refresh_weights_all): the
+            # descriptor arrays are built once (static buffer addresses)
+            if getattr(self, "_refresh_args", None) is None:
+                n = len(self.geoms)
+                meta = (ctypes.c_long * (5 * n))(*[v for g in self.geoms for v in (g.w_off, g.chunk, g.K, g.KP, g.Cout)])
+                wc = (ctypes.c_void_p * n)(*[self.Wc[l].data_ptr() for l in range(n)])
+                wct = (ctypes.c_void_p * n)(*[_lib.ptr(self.WcT[l]) or None for l in range(n)])
+                self._refresh_args = (n, meta, wc, wct)
+            n, meta, wc, wct = self._refresh_args
+            _lib.call("x3_refresh_weights_all", flat.data_ptr(), n, meta, wc, wct, self.M, 1,
+                      self.x3_status.data_ptr(), _lib.stream())
             if self.lstm is not None:
                 ls = self.lstm
                 _lib.call("launch_lstm_refresh_x3", flat.data_ptr(), ls["k_off"], ls["F"], ls["H"], ls["KpT"].data_ptr(),

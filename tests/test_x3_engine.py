@@ -602,6 +602,30 @@ def test_x3_range_overflow_raises_named_error(hip_lib, what):
         tr.flush()
 
 
+def test_x3_refresh_all_layers_one_launch_bit_equal(hip_lib):
+    """Every layer's fp16-pair weight copies in one launch (x3_refresh_weights_all) == one launch per layer
+    (x3_refresh_weights), Wc and WcT bit for bit, after random weights."""
+    from pathnet_gym_amd.ops import _lib
+    tr = _shipped_trainer()
+    hp = tr.model.hip
+    with torch.no_grad():
+        tr.model.store.flat.normal_(0, 0.05)
+    hp.refresh_weights()
+    torch.cuda.synchronize()
+    a = [w.clone() for w in hp.Wc] + [w.clone() for w in hp.WcT if w is not None]
+    for w in list(hp.Wc) + [w for w in hp.WcT if w is not None]:
+        w.zero_()
+    flat = tr.model.store.flat
+    for l, g in enumerate(hp.geoms):
+        _lib.call("x3_refresh_weights", flat.data_ptr(), g.w_off, g.chunk, g.K, g.KP, g.Cout, hp.M,
+                  hp.Wc[l].data_ptr(), _lib.ptr(hp.WcT[l]), 1, hp.x3_status.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    b = [w.clone() for w in hp.Wc] + [w.clone() for w in hp.WcT if w is not None]
+    assert len(a) == len(b) and any(x.abs().sum() > 0 for x in a)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # the reference's default network (BasicLSTMCell(256) after the L=4 trunk, constants.py:30) in fp32x:
 # csrc/lstm_x3.hip against a plain fp32 autograd oracle of the whole update
