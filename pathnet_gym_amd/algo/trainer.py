@@ -351,10 +351,10 @@ class PathNetTrainer:
                 # gradient runs; bucket 2 (the first layer) after it
                 handle = self.comm.exchange_async_split(eng.grad_flat, eng.fitness, eng.counters,
                                                         run_tail=lambda: eng.rollout_backward("tail"),
-                                                        extra=eng.report_tensor())
+                                                        extra=eng.report_parts())
             else:
                 handle = self.comm.exchange_async(eng.grad_flat, eng.fitness, eng.counters,
-                                                  extra=eng.report_tensor())
+                                                  extra=eng.report_parts())
         with tr.phase("optimizer"):
             eng.optimizer_step(lr)              # non-finite reduced gradient: skipped on device, on every rank
         self.global_step += self.cfg.a2c.t_max * self.P * self.E * self.ctx.world

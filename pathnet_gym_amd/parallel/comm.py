@@ -74,6 +74,7 @@ def active_ranges(layout: ParamLayout, expressed: np.ndarray, frozen: np.ndarray
 
 class FusedUpdateComm:
     NCOUNTERS = 4   # agent steps, episodes finished, sum of finished returns, spare
+    NEXTRA = 8      # report values packed behind them on the single-rank path (exchange_async)
 
     def __init__(self, ctx: DistContext, layout: ParamLayout, P_total: int, P_local: int, device,
                  dense_threshold: float = 0.95):
@@ -87,12 +88,16 @@ class FusedUpdateComm:
         self.index = None
         self.ngrad = layout.numel
         self.buf = torch.zeros(layout.numel + P_total + self.NCOUNTERS, dtype=torch.float32, device=device)
-        # static device copy of the reduced [fitness | counters] (read by the device GA / non-finite skip)
-        self.small_dev = torch.zeros(P_total + self.NCOUNTERS, dtype=torch.float32, device=device)
+        # static device copy of the reduced [fitness | counters] (read by the device GA / non-finite skip), followed
+        # by room for the caller's small report: on one rank, exchange_async packs all three with ONE cat and reads
+        # them back with ONE D2H copy
+        self._small_pack = torch.zeros(P_total + self.NCOUNTERS + self.NEXTRA, dtype=torch.float32, device=device)
+        self.small_dev = self._small_pack[:P_total + self.NCOUNTERS]
         self.fit_reduced = self.small_dev[:P_total]
         self.cnt_reduced = self.small_dev[P_total:]
         pin = self.device.type == "cuda"
-        self.host_small = [torch.zeros(P_total + self.NCOUNTERS, dtype=torch.float32, pin_memory=pin) for _ in range(2)]
+        self.host_small = [torch.zeros(P_total + self.NCOUNTERS + self.NEXTRA, dtype=torch.float32, pin_memory=pin)
+                           for _ in range(2)]
         self._flip = 0
         self.force_dense = False
         self.bytes_last = 0
@@ -256,8 +261,14 @@ class FusedUpdateComm:
             rec["tail_gpu_ms"] = e0.elapsed_time(e1)
             rec["n1"], rec["n2"] = n1, n2
             self.overlap_log.append(rec)
+        return self._readback(extra)
+
+    def _readback(self, extra):
+        """Start the D2H of the reduced [fitness | counters] (+ ``extra``) into the pinned double buffer."""
         hb = self.host_small[self._flip]
         ex = None
+        if isinstance(extra, (list, tuple)):
+            extra = torch.cat([e.reshape(-1) for e in extra])
         if extra is not None:
             if getattr(self, "_extra_host", None) is None or self._extra_host[0].shape != extra.shape:
                 self._extra_host = [torch.zeros(extra.shape, dtype=extra.dtype, pin_memory=hb.is_pinned())
@@ -265,7 +276,7 @@ class FusedUpdateComm:
             ex = self._extra_host[self._flip]
             ex.copy_(extra, non_blocking=True)
         self._flip ^= 1
-        hb.copy_(self.small_dev, non_blocking=True)
+        hb[:self.small_dev.numel()].copy_(self.small_dev, non_blocking=True)
         ev = torch.cuda.Event() if hb.is_pinned() else None
         if ev is not None:
             ev.record()
@@ -316,35 +327,44 @@ class FusedUpdateComm:
     def exchange_async(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor, extra=None):
         """Pipelined variant: reduce on the stream, start a non-blocking D2H of [fitness | counters] (+ ``extra``)
         into a pinned double buffer and return a handle for ``collect``; the host does not wait."""
-        P = self.P_total
+        P, NC = self.P_total, self.NCOUNTERS
         if not self.ctx.enabled:
+            self.bytes_last = 0
+            parts = [fitness_local.reshape(-1), counters.reshape(-1)]
+            if isinstance(extra, (list, tuple)):
+                parts += [e.reshape(-1) for e in extra]
+            ne = sum(int(t.numel()) for t in parts) - P - NC
+            if (extra is None or isinstance(extra, (list, tuple))) and ne <= self.NEXTRA and \
+                    all(t.dtype == torch.float32 for t in parts):
+                # one cat into [fitness | counters | report] and one D2H (instead of 2 + 2 copies and 2 D2H)
+                n = P + NC + ne
+                torch.cat(parts, out=self._small_pack[:n])
+                hb = self.host_small[self._flip]
+                self._flip ^= 1
+                hb[:n].copy_(self._small_pack[:n], non_blocking=True)
+                ev = torch.cuda.Event() if hb.is_pinned() else None
+                if ev is not None:
+                    ev.record()
+                return (ev, hb, ne)
             self.small_dev[:P].copy_(fitness_local)
             self.small_dev[P:].copy_(counters)
-            self.bytes_last = 0
         else:
             self._reduce(grad, fitness_local, counters)
-        hb = self.host_small[self._flip]
-        ex = None
-        if extra is not None:
-            if getattr(self, "_extra_host", None) is None or self._extra_host[0].shape != extra.shape:
-                self._extra_host = [torch.zeros(extra.shape, dtype=extra.dtype, pin_memory=hb.is_pinned())
-                                    for _ in range(2)]
-            ex = self._extra_host[self._flip]
-            ex.copy_(extra, non_blocking=True)
-        self._flip ^= 1
-        hb.copy_(self.small_dev, non_blocking=True)
-        ev = torch.cuda.Event() if hb.is_pinned() else None
-        if ev is not None:
-            ev.record()
-        return (ev, hb, ex)
+        return self._readback(extra)
 
     def collect(self, handle):
+        """(fitness [P_total], counters [NCOUNTERS], extra or None) of an ``exchange_async*`` handle; waits for its
+        D2H.  ``extra``: the report packed behind the counters (an int count in the handle) or its own buffer."""
         ev, hb, ex = handle
         if ev is not None:
             ev.synchronize()
         h = hb.numpy()
-        P = self.P_total
-        return h[:P].copy(), h[P:].copy(), (ex.numpy().copy() if ex is not None else None)
+        P, NC = self.P_total, self.NCOUNTERS
+        if isinstance(ex, int):
+            extra = h[P + NC:P + NC + ex].copy() if ex > 0 else None
+        else:
+            extra = ex.numpy().copy() if ex is not None else None
+        return h[:P].copy(), h[P:P + NC].copy(), extra
 
     def exchange(self, grad: torch.Tensor, fitness_local: torch.Tensor, counters: torch.Tensor):
         """All-reduce in place. Returns (fitness_all [P_total] cpu numpy, counters_sum cpu numpy)."""

@@ -639,6 +639,11 @@ class HipEngine:
         pop = self.ga_dev["pop"]
         return self.ga_dev["union_host"].numpy().reshape(pop.L, pop.M).astype(bool)
 
+    def report_parts(self):
+        """(stats [loss_pi, loss_v, entropy, 0], last optimizer step skipped) for the async read-back, the layout of
+        report_tensor; the single-rank exchange packs them behind fitness and counters with one cat and one D2H."""
+        return (self.stats, self.opt_status)
+
     def report_tensor(self) -> torch.Tensor:
         """Assemble [loss_pi, loss_v, entropy, 0, last optimizer step skipped] for the async read-back
         (enqueued after the rollout: the skip flag is the PREVIOUS optimizer step's)."""
