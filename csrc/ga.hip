@@ -214,7 +214,41 @@ __global__ __launch_bounds__(64) void inv_group_kernel(const int* __restrict__ i
   if (lane == 0) gcnt[item] = k;
 }
 
+// The optimizer graph's small tail in one launch (runtime/engine.py _optimizer_body): the local fitness <- the device
+// GA's view, the episode windows of the candidates of tournaments that just fired restarted (fit_window > 0), the
+// frame ring's first-valid-channel row carried (fc_dst = fc_src, n_fc bytes) and the update counter advanced --
+// four to six small torch launches before
+__global__ __launch_bounds__(256) void opt_tail_kernel(const float* __restrict__ fit, const uint8_t* __restrict__ reset,
+                                                       int p_off, int P, int fit_window, float* __restrict__ fitness,
+                                                       float* __restrict__ fit_cnt, float* __restrict__ fit_sum,
+                                                       const uint8_t* __restrict__ fc_src, uint8_t* __restrict__ fc_dst,
+                                                       int n_fc, long long* __restrict__ ctr) {
+  const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (i < P) {
+    fitness[i] = fit[p_off + i];
+    if (fit_window > 0 && reset[p_off + i]) {
+      fit_cnt[i] = 0.f;
+      fit_sum[i] = 0.f;
+    }
+  }
+  if (i < n_fc) fc_dst[i] = fc_src[i];
+  if (i == 0 && ctr) ctr[0] += 1;
+}
+
 extern "C" {
+int launch_opt_tail(const float* fit, const void* reset, int p_off, int P, int fit_window, float* fitness,
+                    float* fit_cnt, float* fit_sum, const void* fc_src, void* fc_dst, int n_fc, long long* ctr,
+                    hipStream_t stream) {
+  if (P < 0 || p_off < 0 || n_fc < 0 || (P > 0 && (!fit || !reset || !fitness || !fit_cnt || !fit_sum)) ||
+      (n_fc > 0 && (!fc_src || !fc_dst))) return -22;
+  const int n = P > n_fc ? P : n_fc;
+  opt_tail_kernel<<<(n > 0 ? n + 255 : 256) / 256, 256, 0, stream>>>(fit, (const uint8_t*)reset, p_off, P, fit_window,
+                                                                    fitness, fit_cnt, fit_sum,
+                                                                    (const uint8_t*)fc_src, (uint8_t*)fc_dst, n_fc,
+                                                                    ctr);
+  return (int)hipGetLastError();
+}
+
 int launch_inv_group(const int* inv_path, const int* inv_slot, const int* inv_cnt, int P, int L, int M, int p0, int np,
                      int* gpath, int* gslot, int* gcnt, hipStream_t stream) {
   if (P <= 0 || L <= 0 || M <= 0 || p0 < 0 || np <= 0 || p0 + np > P || !gpath || !gslot || !gcnt) return -22;

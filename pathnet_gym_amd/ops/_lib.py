@@ -64,6 +64,7 @@ _SIGS = {
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_uint, c_int, P, P, P, P, P, P],
     "launch_pong_digit_tables": [P, c_int, c_int, c_int, c_int, c_int, P],
     "x3_refresh_weights_all": [P, c_int, P, P, P, c_int, c_int, P, P],
+    "launch_opt_tail": [P, P, c_int, c_int, c_int, P, P, P, P, P, c_int, P, P],
     "pong_tables_ints": [],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],

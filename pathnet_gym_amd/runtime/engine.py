@@ -598,7 +598,7 @@ class HipEngine:
         g["fit"].copy_(torch.from_numpy(pop.fitness.astype(np.float32)))
         self._union_ev = None          # the last read-back union described the old genotypes
 
-    def _ga_body(self):
+    def _ga_body(self, sync_fitness: bool = True):
         g = self.ga_dev
         pop = g["pop"]
         hp = self.hip
@@ -613,7 +613,10 @@ class HipEngine:
         _lib.call("launch_active_union", g["geno"].data_ptr(), g["frozen"].data_ptr(), pop.P, pop.L, pop.M,
                   g["union"].data_ptr(), st)
         # local fitness <- the GA's view; ONLY the candidates of tournaments that just fired restart their
-        # episode window (paths still filling theirs keep accumulating)
+        # episode window (paths still filling theirs keep accumulating).  sync_fitness False: the optimizer tail
+        # does it (launch_opt_tail)
+        if not sync_fitness:
+            return
         self.fitness.copy_(g["fit"][g["p_off"]:g["p_off"] + self.P])
         if self.fit_window > 0:
             fired = g["reset"][g["p_off"]:g["p_off"] + self.P].bool()
@@ -694,13 +697,24 @@ class HipEngine:
                   self.lr.data_ptr(), self.opt_status.data_ptr(), o.decay, o.momentum, o.epsilon, o.clip_norm,
                   _lib.stream())
         self.hip.refresh_weights()
+        tail = self.ga_dev is not None and os.environ.get("PATHNET_OPT_TAIL", "1") != "0"
         if self.ga_dev is not None:
-            self._ga_body()
+            self._ga_body(sync_fitness=not tail)
         if self.ring:
             # through an int64 view: 8 bytes per element (the uint8 strided copy ran at ~3.4 TB/s, 92 us per update)
             f64 = self.frames.view(torch.int64) if self.HW % 8 == 0 else self.frames
             src = f64[:, self.T:self.T + 4]
             f64[:, 0:4].copy_(src if self.T >= 4 else src.clone())   # T < 4: the slot ranges overlap
+        if tail:
+            # the GA's local fitness view, fired windows reset, the ring's fc row carried and the counter advanced:
+            # one launch (csrc/ga.hip opt_tail_kernel)
+            g = self.ga_dev
+            _lib.call("launch_opt_tail", g["fit"].data_ptr(), g["reset"].data_ptr(), g["p_off"], self.P,
+                      self.fit_window, self.fitness.data_ptr(), self.fit_cnt.data_ptr(), self.fit_sum.data_ptr(),
+                      self.fc[self.T].data_ptr() if self.ring else None, self.fc[0].data_ptr() if self.ring else None,
+                      self.B if self.ring else 0, self.ctr.data_ptr(), _lib.stream())
+            return
+        if self.ring:
             self.fc[0].copy_(self.fc[self.T])
         self.ctr.add_(1)
 

@@ -602,6 +602,31 @@ def test_x3_range_overflow_raises_named_error(hip_lib, what):
         tr.flush()
 
 
+def test_optimizer_tail_one_launch_matches_torch_ops(hip_lib, monkeypatch):
+    """The optimizer graph's tail in one launch (csrc/ga.hip opt_tail_kernel: the GA's local fitness view, fired
+    windows reset, the ring's fc row carried, the update counter) == the torch ops it replaces, over updates whose
+    tournaments fire (short episodes), through the graph capture and replays."""
+    runs = []
+    for tail in ("0", "1"):
+        monkeypatch.setenv("PATHNET_OPT_TAIL", tail)
+        tr = _shipped_trainer(paths=4, envs=16, tmax=3)
+        tr.cfg.a2c.lr = 0.0
+        tr.env.max_episode_steps = 4
+        e = tr.engine
+        snaps = []
+        for _ in range(6):
+            tr.update()
+            torch.cuda.synchronize()
+            snaps.append((e.fitness.clone(), e.fit_cnt.clone(), e.fit_sum.clone(), e.fc.clone(), e.ctr.clone(),
+                          e.ga_dev["geno"].clone()))
+        tr.flush()
+        runs.append(snaps)
+    assert any(bool(x[1].eq(0).any()) for x in runs[1][2:])
+    for u, (a, b) in enumerate(zip(*runs)):
+        for k, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), (u, k)
+
+
 def test_x3_refresh_all_layers_one_launch_bit_equal(hip_lib):
     """Every layer's fp16-pair weight copies in one launch (x3_refresh_weights_all) == one launch per layer
     (x3_refresh_weights), Wc and WcT bit for bit, after random weights."""
