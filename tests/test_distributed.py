@@ -185,3 +185,28 @@ def test_strong_scaling_four_ranks_reproduce_one_process():
     np.testing.assert_allclose(four["ms"], one["ms"], rtol=1e-4, atol=1e-6)
     for r in range(1, 4):                                      # replicas stay bit-identical across ranks
         assert np.array_equal(res[r]["flat"], four["flat"])
+
+
+def test_single_rank_exchange_packs_the_report():
+    """One rank: fitness, counters and the report parts are packed by one cat and read back by one copy
+    (parallel/comm.py exchange_async); the reduced views the device GA reads hold the fitness and counters; a tensor
+    report and no report keep working."""
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    from pathnet_gym_amd.config import preset
+    cfg = preset("cartpole-cpu")
+    cfg.paths, cfg.envs_per_path = 3, 4
+    tr = PathNetTrainer(cfg, device="cpu")
+    comm = tr.comm
+    assert not comm.ctx.enabled
+    P = comm.P_total
+    fit = torch.arange(P, dtype=torch.float32) + 0.5
+    cnt = torch.tensor([1.0, 2.0, 3.0, 4.0])
+    f, c, e = comm.collect(comm.exchange_async(None, fit, cnt, extra=(torch.tensor([5.0, 6.0, 7.0, 8.0]),
+                                                                      torch.tensor([9.0]))))
+    assert np.array_equal(f, fit.numpy()) and np.array_equal(c, cnt.numpy())
+    assert np.array_equal(e, np.array([5.0, 6.0, 7.0, 8.0, 9.0], dtype=np.float32))
+    assert torch.equal(comm.fit_reduced, fit) and torch.equal(comm.cnt_reduced, cnt)
+    f, c, e = comm.collect(comm.exchange_async(None, fit, cnt, extra=torch.tensor([1.0, 2.0])))
+    assert np.array_equal(e, np.array([1.0, 2.0], dtype=np.float32)) and np.array_equal(c, cnt.numpy())
+    f, c, e = comm.collect(comm.exchange_async(None, fit, cnt))
+    assert e is None and np.array_equal(f, fit.numpy())
