@@ -3912,7 +3912,7 @@ static int X3_PRESPLIT = 1;
 static int X3_FH_D = 3;        // fused last fc + heads: k-steps of fragments in flight (fc_heads_fwd_x3 D)
 static int X3_DG_TARGET = 512;     // 4x4/s2 input gradient (2048 -> 1536 -> 512: 8 paths 224 -> 214 -> 191 -> 167 us with
                                    // the conv2 weight gradient)
-// module-major fc forward k split: 0 = auto by rows (P*T*E <= 512: 4 parts, else 2), else the fixed part count (2 / 4 /
+// module-major fc forward k split: 0 = auto by rows (P*T*E <= 768: 4 parts, else 3), else the fixed part count (2 / 3 / 4 /
 // 8), capped so every part keeps >= 2 k-steps
 static int X3_FC_KS_PARTS = 0;
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
@@ -3952,7 +3952,7 @@ void fast_conv_set_x3_dg3_target(int v) { X3_DG3_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_wg_auto(int v) { X3_WG_AUTO = v; }
 void fast_conv_set_x3_wg_target(int v) { X3_WG_TARGET = v < 0 ? 0 : v; }
 void fast_conv_set_x3_dg_target(int v) { X3_DG_TARGET = v < 0 ? 0 : v; }
-void fast_conv_set_x3_fc_ks_parts(int v) { X3_FC_KS_PARTS = (v == 2 || v == 4 || v == 8) ? v : 0; }
+void fast_conv_set_x3_fc_ks_parts(int v) { X3_FC_KS_PARTS = (v == 2 || v == 3 || v == 4 || v == 8) ? v : 0; }
 
 int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits, const void* Wc, long wlo,
                 const float* flat, long bias_off, int chunk, const int* ai, const int* ac, int layer, int L, int M,
@@ -4340,9 +4340,11 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
     // slot sum in fc_slot_sum2_x3
     int ks = X3_FC_MMV >= 4 ? 4 : 2;
     if (X3_FC_KS_PARTS > 0) ks = X3_FC_KS_PARTS;
-    // 4 parts up to 512 rows (layer A/B, profiles/r5/ab_ks*.json: 8 paths 22.0 (8 parts) -> 21.6, 16 paths 27.9 (2)
-    // -> 23.9, 24 paths 28.3 -> 24.4 us; 32 paths 29.2 (2) vs 33.8 (4))
-    else if (X3_FC_MMV == 3) ks = (long)P * R <= 512 ? 4 : 2;
+    // 4 parts up to 768 rows, else 3 (layer A/B, profiles/r5/ab_ks*.json: 8 paths 22.0 (8 parts) -> 21.6, 16 paths
+    // 27.9 (2) -> 23.9, 24 paths 28.7 (2) / 26.1 (3) / 24.8 (4); 32 paths 29.3 (2) / 28.7 (3) / 33.9 (4); 64 paths
+    // 48.1 (2) / 46.1 (3) / 51.5 (4) us: at two workgroups per CU, 3 parts keep the ~280 units of 64 paths in one
+    // round of 512 slots where 4 parts spill into a second)
+    else if (X3_FC_MMV == 3) ks = (long)P * R <= 768 ? 4 : 3;
     while (ks > 2 && (KP / 32) / ks < 2) ks >>= 1;           // every part keeps >= 2 k-steps
     const int umax = (ks * M * 2 * ((P * R + 127) / 128) + 7) / 8 * 8;
     const unsigned g2 = (unsigned)(((long)P * R * 32 + 255) / 256);
@@ -4365,7 +4367,7 @@ int x3_fc_fwd_mm(const void* X, long xlo, int ldx, void* Y, long ylo, void* bits
         fc_slot_sum2_x3<false, KS_><<<g2, 256, 0, st>>>(Ys, ai, ac, flat, bias_off, chunk, (uint16_t*)bits, br,    \
                                                         layer, L, M, P, E, T, t0, Y, ylo, os);                     \
     }
-    if (ks == 8) MM2KS(8) else if (ks == 4) MM2KS(4) else MM2KS(2)
+    if (ks == 8) MM2KS(8) else if (ks == 4) MM2KS(4) else if (ks == 3) MM2KS(3) else MM2KS(2)
 #undef MM2KS
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
