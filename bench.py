@@ -91,12 +91,17 @@ def solve_key(cfg, preset_name: str) -> dict:
             "rmsp_epsilon": cfg.a2c.rmsp_epsilon}
 
 
-def solve_records(key: dict, n_gpus: int):
-    """Every committed solve run (profiles/solve/*.json, written by scripts/solve.py --out) whose config equals
-    ``key`` on ``n_gpus`` GPUs -- solved or not, every seed -- or None when no run of this exact config exists."""
+def solve_records(key: dict, n_gpus: int, sources: str = None):
+    """The committed solve runs (profiles/solve/*.json, written by scripts/solve.py --out) of exactly this config on
+    ``n_gpus`` GPUs, under the v2 criterion (algo/solve.py: the task horizon where the lr anneal reaches 0, a held-out
+    confirmation of the winning path) and built from the same sources as the running library (``sources``, the
+    build's sources_sha256; None = any build), ONE record per distinct seed (the latest).  Runs that stopped on a wall
+    limit before the horizon without solving say nothing about the horizon and are listed apart.  The statistic is the
+    median over seeds with "unsolved at horizon" counted as infinite: null unless most seeds solved."""
     import glob
+    from pathnet_gym_amd.algo.solve import CRITERION
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "solve")
-    runs = []
+    by_seed, excluded = {}, {"other_config": 0, "pre_v2_criterion": 0, "other_build": 0, "wall_limited": 0}
     for f in sorted(glob.glob(os.path.join(root, "*.json"))):
         try:
             d = json.loads(open(f).read().strip().splitlines()[-1])
@@ -109,17 +114,44 @@ def solve_records(key: dict, n_gpus: int):
         c = dict(c, dtype=c.get("dtype", "bf16"), lr=round(float(c.get("lr", 0.0)), 8),
                  rmsp_epsilon=c.get("rmsp_epsilon", 0.1))
         if any(c.get(k) != key[k] for k in SOLVE_KEYS):
+            excluded["other_config"] += 1
             continue
-        runs.append({"seed": c.get("seed"), "solved": bool(d.get("solved")),
-                     "generations": d.get("generations_to_solve"), "frames": d.get("frames_to_solve"),
-                     "seconds": d.get("seconds_to_solve"), "best_winner": d.get("best_winner_fitness"),
-                     "budget_s": d.get("seconds"), "file": os.path.relpath(f, os.path.dirname(root))})
+        if d.get("criterion") != CRITERION:
+            excluded["pre_v2_criterion"] += 1
+            continue
+        if sources is not None and (d.get("build") or {}).get("sources_sha256") != sources:
+            excluded["other_build"] += 1
+            continue
+        if not d.get("solved") and d.get("stopped") != "horizon":
+            excluded["wall_limited"] += 1
+            continue
+        r = {"seed": c.get("seed"), "solved": bool(d.get("solved")), "generations": d.get("generations_to_solve"),
+             "updates": d.get("updates_to_solve"), "frames": d.get("frames_to_solve"),
+             "seconds": d.get("train_seconds_to_solve") or d.get("seconds_to_solve"), "lr_at_solve": d.get("lr_at_solve"),
+             "heldout_mean": d.get("heldout_mean"), "winner_fitness": d.get("winner_fitness"),
+             "unconfirmed_candidates": sum(1 for x in d.get("candidates", []) if not x.get("confirmed")),
+             "stopped": d.get("stopped"), "deterministic": bool(c.get("deterministic")),
+             "finished_at": d.get("finished_at", 0.0), "file": os.path.relpath(f, os.path.dirname(root))}
+        old = by_seed.get(r["seed"])
+        if old is None or r["finished_at"] >= old["finished_at"]:
+            by_seed[r["seed"]] = r
+    runs = [by_seed[k] for k in sorted(by_seed, key=lambda x: (x is None, x))]
     if not runs:
-        return {"value": None, "note": "no scripts/solve.py run of exactly this config is committed", "config": key}
-    gens = sorted(r["generations"] for r in runs if r["solved"])
-    med = gens[len(gens) // 2] if gens and len(gens) * 2 > len(runs) else None
-    return {"value": med, "statistic": "median over seeds (null unless most seeds solved)",
-            "solved_seeds": len(gens), "seeds": len(runs), "runs": runs, "config": key}
+        return {"value": None, "note": "no v2-criterion scripts/solve.py run of exactly this config and build is "
+                "committed", "config": key, "excluded": excluded, "build_sources_sha256": sources}
+    inf = float("inf")
+    gens = sorted(r["generations"] if r["solved"] else inf for r in runs)
+    upd = sorted(r["updates"] if r["solved"] else inf for r in runs)
+    med = statistics.median(gens)
+    solved = [g for g in gens if g != inf]
+    return {"value": None if med == inf else med,
+            "statistic": "median over distinct seeds, unsolved-at-horizon counted as infinite (null unless most "
+                         "seeds solved)",
+            "min": min(solved) if solved else None, "max": max(gens) if gens[-1] != inf else "unsolved",
+            "updates_median": None if statistics.median(upd) == inf else statistics.median(upd),
+            "solved_seeds": len(solved), "seeds": len(runs), "runs": runs, "config": key, "excluded": excluded,
+            "build_sources_sha256": sources,
+            "criterion": CRITERION}
 
 
 def build_trainer(args, ctx, dtype: str, stagger: bool, paths_total: int = 0):
@@ -153,9 +185,25 @@ def build_trainer(args, ctx, dtype: str, stagger: bool, paths_total: int = 0):
     return cfg, tr
 
 
-def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: bool = False):
+def gpu_telemetry() -> dict:
+    """GPU clock / power / temperature now (torch.cuda's SMI queries, amdsmi on ROCm); {} where unavailable."""
+    import torch
+    out = {}
+    if not torch.cuda.is_available():
+        return out
+    for k, f in (("sclk_mhz", "clock_rate"), ("power", "power_draw"), ("temp_c", "temperature")):
+        try:
+            out[k] = getattr(torch.cuda, f)()
+        except Exception:
+            pass
+    return out
+
+
+def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: bool = False, info=None):
     """W untimed updates, then ``windows`` back-to-back windows of EXACTLY K updates, each between barrier +
-    synchronize on both sides; a window's time is the max over ranks.  Returns [(seconds, frames, generations)]."""
+    synchronize on both sides; a window's time is the max over ranks.  Returns [(seconds, frames, generations)].
+    ``info`` (a list): per window, the GPU telemetry sampled while its last updates still run (before the drain) and
+    the population's mean active modules per layer (mutation can grow a path; the work per update follows it)."""
     import torch
 
     def sync():
@@ -179,12 +227,18 @@ def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: b
         t0 = time.perf_counter()
         for _ in range(steps):
             tr.update()
+        tel = gpu_telemetry() if info is not None else None
         tr.flush()                               # drain the pipelined host bookkeeping of the last update
         if markers and w == 0:
             _plib.call("launch_prof_marker", 2, _plib.stream())
         sync()
         dt = ctx.max_scalar(time.perf_counter() - t0)
         out.append((dt, tr.global_step - step0, tr.pop.generation - gen0))   # whole-job agent steps
+        if info is not None:
+            ex = tr.pop.expressed()
+            tel["active_modules_per_layer"] = [round(float(x), 3) for x in ex.sum(axis=2).mean(axis=0)]
+            tel["ms"] = round(dt / steps * 1e3, 3)
+            info.append(tel)
     return out
 
 
@@ -197,44 +251,37 @@ def window_summary(wins, steps: int) -> dict:
 
 
 def in_run_solve(args, ctx, dtype: str, cap_s: float, paths_total: int = 0) -> dict:
-    """One seed of generations-to-solve on a FRESH trainer of the bench config, observed inside this run (hard wall
-    cap; scripts/solve.py is the multi-seed version): the first tournament whose winner fitness reaches the task's
-    reward threshold.  Every rank takes the same decisions: the GA state (hence "solved") is replicated, and the
-    wall cap is checked every 64 updates on the max over ranks of the elapsed time."""
-    from pathnet_gym_amd.envs.registry import reward_threshold
+    """One seed of generations-to-solve on a FRESH trainer of the bench config, observed inside this run under a hard
+    wall cap (scripts/solve.py is the multi-seed version), with the criterion of algo/solve.py: a tournament winner at
+    the reward threshold, confirmed by a held-out evaluation of its path, before the task horizon.  Every rank takes
+    the same decisions (replicated GA, rank 0's held-out mean, a collective wall-cap check every 32 updates)."""
+    from pathnet_gym_amd.algo.solve import SolveTracker
     cfg, tr = build_trainer(args, ctx, dtype, stagger=False, paths_total=paths_total)
-    thr = reward_threshold(cfg.tasks[0])
     t0 = time.time()
-    last = t0
-    best = -math.inf
-    out = {"seed": cfg.seed, "threshold": thr, "cap_s": round(cap_s, 1), "solved": False,
-           "paths_per_gpu": cfg.paths, "paths_total": tr.P_total}
-    while True:
-        st = tr.update()
+    last = [t0]
+
+    def progress(c=None):
         now = time.time()
-        if now - last > 30 and ctx.is_main:      # progress on stderr (the JSON line stays the only stdout line)
-            last = now
+        if ctx.is_main and (c is not None or now - last[0] > 30):     # stderr: the JSON line stays the only stdout line
+            last[0] = now
             print(f"[bench] solve t={now - t0:.0f}s generation={tr.pop.generation} frames={tr.global_step} "
-                  f"updates={tr.updates} best_winner={best:.2f}", file=sys.stderr, flush=True)
-        if st.tournaments:
-            best = max(best, st.best_winner)
-            if st.best_winner >= thr:
-                out.update(solved=True, generations=tr.pop.generation, frames=tr.global_step, updates=tr.updates,
-                           seconds=round(time.time() - t0, 1))
-                break
-        if tr.updates % 64 == 0 and ctx.max_scalar(time.time() - t0) >= cap_s:
-            break
+                  f"updates={tr.updates} best_winner={trk.best:.2f}" + (f" candidate={c}" if c else ""),
+                  file=sys.stderr, flush=True)
+
+    trk = SolveTracker(tr, wall_s=cap_s, log=progress)
+    while not trk.observe(tr.update()):
+        progress()
     tr.flush()
-    out.update(best_winner=best if best > -math.inf else None, generations_run=tr.pop.generation,
-               frames_run=tr.global_step, updates_run=tr.updates, wall_s=round(time.time() - t0, 1))
+    out = {"seed": cfg.seed, "cap_s": round(cap_s, 1), "paths_per_gpu": cfg.paths, "paths_total": tr.P_total}
+    out.update(trk.record())
     return out
 
 
-def committed_updates_to_solve(key: dict) -> list:
-    """Optimizer updates each committed solved seed of the one-GPU bench config needed (frames / frames per update)."""
-    rec = solve_records(key, 1)
-    per_update = key["paths_per_gpu"] * key["envs_per_path"] * key["t_max"]
-    return sorted(int(round(r["frames"] / per_update)) for r in rec.get("runs", []) if r["solved"] and r["frames"])
+def committed_updates_to_solve(key: dict, sources: str = None) -> list:
+    """Optimizer updates each committed solved seed (solve_records: v2 criterion, this build) of the one-GPU bench
+    config needed."""
+    rec = solve_records(key, 1, sources)
+    return sorted(int(r["updates"]) for r in rec.get("runs", []) if r["solved"] and r["updates"])
 
 
 def self_launch(n: int) -> int:
@@ -336,6 +383,28 @@ def per_rank_shapes(args, ctx, numel: int, upd: list, headline_ms: float) -> dic
                           "updates.  A prediction, not a measured multi-GPU solve"}
 
 
+def reference_preset_windows(args, ctx) -> dict:
+    """The reference's OWN default network (USE_LSTM=True, constants.py:30-31: L=4 = 3 conv + linear 1408->256, M=10,
+    N=4, BasicLSTMCell(256), game_ac_network.py:303-521; 18-way head, ACTION_SIZEZ) on its first task (synthetic
+    Alien, aliencentipede.txt) at the bench's paths x envs, same dtype, windows and warmup as the headline."""
+    from pathnet_gym_amd.config import preset
+    a = argparse.Namespace(**vars(args))
+    a.preset = "reference"
+    a.env = None
+    cfg, trr = build_trainer(a, ctx, args.dtype, False)
+    w = window_summary(timed_windows(trr, ctx, args.steps, args.warmup, args.windows), args.steps)
+    net = cfg.net
+    out = {"preset": "reference", "env": cfg.tasks[0], "dtype": trr.compute_dtype,
+           "model": f"PathNet L={net.L} (conv 8x8/4, 4x4/2, 3x3/1 + fc {net.layers[-1].out}) x M={net.M}, N={net.N}, "
+                    f"LSTM {net.lstm_size}, {net.num_actions} actions",
+           "paths_per_gpu": cfg.paths, "envs_per_path": cfg.envs_per_path, "t_max": cfg.a2c.t_max,
+           "ms_per_update": round(w["ms"], 3), "windows_ms": w["all"], "spread_pct": w["spread_pct"],
+           "frames_per_sec": round(w["frames"] / (w["ms"] * args.steps / 1e3), 1),
+           "frame_ring": bool(getattr(trr.engine, "ring", False)), "lstm_hip": bool(trr.engine.lstm_hip)}
+    del trr
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -377,6 +446,8 @@ def main():
                          "several GPUs, the strong-scaling config, what is left of 480 s, at most 300 s; 0 = off)")
     ap.add_argument("--compare-bf16", type=int, default=None,
                     help="also time the bf16 engine on the same config (default: on for one GPU)")
+    ap.add_argument("--reference-preset", type=int, default=None,
+                    help="also time the reference's own LSTM network (preset 'reference'; default: on for one GPU)")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling windows on several GPUs")
     ap.add_argument("--prof-window", action="store_true",
                     help="launch marker kernels around the first timed window (scripts/prof_window.py summarises the "
@@ -423,7 +494,14 @@ def main():
     compare = args.compare_bf16 if args.compare_bf16 is not None else int(single and args.dtype != "bf16")
     stagger = not args.no_stagger
     cfg, tr = build_trainer(args, ctx, args.dtype, stagger, paths_total=head_total)
-    wins = timed_windows(tr, ctx, args.steps, args.warmup, args.windows, markers=args.prof_window)
+    verified = None
+    if verify_h is not None:
+        # the cold build (8 niced hipcc jobs) runs while torch imports and the trainer builds; it is joined HERE, so
+        # no compiler competes with any timed window
+        verified = finish_build_verify(verify_h)
+        verify_h = None
+    tele = []
+    wins = timed_windows(tr, ctx, args.steps, args.warmup, args.windows, markers=args.prof_window, info=tele)
     ws = window_summary(wins, args.steps)
     dt = ws["ms"] * args.steps / 1e3
     value = ws["frames"] / dt
@@ -451,6 +529,7 @@ def main():
         "windows": args.windows,
         "windows_ms_per_step": ws["all"],
         "spread_pct": ws["spread_pct"],
+        "windows_telemetry": tele,
         "data": (f"synthetic: on-device Atari-style {cfg.tasks[0]} simulator (210x160 RGB -> gray 160x120 x4 "
                  "stack), random-init weights") if len(cfg.net.input_shape) == 3 else
                 f"synthetic: on-device {cfg.tasks[0]}, random-init weights",
@@ -472,7 +551,7 @@ def main():
                   f"fitness {cfg.ga.fitness} over {cfg.ga.window_for(cfg.envs_per_path)} episodes)",
             "pipelined": bool(tr.pipelined),
             "overlap_allreduce": bool(getattr(tr.engine, "split", False)),
-            "deterministic": bool(getattr(tr.model.hip, "deterministic", False)),
+            "deterministic": bool(getattr(tr.model.hip, "reproducible", False)),
             "episode_stagger": stagger,
         },
         "generations_in_timed_window": int(wins[0][2]),
@@ -492,10 +571,15 @@ def main():
         rec["windows_ms_per_step_bf16"] = wb["all"]
         del trb
     torch.cuda.empty_cache() if torch.cuda.is_available() else None
+    ref_on = args.reference_preset if args.reference_preset is not None else int(single and args.preset == "pong")
+    if ref_on:
+        rec["reference_preset"] = reference_preset_windows(args, ctx)
+        torch.cuda.empty_cache() if torch.cuda.is_available() else None
     # strong scaling: the one-GPU population (64 paths) split over the ranks
     key = solve_key(cfg, args.preset)
     key1 = dict(key, paths_per_gpu=args.paths_total, concurrent_tournaments=max(1, args.paths_total // 16))
-    upd = committed_updates_to_solve(key1)
+    sources = (build_info or {}).get("sources_sha256")
+    upd = committed_updates_to_solve(key1, sources)
     strong = None
     if args.scaling == "strong" or (world == 1 and args.paths == args.paths_total):
         strong = {"ms_per_update": round(ws["ms"], 3), "windows_ms": ws["all"], "same_as_headline": True}
@@ -537,10 +621,10 @@ def main():
             rec["strong_scaling"]["in_run_solve"] = r
         else:
             rec["generations_to_solve_in_run"] = r
-    if verify_h is not None:
-        rec.setdefault("build", {})["verified"] = finish_build_verify(verify_h)
+    if verified is not None:
+        rec.setdefault("build", {})["verified"] = verified
     if ctx.is_main:
-        rec["generations_to_solve"] = solve_records(key, world)
+        rec["generations_to_solve"] = solve_records(key, world, sources)
         print(json.dumps(rec), flush=True)
     ctx.destroy()
 

@@ -152,3 +152,42 @@ DEVI uint32_t env_rand_u32(uint32_t seed, uint32_t env_id, uint32_t counter, uin
 }
 
 #define HIP_LAUNCH_CHECK() (hipGetLastError())
+
+// ---------------------------------------------------------------------------------------------------------------
+// Order-independent (bit-reproducible) weight-gradient accumulation: TrainConfig.deterministic with fp32x.
+// Every contribution that would meet others in an fp32 atomic is added as an int64 fixed-point number in units of
+// 2^-FX_SHIFT instead (global_atomic_add_x2 / ds_add_u64).  Integer addition is associative, so the sum does not
+// depend on the order in which workgroups or waves arrive; x3_fx_flush converts it back and adds it to the fp32
+// gradient.  fx == nullptr selects the fp32 atomics (the default, non-deterministic mode).
+// Resolution 2^-34 ~ 5.8e-11 absolute per contribution; range guard: a contribution of magnitude >= FX_LIMIT (or a
+// NaN) sets fx[-1], which the flush turns into the fp32x range flag (runtime.guard.X3RangeError) -- with at most 2^13
+// contributions per entry (every kernel here stays below it) the int64 sum cannot wrap.
+// ---------------------------------------------------------------------------------------------------------------
+#define FX_SHIFT 34
+extern long long* g_fx_accum;      // host side: the accumulator of the backward being launched (csrc/trunk_x3.hip)
+#define FX_LIMIT 65536.f
+DEVI unsigned long long fx_q(float v) { return (unsigned long long)__float2ll_rn(v * 0x1p34f); }
+DEVI void fx_guard(long long* fx, float v) {
+  if (!(fabsf(v) < FX_LIMIT)) atomicOr(reinterpret_cast<unsigned long long*>(fx - 1), 1ull);
+}
+// grad[i] += v, many writers
+DEVI void gacc(float* grad, long long* fx, long i, float v) {
+  if (fx) {
+    fx_guard(fx, v);
+    atomicAdd(reinterpret_cast<unsigned long long*>(fx + i), fx_q(v));
+  } else {
+    atomicAdd(grad + i, v);
+  }
+}
+// LDS partial (a workgroup's bias sums): float atomics, or int64 fixed point in the same (8-byte) slots
+DEVI void lds_acc(float* f, unsigned long long* q, int i, float v, bool det) {
+  if (det) atomicAdd(q + i, fx_q(v));
+  else atomicAdd(f + i, v);
+}
+// fx[i] += q (an LDS fixed-point partial, already quantised), with the same range guard
+DEVI void gacc_q(long long* fx, long i, unsigned long long q) {
+  const long long s = (long long)q;
+  if (s >= (1ll << 50) || s <= -(1ll << 50)) atomicOr(reinterpret_cast<unsigned long long*>(fx - 1), 1ull);
+  atomicAdd(reinterpret_cast<unsigned long long*>(fx + i), q);
+}
+DEVI float fx_f(unsigned long long q) { return (float)((double)(long long)q * 0x1p-34); }

@@ -309,11 +309,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_gemm_x3_kernel(
 __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
     const float* __restrict__ xh, const float* __restrict__ dz, float* __restrict__ grad, long k_off, long b_off,
     int F, int H, long R, int rows_per_chunk, const float* __restrict__ amax_dz, int T,
-    const float* __restrict__ amax_xh) {
+    const float* __restrict__ amax_xh, long long* __restrict__ fx) {
   constexpr int S = 64 + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][32 * S];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][32 * S];
-  __shared__ float dbias[64];
+  __shared__ unsigned long long dbq[64];         // det: int64 fixed point (common.h gacc); else the float view
+  float* const dbias = reinterpret_cast<float*>(dbq);
   const int KK = F + H, G4 = 4 * H;
   const int n0b = blockIdx.x * 64, p0b = blockIdx.y * 64;
   const long r_beg = (long)blockIdx.z * rows_per_chunk;
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
   const bool do_bias = blockIdx.x == 0;
-  if (tid < 64) dbias[tid] = 0.f;
+  if (tid < 64) dbq[tid] = 0ull;
   f4v acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a) { acc[a][0] = {0.f, 0.f, 0.f, 0.f}; acc[a][1] = {0.f, 0.f, 0.f, 0.f}; }
@@ -374,13 +375,16 @@ __global__ __launch_bounds__(256) void lstm_wgrad_x3_kernel(
       for (int r = 0; r < 4; ++r) {
         const int n = n0b + (mt0 + i) * 16 + 4 * grp + r;
         const int p = p0b + (nt0 + jj) * 16 + i16;
-        atomicAdd(&grad[k_off + (long)n * G4 + p], acc[i][jj][r] * (1.0f / (sx * sg)));
+        gacc(grad, fx, k_off + (long)n * G4 + p, acc[i][jj][r] * (1.0f / (sx * sg)));
       }
   if (do_bias) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) atomicAdd(&dbias[sc + c], bpart[c]);
+    for (int c = 0; c < 8; ++c) lds_acc(dbias, dbq, sc + c, bpart[c], fx != nullptr);
     __syncthreads();
-    if (tid < 64) atomicAdd(&grad[b_off + p0b + tid], dbias[tid]);
+    if (tid < 64) {
+      if (fx) gacc_q(fx, b_off + p0b + tid, dbq[tid]);
+      else atomicAdd(&grad[b_off + p0b + tid], dbias[tid]);
+    }
   }
 }
 
@@ -460,7 +464,7 @@ int launch_lstm_wgrad_x3(const float* xh, const float* dz, float* grad, long k_o
   if (F % 64 != 0 || H % 64 != 0 || rows_per_chunk % 32 != 0) return -1;
   dim3 grid((F + H) / 64, (4 * H) / 64, (unsigned)((R + rows_per_chunk - 1) / rows_per_chunk));
   lstm_wgrad_x3_kernel<<<grid, 256, 0, stream>>>(xh, dz, grad, k_off, b_off, F, H, R, rows_per_chunk, amax_dz, T,
-                                                 amax_xh);
+                                                 amax_xh, g_fx_accum);
   return (int)hipGetLastError();
 }
 

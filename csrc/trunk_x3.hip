@@ -155,6 +155,7 @@ DEVI float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
 // (HipPathNet.check_x3_status raises X3RangeError).
 #define X3_RANGE_W 1u        // a weight * 2^X3_W0_SHIFT left the fp16 range (refresh_x3_kernel)
 #define X3_RANGE_ACT 2u      // an activation written as an fp16 pair left the fp16 range (forward epilogues)
+#define X3_RANGE_FX 4u       // deterministic mode: a weight-gradient contribution left the fixed-point range (x3_fx_flush)
 __device__ uint32_t g_x3_range;
 DEVI bool x3_oor(float v) { return !(fabsf(v) < 65504.f); }     // NaN counts as out of range
 DEVI void x3_flag_range(bool bad) {
@@ -1289,7 +1290,8 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
                                                             int P, int E, int T, long bits_rows, int units_per_wg,
                                                             float in_scale, float g_scale,
                                                             const uint8_t* __restrict__ fcv, int nslots,
-                                                            const float* __restrict__ gamax, int pmap) {
+                                                            const float* __restrict__ gamax, int pmap,
+                                                            long long* __restrict__ fx) {
   using SB = Slab<G, OB>;
   static_assert(!RING || (G::U8 && G::CIN == 4 && G::WIN % 4 == 0), "ring input: uint8 4-channel first layer");
   // ring: 4-pixel groups per slab (one 16-byte LDS store each; 8-pixel groups, one round of loads but four stores
@@ -1310,7 +1312,8 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
   constexpr int GIT = (GROWS * 4 + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][NXP][SB::SLABP];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][2][GROWS * GS];
-  __shared__ float dbias[X3_NCT * 16];
+  __shared__ unsigned long long dbq[X3_NCT * 16];       // det: int64 fixed point; else the float view
+  float* const dbias = reinterpret_cast<float*>(dbq);
   __shared__ int mods[X3_MAXM];
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
@@ -1319,7 +1322,7 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
   if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
-  if (tid < X3_NCT * 16) dbias[tid] = 0.f;
+  if (tid < X3_NCT * 16) dbq[tid] = 0ull;
   for (int i = tid; i < 2 * NXP * 64; i += 256) Xs[i / (NXP * 64)][(i / 64) % NXP][SB::SLAB + (i & 63)] = 0;
   const int PE = P * E;
   const int nunits = T * E * SB::NB;
@@ -1594,7 +1597,7 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int k = mt * 16 + 4 * grp + r;
-            if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale * ginv));
+            if (k < G::K) gacc(grad, fx, base + (long)k * 8 + ch, acc[mi][nt][r] * (in_scale * g_scale * ginv));
           }
         }
       }
@@ -1605,7 +1608,7 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
       const int slot = 2 * ct0 + rel;
       if (rel < 2 * NC && slot < cnt) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) atomicAdd(&dbias[slot * 8 + c], acc_b[k][c >> 1][c & 1] * g_scale);
+        for (int c = 0; c < 8; ++c) lds_acc(dbias, dbq, slot * 8 + c, acc_b[k][c >> 1][c & 1] * g_scale, fx != nullptr);
       }
     }
   };
@@ -1618,7 +1621,11 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
     }
   }
   __syncthreads();
-  if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
+  if (tid < cnt * 8) {
+    const long bi = b_off + (long)mods[tid >> 3] * chunk + (tid & 7);
+    if (fx) gacc_q(fx, bi, dbq[tid]);
+    else atomicAdd(&grad[bi], dbias[tid]);
+  }
 }
 
 // ===========================================================================
@@ -1634,7 +1641,8 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
                                                        const int* __restrict__ act_idx,
                                                        const int* __restrict__ act_cnt, int layer, int L, int M, int P,
                                                        int E, int T, long bits_rows, int rows_per_chunk,
-                                                       float in_scale, float g_scale, const float* __restrict__ gamax) {
+                                                       float in_scale, float g_scale, const float* __restrict__ gamax,
+                                                       long long* __restrict__ fx) {
   static_assert(!G::U8 && G::HOWO > X3_WG_RB, "bf16 input; one row wrap per stage");
   constexpr int XS = G::KP + 8;
   constexpr int GS = X3_NCX * 16 + 8;
@@ -1644,7 +1652,8 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
   constexpr int XIT = (X3_WG_RB * G::KC + 511) / 512;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][2][X3_WG_RB * XS];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][2][X3_WG_RB * GS];
-  __shared__ float dbias[X3_NCT * 16];
+  __shared__ unsigned long long dbq[X3_NCT * 16];       // det: int64 fixed point; else the float view
+  float* const dbias = reinterpret_cast<float*>(dbq);
   __shared__ int mods[X3_MAXM];
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
@@ -1652,7 +1661,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
   const int nct = (cnt + 1) >> 1;
   const int tid = threadIdx.x;
   if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
-  if (tid < X3_NCT * 16) dbias[tid] = 0.f;
+  if (tid < X3_NCT * 16) dbq[tid] = 0ull;
   const int Rtot = T * E * G::HOWO;
   const int PE = P * E;
   const int r_begin = blockIdx.x * rows_per_chunk;
@@ -1784,7 +1793,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int k = mt * 16 + 4 * grp + r;
-              if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[mi][nt][r] * (in_scale * g_scale * ginv));
+              if (k < G::K) gacc(grad, fx, base + (long)k * 8 + ch, acc[mi][nt][r] * (in_scale * g_scale * ginv));
             }
           }
         }
@@ -1792,7 +1801,7 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
     }
     if (gact) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) atomicAdd(&dbias[(2 * ct0 + gsl) * 8 + c], bpart[c] * g_scale);
+      for (int c = 0; c < 8; ++c) lds_acc(dbias, dbq, (2 * ct0 + gsl) * 8 + c, bpart[c] * g_scale, fx != nullptr);
     }
   };
   for (int pass = 0; pass < npass; ++pass) {
@@ -1804,7 +1813,11 @@ __global__ __launch_bounds__(512, 2) void conv_wgrad_x3(const bf16_t* __restrict
     }
   }
   __syncthreads();
-  if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
+  if (tid < cnt * 8) {
+    const long bi = b_off + (long)mods[tid >> 3] * chunk + (tid & 7);
+    if (fx) gacc_q(fx, bi, dbq[tid]);
+    else atomicAdd(&grad[bi], dbias[tid]);
+  }
 }
 
 // ===========================================================================
@@ -1843,11 +1856,13 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
                                                                    const int* __restrict__ act_cnt, int layer, int L,
                                                                    int M, int P, int E, int T, long bits_rows,
                                                                    int samples_per_wg, float in_scale, float g_scale,
-                                                                   const float* __restrict__ gamax) {
+                                                                   const float* __restrict__ gamax,
+                                                                   long long* __restrict__ fx) {
   using W = WT3<G>;
   __shared__ __attribute__((aligned(16))) bf16_t Xt[2][2][W::TILEP];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][2][W::NPP * W::GS];
-  __shared__ float dbias[X3_NCT * 16];
+  __shared__ unsigned long long dbq[X3_NCT * 16];       // det: int64 fixed point; else the float view
+  float* const dbias = reinterpret_cast<float*>(dbq);
   __shared__ int mods[X3_MAXM];
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
@@ -1860,7 +1875,7 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
   const int s_end = min(nsamp, s_beg + samples_per_wg);
   if (s_beg >= s_end) return;
   if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
-  if (tid < X3_NCT * 16) dbias[tid] = 0.f;
+  if (tid < X3_NCT * 16) dbq[tid] = 0ull;
   // zero rows 176..191 of both G buffers and the tile pad chunk (never rewritten)
   for (int i = tid; i < 2 * 2 * (W::NPP - W::NPOS) * W::GS; i += W::NT) {
     const int per = (W::NPP - W::NPOS) * W::GS;
@@ -1981,17 +1996,21 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int k = w * 16 + 4 * grp + r;
-          if (k < G::K) atomicAdd(&grad[base + (long)k * 8 + ch], acc[nt][r] * (in_scale * g_scale * ginv));
+          if (k < G::K) gacc(grad, fx, base + (long)k * 8 + ch, acc[nt][r] * (in_scale * g_scale * ginv));
         }
       }
     }
     if (slot_ok) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) atomicAdd(&dbias[(2 * ct0 + a_my) * 8 + c], bpart[c] * g_scale);
+      for (int c = 0; c < 8; ++c) lds_acc(dbias, dbq, (2 * ct0 + a_my) * 8 + c, bpart[c] * g_scale, fx != nullptr);
     }
   }
   __syncthreads();
-  if (tid < cnt * 8) atomicAdd(&grad[b_off + (long)mods[tid >> 3] * chunk + (tid & 7)], dbias[tid]);
+  if (tid < cnt * 8) {
+    const long bi = b_off + (long)mods[tid >> 3] * chunk + (tid & 7);
+    if (fx) gacc_q(fx, bi, dbq[tid]);
+    else atomicAdd(&grad[bi], dbias[tid]);
+  }
 }
 
 // ===========================================================================
@@ -3505,7 +3524,7 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
                                                       const int* __restrict__ inv_slot,
                                                       const int* __restrict__ inv_cnt, int layer, int M, int Pmax,
                                                       int K, int P, int E, int T, long bits_rows, int nsplit,
-                                                      const float* __restrict__ gamax) {
+                                                      const float* __restrict__ gamax, long long* __restrict__ fx) {
   constexpr int XS = 128 + 8;
   constexpr int GS = COUT + 8;
   constexpr int NT = COUT / 32;
@@ -3607,7 +3626,7 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
         const int n = (COUT / 2) * wn + 16 * jj + i16;
         if (k < K) {
           if (nsplit == 1) grad[base + (long)k * COUT + n] = acc[i][jj][r] * ginv;
-          else atomicAdd(&grad[base + (long)k * COUT + n], acc[i][jj][r] * ginv);
+          else gacc(grad, fx, base + (long)k * COUT + n, acc[i][jj][r] * ginv);
         }
       }
   if (do_bias) {
@@ -3619,7 +3638,7 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
       if (grp == 0) {
         const long o = b_off + (long)j * chunk + (COUT / 2) * wn + 16 * jj + i16;
         if (nsplit == 1) grad[o] = v;
-        else atomicAdd(&grad[o], v);
+        else gacc(grad, fx, o, v);
       }
     }
   }
@@ -3635,11 +3654,13 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
                                                    const int* __restrict__ inv_path, const int* __restrict__ inv_slot,
                                                    const int* __restrict__ inv_cnt, int layer, int M, int Pmax, int K,
                                                    int Cout, int P, int E, int T, long bits_rows, float g_scale,
-                                                   int nsplit, const float* __restrict__ gamax) {
+                                                   int nsplit, const float* __restrict__ gamax,
+                                                   long long* __restrict__ fx) {
   constexpr int S = 64 + 8;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][32 * S];
   __shared__ __attribute__((aligned(16))) bf16_t Gs[2][32 * S];
-  __shared__ float dbias[64];
+  __shared__ unsigned long long dbq[64];        // det: int64 fixed point; else the float view
+  float* const dbias = reinterpret_cast<float*>(dbq);
   const int j = blockIdx.z / nsplit, split = blockIdx.z - j * nsplit;
   const int n_all = inv_cnt[layer * M + j];
   const int u_beg = (int)((long)n_all * split / nsplit), u_end = (int)((long)n_all * (split + 1) / nsplit);
@@ -3648,7 +3669,7 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
   const bool do_bias = blockIdx.x == 0;
-  if (tid < 64) dbias[tid] = 0.f;
+  if (tid < 64) dbq[tid] = 0ull;
   const long Rtot = (long)T * E;
   const int PE = P * E;
   const int nwords = Cout / 16;
@@ -3720,16 +3741,23 @@ __global__ __launch_bounds__(256) void fc_wgrad_x3(const bf16_t* __restrict__ X,
         const int n = n0b + (nt0 + jj) * 16 + i16;
         if (k < K && n < Cout) {
           if (nsplit == 1) grad[base + (long)k * Cout + n] = acc[i][jj][r] * ginv;
-          else atomicAdd(&grad[base + (long)k * Cout + n], acc[i][jj][r] * ginv);
+          else gacc(grad, fx, base + (long)k * Cout + n, acc[i][jj][r] * ginv);
         }
       }
   if (do_bias) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) atomicAdd(&dbias[sc + c], bpart[c]);
+    for (int c = 0; c < 8; ++c) lds_acc(dbias, dbq, sc + c, bpart[c], fx != nullptr);
     __syncthreads();
     if (tid < 64 && n0b + tid < Cout) {
-      if (nsplit == 1) grad[b_off + (long)j * chunk + n0b + tid] = dbias[tid];
-      else atomicAdd(&grad[b_off + (long)j * chunk + n0b + tid], dbias[tid]);
+      const long bi = b_off + (long)j * chunk + n0b + tid;
+      if (fx) {
+        if (nsplit == 1) grad[bi] = fx_f(dbq[tid]);
+        else gacc_q(fx, bi, dbq[tid]);
+      } else if (nsplit == 1) {
+        grad[bi] = dbias[tid];
+      } else {
+        atomicAdd(&grad[bi], dbias[tid]);
+      }
     }
   }
 }
@@ -3816,6 +3844,23 @@ __global__ __launch_bounds__(256) void refresh_x3_all_kernel(const float* __rest
   while (i + 1 < rs.n && b >= rs.b0[i + 1]) ++i;
   refresh_x3_tile(flat, rs.w_off[i], rs.chunk[i], rs.K[i], rs.KP[i], rs.Cout[i], rs.M, rs.Wc[i], rs.WcT[i], rs.f16,
                   status, b - rs.b0[i]);
+}
+
+// deterministic mode: grad[i] += fx[i] * 2^-FX_SHIFT and fx[i] = 0 over [n0, n1) (entries no kernel touched stay 0 and
+// are neither read-modified nor written back); fx[-1] (the range guard word) becomes X3_RANGE_FX
+__global__ __launch_bounds__(256) void fx_flush_kernel(long long* __restrict__ fx, float* __restrict__ grad, long n0,
+                                                      long n1) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && fx[-1] != 0) {
+    fx[-1] = 0;
+    atomicOr(&g_x3_range, X3_RANGE_FX);
+  }
+  for (long i = n0 + (long)blockIdx.x * 256 + threadIdx.x; i < n1; i += (long)gridDim.x * 256) {
+    const long long q = fx[i];
+    if (q != 0) {
+      fx[i] = 0;
+      grad[i] += fx_f((unsigned long long)q);
+    }
+  }
 }
 
 // one thread: out[0] = (float)(activation flags since the last fold | weight flags of the last refresh), both reset
@@ -3917,7 +3962,27 @@ static int X3_DG_TARGET = 512;     // 4x4/s2 input gradient (2048 -> 1536 -> 512
 static int X3_FC_KS_PARTS = 0;
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
+// the fixed-point weight-gradient accumulator of the backward being launched (deterministic mode), else nullptr:
+// set by x3_set_fx around one backward's launches (one host thread, as graph capture is), read by the launchers
+long long* g_fx_accum = nullptr;
+
 extern "C" {
+
+// deterministic (bit-reproducible) fp32x backward: fx = an int64 buffer of numel + 1 entries passed as base + 1 (fx[-1]
+// is the range guard word), indexed like the fp32 gradient; nullptr restores the fp32 atomics
+int x3_set_fx(void* fx) {
+  g_fx_accum = reinterpret_cast<long long*>(fx);
+  return 0;
+}
+
+int x3_fx_flush(void* fx, float* grad, long n0, long n1, hipStream_t st) {
+  if (!fx || !grad || n0 < 0 || n1 < n0) return -22;
+  if (n1 == n0) return 0;
+  long blocks = (n1 - n0 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  fx_flush_kernel<<<(unsigned)blocks, 256, 0, st>>>(reinterpret_cast<long long*>(fx), grad, n0, n1);
+  return (int)hipGetLastError();
+}
 
 void fast_conv_set_x3_fwd_nt(int nt) { X3_FWD_NT = nt; }
 void fast_conv_set_x3_c1_wg_ncx(int v) { X3_C1_WG_NCX = v == 2 ? 2 : 3; }
@@ -4136,19 +4201,19 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (X3_C1_WG_NCX == 2 && X3_WGRAD_PF != 1)       // 2 tiles per pass: two stages in flight fit (162 VGPRs)
     conv_wgrad_slab_x3<C1, 2, 2, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum);
   else if (X3_C1_WG_NCX == 2)
     conv_wgrad_slab_x3<C1, 2, 1, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum);
   else if (X3_WGRAD_PF == 2)
     conv_wgrad_slab_x3<C1, 2, 2, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP);
+                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum);
   else
     conv_wgrad_slab_x3<C1, 2, 1, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP);
+                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
@@ -4175,11 +4240,11 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     if (pf == 2)
       conv_wgrad_slab_x3<Gx, OB, 2><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
                                                           ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs, nullptr,
-                                                          0, gamax, X3_SLAB_PMAP);
+                                                          0, gamax, X3_SLAB_PMAP, g_fx_accum);
     else
       conv_wgrad_slab_x3<Gx, OB, 1><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
                                                           ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs, nullptr,
-                                                          0, gamax, X3_SLAB_PMAP);
+                                                          0, gamax, X3_SLAB_PMAP, g_fx_accum);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   };
@@ -4195,7 +4260,7 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     if (spw < 4) spw = 4;
     conv_wgrad_tile_x3<C3><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), WT3<C3>::NT, 0, st>>>(
         (const uint16_t*)X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br,
-        (int)spw, is, gs, gamax);
+        (int)spw, is, gs, gamax, g_fx_accum);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   }
@@ -4207,7 +4272,7 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     if (rpc < X3_WG_RB * 4) rpc = X3_WG_RB * 4;
     conv_wgrad_x3<C3><<<dim3((unsigned)((rows + rpc - 1) / rpc), P), 512, 0, st>>>(
         (const bf16_t*)X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br,
-        (int)rpc, is, gs, gamax);
+        (int)rpc, is, gs, gamax, g_fx_accum);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   }
@@ -4451,7 +4516,7 @@ int x3_fc_wgrad_gm(const void* X, long xlo, int ldx, const void* Gm, long gmlo, 
   const int kt = (K + 127) / 128;
   fc_wgrad_gm_x3<256><<<kt * M * nsplit, 512, 0, st>>>((const bf16_t*)X, xlo, ldx, (const bf16_t*)Gm, gmlo, grad,
                                                        w_off, b_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, Pmax,
-                                                       K, P, E, T, br, nsplit, gamax);
+                                                       K, P, E, T, br, nsplit, gamax, g_fx_accum);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
@@ -4467,7 +4532,7 @@ int x3_fc_wgrad(const void* X, long xlo, int ldx, const float* G, const void* bi
   nsplit = nsplit < 1 ? 1 : (nsplit > Pmax ? Pmax : nsplit);
   fc_wgrad_x3<<<dim3((K + 63) / 64, (Cout + 63) / 64, M * nsplit), 256, 0, st>>>(
       (const bf16_t*)X, xlo, ldx, G, (const uint16_t*)bits, grad, w_off, b_off, chunk, inv_path, inv_slot, inv_cnt,
-      layer, M, Pmax, K, Cout, P, E, T, br, gs, nsplit, gamax);
+      layer, M, Pmax, K, Cout, P, E, T, br, gs, nsplit, gamax, g_fx_accum);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }

@@ -63,3 +63,54 @@ def evaluate_checkpoint(cfg, path: str, episodes: int = 1, max_steps: int = 2000
     rets = evaluate_model(model, env_id, episodes, max_steps, device, frameskip=cfg.frameskip, gray=cfg.gray)
     return {"env": env_id, "task": task, "returns": rets, "best_path": int(np.nanargmax(rets)) if rets else -1,
             "best_return": float(np.nanmax(rets)) if rets else float("nan")}
+
+
+@torch.no_grad()
+def evaluate_path(net_cfg, flat: torch.Tensor, expressed: np.ndarray, env_id: str, task: int = 0,
+                  episodes: int = 64, seed: int = 424242, device="cpu", frameskip: int = 4, gray: str = "rgb",
+                  max_steps: int = 30000, check_every: int = 32) -> dict:
+    """Held-out evaluation of ONE path of a trained super-network: ``episodes`` fresh envs (their own seed, none of
+    the training envs), each playing exactly one episode under the SAMPLED policy (seeded multinomial, so a repeat
+    replays the same episodes) of the path ``expressed`` [L, M] with the weights ``flat`` (copied, never trained).
+    The forward is the fp32 PyTorch oracle (models/pathnet.py trunk_forward_ref): independent of the HIP kernels
+    that produced the training fitness (the env steps in its HIP kernel on a GPU).  The reference's equivalent is its display path (run_policy,
+    game_ac_network.py:458-465); it has no held-out check of a tournament winner.
+
+    Returns {"mean", "min", "max", "finished", "episodes", "steps", "returns"}; an env that finished no episode in
+    ``max_steps`` counts as unfinished (``finished`` < ``episodes``) and is left out of the mean."""
+    model = ACPathNet(net_cfg, 1, device, "torch")
+    model.store.flat.data.copy_(flat.detach().to(model.store.flat.device, torch.float32))
+    model.set_paths(np.asarray(expressed, np.float32)[None])
+    model.task = task
+    gen = torch.Generator(device=device).manual_seed(seed)
+    kw = {} if env_id.startswith("CartPole") else dict(frameskip=frameskip, gray=gray)
+    # on a GPU the env steps in its HIP kernel (bit-exact to the torch game, tests/test_envs.py / test_games_hip.py):
+    # the torch Pong's per-sub-frame ops made a 7 K-step evaluation take 65 s
+    backend = "hip" if torch.device(device).type == "cuda" else "torch"
+    try:
+        env = make(env_id, num_envs=episodes, device=device, seed=seed, backend=backend, **kw)
+    except (NotImplementedError, ValueError, RuntimeError):
+        env = make(env_id, num_envs=episodes, device=device, seed=seed, backend="torch", **kw)
+    obs = env.reset()
+    state = model.init_state(episodes)
+    ret = torch.zeros(episodes, device=device)
+    fin = torch.zeros(episodes, dtype=torch.bool, device=device)
+    steps = 0
+    for steps in range(1, max_steps + 1):
+        logits, _, state = model.forward(obs, episodes, state)
+        a = torch.multinomial(torch.softmax(logits.float(), -1), 1, generator=gen).reshape(-1)
+        obs, _, d, info = env.step(a)
+        d = d.bool()
+        first = d & ~fin
+        ret = torch.where(first, info["episode_return"].float(), ret)
+        fin |= d
+        if state is not None:
+            keep = (~d).float()[:, None]
+            state = (state[0] * keep, state[1] * keep)
+        if steps % check_every == 0 and bool(fin.all()):
+            break
+    r = ret[fin].cpu().numpy().astype(np.float64)
+    return {"mean": float(r.mean()) if r.size else float("nan"), "min": float(r.min()) if r.size else None,
+            "max": float(r.max()) if r.size else None, "finished": int(r.size), "episodes": int(episodes),
+            "steps": int(steps), "policy": "sampled", "seed": int(seed),
+            "returns": [float(x) for x in r]}

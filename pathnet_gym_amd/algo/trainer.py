@@ -58,6 +58,7 @@ class UpdateStats:
     mean_return: float = float("nan")
     tournaments: int = 0
     best_winner: float = float("nan")
+    winner_path: int = -1               # global index of the path that won with best_winner (-1: no tournament)
     steps: int = 0
     skipped: bool = False
     # the update (1-based count) whose optimizer step ``skipped`` refers to: this one when not pipelined; with the
@@ -308,6 +309,7 @@ class PathNetTrainer:
     def update(self) -> UpdateStats:
         lr = anneal_lr(self.cfg.a2c.lr, self.global_step, self.cfg.a2c.max_time_step,
                        self.task_start_step, self.cfg.a2c.lr_anneal)
+        self.last_lr = lr                # the learning rate of the optimizer step this update enqueues
         tr = self.tracer
         if self.pipelined:
             return self._update_pipelined(lr)
@@ -461,7 +463,9 @@ class PathNetTrainer:
             self.pop.genotypes = g
         if events:
             st.tournaments = len(events)
-            st.best_winner = max(e.winner_fitness for e in events)
+            best_ev = max(events, key=lambda e: e.winner_fitness)
+            st.best_winner = best_ev.winner_fitness
+            st.winner_path = int(best_ev.winner)
             thr = reward_threshold(self.cfg.tasks[self.task_idx])
             if self.solved_generation.get(self.task_idx) is None and st.best_winner >= thr:
                 self.solved_generation[self.task_idx] = self.pop.generation - self._task_gen0

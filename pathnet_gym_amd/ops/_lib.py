@@ -161,6 +161,8 @@ _SIGS = {
     "x3_fc_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P, P] + [c_int] * 8 + [c_long, c_float, P, P],
     "x3_refresh_weights": [P, c_long, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
     "x3_status_fold": [P, P, P],
+    "x3_set_fx": [P],
+    "x3_fx_flush": [P, P, c_long, c_long, P],
     "fast_conv_set_x3_fwd_nt": [c_int],
     "fast_conv_set_x3_fwd_lb": [c_int],
     "fast_conv_set_x3_fwd_db": [c_int],

@@ -135,14 +135,21 @@ class HipPathNet:
         # compute_dtype "fp32x": fp32-accurate split-bf16 operands (csrc/trunk_x3.hip): every activation between
         # layers is a (hi, lo) bf16 pair, every MFMA product hi*hi + hi*lo + lo*hi, the last layer's output fp32
         self.x3 = getattr(model, "compute_dtype", "bf16") == "fp32x"
-        if self.x3 and getattr(model, "deterministic", False):
-            raise NotImplementedError("compute_dtype='fp32x' reduces weight gradients with fp32 atomics; use 'fp32' "
-                                      "for bit-reproducible updates")
+        # fp32x, deterministic: every weight-gradient contribution that would meet others in an fp32 atomic is added
+        # as an int64 fixed-point number instead (csrc/common.h gacc: integer addition is associative, so the
+        # arrival order of workgroups and waves no longer matters) and converted back once per backward
+        # (x3_fx_flush); the routing (frame ring, fused LSTM, split heads backward -- already fixed-order) is the
+        # default fp32x one
+        self.fx_det = self.x3 and bool(getattr(model, "deterministic", False))
+        self._fxbuf = None
+        if self.fx_det:
+            n = model.store.layout.numel
+            self._fxbuf = torch.zeros(n + 1, dtype=torch.int64, device=model.device)   # [0]: range guard word
         self.act_dtype = torch.float32 if self.f32 else torch.bfloat16
         # deterministic reductions (TrainConfig.deterministic; implied by fp32): every weight/bias gradient is
         # summed in a fixed order (trunk_f32.hip ordered slabs, heads_reduce_kernel) instead of fp32 atomics,
         # so one seed reproduces the update bit for bit
-        self.deterministic = self.f32 or bool(getattr(model, "deterministic", False))
+        self.deterministic = self.f32 or (bool(getattr(model, "deterministic", False)) and not self.x3)
         self._hpart = None
         self._hsplit = None
         self.L, self.M = cfg.L, cfg.M
@@ -321,6 +328,25 @@ class HipPathNet:
 
     def set_frozen(self, frozen):
         pass   # frozen segments are skipped by the optimizer; kernels compute their grads (cheap)
+
+    @property
+    def reproducible(self) -> bool:
+        """One seed reproduces every update bit for bit (fp32 engine, bf16 ordered reductions, fp32x fixed point)."""
+        return bool(self.deterministic or self.fx_det)
+
+    def fx_begin(self):
+        """Deterministic fp32x: route the weight-gradient launches that follow into the fixed-point accumulator."""
+        if self.fx_det:
+            _lib.call("x3_set_fx", self._fxbuf.data_ptr() + 8)
+
+    def fx_end(self, grad_flat: torch.Tensor, n0: int = 0, n1: Optional[int] = None):
+        """... stop routing, and add the accumulated [n0, n1) into grad_flat (re-zeroing the accumulator)."""
+        if not self.fx_det:
+            return
+        _lib.call("x3_set_fx", None)
+        n1 = grad_flat.numel() if n1 is None else n1
+        _lib.check(grad_flat, torch.float32, numel=self._fxbuf.numel() - 1, name="grad_flat")
+        _lib.call("x3_fx_flush", self._fxbuf.data_ptr() + 8, grad_flat.data_ptr(), n0, n1, _lib.stream())
 
     def fold_x3_status(self, out: torch.Tensor):
         """fp32x: out[0] <- the fp16-pair range flags of the last rollout / weight refresh (csrc/trunk_x3.hip

@@ -127,6 +127,8 @@ class HipEngine:
         self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.zeros(2, dtype=torch.float32, device=dev)      # {lr, skip}
         self.weight = ((1.0 / E) if a2c.env_reduction == "mean_env" else 1.0) * loss_scale(cfg)
+        # end of the first layer's parameters (the overlapped exchange's second bucket, runtime/engine.py split)
+        self._l0_end = max((s.offset + s.numel for s in model.store.layout.segments if s.layer == 0), default=0)
         # optimizer block table (segments split into <= 8192-element blocks)
         self._build_opt_tables()
         self.g_rollout = None
@@ -482,7 +484,9 @@ class HipEngine:
         self.stats[0], self.stats[1], self.stats[2] = lp, lv, ent * T * B
         self.grads[-1].copy_(torch.cat([f.grad for f in feats]))
         self.grad_flat.zero_()
+        self.hip.fx_begin()
         self._layer_bwd_all(T)
+        self.hip.fx_end(self.grad_flat)
         tn = st.layout.trunk_numel
         self.grad_flat[tn:] += st.flat.grad[tn:]
         st.flat.grad = None
@@ -494,8 +498,11 @@ class HipEngine:
     def _rollout_backward_body(self, part: Optional[str] = None):
         """part None: the whole rollout + backward; "head": all of it except the first layer's backward; "tail":
         the first layer's backward only (the overlapped all-reduce runs between them, parallel/comm.py)."""
+        hp = self.hip
         if part == "tail":
+            hp.fx_begin()
             self._layer_bwd_all(self.T, 0, 1)
+            hp.fx_end(self.grad_flat, 0, self._l0_end)
             return
         if self.hybrid:
             return self._rollout_backward_hybrid()
@@ -523,6 +530,7 @@ class HipEngine:
                   self.dlogits.data_ptr(), self.dvalue.data_ptr(), self.stats.data_ptr(), _lib.stream())
         self.grad_flat.zero_()
         L = len(hp.geoms)
+        hp.fx_begin()            # deterministic fp32x: weight gradients in fixed point, added to grad_flat below
         if self.lstm_hip:
             self._lstm_backward()
         else:
@@ -530,6 +538,7 @@ class HipEngine:
             hp.heads_bwd(feat, self.dlogits.reshape(T * B, -1), self.dvalue.reshape(-1), self.grad_flat,
                          self.grads[L - 1], task=self.model.task)
         self._layer_bwd_all(T, 1 if part == "head" else 0)
+        hp.fx_end(self.grad_flat, self._l0_end if part == "head" else 0)
 
     def _rollout_split(self):
         """The rollout as independent per-path-group chains (forward -> sample -> env step, T times, then the

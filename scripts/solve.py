@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Generations-to-solve: the second half of the BASELINE.json headline metric.
 
-"Solved" (the reference defines no criterion) = the
-first GA tournament whose winner fitness (= return of that path's most
-recently finished episode, a3c_training_thread.py:145-147) reaches the env's
-gym ``reward_threshold`` (Pong 18, CartPole-v1 475; the registry spirit of
-gym_doom/__init__.py:21-90).  Reported as tournaments ("generations"), agent
-frames and wall seconds until solve, plus a learning curve in JSONL.
+"Solved" (the reference defines no criterion; algo/solve.py): the first GA tournament whose
+winner fitness reaches the env's ``reward_threshold`` (Pong 18, CartPole-v1 475; the registry spirit of
+gym_doom/__init__.py:21-90) AND whose winning path, evaluated held-out on --confirm-episodes fresh episodes with the
+same weights, reaches --confirm.  Training stops at the task horizon, where the lr anneal reaches 0 (the reference's
+task end, doom_pathnet.py:197,230): a run still unconfirmed there is "unsolved at horizon".  Reported as tournaments
+("generations"), updates, agent frames and wall seconds until solve, every held-out check, and a learning curve in
+JSONL.
 
     python scripts/solve.py --preset pong --minutes 15 [--paths 64 --envs 32]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/solve.py ...
@@ -70,6 +71,9 @@ def main():
     ap.add_argument("--ring", action="store_true", help="first layer on the frame ring (the fp32x bench default)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp32x"], help="HIP engine compute dtype")
     ap.add_argument("--deterministic", action="store_true", help="fixed-order gradient reductions")
+    ap.add_argument("--confirm", type=float, default=17.0,
+                    help="held-out mean return that confirms a solve candidate (algo/solve.py)")
+    ap.add_argument("--confirm-episodes", type=int, default=64, help="fresh episodes of the held-out confirmation")
     args = ap.parse_args()
 
     import torch
@@ -123,9 +127,10 @@ def main():
     if args.paths_total:
         cfg.paths_total = args.paths_total
     cfg.ga.concurrent_tournaments = args.concurrent or max(1, (cfg.paths_total or cfg.paths) // 16)
+    build_info = None
     if cfg.backend in ("hip", "auto") and ctx.device.type == "cuda":
         from pathnet_gym_amd import _build
-        _build.build()
+        build_info = _build.build_info(_build.build())
     tr = PathNetTrainer(cfg, device=ctx.device, ctx=ctx)
     if args.no_ga:
         tr.pop.step = lambda *a, **k: []
@@ -156,12 +161,23 @@ def main():
         os.makedirs(os.path.dirname(args.curve) or ".", exist_ok=True)
         curve = open(args.curve, "a" if args.resume else "w")
 
+    from pathnet_gym_amd.algo.solve import SolveTracker
     t0 = time.time()
     last = t0
     last_ckpt = t0
     u0 = tr.updates
-    best = prior.get("best") if prior.get("best") is not None else -math.inf
-    solved = None
+
+    def log_candidate(c):
+        if ctx.is_main:
+            print(json.dumps({"candidate": c}), flush=True)
+            if curve:
+                curve.write(json.dumps({"candidate": c}) + "\n")
+                curve.flush()
+
+    trk = SolveTracker(tr, confirm_threshold=args.confirm, confirm_episodes=args.confirm_episodes,
+                       wall_s=args.minutes * 60 - prior["seconds"], log=log_candidate)
+    if prior.get("best") is not None:
+        trk.best = prior["best"]
     ret_ema = prior.get("ema")
     while True:
         st = tr.update()
@@ -178,27 +194,24 @@ def main():
             print(json.dumps(rec), flush=True)
         elif not math.isnan(st.mean_return):
             ret_ema = st.mean_return if ret_ema is None else 0.9 * ret_ema + 0.1 * st.mean_return
-        if st.tournaments:
-            best = max(best, st.best_winner)
-            if solved is None and st.best_winner >= thr:
-                solved = dict(generations=tr.pop.generation, frames=tr.global_step, updates=tr.updates,
-                              seconds=round(prior["seconds"] + time.time() - t0, 2), winner_fitness=st.best_winner)
+        stop = trk.observe(st)       # a confirmed solve, the task horizon or the wall limit (same on every rank)
+        if stop and trk.stopped == "solved" and args.keep_going:
+            stop = trk.frames_in_task() >= trk.horizon
         now = time.time()
-        if now - last >= args.report_every or (solved and not args.keep_going):
+        if now - last >= args.report_every or stop:
             last = now
             rec = dict(t=round(prior["seconds"] + now - t0, 1), frames=tr.global_step, updates=tr.updates,
-                       generation=tr.pop.generation, mean_return=ret_ema, best_winner=best,
-                       entropy=st.entropy, frames_per_sec=round(tr.global_step / (now - t0), 1))
+                       generation=tr.pop.generation, mean_return=ret_ema,
+                       best_winner=trk.best if math.isfinite(trk.best) else None,
+                       lr=trk.lr_now(tr.global_step), entropy=st.entropy,
+                       frames_per_sec=round((tr.global_step - trk.tr.task_start_step) / max(now - t0, 1e-9), 1))
             if ctx.is_main:
                 print(json.dumps(rec), flush=True)
                 if curve:
                     curve.write(json.dumps(rec) + "\n")
                     curve.flush()
-        if solved and not args.keep_going:
-            break                                # replicated GA state: every rank breaks at the same update
-        # the wall limit is decided on the max over ranks at a fixed update cadence, so all ranks stop together
-        if tr.updates % 32 == 0 and ctx.max_scalar(now - t0) > args.minutes * 60:
-            break
+        if stop:
+            break                                # replicated decisions: every rank breaks at the same update
         if args.checkpoint and args.ckpt_minutes > 0 and tr.updates % 32 == 0 and \
                 ctx.max_scalar(now - last_ckpt) > args.ckpt_minutes * 60:
             from pathnet_gym_amd.utils import checkpoint as ckpt
@@ -213,25 +226,31 @@ def main():
         ckpt.save(tr, args.checkpoint, light=True)
     el = prior["seconds"] + time.time() - t0
     if ctx.is_main:
-        out = {"metric": "generations_to_solve", "env": cfg.tasks[0], "threshold": thr,
-               "solved": solved is not None, "generations_to_solve": solved and solved["generations"],
-               "frames_to_solve": solved and solved["frames"], "seconds_to_solve": solved and solved["seconds"],
-               "best_winner_fitness": best, "final_mean_return": ret_ema, "generations": tr.pop.generation,
-               "frames": tr.global_step, "updates": tr.updates, "updates_to_solve": solved and solved["updates"],
-               "seconds": round(el, 1), "n_gpus": ctx.world,
-               "segments": prior["segments"] + [{"updates": tr.updates - u0, "seconds": round(time.time() - t0, 1)}],
-               "config": {"preset": args.preset, "paths_per_gpu": cfg.paths, "envs_per_path": cfg.envs_per_path,
-                          "t_max": cfg.a2c.t_max, "lr": cfg.a2c.lr, "B": cfg.ga.B,
-                          "concurrent_tournaments": cfg.ga.concurrent_tournaments, "backend": tr.backend,
-                          "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
-                          "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
-                          "rmsp_epsilon": cfg.a2c.rmsp_epsilon, "grad_scale": cfg.a2c.grad_scale,
-                          "rank_reduction": cfg.a2c.rank_reduction, "frame_ring": bool(getattr(tr.engine, "ring", False)),
-                          "N": cfg.net.N, "fitness": cfg.ga.fitness, "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
-                          "ga": not args.no_ga, "same_path": args.same_path, "dtype": tr.compute_dtype}}
+        r = trk.record()
+        out = {"metric": "generations_to_solve", "env": cfg.tasks[0], "finished_at": round(time.time(), 1)}
+        out.update(r)
+        out.update({"final_mean_return": ret_ema, "generations": tr.pop.generation,
+                    "frames": tr.global_step, "updates": tr.updates,
+                    "seconds": round(el, 1), "n_gpus": ctx.world,
+                    "segments": prior["segments"] + [{"updates": tr.updates - u0, "seconds": round(time.time() - t0, 1)}],
+                    "config": {"preset": args.preset, "paths_per_gpu": cfg.paths, "envs_per_path": cfg.envs_per_path,
+                               "t_max": cfg.a2c.t_max, "lr": cfg.a2c.lr, "B": cfg.ga.B,
+                               "concurrent_tournaments": cfg.ga.concurrent_tournaments, "backend": tr.backend,
+                               "env_reduction": cfg.a2c.env_reduction, "entropy_beta": cfg.a2c.entropy_beta,
+                               "trunk_scale": cfg.net.trunk_scale, "gae_lambda": cfg.a2c.gae_lambda,
+                               "rmsp_epsilon": cfg.a2c.rmsp_epsilon, "grad_scale": cfg.a2c.grad_scale,
+                               "rank_reduction": cfg.a2c.rank_reduction,
+                               "frame_ring": bool(getattr(tr.engine, "ring", False)),
+                               "N": cfg.net.N, "fitness": cfg.ga.fitness,
+                               "fitness_window": cfg.ga.window_for(cfg.envs_per_path),
+                               "ga": not args.no_ga, "same_path": args.same_path, "dtype": tr.compute_dtype,
+                               "deterministic": bool(cfg.deterministic), "lr_anneal": cfg.a2c.lr_anneal,
+                               "max_time_step": cfg.a2c.max_time_step}})
         out["config"]["seed"] = cfg.seed
         if cfg.paths_total:
             out["config"]["paths_total"] = cfg.paths_total
+        if build_info is not None:
+            out["build"] = build_info
         print(json.dumps(out), flush=True)
         if args.out:
             os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)

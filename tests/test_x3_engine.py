@@ -858,3 +858,67 @@ def test_x3_env_step_with_folded_heads_bit_equal(hip_lib, monkeypatch, graph):
     for u, (a, b) in enumerate(zip(*runs)):
         for k, (x, y) in enumerate(zip(a, b)):
             assert torch.equal(x, y), (u, names[k])
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# deterministic fp32x (TrainConfig.deterministic): int64 fixed-point weight-gradient accumulation (csrc/common.h gacc)
+# ---------------------------------------------------------------------------------------------------------------
+def _det_rollout(ring: bool, deterministic: bool):
+    from pathnet_gym_amd.algo.trainer import PathNetTrainer
+    cfg = preset("pong")
+    cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 3, 16, 4
+    cfg.use_graph = False
+    cfg.compute_dtype = "fp32x"
+    cfg.frame_ring = ring
+    cfg.deterministic = deterministic
+    tr = PathNetTrainer(cfg, device=DEV)
+    eng = tr.engine
+    assert eng.ring == ring and tr.model.hip.fx_det == deterministic
+    tr.env.max_episode_steps = 5
+    tr.update()
+    tr.model.set_paths(masks_with_edges(3, cfg.net.L, cfg.net.M, cfg.net.N, seed=2))
+    eng._rollout_backward_body()
+    torch.cuda.synchronize()
+    return tr, eng
+
+
+@pytest.mark.parametrize("ring", [False, True])
+def test_x3_deterministic_gradient_vs_float64_truth(hip_lib, ring):
+    """The fixed-point accumulation keeps the fp32x budget against the float64 autograd truth on every layer (packed
+    stacks: conv1 / conv2 slab, conv3 tile and fc weight gradients; frame ring: the conv1 ring weight gradient), and
+    matches the fp32-atomic mode to fp32 rounding; the accumulator is left zeroed and the range word clear."""
+    tr, eng = _det_rollout(ring, True)
+    g_det = eng.grad_flat.clone()
+    check_layers(f"fp32x deterministic ({'ring' if ring else 'packed'})", tr, g_det, *_oracles(_oracle_grad, tr, eng))
+    assert int(tr.model.hip._fxbuf.abs().sum()) == 0
+    tr.model.hip.check_x3_status()
+    eng._rollout_backward_body()                   # the same stored rollout again: bit-identical
+    torch.cuda.synchronize()
+    assert torch.equal(eng.grad_flat, g_det)
+
+
+def test_x3_deterministic_200_updates_bit_identical(hip_lib):
+    """Two runs of one seed on the shipped path (frame ring, hipGraphs, device GA, pipelined) give bit-identical
+    weights, optimizer slots and genotypes after 200 updates (the fp32-atomic default differs between runs)."""
+    def run():
+        from pathnet_gym_amd.algo.trainer import PathNetTrainer
+        cfg = preset("pong")
+        cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = 8, 16, 5
+        cfg.compute_dtype = "fp32x"
+        cfg.frame_ring = True
+        cfg.use_graph = True
+        cfg.ga.backend = "device"
+        cfg.ga.concurrent_tournaments = 2
+        cfg.deterministic = True
+        tr = PathNetTrainer(cfg, device=DEV)
+        assert tr.engine.ring and tr.engine.use_graph and tr.pipelined and tr.model.hip.reproducible
+        tr.env.max_episode_steps = 7                    # episodes end, fitness windows fill, tournaments fire
+        for _ in range(200):
+            tr.update()
+        tr.flush()
+        torch.cuda.synchronize()
+        return (tr.model.store.flat.detach().clone(), tr.opt.ms.clone(), tr.engine.ga_dev["geno"].clone(),
+                tr.pop.generation)
+    a, b = run(), run()
+    assert a[3] > 0, "no tournament fired"
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]) and a[3] == b[3]
