@@ -199,7 +199,8 @@ def gpu_telemetry() -> dict:
     return out
 
 
-def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: bool = False, info=None):
+def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: bool = False, info=None,
+                  mark_window: int = 0):
     """W untimed updates, then ``windows`` back-to-back windows of EXACTLY K updates, each between barrier +
     synchronize on both sides; a window's time is the max over ranks.  Returns [(seconds, frames, generations)].
     ``info`` (a list): per window, the GPU telemetry sampled while its last updates still run (before the drain) and
@@ -221,15 +222,16 @@ def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: b
         sync()
         gen0 = tr.pop.generation
         step0 = tr.global_step
-        if markers and w == 0:
+        if markers and w == mark_window:
             from pathnet_gym_amd.ops import _lib as _plib
             _plib.call("launch_prof_marker", 1, _plib.stream())
+        host0 = dict(tr.tracer.totals_ms)
         t0 = time.perf_counter()
         for _ in range(steps):
             tr.update()
         tel = gpu_telemetry() if info is not None else None
         tr.flush()                               # drain the pipelined host bookkeeping of the last update
-        if markers and w == 0:
+        if markers and w == mark_window:
             _plib.call("launch_prof_marker", 2, _plib.stream())
         sync()
         dt = ctx.max_scalar(time.perf_counter() - t0)
@@ -238,6 +240,10 @@ def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: b
             ex = tr.pop.expressed()
             tel["active_modules_per_layer"] = [round(float(x), 3) for x in ex.sum(axis=2).mean(axis=0)]
             tel["ms"] = round(dt / steps * 1e3, 3)
+            # host milliseconds per update in each phase of the pipelined loop (utils/tracing.py): "collect" is the
+            # wait for the previous update's read-back, i.e. GPU-bound time; the rest is host work
+            tel["host_ms_per_update"] = {k: round((v - host0.get(k, 0.0)) / steps, 3)
+                                         for k, v in tr.tracer.totals_ms.items() if v - host0.get(k, 0.0) > 0}
             info.append(tel)
     return out
 
@@ -358,7 +364,7 @@ def per_rank_shapes(args, ctx, numel: int, upd: list, headline_ms: float) -> dic
     import torch
     out = {}
     med = upd[len(upd) // 2] if upd else None
-    for n in [int(x) for x in str(args.per_rank_shapes).split(",") if x.strip()]:
+    for n in [int(x) for x in str(args.per_rank_shapes).strip("'\"").split(",") if x.strip()]:
         if n <= 1 or args.paths_total % n:
             continue
         a = argparse.Namespace(**vars(args))
@@ -452,6 +458,7 @@ def main():
     ap.add_argument("--prof-window", action="store_true",
                     help="launch marker kernels around the first timed window (scripts/prof_window.py summarises the "
                          "rocprofv3 kernel trace between them)")
+    ap.add_argument("--prof-window-index", type=int, default=0, help="--prof-window: which timed window to mark")
     ap.add_argument("--per-rank-shapes", default="2,4,8",
                     help="one GPU: also time the strong-scaling per-rank shapes paths_total/N for these N ('' = off)")
     ap.add_argument("--no-verify-build", action="store_true",
@@ -501,7 +508,8 @@ def main():
         verified = finish_build_verify(verify_h)
         verify_h = None
     tele = []
-    wins = timed_windows(tr, ctx, args.steps, args.warmup, args.windows, markers=args.prof_window, info=tele)
+    wins = timed_windows(tr, ctx, args.steps, args.warmup, args.windows, markers=args.prof_window, info=tele,
+                         mark_window=min(args.prof_window_index, args.windows - 1))
     ws = window_summary(wins, args.steps)
     dt = ws["ms"] * args.steps / 1e3
     value = ws["frames"] / dt

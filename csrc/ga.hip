@@ -222,8 +222,22 @@ __global__ __launch_bounds__(256) void opt_tail_kernel(const float* __restrict__
                                                        int p_off, int P, int fit_window, float* __restrict__ fitness,
                                                        float* __restrict__ fit_cnt, float* __restrict__ fit_sum,
                                                        const uint8_t* __restrict__ fc_src, uint8_t* __restrict__ fc_dst,
-                                                       int n_fc, long long* __restrict__ ctr) {
+                                                       int n_fc, long long* __restrict__ ctr,
+                                                       double* __restrict__ lr_sched, float* __restrict__ lr_next) {
   const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+  // the NEXT update's learning rate, on device (no host fill per update): lr_sched = {lr0, max_t, mode, frames per
+  // update, frames done}; frames done += frames per update; lr = lr0 (mode 0, "none") or max(lr0 * (max_t - t) / max_t,
+  // 0) with t = frames done (algo/optim.py anneal_lr: the same double operations, rounded to fp32 once)
+  if (i == 0 && lr_sched) {
+    const double t = lr_sched[4] + lr_sched[3];
+    lr_sched[4] = t;
+    double lr = lr_sched[0];
+    if (lr_sched[2] != 0.0) {
+      lr = lr_sched[0] * (lr_sched[1] - t) / lr_sched[1];
+      lr = lr > 0.0 ? lr : 0.0;
+    }
+    lr_next[0] = (float)lr;
+  }
   if (i < P) {
     fitness[i] = fit[p_off + i];
     if (fit_window > 0 && reset[p_off + i]) {
@@ -238,14 +252,15 @@ __global__ __launch_bounds__(256) void opt_tail_kernel(const float* __restrict__
 extern "C" {
 int launch_opt_tail(const float* fit, const void* reset, int p_off, int P, int fit_window, float* fitness,
                     float* fit_cnt, float* fit_sum, const void* fc_src, void* fc_dst, int n_fc, long long* ctr,
-                    hipStream_t stream) {
+                    double* lr_sched, float* lr_next, hipStream_t stream) {
+  if ((lr_sched != nullptr) != (lr_next != nullptr)) return -22;
   if (P < 0 || p_off < 0 || n_fc < 0 || (P > 0 && (!fit || !reset || !fitness || !fit_cnt || !fit_sum)) ||
       (n_fc > 0 && (!fc_src || !fc_dst))) return -22;
   const int n = P > n_fc ? P : n_fc;
   opt_tail_kernel<<<(n > 0 ? n + 255 : 256) / 256, 256, 0, stream>>>(fit, (const uint8_t*)reset, p_off, P, fit_window,
                                                                     fitness, fit_cnt, fit_sum,
                                                                     (const uint8_t*)fc_src, (uint8_t*)fc_dst, n_fc,
-                                                                    ctr);
+                                                                    ctr, lr_sched, lr_next);
   return (int)hipGetLastError();
 }
 

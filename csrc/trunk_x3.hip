@@ -592,7 +592,8 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
                                                            const int* __restrict__ act_cnt, int layer, int L, int M,
                                                            int P, int E, int T, int t0, long bits_rows,
                                                            int bands_per_wg, float in_scale, float out_scale,
-                                                           const uint8_t* __restrict__ fcv = nullptr, int nslots = 0) {
+                                                           const uint8_t* __restrict__ fcv = nullptr, int nslots = 0,
+                                                           int rbase = 0) {
   using B = BD1<G>;
   constexpr int KPs = G::KP + 8;
   constexpr int NK = G::KP / 32;
@@ -645,16 +646,19 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
     const int s = u / B::NB, oh0 = (u - s * B::NB) * B::OBR;
     const int st = s / E, e = s - st * E;
     const int fc = (int)fcs[s - s_first];
-    const long slot0 = (long)(p * E + e) * nslots + t0 + st;
     const int c = min(tid + 256 * j, B::NCH - 1);
     const int r = c / (G::WIN / 4), cc = c - r * (G::WIN / 4);
     const int ir = min(oh0 * G::S + r, G::HIN - 1);
     constexpr long HW = (long)G::HIN * G::WIN;
-    const uint8_t* src = X + slot0 * HW + (long)ir * G::WIN + cc * 4;
-    return make_uint4(*reinterpret_cast<const uint32_t*>(src + max(0, fc) * HW),
-                      *reinterpret_cast<const uint32_t*>(src + max(1, fc) * HW),
-                      *reinterpret_cast<const uint32_t*>(src + max(2, fc) * HW),
-                      *reinterpret_cast<const uint32_t*>(src + max(3, fc) * HW));
+    // modular ring: channel k of step t lives in slot (rbase + t + max(k, fc)) mod nslots (runtime/engine.py)
+    const uint8_t* src = X + (long)(p * E + e) * nslots * HW + (long)ir * G::WIN + cc * 4;
+    const int s0 = rbase + t0 + st;
+    auto pl = [&](int k) {
+      int sl = s0 + max(k, fc);
+      sl -= sl >= nslots ? nslots : 0;
+      return *reinterpret_cast<const uint32_t*>(src + sl * HW);
+    };
+    return make_uint4(pl(0), pl(1), pl(2), pl(3));
   };
   auto load_band = [&](int u) {
     if constexpr (RING) {
@@ -1291,7 +1295,7 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
                                                             float in_scale, float g_scale,
                                                             const uint8_t* __restrict__ fcv, int nslots,
                                                             const float* __restrict__ gamax, int pmap,
-                                                            long long* __restrict__ fx) {
+                                                            long long* __restrict__ fx, int rbase) {
   using SB = Slab<G, OB>;
   static_assert(!RING || (G::U8 && G::CIN == 4 && G::WIN % 4 == 0), "ring input: uint8 4-channel first layer");
   // ring: 4-pixel groups per slab (one 16-byte LDS store each; 8-pixel groups, one round of loads but four stores
@@ -1396,18 +1400,26 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
       if constexpr (RING) {
         constexpr long HW = (long)G::HIN * G::WIN;
         const int fc = (int)fcs[ut * E + ue - s_first];
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(X) + ((long)(p * E + ue) * nslots + ut) * HW +
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(X) + (long)(p * E + ue) * nslots * HW +
                              (long)ih0 * G::WIN;
+        const int s0 = rbase + ut;               // modular ring (conv1_fwd_band_x2 ring_src)
         const int npx = min(SB::SR, G::HIN - ih0) * G::WIN;
         Rg.navail = npx;
+        long po[4];                               // the 4 channel planes' slot offsets
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          int sl = s0 + max(k, fc);
+          sl -= sl >= nslots ? nslots : 0;
+          po[k] = (long)sl * HW;
+        }
 #pragma unroll
         for (int j = 0; j < XIT4; ++j) {
           const int gi = tid + 256 * j;
           const int e0 = (gi < NG4 && gi * 4 < npx) ? gi * 4 : 0;        // clamped, zeroed at write time
-          Rg.xq[j] = make_uint4(*reinterpret_cast<const uint32_t*>(src + max(0, fc) * HW + e0),
-                                *reinterpret_cast<const uint32_t*>(src + max(1, fc) * HW + e0),
-                                *reinterpret_cast<const uint32_t*>(src + max(2, fc) * HW + e0),
-                                *reinterpret_cast<const uint32_t*>(src + max(3, fc) * HW + e0));
+          Rg.xq[j] = make_uint4(*reinterpret_cast<const uint32_t*>(src + po[0] + e0),
+                                *reinterpret_cast<const uint32_t*>(src + po[1] + e0),
+                                *reinterpret_cast<const uint32_t*>(src + po[2] + e0),
+                                *reinterpret_cast<const uint32_t*>(src + po[3] + e0));
         }
       }
       const long xbase = sg * (long)G::IN_ELEMS + (long)ih0 * SB::RL;
@@ -3516,7 +3528,7 @@ __global__ __launch_bounds__(512) void fc_dgrad_gemm_x3(const bf16_t* __restrict
 // fc weight gradient from the masked hi/lo gradient Gm written by fc_dgrad_x3 (trunk_bwd.hip fc_wgrad_gm_kernel):
 // 128 x COUT tiles, module-major users, 32-row stages of X (hi/lo) and Gm (hi/lo) double-buffered in LDS.
 // ===========================================================================
-template <int COUT>
+template <int COUT, int KT = 128>
 __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__ X, long xlo, int ldx,
                                                       const bf16_t* __restrict__ Gm, long gmlo,
                                                       float* __restrict__ grad, long w_off, long b_off, int chunk,
@@ -3525,18 +3537,20 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
                                                       const int* __restrict__ inv_cnt, int layer, int M, int Pmax,
                                                       int K, int P, int E, int T, long bits_rows, int nsplit,
                                                       const float* __restrict__ gamax, long long* __restrict__ fx) {
-  constexpr int XS = 128 + 8;
+  constexpr int XS = KT + 8;
+  constexpr int MI = KT / 64;              // 16-row m tiles of k per wave (each wave owns KT / 4 k values)
+  constexpr int XC = KT / 128;             // 8-element X chunks per thread and plane
   constexpr int GS = COUT + 8;
   constexpr int NT = COUT / 32;
   __shared__ __attribute__((aligned(16))) bf16_t Xs[2][2][32 * XS];
   __shared__ __attribute__((aligned(16))) bf16_t Gsh[2][2][32 * GS];
-  const int kt = (K + 127) / 128;
+  const int kt = (K + KT - 1) / KT;
   const int zt = blockIdx.x / kt, tile_k = blockIdx.x - zt * kt;
   const int j = zt / nsplit, split = zt - j * nsplit;
   const int n_all = inv_cnt[layer * M + j];
   const int u_beg = (int)((long)n_all * split / nsplit), u_end = (int)((long)n_all * (split + 1) / nsplit);
   if (u_beg >= u_end) return;
-  const int k0 = tile_k * 128;
+  const int k0 = tile_k * KT;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
   const int wk = w >> 1, wn = w & 1;
@@ -3547,21 +3561,24 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
   const int* is = inv_slot + (layer * M + j) * Pmax;
   constexpr int GSEG = COUT / 16;
   const int lr = tid >> 4, lxs = (tid & 15) * 8, lgs = (tid & 15) * GSEG;
-  const bool xin = k0 + lxs < K;
-  s8v xrh, xrl, grh[GSEG / 8], grl[GSEG / 8];
+  s8v xrh[XC], xrl[XC], grh[GSEG / 8], grl[GSEG / 8];
   auto gload = [&](int it) {
     const int ui = it / nrb;
     const int r = (it - ui * nrb) * 32 + lr;
     const int p = ip[u_beg + ui], a = is[u_beg + ui];
-    xrh = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
-    xrl = xrh;
+    const s8v z = (s8v){0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int h = 0; h < GSEG / 8; ++h) { grh[h] = xrh; grl[h] = xrh; }
+    for (int c = 0; c < XC; ++c) { xrh[c] = z; xrl[c] = z; }
+#pragma unroll
+    for (int h = 0; h < GSEG / 8; ++h) { grh[h] = z; grl[h] = z; }
     if (r < Rtot) {
       const long sg = sample_global(p, r, E, PE, 0);
-      if (xin) {
-        xrh = *reinterpret_cast<const s8v*>(X + sg * ldx + k0 + lxs);
-        xrl = *reinterpret_cast<const s8v*>(X + xlo + sg * ldx + k0 + lxs);
+#pragma unroll
+      for (int c = 0; c < XC; ++c) {
+        if (k0 + lxs + 128 * c < K) {
+          xrh[c] = *reinterpret_cast<const s8v*>(X + sg * ldx + k0 + lxs + 128 * c);
+          xrl[c] = *reinterpret_cast<const s8v*>(X + xlo + sg * ldx + k0 + lxs + 128 * c);
+        }
       }
       const bf16_t* gp = Gm + ((long)a * bits_rows + sg) * COUT + lgs;
 #pragma unroll
@@ -3571,9 +3588,9 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
       }
     }
   };
-  f4v acc[2][NT];
+  f4v acc[MI][NT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int jj = 0; jj < NT; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
   float bsum[NT];
@@ -3583,8 +3600,11 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
   gload(0);
   for (int it = 0; it < n_it; ++it) {
     const int buf = it & 1;
-    *reinterpret_cast<s8v*>(Xs[buf][0] + lr * XS + lxs) = xrh;     // the activation's fp16 pair as is (G16)
-    *reinterpret_cast<s8v*>(Xs[buf][1] + lr * XS + lxs) = xrl;
+#pragma unroll
+    for (int c = 0; c < XC; ++c) {                                  // the activation's fp16 pair as is (G16)
+      *reinterpret_cast<s8v*>(Xs[buf][0] + lr * XS + lxs + 128 * c) = xrh[c];
+      *reinterpret_cast<s8v*>(Xs[buf][1] + lr * XS + lxs + 128 * c) = xrl[c];
+    }
 #pragma unroll
     for (int h = 0; h < GSEG / 8; ++h) {
       *reinterpret_cast<s8v*>(Gsh[buf][0] + lr * GS + lgs + 8 * h) = grh[h];
@@ -3592,11 +3612,11 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
     }
     __syncthreads();
     if (it + 1 < n_it) gload(it + 1);
-    s8v afh[2], afl[2];
+    s8v afh[MI], afl[MI];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int o0 = (8 * grp + q) * XS + 32 * wk + 16 * i + 4 * pp;
-      const int o1 = (8 * grp + 4 + q) * XS + 32 * wk + 16 * i + 4 * pp;
+    for (int i = 0; i < MI; ++i) {
+      const int o0 = (8 * grp + q) * XS + (KT / 4) * wk + 16 * i + 4 * pp;
+      const int o1 = (8 * grp + 4 + q) * XS + (KT / 4) * wk + 16 * i + 4 * pp;
       afh[i] = tr8(Xs[buf][0] + o0, Xs[buf][0] + o1);
       afl[i] = tr8(Xs[buf][1] + o0, Xs[buf][1] + o1);
     }
@@ -3606,8 +3626,8 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
       const int o0 = (8 * grp + q) * GS + nb + 4 * pp, o1 = (8 * grp + 4 + q) * GS + nb + 4 * pp;
       const s8v bh = tr8(Gsh[buf][0] + o0, Gsh[buf][0] + o1);
       const s8v bl = tr8(Gsh[buf][1] + o0, Gsh[buf][1] + o1);
-      acc[0][jj] = mma3h(afh[0], afl[0], bh, bl, acc[0][jj]);
-      acc[1][jj] = mma3h(afh[1], afl[1], bh, bl, acc[1][jj]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[i][jj] = mma3h(afh[i], afl[i], bh, bl, acc[i][jj]);
       if (do_bias) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) bsum[jj] += h2f((uint16_t)bh[e]) + h2f((uint16_t)bl[e]);
@@ -3617,12 +3637,12 @@ __global__ __launch_bounds__(512) void fc_wgrad_gm_x3(const bf16_t* __restrict__
   const long base = w_off + (long)j * chunk;
   const float ginv = 1.0f / g16_scale(gamax);          // Gm holds the gradient * 2^e
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int jj = 0; jj < NT; ++jj)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int k = k0 + 32 * wk + 16 * i + 4 * grp + r;
+        const int k = k0 + (KT / 4) * wk + 16 * i + 4 * grp + r;
         const int n = (COUT / 2) * wn + 16 * jj + i16;
         if (k < K) {
           if (nsplit == 1) grad[base + (long)k * COUT + n] = acc[i][jj][r] * ginv;
@@ -3960,6 +3980,7 @@ static int X3_DG_TARGET = 512;     // 4x4/s2 input gradient (2048 -> 1536 -> 512
 // module-major fc forward k split: 0 = auto by rows (P*T*E <= 768: 4 parts, else 3), else the fixed part count (2 / 3 / 4 /
 // 8), capped so every part keeps >= 2 k-steps
 static int X3_FC_KS_PARTS = 0;
+static int X3_FCW_KT = 256;     // fc weight gradient from Gm: k tile 256 (Gm re-read 6x at K = 1408) or 128 (11x)
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
 
 // the fixed-point weight-gradient accumulator of the backward being launched (deterministic mode), else nullptr:
@@ -3992,6 +4013,7 @@ void fast_conv_set_x3_fwd_sw(int sw) { X3_FWD_SW = sw; }
 void fast_conv_set_x3_wg3_tile(int t) { X3_WG3_TILE = t; }
 void fast_conv_set_x3_fc_mmv(int v) { X3_FC_MMV = v; }
 void fast_conv_set_x3_fc_dg_gemm(int v) { X3_FC_DG_GEMM = v; }
+void fast_conv_set_x3_fcw_kt(int v) { X3_FCW_KT = v == 128 ? 128 : 256; }
 void fast_conv_set_x3_dg_w3(int v) { X3_DG_W3 = v; }
 void fast_conv_set_x3_dg_fold(int v) { X3_DG_FOLD = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
@@ -4108,9 +4130,10 @@ int x3_conv_fwd(const void* X, long xlo, int u8in, void* Y, long ylo, void* bits
 // first layer on the frame ring (frames [P*E][nslots][160*120] u8, fc [T+1][P*E] u8; runtime/engine.py frame_ring)
 int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, void* bits, const void* Wc, long wlo,
                       const float* flat, long bias_off, int chunk, const int* ai, const int* ac, int L, int M, int P,
-                      int E, int T, int t0, int nslots, long br, float is, float os, hipStream_t st) {
+                      int E, int T, int t0, int nslots, int rbase, long br, float is, float os, hipStream_t st) {
+  // rbase: the modular ring's base slot (step t's channel k in slot (rbase + t + max(k, fc)) mod nslots)
   if (!frames || !fc || chunk <= 0 || L <= 0 || M <= 0 || P <= 0 || E <= 0 || T <= 0 || t0 < 0 || br <= 0 ||
-      bias_off < 0 || ylo <= 0 || wlo <= 0 || nslots < t0 + T + 3) return -22;
+      bias_off < 0 || ylo <= 0 || wlo <= 0 || nslots < t0 + T + 3 || rbase < 0 || rbase >= nslots) return -22;
   if (M > 2 * X3_NCT) return 0;
   if ((E * C1::HOWO) % 16) return -2;
   const float isc = is / (float)(1 << X3_W0_SHIFT);
@@ -4121,19 +4144,19 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
   if (X3_C1_SB1)
     conv1_fwd_band_x2<C1, true, false, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
         (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
-        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots, rbase);
   else if (X3_C1_F16B)
     conv1_fwd_band_x2<C1, true, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
         (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
-        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots, rbase);
   else if (X3_C1_PIPE)
     conv1_fwd_band_x2<C1, true, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
         (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
-        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots, rbase);
   else
     conv1_fwd_band_x2<C1, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
         (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
-        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots);
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots, rbase);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
@@ -4171,9 +4194,9 @@ int x3_conv23_fwd(const void* X, long xlo, void* Y1, long y1lo, void* bits1, lon
 
 int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, const void* bits, float* grad, long w_off,
                         long b_off, int chunk, const int* ai, const int* ac, int L, int M, int P, int E, int T,
-                        int nslots, long br, float is, float gs, const float* gamax, hipStream_t st) {
+                        int nslots, int rbase, long br, float is, float gs, const float* gamax, hipStream_t st) {
   if (!frames || !fc || chunk <= 0 || L <= 0 || M <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 || w_off < 0 ||
-      b_off < 0 || nslots < T + 3 || !gamax) return -22;
+      b_off < 0 || nslots < T + 3 || rbase < 0 || rbase >= nslots || !gamax) return -22;
   if (M > 2 * X3_NCT) return 0;
   using SB = Slab<C1, 2>;
   const long units = (long)T * E * SB::NB;
@@ -4201,19 +4224,19 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (X3_C1_WG_NCX == 2 && X3_WGRAD_PF != 1)       // 2 tiles per pass: two stages in flight fit (162 VGPRs)
     conv_wgrad_slab_x3<C1, 2, 2, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum, rbase);
   else if (X3_C1_WG_NCX == 2)
     conv_wgrad_slab_x3<C1, 2, 1, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum, rbase);
   else if (X3_WGRAD_PF == 2)
     conv_wgrad_slab_x3<C1, 2, 2, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum);
+                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum, rbase);
   else
     conv_wgrad_slab_x3<C1, 2, 1, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum);
+                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum, rbase);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }
@@ -4240,11 +4263,11 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     if (pf == 2)
       conv_wgrad_slab_x3<Gx, OB, 2><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
                                                           ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs, nullptr,
-                                                          0, gamax, X3_SLAB_PMAP, g_fx_accum);
+                                                          0, gamax, X3_SLAB_PMAP, g_fx_accum, 0);
     else
       conv_wgrad_slab_x3<Gx, OB, 1><<<grid, 256, 0, st>>>(X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk,
                                                           ai, ac, layer, L, M, P, E, T, br, (int)upw, is, gs, nullptr,
-                                                          0, gamax, X3_SLAB_PMAP, g_fx_accum);
+                                                          0, gamax, X3_SLAB_PMAP, g_fx_accum, 0);
     const int rc = (int)hipGetLastError();
     return rc ? -rc : 1;
   };
@@ -4513,10 +4536,20 @@ int x3_fc_wgrad_gm(const void* X, long xlo, int ldx, const void* Gm, long gmlo, 
   if (ldx <= 0 || chunk <= 0 || M <= 0 || Pmax <= 0 || K <= 0 || Cout <= 0 || P <= 0 || E <= 0 || T <= 0 || br <= 0 ||
       nsplit <= 0 || w_off < 0 || b_off < 0 || layer < 0 || xlo <= 0 || gmlo <= 0 || !gamax) return -22;
   if (Cout != 256 || ldx % 8 != 0 || K % 8 != 0) return 0;
-  const int kt = (K + 127) / 128;
-  fc_wgrad_gm_x3<256><<<kt * M * nsplit, 512, 0, st>>>((const bf16_t*)X, xlo, ldx, (const bf16_t*)Gm, gmlo, grad,
-                                                       w_off, b_off, chunk, inv_path, inv_slot, inv_cnt, layer, M, Pmax,
-                                                       K, P, E, T, br, nsplit, gamax, g_fx_accum);
+  if (X3_FCW_KT == 256 && K > 256) {
+    // 256-wide k tiles: the masked gradient Gm (1 KB per row) is re-read once per k tile -- 6 instead of 11 times at
+    // K = 1408
+    const int kt = (K + 255) / 256;
+    fc_wgrad_gm_x3<256, 256><<<kt * M * nsplit, 512, 0, st>>>((const bf16_t*)X, xlo, ldx, (const bf16_t*)Gm, gmlo,
+                                                              grad, w_off, b_off, chunk, inv_path, inv_slot, inv_cnt,
+                                                              layer, M, Pmax, K, P, E, T, br, nsplit, gamax,
+                                                              g_fx_accum);
+  } else {
+    const int kt = (K + 127) / 128;
+    fc_wgrad_gm_x3<256><<<kt * M * nsplit, 512, 0, st>>>((const bf16_t*)X, xlo, ldx, (const bf16_t*)Gm, gmlo, grad,
+                                                         w_off, b_off, chunk, inv_path, inv_slot, inv_cnt, layer, M,
+                                                         Pmax, K, P, E, T, br, nsplit, gamax, g_fx_accum);
+  }
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }

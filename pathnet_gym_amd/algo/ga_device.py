@@ -47,15 +47,55 @@ def ga_rand(seed: int, gen: int, x: int, y: int, z: int) -> int:
     return wang(h ^ (((y & 0xFFFF) << 16) + (z & 0xFFFF)))
 
 
+def wang_np(x: np.ndarray) -> np.ndarray:
+    """``wang`` on a uint64 array holding 32-bit values (element-wise, bit-identical)."""
+    x = x & M32
+    x = (x ^ 61) ^ (x >> 16)
+    x = (x * 9) & M32
+    x ^= x >> 4
+    x = (x * 0x27D4EB2D) & M32
+    x ^= x >> 15
+    return x
+
+
+def ga_rand_np(seed: int, gen: int, x: int, y: np.ndarray, z: np.ndarray) -> np.ndarray:
+    """``ga_rand`` over arrays of (y, z) draws (uint64 in, uint64 out)."""
+    h = wang(wang(seed) ^ (gen & M32))
+    h = wang(h ^ (x & M32))
+    return wang_np(np.uint64(h) ^ (((y & 0xFFFF) << 16) + (z & 0xFFFF)))
+
+
 def counter_mutation(g: np.ndarray, L: int, M: int, N: int, seed: int, gen: int, path: int) -> np.ndarray:
-    """Reference mutation operator with counter-based draws (in place, returned)."""
+    """Reference mutation operator with counter-based draws (in place, returned).  The 2 L M draws are independent of
+    the genotype, so they are computed in one vectorised pass; the per-layer walk over the modules stays sequential
+    (a move can activate a module that a later step of the same layer reads)."""
+    ka = L * N
+    ki = L * (M - N) * M
+    ll, mm = np.meshgrid(np.arange(L, dtype=np.uint64), np.arange(M, dtype=np.uint64), indexing="ij")
+    h0 = ga_rand_np(seed, gen, path, ll, 2 * mm).tolist()
+    h1 = ga_rand_np(seed, gen, path, ll, 2 * mm + 1).tolist()
+    for l in range(L):
+        row0, row1 = h0[l], h1[l]
+        for m in range(M):
+            u24 = row0[m] >> 8                # U = u24 / 2^24;  int(U*K) <= 1  <=>  u24*K < 2^25
+            if g[l, m] == 1:
+                if u24 * ka < (1 << 25):
+                    g[l, m] = 0
+                    g[l, row1[m] % M] = 1
+            elif u24 * ki < (1 << 25):
+                g[l, row1[m] % M] = 1
+    return g
+
+
+def counter_mutation_scalar(g: np.ndarray, L: int, M: int, N: int, seed: int, gen: int, path: int) -> np.ndarray:
+    """The scalar form of counter_mutation (the oracle its vectorised draws are tested against)."""
     ka = L * N
     ki = L * (M - N) * M
     for l in range(L):
         for m in range(M):
             h0 = ga_rand(seed, gen, path, l, 2 * m)
             h1 = ga_rand(seed, gen, path, l, 2 * m + 1)
-            u24 = h0 >> 8                    # U = u24 / 2^24;  int(U*K) <= 1  <=>  u24*K < 2^25
+            u24 = h0 >> 8
             if g[l, m] == 1:
                 if u24 * ka < (1 << 25):
                     g[l, m] = 0

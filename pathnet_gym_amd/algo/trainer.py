@@ -19,6 +19,7 @@ the union over tasks by default.
 """
 from __future__ import annotations
 
+import gc
 import math
 import time
 from dataclasses import dataclass, field
@@ -138,6 +139,13 @@ class PathNetTrainer:
         self.guard = NonFiniteGuard(cfg.max_nonfinite)
         self.watchdog = Watchdog(cfg.watchdog_s, phase=lambda: self.tracer.current) if cfg.watchdog_s > 0 else None
         self._start_task(0, fresh=True)
+        if getattr(cfg, "gc_freeze", True):
+            # move everything built so far (torch / numpy / the engine's ~10^5 Python objects) out of the cyclic
+            # collector's reach: a full collection every ~70 K allocations otherwise walks all of it, a host pause of
+            # tens of ms that the pipelined loop (one update of GPU work queued) cannot hide -- measured as 64-path bench
+            # windows drifting 10.4 -> 12.0 ms after ~65 updates (profiles/r6/README.md)
+            gc.collect()
+            gc.freeze()
 
     # ------------------------------------------------------------------
     # task sequencing (doom_pathnet.py:178-293)
@@ -358,7 +366,11 @@ class PathNetTrainer:
                 handle = self.comm.exchange_async(eng.grad_flat, eng.fitness, eng.counters,
                                                   extra=eng.report_parts())
         with tr.phase("optimizer"):
-            eng.optimizer_step(lr)              # non-finite reduced gradient: skipped on device, on every rank
+            # non-finite reduced gradient: skipped on device, on every rank; the lr anneal runs on device too (the
+            # optimizer tail), the host clock only checks it
+            a2c = self.cfg.a2c
+            clock = self.global_step - (self.task_start_step if a2c.lr_anneal == "per_task" else 0)
+            eng.optimizer_step(lr, sched_t=clock)
         self.global_step += self.cfg.a2c.t_max * self.P * self.E * self.ctx.world
         self.updates += 1
         prev, self._pending = getattr(self, "_pending", None), (handle, self.global_step, self.updates)
@@ -407,7 +419,8 @@ class PathNetTrainer:
 
     def _collect(self, pending) -> UpdateStats:
         handle, step_at, u = pending
-        fit_all, csum, stats = self.comm.collect(handle)
+        with self.tracer.phase("collect"):           # waits for update u's read-back (GPU-bound when it dominates)
+            fit_all, csum, stats = self.comm.collect(handle)
         # stats[4]: whether the optimizer step of update u-1 skipped a non-finite gradient (read before the
         # optimizer of update u ran: one-update lag)
         skip = self._guard_opt(float(stats[4]), u - 1) if u > 1 else False

@@ -232,6 +232,9 @@ class TrainConfig:
     # multi-rank HIP engine: all-reduce everything but the first layer's gradient while that layer's weight-gradient
     # kernel runs (two async buckets, parallel/comm.py); False = one bucket after the whole backward
     overlap_allreduce: bool = True
+    # gc.freeze() once the trainer is built (algo/trainer.py): the objects of the setup leave the cyclic collector, whose
+    # full collections otherwise stall the pipelined update loop by tens of ms every ~70 updates
+    gc_freeze: bool = True
 
     def to_json(self):
         return json.dumps(dataclasses.asdict(self))

@@ -64,7 +64,7 @@ _SIGS = {
     "launch_cartpole_step": [P, P, P, P, P, c_int, c_uint, c_uint, c_int, P, P, P, P, P, P],
     "launch_pong_digit_tables": [P, c_int, c_int, c_int, c_int, c_int, P],
     "x3_refresh_weights_all": [P, c_int, P, P, P, c_int, c_int, P, P],
-    "launch_opt_tail": [P, P, c_int, c_int, c_int, P, P, P, P, P, c_int, P, P],
+    "launch_opt_tail": [P, P, c_int, c_int, c_int, P, P, P, P, P, c_int, P, P, P, P],
     "pong_tables_ints": [],
     "launch_rgb_stack_push": [P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "launch_rects_stack_push": [P, P, c_int, c_int, P, P, P, P, c_int, P],
@@ -139,11 +139,11 @@ _SIGS = {
                    + [c_long, c_float, c_float, P],
     "x3_conv_wgrad": [P, c_long, c_int, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 12
                      + [c_long, c_float, c_float, P, P],
-    "x3_conv1_ring_fwd": [P, P, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 7
+    "x3_conv1_ring_fwd": [P, P, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 8
                          + [c_long, c_float, c_float, P],
     "x3_conv23_fwd": [P, c_long, P, c_long, P, c_long, P, c_long, c_long, c_int, P, c_long, P, c_long, P, c_long,
                       c_long, c_int, P, P, P] + [c_int] * 7 + [c_float, c_float, P],
-    "x3_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 6 + [c_long, c_float, c_float, P,
+    "x3_conv1_ring_wgrad": [P, P, P, P, P, c_long, c_long, c_int, P, P] + [c_int] * 7 + [c_long, c_float, c_float, P,
                                                                                          P],
     "x3_conv_dgrad": [P, P, P, c_long, c_int, P, P] + [c_int] * 12 + [c_long, c_float, P, P, P, P],
     "x3_fc_fwd": [P, c_long, c_int, P, c_long, P, P, c_long, P, c_long, c_int, P, P] + [c_int] * 10
@@ -170,6 +170,7 @@ _SIGS = {
     "fast_conv_set_x3_wg3_tile": [c_int],
     "fast_conv_set_x3_fc_mmv": [c_int],
     "fast_conv_set_x3_fc_dg_gemm": [c_int],
+    "fast_conv_set_x3_fcw_kt": [c_int],
     "fast_conv_set_x3_dg_w3": [c_int],
     "fast_conv_set_x3_c1_f16b": [c_int],
     "fast_conv_set_x3_dg_fold": [c_int],

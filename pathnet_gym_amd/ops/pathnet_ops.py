@@ -950,7 +950,7 @@ class HipPathNet:
             raise ValueError("frame ring too short for the requested steps")
 
     def ring_fwd(self, frames, fc, Y, bits, P: int, E: int, T: int, t0: int, bits_rows: int, p0: int = 0,
-                 np_: Optional[int] = None):
+                 np_: Optional[int] = None, rbase: int = 0):
         """First layer on the frame ring, P paths x E envs x T steps from t0.  p0/np_ (fp32x): paths p0..p0+np_-1 of
         step t0 only (one group of the split rollout): frames, fc, Y, bits and the module tables are passed at the
         group's base (frames at env p0*E, slot t0; fc and the output rows at row t0*P*E + p0*E), so the kernel
@@ -975,18 +975,22 @@ class HipPathNet:
                 args = (frames.data_ptr(), fc.data_ptr(), Y.data_ptr(), x2_lo(Y), bits.data_ptr(),
                         m.act_idx.data_ptr(), m.act_cnt.data_ptr(), P, t0)
             fp, fcp, yp, ylo, bp, aip, acp, Pk, t0k = args
+            if grouped and rbase:
+                raise ValueError("ring_fwd: a path group of the split rollout needs the unwrapped ring (rbase 0)")
             ok = _lib.call_fast("x3_conv1_ring_fwd", fp, fcp, yp, ylo, bp, self.Wc[0].data_ptr(), self.Wc[0][0].numel(),
                                 m.store.flat.data_ptr(), g.b_off, g.chunk, aip, acp, self.L, self.M, Pk, E, T, t0k,
-                                frames.shape[1], bits_rows, g.in_scale, out_scale, _lib.stream())
+                                frames.shape[1], rbase, bits_rows, g.in_scale, out_scale, _lib.stream())
             if not ok:
                 raise RuntimeError(f"fp32x: frame-ring forward has no kernel for P={P}, E={E}, M={self.M}")
             return
+        if rbase:
+            raise ValueError("ring_fwd: the bf16 ring kernels read the unwrapped ring (rbase 0)")
         _lib.call("fast_conv1_ring_fwd", frames.data_ptr(), fc.data_ptr(), Y.data_ptr(), bits.data_ptr(),
                   self.Wh_ring.data_ptr(), m.store.flat.data_ptr(), g.b_off, g.chunk, m.act_idx.data_ptr(),
                   m.act_cnt.data_ptr(), 0, self.L, self.M, P, E, T, t0, frames.shape[1], bits_rows, g.in_scale,
                   out_scale, self.hcorr0.data_ptr(), self.Wc_ring.data_ptr(), _lib.stream())
 
-    def ring_wgrad(self, frames, fc, G, bits, grad_flat, P: int, E: int, T: int, bits_rows: int):
+    def ring_wgrad(self, frames, fc, G, bits, grad_flat, P: int, E: int, T: int, bits_rows: int, rbase: int = 0):
         self._check_ring(frames, fc, P, E, T)
         g = self.geoms[0]
         m = self.model
@@ -995,11 +999,13 @@ class HipPathNet:
             _lib.check(G, torch.float32, name="G")
             ok = _lib.call_fast("x3_conv1_ring_wgrad", frames.data_ptr(), fc.data_ptr(), G.data_ptr(), bits.data_ptr(),
                                 grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(),
-                                m.act_cnt.data_ptr(), self.L, self.M, P, E, T, frames.shape[1], bits_rows, g.in_scale,
-                                g_scale, self._gamax(0), _lib.stream())
+                                m.act_cnt.data_ptr(), self.L, self.M, P, E, T, frames.shape[1], rbase, bits_rows,
+                                g.in_scale, g_scale, self._gamax(0), _lib.stream())
             if not ok:
                 raise RuntimeError(f"fp32x: frame-ring weight gradient has no kernel for P={P}, E={E}, M={self.M}")
             return
+        if rbase:
+            raise ValueError("ring_wgrad: the bf16 ring kernels read the unwrapped ring (rbase 0)")
         _lib.call("fast_conv1_ring_wgrad", frames.data_ptr(), fc.data_ptr(), G.data_ptr(), bits.data_ptr(),
                   grad_flat.data_ptr(), g.w_off, g.b_off, g.chunk, m.act_idx.data_ptr(), m.act_cnt.data_ptr(), 0,
                   self.L, self.M, P, E, T, frames.shape[1], bits_rows, g.in_scale, g_scale, _lib.stream())

@@ -87,7 +87,11 @@ class HipEngine:
             H, W, C = model.cfg.input_shape
             hp.enable_ring()
             self.HW = H * W
-            self.frames = torch.zeros(B, T + 4, H * W, dtype=torch.uint8, device=dev)   # env-major: a stack is contiguous
+            # fp32x: a MODULAR ring of 2T slots (T >= 4): the rollout of parity q starts at base slot q*T, step t's
+            # channel k is slot (q*T + t + max(k, fc[t])) mod 2T, so the next rollout's first stack is already in
+            # place (no per-update copy of the last 4 planes: 157 MB, 51 us at 64 paths); other modes copy them
+            nsl = 2 * T if (hp.x3 and T >= 4) else T + 4
+            self.frames = torch.zeros(B, nsl, H * W, dtype=torch.uint8, device=dev)   # env-major: a stack is contiguous
             self.fc = torch.zeros(T + 1, B, dtype=torch.uint8, device=dev)
         elif self.pixels:
             H, W, C = model.cfg.input_shape
@@ -126,6 +130,18 @@ class HipEngine:
         self.path_part = torch.zeros(P, 2, device=dev)     # per-path (episodes, return sum) of the last rollout
         self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.zeros(2, dtype=torch.float32, device=dev)      # {lr, skip}
+        # the lr anneal on device (optimizer tail, csrc/ga.hip opt_tail_kernel): {lr0, max_t, mode, frames per update,
+        # frames done on the anneal clock}; the tail writes the next update's lr into self.lr, so the steady-state update
+        # needs no host fill (optimizer_step re-seeds it whenever the host's clock is not the one the device predicted)
+        world = 1
+        import torch.distributed as _dist
+        if _dist.is_available() and _dist.is_initialized():
+            world = _dist.get_world_size()
+        self.frames_per_update = T * P * E * world
+        self.lr_sched = torch.tensor([float(a2c.lr), float(a2c.max_time_step), 0.0 if a2c.lr_anneal == "none" else 1.0,
+                                      float(self.frames_per_update), 0.0], dtype=torch.float64, device=dev)
+        self._next_t = None
+        self._skip_set = False
         self.weight = ((1.0 / E) if a2c.env_reduction == "mean_env" else 1.0) * loss_scale(cfg)
         # end of the first layer's parameters (the overlapped exchange's second bucket, runtime/engine.py split)
         self._l0_end = max((s.offset + s.numel for s in model.store.layout.segments if s.layer == 0), default=0)
@@ -167,6 +183,7 @@ class HipEngine:
         self.auto_group_max_paths = int(os.environ.get("PATHNET_AUTO_GROUP_MAX_PATHS", "0"))
         self.groups = self._rollout_groups(getattr(cfg, "rollout_groups", 0))
         self.side_streams = [torch.cuda.Stream(device=dev) for _ in range(self.groups - 1)]
+        self.ring_mod = bool(self.ring and hp.x3 and self.groups == 1 and T >= 4 and self.frames.shape[1] == 2 * T)
         if self.groups > 1 and self.ring:
             for g in range(self.groups):
                 p0, np_ = self._group_range(g)
@@ -199,6 +216,20 @@ class HipEngine:
         """[T, B, ...] observations of the current rollout (steps 0..T-1); None with the frame ring."""
         return None if self._obs_bufs is None else self._obs_bufs[self._par]
 
+    @property
+    def rbase(self) -> int:
+        """Base slot of the running rollout in the modular frame ring (parity x T), 0 otherwise."""
+        return self._par * self.T if self.ring_mod else 0
+
+    def _slot(self, t: int) -> int:
+        """Frame-ring slot of plane t of the running rollout (t = 0..T+3: step t's newest channel is plane t + 3)."""
+        return (self.rbase + t) % self.frames.shape[1] if self.ring_mod else t
+
+    @property
+    def _parities(self) -> bool:
+        """Two rollout graphs, one per parity (observation double buffer, or the modular frame ring)."""
+        return self._obs_bufs is not None or self.ring_mod
+
     def _obs_at(self, t: int) -> torch.Tensor:
         """Input of step t (t == T: the bootstrap input = the next rollout's step 0, in the other buffer)."""
         return self._obs_bufs[self._par][t] if t < self.T else self._obs_bufs[1 - self._par][0]
@@ -228,7 +259,7 @@ class HipEngine:
         B = self.B
         dev = self.device
         c = torch.arange(4, device=dev)
-        idx = t + torch.maximum(c[None, :], self.fc[t].long()[:, None])           # [B, 4] frame slots
+        idx = (self.rbase + t + torch.maximum(c[None, :], self.fc[t].long()[:, None])) % self.frames.shape[1]
         planes = self.frames[torch.arange(B, device=dev)[:, None], idx]           # [B, 4, H*W]
         return planes.permute(0, 2, 1).reshape(B, -1).contiguous()
 
@@ -246,7 +277,7 @@ class HipEngine:
             return
         st = stack.reshape(self.B, self.HW, 4)
         for c in range(4):
-            self.frames[:, c].copy_(st[:, :, c])
+            self.frames[:, self._slot(c)].copy_(st[:, :, c])
         self.fc[0].zero_()
 
     def _build_opt_tables(self):
@@ -295,7 +326,8 @@ class HipEngine:
             h = m.store.layout.heads[m.task if m.cfg.per_task_heads else 0]
             env.step_ring_heads_into(self.acts[-1][t], m.store.flat, h, self.logits[t], self.values[t],
                                      self.actions[t], self.seed, self.ctr, t, self.T + 1, self.row_base, self.frames,
-                                     t + 4, self.fc[t], self.fc[t + 1], self.rewards[t], self.dones[t], self.epret[t])
+                                     self._slot(t + 4), self.fc[t], self.fc[t + 1], self.rewards[t], self.dones[t],
+                                     self.epret[t])
             return
         if grp is not None:
             p0, np_ = self._group_range(grp)
@@ -307,8 +339,8 @@ class HipEngine:
                                 self.dones[t], self.epret[t], b0=p0 * self.E, b1=(p0 + np_) * self.E)
             return
         if self.ring:
-            env.step_ring_into(self.actions[t], self.frames, t + 4, self.fc[t], self.fc[t + 1], self.rewards[t],
-                               self.dones[t], self.epret[t])
+            env.step_ring_into(self.actions[t], self.frames, self._slot(t + 4), self.fc[t], self.fc[t + 1],
+                               self.rewards[t], self.dones[t], self.epret[t])
         elif hasattr(env, "step_into"):
             env.step_into(self.actions[t], self._obs_at(t), self._obs_at(t + 1), self.rewards[t], self.dones[t],
                           self.epret[t])
@@ -330,7 +362,8 @@ class HipEngine:
         if self.ring:
             if grp is None:
                 p0, np_, t0, row0 = 0, self.P, t, 0
-                hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0])
+                hp.ring_fwd(self.frames, self.fc, self.acts[0], self.bits[0], self.P, self.E, 1, t, self.bits_rows[0],
+                            rbase=self.rbase)
             else:
                 # one path group: every launch at the group's first row of step t, the kernels at t0 = 0
                 p0, np_ = self._group_range(grp)
@@ -383,7 +416,7 @@ class HipEngine:
         for l in range(hi - 1, lo - 1, -1):
             if l == 0 and self.ring:
                 hp.ring_wgrad(self.frames, self.fc, self.grads[0], self.bits[0], self.grad_flat, P, E, T,
-                              self.bits_rows[0])
+                              self.bits_rows[0], rbase=self.rbase)
                 continue
             X = self.obs if l == 0 else self.acts[l - 1]
             dX = self.grads[l - 1] if l > 0 else None
@@ -706,10 +739,10 @@ class HipEngine:
                   self.lr.data_ptr(), self.opt_status.data_ptr(), o.decay, o.momentum, o.epsilon, o.clip_norm,
                   _lib.stream())
         self.hip.refresh_weights()
-        tail = self.ga_dev is not None and os.environ.get("PATHNET_OPT_TAIL", "1") != "0"
+        tail = self._tail
         if self.ga_dev is not None:
             self._ga_body(sync_fitness=not tail)
-        if self.ring:
+        if self.ring and not self.ring_mod:
             # through an int64 view: 8 bytes per element (the uint8 strided copy ran at ~3.4 TB/s, 92 us per update)
             f64 = self.frames.view(torch.int64) if self.HW % 8 == 0 else self.frames
             src = f64[:, self.T:self.T + 4]
@@ -721,7 +754,8 @@ class HipEngine:
             _lib.call("launch_opt_tail", g["fit"].data_ptr(), g["reset"].data_ptr(), g["p_off"], self.P,
                       self.fit_window, self.fitness.data_ptr(), self.fit_cnt.data_ptr(), self.fit_sum.data_ptr(),
                       self.fc[self.T].data_ptr() if self.ring else None, self.fc[0].data_ptr() if self.ring else None,
-                      self.B if self.ring else 0, self.ctr.data_ptr(), _lib.stream())
+                      self.B if self.ring else 0, self.ctr.data_ptr(), self.lr_sched.data_ptr(), self.lr.data_ptr(),
+                      _lib.stream())
             return
         if self.ring:
             self.fc[0].copy_(self.fc[self.T])
@@ -736,7 +770,7 @@ class HipEngine:
         par = self._par
         self.g_rollouts = []
         self.g_tails = []
-        for q in ((0, 1) if self._obs_bufs is not None else (par,)):      # one rollout graph per obs parity
+        for q in ((0, 1) if self._parities else (par,)):                  # one rollout graph per parity
             self._par = q
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
@@ -766,15 +800,29 @@ class HipEngine:
                 self._rollout_backward_body(part)
                 self._pending_capture = True
                 return
-            gi = self._par if self._obs_bufs is not None else 0
+            gi = self._par if self._parities else 0
             (self.g_tails[gi] if part == "tail" else self.g_rollouts[gi]).replay()
         else:
             self._rollout_backward_body(part)
 
-    def optimizer_step(self, lr: float, skip: bool = False):
-        """``skip``: host-decided skip (tests); non-finite gradients are skipped by the kernel itself."""
-        self.lr[0:1].fill_(lr)
-        self.lr[1:2].fill_(1.0 if skip else 0.0)
+    @property
+    def _tail(self) -> bool:
+        return self.ga_dev is not None and os.environ.get("PATHNET_OPT_TAIL", "1") != "0"
+
+    def optimizer_step(self, lr: float, skip: bool = False, sched_t: Optional[int] = None):
+        """``skip``: host-decided skip (tests); non-finite gradients are skipped by the kernel itself.  ``sched_t``: the
+        anneal clock (frames) ``lr`` was computed at; with the optimizer tail the device already holds that update's lr
+        (it advanced its own clock by one update's frames), so nothing is written unless the clocks disagree (first
+        update, checkpoint load, a caller without a clock)."""
+        dev_lr = sched_t is not None and self._tail
+        if not dev_lr or self._next_t != sched_t:
+            self.lr[0:1].fill_(lr)
+            if dev_lr:
+                self.lr_sched[4:5].fill_(float(sched_t))
+        if skip != self._skip_set:
+            self.lr[1:2].fill_(1.0 if skip else 0.0)
+            self._skip_set = skip
+        self._next_t = sched_t + self.frames_per_update if dev_lr else None
         if self.use_graph and self.g_opt is not None:
             self.g_opt.replay()
         else:
@@ -782,8 +830,8 @@ class HipEngine:
             if self.use_graph and getattr(self, "_pending_capture", False):
                 self._pending_capture = False
                 self._capture()
-        if self._obs_bufs is not None:
-            self._par ^= 1          # the next rollout starts from the buffer this one's last env step wrote
+        if self._parities:
+            self._par ^= 1          # the next rollout starts from the buffer / ring slots this one's last env step wrote
         self._read_union()
 
     def stats_host(self):

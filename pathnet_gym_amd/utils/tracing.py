@@ -22,12 +22,17 @@ import torch
 
 
 class PhaseTracer:
-    def __init__(self, enabled: bool = True, path: Optional[str] = None, rank: int = 0, max_events: int = 200000):
+    RESOLVE_EVERY = 256
+    def __init__(self, enabled: bool = True, path: Optional[str] = None, rank: int = 0, max_events: int = 200000,
+                 gpu_timing: Optional[bool] = None):
         self.enabled = enabled
         self.path = path
         self.rank = rank
         self.max_events = max_events
-        self.cuda = torch.cuda.is_available()
+        # per-phase GPU timing records two timing events into the stream per phase (~8 per update) and keeps them until
+        # resolved: only when a trace is written (or asked for), and folded every RESOLVE_EVERY phases so the pending
+        # list stays bounded (unbounded, it grew by 8 live events per update in every bench / solve run)
+        self.cuda = torch.cuda.is_available() and (bool(path) if gpu_timing is None else bool(gpu_timing))
         self.totals_ms: Dict[str, float] = defaultdict(float)
         self.gpu_ms: Dict[str, float] = defaultdict(float)
         self.counts: Dict[str, int] = defaultdict(int)
@@ -54,6 +59,8 @@ class PhaseTracer:
             if ev is not None:
                 ev[1].record()
                 self._pending.append((name, ev))
+                if len(self._pending) >= self.RESOLVE_EVERY:
+                    self.resolve()
             self.totals_ms[name] += dt * 1e3
             self.counts[name] += 1
             if self.path and len(self.events) < self.max_events:

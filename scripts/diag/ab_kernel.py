@@ -45,9 +45,9 @@ def main():
 
     def run():
         if a.kernel == "ring_wgrad":
-            hp.ring_wgrad(e.frames, e.fc, e.grads[0], e.bits[0], scratch, P, E, T, e.bits_rows[0])
+            hp.ring_wgrad(e.frames, e.fc, e.grads[0], e.bits[0], scratch, P, E, T, e.bits_rows[0], rbase=e.rbase)
         elif a.kernel == "ring_fwd":
-            hp.ring_fwd(e.frames, e.fc, e.acts[0], e.bits[0], P, E, 1, 3, e.bits_rows[0])
+            hp.ring_fwd(e.frames, e.fc, e.acts[0], e.bits[0], P, E, 1, 3, e.bits_rows[0], rbase=e.rbase)
         elif a.kernel == "conv23_fwd":
             hp.conv23_fwd(1, e.acts[0], e.acts[1], e.bits[1], e.bits_rows[1], e.acts[2], e.bits[2], e.bits_rows[2],
                           P, E, 1, 3)

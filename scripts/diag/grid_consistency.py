@@ -54,7 +54,7 @@ def main():
             setopt(arm)
             g = torch.zeros_like(e.grad_flat)
             if l == 0:
-                hp.ring_wgrad(e.frames, e.fc, e.grads[0], e.bits[0], g, P, E, T, e.bits_rows[0])
+                hp.ring_wgrad(e.frames, e.fc, e.grads[0], e.bits[0], g, P, E, T, e.bits_rows[0], rbase=e.rbase)
                 dx = None
             else:
                 hp.layer_bwd(l, e.acts[l - 1], e.grads[l], e.bits[l], g, e.grads[l - 1], P, E, T, e.bits_rows[l])

@@ -207,3 +207,17 @@ def test_counter_mutation_rates_match_reference_operator():
         moved += before[0, 0] == 1 and g[0, 0] == 0
     # P[int(U*L*N) <= 1] = 2/(L*N), times P[the random target is not module 0 itself] = (M-1)/M
     assert abs(moved / trials_a - 2 / (L * N) * (M - 1) / M) < 0.02
+
+
+def test_counter_mutation_vectorised_draws_match_scalar():
+    """algo/ga_device.counter_mutation draws its 2 L M counter-hash numbers in one numpy pass; the decisions equal
+    the scalar walk's (the device GA kernel's oracle) on random genotypes, seeds, generations and paths."""
+    from pathnet_gym_amd.algo.ga_device import counter_mutation, counter_mutation_scalar
+    rng = np.random.RandomState(0)
+    for _ in range(500):
+        L, M = int(rng.randint(1, 6)), int(rng.randint(2, 11))
+        N = int(rng.randint(1, M))
+        g = (rng.rand(L, M) < 0.5).astype(np.float32)
+        seed, gen, path = int(rng.randint(0, 2 ** 32 - 1)), int(rng.randint(0, 10 ** 7)), int(rng.randint(0, 4096))
+        assert np.array_equal(counter_mutation(g.copy(), L, M, N, seed, gen, path),
+                              counter_mutation_scalar(g.copy(), L, M, N, seed, gen, path))

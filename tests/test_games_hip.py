@@ -122,3 +122,4 @@ def test_hip_game_frame_ring_matches_packed_stacks(hip_lib, name):
         assert torch.equal(stack, obs), t
         ndone += int(d.sum())
     assert ndone > 0
+

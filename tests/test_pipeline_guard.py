@@ -21,10 +21,10 @@ def test_pipelined_skip_is_attributed_to_its_update(hip_lib):
     orig = eng.optimizer_step
     poison = {3, 6}
 
-    def step(lr):
+    def step(lr, **kw):
         if tr.updates + 1 in poison:            # the optimizer step of update 3 / 6 sees a NaN gradient
             eng.grad_flat[7] = float("nan")
-        orig(lr)
+        orig(lr, **kw)
     eng.optimizer_step = step
     seen = {}
     for _ in range(5):

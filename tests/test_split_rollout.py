@@ -132,7 +132,9 @@ def _run_x3_ring(groups, graph, updates=4, paths=8):
     for _ in range(updates):              # eager, capture, replays (the device GA fires tournaments in between)
         tr.update()
         torch.cuda.synchronize()
-        snaps.append({"obs": e.obs_stacks().clone(), "actions": e.actions.clone(), "logits": e.logits.clone(),
+        # the next rollout's first stack (the env state both must agree on; the ring's later slots hold frames of an
+        # earlier rollout, laid out differently by the one-group modular ring and the two-group copied ring)
+        snaps.append({"obs": e.obs_stacks(1).clone(), "actions": e.actions.clone(), "logits": e.logits.clone(),
                       "values": e.values.clone(), "rewards": e.rewards.clone(), "dones": e.dones.clone(),
                       "acts": [a.clone() for a in e.acts], "bits": [b.clone() for b in e.bits],
                       "act_idx": tr.model.act_idx.clone()})

@@ -753,7 +753,7 @@ def test_x3_conv1_ring_wgrad_two_tile_passes_match_default(x3_ring_rollout, ncx,
         lib.fast_conv_set_x3_wgrad_pf(pf if arm == "variant" else 3)
         eng.grad_flat.zero_()
         hp.ring_wgrad(eng.frames, eng.fc, eng.grads[0], eng.bits[0], eng.grad_flat, eng.P, eng.E, eng.T,
-                      eng.bits_rows[0])
+                      eng.bits_rows[0], rbase=eng.rbase)
         torch.cuda.synchronize()
         outs.append(eng.grad_flat[seg].clone())
     lib.fast_conv_set_x3_c1_wg_ncx(2)            # the defaults
@@ -781,7 +781,8 @@ def test_x3_conv1_band_f16_staging_bit_equal(x3_ring_rollout, opt):
         eng.acts[0].zero_()
         eng.bits[0].zero_()
         for t in range(eng.T):
-            hp.ring_fwd(eng.frames, eng.fc, eng.acts[0], eng.bits[0], eng.P, eng.E, 1, t, eng.bits_rows[0])
+            hp.ring_fwd(eng.frames, eng.fc, eng.acts[0], eng.bits[0], eng.P, eng.E, 1, t, eng.bits_rows[0],
+                        rbase=eng.rbase)
         torch.cuda.synchronize()
         outs.append((eng.acts[0].clone(), eng.bits[0].clone()))
     setter(1 if opt == "f16b" else 0)           # the defaults
@@ -892,9 +893,8 @@ def test_x3_deterministic_gradient_vs_float64_truth(hip_lib, ring):
     check_layers(f"fp32x deterministic ({'ring' if ring else 'packed'})", tr, g_det, *_oracles(_oracle_grad, tr, eng))
     assert int(tr.model.hip._fxbuf.abs().sum()) == 0
     tr.model.hip.check_x3_status()
-    eng._rollout_backward_body()                   # the same stored rollout again: bit-identical
-    torch.cuda.synchronize()
-    assert torch.equal(eng.grad_flat, g_det)
+    _, eng2 = _det_rollout(ring, True)             # an identical second trainer: the same rollout, the same bits
+    assert torch.equal(eng2.grad_flat, g_det)
 
 
 def test_x3_deterministic_200_updates_bit_identical(hip_lib):
@@ -922,3 +922,21 @@ def test_x3_deterministic_200_updates_bit_identical(hip_lib):
     a, b = run(), run()
     assert a[3] > 0, "no tournament fired"
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]) and a[3] == b[3]
+
+
+def test_device_lr_schedule_matches_host_anneal(hip_lib):
+    """The optimizer tail advances the lr anneal on device (csrc/ga.hip opt_tail_kernel): after every update the lr
+    waiting for the next one equals the host's anneal_lr (fp32) at the next clock, and no host fill was needed."""
+    from pathnet_gym_amd.algo.optim import anneal_lr
+    tr = _shipped_trainer(paths=4, envs=16, tmax=5)
+    tr.cfg.a2c.max_time_step = 4000                # a short anneal: the lr moves every update and reaches 0
+    eng = tr.engine
+    eng.lr_sched[1] = 4000.0
+    for u in range(14):
+        tr.update()
+        torch.cuda.synchronize()
+        nxt = anneal_lr(tr.cfg.a2c.lr, tr.global_step - tr.task_start_step, 4000, 0, "per_task")
+        assert float(eng.lr[0]) == float(np.float32(nxt)), (u, float(eng.lr[0]), nxt)
+        assert eng._next_t == tr.global_step - tr.task_start_step
+    tr.flush()
+    assert float(eng.lr[0]) == 0.0
