@@ -91,7 +91,7 @@ def solve_key(cfg, preset_name: str) -> dict:
             "rmsp_epsilon": cfg.a2c.rmsp_epsilon}
 
 
-def solve_records(key: dict, n_gpus: int, sources: str = None):
+def solve_records(key: dict, n_gpus: int, sources: str = None, root: str = None):
     """The committed solve runs (profiles/solve/*.json, written by scripts/solve.py --out) of exactly this config on
     ``n_gpus`` GPUs, under the v2 criterion (algo/solve.py: the task horizon where the lr anneal reaches 0, a held-out
     confirmation of the winning path) and built from the same sources as the running library (``sources``, the
@@ -100,7 +100,7 @@ def solve_records(key: dict, n_gpus: int, sources: str = None):
     median over seeds with "unsolved at horizon" counted as infinite: null unless most seeds solved."""
     import glob
     from pathnet_gym_amd.algo.solve import CRITERION
-    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "solve")
+    root = root or os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "solve")
     by_seed, excluded = {}, {"other_config": 0, "pre_v2_criterion": 0, "other_build": 0, "wall_limited": 0}
     for f in sorted(glob.glob(os.path.join(root, "*.json"))):
         try:

@@ -75,3 +75,40 @@ def test_bench_mismatch_guard_on_the_gpu_box(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "0"],
                        cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=4" in r.stderr and not r.stdout.strip(), (r.returncode, r.stderr[-400:])
+
+
+def test_solve_records_v2_one_per_seed_same_build(tmp_path):
+    """bench.solve_records: only v2-criterion records (task horizon + held-out confirmation) of this config and build
+    count, one per seed (the latest), wall-limited runs are set apart, unsolved-at-horizon counts as infinite."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from pathnet_gym_amd.algo.solve import CRITERION
+    from pathnet_gym_amd.config import preset
+    key = bench.solve_key(preset("pong"), "pong")
+    cfgd = dict(key, seed=0, ga=True)
+
+    def rec(name, seed, solved, gens, t, stopped="solved", src="aaaa", crit=CRITERION, **kw):
+        c = dict(cfgd, seed=seed, **kw)
+        d = {"metric": "generations_to_solve", "n_gpus": 1, "criterion": crit, "solved": solved, "stopped": stopped,
+             "generations_to_solve": gens if solved else None, "updates_to_solve": gens * 5 if solved else None,
+             "frames_to_solve": gens * 100 if solved else None, "finished_at": t, "config": c,
+             "build": {"sources_sha256": src}, "candidates": []}
+        (tmp_path / name).write_text(json.dumps(d) + "\n")
+
+    rec("a.json", 1, True, 100, 1.0)
+    rec("b.json", 1, True, 300, 2.0)                       # a later run of seed 1 replaces a.json
+    rec("c.json", 2, False, 0, 1.0, stopped="horizon")     # unsolved at the horizon: counts, as infinite
+    rec("d.json", 3, True, 200, 1.0)
+    rec("e.json", 4, True, 50, 1.0, src="bbbb")            # another build
+    rec("f.json", 5, True, 60, 1.0, crit="old")            # pre-v2 criterion
+    rec("g.json", 6, False, 0, 1.0, stopped="wall")        # wall-limited before the horizon
+    r = bench.solve_records(key, 1, "aaaa", root=str(tmp_path))
+    assert r["seeds"] == 3 and r["solved_seeds"] == 2
+    assert [x["seed"] for x in r["runs"]] == [1, 2, 3]
+    assert r["runs"][0]["generations"] == 300
+    assert r["value"] == 300 and r["min"] == 200 and r["max"] == "unsolved"
+    assert r["excluded"] == {"other_config": 0, "pre_v2_criterion": 1, "other_build": 1, "wall_limited": 1}
+    assert bench.committed_updates_to_solve.__code__.co_argcount == 2
