@@ -151,7 +151,8 @@ def main():
                 old = json.loads(f.read().strip().splitlines()[-1])
             prior = {"seconds": float(old.get("seconds", 0.0)), "segments": list(old.get("segments", []))
                      or [{"updates": old.get("updates"), "seconds": old.get("seconds")}],
-                     "best": old.get("best_winner_fitness"), "ema": old.get("final_mean_return")}
+                     "best": old.get("best_winner_fitness"), "ema": old.get("final_mean_return"),
+                     "candidates": list(old.get("candidates", []))}
         if ctx.is_main:
             print(json.dumps({"resumed": args.checkpoint, "updates": tr.updates, "generation": tr.pop.generation,
                               "frames": tr.global_step, "prior_seconds": prior["seconds"]}), flush=True)
@@ -178,6 +179,7 @@ def main():
                        wall_s=args.minutes * 60 - prior["seconds"], log=log_candidate)
     if prior.get("best") is not None:
         trk.best = prior["best"]
+    trk.candidates = list(prior.get("candidates", []))     # the held-out checks of earlier segments
     ret_ema = prior.get("ema")
     while True:
         st = tr.update()

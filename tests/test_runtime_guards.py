@@ -82,3 +82,21 @@ def test_state_digest_detects_any_change():
 
 def test_performance_line_format():
     assert performance_line(1000, 10.0) == "### Performance : 1000 STEPS in 10 sec. 100 STEPS/sec. 0.36M STEPS/hour"
+
+
+def test_phase_tracer_gpu_events_only_when_tracing(tmp_path):
+    """The per-phase GPU timing events are recorded only when a trace is written (or asked for), and folded every
+    RESOLVE_EVERY phases: the pending list stays bounded (it used to grow by 8 live events per update)."""
+    from pathnet_gym_amd.utils.tracing import PhaseTracer
+    t = PhaseTracer(enabled=True)
+    assert not t.cuda
+    for _ in range(10):
+        with t.phase("x"):
+            pass
+    assert t.counts["x"] == 10 and not t._pending
+    t2 = PhaseTracer(enabled=True, path=str(tmp_path / "tr.json"))
+    assert t2.cuda == torch.cuda.is_available()
+    for _ in range(3 * PhaseTracer.RESOLVE_EVERY):
+        with t2.phase("y"):
+            pass
+    assert len(t2._pending) < PhaseTracer.RESOLVE_EVERY + 1
