@@ -7,7 +7,8 @@ MIN=${3:-17.5}
 S="--preset pong --paths 64 --envs 32 --ring --dtype fp32x --ga-backend device --deterministic --report-every 30"
 pids=()
 for seed in $1 $2; do
-  timeout -k 10 $(python3 -c "print(int($MIN*60+90))") python -u scripts/solve.py --minutes $MIN $S --seed $seed \
+  # "1r": a repeat of seed 1 under its own name (the deterministic mode must reproduce it exactly)
+  timeout -k 10 $(python3 -c "print(int($MIN*60+90))") python -u scripts/solve.py --minutes $MIN $S --seed ${seed%r} \
       --curve $OUT/v2_seed$seed.jsonl --out $OUT/v2_seed$seed.json > $OUT/v2_seed$seed.log 2>&1 &
   pids+=($!)
 done
