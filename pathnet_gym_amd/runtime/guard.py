@@ -36,7 +36,8 @@ class X3RangeError(FloatingPointError):
     """fp32x (split fp16 pairs): a value left the fp16 range.  Bit 0 (value 1) of the status: a weight scaled by
     2^8 -- of any trunk layer (x3_refresh_weights) or the LSTM kernel (lstm_refresh_x3) -- reached 32768 (its pair
     no longer represents it); bit 1 (value 2): an activation written as an fp16 pair (trunk or LSTM state) reached
-    65504.  The status travels in the update's all-reduced counters, so every rank raises together.
+    65504; bit 2 (value 4, deterministic mode): a weight-gradient contribution left the fixed-point accumulator's range.
+    The status travels in the update's all-reduced counters, so every rank raises together.
 
     Lag: the flags are folded into the counters after each rollout, so an overflow raised by the weight refresh at
     the end of update u surfaces with update u + 1.  ``PathNetTrainer.flush()`` (called at task end and before every
@@ -54,6 +55,9 @@ class X3RangeError(FloatingPointError):
                 what.append("a weight x 2^8 (a trunk layer or the LSTM kernel) left the fp16 range (|W| >= 128)")
             if bits & 2:
                 what.append("an activation stored as an fp16 pair reached 65504")
+            if bits & 4:
+                what.append("deterministic mode: a weight-gradient contribution reached the int64 fixed-point range "
+                            "(|g| >= 65536 or NaN, csrc/common.h gacc)")
         super().__init__(f"fp32x range overflow at update {update}: " + "; ".join(what)
                          + " -- use compute_dtype='fp32' for this model / data scale")
 
