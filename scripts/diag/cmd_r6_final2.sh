@@ -4,6 +4,8 @@ set -o pipefail
 OUT=gpurun_out/r6_final
 mkdir -p $OUT
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread -k "typed_fc" > $OUT/pytest_typed.log 2>&1; echo "typed tests rc=$?"
+grep -E "FAILED|passed|failed" $OUT/pytest_typed.log | tail -4
 for arm in nogroup forced nogroup forced; do
   for p in 8 64; do
     if [ $arm = forced ]; then export PATHNET_DIST_FORCE=1; else unset PATHNET_DIST_FORCE; fi
