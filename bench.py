@@ -262,7 +262,11 @@ def in_run_solve(args, ctx, dtype: str, cap_s: float, paths_total: int = 0) -> d
     the reward threshold, confirmed by a held-out evaluation of its path, before the task horizon.  Every rank takes
     the same decisions (replicated GA, rank 0's held-out mean, a collective wall-cap check every 32 updates)."""
     from pathnet_gym_amd.algo.solve import SolveTracker
-    cfg, tr = build_trainer(args, ctx, dtype, stagger=False, paths_total=paths_total)
+    a = argparse.Namespace(**vars(args))
+    if args.solve_deterministic and ctx.world == 1 and dtype == "fp32x":
+        # the committed seeds ran in the deterministic mode (bit-reproducible): this run repeats one of them exactly
+        a.deterministic = True
+    cfg, tr = build_trainer(a, ctx, dtype, stagger=False, paths_total=paths_total)
     t0 = time.time()
     last = [t0]
 
@@ -278,9 +282,28 @@ def in_run_solve(args, ctx, dtype: str, cap_s: float, paths_total: int = 0) -> d
     while not trk.observe(tr.update()):
         progress()
     tr.flush()
-    out = {"seed": cfg.seed, "cap_s": round(cap_s, 1), "paths_per_gpu": cfg.paths, "paths_total": tr.P_total}
+    out = {"seed": cfg.seed, "cap_s": round(cap_s, 1), "paths_per_gpu": cfg.paths, "paths_total": tr.P_total,
+           "deterministic": bool(tr.model.hip is not None and tr.model.hip.reproducible)}
     out.update(trk.record())
     return out
+
+
+def compare_with_committed(run: dict, records: dict) -> dict:
+    """The in-run solve against the committed record of the same seed (same config, build and criterion): in the
+    deterministic mode one seed defines a run, so generations, updates and the held-out mean must be equal."""
+    if not run or not run.get("deterministic"):
+        return {"compared": False, "reason": "the in-run solve was not deterministic"}
+    same = [r for r in (records or {}).get("runs", []) if r.get("seed") == run.get("seed") and r.get("deterministic")]
+    if not same:
+        return {"compared": False, "reason": "no committed deterministic record of this seed, config and build"}
+    r = same[0]
+    if run.get("stopped") != "solved":
+        return {"compared": True, "file": r["file"], "reproduces": False, "reason": f"in-run solve {run.get('stopped')}"}
+    eq = (run.get("generations_to_solve") == r.get("generations") and run.get("updates_to_solve") == r.get("updates")
+          and run.get("heldout_mean") == r.get("heldout_mean"))
+    return {"compared": True, "file": r["file"], "reproduces": bool(eq),
+            "committed": {"generations": r.get("generations"), "updates": r.get("updates"),
+                          "heldout_mean": r.get("heldout_mean")}}
 
 
 def committed_updates_to_solve(key: dict, sources: str = None) -> list:
@@ -450,6 +473,9 @@ def main():
                     help="after the timed windows, run one generations-to-solve seed on a fresh trainer for at most "
                          "this long (default: one GPU, the bench config, what is left of a 560 s run, at most 480 s; "
                          "several GPUs, the strong-scaling config, what is left of 480 s, at most 300 s; 0 = off)")
+    ap.add_argument("--solve-deterministic", type=int, default=1,
+                    help="one GPU, fp32x: run the in-run solve in the deterministic mode, so it repeats the committed "
+                         "record of its seed exactly (reported as generations_to_solve_in_run.vs_committed)")
     ap.add_argument("--compare-bf16", type=int, default=None,
                     help="also time the bf16 engine on the same config (default: on for one GPU)")
     ap.add_argument("--reference-preset", type=int, default=None,
@@ -633,6 +659,9 @@ def main():
         rec.setdefault("build", {})["verified"] = verified
     if ctx.is_main:
         rec["generations_to_solve"] = solve_records(key, world, sources)
+        if rec.get("generations_to_solve_in_run") is not None:
+            rec["generations_to_solve_in_run"]["vs_committed"] = compare_with_committed(
+                rec["generations_to_solve_in_run"], rec["generations_to_solve"])
         print(json.dumps(rec), flush=True)
     ctx.destroy()
 
