@@ -239,6 +239,8 @@ def timed_windows(tr, ctx, steps: int, warmup: int, windows: int = 1, markers: b
         if info is not None:
             ex = tr.pop.expressed()
             tel["active_modules_per_layer"] = [round(float(x), 3) for x in ex.sum(axis=2).mean(axis=0)]
+            # the widest path per layer: a path of more than 4 (or 6) active modules runs extra passes in some kernels
+            tel["active_modules_max_per_layer"] = [int(x) for x in ex.sum(axis=2).max(axis=0)]
             tel["ms"] = round(dt / steps * 1e3, 3)
             # host milliseconds per update in each phase of the pipelined loop (utils/tracing.py): "collect" is the
             # wait for the previous update's read-back, i.e. GPU-bound time; the rest is host work

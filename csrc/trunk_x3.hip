@@ -583,7 +583,18 @@ DEVI uint4 planes_to_px4(uint4 v) {
 #ifndef X3_C1_EARLY_BAND
 #define X3_C1_EARLY_BAND 1
 #endif
-template <class G, bool RING = false, bool PIPE = false, bool F16B = false, bool SB1 = false>
+// BAL: cost-balanced schedule.  A path of 5-6 active modules runs two passes over its bands (NCXT = 2 column tiles per
+// pass), so with one fixed band range per (workgroup, path) its workgroups took twice as long as the others and the
+// launch waited on them (reference preset: 95 -> 162 us per step once the GA grew one path to 5 modules).  With BAL
+// the grid is 1-D and workgroup w takes the w-th equal share of the population's total cost (a band of path p costs
+// its pass count), i.e. a contiguous run of (path, band) units that may span paths; all passes of a band stay in one
+// workgroup, in order (pass > 0 adds into Y), so the output is bit-identical to the per-path grid.
+DEVI int c1_npass(int cnt) {
+  const int nct = (cnt + 1) >> 1;
+  return nct > 2 ? (nct + 1) / 2 : 1;
+}
+
+template <class G, bool RING = false, bool PIPE = false, bool F16B = false, bool SB1 = false, bool BAL = false>
 __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint8_t* __restrict__ X, uint16_t* __restrict__ Y,
                                                            long ylo, uint8_t* __restrict__ bits,
                                                            const uint16_t* __restrict__ Wh, long wlo,
@@ -608,26 +619,63 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
   // RING: the first-valid channel of every sample of the workgroup's bands, staged once.  Read per band from global
   // memory it put a dependent byte load (and a full vmcnt wait) in front of every band's frame loads.
   __shared__ uint8_t fcs[RING ? X3_C1_FWD_FCS : 1];
-  const int p = blockIdx.y;
-  const int cnt = act_cnt[p * L + layer];
-  const int nct = (cnt + 1) >> 1;
+  __shared__ int sched[4];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15, q = grp;
   const int PE = P * E;
   const int nbands = T * E * B::NB;
-  const int b_beg = blockIdx.x * bands_per_wg;
-  const int b_end = min(nbands, b_beg + bands_per_wg);
-  if (b_beg >= b_end) return;
-  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
-  const int s_first = b_beg / B::NB;
-  if constexpr (RING) {
-    const int ns = (b_end - 1) / B::NB - s_first + 1;     // <= X3_C1_FWD_FCS (launcher caps bands_per_wg)
-    for (int i = tid; i < ns; i += 256) {
-      const int s = s_first + i, st = s / E, e = s - st * E;
-      fcs[i] = fcv[(long)(t0 + st) * PE + (long)p * E + e];
+  // this workgroup's units: (path, band) from (seg_p0, seg_b0) up to, not including, (seg_p1, seg_b1)
+  int seg_p0, seg_b0, seg_p1, seg_b1;
+  if constexpr (BAL) {
+    if (w == 0) {
+      int tot = 0;
+      for (int pb = 0; pb < P; pb += 64) {
+        int c = pb + l < P ? c1_npass(act_cnt[(pb + l) * L + layer]) : 0;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m, 64);
+        tot += c;
+      }
+      const long U = (long)tot * nbands;
+      const long ca = U * blockIdx.x / gridDim.x, cb = U * (blockIdx.x + 1) / gridDim.x;
+      long base = 0;
+      for (int pb = 0; pb < P; pb += 64) {
+        const int pp = pb + l;
+        const int np = pp < P ? c1_npass(act_cnt[pp * L + layer]) : 0;
+        int x = np * nbands;                               // inclusive scan of the paths' costs in this chunk
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int y = __shfl_up(x, d, 64);
+          if (l >= d) x += y;
+        }
+        const long incl = base + x, excl = incl - (long)np * nbands;
+        if (np > 0 && ca >= excl && ca < incl) {
+          sched[0] = pp;
+          sched[1] = (int)((ca - excl) / np);
+        }
+        if (np > 0 && cb >= excl && cb < incl) {
+          sched[2] = pp;
+          sched[3] = (int)((cb - excl) / np);
+        }
+        base += __shfl(x, 63, 64);
+      }
+      if (l == 0 && cb >= U) {
+        sched[2] = P - 1;
+        sched[3] = nbands;
+      }
     }
+    __syncthreads();
+    seg_p0 = sched[0];
+    seg_b0 = sched[1];
+    seg_p1 = sched[2];
+    seg_b1 = sched[3];
+    if (seg_p0 == seg_p1 && seg_b0 >= seg_b1) return;
+  } else {
+    seg_p0 = seg_p1 = blockIdx.y;
+    seg_b0 = blockIdx.x * bands_per_wg;
+    seg_b1 = min(nbands, seg_b0 + bands_per_wg);
+    if (seg_b0 >= seg_b1) return;
   }
-  const int npass = nct > NCXT ? (nct + NCXT - 1) / NCXT : 1;
+  int p = seg_p0, cnt = 0, nct = 0, b_beg = 0, b_end = 0, s_first = 0;
   static_assert(B::CIT == 5, "five named staging registers");
   uint4 rg0, rg1, rg2, rg3, rg4;                       // (an indexed array captured by the lambdas went to scratch)
   // band u -> (sample s = u / NB, first output row oh0 = (u % NB) * OBR); the last band's rows past HO read the
@@ -697,6 +745,26 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
   };
 
 
+  // segments: one path's run of bands, at most X3_C1_FWD_FCS - 2 samples (the staged fc bytes) at a time
+  constexpr int MAXB = (X3_C1_FWD_FCS - 2) * B::NB;
+  for (int sp = seg_p0; sp <= seg_p1; ++sp)
+  for (int cb = sp == seg_p0 ? seg_b0 : 0, ce = sp == seg_p1 ? seg_b1 : nbands; cb < ce; cb += MAXB) {
+  p = sp;
+  b_beg = cb;
+  b_end = min(ce, cb + MAXB);
+  if (sp != seg_p0 || cb != seg_b0) __syncthreads();  // the previous segment's LDS reads (mods, fcs, Ws, Xb) done
+  cnt = act_cnt[p * L + layer];
+  nct = (cnt + 1) >> 1;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  s_first = b_beg / B::NB;
+  if constexpr (RING) {
+    const int ns = (b_end - 1) / B::NB - s_first + 1;     // <= X3_C1_FWD_FCS (launcher caps bands_per_wg)
+    for (int i = tid; i < ns; i += 256) {
+      const int s = s_first + i, st = s / E, e = s - st * E;
+      fcs[i] = fcv[(long)(t0 + st) * PE + (long)p * E + e];
+    }
+  }
+  const int npass = nct > NCXT ? (nct + NCXT - 1) / NCXT : 1;
   for (int pass = 0; pass < npass; ++pass) {
     const int ct0 = pass * NCXT;
     const int ncg = nct == 0 ? 1 : min(NCXT, nct - ct0);
@@ -838,6 +906,7 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
     };
     if (ncg == 1) run(std::integral_constant<int, 1>{});
     else run(std::integral_constant<int, 2>{});
+  }
   }
 }
 
@@ -1879,6 +1948,11 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
   const int p = blockIdx.y;
   const int cnt = act_cnt[p * L + layer];
   if (cnt == 0) return;
+  // passes of 2 column tiles (4 slots) are spread over blockIdx.z: a path of 5..8 active slots runs its two passes
+  // in two workgroups of the usual length instead of one of twice the length (the launch's tail)
+  const int nct = (cnt + 1) >> 1;
+  const int npass = (nct + 1) / 2;
+  if ((int)blockIdx.z >= npass) return;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, i16 = l & 15, q = i16 >> 2, pp = i16 & 3;
   const int PE = P * E;
@@ -1918,11 +1992,9 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
   for (int ks = 0; ks < W::NKS; ++ks)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) posoff[ks][hf] = (posoff[ks][hf] < 0 || koff < 0) ? W::TILE : posoff[ks][hf] + koff;
-  const int nct = (cnt + 1) >> 1;
-  const int npass = (nct + 1) / 2;
   const int a_my = tid & 3;                       // the slot (within the pass) of every staging item of this thread
   const float gs = g16_scale(gamax), ginv = 1.0f / gs;   // G16
-  for (int pass = 0; pass < npass; ++pass) {
+  for (int pass = blockIdx.z; pass < npass; pass += gridDim.z) {
     const int ct0 = pass * 2;
     const int nc = min(2, nct - ct0);
     const bool slot_ok = a_my < 2 * nc && 2 * ct0 + a_my < cnt;
@@ -2018,7 +2090,7 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
     }
   }
   __syncthreads();
-  if (tid < cnt * 8) {
+  if (tid < cnt * 8 && ((tid >> 5) % (int)gridDim.z) == (int)blockIdx.z) {   // the slots of this workgroup's passes
     const long bi = b_off + (long)mods[tid >> 3] * chunk + (tid & 7);
     if (fx) gacc_q(fx, bi, dbq[tid]);
     else atomicAdd(&grad[bi], dbias[tid]);
@@ -2033,6 +2105,7 @@ __global__ __launch_bounds__(WT3<G>::NT, 2) void conv_wgrad_tile_x3(const uint16
 // per group of 4, adding into dX); B = the hi/lo weights of those slots.  fp32 dX.  grid = (chunks, P).
 // ===========================================================================
 #define X3_DG_PSTR 32        // one position's 4 slots x 8 maps
+#define X3_DG_SPLIT 2        // conv_dgrad_x3 gridDim.z: the sample split of paths of > 4 active slots
 DEVI int dg_swz(int i) { return (i >> 1) & 3; }
 template <class G>
 struct DGM {
@@ -2048,6 +2121,224 @@ struct DGM {
 
 template <class G, bool W3 = false, bool ALT = false>
 __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
+                                                       const float* __restrict__ flat, long w_off, int chunk,
+                                                       const int* __restrict__ act_idx,
+                                                       const int* __restrict__ act_cnt, int layer, int L, int M, int P,
+                                                       int E, int T, long bits_rows, float g_scale,
+                                                       float* __restrict__ dX, int samples_per_wg,
+                                                       const float* __restrict__ gamax, float* __restrict__ gamax_out,
+                                                       int presplit) {
+  using D = DGM<G>;
+  constexpr int S = D::S;
+  constexpr int NTAPP = (D::NTAP + 3) & ~3;
+  constexpr int GPL = (G::HOWO + 1) * X3_DG_PSTR;
+  constexpr int BPL = D::NTAP * D::NT * 16 * 32;
+  __shared__ __attribute__((aligned(16))) bf16_t Gs[2][GPL];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[W3 ? 3 : 2][BPL];
+  __shared__ int mods[X3_MAXM];
+  __shared__ __attribute__((aligned(16))) uint16_t atap[D::NRT * 16 * NTAPP];
+  __shared__ __attribute__((aligned(8))) uint16_t etab[D::NRT * 16];
+  const int p = blockIdx.y;
+  const int cnt = act_cnt[p * L + layer];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int grp = l >> 4, c16 = l & 15;
+  const int PE = P * E;
+  const int nsamp = T * E;
+  // a path of more than 4 active slots runs a pass per group of 4: with gridDim.z = 2 its workgroup's samples are
+  // split over blockIdx.z (the z = 1 half dispatched after every z = 0 workgroup, so a path of <= 4 slots leaves no
+  // empty workgroups among the first round); a sample's dX is computed by one workgroup in group order whatever the
+  // split (bit-identical)
+  const int ngroup = cnt > 4 ? (cnt + 3) >> 2 : 1;
+  const int nsplit = ngroup > 1 ? (int)gridDim.z : 1;
+  if ((int)blockIdx.z >= nsplit) return;
+  const int c_beg = blockIdx.x * samples_per_wg;
+  const int c_end = min(nsamp, c_beg + samples_per_wg);
+  const int spw = (samples_per_wg + nsplit - 1) / nsplit;
+  const int s_beg = c_beg + (int)blockIdx.z * spw;
+  const int s_end = min(c_end, s_beg + spw);
+  if (s_beg >= s_end) return;
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  __syncthreads();
+  // B[k][n] of slot group g: k = (tap, slot a4, c), n = (ph*S + pw)*8 + ci  ->  W_a[kh][kw][ci][c], hi/lo
+  auto stage_b = [&](int g) {
+    for (int it = tid; it < D::NTAP * D::NT * 16 * 4; it += 256) {
+      const int a4 = it & 3, rest = it >> 2;
+      const int n = rest % (D::NT * 16), tap = rest / (D::NT * 16);
+      const int a = 4 * g + a4;
+      const int ta = tap / D::NA, tb = tap - ta * D::NA;
+      const int cls = n >> 3, ci = n & 7, ph = cls / S, pw = cls - ph * S;
+      const int kh = ph + S * ta, kw = pw + S * tb;
+      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (n < D::NN && a < cnt && kh < G::KH && kw < G::KW) {
+        const float* wp = flat + w_off + (long)mods[a] * chunk + ((kh * G::KW + kw) * 8 + ci) * 8;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = wp[c];
+      }
+      s8v hi, lo;
+      // fp16 pair of W * 2^8 (G16); ALT: odd taps' weights staged negated (the second accumulator chain)
+      split8hs(v, (ALT && (tap & 1)) ? -(float)(1 << X3_W0_SHIFT) : (float)(1 << X3_W0_SHIFT), hi, lo);
+      const int o = (tap * D::NT * 16 + n) * 32 + (a4 ^ dg_swz(n)) * 8;
+      *reinterpret_cast<s8v*>(Bs[0] + o) = hi;
+      *reinterpret_cast<s8v*>(Bs[1] + o) = lo;
+      if constexpr (W3) {                                   // third piece: W * 2^8 - hi - lo
+        const h8v hh = __builtin_bit_cast(h8v, hi), ll = __builtin_bit_cast(h8v, lo);
+        _Float16 r[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) r[c] = (_Float16)(v[c] * (float)(1 << X3_W0_SHIFT) - (float)hh[c] - (float)ll[c]);
+        *reinterpret_cast<s8v*>(Bs[2] + o) = __builtin_bit_cast(s8v, r);
+      }
+    }
+  };
+  constexpr int GIT = (G::HOWO + 255) / 256;
+  float4 g0r[GIT], g1r[GIT];
+  uint8_t gbr[GIT][4];
+  // the output gradient of sample s and the ReLU bits of slot group g
+  auto load_sample = [&](int s, int g) {
+    const long sg = sample_global(p, s, E, PE, 0);
+#pragma unroll
+    for (int j = 0; j < GIT; ++j) {
+      const int pos = tid + 256 * j;
+      if (pos < G::HOWO) {
+        const long go = sg * G::HOWO + pos;
+        g0r[j] = *reinterpret_cast<const float4*>(Gr + go * 8);
+        g1r[j] = *reinterpret_cast<const float4*>(Gr + go * 8 + 4);
+#pragma unroll
+        for (int a4 = 0; a4 < 4; ++a4) {
+          const int a = 4 * g + a4;
+          gbr[j][a4] = a < cnt ? bits[(long)a * bits_rows + go] : (uint8_t)0;
+        }
+      }
+    }
+  };
+  static_assert(S <= 2, "dgrad class limits are packed for strides 1 and 2");
+  static_assert((G::HOWO + 1) * X3_DG_PSTR < (1 << 16), "atap offset field");
+  static_assert((S * (D::NI - 1) * G::WIN + S * (D::NJ - 1)) * 8 < (1 << 14), "etab offset field");
+  for (int sp = tid; sp < D::NRT * 16; sp += 256) {
+    const int ii = sp / D::NJ, jj = sp - ii * D::NJ;
+#pragma unroll
+    for (int tap = 0; tap < NTAPP; ++tap) {
+      const int ta = tap / D::NA, tb = tap - ta * D::NA;
+      const int oh = ii - ta, ow = jj - tb;
+      const bool ok = tap < D::NTAP && sp < D::NSP && oh >= 0 && oh < G::HO && ow >= 0 && ow < G::WO;
+      const int apos = ok ? oh * G::WO + ow : G::HOWO;
+      atap[sp * NTAPP + tap] = (uint16_t)(apos * X3_DG_PSTR + (dg_swz(apos) << 3));
+    }
+    etab[sp] = sp < D::NSP ? (uint16_t)((S * ii * G::WIN + S * jj) * 8 | ((S * ii + 1 < G::HIN) << 14) |
+                                        ((S * jj + 1 < G::WIN) << 15))
+                           : (uint16_t)0xFFFF;
+  }
+  for (int i = tid; i < 2 * X3_DG_PSTR; i += 256) Gs[i / X3_DG_PSTR][G::HOWO * X3_DG_PSTR + (i % X3_DG_PSTR)] = 0;
+  int nofs[D::NT], nph[D::NT], npw[D::NT];
+#pragma unroll
+  for (int nt = 0; nt < D::NT; ++nt) {
+    const int n = nt * 16 + c16;
+    const int cls = n >> 3, ci = n & 7;
+    nph[nt] = n < D::NN ? cls / S : 9;
+    npw[nt] = cls - (cls / S) * S;
+    nofs[nt] = ((cls / S) * G::WIN + npw[nt]) * 8 + ci;
+  }
+  const float gs = g16_scale(gamax), inv = 1.0f / (gs * (float)(1 << X3_W0_SHIFT));
+  float am = 0.f;
+  // slot groups outermost: each group's weights are staged ONCE per workgroup (they were restaged per sample when
+  // the group loop ran inside the sample loop); group g > 0 adds into the dX its own threads wrote for group g - 1
+  for (int g = 0; g < ngroup; ++g) {
+    if (g > 0) __syncthreads();                    // the previous group's LDS reads done
+    stage_b(g);
+    load_sample(s_beg, g);
+    for (int s = s_beg; s < s_end; ++s) {
+      const long sg = sample_global(p, s, E, PE, 0);
+      float* __restrict__ dXs = dX + sg * (long)(G::HIN * G::WIN * 8);
+      __syncthreads();                             // previous LDS reads done; B staged
+#pragma unroll
+      for (int j = 0; j < GIT; ++j) {
+        const int pos = tid + 256 * j;
+        if (pos < G::HOWO) {
+          const float gg[8] = {g0r[j].x * g_scale, g0r[j].y * g_scale, g0r[j].z * g_scale, g0r[j].w * g_scale,
+                               g1r[j].x * g_scale, g1r[j].y * g_scale, g1r[j].z * g_scale, g1r[j].w * g_scale};
+          // presplit: the fp16 pair of G * 2^e once per position, masked per slot (bit-identical to masking the fp32
+          // values and splitting per slot, at a quarter of the conversions)
+          s8v ph, pl;
+          if (presplit) split8hs(gg, gs, ph, pl);
+#pragma unroll
+          for (int a4 = 0; a4 < 4; ++a4) {
+            const int b = (int)gbr[j][a4];
+            s8v hi, lo;
+            if (presplit) {
+              mask_pair8(ph, pl, (uint32_t)b, hi, lo);
+            } else {
+              float m[8];
+              mask8(gg, (uint32_t)b, m);
+              split8hs(m, gs, hi, lo);
+            }
+            const int o = pos * X3_DG_PSTR + (a4 ^ dg_swz(pos)) * 8;
+            *reinterpret_cast<s8v*>(Gs[0] + o) = hi;
+            *reinterpret_cast<s8v*>(Gs[1] + o) = lo;
+          }
+        }
+      }
+      __syncthreads();
+      if (s + 1 < s_end) load_sample(s + 1, g);
+      for (int rt = w; rt < D::NRT; rt += 4) {
+        const uint16_t* tp = atap + (rt * 16 + c16) * NTAPP;
+        f4v acc[D::NT], accn[ALT ? D::NT : 1];
+#pragma unroll
+        for (int nt = 0; nt < D::NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (ALT) {
+#pragma unroll
+          for (int nt = 0; nt < D::NT; ++nt) accn[nt] = {0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int tap = 0; tap < D::NTAP; ++tap) {
+          const int ao = (int)tp[tap] ^ (grp << 3);
+          const s8v ah = *reinterpret_cast<const s8v*>(Gs[0] + ao);
+          const s8v al = *reinterpret_cast<const s8v*>(Gs[1] + ao);
+          // ALT: odd taps (negated weights in LDS) into a second chain, subtracted at the end (the f16 MFMA's -inf
+          // rounding bias enters with alternating signs; fc_dgrad_gemm_x3 FOLD 2)
+          const bool neg = ALT && (tap & 1);
+          const int bo = (tap * D::NT * 16 + c16) * 32 + (grp ^ dg_swz(c16)) * 8;
+#pragma unroll
+          for (int nt = 0; nt < D::NT; ++nt) {
+            const s8v bh = *reinterpret_cast<const s8v*>(Bs[0] + bo + nt * 16 * 32);
+            const s8v bl = *reinterpret_cast<const s8v*>(Bs[1] + bo + nt * 16 * 32);
+            if (neg) {
+              accn[nt] = mma3h(ah, al, bh, bl, accn[nt]);
+            } else {
+              if constexpr (W3) acc[nt] = mfma16_f16(ah, *reinterpret_cast<const s8v*>(Bs[2] + bo + nt * 16 * 32), acc[nt]);
+              acc[nt] = mma3h(ah, al, bh, bl, acc[nt]);
+            }
+          }
+        }
+        if constexpr (ALT) {
+#pragma unroll
+          for (int nt = 0; nt < D::NT; ++nt) acc[nt] -= accn[nt];
+        }
+        const uint2 e4 = *reinterpret_cast<const uint2*>(etab + rt * 16 + 4 * grp);
+        const uint32_t ev[4] = {e4.x & 0xFFFFu, e4.x >> 16, e4.y & 0xFFFFu, e4.y >> 16};
+#pragma unroll
+        for (int nt = 0; nt < D::NT; ++nt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t v = ev[r];
+            const bool okh = nph[nt] == 0 || (nph[nt] == 1 && ((v >> 14) & 1u));
+            const bool okw = npw[nt] == 0 || ((v >> 15) & 1u);
+            if (v != 0xFFFFu && okh && okw) {
+              float* o = dXs + (int)(v & 0x3FFFu) + nofs[nt];
+              const float y = g == 0 ? acc[nt][r] * inv : *o + acc[nt][r] * inv;
+              *o = y;
+              if (g == ngroup - 1) am = fmaxf(am, fabsf(y));
+            }
+          }
+        }
+      }
+    }
+  }
+  g16_flush_amax(am, gamax_out);
+}
+
+// the round-6 form of conv_dgrad_x3 (slot groups inside the sample loop, one chunk per workgroup): kept for the
+// interleaved A/B of the restructured kernel (X3_DG_V0 = 1)
+template <class G, bool W3 = false, bool ALT = false>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_x3v0(const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
                                                        const float* __restrict__ flat, long w_off, int chunk,
                                                        const int* __restrict__ act_idx,
                                                        const int* __restrict__ act_cnt, int layer, int L, int M, int P,
@@ -3943,6 +4234,7 @@ static int X3_C1_F16B = 1;     // band forward: 1 = the band converted to fp16 o
                                // interleaved A/B: 64 paths 97.1 -> 95.8 us, 8 paths 20.9 -> 20.4)
 static int X3_C1_SB1 = 0;      // band forward (ring): 1 = one band buffer, three workgroups per CU (conv1_fwd_band_x2 SB1)
 static int X3_C1_PIPE = 0;     // band forward: 1 = next k-step's LDS fragments read during this k-step's MFMAs
+static int X3_C1_BAL = 1;      // ring band forward: cost-balanced 1-D schedule (conv1_fwd_band_x2 BAL)
 static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
 // input gradients (conv_dgrad_x3, fc_dgrad_gemm_x3): 1 = the weights as THREE fp16 pieces (a fourth MFMA per k-step),
 // exact for fp32 weights: the pair's 2^-23 weight rounding is the same for every row, so it enters a layer's input
@@ -3975,6 +4267,9 @@ static int X3_SLAB_PMAP = 1;
 // staged output gradients: 1 = one fp16-pair split per value, masked per slot (mask_pair8); 0 = mask, then split per slot
 static int X3_PRESPLIT = 1;
 static int X3_FH_D = 3;        // fused last fc + heads: k-steps of fragments in flight (fc_heads_fwd_x3 D)
+static int X3_DG_V0 = 0;         // 1 = conv_dgrad_x3v0 (A/B only)
+static int X3_DG_GSPLIT = X3_DG_SPLIT;   // conv_dgrad_x3 grid split (1 = one chunk per workgroup, no balancing)
+static int X3_DG_CAP = 1;          // conv_dgrad_x3: cap at 2 workgroups per CU (dynamic LDS)
 static int X3_DG_TARGET = 512;     // 4x4/s2 input gradient (2048 -> 1536 -> 512: 8 paths 224 -> 214 -> 191 -> 167 us with
                                    // the conv2 weight gradient)
 // module-major fc forward k split: 0 = auto by rows (P*T*E <= 768: 4 parts, else 3), else the fixed part count (2 / 3 / 4 /
@@ -3982,6 +4277,20 @@ static int X3_DG_TARGET = 512;     // 4x4/s2 input gradient (2048 -> 1536 -> 512
 static int X3_FC_KS_PARTS = 0;
 static int X3_FCW_KT = 256;     // fc weight gradient from Gm: k tile 256 (Gm re-read 6x at K = 1408) or 128 (11x)
 static int X3_FC_DG_GEMM = 1;  // fc input gradient: 1 = fc_gm_x3 + per-path GEMM (fc_dgrad_gemm_x3), 0 = fc_dgrad_x3    // 3x3/s1 weight gradient: 1 = per-sample LDS tile (conv_wgrad_tile_x3), 0 = im2col rows
+
+// dynamic LDS that caps kernel KERN at CAP resident workgroups per CU.  The latency-bound backward kernels' grids are
+// whole rounds of a given occupancy (X3_DG_TARGET: 512 = 2 per CU); a build whose VGPR count lets a third workgroup
+// fit leaves a third of the CUs idle (conv_dgrad_x3 at 168 VGPRs: 580 -> 955 us in the 4x4 layer)
+template <auto KERN, int CAP>
+static size_t lds_cap_pad() {
+  static const size_t pad = [] {
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(KERN)) != hipSuccess) return (size_t)0;
+    const long need = 160L * 1024 / (CAP + 1) + 1;
+    return need > (long)a.sharedSizeBytes ? (size_t)(need - (long)a.sharedSizeBytes) : (size_t)0;
+  }();
+  return pad;
+}
 
 // the fixed-point weight-gradient accumulator of the backward being launched (deterministic mode), else nullptr:
 // set by x3_set_fx around one backward's launches (one host thread, as graph capture is), read by the launchers
@@ -4016,8 +4325,12 @@ void fast_conv_set_x3_fc_dg_gemm(int v) { X3_FC_DG_GEMM = v; }
 void fast_conv_set_x3_fcw_kt(int v) { X3_FCW_KT = v == 128 ? 128 : 256; }
 void fast_conv_set_x3_dg_w3(int v) { X3_DG_W3 = v; }
 void fast_conv_set_x3_dg_fold(int v) { X3_DG_FOLD = v; }
+void fast_conv_set_x3_dg_v0(int v) { X3_DG_V0 = v; }
+void fast_conv_set_x3_dg_gsplit(int v) { X3_DG_GSPLIT = v == 1 ? 1 : X3_DG_SPLIT; }
+void fast_conv_set_x3_dg_cap(int v) { X3_DG_CAP = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
 void fast_conv_set_x3_c1_band(int v) { X3_C1_BAND = v; }
+void fast_conv_set_x3_c1_bal(int v) { X3_C1_BAL = v; }
 void fast_conv_set_x3_c1_sb1(int v) { X3_C1_SB1 = v; }
 void fast_conv_set_x3_c1_pipe(int v) { X3_C1_PIPE = v; }
 void fast_conv_set_x3_c1_f16b(int v) { X3_C1_F16B = v; }
@@ -4141,7 +4454,11 @@ int x3_conv1_ring_fwd(const void* frames, const void* fc, void* Y, long ylo, voi
   long bpw = (nbands * P + X3_C1F_TARGET - 1) / X3_C1F_TARGET;
   if (bpw < X3_C1F_MINB) bpw = X3_C1F_MINB;
   if (bpw > (X3_C1_FWD_FCS - 2) * BD1<C1>::NB) bpw = (X3_C1_FWD_FCS - 2) * BD1<C1>::NB;   // staged fc bytes
-  if (X3_C1_SB1)
+  if (X3_C1_BAL && X3_C1_F16B && !X3_C1_SB1)         // the same workgroup count, cost-balanced over the population
+    conv1_fwd_band_x2<C1, true, false, true, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw) * P), 256, 0, st>>>(
+        (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
+        ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots, rbase);
+  else if (X3_C1_SB1)
     conv1_fwd_band_x2<C1, true, false, false, true><<<dim3((unsigned)((nbands + bpw - 1) / bpw), P), 256, 0, st>>>(
         (const uint8_t*)frames, (uint16_t*)Y, ylo, (uint8_t*)bits, (const uint16_t*)Wc, wlo, flat, bias_off, chunk, ai,
         ac, 0, L, M, P, E, T, t0, br, (int)bpw, isc, os, (const uint8_t*)fc, nslots, rbase);
@@ -4281,7 +4598,7 @@ int x3_conv_wgrad(const void* X, long xlo, int u8in, const float* Gr, const void
     const long nsamp = (long)T * E;
     long spw = (nsamp * P + X3_WG3_TARGET - 1) / X3_WG3_TARGET;   // ~X3_WG3_TARGET workgroups over the launch
     if (spw < 4) spw = 4;
-    conv_wgrad_tile_x3<C3><<<dim3((unsigned)((nsamp + spw - 1) / spw), P), WT3<C3>::NT, 0, st>>>(
+    conv_wgrad_tile_x3<C3><<<dim3((unsigned)((nsamp + spw - 1) / spw), P, 2), WT3<C3>::NT, 0, st>>>(
         (const uint16_t*)X, xlo, Gr, (const uint8_t*)bits, grad, w_off, b_off, chunk, ai, ac, layer, L, M, P, E, T, br,
         (int)spw, is, gs, gamax, g_fx_accum);
     const int rc = (int)hipGetLastError();
@@ -4314,18 +4631,33 @@ int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_o
   const long dgt = x3_is<C2>(Hin, Win, Cin, KH, KW, S, 0) ? X3_DG_TARGET : X3_DG3_TARGET;
   int spw = dgt > 0 ? (int)(((long)nsamp * P + dgt - 1) / dgt) : (nsamp + 31) / 32;
   if (spw < 2) spw = 2;
-  const dim3 grid((unsigned)((nsamp + spw - 1) / spw), P);
+  const dim3 grid((unsigned)((nsamp + spw - 1) / spw), P, X3_DG_GSPLIT);
 #define DGX(Gx)                                                                                                    \
   if (x3_is<Gx>(Hin, Win, Cin, KH, KW, S, 0)) {                                                                    \
-    if (X3_DG_FOLD == 2)                                                                                           \
-      conv_dgrad_x3<Gx, false, true><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac,     \
-                                                           layer, L, M, P, E, T, br, gs, dX, spw, gamax, gamax_out, X3_PRESPLIT); \
-    else if (X3_DG_W3)                                                                                             \
-      conv_dgrad_x3<Gx, true><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, \
-                                                    M, P, E, T, br, gs, dX, spw, gamax, gamax_out, X3_PRESPLIT);    \
-    else                                                                                                           \
-      conv_dgrad_x3<Gx><<<grid, 256, 0, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P,  \
-                                              E, T, br, gs, dX, spw, gamax, gamax_out, X3_PRESPLIT);               \
+    if (X3_DG_V0) {                                                                                                \
+      if (X3_DG_FOLD == 2)                                                                                         \
+        conv_dgrad_x3v0<Gx, false, true><<<dim3(grid.x, P), 256, 0, st>>>(                          \
+            Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs, dX, spw, gamax,      \
+            gamax_out, X3_PRESPLIT);                                                                               \
+      else                                                                                                         \
+        conv_dgrad_x3v0<Gx><<<dim3(grid.x, P), 256, 0, st>>>(                                       \
+            Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs, dX, spw, gamax,      \
+            gamax_out, X3_PRESPLIT);                                                                               \
+    } else if (X3_DG_FOLD == 2) {                                                                                  \
+      const size_t pad = X3_DG_CAP ? lds_cap_pad<conv_dgrad_x3<Gx, false, true>, 2>() : 0;                        \
+      conv_dgrad_x3<Gx, false, true><<<grid, 256, pad, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac,  \
+                                                             layer, L, M, P, E, T, br, gs, dX, spw, gamax,          \
+                                                             gamax_out, X3_PRESPLIT);                               \
+    } else if (X3_DG_W3) {                                                                                         \
+      const size_t pad = X3_DG_CAP ? lds_cap_pad<conv_dgrad_x3<Gx, true, false>, 2>() : 0;                        \
+      conv_dgrad_x3<Gx, true><<<grid, 256, pad, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, \
+                                                      L, M, P, E, T, br, gs, dX, spw, gamax, gamax_out,              \
+                                                      X3_PRESPLIT);                                                 \
+    } else {                                                                                                       \
+      const size_t pad = X3_DG_CAP ? lds_cap_pad<conv_dgrad_x3<Gx, false, false>, 2>() : 0;                       \
+      conv_dgrad_x3<Gx><<<grid, 256, pad, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M,  \
+                                                P, E, T, br, gs, dX, spw, gamax, gamax_out, X3_PRESPLIT);            \
+    }                                                                                                              \
     const int rc = (int)hipGetLastError();                                                                         \
     return rc ? -rc : 1;                                                                                           \
   }

@@ -26,16 +26,19 @@ def main():
     ap.add_argument("--opt", action="append", default=[],
                     help="one arm: name=value[,name=value...] (fast_conv_set_<name>); give every varied name in every arm")
     ap.add_argument("--paths", type=int, default=64)
+    ap.add_argument("--preset", default="pong", help="pong, or reference (L=4 + LSTM: its population has paths of 5 "
+                                                     "active modules in a layer)")
+    ap.add_argument("--updates", type=int, default=2, help="updates before timing")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=6)
     a = ap.parse_args()
-    cfg = preset("pong")
+    cfg = preset(a.preset)
     cfg.paths, cfg.envs_per_path, cfg.a2c.t_max = a.paths, 32, 20
     cfg.compute_dtype = "fp32x"
     cfg.frame_ring = True
     cfg.ga.backend = "device"
     tr = PathNetTrainer(cfg, device="cuda")
-    for _ in range(2):
+    for _ in range(a.updates):
         tr.update()
     tr.flush()
     torch.cuda.synchronize()
@@ -95,7 +98,10 @@ def main():
             torch.cuda.synchronize()
             times[kv].append(s.elapsed_time(t) / a.reps * 1e3)
     out = {kv: {"median_us": round(statistics.median(v), 1), "all_us": [round(x, 1) for x in v]} for kv, v in times.items()}
-    print(json.dumps({"kernel": a.kernel, "paths": a.paths, "arms": out}))
+    cnt = tr.model.act_cnt.cpu()
+    print(json.dumps({"kernel": a.kernel, "layer": a.layer, "part": a.part, "preset": a.preset, "paths": a.paths,
+                      "active_max_per_layer": cnt.max(0).values.tolist(),
+                      "paths_over_4_per_layer": (cnt > 4).sum(0).tolist(), "arms": out}))
 
 
 if __name__ == "__main__":

@@ -15,6 +15,13 @@
 #   scripts/gpu.sh "continual NAME SECONDS <continual.py args>"
 #   scripts/gpu.sh "supervised NAME SECONDS <cli supervised args>"
 #   scripts/gpu.sh "py SECONDS <python args>"                any python entry point (e.g. a diag script)
+#   scripts/gpu.sh "seeds A B MINUTES"                       two generations-to-solve seeds of the bench config at
+#                                                            once (deterministic fp32x, v2 criterion; "1r" = a repeat
+#                                                            of seed 1 under its own name) -> OUT/solve/v2_seed*.json
+#   scripts/gpu.sh "rccl P [WINDOWS]"                        forced one-rank RCCL vs no group at P paths, interleaved
+#                                                            (nogroup forced nogroup forced), median windows
+#   scripts/gpu.sh "windows N <bench.py args>"               N back-to-back windows with per-window telemetry
+#   scripts/gpu.sh "driver"                                  the driver's one-GPU bench command (bench.py --gpus 1)
 #
 # Env: OUT (default gpurun_out/r4).
 set -o pipefail
@@ -126,12 +133,58 @@ step_py() {
   tail -5 "$OUT/py_$nb.log" | cut -c1-300
 }
 
+step_seeds() {
+  local a=$1 b=$2 min=${3:-17.5}
+  mkdir -p "$OUT/solve"
+  local S="--preset pong --paths 64 --envs 32 --ring --dtype fp32x --ga-backend device --deterministic --report-every 30"
+  local pids=() seed rc=0
+  for seed in $a $b; do
+    $T "$(python3 -c "print(int($min*60+90))")" python -u scripts/solve.py --minutes "$min" $S --seed "${seed%r}" \
+        --curve "$OUT/solve/v2_seed$seed.jsonl" --out "$OUT/solve/v2_seed$seed.json" > "$OUT/solve/v2_seed$seed.log" 2>&1 &
+    pids+=($!)
+  done
+  for p in "${pids[@]}"; do wait "$p" || rc=$?; done
+  for seed in $a $b; do
+    tail -1 "$OUT/solve/v2_seed$seed.json" 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('seed $seed', d['stopped'], d['generations_to_solve'], d['updates_to_solve'], d.get('heldout_mean'), d['wall_s'])" \
+      || echo "seed $seed: no record"
+  done
+  [ $rc -eq 0 ] || fail "seeds $a $b" $rc "$OUT/solve/v2_seed$a.log"
+}
+
+step_rccl() {
+  local p=$1 w=${2:-5} arm
+  for arm in nogroup forced nogroup forced; do
+    nb=$((nb + 1))
+    if [ $arm = forced ]; then export PATHNET_DIST_FORCE=1; else unset PATHNET_DIST_FORCE; fi
+    $T 300 python -u bench.py --paths "$p" --paths-total "$p" --steps 20 --warmup 5 --windows "$w" --solve-seconds 0 \
+        --compare-bf16 0 --per-rank-shapes '' --reference-preset 0 --no-verify-build --no-strong \
+        > "$OUT/rccl_${arm}_p${p}_$nb.log" 2>&1 || fail "rccl $arm $p" $? "$OUT/rccl_${arm}_p${p}_$nb.log"
+    grep '^{' "$OUT/rccl_${arm}_p${p}_$nb.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$arm p$p median', d['ms_per_step'], d['windows_ms_per_step'])"
+  done
+  unset PATHNET_DIST_FORCE
+}
+
+step_windows() {
+  local n=$1; shift
+  nb=$((nb + 1))
+  $T 400 python -u bench.py --steps 20 --warmup 5 --windows "$n" --solve-seconds 0 --compare-bf16 0 --per-rank-shapes '' \
+      --reference-preset 0 --no-verify-build "$@" > "$OUT/windows_$nb.log" 2>&1 || fail windows $? "$OUT/windows_$nb.log"
+  grep '^{' "$OUT/windows_$nb.log" > "$OUT/windows_$nb.json"
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read()); print('windows', d['ms_per_step'], d['windows_ms_per_step']); [print(' ', t.get('ms'), t.get('sclk_mhz'), t.get('power'), t.get('active_modules_max_per_layer'), (t.get('host_ms_per_update') or {}).get('collect')) for t in d['windows_telemetry']]" "$OUT/windows_$nb.json"
+}
+
+step_driver() {
+  $T 800 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_driver.log" 2>&1 || fail driver $? "$OUT/bench_driver.log"
+  grep '^{' "$OUT/bench_driver.log" > "$OUT/bench_driver.json"
+  python3 scripts/bench_digest.py "$OUT/bench_driver.json"
+}
+
 for s in "$@"; do
   read -r -a words <<< "$s"
   kind=${words[0]}
   echo "== $s"
   case $kind in
-    tests|smoke|bench|kwin|pmc|solve|continual|supervised|py) "step_$kind" "${words[@]:1}" ;;
+    tests|smoke|bench|kwin|pmc|solve|continual|supervised|py|seeds|rccl|windows|driver) "step_$kind" "${words[@]:1}" ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
 done

@@ -7,6 +7,7 @@ and the post-window bookkeeping are excluded, so the table sums to the timed upd
 """
 import csv
 import os
+import statistics
 import sys
 from collections import defaultdict
 
@@ -26,6 +27,7 @@ def main(path, updates, title):
     by_grid = os.environ.get("PROF_BY_GRID") == "1" and gkey is not None
     tot = defaultdict(float)
     calls = defaultdict(int)
+    durs = defaultdict(list)
     for r in rows:
         t = int(r[t0k])
         if lo < t < hi and "prof_window_marker" not in r[key]:
@@ -34,6 +36,7 @@ def main(path, updates, title):
                 name += f" [grid {r[gkey]}]"
             tot[name] += int(r[t1k]) - t
             calls[name] += 1
+            durs[name].append((int(r[t1k]) - t) / 1e3)
     total = sum(tot.values())
     # busy time = union of the window's dispatch intervals: below the summed kernel time when launches of
     # different streams (the split rollout's path groups) overlap
@@ -51,13 +54,30 @@ def main(path, updates, title):
         busy += cur1 - cur0
     out = [f"# {title}", "", f"source: `{path}` (rocprofv3 --kernel-trace); {updates} timed updates between the "
            f"bench.py --prof-window markers; wall between markers {(hi - lo) / 1e6 / updates:.3f} ms per update", "",
-           "| kernel | calls/update | avg us | ms/update | % |", "|---|---:|---:|---:|---:|"]
+           "| kernel | calls/update | avg us | min / median / max us | ms/update | % |",
+           "|---|---:|---:|---:|---:|---:|"]
     for name in sorted(tot, key=lambda n: -tot[n])[:30]:
         out.append(f"| `{name[:70] if not by_grid else name[:50] + name[name.rfind(' ['):]}` | {calls[name] / updates:.1f} | {tot[name] / calls[name] / 1e3:.1f} | "
+                   f"{min(durs[name]):.1f} / {statistics.median(durs[name]):.1f} / {max(durs[name]):.1f} | "
                    f"{tot[name] / 1e6 / updates:.3f} | {100 * tot[name] / total:.1f} |")
-    out.append(f"| **total GPU kernel time** | | | **{total / 1e6 / updates:.2f}** | 100 |")
-    out.append(f"| **GPU busy (union of dispatch intervals)** | | | **{busy / 1e6 / updates:.2f}** | "
+    out.append(f"| **total GPU kernel time** | | | | **{total / 1e6 / updates:.2f}** | 100 |")
+    out.append(f"| **GPU busy (union of dispatch intervals)** | | | | **{busy / 1e6 / updates:.2f}** | "
                f"{100 * busy / max(total, 1):.0f} |")
+    seq = os.environ.get("PROF_SEQ")
+    if seq:
+        # PROF_SEQ=<substring>: the durations of the matching kernel in dispatch order (per-step patterns), with the
+        # kernel that ran just before each call
+        prev, lines = None, []
+        for r in rows:
+            t = int(r[t0k])
+            if not (lo < t < hi) or "prof_window_marker" in r[key]:
+                continue
+            nm = r[key].split("(")[0].replace("void ", "")
+            if seq in nm:
+                lines.append(f"{(int(r[t1k]) - t) / 1e3:.1f} after {prev[:40] if prev else '-'}")
+            prev = nm
+        out.append("")
+        out.append(f"dispatch-order durations (us) of `{seq}`: " + "; ".join(lines[:84]))
     return "\n".join(out) + "\n"
 
 

@@ -430,7 +430,8 @@ def test_x3_conv_forward_swapped_epilogue_matches_rows_as_a(hip_lib, T, arm):
 
 def test_x3_conv3_wgrad_tile_matches_im2col_rows(x3_rollout):
     """conv_wgrad_tile_x3 (one sample per stage: the input tile converted once, im2col^T read straight from it with
-    transposed LDS reads) == conv_wgrad_x3 (32-row im2col stages) up to fp32 summation order, weights and biases."""
+    transposed LDS reads; a path's passes of 4 slots in separate workgroups, blockIdx.z) == conv_wgrad_x3 (32-row
+    im2col stages) up to fp32 summation order, weights and biases; the all-modules path runs 3 passes."""
     from pathnet_gym_amd.ops import _lib
     tr, eng, _, _, g_hip = x3_rollout
     hp = tr.model.hip
@@ -509,6 +510,35 @@ def test_x3_dgrad_presplit_staging_bit_equal(x3_rollout, l):
     lib.fast_conv_set_x3_presplit(1)
     assert torch.isfinite(dxs[0]).all() and dxs[0].norm() > 0
     assert torch.equal(dxs[0], dxs[1])
+
+
+@pytest.mark.parametrize("l", [1, 2])
+def test_x3_dgrad_group_outer_and_split_bit_equal(x3_rollout, l):
+    """conv_dgrad_x3 with the slot groups outermost (each group's weights staged once per workgroup) and the samples of
+    a path of > 4 active slots split over gridDim.z == the round-6 kernel (conv_dgrad_x3v0: groups inside the sample
+    loop, weights restaged per sample): one workgroup computes a sample's dX in group order either way, so the input
+    gradient and its amax are bit-identical.  masks_with_edges has an all-modules path (3 slot groups)."""
+    from pathnet_gym_amd.ops import _lib
+    tr, eng, _, _, _ = x3_rollout
+    hp = tr.model.hip
+    lib = _lib.lib()
+    assert int(tr.model.act_cnt.view(eng.P, -1)[:, l].max()) > 8
+    outs = []
+    for v0, gsplit in ((1, 1), (0, 1), (0, 2)):
+        lib.fast_conv_set_x3_dg_v0(v0)
+        lib.fast_conv_set_x3_dg_gsplit(gsplit)
+        dX = eng.grads[l - 1]
+        dX.fill_(float("nan"))
+        hp.gamax.zero_()
+        hp.layer_bwd(l, eng.acts[l - 1], eng.grads[l], eng.bits[l], torch.zeros_like(eng.grad_flat), dX, eng.P,
+                     eng.E, eng.T, eng.bits_rows[l], part="d")
+        torch.cuda.synchronize()
+        outs.append((dX[:eng.T * eng.B].clone(), hp.gamax.clone()))
+    lib.fast_conv_set_x3_dg_v0(0)                # the defaults
+    lib.fast_conv_set_x3_dg_gsplit(2)
+    assert torch.isfinite(outs[0][0]).all() and outs[0][0].norm() > 0
+    for d, am in outs[1:]:
+        assert torch.equal(d, outs[0][0]) and torch.equal(am, outs[0][1])
 
 
 @pytest.mark.parametrize("l", [3, 4])
@@ -765,11 +795,13 @@ def test_x3_conv1_ring_wgrad_two_tile_passes_match_default(x3_ring_rollout, ncx,
     assert rel(outs[0], g_hip[seg]) < 1e-6
 
 
-@pytest.mark.parametrize("opt", ["f16b", "sb1"])
+@pytest.mark.parametrize("opt", ["f16b", "sb1", "bal"])
 def test_x3_conv1_band_f16_staging_bit_equal(x3_ring_rollout, opt):
     """conv1_fwd_band_x2 F16B (the band converted to fp16 once while staged, X3_C1_F16B, the default) == the
-    double-buffered per-read conversion, and SB1 (one band buffer, three workgroups per CU, X3_C1_SB1) == the
-    default: the same MFMA operands, so outputs and ReLU bits agree bit for bit."""
+    double-buffered per-read conversion, SB1 (one band buffer, three workgroups per CU, X3_C1_SB1) == the
+    default, and BAL (the cost-balanced 1-D schedule whose workgroups span paths, X3_C1_BAL, the default; the
+    all-modules path runs 3 passes) == the per-path grid: the same MFMA operands and pass order per band, so outputs
+    and ReLU bits agree bit for bit."""
     from pathnet_gym_amd.ops import _lib
     tr, eng, _, _, _ = x3_ring_rollout
     hp = tr.model.hip
@@ -785,7 +817,7 @@ def test_x3_conv1_band_f16_staging_bit_equal(x3_ring_rollout, opt):
                         rbase=eng.rbase)
         torch.cuda.synchronize()
         outs.append((eng.acts[0].clone(), eng.bits[0].clone()))
-    setter(1 if opt == "f16b" else 0)           # the defaults
+    setter(1 if opt in ("f16b", "bal") else 0)  # the defaults
     assert outs[0][0].float().abs().sum() > 0
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
