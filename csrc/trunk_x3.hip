@@ -583,6 +583,49 @@ DEVI uint4 planes_to_px4(uint4 v) {
 #ifndef X3_C1_EARLY_BAND
 #define X3_C1_EARLY_BAND 1
 #endif
+// Cost-balanced 1-D schedule over the (path, item) units of P paths x n items, a unit of path p costing
+// cost(act_cnt[p]) (>= 1): called by ONE wave (all 64 lanes), it writes to sched the range of workgroup blockIdx.x of
+// gridDim.x -- from (sched[0], sched[1]) up to, not including, (sched[2], sched[3]) -- the blockIdx.x-th equal share of
+// the population's total cost, rounded down to unit boundaries (consecutive workgroups' ranges tile the units).
+template <class CostF>
+DEVI void bal_schedule(const int* __restrict__ act_cnt, int L, int layer, int P, int n, CostF cost, int* sched) {
+  const int l = threadIdx.x & 63;
+  int tot = 0;
+  for (int pb = 0; pb < P; pb += 64) {
+    int c = pb + l < P ? cost(act_cnt[(pb + l) * L + layer]) : 0;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m, 64);
+    tot += c;
+  }
+  const long U = (long)tot * n;
+  const long ca = U * blockIdx.x / gridDim.x, cb = U * (blockIdx.x + 1) / gridDim.x;
+  long base = 0;
+  for (int pb = 0; pb < P; pb += 64) {
+    const int pp = pb + l;
+    const int np = pp < P ? cost(act_cnt[pp * L + layer]) : 0;
+    int x = np * n;                                    // inclusive scan of the paths' costs in this chunk
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d, 64);
+      if (l >= d) x += y;
+    }
+    const long incl = base + x, excl = incl - (long)np * n;
+    if (np > 0 && ca >= excl && ca < incl) {
+      sched[0] = pp;
+      sched[1] = (int)((ca - excl) / np);
+    }
+    if (np > 0 && cb >= excl && cb < incl) {
+      sched[2] = pp;
+      sched[3] = (int)((cb - excl) / np);
+    }
+    base += __shfl(x, 63, 64);
+  }
+  if (l == 0 && cb >= U) {
+    sched[2] = P - 1;
+    sched[3] = n;
+  }
+}
+
 // BAL: cost-balanced schedule.  A path of 5-6 active modules runs two passes over its bands (NCXT = 2 column tiles per
 // pass), so with one fixed band range per (workgroup, path) its workgroups took twice as long as the others and the
 // launch waited on them (reference preset: 95 -> 162 us per step once the GA grew one path to 5 modules).  With BAL
@@ -627,47 +670,12 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
   // this workgroup's units: (path, band) from (seg_p0, seg_b0) up to, not including, (seg_p1, seg_b1)
   int seg_p0, seg_b0, seg_p1, seg_b1;
   if constexpr (BAL) {
-    if (w == 0) {
-      int tot = 0;
-      for (int pb = 0; pb < P; pb += 64) {
-        int c = pb + l < P ? c1_npass(act_cnt[(pb + l) * L + layer]) : 0;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m, 64);
-        tot += c;
-      }
-      const long U = (long)tot * nbands;
-      const long ca = U * blockIdx.x / gridDim.x, cb = U * (blockIdx.x + 1) / gridDim.x;
-      long base = 0;
-      for (int pb = 0; pb < P; pb += 64) {
-        const int pp = pb + l;
-        const int np = pp < P ? c1_npass(act_cnt[pp * L + layer]) : 0;
-        int x = np * nbands;                               // inclusive scan of the paths' costs in this chunk
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const int y = __shfl_up(x, d, 64);
-          if (l >= d) x += y;
-        }
-        const long incl = base + x, excl = incl - (long)np * nbands;
-        if (np > 0 && ca >= excl && ca < incl) {
-          sched[0] = pp;
-          sched[1] = (int)((ca - excl) / np);
-        }
-        if (np > 0 && cb >= excl && cb < incl) {
-          sched[2] = pp;
-          sched[3] = (int)((cb - excl) / np);
-        }
-        base += __shfl(x, 63, 64);
-      }
-      if (l == 0 && cb >= U) {
-        sched[2] = P - 1;
-        sched[3] = nbands;
-      }
-    }
+    if (w == 0) bal_schedule(act_cnt, L, layer, P, nbands, [](int c) { return c1_npass(c); }, sched);
     __syncthreads();
-    seg_p0 = sched[0];
-    seg_b0 = sched[1];
-    seg_p1 = sched[2];
-    seg_b1 = sched[3];
+    seg_p0 = __builtin_amdgcn_readfirstlane(sched[0]);     // uniform: SGPRs, scalar address math
+    seg_b0 = __builtin_amdgcn_readfirstlane(sched[1]);
+    seg_p1 = __builtin_amdgcn_readfirstlane(sched[2]);
+    seg_b1 = __builtin_amdgcn_readfirstlane(sched[3]);
     if (seg_p0 == seg_p1 && seg_b0 >= seg_b1) return;
   } else {
     seg_p0 = seg_p1 = blockIdx.y;
@@ -2119,7 +2127,11 @@ struct DGM {
   static constexpr int NT = (NN + 15) / 16;
 };
 
-template <class G, bool W3 = false, bool ALT = false>
+// BAL: the cost-balanced 1-D schedule (bal_schedule; a sample of a path costs its slot-group count): a workgroup's
+// samples may span paths, each sample's dX is still computed by one workgroup in group order (bit-identical)
+DEVI int dg_ngroup(int cnt) { return cnt > 4 ? (cnt + 3) >> 2 : 1; }
+
+template <class G, bool W3 = false, bool ALT = false, bool BAL = false>
 __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict__ Gr, const uint8_t* __restrict__ bits,
                                                        const float* __restrict__ flat, long w_off, int chunk,
                                                        const int* __restrict__ act_idx,
@@ -2138,27 +2150,32 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
   __shared__ int mods[X3_MAXM];
   __shared__ __attribute__((aligned(16))) uint16_t atap[D::NRT * 16 * NTAPP];
   __shared__ __attribute__((aligned(8))) uint16_t etab[D::NRT * 16];
-  const int p = blockIdx.y;
-  const int cnt = act_cnt[p * L + layer];
+  __shared__ int sched[4];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15;
   const int PE = P * E;
   const int nsamp = T * E;
-  // a path of more than 4 active slots runs a pass per group of 4: with gridDim.z = 2 its workgroup's samples are
-  // split over blockIdx.z (the z = 1 half dispatched after every z = 0 workgroup, so a path of <= 4 slots leaves no
-  // empty workgroups among the first round); a sample's dX is computed by one workgroup in group order whatever the
-  // split (bit-identical)
-  const int ngroup = cnt > 4 ? (cnt + 3) >> 2 : 1;
-  const int nsplit = ngroup > 1 ? (int)gridDim.z : 1;
-  if ((int)blockIdx.z >= nsplit) return;
-  const int c_beg = blockIdx.x * samples_per_wg;
-  const int c_end = min(nsamp, c_beg + samples_per_wg);
-  const int spw = (samples_per_wg + nsplit - 1) / nsplit;
-  const int s_beg = c_beg + (int)blockIdx.z * spw;
-  const int s_end = min(c_end, s_beg + spw);
-  if (s_beg >= s_end) return;
-  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
-  __syncthreads();
+  // this workgroup's units: (path, sample) from (seg_p0, seg_s0) up to, not including, (seg_p1, seg_s1)
+  int seg_p0, seg_s0, seg_p1, seg_s1;
+  if constexpr (BAL) {
+    // wave 0 computes the schedule while the other waves build the position tables below (read after the barrier)
+    if (w == 0) bal_schedule(act_cnt, L, layer, P, nsamp, [](int c) { return dg_ngroup(c); }, sched);
+    seg_p0 = seg_s0 = seg_p1 = seg_s1 = 0;
+  } else {
+    // a path of more than 4 active slots runs a pass per group of 4: with gridDim.z = 2 its workgroup's samples are
+    // split over blockIdx.z (the z = 1 half dispatched after every z = 0 workgroup, so a path of <= 4 slots leaves no
+    // empty workgroups among the first round)
+    seg_p0 = seg_p1 = blockIdx.y;
+    const int nsplit = dg_ngroup(act_cnt[seg_p0 * L + layer]) > 1 ? (int)gridDim.z : 1;
+    if ((int)blockIdx.z >= nsplit) return;
+    const int c_beg = blockIdx.x * samples_per_wg;
+    const int c_end = min(nsamp, c_beg + samples_per_wg);
+    const int spw = (samples_per_wg + nsplit - 1) / nsplit;
+    seg_s0 = c_beg + (int)blockIdx.z * spw;
+    seg_s1 = min(c_end, seg_s0 + spw);
+    if (seg_s0 >= seg_s1) return;
+  }
+  int p = 0, cnt = 0;
   // B[k][n] of slot group g: k = (tap, slot a4, c), n = (ph*S + pw)*8 + ci  ->  W_a[kh][kw][ci][c], hi/lo
   auto stage_b = [&](int g) {
     for (int it = tid; it < D::NTAP * D::NT * 16 * 4; it += 256) {
@@ -2239,7 +2256,24 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
   }
   const float gs = g16_scale(gamax), inv = 1.0f / (gs * (float)(1 << X3_W0_SHIFT));
   float am = 0.f;
-  // slot groups outermost: each group's weights are staged ONCE per workgroup (they were restaged per sample when
+  if constexpr (BAL) {
+    __syncthreads();                               // the schedule (and the position tables) visible
+    seg_p0 = __builtin_amdgcn_readfirstlane(sched[0]);     // uniform: SGPRs, scalar address math
+    seg_s0 = __builtin_amdgcn_readfirstlane(sched[1]);
+    seg_p1 = __builtin_amdgcn_readfirstlane(sched[2]);
+    seg_s1 = __builtin_amdgcn_readfirstlane(sched[3]);
+    if (seg_p0 == seg_p1 && seg_s0 >= seg_s1) return;
+  }
+  for (int sp = seg_p0; sp <= seg_p1; ++sp) {
+  const int s_beg = sp == seg_p0 ? seg_s0 : 0, s_end = sp == seg_p1 ? seg_s1 : nsamp;
+  if (s_beg >= s_end) continue;
+  p = sp;
+  cnt = act_cnt[p * L + layer];
+  const int ngroup = dg_ngroup(cnt);
+  __syncthreads();                                 // the previous segment's LDS reads (mods, Bs, Gs) done
+  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  __syncthreads();
+  // slot groups outermost: each group's weights are staged ONCE per segment (they were restaged per sample when
   // the group loop ran inside the sample loop); group g > 0 adds into the dX its own threads wrote for group g - 1
   for (int g = 0; g < ngroup; ++g) {
     if (g > 0) __syncthreads();                    // the previous group's LDS reads done
@@ -2331,6 +2365,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_x3(const float* __restrict_
         }
       }
     }
+  }
   }
   g16_flush_amax(am, gamax_out);
 }
@@ -4267,6 +4302,7 @@ static int X3_SLAB_PMAP = 1;
 // staged output gradients: 1 = one fp16-pair split per value, masked per slot (mask_pair8); 0 = mask, then split per slot
 static int X3_PRESPLIT = 1;
 static int X3_FH_D = 3;        // fused last fc + heads: k-steps of fragments in flight (fc_heads_fwd_x3 D)
+static int X3_DG_BAL = 1;         // conv_dgrad_x3: cost-balanced 1-D schedule (BAL)
 static int X3_DG_V0 = 0;         // 1 = conv_dgrad_x3v0 (A/B only)
 static int X3_DG_GSPLIT = X3_DG_SPLIT;   // conv_dgrad_x3 grid split (1 = one chunk per workgroup, no balancing)
 static int X3_DG_CAP = 1;          // conv_dgrad_x3: cap at 2 workgroups per CU (dynamic LDS)
@@ -4326,6 +4362,7 @@ void fast_conv_set_x3_fcw_kt(int v) { X3_FCW_KT = v == 128 ? 128 : 256; }
 void fast_conv_set_x3_dg_w3(int v) { X3_DG_W3 = v; }
 void fast_conv_set_x3_dg_fold(int v) { X3_DG_FOLD = v; }
 void fast_conv_set_x3_dg_v0(int v) { X3_DG_V0 = v; }
+void fast_conv_set_x3_dg_bal(int v) { X3_DG_BAL = v; }
 void fast_conv_set_x3_dg_gsplit(int v) { X3_DG_GSPLIT = v == 1 ? 1 : X3_DG_SPLIT; }
 void fast_conv_set_x3_dg_cap(int v) { X3_DG_CAP = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
@@ -4643,6 +4680,11 @@ int x3_conv_dgrad(const float* Gr, const void* bits, const float* flat, long w_o
         conv_dgrad_x3v0<Gx><<<dim3(grid.x, P), 256, 0, st>>>(                                       \
             Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs, dX, spw, gamax,      \
             gamax_out, X3_PRESPLIT);                                                                               \
+    } else if (X3_DG_FOLD == 2 && X3_DG_BAL) {     /* the same workgroup count, cost-balanced, 1-D */          \
+      const size_t pad = X3_DG_CAP ? lds_cap_pad<conv_dgrad_x3<Gx, false, true, true>, 2>() : 0;                  \
+      conv_dgrad_x3<Gx, false, true, true><<<dim3(grid.x * P), 256, pad, st>>>(                                    \
+          Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac, layer, L, M, P, E, T, br, gs, dX, spw, gamax,        \
+          gamax_out, X3_PRESPLIT);                                                                                 \
     } else if (X3_DG_FOLD == 2) {                                                                                  \
       const size_t pad = X3_DG_CAP ? lds_cap_pad<conv_dgrad_x3<Gx, false, true>, 2>() : 0;                        \
       conv_dgrad_x3<Gx, false, true><<<grid, 256, pad, st>>>(Gr, (const uint8_t*)bits, flat, w_off, chunk, ai, ac,  \

@@ -123,3 +123,39 @@ def test_hip_game_frame_ring_matches_packed_stacks(hip_lib, name):
         ndone += int(d.sum())
     assert ndone > 0
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", GAME_NAMES)
+def test_rasteriser_banded_walk_bit_equal(hip_lib, name):
+    """csrc/preprocess.hip rects_push_kernel: the banded walk (per-band rectangle bit masks, 164-byte rows, dword
+    fills; auto from 160 rectangles) paints the same image as the walk over every rectangle, pushed stacks and ring
+    planes alike."""
+    from pathnet_gym_amd.ops import _lib
+    lib = _lib.lib()
+    N = 64
+    outs = []
+    for mode in (0, 2):
+        lib.rects_set_banded(mode)
+        e = GAMES[name](N, device="cuda", seed=3, backend="hip")
+        e.max_episode_steps = 20
+        e.reset()
+        frames = torch.zeros(N, 4, 160 * 120, dtype=torch.uint8, device="cuda")
+        fc = torch.zeros(2, N, dtype=torch.uint8, device="cuda")
+        rw, dn, eret = (torch.zeros(N, device="cuda"), torch.zeros(N, dtype=torch.uint8, device="cuda"),
+                        torch.zeros(N, device="cuda"))
+        g = torch.Generator().manual_seed(11)
+        seen = []
+        for t in range(30):
+            a = torch.randint(0, e.num_actions, (N,), generator=g).to(device="cuda", dtype=torch.int32)
+            if t % 2:
+                obs, _, _, _ = e.step(a)
+                seen.append(obs)
+            else:
+                e.step_ring_into(a, frames, t % 4, fc[0], fc[1], rw, dn, eret)
+                seen.append(frames.clone())
+        outs.append(seen)
+    lib.rects_set_banded(1)                      # the default (auto)
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    assert any(o.float().std() > 0 for o in outs[0])

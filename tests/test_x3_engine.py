@@ -514,19 +514,21 @@ def test_x3_dgrad_presplit_staging_bit_equal(x3_rollout, l):
 
 @pytest.mark.parametrize("l", [1, 2])
 def test_x3_dgrad_group_outer_and_split_bit_equal(x3_rollout, l):
-    """conv_dgrad_x3 with the slot groups outermost (each group's weights staged once per workgroup) and the samples of
-    a path of > 4 active slots split over gridDim.z == the round-6 kernel (conv_dgrad_x3v0: groups inside the sample
-    loop, weights restaged per sample): one workgroup computes a sample's dX in group order either way, so the input
-    gradient and its amax are bit-identical.  masks_with_edges has an all-modules path (3 slot groups)."""
+    """conv_dgrad_x3 with the slot groups outermost (each group's weights staged once per workgroup), with the samples
+    of a path of > 4 active slots split over gridDim.z, and on the cost-balanced 1-D schedule whose workgroups span
+    paths (BAL, the default) == the round-6 kernel (conv_dgrad_x3v0: groups inside the sample loop, weights restaged
+    per sample): one workgroup computes a sample's dX in group order either way, so the input gradient and its amax
+    are bit-identical.  masks_with_edges has an all-modules path (3 slot groups)."""
     from pathnet_gym_amd.ops import _lib
     tr, eng, _, _, _ = x3_rollout
     hp = tr.model.hip
     lib = _lib.lib()
     assert int(tr.model.act_cnt.view(eng.P, -1)[:, l].max()) > 8
     outs = []
-    for v0, gsplit in ((1, 1), (0, 1), (0, 2)):
+    for v0, gsplit, bal in ((1, 1, 0), (0, 1, 0), (0, 2, 0), (0, 1, 1)):
         lib.fast_conv_set_x3_dg_v0(v0)
         lib.fast_conv_set_x3_dg_gsplit(gsplit)
+        lib.fast_conv_set_x3_dg_bal(bal)
         dX = eng.grads[l - 1]
         dX.fill_(float("nan"))
         hp.gamax.zero_()
@@ -536,6 +538,7 @@ def test_x3_dgrad_group_outer_and_split_bit_equal(x3_rollout, l):
         outs.append((dX[:eng.T * eng.B].clone(), hp.gamax.clone()))
     lib.fast_conv_set_x3_dg_v0(0)                # the defaults
     lib.fast_conv_set_x3_dg_gsplit(2)
+    lib.fast_conv_set_x3_dg_bal(1)
     assert torch.isfinite(outs[0][0]).all() and outs[0][0].norm() > 0
     for d, am in outs[1:]:
         assert torch.equal(d, outs[0][0]) and torch.equal(am, outs[0][1])
