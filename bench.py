@@ -91,6 +91,27 @@ def solve_key(cfg, preset_name: str) -> dict:
             "rmsp_epsilon": cfg.a2c.rmsp_epsilon}
 
 
+def equivalent_builds(sources: str, root: str) -> dict:
+    """Builds whose committed records count for the build ``sources``: itself, and every build linked to it by a
+    reproducing certificate in root/build_equivalence.json (scripts/certify_build.py: a committed deterministic seed
+    re-run on the newer build gave the same generations, updates, frames and held-out mean), transitively.  Returns
+    {sha: certificate or None}."""
+    try:
+        certs = [c for c in json.loads(open(os.path.join(root, "build_equivalence.json")).read())
+                 if c.get("reproduces") and c.get("from") and c.get("to")]
+    except (OSError, ValueError):
+        certs = []
+    out, todo = {sources: None}, [sources]
+    while todo:
+        cur = todo.pop()
+        for c in certs:
+            for a, b in ((c["from"], c["to"]), (c["to"], c["from"])):
+                if a == cur and b not in out:
+                    out[b] = c
+                    todo.append(b)
+    return out
+
+
 def solve_records(key: dict, n_gpus: int, sources: str = None, root: str = None):
     """The committed solve runs (profiles/solve/*.json, written by scripts/solve.py --out) of exactly this config on
     ``n_gpus`` GPUs, under the v2 criterion (algo/solve.py: the task horizon where the lr anneal reaches 0, a held-out
@@ -102,10 +123,13 @@ def solve_records(key: dict, n_gpus: int, sources: str = None, root: str = None)
     from pathnet_gym_amd.algo.solve import CRITERION
     root = root or os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "solve")
     by_seed, excluded = {}, {"other_config": 0, "pre_v2_criterion": 0, "other_build": 0, "wall_limited": 0}
+    equiv = equivalent_builds(sources, root) if sources is not None else {}
     for f in sorted(glob.glob(os.path.join(root, "*.json"))):
         try:
             d = json.loads(open(f).read().strip().splitlines()[-1])
         except (OSError, ValueError, IndexError):
+            continue
+        if not isinstance(d, dict):                 # build_equivalence.json
             continue
         c = d.get("config") or {}
         if d.get("metric") != "generations_to_solve" or d.get("n_gpus") != n_gpus or not c.get("ga", True) \
@@ -119,7 +143,8 @@ def solve_records(key: dict, n_gpus: int, sources: str = None, root: str = None)
         if d.get("criterion") != CRITERION:
             excluded["pre_v2_criterion"] += 1
             continue
-        if sources is not None and (d.get("build") or {}).get("sources_sha256") != sources:
+        rec_sha = (d.get("build") or {}).get("sources_sha256")
+        if sources is not None and rec_sha not in equiv:
             excluded["other_build"] += 1
             continue
         if not d.get("solved") and d.get("stopped") != "horizon":
@@ -131,7 +156,8 @@ def solve_records(key: dict, n_gpus: int, sources: str = None, root: str = None)
              "heldout_mean": d.get("heldout_mean"), "winner_fitness": d.get("winner_fitness"),
              "unconfirmed_candidates": sum(1 for x in d.get("candidates", []) if not x.get("confirmed")),
              "stopped": d.get("stopped"), "deterministic": bool(c.get("deterministic")),
-             "finished_at": d.get("finished_at", 0.0), "file": os.path.relpath(f, os.path.dirname(root))}
+             "finished_at": d.get("finished_at", 0.0), "file": os.path.relpath(f, os.path.dirname(root)),
+             "build": rec_sha}
         old = by_seed.get(r["seed"])
         if old is None or r["finished_at"] >= old["finished_at"]:
             by_seed[r["seed"]] = r
@@ -151,6 +177,7 @@ def solve_records(key: dict, n_gpus: int, sources: str = None, root: str = None)
             "updates_median": None if statistics.median(upd) == inf else statistics.median(upd),
             "solved_seeds": len(solved), "seeds": len(runs), "runs": runs, "config": key, "excluded": excluded,
             "build_sources_sha256": sources,
+            "equivalent_builds": {k: (v or {}).get("committed_file") for k, v in equiv.items() if k != sources},
             "criterion": CRITERION}
 
 

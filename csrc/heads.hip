@@ -219,6 +219,16 @@ static bool heads_fwd_lanes_launch(const void* feat, int F, const float* flat, l
       return true;
     }
   }
+  // the 18-way head (the reference's ACTION_SIZEZ, the LSTM preset): 16 samples per workgroup as well (the 64-sample
+  // kernel below ran 25 us per step at 2048 samples, 32 workgroups)
+  if (HEADS_S16 && F % 128 == 0 && A <= 18) {
+    const size_t sm = (size_t)(F * 19 + 16 * 19 * 16) * 4;
+    if (sm <= 64 * 1024) {
+      heads_fwd_s16_kernel<18, FT><<<(unsigned)((B - b0 + 15) / 16), 256, sm, stream>>>(
+          (const FT*)feat, F, flat, pw, pb, vw, vb, A, B, logits, value, actions, seed, ctr, t, T, greedy, b0, rb);
+      return true;
+    }
+  }
   const unsigned g = (unsigned)((B - b0 + 63) / 64);
   if (A <= 8) {
     const size_t sm = (size_t)(F * 9 + 3 * 9 * 64) * 4;

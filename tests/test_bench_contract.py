@@ -112,3 +112,16 @@ def test_solve_records_v2_one_per_seed_same_build(tmp_path):
     assert r["value"] == 300 and r["min"] == 200 and r["max"] == "unsolved"
     assert r["excluded"] == {"other_config": 0, "pre_v2_criterion": 1, "other_build": 1, "wall_limited": 1}
     assert bench.committed_updates_to_solve.__code__.co_argcount == 2
+    # a reproducing certificate (scripts/certify_build.py) links build bbbb to build aaaa: seed 4 now counts for
+    # either build; a certificate that did not reproduce links nothing
+    (tmp_path / "build_equivalence.json").write_text(json.dumps([
+        {"from": "aaaa", "to": "cccc", "reproduces": True, "committed_file": "x"},
+        {"from": "cccc", "to": "bbbb", "reproduces": True, "committed_file": "y"},
+        {"from": "aaaa", "to": "dddd", "reproduces": False}]))
+    rec("h.json", 7, True, 70, 1.0, src="dddd")
+    for src in ("aaaa", "bbbb"):
+        r = bench.solve_records(key, 1, src, root=str(tmp_path))
+        assert [x["seed"] for x in r["runs"]] == [1, 2, 3, 4], src
+        assert set(r["equivalent_builds"]) == {"aaaa", "bbbb", "cccc"} - {src}
+        assert r["excluded"]["other_build"] == 1              # dddd's record
+    assert bench.equivalent_builds("dddd", str(tmp_path)) == {"dddd": None}
