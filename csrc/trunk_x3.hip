@@ -587,9 +587,56 @@ DEVI uint4 planes_to_px4(uint4 v) {
 // cost(act_cnt[p]) (>= 1): called by ONE wave (all 64 lanes), it writes to sched the range of workgroup blockIdx.x of
 // gridDim.x -- from (sched[0], sched[1]) up to, not including, (sched[2], sched[3]) -- the blockIdx.x-th equal share of
 // the population's total cost, rounded down to unit boundaries (consecutive workgroups' ranges tile the units).
+// mods_out (optional): the first segment's path's active-module list is loaded into it and its count written to
+// sched[4] (-1: not prefetched), so the kernel's first segment skips two dependent global loads.
 template <class CostF>
-DEVI void bal_schedule(const int* __restrict__ act_cnt, int L, int layer, int P, int n, CostF cost, int* sched) {
+DEVI void bal_schedule(const int* __restrict__ act_cnt, int L, int layer, int P, int n, CostF cost, int* sched,
+                       const int* __restrict__ act_idx = nullptr, int M = 0, int* mods_out = nullptr) {
   const int l = threadIdx.x & 63;
+  if (mods_out && l == 0) sched[4] = -1;
+  if (P <= 64) {
+    // one chunk (every population of <= 64 paths per GPU): one act_cnt load per lane, one scan, 32-bit arithmetic
+    // while the cost bound fits (the schedule is a serial prologue: at 8 paths a launch lasts ~20 us)
+    const int craw = l < P ? act_cnt[l * L + layer] : 0;
+    const int np = l < P ? cost(craw) : 0;
+    int x = np * n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d, 64);
+      if (l >= d) x += y;
+    }
+    const int U = __shfl(x, 63, 64), excl = x - np * n;
+    int ca, cb;
+    if ((long)U * gridDim.x < (1L << 31)) {
+      ca = (int)((unsigned)U * blockIdx.x / gridDim.x);
+      cb = (int)((unsigned)U * (blockIdx.x + 1) / gridDim.x);
+    } else {
+      ca = (int)((long)U * blockIdx.x / gridDim.x);
+      cb = (int)((long)U * (blockIdx.x + 1) / gridDim.x);
+    }
+    if (np > 0 && ca >= excl && ca < x) {
+      sched[0] = l;
+      sched[1] = (ca - excl) / np;
+    }
+    if (np > 0 && cb >= excl && cb < x) {
+      sched[2] = l;
+      sched[3] = (cb - excl) / np;
+    }
+    if (l == 0 && cb >= U) {
+      sched[2] = P - 1;
+      sched[3] = n;
+    }
+    if (mods_out) {
+      const unsigned long long hit = __ballot(np > 0 && ca >= excl && ca < x);
+      if (hit) {
+        const int src = __ffsll((long long)hit) - 1;
+        const int p0 = __shfl(l, src, 64), c0 = __shfl(craw, src, 64);
+        if (l < X3_MAXM) mods_out[l] = l < c0 ? act_idx[(p0 * L + layer) * M + l] : 0;
+        if (l == 0) sched[4] = c0;
+      }
+    }
+    return;
+  }
   int tot = 0;
   for (int pb = 0; pb < P; pb += 64) {
     int c = pb + l < P ? cost(act_cnt[(pb + l) * L + layer]) : 0;
@@ -662,20 +709,21 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
   // RING: the first-valid channel of every sample of the workgroup's bands, staged once.  Read per band from global
   // memory it put a dependent byte load (and a full vmcnt wait) in front of every band's frame loads.
   __shared__ uint8_t fcs[RING ? X3_C1_FWD_FCS : 1];
-  __shared__ int sched[4];
+  __shared__ int sched[5];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int grp = l >> 4, c16 = l & 15, q = grp;
   const int PE = P * E;
   const int nbands = T * E * B::NB;
   // this workgroup's units: (path, band) from (seg_p0, seg_b0) up to, not including, (seg_p1, seg_b1)
-  int seg_p0, seg_b0, seg_p1, seg_b1;
+  int seg_p0, seg_b0, seg_p1, seg_b1, pre_cnt = -1;
   if constexpr (BAL) {
-    if (w == 0) bal_schedule(act_cnt, L, layer, P, nbands, [](int c) { return c1_npass(c); }, sched);
+    if (w == 0) bal_schedule(act_cnt, L, layer, P, nbands, [](int c) { return c1_npass(c); }, sched, act_idx, M, mods);
     __syncthreads();
     seg_p0 = __builtin_amdgcn_readfirstlane(sched[0]);     // uniform: SGPRs, scalar address math
     seg_b0 = __builtin_amdgcn_readfirstlane(sched[1]);
     seg_p1 = __builtin_amdgcn_readfirstlane(sched[2]);
     seg_b1 = __builtin_amdgcn_readfirstlane(sched[3]);
+    pre_cnt = __builtin_amdgcn_readfirstlane(sched[4]);
     if (seg_p0 == seg_p1 && seg_b0 >= seg_b1) return;
   } else {
     seg_p0 = seg_p1 = blockIdx.y;
@@ -761,9 +809,13 @@ __global__ __launch_bounds__(256, SB1 ? 3 : 2) void conv1_fwd_band_x2(const uint
   b_beg = cb;
   b_end = min(ce, cb + MAXB);
   if (sp != seg_p0 || cb != seg_b0) __syncthreads();  // the previous segment's LDS reads (mods, fcs, Ws, Xb) done
-  cnt = act_cnt[p * L + layer];
+  if (BAL && pre_cnt >= 0 && sp == seg_p0 && cb == seg_b0) {
+    cnt = pre_cnt;                                     // mods prefetched by the schedule wave
+  } else {
+    cnt = act_cnt[p * L + layer];
+    if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
+  }
   nct = (cnt + 1) >> 1;
-  if (tid < X3_MAXM) mods[tid] = tid < cnt ? act_idx[(p * L + layer) * M + tid] : 0;
   s_first = b_beg / B::NB;
   if constexpr (RING) {
     const int ns = (b_end - 1) / B::NB - s_first + 1;     // <= X3_C1_FWD_FCS (launcher caps bands_per_wg)
