@@ -450,7 +450,8 @@ def reference_preset_windows(args, ctx) -> dict:
     a.preset = "reference"
     a.env = None
     cfg, trr = build_trainer(a, ctx, args.dtype, False)
-    w = window_summary(timed_windows(trr, ctx, args.steps, args.warmup, args.windows), args.steps)
+    tele = []
+    w = window_summary(timed_windows(trr, ctx, args.steps, args.warmup, args.windows, info=tele), args.steps)
     net = cfg.net
     out = {"preset": "reference", "env": cfg.tasks[0], "dtype": trr.compute_dtype,
            "model": f"PathNet L={net.L} (conv 8x8/4, 4x4/2, 3x3/1 + fc {net.layers[-1].out}) x M={net.M}, N={net.N}, "
@@ -458,7 +459,11 @@ def reference_preset_windows(args, ctx) -> dict:
            "paths_per_gpu": cfg.paths, "envs_per_path": cfg.envs_per_path, "t_max": cfg.a2c.t_max,
            "ms_per_update": round(w["ms"], 3), "windows_ms": w["all"], "spread_pct": w["spread_pct"],
            "frames_per_sec": round(w["frames"] / (w["ms"] * args.steps / 1e3), 1),
-           "frame_ring": bool(getattr(trr.engine, "ring", False)), "lstm_hip": bool(trr.engine.lstm_hip)}
+           "frame_ring": bool(getattr(trr.engine, "ring", False)), "lstm_hip": bool(trr.engine.lstm_hip),
+           # per window: clock, and the population's mean / widest active-module count per layer (a path of more than
+           # 4 modules in the 3x3 layer still lengthens its weight gradient, docs/PERF.md)
+           "windows_telemetry": [{k: t.get(k) for k in ("ms", "sclk_mhz", "active_modules_per_layer",
+                                                        "active_modules_max_per_layer")} for t in tele]}
     del trr
     return out
 
