@@ -1462,9 +1462,17 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
   const int u_beg = blockIdx.x * units_per_wg;
   const int u_end = min(nunits, u_beg + units_per_wg);
   const int s_first = u_beg / SB::NB;
+  // pmap bit 1 (ring, atomic mode): units in env-major order -- sample index e * T + t instead of t * E + e -- so a
+  // workgroup walks one env's consecutive steps and re-reads the 3 frame planes each step shares with the previous
+  // one from L2 (t-major: the next step of an env was another workgroup's, 32 samples on)
+  const bool emaj = RING && (pmap & 2);
+  pmap &= 1;
   if constexpr (RING) {
     const int s_last = min(T * E, (u_end + SB::NB - 1) / SB::NB);
-    for (int i = tid; i < s_last - s_first && i < FCS; i += 256) fcs[i] = fcv[sample_global(p, s_first + i, E, PE, 0)];
+    for (int i = tid; i < s_last - s_first && i < FCS; i += 256) {
+      const int si = s_first + i;
+      fcs[i] = fcv[sample_global(p, emaj ? (si % T) * E + si / T : si, E, PE, 0)];
+    }
   }
   int aoff[SB::KS][2];
 #pragma unroll
@@ -1513,22 +1521,26 @@ __global__ __launch_bounds__(256, NCXP <= 2 ? 3 : 2) void conv_wgrad_slab_x3(con
     {
       const int s0 = u_beg / SB::NB;
       it_band = u_beg - s0 * SB::NB;
-      it_t = s0 / E;
-      it_e = s0 - it_t * E;
+      it_t = emaj ? s0 % T : s0 / E;
+      it_e = emaj ? s0 / T : s0 - it_t * E;
     }
     auto load_stage = [&](Regs& Rg) {
       const int band = it_band, ut = it_t, ue = it_e;
       const long sg = (long)ut * PE + (long)p * E + ue;
       if (++it_band == SB::NB) {
         it_band = 0;
-        if (++it_e == E) { it_e = 0; ++it_t; }
+        if (emaj) {
+          if (++it_t == T) { it_t = 0; ++it_e; }
+        } else {
+          if (++it_e == E) { it_e = 0; ++it_t; }
+        }
       }
       const int ih0 = band * OB * G::S;
       const int navail = min(SB::SR, G::HIN - ih0) * SB::RL;
       Rg.navail = navail;
       if constexpr (RING) {
         constexpr long HW = (long)G::HIN * G::WIN;
-        const int fc = (int)fcs[ut * E + ue - s_first];
+        const int fc = (int)fcs[(emaj ? ue * T + ut : ut * E + ue) - s_first];
         const uint8_t* src = reinterpret_cast<const uint8_t*>(X) + (long)(p * E + ue) * nslots * HW +
                              (long)ih0 * G::WIN;
         const int s0 = rbase + ut;               // modular ring (conv1_fwd_band_x2 ring_src)
@@ -4321,6 +4333,7 @@ static int X3_C1_F16B = 1;     // band forward: 1 = the band converted to fp16 o
                                // interleaved A/B: 64 paths 97.1 -> 95.8 us, 8 paths 20.9 -> 20.4)
 static int X3_C1_SB1 = 0;      // band forward (ring): 1 = one band buffer, three workgroups per CU (conv1_fwd_band_x2 SB1)
 static int X3_C1_PIPE = 0;     // band forward: 1 = next k-step's LDS fragments read during this k-step's MFMAs
+static int X3_C1_EMAJ = 1;     // ring slab weight gradient, atomic mode: env-major unit order
 static int X3_C1_BAL = 1;      // ring band forward: cost-balanced 1-D schedule (conv1_fwd_band_x2 BAL)
 static int X3_C1_BAND = 1;     // first-layer forward: 1 = input band in LDS (conv1_fwd_band_x2), 0 = conv1_fwd_x2    // bf16-activation conv forward: 1 = per-sample LDS tile (conv_fwd_tile_x3), 0 = rows
 // input gradients (conv_dgrad_x3, fc_dgrad_gemm_x3): 1 = the weights as THREE fp16 pieces (a fourth MFMA per k-step),
@@ -4420,6 +4433,7 @@ void fast_conv_set_x3_dg_cap(int v) { X3_DG_CAP = v; }
 void fast_conv_set_x3_fwd_tile(int v) { X3_FWD_TILE = v; }
 void fast_conv_set_x3_c1_band(int v) { X3_C1_BAND = v; }
 void fast_conv_set_x3_c1_bal(int v) { X3_C1_BAL = v; }
+void fast_conv_set_x3_c1_emaj(int v) { X3_C1_EMAJ = v; }
 void fast_conv_set_x3_c1_sb1(int v) { X3_C1_SB1 = v; }
 void fast_conv_set_x3_c1_pipe(int v) { X3_C1_PIPE = v; }
 void fast_conv_set_x3_c1_f16b(int v) { X3_C1_F16B = v; }
@@ -4627,22 +4641,25 @@ int x3_conv1_ring_wgrad(const void* frames, const void* fc, const float* Gr, con
   if (upw < 8) upw = 8;
   if (upw / SB::NB + 2 > X3_RING_FCS) return -22;       // the workgroup's first-valid bytes fit the LDS table
   const dim3 grid((unsigned)((units + upw - 1) / upw), P);
+  // env-major unit order in the atomic mode (the deterministic mode keeps the committed partition of its fixed-point
+  // partial sums, so its runs repeat bit for bit)
+  const int pm = X3_SLAB_PMAP | ((X3_C1_EMAJ && !g_fx_accum) ? 2 : 0);
   if (X3_C1_WG_NCX == 2 && X3_WGRAD_PF != 1)       // 2 tiles per pass: two stages in flight fit (162 VGPRs)
     conv_wgrad_slab_x3<C1, 2, 2, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum, rbase);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax, pm, g_fx_accum, rbase);
   else if (X3_C1_WG_NCX == 2)
     conv_wgrad_slab_x3<C1, 2, 1, true, 2><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off,
                                                                 b_off, chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw,
-                                                                is, gs, (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum, rbase);
+                                                                is, gs, (const uint8_t*)fc, nslots, gamax, pm, g_fx_accum, rbase);
   else if (X3_WGRAD_PF == 2)
     conv_wgrad_slab_x3<C1, 2, 2, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum, rbase);
+                                                             (const uint8_t*)fc, nslots, gamax, pm, g_fx_accum, rbase);
   else
     conv_wgrad_slab_x3<C1, 2, 1, true><<<grid, 256, 0, st>>>(frames, 0, Gr, (const uint8_t*)bits, grad, w_off, b_off,
                                                              chunk, ai, ac, 0, L, M, P, E, T, br, (int)upw, is, gs,
-                                                             (const uint8_t*)fc, nslots, gamax, X3_SLAB_PMAP, g_fx_accum, rbase);
+                                                             (const uint8_t*)fc, nslots, gamax, pm, g_fx_accum, rbase);
   const int rc = (int)hipGetLastError();
   return rc ? -rc : 1;
 }

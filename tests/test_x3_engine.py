@@ -798,6 +798,32 @@ def test_x3_conv1_ring_wgrad_two_tile_passes_match_default(x3_ring_rollout, ncx,
     assert rel(outs[0], g_hip[seg]) < 1e-6
 
 
+def test_x3_conv1_ring_wgrad_env_major_matches_step_major(x3_ring_rollout):
+    """conv_wgrad_slab_x3 on the frame ring with its units in env-major order (X3_C1_EMAJ, the atomic-mode default: a
+    workgroup walks one env's consecutive steps) == the step-major order, weights and biases, up to float-atomic order;
+    the deterministic mode always runs the step-major partition (test_x3_deterministic_*)."""
+    from pathnet_gym_amd.ops import _lib
+    tr, eng, _, _, g_hip = x3_ring_rollout
+    hp = tr.model.hip
+    lib = _lib.lib()
+    g = hp.geoms[0]
+    seg = slice(g.w_off, g.w_off + hp.M * g.chunk)
+    outs = []
+    for emaj in (0, 1):
+        lib.fast_conv_set_x3_c1_emaj(emaj)
+        eng.grad_flat.zero_()
+        hp.ring_wgrad(eng.frames, eng.fc, eng.grads[0], eng.bits[0], eng.grad_flat, eng.P, eng.E, eng.T,
+                      eng.bits_rows[0], rbase=eng.rbase)
+        torch.cuda.synchronize()
+        outs.append(eng.grad_flat[seg].clone())
+    lib.fast_conv_set_x3_c1_emaj(1)               # the default
+    assert outs[0].norm() > 0
+    e = rel(outs[1], outs[0])
+    print(f"conv1 ring wgrad env-major vs step-major: rel {e:.2e}")
+    assert e < 1e-6, e
+    assert rel(outs[1], g_hip[seg]) < 1e-6
+
+
 @pytest.mark.parametrize("opt", ["f16b", "sb1", "bal"])
 def test_x3_conv1_band_f16_staging_bit_equal(x3_ring_rollout, opt):
     """conv1_fwd_band_x2 F16B (the band converted to fp16 once while staged, X3_C1_F16B, the default) == the
